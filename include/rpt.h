@@ -1,0 +1,231 @@
+/*
+ * rpt.h — C-ABI of librpt.so, the MI355X-native (gfx950) ST-DBSCAN + tracking engine.
+ *
+ * Every entry point takes plain pointers, sizes and a hipStream_t passed as void*.
+ * Device pointers are marked (dev), host pointers (host). All device work is
+ * enqueued on `stream`; calls that must return a size to the host synchronise that
+ * stream and say so. Status codes are RPT_* below; the message of the last failure on
+ * the calling thread is rpt_last_error(). No C++ exception crosses this boundary.
+ *
+ * Reference interface each entry replaces (paths relative to the reference repo root):
+ *   rpt_polar_count/rpt_polar_write   load_radar_csv  PointCloudWork/4_temporal_object_tracker.py:184-232
+ *                                     + concatenation build_frame :312-352
+ *                                     (package form radar_pipeline/core/transforms.py:37-79)
+ *   rpt_polar_to_cartesian           radar_pipeline/core/transforms.py:13-34
+ *   rpt_bounds_xy / rpt_land_grid /  build_occupancy_grid :359-391, identify_land_cells :394-410,
+ *   rpt_land_mask / rpt_land_filter  filter_land_from_frame :413-436
+ *   rpt_stdbscan                     st_dbscan  PointCloudWork/3_stdbscan_point_clouds.py:101-136,
+ *                                     radar_pipeline/processors/clustering.py:49-115,
+ *                                     the labelling half of 4_temporal_object_tracker.py:443-506
+ *   rpt_infer_time_from_colors       radar_pipeline/processors/clustering.py:17-46, 3_stdbscan...py:91-98
+ *   rpt_cluster_summaries            per-frame Cluster extraction 4_temporal_object_tracker.py:508-536
+ *   rpt_set_order                    CPython set(frame_labels) iteration order :519
+ *   rpt_lsap                         scipy.optimize.linear_sum_assignment as called at :590
+ *   rpt_tracker_*                    ObjectTracker :543-688 (+ TrackedObject :111-140)
+ *   rpt_synth_echo                   (bench/test input generator; no reference counterpart)
+ */
+#ifndef RPT_H
+#define RPT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RPT_OK 0
+#define RPT_EINVAL 1      /* bad argument (maps to ValueError)                           */
+#define RPT_ENOMEM 2      /* device allocation failed                                     */
+#define RPT_EHIP 3        /* HIP runtime error                                            */
+#define RPT_EEMPTY 4      /* empty input where the reference raises (sklearn ValueError)  */
+#define RPT_ENOTSUP 5     /* input outside what the device path implements                */
+#define RPT_ENONFINITE 6  /* NaN/inf coordinates (sklearn check_array raises ValueError)  */
+
+#define RPT_ECHO_F32 0
+#define RPT_ECHO_U8 1
+
+/* ---- library ---------------------------------------------------------------------- */
+int32_t rpt_version(void);               /* major*10000 + minor*100 + patch            */
+const char* rpt_last_error(void);        /* thread-local; "" when none                 */
+int32_t rpt_device_count(void);          /* hipGetDeviceCount; 0 when no GPU           */
+int32_t rpt_set_device(int32_t device);  /* hipSetDevice                               */
+void rpt_release_scratch(void);          /* free this device's scratch pool            */
+
+/* ---- K1: polar -> Cartesian scatter ---------------------------------------------
+ * A batch of sweeps ("files"), each echo[rows][bins] (f32 or u8), concatenated in file
+ * order (= ascending gain inside a frame, as build_frame does).  Pass 1 counts kept
+ * points (echo > threshold, strictly) and writes the exclusive per-file output offsets
+ * file_offsets[n_files+1] (dev, int64): file f contributes ceil(kept_f / stride) points.
+ * Pass 2 writes x, y, intensity (f32) and gain_out (i32, the file's gain) for every
+ * kept element whose row-major rank inside its file is a multiple of `stride`.
+ *   x = ((scale[row] / bins) * bin) * cos_t[row]   (f32, each op rounded, no FMA)
+ * cos_t/sin_t are the per-row float32 np.cos/np.sin values of the reference (input). */
+int32_t rpt_polar_count(const void* echo, int32_t echo_dtype, int64_t n_files, int32_t rows,
+                        int32_t bins, float threshold, int32_t stride,
+                        int64_t* row_prefix /*dev [n_files*rows+1], kept before each row*/,
+                        int64_t* file_offsets /*dev [n_files+1]*/,
+                        int64_t* total_host /*host, may be NULL: then no sync*/, void* stream);
+int32_t rpt_polar_write(const void* echo, int32_t echo_dtype, int64_t n_files, int32_t rows,
+                        int32_t bins, const float* scale /*dev [n_files*rows]*/,
+                        const float* cos_t /*dev [n_files*rows]*/, const float* sin_t,
+                        const int32_t* gain /*dev [n_files]*/, float threshold, int32_t stride,
+                        const int64_t* row_prefix /*dev, from rpt_polar_count*/,
+                        const int64_t* file_offsets /*dev*/, float* x, float* y,
+                        float* intensity, int32_t* gain_out, void* stream);
+/* Generic form for radar_pipeline.sweep_to_point_cloud: ranges is a full [rows][bins] f32
+ * matrix, intensities f32 [rows][bins]; one sweep.  Outputs x,y,z(=intensity). */
+int32_t rpt_sweep_to_points(const float* intensities, const float* ranges, const float* cos_t,
+                            const float* sin_t, int32_t rows, int32_t bins, float threshold,
+                            int32_t stride, float* x, float* y, float* z, int64_t capacity,
+                            int64_t* n_out_host /*sync*/, void* stream);
+/* x = ranges * cos_t[:,None], y = ranges * sin_t[:,None]  (transforms.py:13-34) */
+int32_t rpt_polar_to_cartesian(const float* cos_t, const float* sin_t, const float* ranges,
+                               int64_t rows, int64_t bins, float* x, float* y, void* stream);
+
+/* ---- K2/K3: land filter ------------------------------------------------------------ */
+/* out4_host = {min x, max x, min y, max y} (float32, exact); synchronises. */
+int32_t rpt_bounds_xy(const float* x, const float* y, int64_t n, float* out4_host, void* stream);
+/* count_grid[(nxe-1)*(nye-1)] int32 and intensity_grid f64 are zeroed then accumulated
+ * with numpy.digitize semantics against the given float64 edges (np.add.at). */
+int32_t rpt_land_grid(const float* x, const float* y, const float* intensity, int64_t n,
+                      const double* x_edges /*dev*/, int32_t nxe, const double* y_edges,
+                      int32_t nye, int32_t* count_grid, double* intensity_grid, void* stream);
+int32_t rpt_land_mask(const int32_t* count_grid, const double* intensity_grid, int64_t cells,
+                      int64_t num_frames, double persistence_threshold, double min_intensity,
+                      uint8_t* land_mask /*dev [cells]*/, int64_t* land_cells_host /*sync*/,
+                      void* stream);
+/* Stable compaction of the points NOT on land.  point_frame[n] (dev, i32) is the frame slot
+ * of each point (non-decreasing), frame_offsets[n_frames+1] (dev, int64) the frame starts;
+ * new_frame_offsets[n_frames+1] (dev) receives the starts of the kept points.
+ * *n_kept_host (sync). */
+int32_t rpt_land_filter(const float* x, const float* y, const float* intensity,
+                        const int32_t* gain, const int32_t* point_frame, int64_t n,
+                        const int64_t* frame_offsets, int32_t n_frames, const double* x_edges,
+                        int32_t nxe, const double* y_edges, int32_t nye,
+                        const uint8_t* land_mask, float* x_out, float* y_out,
+                        float* intensity_out, int32_t* gain_out, int32_t* point_frame_out,
+                        int64_t* new_frame_offsets, int64_t* n_kept_host, void* stream);
+
+/* ---- K4-K8: ST-DBSCAN ------------------------------------------------------------------
+ * coords: dim (2 or 3) float32 component pointers sharing `stride` (elements between
+ * consecutive points: 1 for SoA, dim for an (N,dim) row-major array).  times float32.
+ * Labels (dev, int32 [n]) are bit-identical to the reference BFS: cluster ids ascend with
+ * each cluster's minimum core-point index, border points take the minimum adjacent id,
+ * noise is -1.  Neighbour test: float64 d2 = sum_k (x_k,i - x_k,j)^2 (left to right,
+ * each op rounded) <= eps_space^2, and float32 |t_i - t_j| <= float32(eps_time).
+ * Synchronises once (grid bounds). */
+typedef struct rpt_stdbscan_stats {
+  int64_t n_points;
+  int64_t n_core;
+  int32_t n_clusters;
+  int32_t grid_dims[4];   /* nx, ny, nz (1 for dim 2), nt */
+  int64_t grid_cells;
+  double ms_bounds, ms_grid, ms_core, ms_union, ms_label; /* filled when timing != 0 */
+  int32_t timing;         /* in: 1 = record per-stage times with hipEvents             */
+} rpt_stdbscan_stats;
+int32_t rpt_stdbscan(const float* x, const float* y, const float* z, int64_t stride,
+                     const float* times, int64_t n, double eps_space, double eps_time,
+                     int32_t min_samples, int32_t* labels, rpt_stdbscan_stats* stats,
+                     void* stream);
+
+/* nearest palette colour index (first minimum) as float32: colors u8 [n][3],
+ * palette f32 [n_pal][3] in ascending-gain order. */
+int32_t rpt_infer_time_from_colors(const uint8_t* colors, int64_t n, const float* palette,
+                                   int32_t n_pal, float* times_out, void* stream);
+
+/* ---- K9: per-(frame, label) cluster summaries ---------------------------------------
+ * point_frame[n] (dev, i32, non-decreasing frame slot per point), labels[n] from
+ * rpt_stdbscan.  Segment s = one (frame, label>=0) pair, ordered by (label, frame).
+ * centroid = sequential float32 sum in point order / count (np.mean axis 0);
+ * mean intensity = numpy 1-D float32 mean (pairwise sums over 8192-element chunks).
+ * frame_first_noise[n_frames] (dev, int64) = first point index of label -1 per frame, or -1.
+ * *n_segments_host (sync).  Output arrays have capacity n. */
+int32_t rpt_cluster_summaries(const int32_t* labels, const float* x, const float* y,
+                              const float* intensity, const int32_t* point_frame, int64_t n,
+                              int32_t n_frames, int32_t n_clusters, int32_t* seg_frame,
+                              int32_t* seg_label, int64_t* seg_count, int64_t* seg_first,
+                              float* seg_cx, float* seg_cy, float* seg_mean_i,
+                              int64_t* frame_first_noise, int64_t* n_segments_host,
+                              void* stream);
+
+/* ---- host: per-frame cluster order of the reference -----------------------------------
+ * From the segments of rpt_cluster_summaries (copied to host) and frame_first_noise: for each
+ * frame the segment indices in the order st_dbscan(frames) lists that frame's clusters
+ * (CPython set iteration over the frame's labels inserted in first-occurrence order, -1
+ * discarded).  frame_offsets_out[n_frames+1], order_out[n_segments]. */
+int32_t rpt_order_clusters(int32_t n_frames, int64_t n_segments, const int32_t* seg_frame,
+                           const int32_t* seg_label, const int64_t* seg_first,
+                           const int64_t* frame_first_noise, int64_t* frame_offsets_out,
+                           int64_t* order_out);
+
+/* ---- host: CPython set iteration order --------------------------------------------------
+ * keys = the distinct labels of a frame in first-occurrence order (may include -1).
+ * order_out receives the keys in the order `iter(set(keys))` yields them on CPython 3.10
+ * (int hash = value, hash(-1) = -2), -1 removed (set.discard(-1)).  Returns count. */
+int32_t rpt_set_order(const int32_t* keys, int32_t n, int32_t* order_out);
+
+/* ---- host: rectangular linear sum assignment (scipy 1.15 shortest augmenting path) ----
+ * cost row-major [nr][nc] float64; rows_out/cols_out receive min(nr,nc) pairs sorted by
+ * row, identical to scipy.optimize.linear_sum_assignment including tie-breaking. */
+int32_t rpt_lsap(const double* cost, int32_t nr, int32_t nc, int64_t* rows_out,
+                 int64_t* cols_out);
+
+/* ---- host: ObjectTracker --------------------------------------------------------------- */
+typedef struct rpt_tracker rpt_tracker;
+typedef struct rpt_tracker_params {
+  double max_association_distance; /* 50.0 */
+  int32_t max_missed_frames;        /* 10   */
+  int32_t motion_history_frames;    /* 5    */
+  double stationary_velocity_threshold; /* 1.0 */
+} rpt_tracker_params;
+typedef struct rpt_object_info {
+  int64_t object_id;
+  int32_t object_type;     /* 0 unknown, 1 buoy, 2 boat */
+  int32_t n_positions;     /* == len(frames_seen) */
+  int32_t n_velocities;
+  int64_t last_seen_frame;
+  double average_velocity; /* value of TrackedObject.average_velocity */
+  int32_t average_velocity_is_f32; /* 1 when the reference returns np.float32 */
+  int32_t color[3];
+} rpt_object_info;
+rpt_tracker* rpt_tracker_new(const rpt_tracker_params* params /*NULL = defaults*/);
+void rpt_tracker_free(rpt_tracker* t);
+/* One ObjectTracker.update(clusters, frame_id): clusters in list order. Returns the number
+ * of objects after the update (len of the returned list). */
+int32_t rpt_tracker_update(rpt_tracker* t, int64_t frame_id, int32_t k, const float* cx,
+                           const float* cy, const int64_t* cluster_frame_id);
+/* Batch driver: frames[i] has clusters [offsets[i], offsets[i+1]) already in reference
+ * order; equivalent to calling rpt_tracker_update per frame. */
+int32_t rpt_tracker_run(rpt_tracker* t, int32_t n_frames, const int64_t* frame_ids,
+                        const int64_t* offsets, const float* cx, const float* cy);
+int32_t rpt_tracker_num_objects(const rpt_tracker* t);
+int32_t rpt_tracker_object_info(const rpt_tracker* t, int32_t idx, rpt_object_info* out);
+/* positions (x,y f32) + frames_seen of object idx (dict order); velocities as f64 pairs
+ * (exact widening of the f32 values; velocity 0 is the f64 zero).  Buffers sized from info. */
+int32_t rpt_tracker_object_history(const rpt_tracker* t, int32_t idx, float* px, float* py,
+                                   int64_t* frames, double* vx, double* vy);
+
+/* ---- synthetic input (bench / parity tests) -----------------------------------------
+ * Deterministic u8 echo [n_frames][n_gains][rows][bins] from integer hashes; see
+ * rpt/synth.py for the bit-identical numpy restatement.  Geometry tables come from host. */
+typedef struct rpt_synth_params {
+  uint64_t seed;
+  int32_t rows, bins, n_gains, n_targets;
+  float scale;                  /* Scale column (m) */
+  uint32_t target_fill_u8;      /* target keep threshold on an 8-bit hash draw */
+  uint32_t land_fill_u8;        /* land keep threshold */
+  int32_t land_row0, land_row1, land_bin0; /* land sector [row0,row1) x [bin0, bins) */
+} rpt_synth_params;
+int32_t rpt_synth_echo(const rpt_synth_params* p, int64_t frame0, int64_t n_frames,
+                       const float* cos_t /*dev [rows]*/, const float* sin_t,
+                       const uint32_t* clutter_thresh /*dev [n_gains][bins]*/,
+                       const float* targets /*dev [n_frames][n_targets][4]: tx,ty,r2,-*/,
+                       const int32_t* target_rows /*dev [n_frames][n_targets][2] row lo/hi (incl) */,
+                       const int32_t* target_bins /*dev [n_frames][n_targets][2] bin lo/hi (incl) */,
+                       uint8_t* echo /*dev*/, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RPT_H */

@@ -1,0 +1,90 @@
+"""TEST INFRASTRUCTURE ONLY — the parity oracle for the rpt hot path.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+this package, and only as the checker / the timed CPU baseline; the product (``rpt`` +
+``librpt.so``) never imports or links it.
+
+Contents — a CPU restatement of the reference algorithm for every row of SURVEY.md §8a, each
+function citing the reference file:line it follows (paths relative to the reference root):
+
+* ``stdbscan``          BFS ST-DBSCAN, C (``stdbscan_oracle.c``) — 3_stdbscan_point_clouds.py:101-136
+* ``polar_scatter``     4_temporal_object_tracker.py:200-232 arithmetic on an echo matrix
+* ``build_frames``      build_frame :312-352 concatenation
+* ``land_filter``       :359-436
+* ``frame_clusters``    :508-536 (per-frame Cluster list in CPython set order)
+* ``Tracker``           ObjectTracker :543-688 with the exact numpy dtype flow
+* ``run_path``          stage order of run_pipeline :941-991 (no file I/O)
+
+Pinned by ``tests/golden/*.npz`` — vectors produced by running the reference itself in the
+build container (``tests/golden/make_golden.py``); ``tests/test_oracle_golden.py`` checks every
+function here against them.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+from .path import (  # noqa: F401
+    ANGLE_SCALE,
+    build_frames,
+    frame_clusters,
+    land_filter,
+    polar_scatter,
+    run_path,
+    trig_tables,
+)
+from .tracker import Tracker  # noqa: F401
+
+_HERE = Path(__file__).resolve().parent
+_LIB = None
+
+
+def _lib():
+    global _LIB
+    if _LIB is None:
+        so = _HERE / "liboracle.so"
+        if not so.exists():
+            import subprocess
+
+            subprocess.run(["make", "-s", "-C", str(_HERE)], check=True)
+        lib = C.CDLL(str(so))
+        lib.oracle_stdbscan.restype = C.c_int32
+        lib.oracle_stdbscan.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int64,
+                                        C.c_double, C.c_double, C.c_int32, C.c_void_p]
+        lib.oracle_neighbour_counts.restype = C.c_int32
+        lib.oracle_neighbour_counts.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int64,
+                                                C.c_double, C.c_double, C.c_void_p]
+        _LIB = lib
+    return _LIB
+
+
+def _prep(coords, times):
+    c = np.ascontiguousarray(coords, dtype=np.float32)
+    if c.ndim != 2:
+        raise ValueError("coords must be 2-D")
+    t = np.ascontiguousarray(times, dtype=np.float32)
+    return c, t
+
+
+def stdbscan(coords, times, eps_space: float, eps_time: float, min_samples: int) -> np.ndarray:
+    """Reference BFS labels (3_stdbscan_point_clouds.py:101-136) for float32 coords/times."""
+    c, t = _prep(coords, times)
+    n = c.shape[0]
+    if n == 0:
+        raise ValueError("Found array with 0 sample(s)")
+    labels = np.empty(n, dtype=np.int32)
+    r = _lib().oracle_stdbscan(c.ctypes.data, c.shape[1], t.ctypes.data, n, float(eps_space),
+                               float(eps_time), int(min_samples), labels.ctypes.data)
+    if r < 0:
+        raise MemoryError("oracle_stdbscan failed")
+    return labels
+
+
+def neighbour_counts(coords, times, eps_space: float, eps_time: float) -> np.ndarray:
+    c, t = _prep(coords, times)
+    out = np.empty(c.shape[0], dtype=np.int64)
+    _lib().oracle_neighbour_counts(c.ctypes.data, c.shape[1], t.ctypes.data, c.shape[0],
+                                   float(eps_space), float(eps_time), out.ctypes.data)
+    return out

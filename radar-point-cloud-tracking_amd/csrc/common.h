@@ -1,0 +1,105 @@
+// Shared host/device helpers for librpt (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/rpt.h"
+
+namespace rpt {
+
+// ---- error plumbing (thread-local last error, no exceptions across the ABI) -----------
+void set_error(const char* fmt, ...);
+void clear_error();
+
+#define RPT_HIP(expr)                                                               \
+  do {                                                                              \
+    hipError_t e__ = (expr);                                                        \
+    if (e__ != hipSuccess) {                                                        \
+      ::rpt::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e__),      \
+                       __FILE__, __LINE__);                                         \
+      return RPT_EHIP;                                                              \
+    }                                                                               \
+  } while (0)
+
+#define RPT_TRY(expr)              \
+  do {                             \
+    int32_t s__ = (expr);          \
+    if (s__ != RPT_OK) return s__; \
+  } while (0)
+
+#define RPT_CHECK_LAUNCH() RPT_HIP(hipGetLastError())
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---- scratch pool ------------------------------------------------------------------------
+// A per-device bump arena that grows on demand.  Calls reserve() once with their total
+// need (so no hipMalloc happens mid-call), then carve() 256-byte aligned slices.
+class Scratch {
+ public:
+  int32_t reserve(size_t bytes, hipStream_t stream);
+  void* carve(size_t bytes);
+  template <class T>
+  T* carve_n(size_t n) { return static_cast<T*>(carve(n * sizeof(T))); }
+  void reset() { off_ = 0; }
+  void release();
+  size_t capacity() const { return cap_; }
+
+ private:
+  char* base_ = nullptr;
+  size_t cap_ = 0;
+  size_t off_ = 0;
+};
+Scratch& scratch();  // for the current device
+
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+// Byte budget helper: sum of aligned array sizes.
+struct Budget {
+  size_t bytes = 0;
+  template <class T>
+  void add(size_t n) { bytes += align_up(n * sizeof(T), 256); }
+};
+
+// ---- device utilities --------------------------------------------------------------------
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// number of active lanes below this one with their bit set in `mask`
+__device__ __forceinline__ int rank_in_mask(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+}
+
+inline int grid_for(int64_t n, int block, int cap = 65535 * 8) {
+  int64_t g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+// ---- primitives implemented in prims.hip --------------------------------------------------
+// Exclusive scan of int64 values (in/out may alias).  tmp needs scan_tmp_elems(n) int64s.
+size_t scan_tmp_elems(int64_t n);
+int32_t exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp,
+                           hipStream_t stream);
+// Same for int32 input -> int64 output.
+int32_t exclusive_scan_i32_to_i64(const int32_t* in, int64_t* out, int64_t n, int64_t* tmp,
+                                  hipStream_t stream);
+
+// int32 -> int32 (values must fit; in == out allowed).
+int32_t exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, int64_t* tmp,
+                           hipStream_t stream);
+
+// Stable LSD radix sort of (key,u32 value) pairs on the low `bits` bits of key.
+// Buffers: keys/vals in, keys_alt/vals_alt ping-pong; the result ends in whichever buffer the
+// returned pointer pair names (out_keys/out_vals).  tmp needs radix_tmp_elems(n) int64s.
+size_t radix_tmp_elems(int64_t n);
+int32_t radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt,
+                         int64_t n, int bits, int64_t* tmp, uint32_t** out_keys,
+                         uint32_t** out_vals, hipStream_t stream);
+
+}  // namespace rpt

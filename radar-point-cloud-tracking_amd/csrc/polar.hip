@@ -1,0 +1,478 @@
+// K1: polar -> Cartesian scatter with intensity threshold, per-file stride and gain fusion.
+// Replaces load_radar_csv (PointCloudWork/4_temporal_object_tracker.py:200-232) + build_frame's
+// concatenation (:312-352), and radar_pipeline sweep_to_point_cloud (core/transforms.py:37-79).
+//
+// Layout: echo [file][row][bin] (u8 — 1 B per echo sample, the radar's native 8-bit values — or
+// f32), rows of 1024 bins.  One wave owns one row: with u8 echo a row is exactly one 16-B-per-lane
+// coalesced load (1 KiB per wave instruction); f32 rows take four.  Kept elements are ranked in
+// row-major order with a wave prefix sum over per-lane counts; the file rank comes from the
+// row prefix written by the count pass (two reads of the echo, no atomics, deterministic).
+//
+// Arithmetic (each op rounded to float32, no contraction — the reference is separate numpy ufuncs):
+//   step = scale[row] / (float)bins ; r = step * (float)bin ; x = r * cos_t[row] ; y = r * sin_t[row]
+// cos_t / sin_t are inputs: numpy's float32 SIMD cos/sin are not correctly rounded, so the host
+// evaluates them exactly as the reference does (4096 values per sweep geometry).
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace rpt {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / kWave;
+
+template <class T>
+__device__ __forceinline__ float to_f(T v) {
+  return (float)v;
+}
+
+// Elements per lane per iteration: 16 u8 (one uint4) or 4 f32 (one float4).
+template <class T>
+struct Vec;
+template <>
+struct Vec<uint8_t> {
+  static constexpr int N = 16;
+  using L = uint4;
+  __device__ static void unpack(const L& v, float (&o)[16]) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) o[k] = (float)((w[k >> 2] >> (8 * (k & 3))) & 0xffu);
+  }
+};
+template <>
+struct Vec<float> {
+  static constexpr int N = 4;
+  using L = float4;
+  __device__ static void unpack(const L& v, float (&o)[4]) {
+    o[0] = v.x;
+    o[1] = v.y;
+    o[2] = v.z;
+    o[3] = v.w;
+  }
+};
+
+__device__ __forceinline__ int wave_excl_scan(int v, int* total) {
+  const int lane = threadIdx.x & 63;
+  int incl = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += o;
+  }
+  *total = __shfl(incl, 63, 64);
+  return incl - v;
+}
+
+// Row pass: count kept elements per row.  VEC path needs bins % (64*N) == 0 and aligned rows.
+template <class T, bool VEC>
+__global__ __launch_bounds__(kBlock) void k_row_count(const T* __restrict__ echo,
+                                                     int64_t n_rows, int bins, float thr,
+                                                     int32_t* __restrict__ row_count) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave0 = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / 64;
+  const int64_t n_waves = (int64_t)gridDim.x * kWavesPerBlock;
+  for (int64_t row = wave0; row < n_rows; row += n_waves) {
+    const T* rp = echo + row * bins;
+    int c = 0;
+    if (VEC) {
+      constexpr int N = Vec<T>::N;
+      using L = typename Vec<T>::L;
+      for (int b0 = lane * N; b0 < bins; b0 += 64 * N) {
+        const L v = *reinterpret_cast<const L*>(rp + b0);
+        float f[N];
+        Vec<T>::unpack(v, f);
+#pragma unroll
+        for (int k = 0; k < N; ++k) c += (f[k] > thr) ? 1 : 0;
+      }
+    } else {
+      for (int b = lane; b < bins; b += 64) c += (to_f(rp[b]) > thr) ? 1 : 0;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    if (lane == 0) row_count[row] = c;
+  }
+}
+
+// file_offsets[f] = sum over earlier files of ceil(kept / stride); kept from row_prefix.
+__global__ void k_file_counts(const int64_t* __restrict__ row_prefix, int64_t n_files, int rows,
+                              int stride, int64_t* __restrict__ file_out) {
+  for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < n_files;
+       f += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t kept = row_prefix[(f + 1) * rows] - row_prefix[f * rows];
+    file_out[f] = (kept + stride - 1) / stride;
+  }
+}
+
+struct RowGeo {
+  const float* scale;   // per row (scale mode) or nullptr
+  const float* ranges;  // [row][bin] (ranges mode) or nullptr
+  const float* cos_t;
+  const float* sin_t;
+};
+
+// Row pass 2: write the kept elements whose in-file rank is a multiple of stride.
+template <class T, bool VEC>
+__global__ __launch_bounds__(kBlock) void k_row_write(
+    const T* __restrict__ echo, int64_t n_rows, int rows, int bins, float thr, int stride,
+    RowGeo geo, const int32_t* __restrict__ gain, const int64_t* __restrict__ row_prefix,
+    const int64_t* __restrict__ file_offsets, float* __restrict__ x, float* __restrict__ y,
+    float* __restrict__ val, int32_t* __restrict__ gain_out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave0 = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / 64;
+  const int64_t n_waves = (int64_t)gridDim.x * kWavesPerBlock;
+  const float fb = (float)bins;
+  for (int64_t row = wave0; row < n_rows; row += n_waves) {
+    const int64_t f = row / rows;
+    const T* rp = echo + row * bins;
+    int64_t rank = row_prefix[row] - row_prefix[f * rows];  // rank of this row's first kept
+    const int64_t out0 = file_offsets[f];
+    const float step = geo.scale ? geo.scale[row] / fb : 0.f;
+    const float ct = geo.cos_t[row], st = geo.sin_t[row];
+    const int32_t g = gain ? gain[f] : 0;
+    auto emit = [&](int b, float v, int64_t r) {
+      if (r % stride == 0) {
+        const float rr = geo.ranges ? geo.ranges[row * bins + b] : step * (float)b;
+        const int64_t o = out0 + r / stride;
+        x[o] = rr * ct;
+        y[o] = rr * st;
+        val[o] = v;
+        if (gain_out) gain_out[o] = g;
+      }
+    };
+    if (VEC) {
+      constexpr int N = Vec<T>::N;
+      using L = typename Vec<T>::L;
+      for (int base = 0; base < bins; base += 64 * N) {
+        const int b0 = base + lane * N;
+        const L v = *reinterpret_cast<const L*>(rp + b0);
+        float fv[N];
+        Vec<T>::unpack(v, fv);
+        int c = 0;
+#pragma unroll
+        for (int k = 0; k < N; ++k) c += (fv[k] > thr) ? 1 : 0;
+        int tot;
+        int64_t r = rank + wave_excl_scan(c, &tot);
+        if (c) {
+#pragma unroll
+          for (int k = 0; k < N; ++k)
+            if (fv[k] > thr) emit(b0 + k, fv[k], r++);
+        }
+        rank += tot;
+      }
+    } else {
+      for (int base = 0; base < bins; base += 64) {
+        const int b = base + lane;
+        const float v = (b < bins) ? to_f(rp[b]) : 0.f;
+        const bool keep = (b < bins) && (v > thr);
+        const uint64_t m = __ballot(keep);
+        if (keep) emit(b, v, rank + rank_in_mask(m));
+        rank += __popcll(m);
+      }
+    }
+  }
+}
+
+template <class T>
+int32_t count_impl(const T* echo, int64_t n_files, int rows, int bins, float thr, int stride,
+                   int64_t* row_prefix, int64_t* file_offsets, int64_t* total_host,
+                   hipStream_t st) {
+  const int64_t n_rows = n_files * rows;
+  Scratch& sc = scratch();
+  Budget b;
+  b.add<int32_t>(n_rows);
+  b.add<int64_t>(n_files + 1);
+  b.add<int64_t>(scan_tmp_elems(n_rows + 1) + scan_tmp_elems(n_files + 1));
+  RPT_TRY(sc.reserve(b.bytes, st));
+  int32_t* rc = sc.carve_n<int32_t>(n_rows + 1);
+  int64_t* fo = sc.carve_n<int64_t>(n_files + 1);
+  int64_t* tmp = sc.carve_n<int64_t>(scan_tmp_elems(n_rows + 1) + scan_tmp_elems(n_files + 1));
+  const bool vec = (bins % (64 * Vec<T>::N) == 0) && ((uintptr_t)echo % 16 == 0);
+  const int grid = grid_for(n_rows, kWavesPerBlock, 16384);
+  if (vec)
+    hipLaunchKernelGGL((k_row_count<T, true>), dim3(grid), dim3(kBlock), 0, st, echo, n_rows,
+                       bins, thr, rc);
+  else
+    hipLaunchKernelGGL((k_row_count<T, false>), dim3(grid), dim3(kBlock), 0, st, echo, n_rows,
+                       bins, thr, rc);
+  RPT_CHECK_LAUNCH();
+  RPT_HIP(hipMemsetAsync(rc + n_rows, 0, sizeof(int32_t), st));
+  RPT_TRY(exclusive_scan_i32_to_i64(rc, row_prefix, n_rows + 1, tmp, st));
+  hipLaunchKernelGGL(k_file_counts, dim3(grid_for(n_files, 256, 1024)), dim3(256), 0, st,
+                     row_prefix, n_files, rows, stride, fo);
+  RPT_CHECK_LAUNCH();
+  RPT_HIP(hipMemsetAsync(fo + n_files, 0, sizeof(int64_t), st));
+  RPT_TRY(exclusive_scan_i64(fo, file_offsets, n_files + 1, tmp, st));
+  if (total_host) {
+    RPT_HIP(hipMemcpyAsync(total_host, file_offsets + n_files, sizeof(int64_t),
+                           hipMemcpyDeviceToHost, st));
+    RPT_HIP(hipStreamSynchronize(st));
+  }
+  return RPT_OK;
+}
+
+template <class T>
+int32_t write_impl(const T* echo, int64_t n_files, int rows, int bins, float thr, int stride,
+                   RowGeo geo, const int32_t* gain, const int64_t* row_prefix,
+                   const int64_t* file_offsets, float* x, float* y, float* v, int32_t* gout,
+                   hipStream_t st) {
+  const int64_t n_rows = n_files * rows;
+  const bool vec = (bins % (64 * Vec<T>::N) == 0) && ((uintptr_t)echo % 16 == 0);
+  const int grid = grid_for(n_rows, kWavesPerBlock, 16384);
+  if (vec)
+    hipLaunchKernelGGL((k_row_write<T, true>), dim3(grid), dim3(kBlock), 0, st, echo, n_rows,
+                       rows, bins, thr, stride, geo, gain, row_prefix, file_offsets, x, y, v,
+                       gout);
+  else
+    hipLaunchKernelGGL((k_row_write<T, false>), dim3(grid), dim3(kBlock), 0, st, echo, n_rows,
+                       rows, bins, thr, stride, geo, gain, row_prefix, file_offsets, x, y, v,
+                       gout);
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
+}
+
+__global__ void k_polar_dense(const float* __restrict__ cos_t, const float* __restrict__ sin_t,
+                              const float* __restrict__ ranges, int64_t rows, int64_t bins,
+                              float* __restrict__ x, float* __restrict__ y) {
+  const int64_t n = rows * bins;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / bins;
+    const float rr = ranges[i];
+    x[i] = rr * cos_t[r];
+    y[i] = rr * sin_t[r];
+  }
+}
+
+// ---------------------------------------------------------------- colour -> time
+// clustering.py:39-46: diffs f32, dist2 = ((d0*d0) + d1*d1) + d2*d2, first argmin.
+__global__ void k_colors(const uint8_t* __restrict__ colors, int64_t n,
+                         const float* __restrict__ pal, int n_pal, float* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float r = colors[3 * i], g = colors[3 * i + 1], b = colors[3 * i + 2];
+    int best = 0;
+    float bd = 0.f;
+    for (int k = 0; k < n_pal; ++k) {
+      const float d0 = r - pal[3 * k], d1 = g - pal[3 * k + 1], d2 = b - pal[3 * k + 2];
+      float d = d0 * d0;
+      d = d + d1 * d1;
+      d = d + d2 * d2;
+      // np.argmin: first minimum; a NaN wins immediately (cannot occur for u8 colours)
+      if (k == 0 || d < bd) {
+        bd = d;
+        best = k;
+      }
+    }
+    out[i] = (float)best;
+  }
+}
+
+// ---------------------------------------------------------------- synthetic echo
+// Bit-identical restatement: rpt/synth.py::numpy_echo.
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+constexpr int kMaxTargets = 256;
+
+// One block per (frame, gain, row); threads sweep the bins.
+__global__ __launch_bounds__(kBlock) void k_synth(rpt_synth_params p, int64_t frame0,
+                                                 int64_t n_frames, const float* __restrict__ cos_t,
+                                                 const float* __restrict__ sin_t,
+                                                 const uint32_t* __restrict__ clutter_thresh,
+                                                 const float* __restrict__ targets,
+                                                 const int32_t* __restrict__ trows,
+                                                 const int32_t* __restrict__ tbins,
+                                                 uint8_t* __restrict__ echo) {
+  __shared__ int hits[kMaxTargets];
+  __shared__ int n_hits;
+  const int64_t n_rows_total = n_frames * p.n_gains * p.rows;
+  for (int64_t rr = blockIdx.x; rr < n_rows_total; rr += gridDim.x) {
+    const int row = (int)(rr % p.rows);
+    const int64_t fg = rr / p.rows;
+    const int gi = (int)(fg % p.n_gains);
+    const int64_t fl = fg / p.n_gains;  // local frame
+    const int64_t fa = frame0 + fl;      // absolute frame (hash input)
+    __syncthreads();
+    if (threadIdx.x == 0) n_hits = 0;
+    __syncthreads();
+    for (int k = threadIdx.x; k < p.n_targets; k += blockDim.x) {
+      const int32_t* tr = trows + (fl * p.n_targets + k) * 2;
+      if (row >= tr[0] && row <= tr[1]) hits[atomicAdd(&n_hits, 1)] = k;
+    }
+    __syncthreads();
+    const int nh = n_hits;
+    // deterministic target order: insertion sort of the (few) hits
+    if (threadIdx.x == 0) {
+      for (int a = 1; a < nh; ++a) {
+        const int v = hits[a];
+        int b = a - 1;
+        while (b >= 0 && hits[b] > v) {
+          hits[b + 1] = hits[b];
+          --b;
+        }
+        hits[b + 1] = v;
+      }
+    }
+    __syncthreads();
+    const float step = p.scale / (float)p.bins;
+    const float ct = cos_t[row], st = sin_t[row];
+    const bool land_row = row >= p.land_row0 && row < p.land_row1;
+    uint8_t* out = echo + rr * p.bins;
+    for (int b = threadIdx.x; b < p.bins; b += blockDim.x) {
+      const uint64_t idx = (((uint64_t)(fa * p.n_gains + gi) * (uint64_t)p.rows + row) *
+                            (uint64_t)p.bins) + (uint64_t)b;
+      const uint64_t h = splitmix64(p.seed ^ (idx * 0xD1B54A32D192ED03ull));
+      uint32_t v = 0;
+      if ((uint32_t)(h >> 32) < clutter_thresh[gi * p.bins + b]) v = 11u + (uint32_t)((h >> 16) & 0xffffu) % 29u;
+      if (land_row && b >= p.land_bin0 && (uint32_t)(h & 0xffu) < p.land_fill_u8)
+        v = 150u + (uint32_t)((h >> 8) & 0xffu) % 106u;
+      if (nh) {
+        const float r = step * (float)b;
+        const float xx = r * ct, yy = r * st;
+        for (int q = 0; q < nh; ++q) {
+          const int k = hits[q];
+          const int32_t* tb = tbins + (fl * p.n_targets + k) * 2;
+          if (b < tb[0] || b > tb[1]) continue;
+          const float* tg = targets + (fl * p.n_targets + k) * 4;
+          const float dx = xx - tg[0], dy = yy - tg[1];
+          float d2 = dx * dx;
+          d2 = d2 + dy * dy;
+          if (d2 <= tg[2]) {
+            if ((uint32_t)((h >> 40) & 0xffu) < p.target_fill_u8)
+              v = 60u + (uint32_t)((h >> 48) & 0xffu) % 40u;
+            break;
+          }
+        }
+      }
+      out[b] = (uint8_t)v;
+    }
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- C-ABI bodies
+int32_t polar_count(const void* echo, int32_t dt, int64_t n_files, int32_t rows, int32_t bins,
+                    float thr, int32_t stride, int64_t* row_prefix, int64_t* file_offsets,
+                    int64_t* total_host, hipStream_t st) {
+  if (!echo || n_files < 0 || rows <= 0 || bins <= 0 || stride < 1 || !row_prefix ||
+      !file_offsets) {
+    set_error("rpt_polar_count: bad arguments");
+    return RPT_EINVAL;
+  }
+  if (n_files == 0) {
+    RPT_HIP(hipMemsetAsync(file_offsets, 0, sizeof(int64_t), st));
+    RPT_HIP(hipMemsetAsync(row_prefix, 0, sizeof(int64_t), st));
+    if (total_host) *total_host = 0;
+    return RPT_OK;
+  }
+  if (dt == RPT_ECHO_U8)
+    return count_impl<uint8_t>((const uint8_t*)echo, n_files, rows, bins, thr, stride,
+                               row_prefix, file_offsets, total_host, st);
+  if (dt == RPT_ECHO_F32)
+    return count_impl<float>((const float*)echo, n_files, rows, bins, thr, stride, row_prefix,
+                             file_offsets, total_host, st);
+  set_error("rpt_polar_count: unknown echo dtype %d", dt);
+  return RPT_EINVAL;
+}
+
+int32_t polar_write(const void* echo, int32_t dt, int64_t n_files, int32_t rows, int32_t bins,
+                    const float* scale, const float* cos_t, const float* sin_t,
+                    const int32_t* gain, float thr, int32_t stride, const int64_t* row_prefix,
+                    const int64_t* file_offsets, float* x, float* y, float* v, int32_t* gout,
+                    hipStream_t st) {
+  if (n_files == 0) return RPT_OK;
+  if (!echo || !scale || !cos_t || !sin_t || !row_prefix || !file_offsets || !x || !y || !v ||
+      stride < 1) {
+    set_error("rpt_polar_write: bad arguments");
+    return RPT_EINVAL;
+  }
+  RowGeo geo{scale, nullptr, cos_t, sin_t};
+  if (dt == RPT_ECHO_U8)
+    return write_impl<uint8_t>((const uint8_t*)echo, n_files, rows, bins, thr, stride, geo, gain,
+                               row_prefix, file_offsets, x, y, v, gout, st);
+  if (dt == RPT_ECHO_F32)
+    return write_impl<float>((const float*)echo, n_files, rows, bins, thr, stride, geo, gain,
+                             row_prefix, file_offsets, x, y, v, gout, st);
+  set_error("rpt_polar_write: unknown echo dtype %d", dt);
+  return RPT_EINVAL;
+}
+
+int32_t sweep_to_points(const float* inten, const float* ranges, const float* cos_t,
+                        const float* sin_t, int32_t rows, int32_t bins, float thr,
+                        int32_t stride, float* x, float* y, float* z, int64_t capacity,
+                        int64_t* n_out_host, hipStream_t st) {
+  if (!inten || !ranges || !cos_t || !sin_t || rows <= 0 || bins <= 0 || stride < 1 ||
+      !n_out_host) {
+    set_error("rpt_sweep_to_points: bad arguments");
+    return RPT_EINVAL;
+  }
+  // the count pass uses the pool; keep its outputs in a second reservation-free region
+  int64_t* rp = nullptr;
+  int64_t* fo = nullptr;
+  RPT_HIP(hipMallocAsync((void**)&rp, sizeof(int64_t) * ((int64_t)rows + 1), st));
+  RPT_HIP(hipMallocAsync((void**)&fo, sizeof(int64_t) * 2, st));
+  int64_t total = 0;
+  int32_t s = count_impl<float>(inten, 1, rows, bins, thr, stride, rp, fo, &total, st);
+  if (s == RPT_OK) {
+    if (total > capacity) {
+      set_error("rpt_sweep_to_points: %lld points exceed capacity %lld", (long long)total,
+                (long long)capacity);
+      s = RPT_EINVAL;
+    } else {
+      RowGeo geo{nullptr, ranges, cos_t, sin_t};
+      s = write_impl<float>(inten, 1, rows, bins, thr, stride, geo, nullptr, rp, fo, x, y, z,
+                            nullptr, st);
+    }
+  }
+  (void)hipFreeAsync(rp, st);
+  (void)hipFreeAsync(fo, st);
+  *n_out_host = total;
+  return s;
+}
+
+int32_t polar_to_cartesian(const float* cos_t, const float* sin_t, const float* ranges,
+                           int64_t rows, int64_t bins, float* x, float* y, hipStream_t st) {
+  if (rows * bins == 0) return RPT_OK;
+  hipLaunchKernelGGL(k_polar_dense, dim3(grid_for(rows * bins, 256, 8192)), dim3(256), 0, st,
+                     cos_t, sin_t, ranges, rows, bins, x, y);
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
+}
+
+int32_t infer_time_from_colors(const uint8_t* colors, int64_t n, const float* pal, int32_t n_pal,
+                               float* out, hipStream_t st) {
+  if (n == 0) return RPT_OK;
+  if (n_pal <= 0) {
+    set_error("attempt to get argmin of an empty sequence");
+    return RPT_EINVAL;
+  }
+  hipLaunchKernelGGL(k_colors, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, colors, n, pal,
+                     n_pal, out);
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
+}
+
+int32_t synth_echo(const rpt_synth_params* p, int64_t frame0, int64_t n_frames,
+                   const float* cos_t, const float* sin_t, const uint32_t* clutter_thresh,
+                   const float* targets, const int32_t* trows, const int32_t* tbins,
+                   uint8_t* echo, hipStream_t st) {
+  if (!p || p->n_targets > kMaxTargets || p->rows <= 0 || p->bins <= 0 || p->n_gains <= 0) {
+    set_error("rpt_synth_echo: bad parameters (n_targets <= %d)", kMaxTargets);
+    return RPT_EINVAL;
+  }
+  const int64_t blocks = n_frames * p->n_gains * p->rows;
+  if (blocks == 0) return RPT_OK;
+  hipLaunchKernelGGL(k_synth, dim3((unsigned)std::min<int64_t>(blocks, 65536)), dim3(kBlock), 0,
+                     st, *p, frame0, n_frames, cos_t, sin_t, clutter_thresh, targets, trows,
+                     tbins, echo);
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
+}
+
+}  // namespace rpt

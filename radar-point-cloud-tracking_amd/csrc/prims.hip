@@ -1,0 +1,305 @@
+// Device-wide primitives used by the ST-DBSCAN grid build and the cluster summaries:
+//  * exclusive scan (int64 values) — 3-phase reduce / scan-of-partials / scan-and-add,
+//  * stable LSD radix sort of (u32 key, u32 value) pairs, 8-bit digits, wave-granular
+//    histograms so that a pass needs no block-level barriers inside the scatter loop.
+// Plus the library's error plumbing and per-device scratch pool.
+#include <cstdarg>
+#include <mutex>
+
+#include "common.h"
+
+namespace rpt {
+
+// ------------------------------------------------------------------ error plumbing
+static thread_local std::string g_last_error;
+
+void set_error(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+}
+void clear_error() { g_last_error.clear(); }
+const char* last_error_cstr() { return g_last_error.c_str(); }
+
+// ------------------------------------------------------------------ scratch pool
+int32_t Scratch::reserve(size_t bytes, hipStream_t stream) {
+  off_ = 0;
+  if (bytes <= cap_) return RPT_OK;
+  if (base_) {
+    RPT_HIP(hipStreamSynchronize(stream));
+    RPT_HIP(hipDeviceSynchronize());
+    RPT_HIP(hipFree(base_));
+    base_ = nullptr;
+    cap_ = 0;
+  }
+  size_t want = align_up(bytes + bytes / 4 + (1u << 20), 1u << 20);
+  hipError_t e = hipMalloc(&base_, want);
+  if (e != hipSuccess) {
+    base_ = nullptr;
+    set_error("scratch hipMalloc(%zu bytes) failed: %s", want, hipGetErrorString(e));
+    return RPT_ENOMEM;
+  }
+  cap_ = want;
+  return RPT_OK;
+}
+
+void* Scratch::carve(size_t bytes) {
+  size_t a = align_up(bytes, 256);
+  if (off_ + a > cap_) return nullptr;  // callers reserve() first; a null here is a bug
+  void* p = base_ + off_;
+  off_ += a;
+  return p;
+}
+
+void Scratch::release() {
+  if (base_) hipFree(base_);
+  base_ = nullptr;
+  cap_ = off_ = 0;
+}
+
+static std::mutex g_scratch_mu;
+static std::vector<Scratch*> g_scratch;
+
+Scratch& scratch() {
+  int dev = 0;
+  hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  if ((int)g_scratch.size() <= dev) g_scratch.resize(dev + 1, nullptr);
+  if (!g_scratch[dev]) g_scratch[dev] = new Scratch();
+  return *g_scratch[dev];
+}
+
+void release_scratch_current() {
+  int dev = 0;
+  hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  if ((int)g_scratch.size() > dev && g_scratch[dev]) g_scratch[dev]->release();
+}
+
+// ------------------------------------------------------------------ exclusive scan
+constexpr int kScanBlock = 256;
+constexpr int kScanItems = 8;
+constexpr int kScanTile = kScanBlock * kScanItems;  // 2048
+
+// Block-wide exclusive scan of one int64 per thread; returns the exclusive prefix and
+// writes the block total to *total.
+__device__ __forceinline__ int64_t block_exclusive_scan(int64_t v, int64_t* total) {
+  __shared__ int64_t wsum[kScanBlock / kWave];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  int64_t incl = v;
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    int64_t o = __shfl_up(incl, off, kWave);
+    if (lane >= off) incl += o;
+  }
+  if (lane == kWave - 1) wsum[wid] = incl;
+  __syncthreads();
+  int64_t wprefix = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kScanBlock / kWave; ++w) {
+    int64_t s = wsum[w];
+    if (w < wid) wprefix += s;
+    tot += s;
+  }
+  __syncthreads();  // wsum may be reused by the caller's next call
+  *total = tot;
+  return wprefix + incl - v;
+}
+
+template <class T>
+__global__ __launch_bounds__(kScanBlock) void k_scan_reduce(const T* __restrict__ in, int64_t n,
+                                                           int64_t* __restrict__ partial) {
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  int64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    int64_t i = base + k;
+    if (i < n) s += (int64_t)in[i];
+  }
+  int64_t tot;
+  (void)block_exclusive_scan(s, &tot);
+  if (threadIdx.x == 0) partial[blockIdx.x] = tot;
+}
+
+template <class T, class U>
+__global__ __launch_bounds__(kScanBlock) void k_scan_apply(const T* __restrict__ in, int64_t n,
+                                                          const int64_t* __restrict__ partial,
+                                                          U* __restrict__ out) {
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  int64_t vals[kScanItems];
+  int64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    int64_t i = base + k;
+    vals[k] = (i < n) ? (int64_t)in[i] : 0;
+    s += vals[k];
+  }
+  int64_t tot;
+  int64_t run = block_exclusive_scan(s, &tot) + (partial ? partial[blockIdx.x] : 0);
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    int64_t i = base + k;
+    if (i < n) out[i] = (U)run;
+    run += vals[k];
+  }
+}
+
+size_t scan_tmp_elems(int64_t n) {
+  size_t total = 0;
+  int64_t m = n;
+  while (m > kScanTile) {
+    m = (m + kScanTile - 1) / kScanTile;
+    total += (size_t)m + 64;
+  }
+  return total + 64;
+}
+
+template <class T, class U>
+static int32_t scan_impl(const T* in, U* out, int64_t n, int64_t* tmp, hipStream_t st) {
+  if (n <= 0) return RPT_OK;
+  const int64_t nb = (n + kScanTile - 1) / kScanTile;
+  if (nb == 1) {
+    hipLaunchKernelGGL((k_scan_apply<T, U>), dim3(1), dim3(kScanBlock), 0, st, in, n,
+                       (const int64_t*)nullptr, out);
+    RPT_CHECK_LAUNCH();
+    return RPT_OK;
+  }
+  int64_t* partial = tmp;
+  int64_t* rest = tmp + nb + 64;
+  hipLaunchKernelGGL(k_scan_reduce<T>, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n,
+                     partial);
+  RPT_CHECK_LAUNCH();
+  RPT_TRY((scan_impl<int64_t, int64_t>(partial, partial, nb, rest, st)));
+  hipLaunchKernelGGL((k_scan_apply<T, U>), dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n,
+                     (const int64_t*)partial, out);
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
+}
+
+int32_t exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp,
+                           hipStream_t stream) {
+  return scan_impl<int64_t, int64_t>(in, out, n, tmp, stream);
+}
+int32_t exclusive_scan_i32_to_i64(const int32_t* in, int64_t* out, int64_t n, int64_t* tmp,
+                                  hipStream_t stream) {
+  return scan_impl<int32_t, int64_t>(in, out, n, tmp, stream);
+}
+int32_t exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, int64_t* tmp,
+                           hipStream_t stream) {
+  return scan_impl<int32_t, int32_t>(in, out, n, tmp, stream);
+}
+
+// ------------------------------------------------------------------ radix sort
+constexpr int kSortBlock = 256;
+constexpr int kSortRows = 16;                  // items per lane
+constexpr int kSortWaveItems = kWave * kSortRows;  // 1024 items per wave
+constexpr int kSortWavesPerBlock = kSortBlock / kWave;
+
+// hist[d * n_waves + w] = number of items of wave-chunk w whose digit is d.
+__global__ __launch_bounds__(kSortBlock) void k_radix_hist(const uint32_t* __restrict__ keys,
+                                                          int64_t n, int shift, int64_t n_waves,
+                                                          int64_t* __restrict__ hist) {
+  __shared__ int cnt[kSortWavesPerBlock][256];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wl = threadIdx.x / kWave;
+  for (int d = lane; d < 256; d += kWave) cnt[wl][d] = 0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const int64_t w = (int64_t)blockIdx.x * kSortWavesPerBlock + wl;
+  if (w < n_waves) {
+    const int64_t base = w * kSortWaveItems;
+#pragma unroll 4
+    for (int r = 0; r < kSortRows; ++r) {
+      int64_t i = base + (int64_t)r * kWave + lane;
+      if (i < n) atomicAdd(&cnt[wl][(keys[i] >> shift) & 255u], 1);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (w < n_waves)
+    for (int d = lane; d < 256; d += kWave) hist[(int64_t)d * n_waves + w] = cnt[wl][d];
+}
+
+__global__ __launch_bounds__(kSortBlock) void k_radix_scatter(
+    const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, int64_t n, int shift,
+    int64_t n_waves, const int64_t* __restrict__ offs, uint32_t* __restrict__ keys_out,
+    uint32_t* __restrict__ vals_out) {
+  __shared__ int64_t run[kSortWavesPerBlock][256];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wl = threadIdx.x / kWave;
+  const int64_t w = (int64_t)blockIdx.x * kSortWavesPerBlock + wl;
+  if (w >= n_waves) return;  // whole wave exits together
+  for (int d = lane; d < 256; d += kWave) run[wl][d] = offs[(int64_t)d * n_waves + w];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const int64_t base = w * kSortWaveItems;
+  for (int r = 0; r < kSortRows; ++r) {
+    const int64_t i = base + (int64_t)r * kWave + lane;
+    const bool valid = i < n;
+    uint32_t k = 0, v = 0;
+    if (valid) {
+      k = keys[i];
+      v = vals[i];
+    }
+    const uint32_t d = (k >> shift) & 255u;
+    uint64_t mask = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bb = __ballot(valid && bit);
+      mask &= bit ? bb : ~bb;
+    }
+    const int rank = rank_in_mask(mask);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int64_t pos = run[wl][d] + rank;
+    if (valid) {
+      keys_out[pos] = k;
+      vals_out[pos] = v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (valid && rank == 0) run[wl][d] += __popcll(mask);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+size_t radix_tmp_elems(int64_t n) {
+  const int64_t n_waves = (n + kSortWaveItems - 1) / kSortWaveItems;
+  const int64_t h = 256 * n_waves;
+  return (size_t)h + 64 + scan_tmp_elems(h);
+}
+
+int32_t radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt,
+                         int64_t n, int bits, int64_t* tmp, uint32_t** out_keys,
+                         uint32_t** out_vals, hipStream_t st) {
+  *out_keys = keys;
+  *out_vals = vals;
+  if (n <= 1 || bits <= 0) return RPT_OK;
+  const int64_t n_waves = (n + kSortWaveItems - 1) / kSortWaveItems;
+  const int64_t h = 256 * n_waves;
+  int64_t* hist = tmp;
+  int64_t* scan_tmp = tmp + h + 64;
+  const unsigned blocks = (unsigned)((n_waves + kSortWavesPerBlock - 1) / kSortWavesPerBlock);
+  uint32_t *ks = keys, *vs = vals, *kd = keys_alt, *vd = vals_alt;
+  for (int shift = 0; shift < bits; shift += 8) {
+    hipLaunchKernelGGL(k_radix_hist, dim3(blocks), dim3(kSortBlock), 0, st, ks, n, shift,
+                       n_waves, hist);
+    RPT_CHECK_LAUNCH();
+    RPT_TRY(exclusive_scan_i64(hist, hist, h, scan_tmp, st));
+    hipLaunchKernelGGL(k_radix_scatter, dim3(blocks), dim3(kSortBlock), 0, st, ks, vs, n, shift,
+                       n_waves, (const int64_t*)hist, kd, vd);
+    RPT_CHECK_LAUNCH();
+    std::swap(ks, kd);
+    std::swap(vs, vd);
+  }
+  *out_keys = ks;
+  *out_vals = vs;
+  return RPT_OK;
+}
+
+}  // namespace rpt

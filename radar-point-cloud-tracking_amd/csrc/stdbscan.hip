@@ -1,0 +1,902 @@
+// ST-DBSCAN on gfx950: uniform space x time grid, exact neighbour predicate, deterministic
+// union-find labelling.  Replaces the BallTree + Python BFS of
+//   PointCloudWork/3_stdbscan_point_clouds.py:101-136,
+//   radar_pipeline/processors/clustering.py:49-115 and
+//   PointCloudWork/4_temporal_object_tracker.py:466-506.
+//
+// Semantics reproduced bit-exactly:
+//   nbr(i,j)  <=>  d2(i,j) <= eps^2  (float64: ((xi-xj)^2 + (yi-yj)^2 [+ (zi-zj)^2]), each op
+//                  rounded, no FMA — sklearn's euclidean rdist on float64 copies of the f32 input)
+//             and  |t_j - t_i| <= eps_t  (float32 arithmetic; eps_t rounded to float32 — the
+//                  reference compares np.float32 values with a Python float under NEP 50)
+//   core(i)   <=>  |{ j : nbr(i,j) }| >= min_samples   (the count includes i itself)
+//   clusters  =    connected components of the core-core graph, numbered in ascending order of
+//                  each component's minimum core-point index (the order the BFS starts them)
+//   border    =    non-core point with a core neighbour: minimum adjacent cluster id
+//   noise     =    -1
+//
+// Pipeline (K4..K8 of SURVEY.md §8a):
+//   k_bounds      min/max per dimension and time, "times integral" flag        (1 sync)
+//   k_keys        cell key per point: ((slab*nz + cz)*ny + cy)*nx + cx
+//   radix sort    stable, so every cell lists its points in index order
+//   k_gather      sorted float4 {x, y, z|t, t} + original index
+//   k_cell_count  -> exclusive scan -> cell_start[C+1]
+//   k_cell_box    per occupied cell: bounding box in space and time, "mutual" flag
+//                 (box diagonal within eps and time span within eps_t: every pair adjacent)
+//   k_core        neighbour count with early exit at min_samples; whole-cell accept/reject
+//   k_rep         first core point of each cell
+//   k_union       core-core union-find (min-index hooking); one edge per mutual cell suffices
+//   k_compress    root of every point
+//   k_cmin        minimum original index per component
+//   k_ismin/scan  cluster id = rank of the component minimum among all minima
+//   k_label       core: own id; non-core: min id over adjacent core points, else -1
+//
+// Cell side is eps/2 (x (1+2^-20)), so every neighbour lies within +-2 cells and any cell's
+// diagonal is at most eps*sqrt(dim)/2 <= eps for dim <= 3, which makes dense cells "mutual".
+#include <cfloat>
+#include <climits>
+#include <cmath>
+#include <cstring>
+
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace rpt {
+
+namespace {
+
+constexpr int kBlock = 256;
+
+// ---------------------------------------------------------------- order-preserving f32 <-> u32
+__device__ __forceinline__ uint32_t f2ord(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+inline float ord2f(uint32_t u) {  // host side
+  uint32_t v = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
+  float f;
+  std::memcpy(&f, &v, 4);
+  return f;
+}
+
+struct Bounds {
+  uint32_t mn[4];   // ordered-u32 minima of x, y, z, t (t over finite values only)
+  uint32_t mx[4];
+  int32_t nonfinite_xyz;  // any NaN/inf coordinate
+  int32_t nonintegral_t;  // any finite t with t != floor(t) or |t| >= 2^24
+  int32_t n_finite_t;
+  int32_t pad;
+};
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_bounds(const float* __restrict__ x,
+                                                  const float* __restrict__ y,
+                                                  const float* __restrict__ z, int64_t stride,
+                                                  const float* __restrict__ t, int64_t n,
+                                                  Bounds* __restrict__ out) {
+  uint32_t mn[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+  uint32_t mx[4] = {0u, 0u, 0u, 0u};
+  int nonfin = 0, nonint = 0, nfin = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float v[4];
+    v[0] = x[i * stride];
+    v[1] = y[i * stride];
+    v[2] = (D == 3) ? z[i * stride] : 0.f;
+    v[3] = t[i];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (!isfinite(v[k])) nonfin = 1;
+      uint32_t o = f2ord(v[k]);
+      mn[k] = min(mn[k], o);
+      mx[k] = max(mx[k], o);
+    }
+    if (isfinite(v[3])) {
+      ++nfin;
+      uint32_t o = f2ord(v[3]);
+      mn[3] = min(mn[3], o);
+      mx[3] = max(mx[3], o);
+      if (v[3] != floorf(v[3]) || fabsf(v[3]) >= 16777216.f) nonint = 1;
+    }
+  }
+  // wave reduce then one atomic per wave
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      mn[k] = min(mn[k], (uint32_t)__shfl_xor((int)mn[k], off));
+      mx[k] = max(mx[k], (uint32_t)__shfl_xor((int)mx[k], off));
+    }
+    nonfin |= __shfl_xor(nonfin, off);
+    nonint |= __shfl_xor(nonint, off);
+    nfin += __shfl_xor(nfin, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      atomicMin(&out->mn[k], mn[k]);
+      atomicMax(&out->mx[k], mx[k]);
+    }
+    if (nonfin) atomicOr(&out->nonfinite_xyz, 1);
+    if (nonint) atomicOr(&out->nonintegral_t, 1);
+    atomicAdd(&out->n_finite_t, nfin);
+  }
+}
+
+__global__ void k_bounds_init(Bounds* b) {
+  for (int k = 0; k < 4; ++k) {
+    b->mn[k] = 0xffffffffu;
+    b->mx[k] = 0u;
+  }
+  b->nonfinite_xyz = 0;
+  b->nonintegral_t = 0;
+  b->n_finite_t = 0;
+  b->pad = 0;
+}
+
+// ---------------------------------------------------------------- grid geometry
+struct Geom {
+  double ox, oy, oz, ot;  // origins (minima)
+  double cs;              // spatial cell side
+  double ct;              // time slab width
+  int nx, ny, nz, nt;
+  int64_t cells;          // nx*ny*nz*nt (an extra "isolated" cell C holds non-finite t)
+  double eps2;            // eps_space^2 (float64)
+  float epst;             // float32(eps_time)
+  int min_samples;
+};
+
+__device__ __forceinline__ int cell_of(double v, double o, double cs, int n) {
+  double q = floor((v - o) / cs);
+  int c = (q < 0.0) ? 0 : (q >= (double)n ? n - 1 : (int)q);
+  return c;
+}
+__device__ __forceinline__ int slab_of(float t, const Geom& g) {
+  return cell_of((double)t, g.ot, g.ct, g.nt);
+}
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_keys(const float* __restrict__ x,
+                                                const float* __restrict__ y,
+                                                const float* __restrict__ z, int64_t stride,
+                                                const float* __restrict__ t, int64_t n, Geom g,
+                                                uint32_t* __restrict__ keys,
+                                                uint32_t* __restrict__ vals,
+                                                int32_t* __restrict__ cell_count) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float ti = t[i];
+    uint32_t key;
+    if (!isfinite(ti)) {
+      key = (uint32_t)g.cells;  // isolated: matches nothing, not even itself
+    } else {
+      const int cx = cell_of((double)x[i * stride], g.ox, g.cs, g.nx);
+      const int cy = cell_of((double)y[i * stride], g.oy, g.cs, g.ny);
+      const int cz = (D == 3) ? cell_of((double)z[i * stride], g.oz, g.cs, g.nz) : 0;
+      const int s = slab_of(ti, g);
+      key = (uint32_t)((((int64_t)s * g.nz + cz) * g.ny + cy) * g.nx + cx);
+    }
+    keys[i] = key;
+    vals[i] = (uint32_t)i;
+    atomicAdd(&cell_count[key], 1);
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_gather(const float* __restrict__ x,
+                                                  const float* __restrict__ y,
+                                                  const float* __restrict__ z, int64_t stride,
+                                                  const float* __restrict__ t, int64_t n,
+                                                  const uint32_t* __restrict__ skeys,
+                                                  const uint32_t* __restrict__ svals,
+                                                  float4* __restrict__ pts,
+                                                  int32_t* __restrict__ sorig,
+                                                  int32_t* __restrict__ skey) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = svals[s];
+    float4 p;
+    p.x = x[i * stride];
+    p.y = y[i * stride];
+    p.w = t[i];
+    p.z = (D == 3) ? z[i * stride] : p.w;
+    pts[s] = p;
+    sorig[s] = (int32_t)i;
+    skey[s] = (int32_t)skeys[s];
+  }
+}
+
+// Per-cell bounding boxes.  boxA = {xmin, xmax, ymin, ymax}, boxB = {zmin, zmax, tmin, tmax}.
+// mutual[c] = 1 when every pair of points in the cell passes the neighbour test (computed
+// conservatively from the box with the same rounding as the pair test).
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ pts,
+                                                    const int32_t* __restrict__ cell_start,
+                                                    int64_t cells, Geom g,
+                                                    float4* __restrict__ boxA,
+                                                    float4* __restrict__ boxB,
+                                                    uint8_t* __restrict__ mutual) {
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < cells;
+       c += (int64_t)gridDim.x * blockDim.x) {
+    const int b = cell_start[c], e = cell_start[c + 1];
+    if (b == e) continue;
+    float4 p = pts[b];
+    float x0 = p.x, x1 = p.x, y0 = p.y, y1 = p.y, z0 = p.z, z1 = p.z, t0 = p.w, t1 = p.w;
+    for (int j = b + 1; j < e; ++j) {
+      p = pts[j];
+      x0 = fminf(x0, p.x); x1 = fmaxf(x1, p.x);
+      y0 = fminf(y0, p.y); y1 = fmaxf(y1, p.y);
+      z0 = fminf(z0, p.z); z1 = fmaxf(z1, p.z);
+      t0 = fminf(t0, p.w); t1 = fmaxf(t1, p.w);
+    }
+    boxA[c] = make_float4(x0, x1, y0, y1);
+    boxB[c] = make_float4(z0, z1, t0, t1);
+    const double dx = (double)x1 - (double)x0;
+    const double dy = (double)y1 - (double)y0;
+    double d2 = dx * dx + dy * dy;
+    if (D == 3) {
+      const double dz = (double)z1 - (double)z0;
+      d2 = d2 + dz * dz;
+    }
+    const float dt = t1 - t0;
+    mutual[c] = (d2 <= g.eps2 && dt <= g.epst) ? 1 : 0;
+  }
+}
+
+// Actual time range per slab (slabs are the slowest key dimension, so each slab's points are
+// contiguous in sorted order).  One block per slab.
+__global__ __launch_bounds__(kBlock) void k_slab_range(const float4* __restrict__ pts,
+                                                      const int32_t* __restrict__ cell_start,
+                                                      int64_t cells_per_slab, int nt,
+                                                      float2* __restrict__ slab_t) {
+  const int s = blockIdx.x;
+  if (s >= nt) return;
+  const int b = cell_start[(int64_t)s * cells_per_slab];
+  const int e = cell_start[(int64_t)(s + 1) * cells_per_slab];
+  float lo = FLT_MAX, hi = -FLT_MAX;
+  for (int j = b + threadIdx.x; j < e; j += blockDim.x) {
+    const float tv = pts[j].w;
+    lo = fminf(lo, tv);
+    hi = fmaxf(hi, tv);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    lo = fminf(lo, __shfl_xor(lo, off));
+    hi = fmaxf(hi, __shfl_xor(hi, off));
+  }
+  __shared__ float slo[kBlock / 64], shi[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) {
+    slo[threadIdx.x / 64] = lo;
+    shi[threadIdx.x / 64] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kBlock / 64; ++w) {
+      lo = fminf(lo, slo[w]);
+      hi = fmaxf(hi, shi[w]);
+    }
+    // empty slab: lo > hi, never matches
+    slab_t[s] = make_float2(lo, hi);
+  }
+}
+
+// ---------------------------------------------------------------- neighbour predicates
+// Exact pair test (see file header).
+template <int D>
+__device__ __forceinline__ bool adjacent(const float4& a, const float4& b, const Geom& g) {
+  const float dt = fabsf(a.w - b.w);
+  const double dx = (double)a.x - (double)b.x;
+  const double dy = (double)a.y - (double)b.y;
+  double d2 = dx * dx + dy * dy;
+  if (D == 3) {
+    const double dz = (double)a.z - (double)b.z;
+    d2 = d2 + dz * dz;
+  }
+  return (d2 <= g.eps2) && (dt <= g.epst);
+}
+
+// |p - [lo, hi]| lower bound and the farthest-end distance, float64, each rounded like the pair
+// test (monotone), so classification never contradicts the pair test.
+__device__ __forceinline__ void span_dist(float p, float lo, float hi, double& dmin,
+                                          double& dmax) {
+  const double dp = (double)p;
+  dmin = (p < lo) ? ((double)lo - dp) : ((p > hi) ? (dp - (double)hi) : 0.0);
+  dmax = fmax(fabs(dp - (double)lo), fabs(dp - (double)hi));
+}
+
+// 0: no point of the cell can be adjacent; 1: every point is adjacent; 2: test pairs.
+template <int D>
+__device__ __forceinline__ int classify(const float4& p, const float4& A, const float4& B,
+                                        const Geom& g) {
+  // time (float32, same rounding as the pair test)
+  const float tlo = B.z, thi = B.w;
+  const float tmin = (p.w < tlo) ? (tlo - p.w) : ((p.w > thi) ? (p.w - thi) : 0.f);
+  if (!(tmin <= g.epst)) return 0;
+  const float tmax = fmaxf(fabsf(p.w - tlo), fabsf(p.w - thi));
+  double mnx, mxx, mny, mxy;
+  span_dist(p.x, A.x, A.y, mnx, mxx);
+  span_dist(p.y, A.z, A.w, mny, mxy);
+  double dmin = mnx * mnx + mny * mny;
+  double dmax = mxx * mxx + mxy * mxy;
+  if (D == 3) {
+    double mnz, mxz;
+    span_dist(p.z, B.x, B.y, mnz, mxz);
+    dmin = dmin + mnz * mnz;
+    dmax = dmax + mxz * mxz;
+  }
+  if (!(dmin <= g.eps2)) return 0;
+  return (dmax <= g.eps2 && tmax <= g.epst) ? 1 : 2;
+}
+
+// Candidate-cell enumeration shared by the three scan kernels.  Calls f(cell, begin, end, cls)
+// for every non-empty cell that may hold a neighbour of point p (own cell included); f returns
+// true to stop the enumeration.
+template <int D, class F>
+__device__ __forceinline__ void for_each_cell(const float4& p, int32_t key, const Geom& g,
+                                              const int32_t* __restrict__ cell_start,
+                                              const float4* __restrict__ boxA,
+                                              const float4* __restrict__ boxB,
+                                              const float2* __restrict__ slab_t, F&& f) {
+  const int cx = key % g.nx;
+  int r = key / g.nx;
+  const int cy = r % g.ny;
+  r /= g.ny;
+  const int cz = (D == 3) ? (r % g.nz) : 0;
+  const int cs = (D == 3) ? (r / g.nz) : r;
+  // conservative slab window (+-1 slack), culled by each slab's actual time range
+  const double tp = (double)p.w, et = (double)g.epst;
+  int s0 = (int)fmax(floor((tp - et - g.ot) / g.ct) - 1.0, 0.0);
+  int s1 = (int)fmin(floor((tp + et - g.ot) / g.ct) + 1.0, (double)(g.nt - 1));
+  const int x0 = max(cx - 2, 0), x1 = min(cx + 2, g.nx - 1);
+  const int y0 = max(cy - 2, 0), y1 = min(cy + 2, g.ny - 1);
+  const int z0 = (D == 3) ? max(cz - 2, 0) : 0, z1 = (D == 3) ? min(cz + 2, g.nz - 1) : 0;
+  (void)cs;
+  for (int s = s0; s <= s1; ++s) {
+    const float2 sr = slab_t[s];
+    if (sr.x > sr.y) continue;  // empty slab
+    const float smin = (p.w < sr.x) ? (sr.x - p.w) : ((p.w > sr.y) ? (p.w - sr.y) : 0.f);
+    if (!(smin <= g.epst)) continue;
+    for (int zz = z0; zz <= z1; ++zz) {
+      for (int yy = y0; yy <= y1; ++yy) {
+        const int64_t row = (((int64_t)s * g.nz + zz) * g.ny + yy) * g.nx;
+        int b = cell_start[row + x0];
+        for (int xx = x0; xx <= x1; ++xx) {
+          const int e = cell_start[row + xx + 1];
+          if (e > b) {
+            const int64_t c = row + xx;
+            const int cls = classify<D>(p, boxA[c], boxB[c], g);
+            if (cls != 0 && f(c, b, e, cls)) return;
+          }
+          b = e;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- K5: core flags
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_core(const float4* __restrict__ pts,
+                                                const int32_t* __restrict__ skey, int64_t n,
+                                                Geom g, const int32_t* __restrict__ cell_start,
+                                                const float4* __restrict__ boxA,
+                                                const float4* __restrict__ boxB,
+                                                const float2* __restrict__ slab_t,
+                                                uint8_t* __restrict__ core) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const int32_t key = skey[s];
+  if ((int64_t)key >= g.cells) {  // non-finite time: no neighbours at all
+    core[s] = (0 >= g.min_samples) ? 1 : 0;
+    return;
+  }
+  const float4 p = pts[s];
+  const int need = g.min_samples;
+  int cnt = 0;
+  if (need > 0) {
+    for_each_cell<D>(p, key, g, cell_start, boxA, boxB, slab_t,
+                     [&](int64_t c, int b, int e, int cls) -> bool {
+                       if (cls == 1) {
+                         cnt += e - b;
+                       } else {
+                         for (int j = b; j < e; ++j) {
+                           if (adjacent<D>(p, pts[j], g)) {
+                             if (++cnt >= need) return true;
+                           }
+                         }
+                       }
+                       return cnt >= need;
+                     });
+  }
+  core[s] = (cnt >= need) ? 1 : 0;
+}
+
+// first core point (sorted index) of each cell, -1 when none
+__global__ __launch_bounds__(kBlock) void k_rep(const int32_t* __restrict__ cell_start,
+                                               int64_t cells, const uint8_t* __restrict__ core,
+                                               int32_t* __restrict__ rep) {
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < cells;
+       c += (int64_t)gridDim.x * blockDim.x) {
+    const int b = cell_start[c], e = cell_start[c + 1];
+    int r = -1;
+    for (int j = b; j < e; ++j)
+      if (core[j]) {
+        r = j;
+        break;
+      }
+    rep[c] = r;
+  }
+}
+
+// ---------------------------------------------------------------- union-find
+__device__ __forceinline__ int uf_load(const int32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void uf_store(int32_t* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Path-halving find.  Parents only ever decrease, so a stale read is an older ancestor and
+// every returned root was a true ancestor at some point (connectivity is never overstated).
+__device__ __forceinline__ int uf_find(int32_t* parent, int x) {
+  while (true) {
+    const int p = uf_load(parent + x);
+    if (p == x) return x;
+    const int gp = uf_load(parent + p);
+    if (gp == p) return p;
+    uf_store(parent + x, gp);
+    x = gp;
+  }
+}
+// Hook the larger root under the smaller one: every tree's root is its minimum index.
+__device__ __forceinline__ void uf_unite(int32_t* parent, int a, int b) {
+  while (true) {
+    a = uf_find(parent, a);
+    b = uf_find(parent, b);
+    if (a == b) return;
+    if (a < b) {
+      const int tmp = a;
+      a = b;
+      b = tmp;
+    }
+    const int old = atomicCAS(parent + a, a, b);
+    if (old == a) return;
+    a = old;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_parent_init(int32_t* parent, int64_t n) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x)
+    parent[s] = (int32_t)s;
+}
+
+// K6: core-core union.  Edge (s, j) with j in cell c:
+//   * c mutual: all of c's core points are pairwise adjacent, hence one component; one edge
+//     from s into c (to rep[c] when the whole cell is adjacent, else to the first adjacent core
+//     point) spans every edge from s into c.
+//   * c not mutual: every adjacent core j > s (the edge from the smaller end covers the pair;
+//     when cell(s) is mutual the larger end's first-hit edge covers it too).
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_union(const float4* __restrict__ pts,
+                                                 const int32_t* __restrict__ skey, int64_t n,
+                                                 Geom g, const int32_t* __restrict__ cell_start,
+                                                 const float4* __restrict__ boxA,
+                                                 const float4* __restrict__ boxB,
+                                                 const float2* __restrict__ slab_t,
+                                                 const uint8_t* __restrict__ core,
+                                                 const int32_t* __restrict__ rep,
+                                                 const uint8_t* __restrict__ mutual,
+                                                 int32_t* __restrict__ parent) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n || !core[s]) return;
+  const int32_t key = skey[s];
+  if ((int64_t)key >= g.cells) return;
+  const float4 p = pts[s];
+  const int si = (int)s;
+  for_each_cell<D>(p, key, g, cell_start, boxA, boxB, slab_t,
+                   [&](int64_t c, int b, int e, int cls) -> bool {
+                     const int r = rep[c];
+                     if (r < 0) return false;
+                     if (mutual[c]) {
+                       if (cls == 1) {
+                         uf_unite(parent, si, r);
+                         return false;
+                       }
+                       if (uf_find(parent, si) == uf_find(parent, r)) return false;
+                       for (int j = r; j < e; ++j) {
+                         if (core[j] && adjacent<D>(p, pts[j], g)) {
+                           uf_unite(parent, si, j);
+                           break;
+                         }
+                       }
+                     } else {
+                       for (int j = max(b, si + 1); j < e; ++j) {
+                         if (core[j] && (cls == 1 || adjacent<D>(p, pts[j], g)))
+                           uf_unite(parent, si, j);
+                       }
+                     }
+                     return false;
+                   });
+}
+
+// root of every core point; ccmin = component minimum original index (filled in two steps)
+__global__ __launch_bounds__(kBlock) void k_compress(int32_t* __restrict__ parent,
+                                                    const uint8_t* __restrict__ core, int64_t n,
+                                                    const int32_t* __restrict__ sorig,
+                                                    int32_t* __restrict__ cmin) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    if (!core[s]) continue;
+    int x = (int)s;
+    int p = parent[x];
+    while (p != x) {
+      x = p;
+      p = parent[x];
+    }
+    atomicMin(&cmin[x], sorig[s]);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill_i32(int32_t* p, int64_t n, int32_t v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
+// ccmin[s] = component-min original index for core points, -1 otherwise; flags the minima.
+__global__ __launch_bounds__(kBlock) void k_ccmin(const int32_t* __restrict__ parent,
+                                                 const uint8_t* __restrict__ core, int64_t n,
+                                                 const int32_t* __restrict__ sorig,
+                                                 const int32_t* __restrict__ cmin,
+                                                 int32_t* __restrict__ ccmin,
+                                                 int32_t* __restrict__ is_min) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    if (!core[s]) {
+      ccmin[s] = -1;
+      continue;
+    }
+    int x = (int)s;
+    int p = parent[x];
+    while (p != x) {
+      x = p;
+      p = parent[x];
+    }
+    const int m = cmin[x];
+    ccmin[s] = m;
+    if (m == sorig[s]) is_min[m] = 1;
+  }
+}
+
+// K7/K8: final labels in original order.
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts,
+                                                 const int32_t* __restrict__ skey, int64_t n,
+                                                 Geom g, const int32_t* __restrict__ cell_start,
+                                                 const float4* __restrict__ boxA,
+                                                 const float4* __restrict__ boxB,
+                                                 const float2* __restrict__ slab_t,
+                                                 const int32_t* __restrict__ ccmin,
+                                                 const int32_t* __restrict__ rep,
+                                                 const uint8_t* __restrict__ mutual,
+                                                 const int32_t* __restrict__ sorig,
+                                                 const int32_t* __restrict__ cid,
+                                                 int32_t* __restrict__ labels) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const int own = ccmin[s];
+  if (own >= 0) {
+    labels[sorig[s]] = cid[own];
+    return;
+  }
+  const int32_t key = skey[s];
+  int best = INT_MAX;
+  if ((int64_t)key < g.cells) {
+    const float4 p = pts[s];
+    for_each_cell<D>(p, key, g, cell_start, boxA, boxB, slab_t,
+                     [&](int64_t c, int b, int e, int cls) -> bool {
+                       const int r = rep[c];
+                       if (r < 0) return false;
+                       if (mutual[c]) {
+                         if (cls == 1) {
+                           best = min(best, ccmin[r]);
+                           return false;
+                         }
+                         if (ccmin[r] >= best) return false;  // cannot improve
+                         for (int j = r; j < e; ++j) {
+                           const int m = ccmin[j];
+                           if (m >= 0 && adjacent<D>(p, pts[j], g)) {
+                             best = min(best, m);
+                             break;
+                           }
+                         }
+                       } else {
+                         for (int j = r; j < e; ++j) {
+                           const int m = ccmin[j];
+                           if (m >= 0 && m < best && (cls == 1 || adjacent<D>(p, pts[j], g)))
+                             best = m;
+                         }
+                       }
+                       return false;
+                     });
+  }
+  labels[sorig[s]] = (best == INT_MAX) ? -1 : cid[best];
+}
+
+// Degenerate parameters (negative/NaN eps): nobody has a neighbour, not even itself.
+__global__ __launch_bounds__(kBlock) void k_isolated_labels(int32_t* labels, int64_t n,
+                                                           int singletons) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    labels[i] = singletons ? (int32_t)i : -1;
+}
+
+// Non-finite-time points are isolated; with min_samples <= 0 they are singleton clusters and
+// flagged as their own component minimum (handled by k_ccmin via parent = self).
+
+struct Timer {
+  bool on = false;
+  hipStream_t st{};
+  hipEvent_t ev[8]{};
+  int k = 0;
+  void start(bool enable, hipStream_t s) {
+    on = enable;
+    st = s;
+    if (!on) return;
+    for (auto& e : ev) (void)hipEventCreate(&e);
+    (void)hipEventRecord(ev[k++], st);
+  }
+  void mark() {
+    if (on && k < 8) (void)hipEventRecord(ev[k++], st);
+  }
+  double ms(int i) {
+    float t = 0;
+    (void)hipEventElapsedTime(&t, ev[i], ev[i + 1]);
+    return t;
+  }
+  ~Timer() {
+    if (on)
+      for (auto& e : ev) (void)hipEventDestroy(e);
+  }
+};
+
+template <int D>
+int32_t stdbscan_impl(const float* x, const float* y, const float* z, int64_t stride,
+                      const float* t, int64_t n, double eps_space, double eps_time,
+                      int32_t min_samples, int32_t* labels, rpt_stdbscan_stats* stats,
+                      hipStream_t st) {
+  Timer tm;
+  tm.start(stats && stats->timing, st);
+  const float epst = (float)eps_time;
+  const int gb = grid_for(n, kBlock, 2048);
+  // ---- degenerate parameters: no pair (not even i,i) passes the predicate
+  if (!(eps_space >= 0.0) || !(epst >= 0.0f)) {
+    hipLaunchKernelGGL(k_isolated_labels, dim3(gb), dim3(kBlock), 0, st, labels, n,
+                       min_samples <= 0 ? 1 : 0);
+    RPT_CHECK_LAUNCH();
+    if (stats) {
+      stats->n_points = n;
+      stats->n_core = min_samples <= 0 ? n : 0;
+      stats->n_clusters = min_samples <= 0 ? (int32_t)n : 0;
+    }
+    return RPT_OK;
+  }
+  Scratch& sc = scratch();
+  // ---- bounds (one small sync)
+  {
+    Budget bb;
+    bb.add<Bounds>(1);
+    RPT_TRY(sc.reserve(bb.bytes, st));
+  }
+  Bounds* d_b = sc.carve_n<Bounds>(1);
+  hipLaunchKernelGGL(k_bounds_init, dim3(1), dim3(1), 0, st, d_b);
+  hipLaunchKernelGGL(k_bounds<D>, dim3(gb), dim3(kBlock), 0, st, x, y, z, stride, t, n, d_b);
+  RPT_CHECK_LAUNCH();
+  Bounds hb;
+  RPT_HIP(hipMemcpyAsync(&hb, d_b, sizeof(Bounds), hipMemcpyDeviceToHost, st));
+  RPT_HIP(hipStreamSynchronize(st));
+  tm.mark();
+  if (hb.nonfinite_xyz) {
+    set_error("Input contains NaN or infinity in coordinates");
+    return RPT_ENONFINITE;
+  }
+  // ---- geometry
+  Geom g{};
+  g.eps2 = eps_space * eps_space;
+  g.epst = epst;
+  g.min_samples = min_samples;
+  double lo[4], hi[4];
+  for (int k = 0; k < 4; ++k) {
+    lo[k] = (double)ord2f(hb.mn[k]);
+    hi[k] = (double)ord2f(hb.mx[k]);
+  }
+  if (hb.n_finite_t == 0) {
+    lo[3] = hi[3] = 0.0;
+  }
+  const double margin = 1.0 + 1.0 / 1048576.0;  // 2^-20
+  double cs = (eps_space > 0.0 ? eps_space * 0.5 : 1.0) * margin;
+  double ct;
+  if (!hb.nonintegral_t)
+    ct = 1.0;  // one slab per integer time value (frame id)
+  else
+    ct = (epst > 0.f ? (double)epst : 1.0) * margin;
+  const int64_t cmax = std::max<int64_t>(int64_t(1) << 22, 4 * n) < (int64_t(1) << 30)
+                           ? std::max<int64_t>(int64_t(1) << 22, 4 * n)
+                           : (int64_t(1) << 30);
+  auto dims = [&](double ext, double side) -> int64_t {
+    double q = floor(ext / side) + 1.0;
+    return q > 1e9 ? (int64_t)1e9 : (int64_t)q;
+  };
+  int64_t nx, ny, nz, nt;
+  for (int it = 0; it < 200; ++it) {
+    nx = dims(hi[0] - lo[0], cs);
+    ny = dims(hi[1] - lo[1], cs);
+    nz = (D == 3) ? dims(hi[2] - lo[2], cs) : 1;
+    nt = dims(hi[3] - lo[3], ct);
+    const double cells = (double)nx * ny * nz * nt;
+    if (cells <= (double)cmax) break;
+    if ((double)nt > (double)nx * ny * nz)
+      ct *= 2.0;
+    else
+      cs *= 2.0;
+  }
+  g.ox = lo[0];
+  g.oy = lo[1];
+  g.oz = lo[2];
+  g.ot = lo[3];
+  g.cs = cs;
+  g.ct = ct;
+  g.nx = (int)nx;
+  g.ny = (int)ny;
+  g.nz = (int)nz;
+  g.nt = (int)nt;
+  g.cells = nx * ny * nz * nt;
+  const int64_t C = g.cells;
+  const int64_t C1 = C + 1;  // + isolated cell (non-finite t)
+  // ---- scratch
+  Budget bud;
+  bud.add<Bounds>(1);
+  bud.add<uint32_t>(n);  // keys
+  bud.add<uint32_t>(n);  // vals
+  bud.add<uint32_t>(n);  // keys_alt
+  bud.add<uint32_t>(n);  // vals_alt
+  bud.add<int64_t>(radix_tmp_elems(n));
+  bud.add<float4>(n);        // pts
+  bud.add<int32_t>(n);       // sorig
+  bud.add<int32_t>(n);       // skey
+  bud.add<int32_t>(C1 + 1);  // cell_start (count, then scanned)
+  bud.add<int64_t>(scan_tmp_elems(C1 + 1) + scan_tmp_elems(n + 1));
+  bud.add<float4>(C1);  // boxA
+  bud.add<float4>(C1);  // boxB
+  bud.add<uint8_t>(C1);  // mutual
+  bud.add<int32_t>(C1);  // rep
+  bud.add<float2>(nt);   // slab_t
+  bud.add<uint8_t>(n);   // core
+  bud.add<int32_t>(n);   // parent
+  bud.add<int32_t>(n);   // cmin
+  bud.add<int32_t>(n);   // ccmin
+  bud.add<int32_t>(n + 1);  // is_min -> cid
+  RPT_TRY(sc.reserve(bud.bytes, st));
+  (void)sc.carve_n<Bounds>(1);
+  uint32_t* keys = sc.carve_n<uint32_t>(n);
+  uint32_t* vals = sc.carve_n<uint32_t>(n);
+  uint32_t* keys_alt = sc.carve_n<uint32_t>(n);
+  uint32_t* vals_alt = sc.carve_n<uint32_t>(n);
+  int64_t* rtmp = sc.carve_n<int64_t>(radix_tmp_elems(n));
+  float4* pts = sc.carve_n<float4>(n);
+  int32_t* sorig = sc.carve_n<int32_t>(n);
+  int32_t* skey = sc.carve_n<int32_t>(n);
+  int32_t* cell_start = sc.carve_n<int32_t>(C1 + 1);
+  int64_t* stmp = sc.carve_n<int64_t>(scan_tmp_elems(C1 + 1) + scan_tmp_elems(n + 1));
+  float4* boxA = sc.carve_n<float4>(C1);
+  float4* boxB = sc.carve_n<float4>(C1);
+  uint8_t* mutual = sc.carve_n<uint8_t>(C1);
+  int32_t* rep = sc.carve_n<int32_t>(C1);
+  float2* slab_t = sc.carve_n<float2>(nt);
+  uint8_t* core = sc.carve_n<uint8_t>(n);
+  int32_t* parent = sc.carve_n<int32_t>(n);
+  int32_t* cmin = sc.carve_n<int32_t>(n);
+  int32_t* ccmin = sc.carve_n<int32_t>(n);
+  int32_t* cid = sc.carve_n<int32_t>(n + 1);
+  if (!cid) {
+    set_error("internal: scratch carve overflow");
+    return RPT_ENOMEM;
+  }
+  // ---- K4: grid build
+  RPT_HIP(hipMemsetAsync(cell_start, 0, sizeof(int32_t) * (C1 + 1), st));
+  hipLaunchKernelGGL(k_keys<D>, dim3(gb), dim3(kBlock), 0, st, x, y, z, stride, t, n, g, keys,
+                     vals, cell_start);
+  RPT_CHECK_LAUNCH();
+  int bits = 1;
+  while ((int64_t(1) << bits) <= C1) ++bits;
+  uint32_t *sk, *sv;
+  RPT_TRY(radix_sort_pairs(keys, vals, keys_alt, vals_alt, n, bits, rtmp, &sk, &sv, st));
+  hipLaunchKernelGGL(k_gather<D>, dim3(gb), dim3(kBlock), 0, st, x, y, z, stride, t, n, sk, sv,
+                     pts, sorig, skey);
+  RPT_CHECK_LAUNCH();
+  RPT_TRY(exclusive_scan_i32(cell_start, cell_start, C1 + 1, stmp, st));
+  const int gc = grid_for(C, kBlock, 8192);
+  hipLaunchKernelGGL(k_cell_box<D>, dim3(gc), dim3(kBlock), 0, st, pts, cell_start, C, g, boxA,
+                     boxB, mutual);
+  RPT_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_slab_range, dim3((unsigned)nt), dim3(kBlock), 0, st, pts, cell_start,
+                     (int64_t)(C / nt), (int)nt, slab_t);
+  RPT_CHECK_LAUNCH();
+  tm.mark();
+  // ---- K5: core flags
+  const unsigned gp = (unsigned)((n + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(k_core<D>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
+                     boxA, boxB, slab_t, core);
+  RPT_CHECK_LAUNCH();
+  tm.mark();
+  // ---- K6: union
+  hipLaunchKernelGGL(k_rep, dim3(gc), dim3(kBlock), 0, st, cell_start, C, core, rep);
+  hipLaunchKernelGGL(k_parent_init, dim3(gb), dim3(kBlock), 0, st, parent, n);
+  hipLaunchKernelGGL(k_union<D>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
+                     boxA, boxB, slab_t, core, rep, mutual, parent);
+  RPT_CHECK_LAUNCH();
+  tm.mark();
+  // ---- K7/K8: component minima, ids, labels
+  hipLaunchKernelGGL(k_fill_i32, dim3(gb), dim3(kBlock), 0, st, cmin, n, (int32_t)INT_MAX);
+  hipLaunchKernelGGL(k_compress, dim3(gb), dim3(kBlock), 0, st, parent, core, n, sorig, cmin);
+  RPT_HIP(hipMemsetAsync(cid, 0, sizeof(int32_t) * (n + 1), st));
+  hipLaunchKernelGGL(k_ccmin, dim3(gb), dim3(kBlock), 0, st, parent, core, n, sorig, cmin,
+                     ccmin, cid);
+  RPT_CHECK_LAUNCH();
+  RPT_TRY(exclusive_scan_i32(cid, cid, n + 1, stmp, st));
+  hipLaunchKernelGGL(k_label<D>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
+                     boxA, boxB, slab_t, ccmin, rep, mutual, sorig, cid, labels);
+  RPT_CHECK_LAUNCH();
+  tm.mark();
+  if (stats) {
+    int32_t ncl = 0;
+    RPT_HIP(hipMemcpyAsync(&ncl, cid + n, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    RPT_HIP(hipStreamSynchronize(st));
+    stats->n_points = n;
+    stats->n_clusters = ncl;
+    stats->n_core = -1;
+    stats->grid_dims[0] = g.nx;
+    stats->grid_dims[1] = g.ny;
+    stats->grid_dims[2] = g.nz;
+    stats->grid_dims[3] = g.nt;
+    stats->grid_cells = C;
+    if (tm.on) {
+      RPT_HIP(hipEventSynchronize(tm.ev[tm.k - 1]));
+      stats->ms_bounds = tm.ms(0);
+      stats->ms_grid = tm.ms(1);
+      stats->ms_core = tm.ms(2);
+      stats->ms_union = tm.ms(3);
+      stats->ms_label = tm.ms(4);
+    }
+  }
+  return RPT_OK;
+}
+
+}  // namespace
+
+int32_t stdbscan(const float* x, const float* y, const float* z, int64_t stride, const float* t,
+                 int64_t n, double eps_space, double eps_time, int32_t min_samples,
+                 int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st, int dim) {
+  if (n <= 0) {
+    set_error("Found array with 0 sample(s) (shape=(0, %d)) while a minimum of 1 is required.",
+              dim);
+    return RPT_EEMPTY;
+  }
+  if (n >= (int64_t(1) << 31) - 2) {
+    set_error("rpt_stdbscan: n=%lld exceeds the int32 index space", (long long)n);
+    return RPT_ENOTSUP;
+  }
+  if (!x || !y || !t || !labels || (dim == 3 && !z) || stride < 1) {
+    set_error("rpt_stdbscan: null pointer or bad stride");
+    return RPT_EINVAL;
+  }
+  if (dim == 2) return stdbscan_impl<2>(x, y, z, stride, t, n, eps_space, eps_time, min_samples,
+                                        labels, stats, st);
+  if (dim == 3) return stdbscan_impl<3>(x, y, z, stride, t, n, eps_space, eps_time, min_samples,
+                                        labels, stats, st);
+  set_error("rpt_stdbscan: dim must be 2 or 3 (got %d)", dim);
+  return RPT_ENOTSUP;
+}
+
+}  // namespace rpt

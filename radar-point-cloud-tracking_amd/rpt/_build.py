@@ -1,0 +1,92 @@
+"""Build librpt.so (HIP kernels for gfx950 + host runtime) in-tree with hipcc.
+
+No CMake, no torch extension machinery: every ``csrc/*.hip`` / ``csrc/*.cpp`` is compiled to an
+object with ``hipcc --offload-arch=gfx950`` and linked into ``rpt/librpt.so``.  Objects are
+rebuilt only when a source or header is newer.  ``-ffp-contract=off`` is global: the parity
+contract (bit-identical labels and centroids) forbids FMA contraction of the reference's
+separately rounded float operations.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+CSRC = PKG_DIR.parent / "csrc"
+INCLUDE = PKG_DIR.parent.parent / "include"
+BUILD = PKG_DIR.parent / "build"
+LIB = PKG_DIR / "librpt.so"
+
+ARCH = os.environ.get("RPT_OFFLOAD_ARCH", "gfx950")
+COMMON_FLAGS = [
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "-ffp-contract=off",
+    f"--offload-arch={ARCH}",
+    "-Wall",
+    "-Wno-unused-function",
+    "-Wno-unused-result",
+    f"-I{INCLUDE}",
+    f"-I{CSRC}",
+]
+
+
+def _hipcc() -> str:
+    exe = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not Path(exe).exists():
+        raise RuntimeError("hipcc not found: the ROCm toolchain is required to build librpt")
+    return exe
+
+
+def _sources() -> list[Path]:
+    return sorted(list(CSRC.glob("*.hip")) + list(CSRC.glob("*.cpp")))
+
+
+def _headers_mtime() -> float:
+    hs = list(CSRC.glob("*.h")) + list(INCLUDE.glob("*.h"))
+    return max((h.stat().st_mtime for h in hs), default=0.0)
+
+
+def _compile(src: Path, obj: Path) -> str:
+    cmd = [_hipcc(), *COMMON_FLAGS, "-c", str(src), "-o", str(obj)]
+    if src.suffix == ".cpp":
+        cmd.insert(1, "-x")
+        cmd.insert(2, "hip")
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr}")
+    return r.stderr
+
+
+def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -> Path:
+    BUILD.mkdir(parents=True, exist_ok=True)
+    hdr_t = _headers_mtime()
+    todo = []
+    objs = []
+    for src in _sources():
+        obj = BUILD / (src.name + ".o")
+        objs.append(obj)
+        if force or not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, hdr_t):
+            todo.append((src, obj))
+    jobs = jobs or min(8, max(1, os.cpu_count() or 1))
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        for (src, _), warn in zip(todo, ex.map(lambda a: _compile(*a), todo)):
+            if verbose and warn.strip():
+                print(f"[rpt build] {src.name}:\n{warn}")
+    if todo or not LIB.exists():
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB),
+               *[str(o) for o in objs]]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link of librpt.so failed:\n{r.stderr}")
+    if verbose:
+        print(f"[rpt build] {LIB} ({len(todo)} objects rebuilt)")
+    return LIB
+
+
+if __name__ == "__main__":
+    build(verbose=True)

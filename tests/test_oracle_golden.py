@@ -1,0 +1,126 @@
+"""Pin the oracle: every oracle function reproduces the vectors produced by running the reference
+itself (tests/golden/make_golden.py).  CPU only."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import oracle
+from oracle import path as op
+
+
+def test_stdbscan_oracle_matches_reference_labels(golden):
+    g = golden("g2_stdbscan.npz")
+    for k in range(int(g["n_cases"])):
+        eps, et, ms = g[f"c{k}_params"]
+        lab = oracle.stdbscan(g[f"c{k}_coords"], g[f"c{k}_times"], eps, et, int(ms))
+        np.testing.assert_array_equal(lab, g[f"c{k}_labels"], err_msg=f"case {k} {g[f'c{k}_kind']}")
+
+
+def test_polar_oracle_matches_load_radar_csv(golden):
+    g = golden("g1_polar.npz")
+    for k in range(3):
+        cos_t, sin_t = op.trig_tables(g[f"f{k}_angle"])
+        x, y, v = op.polar_scatter(g[f"f{k}_echo"], g[f"f{k}_scale"], cos_t, sin_t)
+        np.testing.assert_array_equal(x, g[f"f{k}_x"])
+        np.testing.assert_array_equal(y, g[f"f{k}_y"])
+        np.testing.assert_array_equal(v, g[f"f{k}_i"])
+        # package form (radar_pipeline sweep_to_point_cloud: threshold 0, stride 16)
+        xp, yp, zp = op.polar_scatter(g[f"f{k}_echo"], g[f"f{k}_scale"], cos_t, sin_t,
+                                      threshold=0.0, stride=16)
+        np.testing.assert_array_equal(xp, g[f"f{k}_pkg_x"])
+        np.testing.assert_array_equal(yp, g[f"f{k}_pkg_y"])
+        np.testing.assert_array_equal(zp, g[f"f{k}_pkg_z"])
+
+
+def test_build_frames_oracle_matches_build_frame(golden):
+    g = golden("g1_polar.npz")
+    per_gain = {}
+    for k in range(3):
+        cos_t, sin_t = op.trig_tables(g[f"f{k}_angle"])
+        per_gain[int(g[f"f{k}_gain"])] = op.polar_scatter(g[f"f{k}_echo"], g[f"f{k}_scale"],
+                                                          cos_t, sin_t)
+    frames = op.build_frames([per_gain])
+    assert len(frames) == 1
+    _, pts, gains = frames[0]
+    np.testing.assert_array_equal(pts, g["frame_points"])
+    np.testing.assert_array_equal(gains, g["frame_gains"])
+
+
+def _g3_frames(g):
+    n = int(g["n_frames"])
+    return [(int(g[f"in{k}_fid"]), g[f"in{k}_points"], g[f"in{k}_gains"]) for k in range(n)]
+
+
+def test_land_oracle_matches_reference(golden):
+    g = golden("g3_land.npz")
+    frames = _g3_frames(g)
+    out, cnt, tot, land, (xe, ye) = op.land_filter(frames)
+    np.testing.assert_array_equal(xe, g["x_edges"])
+    np.testing.assert_array_equal(ye, g["y_edges"])
+    np.testing.assert_array_equal(cnt, g["count"])
+    np.testing.assert_array_equal(tot, g["intensity"])
+    np.testing.assert_array_equal(land, g["land"])
+    assert land.any(), "fixture should contain land cells"
+    for k, (_, p, gg) in enumerate(out):
+        np.testing.assert_array_equal(p, g[f"out{k}_points"])
+        np.testing.assert_array_equal(gg, g[f"out{k}_gains"])
+
+
+def _g4_case(g, k):
+    frames = [(int(g[f"c{k}_f{j}_fid"]), g[f"c{k}_f{j}_points"], None)
+              for j in range(int(g[f"c{k}_nframes"]))]
+    eps, et, ms = g[f"c{k}_params"]
+    return frames, float(eps), float(et), int(ms)
+
+
+def test_frame_clusters_oracle_matches_reference(golden):
+    g = golden("g4_clusters.npz")
+    for k in range(int(g["n_cases"])):
+        frames, eps, et, ms = _g4_case(g, k)
+        xy, t = op.stack_coords(frames)
+        labels = oracle.stdbscan(xy, t, eps, et, ms)
+        res = op.frame_clusters(frames, labels)
+        rows = [(fid, *c) for fid, _, _ in frames for c in res.get(fid, [])]
+        assert len(rows) == len(g[f"c{k}_frame"])
+        np.testing.assert_array_equal([r[0] for r in rows], g[f"c{k}_frame"])
+        np.testing.assert_array_equal([r[1] for r in rows], g[f"c{k}_label"])
+        np.testing.assert_array_equal([r[2] for r in rows], g[f"c{k}_count"])
+        np.testing.assert_array_equal(np.array([r[3][0] for r in rows], np.float32), g[f"c{k}_cx"])
+        np.testing.assert_array_equal(np.array([r[3][1] for r in rows], np.float32), g[f"c{k}_cy"])
+        np.testing.assert_array_equal([r[4] for r in rows], g[f"c{k}_mean_i"])
+
+
+def replay_tracker(g, s, make):
+    """Feed sequence s of g5 into a tracker built by make(); returns (tracker, alive lists)."""
+    frames = g[f"s{s}_frames"]
+    off = g[f"s{s}_offsets"]
+    cents = g[f"s{s}_cents"]
+    trk = make()
+    alive = []
+    for i, f in enumerate(frames):
+        cl = [(cents[j], int(f)) for j in range(off[i], off[i + 1])]
+        objs = trk.update(cl, int(f))
+        alive.append([o.object_id for o in objs])
+    return trk, alive
+
+
+def test_tracker_oracle_matches_reference(golden):
+    g = golden("g5_tracker.npz")
+    for s in range(int(g["n_seqs"])):
+        trk, alive = replay_tracker(g, s, oracle.Tracker)
+        ao = g[f"s{s}_alive_off"]
+        for i, a in enumerate(alive):
+            assert a == list(g[f"s{s}_alive"][ao[i]:ao[i + 1]])
+        objs = list(trk.objects.values())
+        np.testing.assert_array_equal([o.object_id for o in objs], g[f"s{s}_obj_id"])
+        np.testing.assert_array_equal([o.object_type for o in objs], g[f"s{s}_obj_type"])
+        pos = np.vstack([np.vstack(o.positions) for o in objs]).astype(np.float32)
+        np.testing.assert_array_equal(pos, g[f"s{s}_obj_pos"])
+        vel = np.vstack([np.vstack(o.velocities).astype(np.float64) for o in objs])
+        np.testing.assert_array_equal(vel, g[f"s{s}_obj_vel"])
+        np.testing.assert_array_equal([float(o.average_velocity) for o in objs],
+                                      g[f"s{s}_obj_avgv"])
+        np.testing.assert_array_equal([isinstance(o.average_velocity, np.float32) for o in objs],
+                                      g[f"s{s}_obj_avgv_f32"])
+        np.testing.assert_array_equal([o.color for o in objs], g[f"s{s}_obj_color"])
