@@ -71,8 +71,14 @@ int32_t rpt_polar_write(const void* echo, int32_t echo_dtype, int64_t n_files, i
                         const float* cos_t /*dev [n_files*rows]*/, const float* sin_t,
                         const int32_t* gain /*dev [n_files]*/, float threshold, int32_t stride,
                         const int64_t* row_prefix /*dev, from rpt_polar_count*/,
-                        const int64_t* file_offsets /*dev*/, float* x, float* y,
-                        float* intensity, int32_t* gain_out, void* stream);
+                        const int64_t* file_offsets /*dev*/, int32_t files_per_frame,
+                        float* x, float* y, float* intensity, int32_t* gain_out /*nullable*/,
+                        int32_t* point_frame_out /*nullable: file / files_per_frame*/,
+                        void* stream);
+/* times_out[i] = (float)frame_ids[point_frame[i]] (frame_ids dev int64 per frame slot; NULL =
+ * the slot itself): the float32 frame_ids stack of 4_temporal_object_tracker.py:460-467. */
+int32_t rpt_frame_times(const int32_t* point_frame, int64_t n, const int64_t* frame_ids,
+                        float* times_out, void* stream);
 /* Generic form for radar_pipeline.sweep_to_point_cloud: ranges is a full [rows][bins] f32
  * matrix, intensities f32 [rows][bins]; one sweep.  Outputs x,y,z(=intensity). */
 int32_t rpt_sweep_to_points(const float* intensities, const float* ranges, const float* cos_t,

@@ -12,6 +12,45 @@ void release_scratch_current();
 int32_t stdbscan(const float* x, const float* y, const float* z, int64_t stride, const float* t,
                  int64_t n, double eps_space, double eps_time, int32_t min_samples,
                  int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st, int dim);
+int32_t polar_count(const void* echo, int32_t dt, int64_t n_files, int32_t rows, int32_t bins,
+                    float thr, int32_t stride, int64_t* row_prefix, int64_t* file_offsets,
+                    int64_t* total_host, hipStream_t st);
+int32_t polar_write(const void* echo, int32_t dt, int64_t n_files, int32_t rows, int32_t bins,
+                    const float* scale, const float* cos_t, const float* sin_t,
+                    const int32_t* gain, float thr, int32_t stride, const int64_t* row_prefix,
+                    const int64_t* file_offsets, int32_t files_per_frame, float* x, float* y,
+                    float* v, int32_t* gout, int32_t* pf, hipStream_t st);
+int32_t frame_times(const int32_t* pf, int64_t n, const int64_t* ids, float* t, hipStream_t st);
+int32_t sweep_to_points(const float* inten, const float* ranges, const float* cos_t,
+                        const float* sin_t, int32_t rows, int32_t bins, float thr,
+                        int32_t stride, float* x, float* y, float* z, int64_t capacity,
+                        int64_t* n_out_host, hipStream_t st);
+int32_t polar_to_cartesian(const float* cos_t, const float* sin_t, const float* ranges,
+                           int64_t rows, int64_t bins, float* x, float* y, hipStream_t st);
+int32_t infer_time_from_colors(const uint8_t* colors, int64_t n, const float* pal, int32_t n_pal,
+                               float* out, hipStream_t st);
+int32_t synth_echo(const rpt_synth_params* p, int64_t frame0, int64_t n_frames,
+                   const float* cos_t, const float* sin_t, const uint32_t* clutter_thresh,
+                   const float* targets, const int32_t* trows, const int32_t* tbins,
+                   uint8_t* echo, hipStream_t st);
+int32_t bounds_xy(const float* x, const float* y, int64_t n, float* out4, hipStream_t st);
+int32_t land_grid(const float* x, const float* y, const float* val, int64_t n, const double* xe,
+                  int32_t nxe, const double* ye, int32_t nye, int32_t* cnt, double* tot,
+                  hipStream_t st);
+int32_t land_mask(const int32_t* cnt, const double* tot, int64_t cells, int64_t num_frames,
+                  double pthr, double ithr, uint8_t* land, int64_t* n_land_host,
+                  hipStream_t st);
+int32_t land_filter(const float* x, const float* y, const float* v, const int32_t* g,
+                    const int32_t* pf, int64_t n, const int64_t* frame_off, int32_t n_frames,
+                    const double* xe, int32_t nxe, const double* ye, int32_t nye,
+                    const uint8_t* land, float* xo, float* yo, float* vo, int32_t* go,
+                    int32_t* pfo, int64_t* new_off, int64_t* n_kept_host, hipStream_t st);
+int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
+                          const float* inten, const int32_t* pf, int64_t n, int32_t n_frames,
+                          int32_t n_clusters, int32_t* o_frame, int32_t* o_label,
+                          int64_t* o_count, int64_t* o_first, float* o_cx, float* o_cy,
+                          float* o_mi, int64_t* frame_first_noise, int64_t* n_seg_host,
+                          hipStream_t st);
 }  // namespace rpt
 
 extern "C" {
@@ -41,6 +80,114 @@ int32_t rpt_stdbscan(const float* x, const float* y, const float* z, int64_t str
   const int dim = z ? 3 : 2;
   return rpt::stdbscan(x, y, z, stride, times, n, eps_space, eps_time, min_samples, labels,
                        stats, rpt::as_stream(stream), dim);
+}
+
+int32_t rpt_polar_count(const void* echo, int32_t echo_dtype, int64_t n_files, int32_t rows,
+                        int32_t bins, float threshold, int32_t stride, int64_t* row_prefix,
+                        int64_t* file_offsets, int64_t* total_host, void* stream) {
+  rpt::clear_error();
+  return rpt::polar_count(echo, echo_dtype, n_files, rows, bins, threshold, stride, row_prefix,
+                          file_offsets, total_host, rpt::as_stream(stream));
+}
+
+int32_t rpt_polar_write(const void* echo, int32_t echo_dtype, int64_t n_files, int32_t rows,
+                        int32_t bins, const float* scale, const float* cos_t, const float* sin_t,
+                        const int32_t* gain, float threshold, int32_t stride,
+                        const int64_t* row_prefix, const int64_t* file_offsets,
+                        int32_t files_per_frame, float* x, float* y, float* intensity,
+                        int32_t* gain_out, int32_t* point_frame_out, void* stream) {
+  rpt::clear_error();
+  return rpt::polar_write(echo, echo_dtype, n_files, rows, bins, scale, cos_t, sin_t, gain,
+                          threshold, stride, row_prefix, file_offsets, files_per_frame, x, y,
+                          intensity, gain_out, point_frame_out, rpt::as_stream(stream));
+}
+
+int32_t rpt_frame_times(const int32_t* point_frame, int64_t n, const int64_t* frame_ids,
+                        float* times_out, void* stream) {
+  rpt::clear_error();
+  return rpt::frame_times(point_frame, n, frame_ids, times_out, rpt::as_stream(stream));
+}
+
+int32_t rpt_sweep_to_points(const float* intensities, const float* ranges, const float* cos_t,
+                            const float* sin_t, int32_t rows, int32_t bins, float threshold,
+                            int32_t stride, float* x, float* y, float* z, int64_t capacity,
+                            int64_t* n_out_host, void* stream) {
+  rpt::clear_error();
+  return rpt::sweep_to_points(intensities, ranges, cos_t, sin_t, rows, bins, threshold, stride,
+                              x, y, z, capacity, n_out_host, rpt::as_stream(stream));
+}
+
+int32_t rpt_polar_to_cartesian(const float* cos_t, const float* sin_t, const float* ranges,
+                               int64_t rows, int64_t bins, float* x, float* y, void* stream) {
+  rpt::clear_error();
+  return rpt::polar_to_cartesian(cos_t, sin_t, ranges, rows, bins, x, y,
+                                 rpt::as_stream(stream));
+}
+
+int32_t rpt_bounds_xy(const float* x, const float* y, int64_t n, float* out4_host,
+                      void* stream) {
+  rpt::clear_error();
+  return rpt::bounds_xy(x, y, n, out4_host, rpt::as_stream(stream));
+}
+
+int32_t rpt_land_grid(const float* x, const float* y, const float* intensity, int64_t n,
+                      const double* x_edges, int32_t nxe, const double* y_edges, int32_t nye,
+                      int32_t* count_grid, double* intensity_grid, void* stream) {
+  rpt::clear_error();
+  return rpt::land_grid(x, y, intensity, n, x_edges, nxe, y_edges, nye, count_grid,
+                        intensity_grid, rpt::as_stream(stream));
+}
+
+int32_t rpt_land_mask(const int32_t* count_grid, const double* intensity_grid, int64_t cells,
+                      int64_t num_frames, double persistence_threshold, double min_intensity,
+                      uint8_t* land_mask, int64_t* land_cells_host, void* stream) {
+  rpt::clear_error();
+  return rpt::land_mask(count_grid, intensity_grid, cells, num_frames, persistence_threshold,
+                        min_intensity, land_mask, land_cells_host, rpt::as_stream(stream));
+}
+
+int32_t rpt_land_filter(const float* x, const float* y, const float* intensity,
+                        const int32_t* gain, const int32_t* point_frame, int64_t n,
+                        const int64_t* frame_offsets, int32_t n_frames, const double* x_edges,
+                        int32_t nxe, const double* y_edges, int32_t nye,
+                        const uint8_t* land_mask, float* x_out, float* y_out,
+                        float* intensity_out, int32_t* gain_out, int32_t* point_frame_out,
+                        int64_t* new_frame_offsets, int64_t* n_kept_host, void* stream) {
+  rpt::clear_error();
+  return rpt::land_filter(x, y, intensity, gain, point_frame, n, frame_offsets, n_frames,
+                          x_edges, nxe, y_edges, nye, land_mask, x_out, y_out, intensity_out,
+                          gain_out, point_frame_out, new_frame_offsets, n_kept_host,
+                          rpt::as_stream(stream));
+}
+
+int32_t rpt_infer_time_from_colors(const uint8_t* colors, int64_t n, const float* palette,
+                                   int32_t n_pal, float* times_out, void* stream) {
+  rpt::clear_error();
+  return rpt::infer_time_from_colors(colors, n, palette, n_pal, times_out,
+                                     rpt::as_stream(stream));
+}
+
+int32_t rpt_cluster_summaries(const int32_t* labels, const float* x, const float* y,
+                              const float* intensity, const int32_t* point_frame, int64_t n,
+                              int32_t n_frames, int32_t n_clusters, int32_t* seg_frame,
+                              int32_t* seg_label, int64_t* seg_count, int64_t* seg_first,
+                              float* seg_cx, float* seg_cy, float* seg_mean_i,
+                              int64_t* frame_first_noise, int64_t* n_segments_host,
+                              void* stream) {
+  rpt::clear_error();
+  return rpt::cluster_summaries(labels, x, y, intensity, point_frame, n, n_frames, n_clusters,
+                                seg_frame, seg_label, seg_count, seg_first, seg_cx, seg_cy,
+                                seg_mean_i, frame_first_noise, n_segments_host,
+                                rpt::as_stream(stream));
+}
+
+int32_t rpt_synth_echo(const rpt_synth_params* p, int64_t frame0, int64_t n_frames,
+                       const float* cos_t, const float* sin_t, const uint32_t* clutter_thresh,
+                       const float* targets, const int32_t* target_rows,
+                       const int32_t* target_bins, uint8_t* echo, void* stream) {
+  rpt::clear_error();
+  return rpt::synth_echo(p, frame0, n_frames, cos_t, sin_t, clutter_thresh, targets,
+                         target_rows, target_bins, echo, rpt::as_stream(stream));
 }
 
 }  // extern "C"

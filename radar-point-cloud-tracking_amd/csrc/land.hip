@@ -1,0 +1,277 @@
+// K2/K3: land (persistent background) filter.  Replaces build_occupancy_grid, identify_land_cells
+// and filter_land_from_frame (PointCloudWork/4_temporal_object_tracker.py:359-436).
+//
+// Grid semantics are numpy's: edges are the float64 np.arange(min, max + res, res) the host
+// builds from the float32 bounds (rpt_bounds_xy); a point's cell is
+// clip(searchsorted(edges, v, 'right') - 1, 0, n_edges - 2) — an exact binary search over the
+// edge array staged in LDS, so no floating-point re-derivation of the edges can disagree.
+// Counts are int32 atomics (order-free); intensity sums are float64 atomics, exact for the
+// integer echo values of the radar path (sums < 2^53), like np.add.at's sequential order.
+#include <cstring>
+
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace rpt {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kMaxEdges = 4096;  // LDS stage; larger grids fall back to global-memory search
+
+__device__ __forceinline__ uint32_t f2ord(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__global__ __launch_bounds__(kBlock) void k_bounds_xy(const float* __restrict__ x,
+                                                     const float* __restrict__ y, int64_t n,
+                                                     uint32_t* __restrict__ out) {
+  uint32_t mnx = 0xffffffffu, mxx = 0u, mny = 0xffffffffu, mxy = 0u;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t a = f2ord(x[i]), b = f2ord(y[i]);
+    mnx = min(mnx, a);
+    mxx = max(mxx, a);
+    mny = min(mny, b);
+    mxy = max(mxy, b);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    mnx = min(mnx, (uint32_t)__shfl_xor((int)mnx, off));
+    mxx = max(mxx, (uint32_t)__shfl_xor((int)mxx, off));
+    mny = min(mny, (uint32_t)__shfl_xor((int)mny, off));
+    mxy = max(mxy, (uint32_t)__shfl_xor((int)mxy, off));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(out + 0, mnx);
+    atomicMax(out + 1, mxx);
+    atomicMin(out + 2, mny);
+    atomicMax(out + 3, mxy);
+  }
+}
+
+__global__ void k_bounds_xy_init(uint32_t* o) {
+  o[0] = 0xffffffffu;
+  o[1] = 0u;
+  o[2] = 0xffffffffu;
+  o[3] = 0u;
+}
+
+// number of edges <= v  (np.searchsorted(edges, v, side='right'))
+__device__ __forceinline__ int count_le(const double* e, int ne, double v) {
+  int lo = 0, hi = ne;
+  while (lo < hi) {
+    const int m = (lo + hi) >> 1;
+    if (e[m] <= v)
+      lo = m + 1;
+    else
+      hi = m;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ int clip_idx(int c, int hi) { return c < 0 ? 0 : (c > hi ? hi : c); }
+
+// Stage both edge arrays in LDS when they fit.
+struct Edges {
+  const double* xe;
+  const double* ye;
+  int nxe, nye;
+};
+__device__ __forceinline__ Edges stage_edges(const double* xe, int nxe, const double* ye, int nye,
+                                             double* lds) {
+  Edges E{xe, ye, nxe, nye};
+  if (nxe + nye <= kMaxEdges) {
+    for (int i = threadIdx.x; i < nxe; i += blockDim.x) lds[i] = xe[i];
+    for (int i = threadIdx.x; i < nye; i += blockDim.x) lds[nxe + i] = ye[i];
+    __syncthreads();
+    E.xe = lds;
+    E.ye = lds + nxe;
+  }
+  return E;
+}
+
+__global__ __launch_bounds__(kBlock) void k_land_grid(const float* __restrict__ x,
+                                                     const float* __restrict__ y,
+                                                     const float* __restrict__ val, int64_t n,
+                                                     const double* __restrict__ xe, int nxe,
+                                                     const double* __restrict__ ye, int nye,
+                                                     int32_t* __restrict__ cnt,
+                                                     double* __restrict__ tot) {
+  __shared__ double lds[kMaxEdges];
+  const Edges E = stage_edges(xe, nxe, ye, nye, lds);
+  const int ny = nye - 1;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int ix = clip_idx(count_le(E.xe, nxe, (double)x[i]) - 1, nxe - 2);
+    const int iy = clip_idx(count_le(E.ye, nye, (double)y[i]) - 1, nye - 2);
+    const int64_t c = (int64_t)ix * ny + iy;
+    atomicAdd(cnt + c, 1);
+    atomicAdd(tot + c, (double)val[i]);
+  }
+}
+
+// identify_land_cells :400-408, all float64
+__global__ void k_land_mask(const int32_t* __restrict__ cnt, const double* __restrict__ tot,
+                            int64_t cells, double nf, double pthr, double ithr,
+                            uint8_t* __restrict__ land, int32_t* __restrict__ n_land) {
+  int local = 0;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < cells;
+       c += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t k = cnt[c];
+    const double pers = (double)k / nf;
+    const double avg = (k > 0) ? tot[c] / (double)k : 0.0;
+    const bool is_land = (pers >= pthr) && (avg >= ithr);
+    land[c] = is_land ? 1 : 0;
+    local += is_land ? 1 : 0;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) local += __shfl_xor(local, off);
+  if ((threadIdx.x & 63) == 0 && local) atomicAdd(n_land, local);
+}
+
+__global__ __launch_bounds__(kBlock) void k_land_keep(const float* __restrict__ x,
+                                                     const float* __restrict__ y, int64_t n,
+                                                     const double* __restrict__ xe, int nxe,
+                                                     const double* __restrict__ ye, int nye,
+                                                     const uint8_t* __restrict__ land,
+                                                     int32_t* __restrict__ keep) {
+  __shared__ double lds[kMaxEdges];
+  const Edges E = stage_edges(xe, nxe, ye, nye, lds);
+  const int ny = nye - 1;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int ix = clip_idx(count_le(E.xe, nxe, (double)x[i]) - 1, nxe - 2);
+    const int iy = clip_idx(count_le(E.ye, nye, (double)y[i]) - 1, nye - 2);
+    keep[i] = land[(int64_t)ix * ny + iy] ? 0 : 1;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_land_scatter(
+    const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ v,
+    const int32_t* __restrict__ g, const int32_t* __restrict__ pf, int64_t n,
+    const int32_t* __restrict__ keep, const int64_t* __restrict__ pos, float* __restrict__ xo,
+    float* __restrict__ yo, float* __restrict__ vo, int32_t* __restrict__ go,
+    int32_t* __restrict__ pfo) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (!keep[i]) continue;
+    const int64_t o = pos[i];
+    xo[o] = x[i];
+    yo[o] = y[i];
+    vo[o] = v[i];
+    if (go) go[o] = g[i];
+    if (pfo) pfo[o] = pf[i];
+  }
+}
+
+__global__ void k_new_offsets(const int64_t* __restrict__ pos, const int64_t* __restrict__ off,
+                              int n_frames, int64_t* __restrict__ out) {
+  for (int f = blockIdx.x * blockDim.x + threadIdx.x; f <= n_frames; f += gridDim.x * blockDim.x)
+    out[f] = pos[off[f]];
+}
+
+}  // namespace
+
+int32_t bounds_xy(const float* x, const float* y, int64_t n, float* out4, hipStream_t st) {
+  if (n <= 0) {
+    set_error("zero-size array to reduction operation minimum which has no identity");
+    return RPT_EEMPTY;
+  }
+  Scratch& sc = scratch();
+  RPT_TRY(sc.reserve(256, st));
+  uint32_t* d = sc.carve_n<uint32_t>(4);
+  hipLaunchKernelGGL(k_bounds_xy_init, dim3(1), dim3(1), 0, st, d);
+  hipLaunchKernelGGL(k_bounds_xy, dim3(grid_for(n, kBlock, 2048)), dim3(kBlock), 0, st, x, y, n,
+                     d);
+  RPT_CHECK_LAUNCH();
+  uint32_t h[4];
+  RPT_HIP(hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, st));
+  RPT_HIP(hipStreamSynchronize(st));
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t u = h[k];
+    const uint32_t v = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
+    std::memcpy(out4 + k, &v, 4);
+  }
+  return RPT_OK;
+}
+
+int32_t land_grid(const float* x, const float* y, const float* val, int64_t n, const double* xe,
+                  int32_t nxe, const double* ye, int32_t nye, int32_t* cnt, double* tot,
+                  hipStream_t st) {
+  if (nxe < 2 || nye < 2) {
+    set_error("rpt_land_grid: need at least two edges per axis");
+    return RPT_EINVAL;
+  }
+  const int64_t cells = (int64_t)(nxe - 1) * (nye - 1);
+  RPT_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t) * cells, st));
+  RPT_HIP(hipMemsetAsync(tot, 0, sizeof(double) * cells, st));
+  if (n == 0) return RPT_OK;
+  hipLaunchKernelGGL(k_land_grid, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, st, x, y,
+                     val, n, xe, nxe, ye, nye, cnt, tot);
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
+}
+
+int32_t land_mask(const int32_t* cnt, const double* tot, int64_t cells, int64_t num_frames,
+                  double pthr, double ithr, uint8_t* land, int64_t* n_land_host,
+                  hipStream_t st) {
+  Scratch& sc = scratch();
+  RPT_TRY(sc.reserve(256, st));
+  int32_t* d = sc.carve_n<int32_t>(1);
+  RPT_HIP(hipMemsetAsync(d, 0, sizeof(int32_t), st));
+  const double nf = (double)(num_frames > 1 ? num_frames : 1);
+  if (cells > 0) {
+    hipLaunchKernelGGL(k_land_mask, dim3(grid_for(cells, 256, 1024)), dim3(256), 0, st, cnt, tot,
+                       cells, nf, pthr, ithr, land, d);
+    RPT_CHECK_LAUNCH();
+  }
+  if (n_land_host) {
+    int32_t h = 0;
+    RPT_HIP(hipMemcpyAsync(&h, d, sizeof h, hipMemcpyDeviceToHost, st));
+    RPT_HIP(hipStreamSynchronize(st));
+    *n_land_host = h;
+  }
+  return RPT_OK;
+}
+
+int32_t land_filter(const float* x, const float* y, const float* v, const int32_t* g,
+                    const int32_t* pf, int64_t n, const int64_t* frame_off, int32_t n_frames,
+                    const double* xe, int32_t nxe, const double* ye, int32_t nye,
+                    const uint8_t* land, float* xo, float* yo, float* vo, int32_t* go,
+                    int32_t* pfo, int64_t* new_off, int64_t* n_kept_host, hipStream_t st) {
+  Scratch& sc = scratch();
+  Budget b;
+  b.add<int32_t>(n + 1);
+  b.add<int64_t>(n + 1);
+  b.add<int64_t>(scan_tmp_elems(n + 1));
+  RPT_TRY(sc.reserve(b.bytes, st));
+  int32_t* keep = sc.carve_n<int32_t>(n + 1);
+  int64_t* pos = sc.carve_n<int64_t>(n + 1);
+  int64_t* tmp = sc.carve_n<int64_t>(scan_tmp_elems(n + 1));
+  RPT_HIP(hipMemsetAsync(keep + n, 0, sizeof(int32_t), st));
+  if (n > 0) {
+    hipLaunchKernelGGL(k_land_keep, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, st, x, y,
+                       n, xe, nxe, ye, nye, land, keep);
+    RPT_CHECK_LAUNCH();
+  }
+  RPT_TRY(exclusive_scan_i32_to_i64(keep, pos, n + 1, tmp, st));
+  if (n > 0) {
+    hipLaunchKernelGGL(k_land_scatter, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, st, x,
+                       y, v, g, pf, n, keep, pos, xo, yo, vo, go, pfo);
+    RPT_CHECK_LAUNCH();
+  }
+  if (new_off && frame_off) {
+    hipLaunchKernelGGL(k_new_offsets, dim3(grid_for(n_frames + 1, 256, 64)), dim3(256), 0, st,
+                       pos, frame_off, n_frames, new_off);
+    RPT_CHECK_LAUNCH();
+  }
+  if (n_kept_host) {
+    RPT_HIP(hipMemcpyAsync(n_kept_host, pos + n, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    RPT_HIP(hipStreamSynchronize(st));
+  }
+  return RPT_OK;
+}
+
+}  // namespace rpt

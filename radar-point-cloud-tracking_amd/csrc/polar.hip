@@ -116,8 +116,9 @@ template <class T, bool VEC>
 __global__ __launch_bounds__(kBlock) void k_row_write(
     const T* __restrict__ echo, int64_t n_rows, int rows, int bins, float thr, int stride,
     RowGeo geo, const int32_t* __restrict__ gain, const int64_t* __restrict__ row_prefix,
-    const int64_t* __restrict__ file_offsets, float* __restrict__ x, float* __restrict__ y,
-    float* __restrict__ val, int32_t* __restrict__ gain_out) {
+    const int64_t* __restrict__ file_offsets, int files_per_frame, float* __restrict__ x,
+    float* __restrict__ y, float* __restrict__ val, int32_t* __restrict__ gain_out,
+    int32_t* __restrict__ pf_out) {
   const int lane = threadIdx.x & 63;
   const int64_t wave0 = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / 64;
   const int64_t n_waves = (int64_t)gridDim.x * kWavesPerBlock;
@@ -130,6 +131,7 @@ __global__ __launch_bounds__(kBlock) void k_row_write(
     const float step = geo.scale ? geo.scale[row] / fb : 0.f;
     const float ct = geo.cos_t[row], st = geo.sin_t[row];
     const int32_t g = gain ? gain[f] : 0;
+    const int32_t fr = (int32_t)(f / files_per_frame);
     auto emit = [&](int b, float v, int64_t r) {
       if (r % stride == 0) {
         const float rr = geo.ranges ? geo.ranges[row * bins + b] : step * (float)b;
@@ -138,6 +140,7 @@ __global__ __launch_bounds__(kBlock) void k_row_write(
         y[o] = rr * st;
         val[o] = v;
         if (gain_out) gain_out[o] = g;
+        if (pf_out) pf_out[o] = fr;
       }
     };
     if (VEC) {
@@ -180,7 +183,7 @@ int32_t count_impl(const T* echo, int64_t n_files, int rows, int bins, float thr
   const int64_t n_rows = n_files * rows;
   Scratch& sc = scratch();
   Budget b;
-  b.add<int32_t>(n_rows);
+  b.add<int32_t>(n_rows + 1);
   b.add<int64_t>(n_files + 1);
   b.add<int64_t>(scan_tmp_elems(n_rows + 1) + scan_tmp_elems(n_files + 1));
   RPT_TRY(sc.reserve(b.bytes, st));
@@ -214,21 +217,30 @@ int32_t count_impl(const T* echo, int64_t n_files, int rows, int bins, float thr
 template <class T>
 int32_t write_impl(const T* echo, int64_t n_files, int rows, int bins, float thr, int stride,
                    RowGeo geo, const int32_t* gain, const int64_t* row_prefix,
-                   const int64_t* file_offsets, float* x, float* y, float* v, int32_t* gout,
-                   hipStream_t st) {
+                   const int64_t* file_offsets, int fpf, float* x, float* y, float* v,
+                   int32_t* gout, int32_t* pf, hipStream_t st) {
   const int64_t n_rows = n_files * rows;
   const bool vec = (bins % (64 * Vec<T>::N) == 0) && ((uintptr_t)echo % 16 == 0);
   const int grid = grid_for(n_rows, kWavesPerBlock, 16384);
   if (vec)
     hipLaunchKernelGGL((k_row_write<T, true>), dim3(grid), dim3(kBlock), 0, st, echo, n_rows,
-                       rows, bins, thr, stride, geo, gain, row_prefix, file_offsets, x, y, v,
-                       gout);
+                       rows, bins, thr, stride, geo, gain, row_prefix, file_offsets, fpf, x, y,
+                       v, gout, pf);
   else
     hipLaunchKernelGGL((k_row_write<T, false>), dim3(grid), dim3(kBlock), 0, st, echo, n_rows,
-                       rows, bins, thr, stride, geo, gain, row_prefix, file_offsets, x, y, v,
-                       gout);
+                       rows, bins, thr, stride, geo, gain, row_prefix, file_offsets, fpf, x, y,
+                       v, gout, pf);
   RPT_CHECK_LAUNCH();
   return RPT_OK;
+}
+
+__global__ void k_frame_times(const int32_t* __restrict__ pf, int64_t n,
+                              const int64_t* __restrict__ ids, float* __restrict__ t) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t f = pf[i];
+    t[i] = (float)(ids ? ids[f] : (int64_t)f);
+  }
 }
 
 __global__ void k_polar_dense(const float* __restrict__ cos_t, const float* __restrict__ sin_t,
@@ -384,9 +396,13 @@ int32_t polar_count(const void* echo, int32_t dt, int64_t n_files, int32_t rows,
 int32_t polar_write(const void* echo, int32_t dt, int64_t n_files, int32_t rows, int32_t bins,
                     const float* scale, const float* cos_t, const float* sin_t,
                     const int32_t* gain, float thr, int32_t stride, const int64_t* row_prefix,
-                    const int64_t* file_offsets, float* x, float* y, float* v, int32_t* gout,
-                    hipStream_t st) {
+                    const int64_t* file_offsets, int32_t fpf, float* x, float* y, float* v,
+                    int32_t* gout, int32_t* pf, hipStream_t st) {
   if (n_files == 0) return RPT_OK;
+  if (fpf < 1) {
+    set_error("rpt_polar_write: files_per_frame must be >= 1");
+    return RPT_EINVAL;
+  }
   if (!echo || !scale || !cos_t || !sin_t || !row_prefix || !file_offsets || !x || !y || !v ||
       stride < 1) {
     set_error("rpt_polar_write: bad arguments");
@@ -395,10 +411,10 @@ int32_t polar_write(const void* echo, int32_t dt, int64_t n_files, int32_t rows,
   RowGeo geo{scale, nullptr, cos_t, sin_t};
   if (dt == RPT_ECHO_U8)
     return write_impl<uint8_t>((const uint8_t*)echo, n_files, rows, bins, thr, stride, geo, gain,
-                               row_prefix, file_offsets, x, y, v, gout, st);
+                               row_prefix, file_offsets, fpf, x, y, v, gout, pf, st);
   if (dt == RPT_ECHO_F32)
     return write_impl<float>((const float*)echo, n_files, rows, bins, thr, stride, geo, gain,
-                             row_prefix, file_offsets, x, y, v, gout, st);
+                             row_prefix, file_offsets, fpf, x, y, v, gout, pf, st);
   set_error("rpt_polar_write: unknown echo dtype %d", dt);
   return RPT_EINVAL;
 }
@@ -426,14 +442,21 @@ int32_t sweep_to_points(const float* inten, const float* ranges, const float* co
       s = RPT_EINVAL;
     } else {
       RowGeo geo{nullptr, ranges, cos_t, sin_t};
-      s = write_impl<float>(inten, 1, rows, bins, thr, stride, geo, nullptr, rp, fo, x, y, z,
-                            nullptr, st);
+      s = write_impl<float>(inten, 1, rows, bins, thr, stride, geo, nullptr, rp, fo, 1, x, y, z,
+                            nullptr, nullptr, st);
     }
   }
   (void)hipFreeAsync(rp, st);
   (void)hipFreeAsync(fo, st);
   *n_out_host = total;
   return s;
+}
+
+int32_t frame_times(const int32_t* pf, int64_t n, const int64_t* ids, float* t, hipStream_t st) {
+  if (n == 0) return RPT_OK;
+  hipLaunchKernelGGL(k_frame_times, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, pf, n, ids, t);
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
 }
 
 int32_t polar_to_cartesian(const float* cos_t, const float* sin_t, const float* ranges,

@@ -55,7 +55,7 @@ void* Scratch::carve(size_t bytes) {
 }
 
 void Scratch::release() {
-  if (base_) hipFree(base_);
+  if (base_) (void)hipFree(base_);
   base_ = nullptr;
   cap_ = off_ = 0;
 }
@@ -65,7 +65,7 @@ static std::vector<Scratch*> g_scratch;
 
 Scratch& scratch() {
   int dev = 0;
-  hipGetDevice(&dev);
+  (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(g_scratch_mu);
   if ((int)g_scratch.size() <= dev) g_scratch.resize(dev + 1, nullptr);
   if (!g_scratch[dev]) g_scratch[dev] = new Scratch();
@@ -74,7 +74,7 @@ Scratch& scratch() {
 
 void release_scratch_current() {
   int dev = 0;
-  hipGetDevice(&dev);
+  (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(g_scratch_mu);
   if ((int)g_scratch.size() > dev && g_scratch[dev]) g_scratch[dev]->release();
 }

@@ -1,0 +1,240 @@
+// K9: per-(frame, label) cluster summaries.  Replaces the per-frame Cluster extraction of
+// PointCloudWork/4_temporal_object_tracker.py:508-536 (Cluster :143-158).
+//
+// Reduction orders are numpy's, reproduced exactly:
+//   centroid       = np.mean(pts (k,2) float32, axis=0): sequential float32 sum in point order
+//                    starting from the first point, then one float32 division by k;
+//   mean_intensity = np.mean(I (k,) float32): np.add.reduce over 8192-element buffer chunks,
+//                    each chunk summed pairwise (numpy pairwise_sum: 8 accumulators up to 128
+//                    elements, halving split above), chunks accumulated sequentially, then a
+//                    float32 division by k.
+// Segments: a stable radix sort of (label+1, index) keeps each label's points in index order, so
+// every (label, frame) run is contiguous and ordered; one thread walks each run.
+#include <climits>
+
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace rpt {
+namespace {
+
+constexpr int kBlock = 256;
+
+__global__ void k_sum_keys(const int32_t* __restrict__ labels, int64_t n,
+                           uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                           const int32_t* __restrict__ pf,
+                           unsigned long long* __restrict__ first_noise) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t l = labels[i];
+    keys[i] = (uint32_t)(l + 1);  // noise (-1) -> 0, sorts first
+    vals[i] = (uint32_t)i;
+    if (l < 0) atomicMin(first_noise + pf[i], (unsigned long long)i);
+  }
+}
+
+// head[p] = 1 where a (label, frame) run starts among clustered points
+__global__ void k_heads(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
+                        const int32_t* __restrict__ pf, int64_t n, int32_t* __restrict__ head) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    int h = 0;
+    if (sk[p] != 0u) {
+      h = (p == 0) || sk[p] != sk[p - 1] || pf[sv[p]] != pf[sv[p - 1]];
+    }
+    head[p] = h;
+  }
+}
+
+__global__ void k_seg_starts(const int32_t* __restrict__ head, const int64_t* __restrict__ pos,
+                             int64_t n, int64_t* __restrict__ seg_start) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n;
+       p += (int64_t)gridDim.x * blockDim.x)
+    if (head[p]) seg_start[pos[p]] = p;
+}
+
+// numpy pairwise_sum over a[idx[b .. b+len)] (float32), iterative form of the recursion.
+__device__ float pairwise_f32(const float* __restrict__ val, const uint32_t* __restrict__ idx,
+                              int64_t b, int64_t len) {
+  // explicit stack of (begin, len, state); state 0 = fresh, 1 = left done (partial on vstack)
+  int64_t sb[48], sl[48];
+  int st[48];
+  float vs[48];
+  int sp = 0, vp = 0;
+  sb[0] = b;
+  sl[0] = len;
+  st[0] = 0;
+  sp = 1;
+  while (sp > 0) {
+    const int64_t bb = sb[sp - 1], ll = sl[sp - 1];
+    if (ll < 8) {
+      float r = 0.f;  // np: res = 0.; res += a[i]
+      for (int64_t i = 0; i < ll; ++i) r = r + val[idx[bb + i]];
+      --sp;
+      vs[vp++] = r;
+    } else if (ll <= 128) {
+      float r[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] = val[idx[bb + k]];
+      int64_t i = 8;
+      for (; i < ll - (ll % 8); i += 8) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] = r[k] + val[idx[bb + i + k]];
+      }
+      float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+      for (; i < ll; ++i) res = res + val[idx[bb + i]];
+      --sp;
+      vs[vp++] = res;
+    } else {
+      int64_t n2 = ll / 2;
+      n2 -= n2 % 8;
+      if (st[sp - 1] == 0) {
+        st[sp - 1] = 1;
+        sb[sp] = bb;  // left half first
+        sl[sp] = n2;
+        st[sp] = 0;
+        ++sp;
+      } else if (st[sp - 1] == 1) {
+        st[sp - 1] = 2;
+        sb[sp] = bb + n2;
+        sl[sp] = ll - n2;
+        st[sp] = 0;
+        ++sp;
+      } else {
+        const float right = vs[--vp];
+        const float left = vs[--vp];
+        --sp;
+        vs[vp++] = left + right;
+      }
+    }
+  }
+  return vs[0];
+}
+
+__global__ void k_summarize(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
+                            const int64_t* __restrict__ seg_start, int64_t n_seg, int64_t n,
+                            const float* __restrict__ x, const float* __restrict__ y,
+                            const float* __restrict__ inten, const int32_t* __restrict__ pf,
+                            int32_t* __restrict__ o_frame, int32_t* __restrict__ o_label,
+                            int64_t* __restrict__ o_count, int64_t* __restrict__ o_first,
+                            float* __restrict__ o_cx, float* __restrict__ o_cy,
+                            float* __restrict__ o_mi) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n_seg;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = seg_start[s];
+    const int64_t e = (s + 1 < n_seg) ? seg_start[s + 1] : n;
+    const int64_t k = e - b;
+    const uint32_t i0 = sv[b];
+    float sx = x[i0], sy = y[i0];
+    for (int64_t p = b + 1; p < e; ++p) {
+      const uint32_t i = sv[p];
+      sx = sx + x[i];
+      sy = sy + y[i];
+    }
+    const float fk = (float)k;
+    float tot = 0.f;
+    for (int64_t c = 0; c < k; c += 8192) {
+      const int64_t len = (k - c < 8192) ? (k - c) : 8192;
+      tot = tot + pairwise_f32(inten, sv, b + c, len);
+    }
+    o_frame[s] = pf[i0];
+    o_label[s] = (int32_t)sk[b] - 1;
+    o_count[s] = k;
+    o_first[s] = i0;
+    o_cx[s] = sx / fk;
+    o_cy[s] = sy / fk;
+    o_mi[s] = tot / fk;
+  }
+}
+
+__global__ void k_noise_finish(const unsigned long long* __restrict__ fn, int n_frames,
+                               int64_t* __restrict__ out) {
+  for (int f = blockIdx.x * blockDim.x + threadIdx.x; f < n_frames; f += gridDim.x * blockDim.x)
+    out[f] = (fn[f] == ~0ull) ? -1 : (int64_t)fn[f];
+}
+
+__global__ void k_fill_u64(unsigned long long* p, int64_t n, unsigned long long v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
+}  // namespace
+
+int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
+                          const float* inten, const int32_t* pf, int64_t n, int32_t n_frames,
+                          int32_t n_clusters, int32_t* o_frame, int32_t* o_label,
+                          int64_t* o_count, int64_t* o_first, float* o_cx, float* o_cy,
+                          float* o_mi, int64_t* frame_first_noise, int64_t* n_seg_host,
+                          hipStream_t st) {
+  if (n < 0 || n_frames < 0 || n_clusters < 0 || !n_seg_host) {
+    set_error("rpt_cluster_summaries: bad arguments");
+    return RPT_EINVAL;
+  }
+  if (n >= (int64_t(1) << 32) - 1) {
+    set_error("rpt_cluster_summaries: n exceeds the u32 index space");
+    return RPT_ENOTSUP;
+  }
+  Scratch& sc = scratch();
+  Budget b;
+  for (int k = 0; k < 4; ++k) b.add<uint32_t>(n + 1);
+  b.add<int64_t>(radix_tmp_elems(n));
+  b.add<int32_t>(n + 1);
+  b.add<int64_t>(n + 1);
+  b.add<int64_t>(n + 1);
+  b.add<int64_t>(scan_tmp_elems(n + 1));
+  b.add<unsigned long long>(n_frames + 1);
+  RPT_TRY(sc.reserve(b.bytes, st));
+  uint32_t* keys = sc.carve_n<uint32_t>(n + 1);
+  uint32_t* vals = sc.carve_n<uint32_t>(n + 1);
+  uint32_t* ka = sc.carve_n<uint32_t>(n + 1);
+  uint32_t* va = sc.carve_n<uint32_t>(n + 1);
+  int64_t* rtmp = sc.carve_n<int64_t>(radix_tmp_elems(n));
+  int32_t* head = sc.carve_n<int32_t>(n + 1);
+  int64_t* pos = sc.carve_n<int64_t>(n + 1);
+  int64_t* seg_start = sc.carve_n<int64_t>(n + 1);
+  int64_t* tmp = sc.carve_n<int64_t>(scan_tmp_elems(n + 1));
+  unsigned long long* fn = sc.carve_n<unsigned long long>(n_frames + 1);
+  if (n_frames > 0)
+    hipLaunchKernelGGL(k_fill_u64, dim3(grid_for(n_frames, 256, 64)), dim3(256), 0, st, fn,
+                       (int64_t)n_frames, ~0ull);
+  if (n == 0) {
+    *n_seg_host = 0;
+    if (n_frames > 0 && frame_first_noise)
+      hipLaunchKernelGGL(k_noise_finish, dim3(grid_for(n_frames, 256, 64)), dim3(256), 0, st,
+                         fn, n_frames, frame_first_noise);
+    RPT_CHECK_LAUNCH();
+    return RPT_OK;
+  }
+  const int g = grid_for(n, kBlock, 8192);
+  hipLaunchKernelGGL(k_sum_keys, dim3(g), dim3(kBlock), 0, st, labels, n, keys, vals, pf, fn);
+  RPT_CHECK_LAUNCH();
+  int bits = 1;
+  while ((int64_t(1) << bits) <= (int64_t)n_clusters) ++bits;
+  uint32_t *sk, *sv;
+  RPT_TRY(radix_sort_pairs(keys, vals, ka, va, n, bits, rtmp, &sk, &sv, st));
+  hipLaunchKernelGGL(k_heads, dim3(g), dim3(kBlock), 0, st, sk, sv, pf, n, head);
+  RPT_HIP(hipMemsetAsync(head + n, 0, sizeof(int32_t), st));
+  RPT_TRY(exclusive_scan_i32_to_i64(head, pos, n + 1, tmp, st));
+  hipLaunchKernelGGL(k_seg_starts, dim3(g), dim3(kBlock), 0, st, head, pos, n, seg_start);
+  RPT_CHECK_LAUNCH();
+  int64_t n_seg = 0;
+  RPT_HIP(hipMemcpyAsync(&n_seg, pos + n, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  RPT_HIP(hipStreamSynchronize(st));
+  if (n_seg > 0) {
+    hipLaunchKernelGGL(k_summarize, dim3(grid_for(n_seg, 64, 8192)), dim3(64), 0, st, sk, sv,
+                       seg_start, n_seg, n, x, y, inten, pf, o_frame, o_label, o_count, o_first,
+                       o_cx, o_cy, o_mi);
+    RPT_CHECK_LAUNCH();
+  }
+  if (n_frames > 0 && frame_first_noise) {
+    hipLaunchKernelGGL(k_noise_finish, dim3(grid_for(n_frames, 256, 64)), dim3(256), 0, st, fn,
+                       n_frames, frame_first_noise);
+    RPT_CHECK_LAUNCH();
+  }
+  *n_seg_host = n_seg;
+  return RPT_OK;
+}
+
+}  // namespace rpt

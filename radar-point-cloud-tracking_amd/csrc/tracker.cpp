@@ -1,0 +1,564 @@
+// Host-side sequential stage of the path: per-frame cluster order,
+// Hungarian association and object state.  Replaces ObjectTracker / TrackedObject of
+// PointCloudWork/4_temporal_object_tracker.py:111-140, 543-688 and the cluster ordering of
+// :519-522, reproducing the reference's numerics exactly:
+//
+//  * cluster order in a frame = CPython 3.10 `set` iteration order of the frame's labels
+//    inserted in first-occurrence order (np.int32 hash = value, hash(-1) = -2), -1 discarded;
+//  * linear_sum_assignment = scipy 1.15 rectangular LSAP (shortest augmenting path, Crouse
+//    2016) including its tie-breaking (remaining columns scanned in reverse order, a tie on the
+//    minimum prefers an unassigned column) and the transpose for tall matrices;
+//  * TrackedObject.predict_position: mean of the last 5 velocities — float64 while the initial
+//    float64 zero velocity is in the window, float32 afterwards (numpy result-type promotion);
+//    the cost is np.linalg.norm: float64 dot (OpenBLAS ddot: sqrt(fma(dy,dy,dx*dx))) or float32
+//    dot (sdot: sqrtf(dx*dx + dy*dy), no FMA) — both measured against the reference in
+//    tests/golden/g5_tracker.npz;
+//  * velocities (c - last) / frames_elapsed in float32; average_velocity = mean of norms
+//    (float64 mean when the window holds the float64 zero, float32 otherwise).
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <numeric>
+#include <vector>
+
+#include "common.h"
+
+#pragma STDC FP_CONTRACT OFF
+
+namespace rpt {
+
+// ------------------------------------------------------------------ CPython set emulation
+namespace {
+
+struct PySetEmu {
+  struct Entry {
+    int64_t hash;
+    int32_t key;
+    bool used;
+  };
+  std::vector<Entry> table;
+  size_t mask = 7, fill = 0, used = 0;
+  PySetEmu() : table(8, Entry{0, 0, false}) {}
+
+  static int64_t hash_of(int32_t v) { return v == -1 ? -2 : (int64_t)v; }
+
+  static void insert_clean(std::vector<Entry>& t, size_t mask, int32_t key, int64_t hash) {
+    size_t perturb = (size_t)hash;
+    size_t i = (size_t)hash & mask;
+    while (true) {
+      Entry* e = &t[i];
+      if (!e->used) {
+        *e = Entry{hash, key, true};
+        return;
+      }
+      if (i + 9 <= mask) {
+        for (int j = 0; j < 9; ++j) {
+          ++e;
+          if (!e->used) {
+            *e = Entry{hash, key, true};
+            return;
+          }
+        }
+      }
+      perturb >>= 5;
+      i = (i * 5 + 1 + perturb) & mask;
+    }
+  }
+
+  void resize(size_t minused) {
+    size_t newsize = 8;
+    while (newsize <= minused) newsize <<= 1;
+    std::vector<Entry> nt(newsize, Entry{0, 0, false});
+    for (const Entry& e : table)
+      if (e.used) insert_clean(nt, newsize - 1, e.key, e.hash);
+    table.swap(nt);
+    mask = newsize - 1;
+    fill = used;
+  }
+
+  // set_add_entry for a key known to be absent (distinct first-occurrence sequence)
+  void add(int32_t key) {
+    const int64_t hash = hash_of(key);
+    size_t perturb = (size_t)hash;
+    size_t i = (size_t)hash & mask;
+    Entry* e = &table[i];
+    while (true) {
+      if (!e->used) break;
+      if (e->hash == hash && e->key == key) return;
+      if (i + 9 <= mask) {
+        bool found = false;
+        for (int j = 0; j < 9; ++j) {
+          ++e;
+          if (!e->used) {
+            found = true;
+            break;
+          }
+          if (e->hash == hash && e->key == key) return;
+        }
+        if (found) break;
+      }
+      perturb >>= 5;
+      i = (i * 5 + 1 + perturb) & mask;
+      e = &table[i];
+    }
+    *e = Entry{hash, key, true};
+    ++fill;
+    ++used;
+    if (fill * 5 >= mask * 3) resize(used > 50000 ? used * 2 : used * 4);
+  }
+};
+
+}  // namespace
+
+int32_t set_order(const int32_t* keys, int32_t n, int32_t* out) {
+  PySetEmu s;
+  for (int32_t i = 0; i < n; ++i) s.add(keys[i]);
+  int32_t m = 0;
+  for (const auto& e : s.table)
+    if (e.used && e.key != -1) out[m++] = e.key;
+  return m;
+}
+
+int32_t order_clusters(int32_t n_frames, int64_t n_seg, const int32_t* seg_frame,
+                       const int32_t* seg_label, const int64_t* seg_first,
+                       const int64_t* frame_first_noise, int64_t* frame_off, int64_t* order) {
+  // bucket segments by frame
+  std::vector<int64_t> cnt(n_frames + 1, 0);
+  for (int64_t s = 0; s < n_seg; ++s) {
+    if (seg_frame[s] < 0 || seg_frame[s] >= n_frames) {
+      set_error("rpt_order_clusters: segment frame %d out of range", seg_frame[s]);
+      return RPT_EINVAL;
+    }
+    ++cnt[seg_frame[s] + 1];
+  }
+  for (int32_t f = 0; f < n_frames; ++f) cnt[f + 1] += cnt[f];
+  for (int32_t f = 0; f <= n_frames; ++f) frame_off[f] = cnt[f];
+  std::vector<int64_t> byf(n_seg);
+  std::vector<int64_t> cur(cnt.begin(), cnt.end() - 1);
+  for (int64_t s = 0; s < n_seg; ++s) byf[cur[seg_frame[s]]++] = s;
+  std::vector<std::pair<int64_t, int32_t>> occ;  // (first index, label)
+  std::vector<int32_t> keys, ord;
+  std::vector<int64_t> lab2seg;
+  for (int32_t f = 0; f < n_frames; ++f) {
+    const int64_t b = cnt[f], e = cnt[f + 1];
+    occ.clear();
+    for (int64_t q = b; q < e; ++q) occ.emplace_back(seg_first[byf[q]], seg_label[byf[q]]);
+    if (frame_first_noise && frame_first_noise[f] >= 0) occ.emplace_back(frame_first_noise[f], -1);
+    std::sort(occ.begin(), occ.end());
+    keys.resize(occ.size());
+    for (size_t q = 0; q < occ.size(); ++q) keys[q] = occ[q].second;
+    ord.resize(occ.size());
+    const int32_t m = set_order(keys.data(), (int32_t)keys.size(), ord.data());
+    // label -> segment (labels are unique within a frame)
+    std::vector<std::pair<int32_t, int64_t>> l2s;
+    l2s.reserve(e - b);
+    for (int64_t q = b; q < e; ++q) l2s.emplace_back(seg_label[byf[q]], byf[q]);
+    std::sort(l2s.begin(), l2s.end());
+    for (int32_t q = 0; q < m; ++q) {
+      auto it = std::lower_bound(l2s.begin(), l2s.end(), std::make_pair(ord[q], int64_t(-1)));
+      order[b + q] = it->second;
+    }
+  }
+  return RPT_OK;
+}
+
+// ------------------------------------------------------------------ scipy LSAP
+namespace {
+
+int64_t augmenting_path(int64_t nc, const double* cost, std::vector<double>& u,
+                        std::vector<double>& v, std::vector<int64_t>& path,
+                        std::vector<int64_t>& row4col, std::vector<double>& spc, int64_t i,
+                        std::vector<char>& SR, std::vector<char>& SC,
+                        std::vector<int64_t>& remaining, double* p_min) {
+  double minVal = 0;
+  int64_t num_remaining = nc;
+  for (int64_t it = 0; it < nc; ++it) remaining[it] = nc - it - 1;
+  std::fill(SR.begin(), SR.end(), 0);
+  std::fill(SC.begin(), SC.end(), 0);
+  std::fill(spc.begin(), spc.end(), std::numeric_limits<double>::infinity());
+  int64_t sink = -1;
+  while (sink == -1) {
+    int64_t index = -1;
+    double lowest = std::numeric_limits<double>::infinity();
+    SR[i] = 1;
+    for (int64_t it = 0; it < num_remaining; ++it) {
+      const int64_t j = remaining[it];
+      const double r = minVal + cost[i * nc + j] - u[i] - v[j];
+      if (r < spc[j]) {
+        path[j] = i;
+        spc[j] = r;
+      }
+      if (spc[j] < lowest || (spc[j] == lowest && row4col[j] == -1)) {
+        lowest = spc[j];
+        index = it;
+      }
+    }
+    minVal = lowest;
+    if (minVal == std::numeric_limits<double>::infinity()) return -1;
+    const int64_t j = remaining[index];
+    if (row4col[j] == -1)
+      sink = j;
+    else
+      i = row4col[j];
+    SC[j] = 1;
+    remaining[index] = remaining[--num_remaining];
+  }
+  *p_min = minVal;
+  return sink;
+}
+
+}  // namespace
+
+int32_t lsap(const double* cost_in, int32_t nr_in, int32_t nc_in, int64_t* a, int64_t* b) {
+  int64_t nr = nr_in, nc = nc_in;
+  if (nr == 0 || nc == 0) return RPT_OK;
+  const bool transpose = nc < nr;
+  std::vector<double> tmp;
+  const double* cost = cost_in;
+  if (transpose) {
+    tmp.resize(nr * nc);
+    for (int64_t i = 0; i < nr; ++i)
+      for (int64_t j = 0; j < nc; ++j) tmp[j * nr + i] = cost_in[i * nc + j];
+    std::swap(nr, nc);
+    cost = tmp.data();
+  }
+  for (int64_t i = 0; i < nr * nc; ++i) {
+    if (cost[i] != cost[i] || cost[i] == -std::numeric_limits<double>::infinity()) {
+      set_error("matrix contains invalid numeric entries");
+      return RPT_EINVAL;
+    }
+  }
+  std::vector<double> u(nr, 0), v(nc, 0), spc(nc);
+  std::vector<int64_t> path(nc, -1), col4row(nr, -1), row4col(nc, -1), remaining(nc);
+  std::vector<char> SR(nr), SC(nc);
+  for (int64_t cur = 0; cur < nr; ++cur) {
+    double minVal;
+    const int64_t sink =
+        augmenting_path(nc, cost, u, v, path, row4col, spc, cur, SR, SC, remaining, &minVal);
+    if (sink < 0) {
+      set_error("cost matrix is infeasible");
+      return RPT_EINVAL;
+    }
+    u[cur] += minVal;
+    for (int64_t i = 0; i < nr; ++i)
+      if (SR[i] && i != cur) u[i] += minVal - spc[col4row[i]];
+    for (int64_t j = 0; j < nc; ++j)
+      if (SC[j]) v[j] -= minVal - spc[j];
+    int64_t j = sink;
+    while (true) {
+      const int64_t i = path[j];
+      row4col[j] = i;
+      std::swap(col4row[i], j);
+      if (i == cur) break;
+    }
+  }
+  if (transpose) {
+    std::vector<int64_t> idx(nr);
+    std::iota(idx.begin(), idx.end(), 0);
+    std::sort(idx.begin(), idx.end(), [&](int64_t p, int64_t q) { return col4row[p] < col4row[q]; });
+    for (int64_t k = 0; k < nr; ++k) {
+      a[k] = col4row[idx[k]];
+      b[k] = idx[k];
+    }
+  } else {
+    for (int64_t k = 0; k < nr; ++k) {
+      a[k] = k;
+      b[k] = col4row[k];
+    }
+  }
+  return RPT_OK;
+}
+
+// ------------------------------------------------------------------ tracker
+namespace {
+
+enum { kUnknown = 0, kBuoy = 1, kBoat = 2 };
+
+struct Vel {
+  float x, y;
+  bool f64_zero;  // the float64 [0, 0] every object starts with
+};
+
+struct Object {
+  int64_t id;
+  int type = kUnknown;
+  std::vector<float> px, py;
+  std::vector<int64_t> frames;
+  int64_t last_seen;
+  std::vector<Vel> vel;
+  int color[3];
+};
+
+inline float f32_norm(float x, float y) {  // np.linalg.norm float32: sdot without FMA
+  const float xx = x * x;
+  const float yy = y * y;
+  return std::sqrt(xx + yy);
+}
+inline double f64_norm(double x, double y) {  // np.linalg.norm float64: ddot with FMA
+  return std::sqrt(std::fma(y, y, x * x));
+}
+
+}  // namespace
+
+struct Tracker {
+  rpt_tracker_params p;
+  std::vector<Object> objs;  // insertion (= id) order, like the reference dict
+  int64_t next_id = 1;
+  int64_t current = 0;
+  // scratch
+  std::vector<double> cost;
+  std::vector<int64_t> ra, ca;
+  std::vector<int> live;
+
+  static void color_of(int64_t oid, int* rgb) {  // _generate_color :666-688 (float64)
+    const double hue = std::fmod((double)oid * 0.618033988749895, 1.0);
+    const int h_i = (int)(hue * 6);
+    const double f = hue * 6 - h_i;
+    const double q = 1 - f;
+    double r, g, b;
+    switch (h_i) {
+      case 0: r = 1; g = f; b = 0; break;
+      case 1: r = q; g = 1; b = 0; break;
+      case 2: r = 0; g = 1; b = f; break;
+      case 3: r = 0; g = q; b = 1; break;
+      case 4: r = f; g = 0; b = 1; break;
+      default: r = 1; g = 0; b = q; break;
+    }
+    rgb[0] = (int)(r * 255);
+    rgb[1] = (int)(g * 255);
+    rgb[2] = (int)(b * 255);
+  }
+
+  void create(float cx, float cy, int64_t fid) {
+    Object o;
+    o.id = next_id;
+    o.px.push_back(cx);
+    o.py.push_back(cy);
+    o.frames.push_back(fid);
+    o.last_seen = fid;
+    o.vel.push_back(Vel{0.f, 0.f, true});
+    color_of(next_id, o.color);
+    objs.push_back(std::move(o));
+    ++next_id;
+  }
+
+  // average_velocity :127-133; returns value and whether numpy yields float32
+  double avg_velocity(const Object& o, bool* is_f32) const {
+    *is_f32 = false;
+    if (o.vel.size() < 2) return 0.0;
+    const size_t H = (size_t)p.motion_history_frames;
+    const size_t b = o.vel.size() > H ? o.vel.size() - H : 0;
+    bool has64 = false;
+    for (size_t k = b; k < o.vel.size(); ++k) has64 |= o.vel[k].f64_zero;
+    const size_t m = o.vel.size() - b;
+    if (has64) {  // np.mean over float64 array (< 8 values: sequential from 0.)
+      double s = 0.0;
+      for (size_t k = b; k < o.vel.size(); ++k)
+        s = s + (o.vel[k].f64_zero ? 0.0 : (double)f32_norm(o.vel[k].x, o.vel[k].y));
+      return s / (double)m;
+    }
+    float s = 0.f;
+    for (size_t k = b; k < o.vel.size(); ++k) s = s + f32_norm(o.vel[k].x, o.vel[k].y);
+    *is_f32 = true;
+    return (double)(s / (float)m);
+  }
+
+  // cost of cluster (cx,cy) vs object prediction (:135-140, :586-587)
+  double cost_of(const Object& o, float cx, float cy, int64_t ahead) const {
+    const size_t H = (size_t)p.motion_history_frames;
+    const size_t b = o.vel.size() > H ? o.vel.size() - H : 0;
+    const size_t m = o.vel.size() - b;
+    bool has64 = false;
+    for (size_t k = b; k < o.vel.size(); ++k) has64 |= o.vel[k].f64_zero;
+    const float lx = o.px.back(), ly = o.py.back();
+    if (has64) {
+      // np.mean(axis=0) float64: first row then sequential adds, one division
+      double sx = o.vel[b].f64_zero ? 0.0 : (double)o.vel[b].x;
+      double sy = o.vel[b].f64_zero ? 0.0 : (double)o.vel[b].y;
+      for (size_t k = b + 1; k < o.vel.size(); ++k) {
+        sx = sx + (o.vel[k].f64_zero ? 0.0 : (double)o.vel[k].x);
+        sy = sy + (o.vel[k].f64_zero ? 0.0 : (double)o.vel[k].y);
+      }
+      const double mx = sx / (double)m, my = sy / (double)m;
+      const double px = (double)lx + mx * (double)ahead;
+      const double py = (double)ly + my * (double)ahead;
+      return f64_norm((double)cx - px, (double)cy - py);
+    }
+    float sx = o.vel[b].x, sy = o.vel[b].y;
+    for (size_t k = b + 1; k < o.vel.size(); ++k) {
+      sx = sx + o.vel[k].x;
+      sy = sy + o.vel[k].y;
+    }
+    const float mx = sx / (float)m, my = sy / (float)m;
+    const float px = lx + mx * (float)ahead;
+    const float py = ly + my * (float)ahead;
+    return (double)f32_norm(cx - px, cy - py);
+  }
+
+  void cleanup() {
+    std::vector<Object> keep;
+    keep.reserve(objs.size());
+    for (auto& o : objs)
+      if (!(current - o.last_seen > p.max_missed_frames)) keep.push_back(std::move(o));
+    objs.swap(keep);
+  }
+
+  int32_t update(int64_t fid, int32_t k, const float* cx, const float* cy, const int64_t* cfid) {
+    current = fid;
+    if (k == 0) {
+      cleanup();
+      return (int32_t)objs.size();
+    }
+    if (objs.empty()) {
+      for (int32_t i = 0; i < k; ++i) create(cx[i], cy[i], cfid ? cfid[i] : fid);
+      return (int32_t)objs.size();
+    }
+    live.clear();
+    for (int q = 0; q < (int)objs.size(); ++q)
+      if (fid - objs[q].last_seen <= p.max_missed_frames) live.push_back(q);
+    if (live.empty()) {
+      for (int32_t i = 0; i < k; ++i) create(cx[i], cy[i], cfid ? cfid[i] : fid);
+      return (int32_t)objs.size();
+    }
+    const int32_t m = (int32_t)live.size();
+    cost.assign((size_t)k * m, 0.0);
+    for (int32_t j = 0; j < m; ++j) {
+      const Object& o = objs[live[j]];
+      const int64_t ahead = fid - o.last_seen;
+      for (int32_t i = 0; i < k; ++i) cost[(size_t)i * m + j] = cost_of(o, cx[i], cy[i], ahead);
+    }
+    const int32_t np_ = std::min(k, m);
+    ra.assign(np_, 0);
+    ca.assign(np_, 0);
+    const int32_t ls = lsap(cost.data(), k, m, ra.data(), ca.data());
+    if (ls != RPT_OK) return -ls;  // negative = error (counts are >= 0)
+    std::vector<char> assigned(k, 0);
+    for (int32_t q = 0; q < np_; ++q) {
+      const int64_t i = ra[q], j = ca[q];
+      if (cost[(size_t)i * m + j] <= p.max_association_distance) {
+        Object& o = objs[live[j]];
+        const int64_t fe = fid - o.last_seen;
+        if (fe > 0) {
+          const float fef = (float)fe;
+          o.vel.push_back(Vel{(cx[i] - o.px.back()) / fef, (cy[i] - o.py.back()) / fef, false});
+        }
+        o.px.push_back(cx[i]);
+        o.py.push_back(cy[i]);
+        o.frames.push_back(fid);
+        o.last_seen = fid;
+        if ((int)o.vel.size() < p.motion_history_frames) {
+          o.type = kUnknown;
+        } else {
+          bool f32;
+          const double av = avg_velocity(o, &f32);
+          o.type = (av < p.stationary_velocity_threshold) ? kBuoy : kBoat;
+        }
+        assigned[i] = 1;
+      }
+    }
+    for (int32_t i = 0; i < k; ++i)
+      if (!assigned[i]) create(cx[i], cy[i], cfid ? cfid[i] : fid);
+    cleanup();
+    return (int32_t)objs.size();
+  }
+};
+
+}  // namespace rpt
+
+using rpt::Tracker;
+
+extern "C" {
+
+struct rpt_tracker {
+  Tracker t;
+};
+
+int32_t rpt_set_order(const int32_t* keys, int32_t n, int32_t* order_out) {
+  return rpt::set_order(keys, n, order_out);
+}
+
+int32_t rpt_order_clusters(int32_t n_frames, int64_t n_segments, const int32_t* seg_frame,
+                           const int32_t* seg_label, const int64_t* seg_first,
+                           const int64_t* frame_first_noise, int64_t* frame_offsets_out,
+                           int64_t* order_out) {
+  rpt::clear_error();
+  return rpt::order_clusters(n_frames, n_segments, seg_frame, seg_label, seg_first,
+                             frame_first_noise, frame_offsets_out, order_out);
+}
+
+int32_t rpt_lsap(const double* cost, int32_t nr, int32_t nc, int64_t* rows_out,
+                 int64_t* cols_out) {
+  rpt::clear_error();
+  return rpt::lsap(cost, nr, nc, rows_out, cols_out);
+}
+
+rpt_tracker* rpt_tracker_new(const rpt_tracker_params* params) {
+  auto* h = new rpt_tracker();
+  if (params) {
+    h->t.p = *params;
+  } else {
+    h->t.p.max_association_distance = 50.0;
+    h->t.p.max_missed_frames = 10;
+    h->t.p.motion_history_frames = 5;
+    h->t.p.stationary_velocity_threshold = 1.0;
+  }
+  return h;
+}
+
+void rpt_tracker_free(rpt_tracker* t) { delete t; }
+
+int32_t rpt_tracker_update(rpt_tracker* t, int64_t frame_id, int32_t k, const float* cx,
+                           const float* cy, const int64_t* cluster_frame_id) {
+  rpt::clear_error();
+  return t->t.update(frame_id, k, cx, cy, cluster_frame_id);
+}
+
+int32_t rpt_tracker_run(rpt_tracker* t, int32_t n_frames, const int64_t* frame_ids,
+                        const int64_t* offsets, const float* cx, const float* cy) {
+  rpt::clear_error();
+  int32_t r = 0;
+  for (int32_t f = 0; f < n_frames; ++f) {
+    const int64_t b = offsets[f];
+    const int32_t k = (int32_t)(offsets[f + 1] - b);
+    r = t->t.update(frame_ids[f], k, cx + b, cy + b, nullptr);
+    if (r < 0) return r;
+  }
+  return r;
+}
+
+int32_t rpt_tracker_num_objects(const rpt_tracker* t) { return (int32_t)t->t.objs.size(); }
+
+int32_t rpt_tracker_object_info(const rpt_tracker* t, int32_t idx, rpt_object_info* out) {
+  if (idx < 0 || idx >= (int32_t)t->t.objs.size()) return RPT_EINVAL;
+  const auto& o = t->t.objs[idx];
+  out->object_id = o.id;
+  out->object_type = o.type;
+  out->n_positions = (int32_t)o.px.size();
+  out->n_velocities = (int32_t)o.vel.size();
+  out->last_seen_frame = o.last_seen;
+  bool f32 = false;
+  out->average_velocity = t->t.avg_velocity(o, &f32);
+  out->average_velocity_is_f32 = f32 ? 1 : 0;
+  for (int c = 0; c < 3; ++c) out->color[c] = o.color[c];
+  return RPT_OK;
+}
+
+int32_t rpt_tracker_object_history(const rpt_tracker* t, int32_t idx, float* px, float* py,
+                                   int64_t* frames, double* vx, double* vy) {
+  if (idx < 0 || idx >= (int32_t)t->t.objs.size()) return RPT_EINVAL;
+  const auto& o = t->t.objs[idx];
+  for (size_t k = 0; k < o.px.size(); ++k) {
+    if (px) px[k] = o.px[k];
+    if (py) py[k] = o.py[k];
+    if (frames) frames[k] = o.frames[k];
+  }
+  for (size_t k = 0; k < o.vel.size(); ++k) {
+    if (vx) vx[k] = o.vel[k].f64_zero ? 0.0 : (double)o.vel[k].x;
+    if (vy) vy[k] = o.vel[k].f64_zero ? 0.0 : (double)o.vel[k].y;
+  }
+  return RPT_OK;
+}
+
+}  // extern "C"

@@ -96,7 +96,8 @@ _SIGS = [
      [vp, C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_float, C.c_int32, vp, vp, c_i64p, vp]),
     ("rpt_polar_write", C.c_int32,
      [vp, C.c_int32, C.c_int64, C.c_int32, C.c_int32, vp, vp, vp, vp, C.c_float, C.c_int32, vp,
-      vp, vp, vp, vp, vp, vp]),
+      vp, C.c_int32, vp, vp, vp, vp, vp, vp]),
+    ("rpt_frame_times", C.c_int32, [vp, C.c_int64, vp, vp, vp]),
     ("rpt_sweep_to_points", C.c_int32,
      [vp, vp, vp, vp, C.c_int32, C.c_int32, C.c_float, C.c_int32, vp, vp, vp, C.c_int64, c_i64p,
       vp]),

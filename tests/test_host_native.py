@@ -1,0 +1,157 @@
+"""Host-side halves of librpt (no GPU needed): C-ABI exports, CPython set-order emulation,
+scipy-exact LSAP, and the C++ ObjectTracker against the reference's golden sequences."""
+from __future__ import annotations
+
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+from scipy.optimize import linear_sum_assignment
+
+from test_oracle_golden import replay_tracker
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def test_library_exports_every_header_symbol():
+    from rpt import _abi
+
+    lib = _abi.load()
+    hdr = (ROOT / "include" / "rpt.h").read_text()
+    declared = sorted(set(re.findall(r"\b(rpt_[a-z0-9_]+)\s*\(", hdr)))
+    assert len(declared) >= 25
+    missing = [s for s in declared if getattr(lib, s, None) is None]
+    assert missing == [], f"declared in include/rpt.h but not exported: {missing}"
+    assert lib.rpt_missing_symbols == []
+    bound = set(_abi.EXPORTED)
+    assert set(declared) <= bound, f"not bound in rpt/_abi.py: {set(declared) - bound}"
+    assert lib.rpt_version() >= 100
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_set_order_matches_cpython(seed):
+    from rpt.native_tracker import set_order
+
+    rng = np.random.default_rng(seed)
+    n = int(rng.choice([1, 3, 5, 8, 20, 60, 200, 1500]))
+    hi = int(rng.choice([10, 64, 1000, 10**6]))
+    vals = rng.integers(0, hi, n * 2)
+    if rng.random() < 0.7:
+        vals = np.insert(vals, int(rng.integers(0, len(vals) + 1)), -1)
+    seq = []
+    seen = set()
+    for v in vals.tolist():
+        if v not in seen:
+            seen.add(v)
+            seq.append(v)
+    arr = np.array(seq, dtype=np.int32)
+    ref = set(arr)          # np.int32 elements, exactly as the reference builds it
+    ref.discard(-1)
+    assert set_order(seq) == [int(v) for v in ref]
+
+
+def _lsap_cases():
+    rng = np.random.default_rng(0)
+    for k in range(60):
+        nr, nc = rng.integers(1, 30, 2)
+        kind = k % 4
+        if kind == 0:
+            c = rng.random((nr, nc)) * 100
+        elif kind == 1:
+            c = rng.integers(0, 4, (nr, nc)).astype(np.float64)  # heavy ties
+        elif kind == 2:
+            c = np.full((nr, nc), 7.0)
+        else:
+            c = np.round(rng.random((nr, nc)) * 50, 1)
+        yield c
+    yield np.zeros((0, 3))
+    yield np.array([[np.inf, 1.0], [2.0, np.inf]])
+
+
+@pytest.mark.parametrize("i", range(62))
+def test_lsap_matches_scipy(i):
+    from rpt.native_tracker import lsap
+
+    c = list(_lsap_cases())[i]
+    ra, ca = linear_sum_assignment(c)
+    rb, cb = lsap(c)
+    np.testing.assert_array_equal(ra, rb)
+    np.testing.assert_array_equal(ca, cb)
+
+
+def test_lsap_invalid():
+    from rpt.native_tracker import lsap
+
+    with pytest.raises(ValueError):
+        lsap(np.array([[np.nan, 1.0]]))
+    with pytest.raises(ValueError):
+        lsap(np.array([[np.inf, np.inf], [1.0, np.inf]]))
+
+
+class _Adapter:
+    """Feed the g5 replay helper through the native tracker."""
+
+    def __init__(self):
+        from rpt.native_tracker import NativeTracker
+
+        self.t = NativeTracker()
+
+    def update(self, clusters, frame_id):
+        cx = np.array([c[0][0] for c in clusters], np.float32)
+        cy = np.array([c[0][1] for c in clusters], np.float32)
+        self.t.update_arrays(frame_id, cx, cy, [c[1] for c in clusters])
+        return self.t.objects()
+
+    @property
+    def objects(self):
+        return {o.object_id: o for o in self.t.objects()}
+
+
+def test_native_tracker_matches_reference(golden):
+    g = golden("g5_tracker.npz")
+    for s in range(int(g["n_seqs"])):
+        trk, alive = replay_tracker(g, s, _Adapter)
+        ao = g[f"s{s}_alive_off"]
+        for i, a in enumerate(alive):
+            assert a == list(g[f"s{s}_alive"][ao[i]:ao[i + 1]]), f"seq {s} frame {i}"
+        objs = list(trk.objects.values())
+        np.testing.assert_array_equal([o.object_id for o in objs], g[f"s{s}_obj_id"])
+        np.testing.assert_array_equal([o.object_type for o in objs], g[f"s{s}_obj_type"])
+        pos = np.vstack([np.vstack(o.positions) for o in objs]).astype(np.float32)
+        np.testing.assert_array_equal(pos, g[f"s{s}_obj_pos"])
+        vel = np.vstack([np.vstack(o.velocities).astype(np.float64) for o in objs])
+        np.testing.assert_array_equal(vel, g[f"s{s}_obj_vel"])
+        np.testing.assert_array_equal([float(o.average_velocity) for o in objs],
+                                      g[f"s{s}_obj_avgv"])
+        np.testing.assert_array_equal([isinstance(o.average_velocity, np.float32) for o in objs],
+                                      g[f"s{s}_obj_avgv_f32"])
+        np.testing.assert_array_equal([o.color for o in objs], g[f"s{s}_obj_color"])
+
+
+def test_native_tracker_random_vs_oracle():
+    """Longer random sequences (births, deaths, gating, f64->f32 switch) vs the pinned oracle."""
+    import oracle
+
+    rng = np.random.default_rng(11)
+    for rep in range(6):
+        o = oracle.Tracker()
+        n = _Adapter()
+        pos = rng.random((12, 2)) * 300 - 150
+        vel = rng.normal(0, 2.0, (12, 2))
+        for f in range(60):
+            if rng.random() < 0.1:
+                continue  # frame dropped (id gap)
+            cl = [pos[k] + vel[k] * f + rng.normal(0, 0.5, 2) for k in range(12)
+                  if rng.random() < 0.8]
+            cl += [rng.random(2) * 400 - 200 for _ in range(int(rng.integers(0, 4)))]
+            cl = [(np.asarray(c, np.float32), f) for c in cl]
+            o.update(cl, f)
+            n.update(cl, f)
+        a = list(o.objects.values())
+        b = list(n.objects.values())
+        assert [x.object_id for x in a] == [x.object_id for x in b]
+        assert [x.object_type for x in a] == [x.object_type for x in b]
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(np.vstack(x.positions), np.vstack(y.positions))
+            assert x.frames_seen == y.frames_seen
