@@ -1,0 +1,176 @@
+#!/usr/bin/env python3
+"""Benchmark: Mpoints/s clustered+tracked on synthetic 1024-echo frames (BASELINE.json metric).
+
+One step = the reference's per-frame path (4_temporal_object_tracker.py run_pipeline :941-991)
+over a frame stack whose u8 echo is already resident in HBM: K1 polar scatter + 3-gain fusion,
+land filter (> 10 frames), ST-DBSCAN over the stack, per-frame cluster summaries, reference
+cluster order and the Hungarian tracker on the host — ending with final tracker state on the
+host.  value = points produced by K1 over the stack ("Total points", :950-951) / step time.
+
+Workload at N=1: configs[2] of BASELINE.json — 100-frame 3-gain fused stack, ST-DBSCAN +
+tracking (configs[1], one 50k-point frame, is launch-latency bound and is a parity case).
+Multi-GPU: every rank owns `--frames` contiguous frames of one global stack (weak scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--no-cpu-baseline]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+for p in (str(ROOT / "radar-point-cloud-tracking_amd"), str(ROOT)):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+K5_BYTES_PER_POINT = 17.0  # SURVEY.md §8(d) compulsory model of the neighbour-search kernel
+
+
+def _log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(echo_host: np.ndarray, cfg, geo, max_seconds: float = 30.0):
+    """Oracle (the pinned CPU restatement, 1 thread) on the first frames of the same workload."""
+    import oracle
+    from oracle import path as op
+
+    F, G, R, B = echo_host.shape
+    t0 = time.perf_counter()
+    per_frame = []
+    for f in range(F):
+        per_frame.append({gain: op.polar_scatter(echo_host[f, k], np.full(R, cfg.scale, np.float32),
+                                                 geo.cos_t, geo.sin_t)
+                          for k, gain in enumerate(cfg.gains)})
+        if time.perf_counter() - t0 > max_seconds:
+            break
+    frames = op.build_frames(per_frame)
+    npts = sum(len(p) for _, p, _ in frames)
+    op.run_path(frames)
+    dt = time.perf_counter() - t0
+    del oracle
+    return npts, len(frames), dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--frames", type=int, default=100, help="frames per GPU")
+    ap.add_argument("--cpu-frames", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-timing", action="store_true", help="skip per-stage hipEvent timing")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from rpt import _abi
+    from rpt.pipeline import FrameStackPipeline, PathParams
+    from rpt.synth import DeviceSynth, SynthConfig
+
+    _abi.load()
+    cfg = SynthConfig(n_frames=args.frames, frame0=rank * args.frames)
+    ds = DeviceSynth(cfg, dev)
+    echo = ds.echo()
+    torch.cuda.synchronize(dev)
+    pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), dev,
+                              timing=not args.no_timing)
+    pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
+                      cfg.n_frames * len(cfg.gains))
+
+    for _ in range(args.warmup):
+        pipe.run(echo)
+    torch.cuda.synchronize(dev)
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    stage_acc = {}
+    k5_ms = []
+    res = None
+    for _ in range(args.steps):
+        res = pipe.run(echo)
+        for k, v in res.stage_ms.items():
+            stage_acc[k] = stage_acc.get(k, 0.0) + v
+        if res.stage_ms:
+            k5_ms.append(res.stage_ms["dbscan_core"])
+    torch.cuda.synchronize(dev)
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    pts = float(res.n_points)
+    if dist:
+        t = torch.tensor([dt, pts], dtype=torch.float64, device=dev)
+        tmax = t.clone()
+        tdist.all_reduce(tmax[:1], op=tdist.ReduceOp.MAX)
+        tdist.all_reduce(t[1:], op=tdist.ReduceOp.SUM)
+        dt, pts = float(tmax[0]), float(t[1])
+    value = pts * args.steps / dt / 1e6
+    ms_step = dt / args.steps * 1e3
+
+    roof = None
+    if k5_ms:
+        k5 = float(np.mean(k5_ms))
+        n_in = res.n_clustered_input
+        achieved = K5_BYTES_PER_POINT * n_in / (k5 * 1e-3) / 1e9
+        roof = {"kernel": "k_core (K5 neighbour count / core flag)", "bound": "hbm",
+                "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "bytes_model": "17 B/point x points entering ST-DBSCAN (SURVEY.md 8d)",
+                "avg_ms": round(k5, 4), "points": n_in}
+    stage = {k: round(v / args.steps, 3) for k, v in stage_acc.items()}
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline and not dist:
+        cf = min(args.cpu_frames, args.frames)
+        eh = echo[:cf].cpu().numpy()
+        npts, nfr, cdt = cpu_baseline(eh, cfg, ds.geo)
+        cpu = {"value": round(npts / cdt / 1e6, 5), "unit": "Mpoints/s", "cores": 1,
+               "kind": "port",
+               "sample": f"first {nfr} frames of the same stack ({npts} points): oracle numpy "
+                         f"polar scatter + C BFS ST-DBSCAN + numpy/scipy tracker, 1 thread, "
+                         f"{cdt:.1f} s"}
+    if rank == 0:
+        out = {
+            "metric": "Mpoints/s clustered+tracked, 1024-echo synthetic frames; 1/2/4/8-GPU scaling",
+            "value": round(value, 3), "unit": "Mpoints/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8 echo / f32 geometry / f64 distance",
+            "data": "synthetic (device-generated, seeded)",
+            "config": {"workload": f"{args.frames}-frame 3-gain fused stack per GPU "
+                                   f"(4096 az x 1024 echo u8), land filter + ST-DBSCAN eps 8 / "
+                                   f"eps_t 2 / min 15 + Hungarian tracking (BASELINE configs[2])",
+                       "frames_per_gpu": args.frames, "points_per_step": int(pts),
+                       "points_clustered_rank0": res.n_clustered_input,
+                       "clusters_rank0": res.n_clusters, "segments_rank0": res.n_segments,
+                       "objects_rank0": len(res.tracker),
+                       "parallelism": f"frame-sharded x{world}" if dist else "single GPU"},
+            "roofline": roof, "cpu_baseline": cpu, "stage_ms": stage,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

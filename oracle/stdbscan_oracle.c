@@ -14,8 +14,10 @@
  *   = sum of squared differences, left to right) and the reference's float32 time filter:
  *     d2 = (xi-xj)^2 + (yi-yj)^2 [+ (zi-zj)^2] <= eps^2   (float64, no FMA)
  *     |float32(t_j - t_i)| <= float32(eps_t)               (NEP 50: Python float -> float32)
- * Neighbour search: points sorted by time; each query scans the time window (with generous
- * slack) and applies the exact predicate, so the oracle is exact and O(n * window).
+ * Neighbour search (candidates only; the exact predicate above decides): when every finite
+ * time is an integer (frame ids) a sorted (slab, cell) key grid with cell side >= eps is probed
+ * over +-1 cells and floor(eps_t)+1 slabs; otherwise points are sorted by time and the time
+ * window (with generous slack) is scanned.
  * Build: gcc -O2 -ffp-contract=off -shared -fPIC (oracle/Makefile, __graft_entry__.build()).
  */
 #include <math.h>
@@ -33,6 +35,15 @@ typedef struct {
   int64_t* order; /* indices sorted by time (non-finite last) */
   float* tsorted;
   int64_t n_finite;
+  /* grid mode (all finite times integral): key = ((slab*nz + cz)*ny + cy)*nx + cx */
+  int grid;
+  double lo[3], cs;
+  int64_t nd[3];
+  double tmin;
+  int64_t smax;
+  int64_t* gkey;   /* sorted keys */
+  int64_t* gidx;   /* point index per sorted key */
+  int64_t n_grid;
 } ctx_t;
 
 static const float* g_t_for_sort;
@@ -63,10 +74,124 @@ static int adjacent(const ctx_t* x, int64_t i, int64_t j) {
   return (d2 <= x->eps2) && (dt <= x->epst);
 }
 
+static int64_t cell1(double v, double lo, double cs, int64_t n) {
+  double q = floor((v - lo) / cs);
+  if (q < 0) return 0;
+  if (q >= (double)n) return n - 1;
+  return (int64_t)q;
+}
+
+static int64_t key_of(const ctx_t* x, int64_t slab, const int64_t* c) {
+  int64_t k = slab;
+  for (int d = x->dim - 1; d >= 0; --d) k = k * x->nd[d] + c[d];
+  return k;
+}
+
+static int cmp_pair(const void* a, const void* b) {
+  const int64_t* p = (const int64_t*)a;
+  const int64_t* q = (const int64_t*)b;
+  if (p[0] != q[0]) return p[0] < q[0] ? -1 : 1;
+  return (p[1] < q[1]) ? -1 : (p[1] > q[1]);
+}
+
+/* grid mode: used when every finite time is an integer below 2^24 (frame ids) and eps >= 0 */
+static void build_grid(ctx_t* x) {
+  x->grid = 0;
+  if (!(x->epst >= 0.0f) || !(x->eps2 >= 0.0) || x->dim > 3) return;
+  double tmin = INFINITY, tmax = -INFINITY;
+  for (int d = 0; d < x->dim; ++d) { x->lo[d] = INFINITY; }
+  double hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int64_t i = 0; i < x->n; ++i) {
+    float t = x->t[i];
+    if (!isfinite(t)) continue;
+    if (t != floorf(t) || fabsf(t) >= 16777216.f) return;
+    if (t < tmin) tmin = t;
+    if (t > tmax) tmax = t;
+    for (int d = 0; d < x->dim; ++d) {
+      double v = x->c[i * x->dim + d];
+      if (v < x->lo[d]) x->lo[d] = v;
+      if (v > hi[d]) hi[d] = v;
+    }
+  }
+  if (!(tmin <= tmax)) return;
+  double eps = sqrt(x->eps2);
+  x->cs = (eps > 0 ? eps : 1.0) * (1.0 + 1.0 / 1048576.0);
+  double cells = 1.0;
+  for (int d = 0; d < x->dim; ++d) {
+    if (!isfinite(x->lo[d]) || !isfinite(hi[d])) return;
+    /* keep the composite key in range; coarser cells stay exact (neighbours within +-1) */
+    double nd = floor((hi[d] - x->lo[d]) / x->cs) + 1.0;
+    while (nd > 4.0e5) { x->cs *= 2.0; nd = floor((hi[d] - x->lo[d]) / x->cs) + 1.0; }
+    x->nd[d] = (int64_t)nd;
+    cells *= nd;
+  }
+  if (cells * (tmax - tmin + 1.0) > 9.0e18) return;
+  x->tmin = tmin;
+  x->smax = (int64_t)(tmax - tmin);
+  int64_t* pairs = (int64_t*)malloc(sizeof(int64_t) * 2 * (size_t)(x->n > 0 ? x->n : 1));
+  x->gkey = (int64_t*)malloc(sizeof(int64_t) * (size_t)(x->n > 0 ? x->n : 1));
+  x->gidx = (int64_t*)malloc(sizeof(int64_t) * (size_t)(x->n > 0 ? x->n : 1));
+  int64_t m = 0;
+  for (int64_t i = 0; i < x->n; ++i) {
+    float t = x->t[i];
+    if (!isfinite(t)) continue;
+    int64_t c[3];
+    for (int d = 0; d < x->dim; ++d) c[d] = cell1(x->c[i * x->dim + d], x->lo[d], x->cs, x->nd[d]);
+    pairs[2 * m] = key_of(x, (int64_t)((double)t - tmin), c);
+    pairs[2 * m + 1] = i;
+    ++m;
+  }
+  qsort(pairs, (size_t)m, 2 * sizeof(int64_t), cmp_pair);
+  for (int64_t k = 0; k < m; ++k) { x->gkey[k] = pairs[2 * k]; x->gidx[k] = pairs[2 * k + 1]; }
+  free(pairs);
+  x->n_grid = m;
+  x->grid = 1;
+}
+
+static int64_t lower_key(const ctx_t* x, int64_t key) {
+  int64_t a = 0, b = x->n_grid;
+  while (a < b) {
+    int64_t m = (a + b) / 2;
+    if (x->gkey[m] < key) a = m + 1; else b = m;
+  }
+  return a;
+}
+
+static int64_t neighbours_grid(const ctx_t* x, int64_t i, int64_t* buf) {
+  float ti = x->t[i];
+  int64_t slab = (int64_t)((double)ti - x->tmin);
+  double dsd = floor((double)x->epst) + 1.0;
+  int64_t ds = dsd > (double)(x->smax + 1) ? x->smax + 1 : (int64_t)dsd;
+  int64_t c0[3] = {0, 0, 0}, lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+  for (int d = 0; d < x->dim; ++d) {
+    c0[d] = cell1(x->c[i * x->dim + d], x->lo[d], x->cs, x->nd[d]);
+    lo[d] = c0[d] > 0 ? c0[d] - 1 : 0;
+    hi[d] = c0[d] + 1 < x->nd[d] ? c0[d] + 1 : x->nd[d] - 1;
+  }
+  int64_t cnt = 0;
+  for (int64_t s = slab - ds; s <= slab + ds; ++s) {
+    if (s < 0 || s > x->smax) continue;
+    int64_t c[3];
+    for (c[2] = (x->dim == 3 ? lo[2] : 0); c[2] <= (x->dim == 3 ? hi[2] : 0); ++c[2])
+      for (c[1] = lo[1]; c[1] <= hi[1]; ++c[1]) {
+        c[0] = lo[0];
+        int64_t k0 = key_of(x, s, c);
+        c[0] = hi[0];
+        int64_t k1 = key_of(x, s, c);
+        for (int64_t p = lower_key(x, k0); p < x->n_grid && x->gkey[p] <= k1; ++p) {
+          int64_t j = x->gidx[p];
+          if (adjacent(x, i, j)) buf[cnt++] = j;
+        }
+      }
+  }
+  return cnt;
+}
+
 /* writes neighbours of i into buf (capacity n); returns count */
 static int64_t neighbours(const ctx_t* x, int64_t i, int64_t* buf) {
   float ti = x->t[i];
   if (!isfinite(ti) || !(x->epst >= 0.0f) || !(x->eps2 >= 0.0)) return 0;
+  if (x->grid) return neighbours_grid(x, i, buf);
   double slack = 1e-3 * (fabs((double)x->epst) + fabs((double)ti)) + 1e-6;
   double lo = (double)ti - (double)x->epst - slack;
   double hi = (double)ti + (double)x->epst + slack;
@@ -112,6 +237,8 @@ int32_t oracle_stdbscan(const float* coords, int32_t dim, const float* times, in
     x.tsorted[k] = times[x.order[k]];
     if (isfinite(x.tsorted[k])) x.n_finite = k + 1;
   }
+  x.gkey = x.gidx = NULL;
+  build_grid(&x);
   for (int64_t i = 0; i < n; ++i) labels[i] = -1;
   int32_t cid = 0;
   for (int64_t i = 0; i < n; ++i) {
@@ -138,6 +265,7 @@ int32_t oracle_stdbscan(const float* coords, int32_t dim, const float* times, in
     ++cid;
   }
   free(x.order); free(x.tsorted); free(nb); free(nb2); free(stack); free(visited); free(inseed);
+  free(x.gkey); free(x.gidx);
   return cid;
 }
 
@@ -160,7 +288,9 @@ int32_t oracle_neighbour_counts(const float* coords, int32_t dim, const float* t
     x.tsorted[k] = times[x.order[k]];
     if (isfinite(x.tsorted[k])) x.n_finite = k + 1;
   }
+  x.gkey = x.gidx = NULL;
+  build_grid(&x);
   for (int64_t i = 0; i < n; ++i) counts[i] = neighbours(&x, i, nb);
-  free(x.order); free(x.tsorted); free(nb);
+  free(x.order); free(x.tsorted); free(nb); free(x.gkey); free(x.gidx);
   return 0;
 }

@@ -43,7 +43,21 @@ __global__ __launch_bounds__(kBlock) void k_bounds_xy(const float* __restrict__ 
     mny = min(mny, (uint32_t)__shfl_xor((int)mny, off));
     mxy = max(mxy, (uint32_t)__shfl_xor((int)mxy, off));
   }
+  __shared__ uint32_t sm[kBlock / 64][4];
   if ((threadIdx.x & 63) == 0) {
+    sm[threadIdx.x / 64][0] = mnx;
+    sm[threadIdx.x / 64][1] = mxx;
+    sm[threadIdx.x / 64][2] = mny;
+    sm[threadIdx.x / 64][3] = mxy;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kBlock / 64; ++w) {
+      mnx = min(mnx, sm[w][0]);
+      mxx = max(mxx, sm[w][1]);
+      mny = min(mny, sm[w][2]);
+      mxy = max(mxy, sm[w][3]);
+    }
     atomicMin(out + 0, mnx);
     atomicMax(out + 1, mxx);
     atomicMin(out + 2, mny);
@@ -90,6 +104,51 @@ __device__ __forceinline__ Edges stage_edges(const double* xe, int nxe, const do
     E.ye = lds + nxe;
   }
   return E;
+}
+
+// LDS-privatised form: int32 counts + f64 sums of the whole grid per block (fits when
+// cells * 12 B + edges <= ~150 KiB), flushed with one atomic per non-empty cell.
+constexpr int kLdsGridCells = 10240;
+__global__ __launch_bounds__(kBlock) void k_land_grid_lds(const float* __restrict__ x,
+                                                         const float* __restrict__ y,
+                                                         const float* __restrict__ val, int64_t n,
+                                                         const double* __restrict__ xe, int nxe,
+                                                         const double* __restrict__ ye, int nye,
+                                                         int32_t* __restrict__ cnt,
+                                                         double* __restrict__ tot) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* lds_e = reinterpret_cast<double*>(smem);                    // nxe + nye edges
+  const int ne = nxe + nye;
+  const int ne_al = (ne + 1) & ~1;
+  double* lds_t = lds_e + ne_al;                                       // cells f64 sums
+  const int ny = nye - 1;
+  const int cells = (nxe - 1) * ny;
+  int32_t* lds_c = reinterpret_cast<int32_t*>(lds_t + cells);          // cells counts
+  for (int i = threadIdx.x; i < nxe; i += blockDim.x) lds_e[i] = xe[i];
+  for (int i = threadIdx.x; i < nye; i += blockDim.x) lds_e[nxe + i] = ye[i];
+  for (int c = threadIdx.x; c < cells; c += blockDim.x) {
+    lds_t[c] = 0.0;
+    lds_c[c] = 0;
+  }
+  __syncthreads();
+  const double* ex = lds_e;
+  const double* ey = lds_e + nxe;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int ix = clip_idx(count_le(ex, nxe, (double)x[i]) - 1, nxe - 2);
+    const int iy = clip_idx(count_le(ey, nye, (double)y[i]) - 1, nye - 2);
+    const int c = ix * ny + iy;
+    atomicAdd(lds_c + c, 1);
+    atomicAdd(lds_t + c, (double)val[i]);
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < cells; c += blockDim.x) {
+    const int k = lds_c[c];
+    if (k) {
+      atomicAdd(cnt + c, k);
+      atomicAdd(tot + c, lds_t[c]);
+    }
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void k_land_grid(const float* __restrict__ x,
@@ -183,7 +242,7 @@ int32_t bounds_xy(const float* x, const float* y, int64_t n, float* out4, hipStr
   RPT_TRY(sc.reserve(256, st));
   uint32_t* d = sc.carve_n<uint32_t>(4);
   hipLaunchKernelGGL(k_bounds_xy_init, dim3(1), dim3(1), 0, st, d);
-  hipLaunchKernelGGL(k_bounds_xy, dim3(grid_for(n, kBlock, 2048)), dim3(kBlock), 0, st, x, y, n,
+  hipLaunchKernelGGL(k_bounds_xy, dim3(grid_for(n, kBlock, 1024)), dim3(kBlock), 0, st, x, y, n,
                      d);
   RPT_CHECK_LAUNCH();
   uint32_t h[4];
@@ -208,8 +267,17 @@ int32_t land_grid(const float* x, const float* y, const float* val, int64_t n, c
   RPT_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t) * cells, st));
   RPT_HIP(hipMemsetAsync(tot, 0, sizeof(double) * cells, st));
   if (n == 0) return RPT_OK;
-  hipLaunchKernelGGL(k_land_grid, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, st, x, y,
-                     val, n, xe, nxe, ye, nye, cnt, tot);
+  const int64_t ne_al = ((int64_t)nxe + nye + 1) & ~int64_t(1);
+  const size_t lds = (size_t)ne_al * 8 + (size_t)cells * 12;
+  if (cells <= kLdsGridCells && lds <= 150 * 1024) {
+    RPT_HIP(hipFuncSetAttribute((const void*)k_land_grid_lds,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k_land_grid_lds, dim3(grid_for(n, kBlock, 512)), dim3(kBlock), lds, st, x,
+                       y, val, n, xe, nxe, ye, nye, cnt, tot);
+  } else {
+    hipLaunchKernelGGL(k_land_grid, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, st, x, y,
+                       val, n, xe, nxe, ye, nye, cnt, tot);
+  }
   RPT_CHECK_LAUNCH();
   return RPT_OK;
 }

@@ -112,7 +112,29 @@ __global__ __launch_bounds__(kBlock) void k_bounds(const float* __restrict__ x,
     nonint |= __shfl_xor(nonint, off);
     nfin += __shfl_xor(nfin, off);
   }
+  __shared__ uint32_t smn[kBlock / 64][4], smx[kBlock / 64][4];
+  __shared__ int sfl[kBlock / 64][3];
+  const int w = threadIdx.x / 64;
   if ((threadIdx.x & 63) == 0) {
+    for (int k = 0; k < 4; ++k) {
+      smn[w][k] = mn[k];
+      smx[w][k] = mx[k];
+    }
+    sfl[w][0] = nonfin;
+    sfl[w][1] = nonint;
+    sfl[w][2] = nfin;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int v = 1; v < kBlock / 64; ++v) {
+      for (int k = 0; k < 4; ++k) {
+        mn[k] = min(mn[k], smn[v][k]);
+        mx[k] = max(mx[k], smx[v][k]);
+      }
+      nonfin |= sfl[v][0];
+      nonint |= sfl[v][1];
+      nfin += sfl[v][2];
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       atomicMin(&out->mn[k], mn[k]);
@@ -383,6 +405,7 @@ __global__ __launch_bounds__(kBlock) void k_core(const float4* __restrict__ pts,
                                                 const float4* __restrict__ boxA,
                                                 const float4* __restrict__ boxB,
                                                 const float2* __restrict__ slab_t,
+                                                const uint8_t* __restrict__ mutual,
                                                 uint8_t* __restrict__ core) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;
@@ -394,6 +417,14 @@ __global__ __launch_bounds__(kBlock) void k_core(const float4* __restrict__ pts,
   const float4 p = pts[s];
   const int need = g.min_samples;
   int cnt = 0;
+  // own cell first: a mutual cell holding >= min_samples points makes all of them core
+  if (need > 0 && mutual[key]) {
+    const int own = cell_start[key + 1] - cell_start[key];
+    if (own >= need) {
+      core[s] = 1;
+      return;
+    }
+  }
   if (need > 0) {
     for_each_cell<D>(p, key, g, cell_start, boxA, boxB, slab_t,
                      [&](int64_t c, int b, int e, int cls) -> bool {
@@ -448,13 +479,16 @@ __device__ __forceinline__ int uf_find(int32_t* parent, int x) {
     x = gp;
   }
 }
-// Hook the larger root under the smaller one: every tree's root is its minimum index.
-__device__ __forceinline__ void uf_unite(int32_t* parent, int a, int b) {
+// Hook the root with the larger ORIGINAL index under the other (parents always have a smaller
+// original index): every tree's root is the component's minimum original index, which is what
+// the reference numbers clusters by — so no reduction over the component is needed.
+__device__ __forceinline__ void uf_unite(int32_t* parent, const int32_t* __restrict__ sorig,
+                                         int a, int b) {
   while (true) {
     a = uf_find(parent, a);
     b = uf_find(parent, b);
     if (a == b) return;
-    if (a < b) {
+    if (sorig[a] < sorig[b]) {
       const int tmp = a;
       a = b;
       b = tmp;
@@ -465,10 +499,119 @@ __device__ __forceinline__ void uf_unite(int32_t* parent, int a, int b) {
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_parent_init(int32_t* parent, int64_t n) {
+// Star initialisation: every core point of a mutual cell hangs under the cell's first core point
+// (its minimum original index: cells list points in index order), other points are roots.
+__global__ __launch_bounds__(kBlock) void k_parent_init(int32_t* parent, int64_t n,
+                                                       const uint8_t* __restrict__ core,
+                                                       const int32_t* __restrict__ skey,
+                                                       const uint8_t* __restrict__ mutual,
+                                                       const int32_t* __restrict__ rep,
+                                                       int64_t cells) {
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
-       s += (int64_t)gridDim.x * blockDim.x)
-    parent[s] = (int32_t)s;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t k = skey[s];
+    parent[s] = (core[s] && (int64_t)k < cells && mutual[k]) ? rep[k] : (int32_t)s;
+  }
+}
+
+// Box-box classification of two cells with the pair test's rounding (monotone bounds):
+// 0 no pair can be adjacent, 1 every pair is adjacent, 2 undecided.
+template <int D>
+__device__ __forceinline__ int classify_cells(const float4& A1, const float4& B1,
+                                              const float4& A2, const float4& B2,
+                                              const Geom& g) {
+  auto gap = [](float a0, float a1, float b0, float b1) -> float {
+    return (b0 > a1) ? (b0 - a1) : ((a0 > b1) ? (a0 - b1) : 0.f);
+  };
+  auto gapd = [](float a0, float a1, float b0, float b1) -> double {
+    return (b0 > a1) ? ((double)b0 - (double)a1) : ((a0 > b1) ? ((double)a0 - (double)b1) : 0.0);
+  };
+  const float tg = gap(A2.z, A2.w, B2.z, B2.w);
+  if (!(tg <= g.epst)) return 0;
+  const float tm = fmaxf(fabsf(B2.w - A2.z), fabsf(A2.w - B2.z));
+  const double gx = gapd(A1.x, A1.y, B1.x, B1.y), gy = gapd(A1.z, A1.w, B1.z, B1.w);
+  double dmin = gx * gx + gy * gy;
+  const double mx = fmax(fabs((double)B1.y - (double)A1.x), fabs((double)A1.y - (double)B1.x));
+  const double my = fmax(fabs((double)B1.w - (double)A1.z), fabs((double)A1.w - (double)B1.z));
+  double dmax = mx * mx + my * my;
+  if (D == 3) {
+    const double gz = gapd(A2.x, A2.y, B2.x, B2.y);
+    dmin = dmin + gz * gz;
+    const double mz = fmax(fabs((double)B2.y - (double)A2.x), fabs((double)A2.y - (double)B2.x));
+    dmax = dmax + mz * mz;
+  }
+  if (!(dmin <= g.eps2)) return 0;
+  return (dmax <= g.eps2 && tm <= g.epst) ? 1 : 2;
+}
+
+// K6a: mutual-cell x mutual-cell unions, one thread per cell A, each unordered pair once (B > A).
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict__ pts,
+                                                       int64_t cells, Geom g,
+                                                       const int32_t* __restrict__ cell_start,
+                                                       const float4* __restrict__ boxA,
+                                                       const float4* __restrict__ boxB,
+                                                       const float2* __restrict__ slab_t,
+                                                       const uint8_t* __restrict__ core,
+                                                       const int32_t* __restrict__ rep,
+                                                       const uint8_t* __restrict__ mutual,
+                                                       const int32_t* __restrict__ sorig,
+                                                       int32_t* __restrict__ parent) {
+  for (int64_t ca = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; ca < cells;
+       ca += (int64_t)gridDim.x * blockDim.x) {
+    const int ra = rep[ca];
+    if (ra < 0 || !mutual[ca]) continue;
+    const int ea = cell_start[ca + 1];
+    const float4 A1 = boxA[ca], A2 = boxB[ca];
+    const int cx = (int)(ca % g.nx);
+    int64_t r = ca / g.nx;
+    const int cy = (int)(r % g.ny);
+    r /= g.ny;
+    const int cz = (D == 3) ? (int)(r % g.nz) : 0;
+    const double et = (double)g.epst;
+    const int s0 = (int)fmax(floor(((double)A2.z - et - g.ot) / g.ct) - 1.0, 0.0);
+    const int s1 = (int)fmin(floor(((double)A2.w + et - g.ot) / g.ct) + 1.0, (double)(g.nt - 1));
+    const int x0 = max(cx - 2, 0), x1 = min(cx + 2, g.nx - 1);
+    const int y0 = max(cy - 2, 0), y1 = min(cy + 2, g.ny - 1);
+    const int z0 = (D == 3) ? max(cz - 2, 0) : 0, z1 = (D == 3) ? min(cz + 2, g.nz - 1) : 0;
+    for (int sl = s0; sl <= s1; ++sl) {
+      const float2 sr = slab_t[sl];
+      if (sr.x > sr.y) continue;
+      for (int zz = z0; zz <= z1; ++zz) {
+        for (int yy = y0; yy <= y1; ++yy) {
+          const int64_t row = (((int64_t)sl * g.nz + zz) * g.ny + yy) * g.nx;
+          for (int xx = x0; xx <= x1; ++xx) {
+            const int64_t cb = row + xx;
+            if (cb <= ca) continue;
+            const int rb = rep[cb];
+            if (rb < 0 || !mutual[cb]) continue;
+            const int cls = classify_cells<D>(A1, boxA[cb], A2, boxB[cb], g);
+            if (cls == 0) continue;
+            if (cls == 1) {
+              uf_unite(parent, sorig, ra, rb);
+              continue;
+            }
+            if (uf_find(parent, ra) == uf_find(parent, rb)) continue;
+            const int eb = cell_start[cb + 1];
+            const float4 B1 = boxA[cb], B2 = boxB[cb];
+            bool hit = false;
+            for (int a = ra; a < ea && !hit; ++a) {
+              if (!core[a]) continue;
+              const float4 pa = pts[a];
+              if (classify<D>(pa, B1, B2, g) == 0) continue;
+              for (int b = rb; b < eb; ++b) {
+                if (core[b] && adjacent<D>(pa, pts[b], g)) {
+                  hit = true;
+                  break;
+                }
+              }
+            }
+            if (hit) uf_unite(parent, sorig, ra, rb);
+          }
+        }
+      }
+    }
+  }
 }
 
 // K6: core-core union.  Edge (s, j) with j in cell c:
@@ -487,11 +630,13 @@ __global__ __launch_bounds__(kBlock) void k_union(const float4* __restrict__ pts
                                                  const uint8_t* __restrict__ core,
                                                  const int32_t* __restrict__ rep,
                                                  const uint8_t* __restrict__ mutual,
+                                                 const int32_t* __restrict__ sorig,
                                                  int32_t* __restrict__ parent) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n || !core[s]) return;
   const int32_t key = skey[s];
   if ((int64_t)key >= g.cells) return;
+  if (mutual[key]) return;  // handled by the star init + k_union_cells
   const float4 p = pts[s];
   const int si = (int)s;
   for_each_cell<D>(p, key, g, cell_start, boxA, boxB, slab_t,
@@ -500,20 +645,20 @@ __global__ __launch_bounds__(kBlock) void k_union(const float4* __restrict__ pts
                      if (r < 0) return false;
                      if (mutual[c]) {
                        if (cls == 1) {
-                         uf_unite(parent, si, r);
+                         uf_unite(parent, sorig, si, r);
                          return false;
                        }
                        if (uf_find(parent, si) == uf_find(parent, r)) return false;
                        for (int j = r; j < e; ++j) {
                          if (core[j] && adjacent<D>(p, pts[j], g)) {
-                           uf_unite(parent, si, j);
+                           uf_unite(parent, sorig, si, j);
                            break;
                          }
                        }
                      } else {
                        for (int j = max(b, si + 1); j < e; ++j) {
                          if (core[j] && (cls == 1 || adjacent<D>(p, pts[j], g)))
-                           uf_unite(parent, si, j);
+                           uf_unite(parent, sorig, si, j);
                        }
                      }
                      return false;
@@ -521,20 +666,15 @@ __global__ __launch_bounds__(kBlock) void k_union(const float4* __restrict__ pts
 }
 
 // root of every core point; ccmin = component minimum original index (filled in two steps)
-__global__ __launch_bounds__(kBlock) void k_compress(int32_t* __restrict__ parent,
+__global__ __launch_bounds__(kBlock) void k_compress(int32_t* parent,
                                                     const uint8_t* __restrict__ core, int64_t n,
                                                     const int32_t* __restrict__ sorig,
                                                     int32_t* __restrict__ cmin) {
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
        s += (int64_t)gridDim.x * blockDim.x) {
     if (!core[s]) continue;
-    int x = (int)s;
-    int p = parent[x];
-    while (p != x) {
-      x = p;
-      p = parent[x];
-    }
-    atomicMin(&cmin[x], sorig[s]);
+    const int r = uf_find(parent, (int)s);  // path halving keeps every walk short
+    uf_store(parent + s, r);
   }
 }
 
@@ -545,31 +685,50 @@ __global__ __launch_bounds__(kBlock) void k_fill_i32(int32_t* p, int64_t n, int3
 }
 
 // ccmin[s] = component-min original index for core points, -1 otherwise; flags the minima.
-__global__ __launch_bounds__(kBlock) void k_ccmin(const int32_t* __restrict__ parent,
+__global__ __launch_bounds__(kBlock) void k_ccmin(int32_t* parent,
                                                  const uint8_t* __restrict__ core, int64_t n,
                                                  const int32_t* __restrict__ sorig,
                                                  const int32_t* __restrict__ cmin,
                                                  int32_t* __restrict__ ccmin,
-                                                 int32_t* __restrict__ is_min) {
-  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
-       s += (int64_t)gridDim.x * blockDim.x) {
-    if (!core[s]) {
+                                                 int32_t* __restrict__ is_min,
+                                                 int32_t* __restrict__ nc_list,
+                                                 int32_t* __restrict__ nc_count) {
+  // grid-stride with whole waves per iteration so the ballot covers 64 consecutive points
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n;
+       base += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = base + threadIdx.x;
+    const bool valid = s < n;
+    const bool nc = valid && !core[s];
+    const uint64_t bm = __ballot(nc);
+    int off = 0;
+    if ((threadIdx.x & 63) == 0 && bm) off = atomicAdd(nc_count, __popcll(bm));
+    off = __shfl(off, 0, 64);
+    if (nc) {
+      nc_list[off + rank_in_mask(bm)] = (int32_t)s;
       ccmin[s] = -1;
-      continue;
     }
-    int x = (int)s;
-    int p = parent[x];
-    while (p != x) {
-      x = p;
-      p = parent[x];
-    }
-    const int m = cmin[x];
+    if (!valid || nc) continue;
+    const int x = uf_find(parent, (int)s);
+    const int m = sorig[x];
     ccmin[s] = m;
-    if (m == sorig[s]) is_min[m] = 1;
+    if (x == (int)s) is_min[m] = 1;
   }
 }
 
-// K7/K8: final labels in original order.
+// K7/K8 (core points): label = id of the component minimum
+__global__ __launch_bounds__(kBlock) void k_label_core(const int32_t* __restrict__ ccmin,
+                                                      int64_t n,
+                                                      const int32_t* __restrict__ sorig,
+                                                      const int32_t* __restrict__ cid,
+                                                      int32_t* __restrict__ labels) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    const int own = ccmin[s];
+    if (own >= 0) labels[sorig[s]] = cid[own];
+  }
+}
+
+// K7/K8 (non-core points, compacted list): min adjacent cluster id, else -1.
 template <int D>
 __global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts,
                                                  const int32_t* __restrict__ skey, int64_t n,
@@ -582,14 +741,13 @@ __global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts
                                                  const uint8_t* __restrict__ mutual,
                                                  const int32_t* __restrict__ sorig,
                                                  const int32_t* __restrict__ cid,
+                                                 const int32_t* __restrict__ nc_list,
+                                                 const int32_t* __restrict__ nc_count,
                                                  int32_t* __restrict__ labels) {
-  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n) return;
-  const int own = ccmin[s];
-  if (own >= 0) {
-    labels[sorig[s]] = cid[own];
-    return;
-  }
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= *nc_count) return;
+  const int64_t s = nc_list[q];
+  (void)n;
   const int32_t key = skey[s];
   int best = INT_MAX;
   if ((int64_t)key < g.cells) {
@@ -691,7 +849,8 @@ int32_t stdbscan_impl(const float* x, const float* y, const float* z, int64_t st
   }
   Bounds* d_b = sc.carve_n<Bounds>(1);
   hipLaunchKernelGGL(k_bounds_init, dim3(1), dim3(1), 0, st, d_b);
-  hipLaunchKernelGGL(k_bounds<D>, dim3(gb), dim3(kBlock), 0, st, x, y, z, stride, t, n, d_b);
+  hipLaunchKernelGGL(k_bounds<D>, dim3(grid_for(n, kBlock, 1024)), dim3(kBlock), 0, st, x, y, z,
+                     stride, t, n, d_b);
   RPT_CHECK_LAUNCH();
   Bounds hb;
   RPT_HIP(hipMemcpyAsync(&hb, d_b, sizeof(Bounds), hipMemcpyDeviceToHost, st));
@@ -777,6 +936,7 @@ int32_t stdbscan_impl(const float* x, const float* y, const float* z, int64_t st
   bud.add<int32_t>(n);   // cmin
   bud.add<int32_t>(n);   // ccmin
   bud.add<int32_t>(n + 1);  // is_min -> cid
+  bud.add<int32_t>(n + 1);  // non-core list (+count)
   RPT_TRY(sc.reserve(bud.bytes, st));
   (void)sc.carve_n<Bounds>(1);
   uint32_t* keys = sc.carve_n<uint32_t>(n);
@@ -799,7 +959,9 @@ int32_t stdbscan_impl(const float* x, const float* y, const float* z, int64_t st
   int32_t* cmin = sc.carve_n<int32_t>(n);
   int32_t* ccmin = sc.carve_n<int32_t>(n);
   int32_t* cid = sc.carve_n<int32_t>(n + 1);
-  if (!cid) {
+  int32_t* nc_list = sc.carve_n<int32_t>(n + 1);
+  int32_t* nc_count = nc_list + n;
+  if (!nc_list) {
     set_error("internal: scratch carve overflow");
     return RPT_ENOMEM;
   }
@@ -827,26 +989,31 @@ int32_t stdbscan_impl(const float* x, const float* y, const float* z, int64_t st
   // ---- K5: core flags
   const unsigned gp = (unsigned)((n + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(k_core<D>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
-                     boxA, boxB, slab_t, core);
+                     boxA, boxB, slab_t, mutual, core);
   RPT_CHECK_LAUNCH();
   tm.mark();
   // ---- K6: union
   hipLaunchKernelGGL(k_rep, dim3(gc), dim3(kBlock), 0, st, cell_start, C, core, rep);
-  hipLaunchKernelGGL(k_parent_init, dim3(gb), dim3(kBlock), 0, st, parent, n);
+  hipLaunchKernelGGL(k_parent_init, dim3(gb), dim3(kBlock), 0, st, parent, n, core, skey, mutual,
+                     rep, C);
+  hipLaunchKernelGGL(k_union_cells<D>, dim3(gc), dim3(kBlock), 0, st, pts, C, g, cell_start, boxA,
+                     boxB, slab_t, core, rep, mutual, sorig, parent);
   hipLaunchKernelGGL(k_union<D>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
-                     boxA, boxB, slab_t, core, rep, mutual, parent);
+                     boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
   RPT_CHECK_LAUNCH();
   tm.mark();
   // ---- K7/K8: component minima, ids, labels
-  hipLaunchKernelGGL(k_fill_i32, dim3(gb), dim3(kBlock), 0, st, cmin, n, (int32_t)INT_MAX);
   hipLaunchKernelGGL(k_compress, dim3(gb), dim3(kBlock), 0, st, parent, core, n, sorig, cmin);
   RPT_HIP(hipMemsetAsync(cid, 0, sizeof(int32_t) * (n + 1), st));
+  RPT_HIP(hipMemsetAsync(nc_count, 0, sizeof(int32_t), st));
   hipLaunchKernelGGL(k_ccmin, dim3(gb), dim3(kBlock), 0, st, parent, core, n, sorig, cmin,
-                     ccmin, cid);
+                     ccmin, cid, nc_list, nc_count);
   RPT_CHECK_LAUNCH();
   RPT_TRY(exclusive_scan_i32(cid, cid, n + 1, stmp, st));
+  hipLaunchKernelGGL(k_label_core, dim3(gb), dim3(kBlock), 0, st, ccmin, n, sorig, cid, labels);
   hipLaunchKernelGGL(k_label<D>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
-                     boxA, boxB, slab_t, ccmin, rep, mutual, sorig, cid, labels);
+                     boxA, boxB, slab_t, ccmin, rep, mutual, sorig, cid, nc_list, nc_count,
+                     labels);
   RPT_CHECK_LAUNCH();
   tm.mark();
   if (stats) {

@@ -54,13 +54,12 @@ __global__ void k_seg_starts(const int32_t* __restrict__ head, const int64_t* __
     if (head[p]) seg_start[pos[p]] = p;
 }
 
-// numpy pairwise_sum over a[idx[b .. b+len)] (float32), iterative form of the recursion.
-__device__ float pairwise_f32(const float* __restrict__ val, const uint32_t* __restrict__ idx,
-                              int64_t b, int64_t len) {
-  // explicit stack of (begin, len, state); state 0 = fresh, 1 = left done (partial on vstack)
-  int64_t sb[48], sl[48];
-  int st[48];
-  float vs[48];
+// numpy pairwise_sum over a[b .. b+len) (float32), iterative form of the recursion.  Only
+// reached when intensities are not small non-negative integers (see k_summarize).
+__device__ float pairwise_f32(const float* __restrict__ a, int64_t b, int64_t len) {
+  int64_t sb[40], sl[40];
+  int st[40];
+  float vs[40];
   int sp = 0, vp = 0;
   sb[0] = b;
   sl[0] = len;
@@ -69,21 +68,21 @@ __device__ float pairwise_f32(const float* __restrict__ val, const uint32_t* __r
   while (sp > 0) {
     const int64_t bb = sb[sp - 1], ll = sl[sp - 1];
     if (ll < 8) {
-      float r = 0.f;  // np: res = 0.; res += a[i]
-      for (int64_t i = 0; i < ll; ++i) r = r + val[idx[bb + i]];
+      float r = 0.f;  // numpy: res = 0.; res += a[i]
+      for (int64_t i = 0; i < ll; ++i) r = r + a[bb + i];
       --sp;
       vs[vp++] = r;
     } else if (ll <= 128) {
       float r[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) r[k] = val[idx[bb + k]];
+      for (int k = 0; k < 8; ++k) r[k] = a[bb + k];
       int64_t i = 8;
       for (; i < ll - (ll % 8); i += 8) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) r[k] = r[k] + val[idx[bb + i + k]];
+        for (int k = 0; k < 8; ++k) r[k] = r[k] + a[bb + i + k];
       }
       float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-      for (; i < ll; ++i) res = res + val[idx[bb + i]];
+      for (; i < ll; ++i) res = res + a[bb + i];
       --sp;
       vs[vp++] = res;
     } else {
@@ -112,10 +111,28 @@ __device__ float pairwise_f32(const float* __restrict__ val, const uint32_t* __r
   return vs[0];
 }
 
+// points of every run gathered contiguously (coalesced writes, one gather read per point)
+__global__ void k_gather_runs(const uint32_t* __restrict__ sv, int64_t n,
+                              const float* __restrict__ x, const float* __restrict__ y,
+                              const float* __restrict__ inten, float* __restrict__ gx,
+                              float* __restrict__ gy, float* __restrict__ gi) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t i = sv[p];
+    gx[p] = x[i];
+    gy[p] = y[i];
+    gi[p] = inten[i];
+  }
+}
+
+// One lane per (frame, label) run: sequential float32 sums in index order (np.mean axis 0).
+// Mean intensity: when every intensity is a non-negative integer and the running sum stays
+// below 2^24, every summation order is exact, so the sequential sum equals numpy's pairwise
+// result; otherwise numpy's chunked pairwise sum is evaluated.
 __global__ void k_summarize(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
                             const int64_t* __restrict__ seg_start, int64_t n_seg, int64_t n,
-                            const float* __restrict__ x, const float* __restrict__ y,
-                            const float* __restrict__ inten, const int32_t* __restrict__ pf,
+                            const float* __restrict__ gx, const float* __restrict__ gy,
+                            const float* __restrict__ gi, const int32_t* __restrict__ pf,
                             int32_t* __restrict__ o_frame, int32_t* __restrict__ o_label,
                             int64_t* __restrict__ o_count, int64_t* __restrict__ o_first,
                             float* __restrict__ o_cx, float* __restrict__ o_cy,
@@ -125,26 +142,56 @@ __global__ void k_summarize(const uint32_t* __restrict__ sk, const uint32_t* __r
     const int64_t b = seg_start[s];
     const int64_t e = (s + 1 < n_seg) ? seg_start[s + 1] : n;
     const int64_t k = e - b;
-    const uint32_t i0 = sv[b];
-    float sx = x[i0], sy = y[i0];
-    for (int64_t p = b + 1; p < e; ++p) {
-      const uint32_t i = sv[p];
-      sx = sx + x[i];
-      sy = sy + y[i];
+    float sx = gx[b], sy = gy[b];
+    float si = gi[b];
+    bool small_int = (si >= 0.f) && (si == floorf(si));
+    // batches of kU independent loads, then the order-preserving sequential adds: one memory
+    // latency per batch instead of per element
+    constexpr int kU = 32;
+    int64_t p = b + 1;
+    for (; p + kU <= e; p += kU) {
+      float bx[kU], by[kU], bi[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        bx[u] = gx[p + u];
+        by[u] = gy[p + u];
+        bi[u] = gi[p + u];
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        sx = sx + bx[u];
+        sy = sy + by[u];
+        small_int = small_int && (bi[u] >= 0.f) && (bi[u] == floorf(bi[u]));
+        si = si + bi[u];
+      }
+    }
+    for (; p < e; ++p) {
+      sx = sx + gx[p];
+      sy = sy + gy[p];
+      const float v = gi[p];
+      small_int = small_int && (v >= 0.f) && (v == floorf(v));
+      si = si + v;
     }
     const float fk = (float)k;
-    float tot = 0.f;
-    for (int64_t c = 0; c < k; c += 8192) {
-      const int64_t len = (k - c < 8192) ? (k - c) : 8192;
-      tot = tot + pairwise_f32(inten, sv, b + c, len);
+    float mi;
+    if (small_int && si < 16777216.f) {
+      mi = si / fk;
+    } else {
+      float tot = 0.f;
+      for (int64_t c = 0; c < k; c += 8192) {
+        const int64_t len = (k - c < 8192) ? (k - c) : 8192;
+        tot = tot + pairwise_f32(gi, b + c, len);
+      }
+      mi = tot / fk;
     }
+    const uint32_t i0 = sv[b];
     o_frame[s] = pf[i0];
     o_label[s] = (int32_t)sk[b] - 1;
     o_count[s] = k;
     o_first[s] = i0;
     o_cx[s] = sx / fk;
     o_cy[s] = sy / fk;
-    o_mi[s] = tot / fk;
+    o_mi[s] = mi;
   }
 }
 
@@ -185,6 +232,7 @@ int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
   b.add<int64_t>(n + 1);
   b.add<int64_t>(scan_tmp_elems(n + 1));
   b.add<unsigned long long>(n_frames + 1);
+  for (int k = 0; k < 3; ++k) b.add<float>(n + 1);
   RPT_TRY(sc.reserve(b.bytes, st));
   uint32_t* keys = sc.carve_n<uint32_t>(n + 1);
   uint32_t* vals = sc.carve_n<uint32_t>(n + 1);
@@ -196,6 +244,9 @@ int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
   int64_t* seg_start = sc.carve_n<int64_t>(n + 1);
   int64_t* tmp = sc.carve_n<int64_t>(scan_tmp_elems(n + 1));
   unsigned long long* fn = sc.carve_n<unsigned long long>(n_frames + 1);
+  float* gx = sc.carve_n<float>(n + 1);
+  float* gy = sc.carve_n<float>(n + 1);
+  float* gi = sc.carve_n<float>(n + 1);
   if (n_frames > 0)
     hipLaunchKernelGGL(k_fill_u64, dim3(grid_for(n_frames, 256, 64)), dim3(256), 0, st, fn,
                        (int64_t)n_frames, ~0ull);
@@ -223,8 +274,10 @@ int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
   RPT_HIP(hipMemcpyAsync(&n_seg, pos + n, sizeof(int64_t), hipMemcpyDeviceToHost, st));
   RPT_HIP(hipStreamSynchronize(st));
   if (n_seg > 0) {
+    hipLaunchKernelGGL(k_gather_runs, dim3(g), dim3(kBlock), 0, st, sv, n, x, y, inten, gx, gy,
+                       gi);
     hipLaunchKernelGGL(k_summarize, dim3(grid_for(n_seg, 64, 8192)), dim3(64), 0, st, sk, sv,
-                       seg_start, n_seg, n, x, y, inten, pf, o_frame, o_label, o_count, o_first,
+                       seg_start, n_seg, n, gx, gy, gi, pf, o_frame, o_label, o_count, o_first,
                        o_cx, o_cy, o_mi);
     RPT_CHECK_LAUNCH();
   }

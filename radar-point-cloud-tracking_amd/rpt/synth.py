@@ -35,7 +35,7 @@ class SynthConfig:
     bins: int = 1024
     gains: Tuple[int, ...] = (40, 50, 75)
     scale: float = 231.5
-    n_targets: int = 40
+    n_targets: int = 56
     seed: int = 0
     target_seed: int = 123
     clutter_density: float = 0.012          # kept echo cells per m^2 per sweep (before stride)
