@@ -135,6 +135,36 @@ int32_t rpt_stdbscan(const float* x, const float* y, const float* z, int64_t str
                      int32_t min_samples, int32_t* labels, rpt_stdbscan_stats* stats,
                      void* stream);
 
+/* ---- phased ST-DBSCAN (frame-sharded multi-GPU) -------------------------------------
+ * The fused rpt_stdbscan split into phases so ranks can exchange halo data between them:
+ * build (bounds + grid, 1 sync) -> core (flags, optionally copied out in original order) ->
+ * set_core (overwrite flags, e.g. halo points with their owner's) -> components (comp[i] = min
+ * original index of i's core component, -1 for non-core) -> labels_global (ids from global
+ * representatives).  The handle owns its device memory. */
+typedef struct rpt_dbscan rpt_dbscan;
+rpt_dbscan* rpt_dbscan_create(void);
+void rpt_dbscan_destroy(rpt_dbscan* h);
+int32_t rpt_dbscan_build(rpt_dbscan* h, const float* x, const float* y, const float* z,
+                         int64_t stride, const float* times, int64_t n, double eps_space,
+                         double eps_time, int32_t min_samples, void* stream);
+int32_t rpt_dbscan_core(rpt_dbscan* h, uint8_t* core_out /*dev [n] or NULL*/, void* stream);
+int32_t rpt_dbscan_set_core(rpt_dbscan* h, const uint8_t* core_in /*dev [n]*/, void* stream);
+int32_t rpt_dbscan_components(rpt_dbscan* h, int32_t* comp_out /*dev [n]*/, void* stream);
+/* rep[i] (dev int64 [n]): global representative of core point i (-1 otherwise); reps_sorted
+ * (dev int64 [n_reps]) all representatives ascending; label = rank of the representative;
+ * non-core points take the smallest adjacent representative (reference border rule). */
+int32_t rpt_dbscan_labels_global(rpt_dbscan* h, const int64_t* rep, const int64_t* reps_sorted,
+                                 int64_t n_reps, int32_t* labels, void* stream);
+/* rep_out[i] = map(comp[i] + base) for comp[i] >= 0 (map = sorted keys -> vals, identity when
+ * absent), -1 otherwise. */
+int32_t rpt_remap_components(const int32_t* comp, int64_t n, int64_t base, const int64_t* keys,
+                             const int64_t* vals, int64_t n_keys, int64_t* rep_out,
+                             void* stream);
+/* Global indices g = base + i, i in [lo, hi), with rep[i] == g, ascending; *count_host (sync). */
+int32_t rpt_select_roots(const int64_t* rep, int64_t base, int64_t lo, int64_t hi,
+                         int64_t* out /*dev, capacity hi-lo*/, int64_t* count_host,
+                         void* stream);
+
 /* nearest palette colour index (first minimum) as float32: colors u8 [n][3],
  * palette f32 [n_pal][3] in ascending-gain order. */
 int32_t rpt_infer_time_from_colors(const uint8_t* colors, int64_t n, const float* palette,

@@ -51,9 +51,81 @@ int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
                           int64_t* o_count, int64_t* o_first, float* o_cx, float* o_cy,
                           float* o_mi, int64_t* frame_first_noise, int64_t* n_seg_host,
                           hipStream_t st);
+struct DbscanState;
+DbscanState* dbscan_create();
+void dbscan_destroy(DbscanState* s);
+int32_t dbscan_build(DbscanState* S, const float* x, const float* y, const float* z,
+                     int64_t stride, const float* t, int64_t n, double eps_space,
+                     double eps_time, int32_t ms, hipStream_t st);
+int32_t dbscan_core(DbscanState* S, uint8_t* core_out, hipStream_t st);
+int32_t dbscan_set_core(DbscanState* S, const uint8_t* core_in, hipStream_t st);
+int32_t dbscan_components(DbscanState* S, int32_t* comp_out, hipStream_t st);
+int32_t dbscan_labels_global(DbscanState* S, const int64_t* rep, const int64_t* reps, int64_t nr,
+                             int32_t* labels, hipStream_t st);
+int32_t remap_components(const int32_t* comp, int64_t n, int64_t base, const int64_t* keys,
+                         const int64_t* vals, int64_t nk, int64_t* out, hipStream_t st);
+int32_t select_roots(const int64_t* rep, int64_t base, int64_t lo, int64_t hi, int64_t* out,
+                     int64_t* count_host, hipStream_t st);
 }  // namespace rpt
 
+struct rpt_dbscan {
+  rpt::DbscanState* s;
+};
+
 extern "C" {
+
+rpt_dbscan* rpt_dbscan_create(void) { return new rpt_dbscan{rpt::dbscan_create()}; }
+
+void rpt_dbscan_destroy(rpt_dbscan* h) {
+  if (!h) return;
+  rpt::dbscan_destroy(h->s);
+  delete h;
+}
+
+int32_t rpt_dbscan_build(rpt_dbscan* h, const float* x, const float* y, const float* z,
+                         int64_t stride, const float* times, int64_t n, double eps_space,
+                         double eps_time, int32_t min_samples, void* stream) {
+  rpt::clear_error();
+  return rpt::dbscan_build(h->s, x, y, z, stride, times, n, eps_space, eps_time, min_samples,
+                           rpt::as_stream(stream));
+}
+
+int32_t rpt_dbscan_core(rpt_dbscan* h, uint8_t* core_out, void* stream) {
+  rpt::clear_error();
+  return rpt::dbscan_core(h->s, core_out, rpt::as_stream(stream));
+}
+
+int32_t rpt_dbscan_set_core(rpt_dbscan* h, const uint8_t* core_in, void* stream) {
+  rpt::clear_error();
+  return rpt::dbscan_set_core(h->s, core_in, rpt::as_stream(stream));
+}
+
+int32_t rpt_dbscan_components(rpt_dbscan* h, int32_t* comp_out, void* stream) {
+  rpt::clear_error();
+  return rpt::dbscan_components(h->s, comp_out, rpt::as_stream(stream));
+}
+
+int32_t rpt_dbscan_labels_global(rpt_dbscan* h, const int64_t* rep, const int64_t* reps_sorted,
+                                 int64_t n_reps, int32_t* labels, void* stream) {
+  rpt::clear_error();
+  return rpt::dbscan_labels_global(h->s, rep, reps_sorted, n_reps, labels,
+                                   rpt::as_stream(stream));
+}
+
+int32_t rpt_remap_components(const int32_t* comp, int64_t n, int64_t base, const int64_t* keys,
+                             const int64_t* vals, int64_t n_keys, int64_t* rep_out,
+                             void* stream) {
+  rpt::clear_error();
+  return rpt::remap_components(comp, n, base, keys, vals, n_keys, rep_out,
+                               rpt::as_stream(stream));
+}
+
+int32_t rpt_select_roots(const int64_t* rep, int64_t base, int64_t lo, int64_t hi, int64_t* out,
+                         int64_t* count_host, void* stream) {
+  rpt::clear_error();
+  return rpt::select_roots(rep, base, lo, hi, out, count_host, rpt::as_stream(stream));
+}
+
 
 int32_t rpt_version(void) { return 100; }  // 0.1.0
 

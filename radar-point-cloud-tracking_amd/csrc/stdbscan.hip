@@ -37,6 +37,7 @@
 #include <climits>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 
 #include "common.h"
 
@@ -545,7 +546,11 @@ __device__ __forceinline__ int classify_cells(const float4& A1, const float4& B1
 }
 
 // K6a: mutual-cell x mutual-cell unions, one thread per cell A, each unordered pair once (B > A).
-template <int D>
+// PARTIAL = false: only pairs the boxes prove fully adjacent (cheap, no search).
+// PARTIAL = true : undecided pairs whose roots still differ after the first pass (a kernel
+//                  boundary later, so most such pairs are already connected), searched for one
+//                  adjacent core pair with both sides culled against the other cell's box.
+template <int D, bool PARTIAL>
 __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict__ pts,
                                                        int64_t cells, Geom g,
                                                        const int32_t* __restrict__ cell_start,
@@ -586,21 +591,21 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
             const int rb = rep[cb];
             if (rb < 0 || !mutual[cb]) continue;
             const int cls = classify_cells<D>(A1, boxA[cb], A2, boxB[cb], g);
-            if (cls == 0) continue;
-            if (cls == 1) {
-              uf_unite(parent, sorig, ra, rb);
+            if (!PARTIAL) {
+              if (cls == 1) uf_unite(parent, sorig, ra, rb);
               continue;
             }
+            if (cls != 2) continue;
             if (uf_find(parent, ra) == uf_find(parent, rb)) continue;
             const int eb = cell_start[cb + 1];
-            const float4 B1 = boxA[cb], B2 = boxB[cb];
+            // B's core points that can reach A's box at all
             bool hit = false;
-            for (int a = ra; a < ea && !hit; ++a) {
-              if (!core[a]) continue;
-              const float4 pa = pts[a];
-              if (classify<D>(pa, B1, B2, g) == 0) continue;
-              for (int b = rb; b < eb; ++b) {
-                if (core[b] && adjacent<D>(pa, pts[b], g)) {
+            for (int b = rb; b < eb && !hit; ++b) {
+              if (!core[b]) continue;
+              const float4 pb = pts[b];
+              if (classify<D>(pb, A1, A2, g) == 0) continue;
+              for (int a = ra; a < ea; ++a) {
+                if (core[a] && adjacent<D>(pb, pts[a], g)) {
                   hit = true;
                   break;
                 }
@@ -793,6 +798,80 @@ __global__ __launch_bounds__(kBlock) void k_isolated_labels(int32_t* labels, int
 // Non-finite-time points are isolated; with min_samples <= 0 they are singleton clusters and
 // flagged as their own component minimum (handled by k_ccmin via parent = self).
 
+// ---------------------------------------------------------------- phased state (multi-GPU)
+__global__ void k_core_to_orig(const uint8_t* __restrict__ core, const int32_t* __restrict__ sorig,
+                               int64_t n, uint8_t* __restrict__ out) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x)
+    out[sorig[s]] = core[s];
+}
+__global__ void k_core_from_orig(const uint8_t* __restrict__ in, const int32_t* __restrict__ sorig,
+                                 int64_t n, uint8_t* __restrict__ core) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x)
+    core[s] = in[sorig[s]] ? 1 : 0;
+}
+// comp[orig] = minimum original index of the point's core component, -1 for non-core
+__global__ void k_comp_out(int32_t* parent, const uint8_t* __restrict__ core,
+                           const int32_t* __restrict__ sorig, int64_t n,
+                           int32_t* __restrict__ comp) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x)
+    comp[sorig[s]] = core[s] ? sorig[uf_find(parent, (int)s)] : -1;
+}
+// srep[s] = rep[sorig[s]] for core points (global representative), -1 otherwise
+__global__ void k_srep(const int64_t* __restrict__ rep, const uint8_t* __restrict__ core,
+                       const int32_t* __restrict__ sorig, int64_t n, int64_t* __restrict__ srep) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x)
+    srep[s] = core[s] ? rep[sorig[s]] : -1;
+}
+__device__ __forceinline__ int32_t rep_id(const int64_t* __restrict__ reps, int64_t nr, int64_t v) {
+  int64_t lo = 0, hi = nr;
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (reps[m] < v) lo = m + 1; else hi = m;
+  }
+  return (lo < nr && reps[lo] == v) ? (int32_t)lo : -2;  // -2: representative missing (bug)
+}
+// Final labels from global representatives: core -> id(rep); non-core -> id(min rep over adjacent
+// core points); ids = rank of the representative in the sorted global list.
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_label_global(
+    const float4* __restrict__ pts, const int32_t* __restrict__ skey, int64_t n, Geom g,
+    const int32_t* __restrict__ cell_start, const float4* __restrict__ boxA,
+    const float4* __restrict__ boxB, const float2* __restrict__ slab_t,
+    const int64_t* __restrict__ srep, const int32_t* __restrict__ rep,
+    const uint8_t* __restrict__ mutual, const int32_t* __restrict__ sorig,
+    const int64_t* __restrict__ reps, int64_t nr, int32_t* __restrict__ labels) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const int64_t own = srep[s];
+  if (own >= 0) {
+    labels[sorig[s]] = rep_id(reps, nr, own);
+    return;
+  }
+  const int32_t key = skey[s];
+  int64_t best = INT64_MAX;
+  if ((int64_t)key < g.cells) {
+    const float4 p = pts[s];
+    for_each_cell<D>(p, key, g, cell_start, boxA, boxB, slab_t,
+                     [&](int64_t c, int b, int e, int cls) -> bool {
+                       const int r = rep[c];
+                       if (r < 0) return false;
+                       for (int j = r; j < e; ++j) {
+                         const int64_t m = srep[j];
+                         if (m >= 0 && m < best && (cls == 1 || adjacent<D>(p, pts[j], g))) {
+                           best = m;
+                           if (mutual[c]) break;  // one component per mutual cell
+                         }
+                       }
+                       return false;
+                     });
+  }
+  labels[sorig[s]] = (best == INT64_MAX) ? -1 : rep_id(reps, nr, best);
+}
+
 struct Timer {
   bool on = false;
   hipStream_t st{};
@@ -801,8 +880,10 @@ struct Timer {
   void start(bool enable, hipStream_t s) {
     on = enable;
     st = s;
+    k = 0;
     if (!on) return;
-    for (auto& e : ev) (void)hipEventCreate(&e);
+    for (auto& e : ev)
+      if (!e) (void)hipEventCreate(&e);
     (void)hipEventRecord(ev[k++], st);
   }
   void mark() {
@@ -814,40 +895,57 @@ struct Timer {
     return t;
   }
   ~Timer() {
-    if (on)
-      for (auto& e : ev) (void)hipEventDestroy(e);
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
   }
 };
 
-template <int D>
-int32_t stdbscan_impl(const float* x, const float* y, const float* z, int64_t stride,
-                      const float* t, int64_t n, double eps_space, double eps_time,
-                      int32_t min_samples, int32_t* labels, rpt_stdbscan_stats* stats,
-                      hipStream_t st) {
+}  // namespace
+
+// One ST-DBSCAN problem on one device, split in phases so that a frame-sharded multi-GPU run
+// can exchange halo core flags and component ids between them.  Owns its device memory.
+struct DbscanState {
+  Scratch arena;
+  int dim = 2;
+  int64_t n = 0;
+  bool degenerate = false;  // negative/NaN eps: no pair passes, not even (i, i)
+  int32_t min_samples = 0;
+  Geom g{};
+  int64_t C = 0, nt = 0;
+  float4* pts = nullptr;
+  int32_t *sorig = nullptr, *skey = nullptr, *cell_start = nullptr, *rep = nullptr;
+  float4 *boxA = nullptr, *boxB = nullptr;
+  uint8_t *mutual = nullptr, *core = nullptr;
+  float2* slab_t = nullptr;
+  int32_t *parent = nullptr, *ccmin = nullptr, *cid = nullptr, *nc_list = nullptr;
+  int64_t* srep = nullptr;
+  int64_t* stmp = nullptr;
   Timer tm;
-  tm.start(stats && stats->timing, st);
-  const float epst = (float)eps_time;
+
+  template <int D>
+  int32_t build_t(const float* x, const float* y, const float* z, int64_t stride, const float* t,
+                  double eps_space, double eps_time, hipStream_t st);
+  int32_t build(const float* x, const float* y, const float* z, int64_t stride, const float* t,
+                int64_t n_, double eps_space, double eps_time, int32_t ms, bool timing,
+                hipStream_t st);
+  int32_t core_pass(hipStream_t st);
+  int32_t union_pass(hipStream_t st);
+  int32_t labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st);
+  int32_t labels_global(const int64_t* rep_orig, const int64_t* reps, int64_t nr,
+                        int32_t* labels, hipStream_t st);
+};
+
+template <int D>
+int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int64_t stride,
+                             const float* t, double eps_space, double eps_time, hipStream_t st) {
   const int gb = grid_for(n, kBlock, 2048);
-  // ---- degenerate parameters: no pair (not even i,i) passes the predicate
-  if (!(eps_space >= 0.0) || !(epst >= 0.0f)) {
-    hipLaunchKernelGGL(k_isolated_labels, dim3(gb), dim3(kBlock), 0, st, labels, n,
-                       min_samples <= 0 ? 1 : 0);
-    RPT_CHECK_LAUNCH();
-    if (stats) {
-      stats->n_points = n;
-      stats->n_core = min_samples <= 0 ? n : 0;
-      stats->n_clusters = min_samples <= 0 ? (int32_t)n : 0;
-    }
-    return RPT_OK;
-  }
-  Scratch& sc = scratch();
-  // ---- bounds (one small sync)
+  // ---- bounds (one small sync); the arena is re-reserved below, so copy results out first
   {
     Budget bb;
     bb.add<Bounds>(1);
-    RPT_TRY(sc.reserve(bb.bytes, st));
+    RPT_TRY(arena.reserve(bb.bytes, st));
   }
-  Bounds* d_b = sc.carve_n<Bounds>(1);
+  Bounds* d_b = arena.carve_n<Bounds>(1);
   hipLaunchKernelGGL(k_bounds_init, dim3(1), dim3(1), 0, st, d_b);
   hipLaunchKernelGGL(k_bounds<D>, dim3(grid_for(n, kBlock, 1024)), dim3(kBlock), 0, st, x, y, z,
                      stride, t, n, d_b);
@@ -860,8 +958,8 @@ int32_t stdbscan_impl(const float* x, const float* y, const float* z, int64_t st
     set_error("Input contains NaN or infinity in coordinates");
     return RPT_ENONFINITE;
   }
-  // ---- geometry
-  Geom g{};
+  const float epst = (float)eps_time;
+  g = Geom{};
   g.eps2 = eps_space * eps_space;
   g.epst = epst;
   g.min_samples = min_samples;
@@ -870,31 +968,23 @@ int32_t stdbscan_impl(const float* x, const float* y, const float* z, int64_t st
     lo[k] = (double)ord2f(hb.mn[k]);
     hi[k] = (double)ord2f(hb.mx[k]);
   }
-  if (hb.n_finite_t == 0) {
-    lo[3] = hi[3] = 0.0;
-  }
+  if (hb.n_finite_t == 0) lo[3] = hi[3] = 0.0;
   const double margin = 1.0 + 1.0 / 1048576.0;  // 2^-20
   double cs = (eps_space > 0.0 ? eps_space * 0.5 : 1.0) * margin;
-  double ct;
-  if (!hb.nonintegral_t)
-    ct = 1.0;  // one slab per integer time value (frame id)
-  else
-    ct = (epst > 0.f ? (double)epst : 1.0) * margin;
-  const int64_t cmax = std::max<int64_t>(int64_t(1) << 22, 4 * n) < (int64_t(1) << 30)
-                           ? std::max<int64_t>(int64_t(1) << 22, 4 * n)
-                           : (int64_t(1) << 30);
+  double ct = !hb.nonintegral_t ? 1.0 : (epst > 0.f ? (double)epst : 1.0) * margin;
+  const int64_t cmax = std::min<int64_t>(std::max<int64_t>(int64_t(1) << 22, 4 * n),
+                                         int64_t(1) << 30);
   auto dims = [&](double ext, double side) -> int64_t {
-    double q = floor(ext / side) + 1.0;
+    const double q = floor(ext / side) + 1.0;
     return q > 1e9 ? (int64_t)1e9 : (int64_t)q;
   };
-  int64_t nx, ny, nz, nt;
+  int64_t nx = 1, ny = 1, nz = 1;
   for (int it = 0; it < 200; ++it) {
     nx = dims(hi[0] - lo[0], cs);
     ny = dims(hi[1] - lo[1], cs);
     nz = (D == 3) ? dims(hi[2] - lo[2], cs) : 1;
     nt = dims(hi[3] - lo[3], ct);
-    const double cells = (double)nx * ny * nz * nt;
-    if (cells <= (double)cmax) break;
+    if ((double)nx * ny * nz * nt <= (double)cmax) break;
     if ((double)nt > (double)nx * ny * nz)
       ct *= 2.0;
     else
@@ -911,61 +1001,55 @@ int32_t stdbscan_impl(const float* x, const float* y, const float* z, int64_t st
   g.nz = (int)nz;
   g.nt = (int)nt;
   g.cells = nx * ny * nz * nt;
-  const int64_t C = g.cells;
-  const int64_t C1 = C + 1;  // + isolated cell (non-finite t)
-  // ---- scratch
+  C = g.cells;
+  const int64_t C1 = C + 1;  // + the isolated cell (non-finite t)
   Budget bud;
   bud.add<Bounds>(1);
-  bud.add<uint32_t>(n);  // keys
-  bud.add<uint32_t>(n);  // vals
-  bud.add<uint32_t>(n);  // keys_alt
-  bud.add<uint32_t>(n);  // vals_alt
+  for (int k = 0; k < 4; ++k) bud.add<uint32_t>(n);  // keys, vals, alt
   bud.add<int64_t>(radix_tmp_elems(n));
-  bud.add<float4>(n);        // pts
+  bud.add<float4>(n);
   bud.add<int32_t>(n);       // sorig
   bud.add<int32_t>(n);       // skey
-  bud.add<int32_t>(C1 + 1);  // cell_start (count, then scanned)
+  bud.add<int32_t>(C1 + 1);  // cell_start
   bud.add<int64_t>(scan_tmp_elems(C1 + 1) + scan_tmp_elems(n + 1));
-  bud.add<float4>(C1);  // boxA
-  bud.add<float4>(C1);  // boxB
-  bud.add<uint8_t>(C1);  // mutual
+  bud.add<float4>(C1);
+  bud.add<float4>(C1);
+  bud.add<uint8_t>(C1);
   bud.add<int32_t>(C1);  // rep
-  bud.add<float2>(nt);   // slab_t
-  bud.add<uint8_t>(n);   // core
-  bud.add<int32_t>(n);   // parent
-  bud.add<int32_t>(n);   // cmin
-  bud.add<int32_t>(n);   // ccmin
-  bud.add<int32_t>(n + 1);  // is_min -> cid
+  bud.add<float2>(nt);
+  bud.add<uint8_t>(n);      // core
+  bud.add<int32_t>(n);      // parent
+  bud.add<int32_t>(n);      // ccmin
+  bud.add<int32_t>(n + 1);  // cid
   bud.add<int32_t>(n + 1);  // non-core list (+count)
-  RPT_TRY(sc.reserve(bud.bytes, st));
-  (void)sc.carve_n<Bounds>(1);
-  uint32_t* keys = sc.carve_n<uint32_t>(n);
-  uint32_t* vals = sc.carve_n<uint32_t>(n);
-  uint32_t* keys_alt = sc.carve_n<uint32_t>(n);
-  uint32_t* vals_alt = sc.carve_n<uint32_t>(n);
-  int64_t* rtmp = sc.carve_n<int64_t>(radix_tmp_elems(n));
-  float4* pts = sc.carve_n<float4>(n);
-  int32_t* sorig = sc.carve_n<int32_t>(n);
-  int32_t* skey = sc.carve_n<int32_t>(n);
-  int32_t* cell_start = sc.carve_n<int32_t>(C1 + 1);
-  int64_t* stmp = sc.carve_n<int64_t>(scan_tmp_elems(C1 + 1) + scan_tmp_elems(n + 1));
-  float4* boxA = sc.carve_n<float4>(C1);
-  float4* boxB = sc.carve_n<float4>(C1);
-  uint8_t* mutual = sc.carve_n<uint8_t>(C1);
-  int32_t* rep = sc.carve_n<int32_t>(C1);
-  float2* slab_t = sc.carve_n<float2>(nt);
-  uint8_t* core = sc.carve_n<uint8_t>(n);
-  int32_t* parent = sc.carve_n<int32_t>(n);
-  int32_t* cmin = sc.carve_n<int32_t>(n);
-  int32_t* ccmin = sc.carve_n<int32_t>(n);
-  int32_t* cid = sc.carve_n<int32_t>(n + 1);
-  int32_t* nc_list = sc.carve_n<int32_t>(n + 1);
-  int32_t* nc_count = nc_list + n;
-  if (!nc_list) {
+  bud.add<int64_t>(n);      // srep (global finalize)
+  RPT_TRY(arena.reserve(bud.bytes, st));
+  (void)arena.carve_n<Bounds>(1);
+  uint32_t* keys = arena.carve_n<uint32_t>(n);
+  uint32_t* vals = arena.carve_n<uint32_t>(n);
+  uint32_t* keys_alt = arena.carve_n<uint32_t>(n);
+  uint32_t* vals_alt = arena.carve_n<uint32_t>(n);
+  int64_t* rtmp = arena.carve_n<int64_t>(radix_tmp_elems(n));
+  pts = arena.carve_n<float4>(n);
+  sorig = arena.carve_n<int32_t>(n);
+  skey = arena.carve_n<int32_t>(n);
+  cell_start = arena.carve_n<int32_t>(C1 + 1);
+  stmp = arena.carve_n<int64_t>(scan_tmp_elems(C1 + 1) + scan_tmp_elems(n + 1));
+  boxA = arena.carve_n<float4>(C1);
+  boxB = arena.carve_n<float4>(C1);
+  mutual = arena.carve_n<uint8_t>(C1);
+  rep = arena.carve_n<int32_t>(C1);
+  slab_t = arena.carve_n<float2>(nt);
+  core = arena.carve_n<uint8_t>(n);
+  parent = arena.carve_n<int32_t>(n);
+  ccmin = arena.carve_n<int32_t>(n);
+  cid = arena.carve_n<int32_t>(n + 1);
+  nc_list = arena.carve_n<int32_t>(n + 1);
+  srep = arena.carve_n<int64_t>(n);
+  if (!srep) {
     set_error("internal: scratch carve overflow");
     return RPT_ENOMEM;
   }
-  // ---- K4: grid build
   RPT_HIP(hipMemsetAsync(cell_start, 0, sizeof(int32_t) * (C1 + 1), st));
   hipLaunchKernelGGL(k_keys<D>, dim3(gb), dim3(kBlock), 0, st, x, y, z, stride, t, n, g, keys,
                      vals, cell_start);
@@ -986,34 +1070,97 @@ int32_t stdbscan_impl(const float* x, const float* y, const float* z, int64_t st
                      (int64_t)(C / nt), (int)nt, slab_t);
   RPT_CHECK_LAUNCH();
   tm.mark();
-  // ---- K5: core flags
+  return RPT_OK;
+}
+
+int32_t DbscanState::build(const float* x, const float* y, const float* z, int64_t stride,
+                           const float* t, int64_t n_, double eps_space, double eps_time,
+                           int32_t ms, bool timing, hipStream_t st) {
+  n = n_;
+  dim = z ? 3 : 2;
+  min_samples = ms;
+  tm.start(timing, st);
+  degenerate = !(eps_space >= 0.0) || !((float)eps_time >= 0.0f);
+  if (degenerate) return RPT_OK;
+  return dim == 2 ? build_t<2>(x, y, z, stride, t, eps_space, eps_time, st)
+                  : build_t<3>(x, y, z, stride, t, eps_space, eps_time, st);
+}
+
+int32_t DbscanState::core_pass(hipStream_t st) {
+  if (degenerate) return RPT_OK;
   const unsigned gp = (unsigned)((n + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(k_core<D>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
-                     boxA, boxB, slab_t, mutual, core);
+  if (dim == 2)
+    hipLaunchKernelGGL(k_core<2>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
+                       boxA, boxB, slab_t, mutual, core);
+  else
+    hipLaunchKernelGGL(k_core<3>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
+                       boxA, boxB, slab_t, mutual, core);
   RPT_CHECK_LAUNCH();
   tm.mark();
-  // ---- K6: union
+  return RPT_OK;
+}
+
+int32_t DbscanState::union_pass(hipStream_t st) {
+  if (degenerate) return RPT_OK;
+  const int gb = grid_for(n, kBlock, 2048);
+  const int gc = grid_for(C, kBlock, 8192);
+  const unsigned gp = (unsigned)((n + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(k_rep, dim3(gc), dim3(kBlock), 0, st, cell_start, C, core, rep);
   hipLaunchKernelGGL(k_parent_init, dim3(gb), dim3(kBlock), 0, st, parent, n, core, skey, mutual,
                      rep, C);
-  hipLaunchKernelGGL(k_union_cells<D>, dim3(gc), dim3(kBlock), 0, st, pts, C, g, cell_start, boxA,
-                     boxB, slab_t, core, rep, mutual, sorig, parent);
-  hipLaunchKernelGGL(k_union<D>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
-                     boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
+  if (dim == 2) {
+    hipLaunchKernelGGL((k_union_cells<2, false>), dim3(gc), dim3(kBlock), 0, st, pts, C, g,
+                       cell_start, boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
+    hipLaunchKernelGGL((k_union_cells<2, true>), dim3(gc), dim3(kBlock), 0, st, pts, C, g,
+                       cell_start, boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
+    hipLaunchKernelGGL(k_union<2>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
+                       boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
+  } else {
+    hipLaunchKernelGGL((k_union_cells<3, false>), dim3(gc), dim3(kBlock), 0, st, pts, C, g,
+                       cell_start, boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
+    hipLaunchKernelGGL((k_union_cells<3, true>), dim3(gc), dim3(kBlock), 0, st, pts, C, g,
+                       cell_start, boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
+    hipLaunchKernelGGL(k_union<3>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
+                       boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
+  }
+  RPT_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_compress, dim3(gb), dim3(kBlock), 0, st, parent, core, n, sorig,
+                     (int32_t*)nullptr);
   RPT_CHECK_LAUNCH();
   tm.mark();
-  // ---- K7/K8: component minima, ids, labels
-  hipLaunchKernelGGL(k_compress, dim3(gb), dim3(kBlock), 0, st, parent, core, n, sorig, cmin);
+  return RPT_OK;
+}
+
+int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st) {
+  const int gb = grid_for(n, kBlock, 2048);
+  if (degenerate) {
+    hipLaunchKernelGGL(k_isolated_labels, dim3(gb), dim3(kBlock), 0, st, labels, n,
+                       min_samples <= 0 ? 1 : 0);
+    RPT_CHECK_LAUNCH();
+    if (stats) {
+      stats->n_points = n;
+      stats->n_core = min_samples <= 0 ? n : 0;
+      stats->n_clusters = min_samples <= 0 ? (int32_t)n : 0;
+    }
+    return RPT_OK;
+  }
+  const unsigned gp = (unsigned)((n + kBlock - 1) / kBlock);
+  int32_t* nc_count = nc_list + n;
   RPT_HIP(hipMemsetAsync(cid, 0, sizeof(int32_t) * (n + 1), st));
   RPT_HIP(hipMemsetAsync(nc_count, 0, sizeof(int32_t), st));
-  hipLaunchKernelGGL(k_ccmin, dim3(gb), dim3(kBlock), 0, st, parent, core, n, sorig, cmin,
-                     ccmin, cid, nc_list, nc_count);
+  hipLaunchKernelGGL(k_ccmin, dim3(gb), dim3(kBlock), 0, st, parent, core, n, sorig,
+                     (const int32_t*)nullptr, ccmin, cid, nc_list, nc_count);
   RPT_CHECK_LAUNCH();
   RPT_TRY(exclusive_scan_i32(cid, cid, n + 1, stmp, st));
   hipLaunchKernelGGL(k_label_core, dim3(gb), dim3(kBlock), 0, st, ccmin, n, sorig, cid, labels);
-  hipLaunchKernelGGL(k_label<D>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
-                     boxA, boxB, slab_t, ccmin, rep, mutual, sorig, cid, nc_list, nc_count,
-                     labels);
+  if (dim == 2)
+    hipLaunchKernelGGL(k_label<2>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
+                       boxA, boxB, slab_t, ccmin, rep, mutual, sorig, cid, nc_list, nc_count,
+                       labels);
+  else
+    hipLaunchKernelGGL(k_label<3>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
+                       boxA, boxB, slab_t, ccmin, rep, mutual, sorig, cid, nc_list, nc_count,
+                       labels);
   RPT_CHECK_LAUNCH();
   tm.mark();
   if (stats) {
@@ -1028,7 +1175,7 @@ int32_t stdbscan_impl(const float* x, const float* y, const float* z, int64_t st
     stats->grid_dims[2] = g.nz;
     stats->grid_dims[3] = g.nt;
     stats->grid_cells = C;
-    if (tm.on) {
+    if (tm.on && tm.k >= 6) {
       RPT_HIP(hipEventSynchronize(tm.ev[tm.k - 1]));
       stats->ms_bounds = tm.ms(0);
       stats->ms_grid = tm.ms(1);
@@ -1040,11 +1187,29 @@ int32_t stdbscan_impl(const float* x, const float* y, const float* z, int64_t st
   return RPT_OK;
 }
 
-}  // namespace
+int32_t DbscanState::labels_global(const int64_t* rep_orig, const int64_t* reps, int64_t nr,
+                                   int32_t* labels, hipStream_t st) {
+  if (degenerate) {
+    set_error("rpt_dbscan_labels_global: degenerate parameters are handled by rpt_stdbscan");
+    return RPT_ENOTSUP;
+  }
+  const int gb = grid_for(n, kBlock, 2048);
+  const unsigned gp = (unsigned)((n + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(k_srep, dim3(gb), dim3(kBlock), 0, st, rep_orig, core, sorig, n, srep);
+  if (dim == 2)
+    hipLaunchKernelGGL(k_label_global<2>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g,
+                       cell_start, boxA, boxB, slab_t, srep, rep, mutual, sorig, reps, nr,
+                       labels);
+  else
+    hipLaunchKernelGGL(k_label_global<3>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g,
+                       cell_start, boxA, boxB, slab_t, srep, rep, mutual, sorig, reps, nr,
+                       labels);
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
+}
 
-int32_t stdbscan(const float* x, const float* y, const float* z, int64_t stride, const float* t,
-                 int64_t n, double eps_space, double eps_time, int32_t min_samples,
-                 int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st, int dim) {
+static int32_t check_args(const float* x, const float* y, const float* z, int64_t stride,
+                          const float* t, int64_t n, int dim) {
   if (n <= 0) {
     set_error("Found array with 0 sample(s) (shape=(0, %d)) while a minimum of 1 is required.",
               dim);
@@ -1054,16 +1219,84 @@ int32_t stdbscan(const float* x, const float* y, const float* z, int64_t stride,
     set_error("rpt_stdbscan: n=%lld exceeds the int32 index space", (long long)n);
     return RPT_ENOTSUP;
   }
-  if (!x || !y || !t || !labels || (dim == 3 && !z) || stride < 1) {
+  if (!x || !y || !t || (dim == 3 && !z) || stride < 1) {
     set_error("rpt_stdbscan: null pointer or bad stride");
     return RPT_EINVAL;
   }
-  if (dim == 2) return stdbscan_impl<2>(x, y, z, stride, t, n, eps_space, eps_time, min_samples,
-                                        labels, stats, st);
-  if (dim == 3) return stdbscan_impl<3>(x, y, z, stride, t, n, eps_space, eps_time, min_samples,
-                                        labels, stats, st);
-  set_error("rpt_stdbscan: dim must be 2 or 3 (got %d)", dim);
-  return RPT_ENOTSUP;
+  return RPT_OK;
+}
+
+static std::mutex g_state_mu;
+static std::vector<DbscanState*> g_states;  // per device, for the fused single-call path
+
+int32_t stdbscan(const float* x, const float* y, const float* z, int64_t stride, const float* t,
+                 int64_t n, double eps_space, double eps_time, int32_t min_samples,
+                 int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st, int dim) {
+  RPT_TRY(check_args(x, y, z, stride, t, n, dim));
+  if (!labels) {
+    set_error("rpt_stdbscan: null labels");
+    return RPT_EINVAL;
+  }
+  int dev = 0;
+  RPT_HIP(hipGetDevice(&dev));
+  DbscanState* S;
+  {
+    std::lock_guard<std::mutex> lk(g_state_mu);
+    if ((int)g_states.size() <= dev) g_states.resize(dev + 1, nullptr);
+    if (!g_states[dev]) g_states[dev] = new DbscanState();
+    S = g_states[dev];
+  }
+  RPT_TRY(S->build(x, y, z, stride, t, n, eps_space, eps_time, min_samples,
+                   stats && stats->timing, st));
+  RPT_TRY(S->core_pass(st));
+  RPT_TRY(S->union_pass(st));
+  return S->labels_local(labels, stats, st);
+}
+
+// ---- phased C-ABI bodies
+DbscanState* dbscan_create() { return new DbscanState(); }
+void dbscan_destroy(DbscanState* s) {
+  if (s) {
+    s->arena.release();
+    delete s;
+  }
+}
+int32_t dbscan_build(DbscanState* S, const float* x, const float* y, const float* z,
+                     int64_t stride, const float* t, int64_t n, double eps_space,
+                     double eps_time, int32_t ms, hipStream_t st) {
+  RPT_TRY(check_args(x, y, z, stride, t, n, z ? 3 : 2));
+  RPT_TRY(S->build(x, y, z, stride, t, n, eps_space, eps_time, ms, false, st));
+  if (S->degenerate) {
+    set_error("rpt_dbscan_build: negative or NaN eps (use rpt_stdbscan)");
+    return RPT_ENOTSUP;
+  }
+  return RPT_OK;
+}
+int32_t dbscan_core(DbscanState* S, uint8_t* core_out, hipStream_t st) {
+  RPT_TRY(S->core_pass(st));
+  if (core_out) {
+    hipLaunchKernelGGL(k_core_to_orig, dim3(grid_for(S->n, kBlock, 2048)), dim3(kBlock), 0, st,
+                       S->core, S->sorig, S->n, core_out);
+    RPT_CHECK_LAUNCH();
+  }
+  return RPT_OK;
+}
+int32_t dbscan_set_core(DbscanState* S, const uint8_t* core_in, hipStream_t st) {
+  hipLaunchKernelGGL(k_core_from_orig, dim3(grid_for(S->n, kBlock, 2048)), dim3(kBlock), 0, st,
+                     core_in, S->sorig, S->n, S->core);
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
+}
+int32_t dbscan_components(DbscanState* S, int32_t* comp_out, hipStream_t st) {
+  RPT_TRY(S->union_pass(st));
+  hipLaunchKernelGGL(k_comp_out, dim3(grid_for(S->n, kBlock, 2048)), dim3(kBlock), 0, st,
+                     S->parent, S->core, S->sorig, S->n, comp_out);
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
+}
+int32_t dbscan_labels_global(DbscanState* S, const int64_t* rep, const int64_t* reps, int64_t nr,
+                             int32_t* labels, hipStream_t st) {
+  return S->labels_global(rep, reps, nr, labels, st);
 }
 
 }  // namespace rpt

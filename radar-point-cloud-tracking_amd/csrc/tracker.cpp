@@ -365,6 +365,43 @@ struct Tracker {
     return (double)(s / (float)m);
   }
 
+  // prediction of object o `ahead` frames on (:135-140), in the dtype numpy would use
+  struct Pred {
+    bool f64;
+    double x, y;  // float64 prediction (f64) or the float32 value widened
+  };
+  Pred predict(const Object& o, int64_t ahead) const {
+    const size_t H = (size_t)p.motion_history_frames;
+    const size_t b = o.vel.size() > H ? o.vel.size() - H : 0;
+    const size_t m = o.vel.size() - b;
+    bool has64 = false;
+    for (size_t k = b; k < o.vel.size(); ++k) has64 |= o.vel[k].f64_zero;
+    const float lx = o.px.back(), ly = o.py.back();
+    if (has64) {
+      double sx = o.vel[b].f64_zero ? 0.0 : (double)o.vel[b].x;
+      double sy = o.vel[b].f64_zero ? 0.0 : (double)o.vel[b].y;
+      for (size_t k = b + 1; k < o.vel.size(); ++k) {
+        sx = sx + (o.vel[k].f64_zero ? 0.0 : (double)o.vel[k].x);
+        sy = sy + (o.vel[k].f64_zero ? 0.0 : (double)o.vel[k].y);
+      }
+      const double mx = sx / (double)m, my = sy / (double)m;
+      return Pred{true, (double)lx + mx * (double)ahead, (double)ly + my * (double)ahead};
+    }
+    float sx = o.vel[b].x, sy = o.vel[b].y;
+    for (size_t k = b + 1; k < o.vel.size(); ++k) {
+      sx = sx + o.vel[k].x;
+      sy = sy + o.vel[k].y;
+    }
+    const float mx = sx / (float)m, my = sy / (float)m;
+    const float px = lx + mx * (float)ahead;
+    const float py = ly + my * (float)ahead;
+    return Pred{false, (double)px, (double)py};
+  }
+  static double cost_pred(const Pred& q, float cx, float cy) {
+    if (q.f64) return f64_norm((double)cx - q.x, (double)cy - q.y);
+    return (double)f32_norm(cx - (float)q.x, cy - (float)q.y);
+  }
+
   // cost of cluster (cx,cy) vs object prediction (:135-140, :586-587)
   double cost_of(const Object& o, float cx, float cy, int64_t ahead) const {
     const size_t H = (size_t)p.motion_history_frames;
@@ -426,8 +463,8 @@ struct Tracker {
     cost.assign((size_t)k * m, 0.0);
     for (int32_t j = 0; j < m; ++j) {
       const Object& o = objs[live[j]];
-      const int64_t ahead = fid - o.last_seen;
-      for (int32_t i = 0; i < k; ++i) cost[(size_t)i * m + j] = cost_of(o, cx[i], cy[i], ahead);
+      const Pred q = predict(o, fid - o.last_seen);  // depends on the object only
+      for (int32_t i = 0; i < k; ++i) cost[(size_t)i * m + j] = cost_pred(q, cx[i], cy[i]);
     }
     const int32_t np_ = std::min(k, m);
     ra.assign(np_, 0);

@@ -114,6 +114,16 @@ _SIGS = [
      [vp, vp, vp, C.c_int64, vp, C.c_int64, C.c_double, C.c_double, C.c_int32, vp,
       C.POINTER(StdbscanStats), vp]),
     ("rpt_infer_time_from_colors", C.c_int32, [vp, C.c_int64, vp, C.c_int32, vp, vp]),
+    ("rpt_dbscan_create", vp, []),
+    ("rpt_dbscan_destroy", None, [vp]),
+    ("rpt_dbscan_build", C.c_int32,
+     [vp, vp, vp, vp, C.c_int64, vp, C.c_int64, C.c_double, C.c_double, C.c_int32, vp]),
+    ("rpt_dbscan_core", C.c_int32, [vp, vp, vp]),
+    ("rpt_dbscan_set_core", C.c_int32, [vp, vp, vp]),
+    ("rpt_dbscan_components", C.c_int32, [vp, vp, vp]),
+    ("rpt_dbscan_labels_global", C.c_int32, [vp, vp, vp, C.c_int64, vp, vp]),
+    ("rpt_remap_components", C.c_int32, [vp, C.c_int64, C.c_int64, vp, vp, C.c_int64, vp, vp]),
+    ("rpt_select_roots", C.c_int32, [vp, C.c_int64, C.c_int64, C.c_int64, vp, c_i64p, vp]),
     ("rpt_cluster_summaries", C.c_int32,
      [vp, vp, vp, vp, vp, C.c_int64, C.c_int32, C.c_int32, vp, vp, vp, vp, vp, vp, vp, vp,
       c_i64p, vp]),
