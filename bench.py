@@ -88,17 +88,34 @@ def main():
     from rpt.synth import DeviceSynth, SynthConfig
 
     _abi.load()
-    cfg = SynthConfig(n_frames=args.frames, frame0=rank * args.frames)
+    F = args.frames
+    cfg = SynthConfig(n_frames=F, frame0=rank * F)
     ds = DeviceSynth(cfg, dev)
     echo = ds.echo()
     torch.cuda.synchronize(dev)
-    pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), dev,
-                              timing=not args.no_timing)
-    pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
-                      cfg.n_frames * len(cfg.gains))
+    timing = not args.no_timing
+    if dist:
+        # frame-sharded global stack: rank r owns frames [r*F, (r+1)*F) (rpt/dist.py)
+        from rpt.dist import Comm, ShardedStackPipeline
+        from rpt.stages import HipOps
+
+        ops = HipOps(dev, timing=timing)
+        pipe = ShardedStackPipeline(ops, Comm(dev), cfg.gains, cfg.rows, cfg.bins, PathParams(),
+                                    timing=timing)
+        G = len(cfg.gains)
+        pipe.set_geometry(
+            tuple(torch.from_numpy(np.tile(a, F * G)).to(dev) for a in
+                  (np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t)),
+            torch.tensor(list(cfg.gains) * F, dtype=torch.int32, device=dev))
+        run = lambda: pipe.run(echo, _abi.ECHO_U8, rank * F)  # noqa: E731
+    else:
+        pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), dev, timing=timing)
+        pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
+                          cfg.n_frames * len(cfg.gains))
+        run = lambda: pipe.run(echo)  # noqa: E731
 
     for _ in range(args.warmup):
-        pipe.run(echo)
+        run()
     torch.cuda.synchronize(dev)
     if dist:
         tdist.barrier()
@@ -108,30 +125,37 @@ def main():
     k5_ms = []
     res = None
     for _ in range(args.steps):
-        res = pipe.run(echo)
+        res = run()
         for k, v in res.stage_ms.items():
             stage_acc[k] = stage_acc.get(k, 0.0) + v
-        if res.stage_ms:
-            k5_ms.append(res.stage_ms["dbscan_core"])
+        if timing:
+            k5_ms.append(res.stage_ms["dbscan_core"] if not dist else ops.last_core_ms())
     torch.cuda.synchronize(dev)
     if dist:
         tdist.barrier()
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
-    pts = float(res.n_points)
     if dist:
-        t = torch.tensor([dt, pts], dtype=torch.float64, device=dev)
-        tmax = t.clone()
-        tdist.all_reduce(tmax[:1], op=tdist.ReduceOp.MAX)
-        tdist.all_reduce(t[1:], op=tdist.ReduceOp.SUM)
-        dt, pts = float(tmax[0]), float(t[1])
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = float(t[0])
+        pts = float(res.n_points_global)        # K1 points of the whole global stack
+        n_core_in = ops.core_points             # [halo | own | halo] points of this rank
+        summary = {"points_clustered_rank0": res.n_clustered_local, "clusters": res.n_clusters,
+                   "segments": res.n_segments, "objects": len(res.tracker)
+                   if res.tracker is not None else None}
+    else:
+        pts = float(res.n_points)
+        n_core_in = res.n_clustered_input
+        summary = {"points_clustered_rank0": res.n_clustered_input, "clusters": res.n_clusters,
+                   "segments": res.n_segments, "objects": len(res.tracker)}
     value = pts * args.steps / dt / 1e6
     ms_step = dt / args.steps * 1e3
 
     roof = None
     if k5_ms:
         k5 = float(np.mean(k5_ms))
-        n_in = res.n_clustered_input
+        n_in = n_core_in
         achieved = K5_BYTES_PER_POINT * n_in / (k5 * 1e-3) / 1e9
         roof = {"kernel": "k_core (K5 neighbour count / core flag)", "bound": "hbm",
                 "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -161,9 +185,7 @@ def main():
                                    f"(4096 az x 1024 echo u8), land filter + ST-DBSCAN eps 8 / "
                                    f"eps_t 2 / min 15 + Hungarian tracking (BASELINE configs[2])",
                        "frames_per_gpu": args.frames, "points_per_step": int(pts),
-                       "points_clustered_rank0": res.n_clustered_input,
-                       "clusters_rank0": res.n_clusters, "segments_rank0": res.n_segments,
-                       "objects_rank0": len(res.tracker),
+                       **summary,
                        "parallelism": f"frame-sharded x{world}" if dist else "single GPU"},
             "roofline": roof, "cpu_baseline": cpu, "stage_ms": stage,
         }

@@ -1,0 +1,331 @@
+"""Frame-sharded multi-GPU run of the path: one process per GPU, torch.distributed
+(backend "nccl" = RCCL over xGMI on MI355X; "gloo" with host staging for CPU tests / several
+ranks sharing one GPU).
+
+Rank r owns the contiguous frame range [r*F, (r+1)*F) of one global stack.  ST-DBSCAN is global
+over the stack (the reference clusters all frames at once, 4_temporal_object_tracker.py:466-506)
+so the ranks cooperate; the result is identical to a single-device run:
+
+  1. K1 on own frames.                                                     (local)
+  2. land filter when the GLOBAL number of built frames exceeds 10: bounds all_reduce MIN/MAX,
+     identical float64 edges everywhere, count / intensity grids all_reduce SUM (integer-valued,
+     so exact), mask, local compaction.                                   (2 all_reduce rounds)
+  3. global point numbering: all_gather of kept counts (frames are in rank order).
+  4. halo: h = floor(eps_t) frames to each neighbour (points of the first / last h frames,
+     send/recv), so every owned point sees all its space-time neighbours.      (P2P)
+  5. core flags on [halo | own | halo]; halo flags replaced by their owners' flags.  (P2P)
+  6. local components (min-index union-find); halo points' component ids exchanged with their
+     owners, equivalences all_gather'ed, merged on the host (tiny), every component mapped to
+     its global minimum core index.                                       (P2P + all_gather)
+  7. global representatives: each rank lists the ones it owns, all_gather -> sorted; labels =
+     rank of the representative; border points take the smallest adjacent one.  (all_gather)
+  8. K9 summaries on own frames, gathered to rank 0, which runs the sequential tracker.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .pipeline import PathParams
+from .stages import LAND_GRID_RESOLUTION, Points, order_and_track
+
+_MIN, _MAX, _SUM = dist.ReduceOp.MIN, dist.ReduceOp.MAX, dist.ReduceOp.SUM
+
+
+class Comm:
+    """torch.distributed helpers; tensors are staged through host memory for gloo."""
+
+    def __init__(self, dev: torch.device, group=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.dev = dev
+        self.host = dist.get_backend(group) == "gloo"
+        self.cdev = torch.device("cpu") if self.host else dev
+
+    def _c(self, t: torch.Tensor) -> torch.Tensor:
+        return t.to(self.cdev).contiguous()
+
+    def all_reduce(self, t: torch.Tensor, op) -> torch.Tensor:
+        c = self._c(t).clone()
+        dist.all_reduce(c, op=op, group=self.group)
+        return c.to(t.device)
+
+    def all_gather_var(self, t: torch.Tensor) -> List[torch.Tensor]:
+        """all_gather of 1-D tensors of different lengths (returned on the input's device)."""
+        c = self._c(t).reshape(-1)
+        n = torch.tensor([c.numel()], dtype=torch.int64, device=self.cdev)
+        ns = [torch.zeros_like(n) for _ in range(self.world)]
+        dist.all_gather(ns, n, group=self.group)
+        ns = [int(v.item()) for v in ns]
+        m = max(ns) if ns else 0
+        pad = torch.zeros(max(m, 1), dtype=c.dtype, device=self.cdev)
+        pad[:c.numel()] = c
+        outs = [torch.empty_like(pad) for _ in range(self.world)]
+        dist.all_gather(outs, pad, group=self.group)
+        return [o[:k].to(t.device) for o, k in zip(outs, ns)]
+
+    def exchange(self, to_prev: Optional[torch.Tensor], to_next: Optional[torch.Tensor]
+                 ) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
+        """Send to_prev to rank-1 and to_next to rank+1; receive what they send back (the
+        neighbour's to_next / to_prev).  1-D tensors of one dtype; sizes are exchanged first."""
+        r, w = self.rank, self.world
+        has_prev, has_next = r > 0, r < w - 1
+        ref = to_prev if to_prev is not None else to_next
+        if ref is None:
+            return None, None
+        dt = ref.dtype
+
+        def p2p(sends, recvs):
+            ops = []
+            for peer, t in sends:
+                ops.append(dist.P2POp(dist.isend, t, peer, self.group))
+            for peer, t in recvs:
+                ops.append(dist.P2POp(dist.irecv, t, peer, self.group))
+            if ops:
+                for req in dist.batch_isend_irecv(ops):
+                    req.wait()
+
+        sz = lambda t: torch.tensor([t.numel() if t is not None else 0],  # noqa: E731
+                                    dtype=torch.int64, device=self.cdev)
+        rp = torch.zeros(1, dtype=torch.int64, device=self.cdev)
+        rn = torch.zeros(1, dtype=torch.int64, device=self.cdev)
+        sends, recvs = [], []
+        if has_prev:
+            sends.append((r - 1, sz(to_prev)))
+            recvs.append((r - 1, rp))
+        if has_next:
+            sends.append((r + 1, sz(to_next)))
+            recvs.append((r + 1, rn))
+        p2p(sends, recvs)
+        bp = torch.empty(int(rp.item()), dtype=dt, device=self.cdev) if has_prev else None
+        bn = torch.empty(int(rn.item()), dtype=dt, device=self.cdev) if has_next else None
+        sends, recvs = [], []
+        if has_prev and to_prev is not None and to_prev.numel():
+            sends.append((r - 1, self._c(to_prev)))
+        if has_next and to_next is not None and to_next.numel():
+            sends.append((r + 1, self._c(to_next)))
+        if bp is not None and bp.numel():
+            recvs.append((r - 1, bp))
+        if bn is not None and bn.numel():
+            recvs.append((r + 1, bn))
+        p2p(sends, recvs)
+        dev = ref.device
+        return (bp.to(dev) if bp is not None else None), (bn.to(dev) if bn is not None else None)
+
+
+class _UF:
+    def __init__(self):
+        self.p: Dict[int, int] = {}
+
+    def find(self, a: int) -> int:
+        p = self.p
+        p.setdefault(a, a)
+        root = a
+        while p[root] != root:
+            root = p[root]
+        while p[a] != root:
+            p[a], a = root, p[a]
+        return root
+
+    def union(self, a: int, b: int):
+        ra, rb = self.find(a), self.find(b)
+        if ra != rb:
+            if ra < rb:
+                self.p[rb] = ra
+            else:
+                self.p[ra] = rb
+
+
+def merge_equivalences(pairs: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """pairs [k][2] of global component ids known to be one component -> (keys, reps) sorted,
+    rep = minimum id of each class (= the global minimum core index)."""
+    uf = _UF()
+    for a, b in pairs.tolist():
+        uf.union(int(a), int(b))
+    keys = np.array(sorted(uf.p.keys()), dtype=np.int64)
+    reps = np.array([uf.find(int(k)) for k in keys], dtype=np.int64)
+    return keys, reps
+
+
+@dataclass
+class ShardResult:
+    n_points_local: int
+    n_points_global: int
+    n_clustered_local: int
+    n_clusters: int
+    labels_local: Optional[torch.Tensor]        # labels of this rank's kept points
+    n_segments: int = 0
+    tracker: object = None                      # rank 0 only
+    frame_order_offsets: Optional[np.ndarray] = None
+    frame_order: Optional[np.ndarray] = None
+    seg: Optional[Dict[str, np.ndarray]] = None  # rank 0: all segments, global frame slots
+    built_global: Optional[np.ndarray] = None
+    stage_ms: Dict[str, float] = field(default_factory=dict)
+
+
+class ShardedStackPipeline:
+    """The path over a global stack whose frames are split across ranks (see module doc)."""
+
+    def __init__(self, ops, comm: Comm, gains: Sequence[int], rows: int, bins: int,
+                 params: PathParams = None, timing: bool = False):
+        self.ops = ops
+        self.comm = comm
+        self.gains = [int(g) for g in gains]
+        self.rows, self.bins = rows, bins
+        self.p = params or PathParams()
+        self.timing = timing
+
+    def set_geometry(self, geo, gain_d):
+        self.geo, self.gain_d = geo, gain_d
+
+    def run(self, echo, dt: int, frame0: int) -> ShardResult:
+        p, ops, comm = self.p, self.ops, self.comm
+        G = len(self.gains)
+        F = int(echo.shape[0])
+        W, r = comm.world, comm.rank
+        marks = [("start", time.perf_counter())]
+
+        def mark(name):
+            if self.timing:
+                marks.append((name, time.perf_counter()))
+        # 1. K1
+        pts = ops.polar(echo, dt, self.rows, self.bins, self.geo, self.gain_d, p.threshold,
+                        p.stride, G)
+        n_local = pts.n
+        built_local = np.nonzero(np.diff(pts.frame_off) > 0)[0]
+        cnts = comm.all_gather_var(torch.tensor([n_local, len(built_local)], dtype=torch.int64))
+        n_global = int(sum(int(c[0]) for c in cnts))
+        n_built = int(sum(int(c[1]) for c in cnts))
+        mark("polar")
+        # 2. land filter (global grid)
+        if p.land_filter and n_built > 10 and n_global > 0:
+            if pts.n:
+                b = ops.bounds(pts)
+            else:
+                b = np.array([np.inf, -np.inf, np.inf, -np.inf], np.float32)
+            lo = comm.all_reduce(torch.tensor([b[0], b[2]], dtype=torch.float32), _MIN).numpy()
+            hi = comm.all_reduce(torch.tensor([b[1], b[3]], dtype=torch.float32), _MAX).numpy()
+            xe = np.arange(np.float32(lo[0]), np.float32(hi[0]) + LAND_GRID_RESOLUTION,
+                           LAND_GRID_RESOLUTION)
+            ye = np.arange(np.float32(lo[1]), np.float32(hi[1]) + LAND_GRID_RESOLUTION,
+                           LAND_GRID_RESOLUTION)
+            cnt, tot = ops.land_grid(pts, xe, ye)
+            cnt = comm.all_reduce(cnt, _SUM)
+            tot = comm.all_reduce(tot, _SUM)
+            pts, _ = ops.land_apply(pts, cnt, tot, n_built, xe, ye)
+        mark("land")
+        # 3. global numbering
+        kept = comm.all_gather_var(torch.tensor([pts.n], dtype=torch.int64))
+        kept = [int(k[0]) for k in kept]
+        P = int(sum(kept[:r]))
+        n_in_global = int(sum(kept))
+        if n_in_global == 0:
+            raise ValueError("Found array with 0 sample(s) (shape=(0, 2)) while a minimum of 1 "
+                             "is required.")
+        t_own = ops.frame_times(pts, frame0)
+        # 4. halo exchange: points of the first / last h frames
+        h = int(np.floor(p.eps_time)) if np.isfinite(p.eps_time) and p.eps_time >= 0 else 0
+        if W > 1 and h > F:
+            raise ValueError(f"each rank needs at least floor(eps_time)={h} frames")
+        h = min(h, F)
+        fo = pts.frame_off
+        a_first, a_last = int(fo[min(h, F)]), int(fo[F - h]) if h else pts.n
+        n_own = pts.n
+        own_xyt = torch.stack([pts.x, pts.y, t_own]) if n_own else \
+            torch.zeros((3, 0), dtype=torch.float32, device=pts.x.device)
+        send_prev = own_xyt[:, :a_first].reshape(-1) if h else None
+        send_next = own_xyt[:, a_last:].reshape(-1) if h else None
+        if W > 1 and h > 0:
+            hp, hn = comm.exchange(send_prev, send_next)
+        else:
+            hp = hn = None
+        hp = hp.reshape(3, -1) if hp is not None else own_xyt[:, :0]
+        hn = hn.reshape(3, -1) if hn is not None else own_xyt[:, :0]
+        n_prev, n_next = hp.shape[1], hn.shape[1]
+        allxyt = torch.cat([hp, own_xyt, hn], dim=1).contiguous()
+        base = P - n_prev
+        mark("halo")
+        # 5. core flags, halo flags from their owners
+        X, Y, T = allxyt[0].contiguous(), allxyt[1].contiguous(), allxyt[2].contiguous()
+        core = ops.dbscan_core(X, Y, T, p.eps_space, p.eps_time, p.min_samples)
+        if W > 1 and h > 0:
+            c_own = core[n_prev:n_prev + n_own]
+            cp, cn = comm.exchange(c_own[:a_first].contiguous(), c_own[a_last:].contiguous())
+            if cp is not None and n_prev:
+                core[:n_prev] = cp
+            if cn is not None and n_next:
+                core[n_prev + n_own:] = cn
+        # 6. components + equivalences across ranks
+        comp = ops.dbscan_components(core)
+        compg = torch.where(comp >= 0, comp.to(torch.int64) + base,
+                            torch.full_like(comp, -1, dtype=torch.int64))
+        pairs = np.zeros((0, 2), np.int64)
+        if W > 1 and h > 0:
+            g_own = compg[n_prev:n_prev + n_own]
+            op_, on_ = comm.exchange(g_own[:a_first].contiguous(), g_own[a_last:].contiguous())
+            ps = []
+            if op_ is not None and n_prev:
+                ps.append(torch.stack([compg[:n_prev], op_], 1))
+            if on_ is not None and n_next:
+                ps.append(torch.stack([compg[n_prev + n_own:], on_], 1))
+            if ps:
+                pr = torch.cat(ps).cpu().numpy()
+                pr = pr[(pr[:, 0] >= 0) & (pr[:, 1] >= 0) & (pr[:, 0] != pr[:, 1])]
+                pairs = np.unique(pr, axis=0) if len(pr) else pairs
+            allp = comm.all_gather_var(torch.from_numpy(pairs.reshape(-1).copy()))
+            pairs = np.concatenate([a.numpy() for a in allp]).reshape(-1, 2) if allp else pairs
+        keys, vals = merge_equivalences(pairs)
+        rep = ops.remap(comp, base, keys, vals)
+        # 7. global representatives and labels
+        roots = ops.select_roots(rep, base, n_prev, n_prev + n_own)
+        all_roots = comm.all_gather_var(roots) if W > 1 else [roots]
+        reps_sorted = torch.cat([a.to(rep.device) for a in all_roots])
+        labels_all = ops.dbscan_labels_global(rep, reps_sorted)
+        labels = labels_all[n_prev:n_prev + n_own]
+        n_clusters = int(reps_sorted.numel())
+        mark("stdbscan")
+        # 8. summaries, gathered to rank 0
+        seg, first_noise = ops.summaries(pts, labels, n_clusters)
+        seg_frame_global = seg["frame"].astype(np.int64) + frame0
+        packed = np.stack([seg_frame_global, seg["label"].astype(np.int64),
+                           seg["count"].astype(np.int64), seg["first"].astype(np.int64)],
+                          1).reshape(-1)
+        fl = np.stack([seg["cx"], seg["cy"], seg["mi"]], 1).astype(np.float32).reshape(-1)
+        noise = first_noise.astype(np.int64)
+        built_g = (built_local + frame0).astype(np.int64)
+        if W > 1:
+            g_int = comm.all_gather_var(torch.from_numpy(packed.copy()))
+            g_flt = comm.all_gather_var(torch.from_numpy(fl.copy()))
+            g_noise = comm.all_gather_var(torch.from_numpy(noise.copy()))
+            g_built = comm.all_gather_var(torch.from_numpy(built_g.copy()))
+        else:
+            g_int = [torch.from_numpy(packed.copy())]
+            g_flt, g_noise, g_built = ([torch.from_numpy(fl)], [torch.from_numpy(noise)],
+                                       [torch.from_numpy(built_g)])
+        mark("summaries")
+        res = ShardResult(n_points_local=n_local, n_points_global=n_global,
+                          n_clustered_local=n_own, n_clusters=n_clusters, labels_local=labels)
+        if r == 0:
+            ints = np.concatenate([a.cpu().numpy() for a in g_int]).reshape(-1, 4)
+            flts = np.concatenate([a.cpu().numpy() for a in g_flt]).reshape(-1, 3)
+            all_seg = {"frame": ints[:, 0].astype(np.int32), "label": ints[:, 1].astype(np.int32),
+                       "count": ints[:, 2], "first": ints[:, 3],
+                       "cx": flts[:, 0].copy(), "cy": flts[:, 1].copy(), "mi": flts[:, 2].copy()}
+            all_noise = np.concatenate([a.cpu().numpy() for a in g_noise]).astype(np.int64)
+            built = np.concatenate([a.cpu().numpy() for a in g_built]).astype(np.int64)
+            n_frames = F * W
+            fo_, order, trk = order_and_track(n_frames, built, all_seg, all_noise, p)
+            res.tracker, res.frame_order_offsets, res.frame_order = trk, fo_, order
+            res.seg, res.built_global = all_seg, built
+            res.n_segments = len(all_seg["frame"])
+        mark("tracker")
+        if self.timing:
+            for (a, ta), (b, tb) in zip(marks[:-1], marks[1:]):
+                res.stage_ms[b] = (tb - ta) * 1e3
+        return res

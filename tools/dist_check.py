@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Multi-rank check of the frame-sharded path on GPU(s): every rank runs rpt.dist's
+ShardedStackPipeline on its frame range; rank 0 also runs the single-GPU FrameStackPipeline over
+the whole stack and asserts identical labels, per-frame cluster rows and tracked objects.
+
+    python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29511 tools/dist_check.py --backend gloo --frames 14
+(--backend gloo lets several ranks share one GPU; nccl = RCCL needs one GPU per rank.)
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+for _p in (str(ROOT / "radar-point-cloud-tracking_amd"), str(ROOT)):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--backend", default="gloo")
+    ap.add_argument("--frames", type=int, default=14, help="frames per rank")
+    ap.add_argument("--rows", type=int, default=4096)
+    args = ap.parse_args()
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))
+    torch.cuda.set_device(dev)
+    if args.backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group("gloo")
+
+    from rpt import _abi
+    from rpt.dist import Comm, ShardedStackPipeline
+    from rpt.pipeline import FrameStackPipeline, PathParams
+    from rpt.stages import HipOps
+    from rpt.synth import DeviceSynth, SynthConfig
+
+    F = args.frames
+    cfg = SynthConfig(n_frames=F, rows=args.rows, frame0=rank * F)
+    ds = DeviceSynth(cfg, dev)
+    echo = ds.echo()
+    ops = HipOps(dev)
+    pipe = ShardedStackPipeline(ops, Comm(dev), cfg.gains, cfg.rows, cfg.bins, PathParams())
+    geo = tuple(torch.from_numpy(np.tile(a, F * 3)).to(dev) for a in
+                (np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t))
+    pipe.set_geometry(geo, torch.tensor(list(cfg.gains) * F, dtype=torch.int32, device=dev))
+    res = pipe.run(echo, _abi.ECHO_U8, rank * F)
+    labels = Comm(dev).all_gather_var(res.labels_local.to(torch.int64))
+    ok = True
+    if rank == 0:
+        full = SynthConfig(n_frames=F * world, rows=args.rows)
+        dsf = DeviceSynth(full, dev)
+        single = FrameStackPipeline(full.gains, full.rows, full.bins, PathParams(), dev)
+        single.set_geometry(np.full(full.rows, full.scale, np.float32), dsf.geo.cos_t,
+                            dsf.geo.sin_t, full.n_frames * 3)
+        ref = single.run(dsf.echo(), keep_points=True)
+        got = torch.cat([l.cpu() for l in labels]).numpy()
+        exp = ref.labels.cpu().numpy().astype(np.int64)
+        ok &= bool(np.array_equal(got, exp))
+        rows = lambda r: [(f, int(r.seg["label"][s]), int(r.seg["count"][s]), float(r.seg["cx"][s]),  # noqa: E731
+                           float(r.seg["cy"][s]), float(r.seg["mi"][s]))
+                          for f in range(len(r.frame_order_offsets) - 1)
+                          for s in r.frame_order[r.frame_order_offsets[f]:r.frame_order_offsets[f + 1]]]
+        ok &= rows(res) == rows(ref)
+        a, b = res.tracker.objects(), ref.tracker.objects()
+        ok &= [o.object_id for o in a] == [o.object_id for o in b]
+        ok &= all(np.array_equal(np.vstack(x.positions), np.vstack(y.positions)) for x, y in zip(a, b))
+        print(f"[dist_check] world={world} backend={args.backend} points={res.n_points_global} "
+              f"clusters={res.n_clusters} segments={res.n_segments} objects={len(a)} "
+              f"labels_equal={np.array_equal(got, exp)} ok={ok}", flush=True)
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    flag = Comm(dev).all_reduce(flag, dist.ReduceOp.MIN)
+    dist.destroy_process_group()
+    sys.exit(0 if int(flag.item()) == 1 else 1)
+
+
+if __name__ == "__main__":
+    main()
