@@ -58,19 +58,45 @@ __global__ __launch_bounds__(kBlock) void k_bounds_xy(const float* __restrict__ 
       mny = min(mny, sm[w][2]);
       mxy = max(mxy, sm[w][3]);
     }
-    atomicMin(out + 0, mnx);
-    atomicMax(out + 1, mxx);
-    atomicMin(out + 2, mny);
-    atomicMax(out + 3, mxy);
+    // per-block partial; k_bounds_xy_final reduces them (no same-address atomics)
+    out[4 * blockIdx.x + 0] = mnx;
+    out[4 * blockIdx.x + 1] = mxx;
+    out[4 * blockIdx.x + 2] = mny;
+    out[4 * blockIdx.x + 3] = mxy;
   }
 }
 
-__global__ void k_bounds_xy_init(uint32_t* o) {
-  o[0] = 0xffffffffu;
-  o[1] = 0u;
-  o[2] = 0xffffffffu;
-  o[3] = 0u;
+__global__ __launch_bounds__(kBlock) void k_bounds_xy_final(const uint32_t* __restrict__ part,
+                                                           int nb, uint32_t* __restrict__ out) {
+  uint32_t v[4] = {0xffffffffu, 0u, 0xffffffffu, 0u};
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    v[0] = min(v[0], part[4 * b + 0]);
+    v[1] = max(v[1], part[4 * b + 1]);
+    v[2] = min(v[2], part[4 * b + 2]);
+    v[3] = max(v[3], part[4 * b + 3]);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    v[0] = min(v[0], (uint32_t)__shfl_xor((int)v[0], off));
+    v[1] = max(v[1], (uint32_t)__shfl_xor((int)v[1], off));
+    v[2] = min(v[2], (uint32_t)__shfl_xor((int)v[2], off));
+    v[3] = max(v[3], (uint32_t)__shfl_xor((int)v[3], off));
+  }
+  __shared__ uint32_t sm[kBlock / 64][4];
+  if ((threadIdx.x & 63) == 0)
+    for (int k = 0; k < 4; ++k) sm[threadIdx.x / 64][k] = v[k];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kBlock / 64; ++w) {
+      v[0] = min(v[0], sm[w][0]);
+      v[1] = max(v[1], sm[w][1]);
+      v[2] = min(v[2], sm[w][2]);
+      v[3] = max(v[3], sm[w][3]);
+    }
+    for (int k = 0; k < 4; ++k) out[k] = v[k];
+  }
 }
+
 
 // number of edges <= v  (np.searchsorted(edges, v, side='right'))
 __device__ __forceinline__ int count_le(const double* e, int ne, double v) {
@@ -238,12 +264,16 @@ int32_t bounds_xy(const float* x, const float* y, int64_t n, float* out4, hipStr
     set_error("zero-size array to reduction operation minimum which has no identity");
     return RPT_EEMPTY;
   }
+  const int nb = grid_for(n, kBlock, 1024);
   Scratch& sc = scratch();
-  RPT_TRY(sc.reserve(256, st));
+  Budget bud;
+  bud.add<uint32_t>(4);
+  bud.add<uint32_t>(4 * (int64_t)nb);
+  RPT_TRY(sc.reserve(bud.bytes, st));
   uint32_t* d = sc.carve_n<uint32_t>(4);
-  hipLaunchKernelGGL(k_bounds_xy_init, dim3(1), dim3(1), 0, st, d);
-  hipLaunchKernelGGL(k_bounds_xy, dim3(grid_for(n, kBlock, 1024)), dim3(kBlock), 0, st, x, y, n,
-                     d);
+  uint32_t* part = sc.carve_n<uint32_t>(4 * (int64_t)nb);
+  hipLaunchKernelGGL(k_bounds_xy, dim3(nb), dim3(kBlock), 0, st, x, y, n, part);
+  hipLaunchKernelGGL(k_bounds_xy_final, dim3(1), dim3(kBlock), 0, st, part, nb, d);
   RPT_CHECK_LAUNCH();
   uint32_t h[4];
   RPT_HIP(hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, st));

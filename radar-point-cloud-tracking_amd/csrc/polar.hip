@@ -123,25 +123,24 @@ __global__ __launch_bounds__(kBlock) void k_row_write(
   const int64_t wave0 = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / 64;
   const int64_t n_waves = (int64_t)gridDim.x * kWavesPerBlock;
   const float fb = (float)bins;
+  const uint32_t ustride = (uint32_t)stride;
   for (int64_t row = wave0; row < n_rows; row += n_waves) {
-    const int64_t f = row / rows;
+    const int64_t f = (int64_t)((uint32_t)row / (uint32_t)rows);  // n_rows < 2^32 (host check)
     const T* rp = echo + row * bins;
-    int64_t rank = row_prefix[row] - row_prefix[f * rows];  // rank of this row's first kept
+    // in-file rank of this row's first kept element (< rows*bins, fits 32 bits)
+    uint32_t rank = (uint32_t)(row_prefix[row] - row_prefix[f * rows]);
     const int64_t out0 = file_offsets[f];
     const float step = geo.scale ? geo.scale[row] / fb : 0.f;
     const float ct = geo.cos_t[row], st = geo.sin_t[row];
     const int32_t g = gain ? gain[f] : 0;
-    const int32_t fr = (int32_t)(f / files_per_frame);
-    auto emit = [&](int b, float v, int64_t r) {
-      if (r % stride == 0) {
-        const float rr = geo.ranges ? geo.ranges[row * bins + b] : step * (float)b;
-        const int64_t o = out0 + r / stride;
-        x[o] = rr * ct;
-        y[o] = rr * st;
-        val[o] = v;
-        if (gain_out) gain_out[o] = g;
-        if (pf_out) pf_out[o] = fr;
-      }
+    const int32_t fr = (int32_t)((uint32_t)f / (uint32_t)files_per_frame);
+    auto put = [&](int b, float v, int64_t o) {
+      const float rr = geo.ranges ? geo.ranges[row * bins + b] : step * (float)b;
+      x[o] = rr * ct;
+      y[o] = rr * st;
+      val[o] = v;
+      if (gain_out) gain_out[o] = g;
+      if (pf_out) pf_out[o] = fr;
     };
     if (VEC) {
       constexpr int N = Vec<T>::N;
@@ -155,13 +154,26 @@ __global__ __launch_bounds__(kBlock) void k_row_write(
 #pragma unroll
         for (int k = 0; k < N; ++k) c += (fv[k] > thr) ? 1 : 0;
         int tot;
-        int64_t r = rank + wave_excl_scan(c, &tot);
+        const uint32_t r = rank + (uint32_t)wave_excl_scan(c, &tot);
         if (c) {
+          // kept elements with in-file rank % stride == 0 are emitted: one 32-bit division per
+          // lane, then a countdown to the next emitted rank
+          const uint32_t q = r / ustride, rem = r - q * ustride;
+          uint32_t skip = rem ? ustride - rem : 0u;
+          int64_t o = out0 + q + (rem ? 1 : 0);
 #pragma unroll
-          for (int k = 0; k < N; ++k)
-            if (fv[k] > thr) emit(b0 + k, fv[k], r++);
+          for (int k = 0; k < N; ++k) {
+            if (fv[k] > thr) {
+              if (skip == 0u) {
+                put(b0 + k, fv[k], o++);
+                skip = ustride - 1u;
+              } else {
+                --skip;
+              }
+            }
+          }
         }
-        rank += tot;
+        rank += (uint32_t)tot;
       }
     } else {
       for (int base = 0; base < bins; base += 64) {
@@ -169,8 +181,12 @@ __global__ __launch_bounds__(kBlock) void k_row_write(
         const float v = (b < bins) ? to_f(rp[b]) : 0.f;
         const bool keep = (b < bins) && (v > thr);
         const uint64_t m = __ballot(keep);
-        if (keep) emit(b, v, rank + rank_in_mask(m));
-        rank += __popcll(m);
+        if (keep) {
+          const uint32_t r = rank + (uint32_t)rank_in_mask(m);
+          const uint32_t q = r / ustride;
+          if (r - q * ustride == 0u) put(b, v, out0 + q);
+        }
+        rank += (uint32_t)__popcll(m);
       }
     }
   }
@@ -220,6 +236,11 @@ int32_t write_impl(const T* echo, int64_t n_files, int rows, int bins, float thr
                    const int64_t* file_offsets, int fpf, float* x, float* y, float* v,
                    int32_t* gout, int32_t* pf, hipStream_t st) {
   const int64_t n_rows = n_files * rows;
+  if ((int64_t)rows * bins >= (int64_t(1) << 32) || n_rows >= (int64_t(1) << 32) || stride < 1 ||
+      fpf < 1) {
+    set_error("rpt_polar_write: rows*bins and n_files*rows must be < 2^32, stride/fpf >= 1");
+    return RPT_ENOTSUP;
+  }
   const bool vec = (bins % (64 * Vec<T>::N) == 0) && ((uintptr_t)echo % 16 == 0);
   const int grid = grid_for(n_rows, kWavesPerBlock, 16384);
   if (vec)

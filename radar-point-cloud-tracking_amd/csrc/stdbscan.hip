@@ -101,7 +101,7 @@ __global__ __launch_bounds__(kBlock) void k_bounds(const float* __restrict__ x,
       if (v[3] != floorf(v[3]) || fabsf(v[3]) >= 16777216.f) nonint = 1;
     }
   }
-  // wave reduce then one atomic per wave
+  // wave reduce, then one partial per block
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
 #pragma unroll
@@ -136,26 +136,76 @@ __global__ __launch_bounds__(kBlock) void k_bounds(const float* __restrict__ x,
       nonint |= sfl[v][1];
       nfin += sfl[v][2];
     }
-#pragma unroll
+    // per-block partial, reduced by k_bounds_final (no same-address atomics)
+    Bounds& o = out[blockIdx.x];
     for (int k = 0; k < 4; ++k) {
-      atomicMin(&out->mn[k], mn[k]);
-      atomicMax(&out->mx[k], mx[k]);
+      o.mn[k] = mn[k];
+      o.mx[k] = mx[k];
     }
-    if (nonfin) atomicOr(&out->nonfinite_xyz, 1);
-    if (nonint) atomicOr(&out->nonintegral_t, 1);
-    atomicAdd(&out->n_finite_t, nfin);
+    o.nonfinite_xyz = nonfin;
+    o.nonintegral_t = nonint;
+    o.n_finite_t = nfin;
+    o.pad = 0;
   }
 }
 
-__global__ void k_bounds_init(Bounds* b) {
-  for (int k = 0; k < 4; ++k) {
-    b->mn[k] = 0xffffffffu;
-    b->mx[k] = 0u;
+__global__ __launch_bounds__(kBlock) void k_bounds_final(const Bounds* __restrict__ part, int nb,
+                                                        Bounds* __restrict__ out) {
+  uint32_t mn[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+  uint32_t mx[4] = {0u, 0u, 0u, 0u};
+  int nonfin = 0, nonint = 0, nfin = 0;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    const Bounds& p = part[b];
+    for (int k = 0; k < 4; ++k) {
+      mn[k] = min(mn[k], p.mn[k]);
+      mx[k] = max(mx[k], p.mx[k]);
+    }
+    nonfin |= p.nonfinite_xyz;
+    nonint |= p.nonintegral_t;
+    nfin += p.n_finite_t;
   }
-  b->nonfinite_xyz = 0;
-  b->nonintegral_t = 0;
-  b->n_finite_t = 0;
-  b->pad = 0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      mn[k] = min(mn[k], (uint32_t)__shfl_xor((int)mn[k], off));
+      mx[k] = max(mx[k], (uint32_t)__shfl_xor((int)mx[k], off));
+    }
+    nonfin |= __shfl_xor(nonfin, off);
+    nonint |= __shfl_xor(nonint, off);
+    nfin += __shfl_xor(nfin, off);
+  }
+  __shared__ Bounds sb[kBlock / 64];
+  const int w = threadIdx.x / 64;
+  if ((threadIdx.x & 63) == 0) {
+    for (int k = 0; k < 4; ++k) {
+      sb[w].mn[k] = mn[k];
+      sb[w].mx[k] = mx[k];
+    }
+    sb[w].nonfinite_xyz = nonfin;
+    sb[w].nonintegral_t = nonint;
+    sb[w].n_finite_t = nfin;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int v = 1; v < kBlock / 64; ++v) {
+      for (int k = 0; k < 4; ++k) {
+        mn[k] = min(mn[k], sb[v].mn[k]);
+        mx[k] = max(mx[k], sb[v].mx[k]);
+      }
+      nonfin |= sb[v].nonfinite_xyz;
+      nonint |= sb[v].nonintegral_t;
+      nfin += sb[v].n_finite_t;
+    }
+    for (int k = 0; k < 4; ++k) {
+      out->mn[k] = mn[k];
+      out->mx[k] = mx[k];
+    }
+    out->nonfinite_xyz = nonfin;
+    out->nonintegral_t = nonint;
+    out->n_finite_t = nfin;
+    out->pad = 0;
+  }
 }
 
 // ---------------------------------------------------------------- grid geometry
@@ -185,8 +235,7 @@ __global__ __launch_bounds__(kBlock) void k_keys(const float* __restrict__ x,
                                                 const float* __restrict__ z, int64_t stride,
                                                 const float* __restrict__ t, int64_t n, Geom g,
                                                 uint32_t* __restrict__ keys,
-                                                uint32_t* __restrict__ vals,
-                                                int32_t* __restrict__ cell_count) {
+                                                uint32_t* __restrict__ vals) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const float ti = t[i];
@@ -202,7 +251,6 @@ __global__ __launch_bounds__(kBlock) void k_keys(const float* __restrict__ x,
     }
     keys[i] = key;
     vals[i] = (uint32_t)i;
-    atomicAdd(&cell_count[key], 1);
   }
 }
 
@@ -230,40 +278,115 @@ __global__ __launch_bounds__(kBlock) void k_gather(const float* __restrict__ x,
   }
 }
 
-// Per-cell bounding boxes.  boxA = {xmin, xmax, ymin, ymax}, boxB = {zmin, zmax, tmin, tmax}.
-// mutual[c] = 1 when every pair of points in the cell passes the neighbour test (computed
-// conservatively from the box with the same rounding as the pair test).
+// Cell occupancy from the sorted keys (no atomics on hot cells): a run's head subtracts its start
+// and its tail adds its end, so cell_count[c] = run length (two uncontended atomics per occupied
+// cell); head flags (scanned later) give the occupied-cell list in ascending key order.
+__global__ __launch_bounds__(kBlock) void k_cell_runs(const int32_t* __restrict__ skey, int64_t n,
+                                                     int32_t* __restrict__ cell_count,
+                                                     int32_t* __restrict__ head) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t k = skey[s];
+    const bool h = (s == 0) || skey[s - 1] != k;
+    const bool t = (s == n - 1) || skey[s + 1] != k;
+    if (h && t) {
+      cell_count[k] = 1;
+    } else {
+      if (h) atomicAdd(cell_count + k, -(int32_t)s);
+      if (t) atomicAdd(cell_count + k, (int32_t)(s + 1));
+    }
+    head[s] = h ? 1 : 0;
+  }
+}
+
+// pos = exclusive scan of the head flags: cell of every run head -> occ[pos]
+__global__ __launch_bounds__(kBlock) void k_occ_list(const int32_t* __restrict__ skey, int64_t n,
+                                                    const int32_t* __restrict__ pos,
+                                                    int32_t* __restrict__ occ) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x)
+    if (pos[s + 1] != pos[s]) occ[pos[s]] = skey[s];
+}
+
+// grids of the persistent wave-per-item kernels (item counts live on the device)
+inline int wave_grid(int64_t max_items) { return grid_for(max_items, kBlock / 64, 4096); }
+inline int tile_grid(int64_t n) { return grid_for(n, kBlock * 16, 2048); }
+
+__device__ __forceinline__ float wave_minf(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off));
+  return v;
+}
+__device__ __forceinline__ float wave_maxf(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+  return v;
+}
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+__device__ __forceinline__ int64_t wave_min64(int64_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const int64_t o = __shfl_xor(v, off);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+// Per-cell bounding boxes, one wave per occupied cell.  boxA = {xmin, xmax, ymin, ymax},
+// boxB = {zmin, zmax, tmin, tmax}.  mutual[c] = 1 when every pair of points in the cell passes
+// the neighbour test (computed conservatively from the box with the same rounding as the pair
+// test).
 template <int D>
 __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ pts,
                                                     const int32_t* __restrict__ cell_start,
-                                                    int64_t cells, Geom g,
+                                                    const int32_t* __restrict__ occ,
+                                                    const int32_t* __restrict__ n_occ, Geom g,
                                                     float4* __restrict__ boxA,
                                                     float4* __restrict__ boxB,
                                                     uint8_t* __restrict__ mutual) {
-  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < cells;
-       c += (int64_t)gridDim.x * blockDim.x) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+  const int64_t no = *n_occ;
+  for (int64_t q = w0; q < no; q += nw) {
+    const int c = occ[q];
     const int b = cell_start[c], e = cell_start[c + 1];
-    if (b == e) continue;
-    float4 p = pts[b];
-    float x0 = p.x, x1 = p.x, y0 = p.y, y1 = p.y, z0 = p.z, z1 = p.z, t0 = p.w, t1 = p.w;
-    for (int j = b + 1; j < e; ++j) {
-      p = pts[j];
+    float x0 = FLT_MAX, x1 = -FLT_MAX, y0 = FLT_MAX, y1 = -FLT_MAX;
+    float z0 = FLT_MAX, z1 = -FLT_MAX, t0 = FLT_MAX, t1 = -FLT_MAX;
+    for (int j = b + lane; j < e; j += 64) {
+      const float4 p = pts[j];
       x0 = fminf(x0, p.x); x1 = fmaxf(x1, p.x);
       y0 = fminf(y0, p.y); y1 = fmaxf(y1, p.y);
       z0 = fminf(z0, p.z); z1 = fmaxf(z1, p.z);
       t0 = fminf(t0, p.w); t1 = fmaxf(t1, p.w);
     }
-    boxA[c] = make_float4(x0, x1, y0, y1);
-    boxB[c] = make_float4(z0, z1, t0, t1);
-    const double dx = (double)x1 - (double)x0;
-    const double dy = (double)y1 - (double)y0;
-    double d2 = dx * dx + dy * dy;
+    x0 = wave_minf(x0); x1 = wave_maxf(x1);
+    y0 = wave_minf(y0); y1 = wave_maxf(y1);
+    t0 = wave_minf(t0); t1 = wave_maxf(t1);
     if (D == 3) {
-      const double dz = (double)z1 - (double)z0;
-      d2 = d2 + dz * dz;
+      z0 = wave_minf(z0);
+      z1 = wave_maxf(z1);
+    } else {
+      z0 = t0;  // 2-D: pts[].z carries t (unused by the 2-D tests)
+      z1 = t1;
     }
-    const float dt = t1 - t0;
-    mutual[c] = (d2 <= g.eps2 && dt <= g.epst) ? 1 : 0;
+    if (lane == 0) {
+      boxA[c] = make_float4(x0, x1, y0, y1);
+      boxB[c] = make_float4(z0, z1, t0, t1);
+      const double dx = (double)x1 - (double)x0;
+      const double dy = (double)y1 - (double)y0;
+      double d2 = dx * dx + dy * dy;
+      if (D == 3) {
+        const double dz = (double)z1 - (double)z0;
+        d2 = d2 + dz * dz;
+      }
+      const float dt = t1 - t0;
+      mutual[c] = (d2 <= g.eps2 && dt <= g.epst) ? 1 : 0;
+    }
   }
 }
 
@@ -398,50 +521,203 @@ __device__ __forceinline__ void for_each_cell(const float4& p, int32_t key, cons
   }
 }
 
-// ---------------------------------------------------------------- K5: core flags
+__device__ __forceinline__ int32_t rep_id(const int64_t* __restrict__ reps, int64_t nr, int64_t v) {
+  int64_t lo = 0, hi = nr;
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (reps[m] < v) lo = m + 1; else hi = m;
+  }
+  return (lo < nr && reps[lo] == v) ? (int32_t)lo : -2;  // -2: representative missing (bug)
+}
+
+// ---------------------------------------------------------------- block-aggregated append
+// Every thread of the block evaluates pred(s) for kItems sorted indices of one 256*kItems tile;
+// the indices with pred true are appended to list with ONE global atomic per tile (thousands of
+// same-address atomics per launch otherwise serialise in L2).  Order inside a tile is
+// thread-major; consumers do not depend on the order.
+constexpr int kItems = 16;
+template <class P>
+__device__ __forceinline__ void block_append(int64_t tile0, int64_t n, P&& pred,
+                                             int32_t* __restrict__ list,
+                                             int32_t* __restrict__ counter) {
+  __shared__ int s_wsum[kBlock / 64];
+  __shared__ int s_base;
+  uint32_t bits = 0;
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) {
+    const int64_t s = tile0 + (int64_t)k * kBlock + threadIdx.x;
+    if (s < n && pred(s)) bits |= 1u << k;
+  }
+  const int c = __popc(bits);
+  // block exclusive scan of c
+  const int lane = threadIdx.x & 63, w = threadIdx.x / 64;
+  int incl = c;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += o;
+  }
+  if (lane == 63) s_wsum[w] = incl;
+  __syncthreads();
+  int before = 0, total = 0;
+#pragma unroll
+  for (int v = 0; v < kBlock / 64; ++v) {
+    const int t = s_wsum[v];
+    before += (v < w) ? t : 0;
+    total += t;
+  }
+  if (threadIdx.x == 0) s_base = total ? atomicAdd(counter, total) : 0;
+  __syncthreads();
+  int o = s_base + before + incl - c;
+  while (bits) {
+    const int k = __ffs(bits) - 1;
+    bits &= bits - 1;
+    list[o++] = (int32_t)(tile0 + (int64_t)k * kBlock + threadIdx.x);
+  }
+  __syncthreads();  // s_wsum / s_base reuse by the next tile
+}
+
+// ---------------------------------------------------------------- candidate windows
+// The cells that may hold a neighbour of point p: +-2 cells in space, the slab window of
+// [t - eps_t, t + eps_t] with +-1 slab of slack (culled per slab by its actual time range).
+struct Window {
+  int s0, x0, y0, z0;
+  int nS, nZ, nY, nX;
+  int total;
+};
+
 template <int D>
-__global__ __launch_bounds__(kBlock) void k_core(const float4* __restrict__ pts,
-                                                const int32_t* __restrict__ skey, int64_t n,
-                                                Geom g, const int32_t* __restrict__ cell_start,
-                                                const float4* __restrict__ boxA,
-                                                const float4* __restrict__ boxB,
-                                                const float2* __restrict__ slab_t,
-                                                const uint8_t* __restrict__ mutual,
-                                                uint8_t* __restrict__ core) {
-  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n) return;
-  const int32_t key = skey[s];
-  if ((int64_t)key >= g.cells) {  // non-finite time: no neighbours at all
-    core[s] = (0 >= g.min_samples) ? 1 : 0;
-    return;
-  }
-  const float4 p = pts[s];
+__device__ __forceinline__ Window make_window(int cx, int cy, int cz, double tlo, double thi,
+                                              const Geom& g) {
+  Window w;
+  const double et = (double)g.epst;
+  w.s0 = (int)fmax(floor((tlo - et - g.ot) / g.ct) - 1.0, 0.0);
+  const int s1 = (int)fmin(floor((thi + et - g.ot) / g.ct) + 1.0, (double)(g.nt - 1));
+  w.x0 = max(cx - 2, 0);
+  w.y0 = max(cy - 2, 0);
+  w.z0 = (D == 3) ? max(cz - 2, 0) : 0;
+  w.nS = max(s1 - w.s0 + 1, 0);
+  w.nX = min(cx + 2, g.nx - 1) - w.x0 + 1;
+  w.nY = min(cy + 2, g.ny - 1) - w.y0 + 1;
+  w.nZ = (D == 3) ? (min(cz + 2, g.nz - 1) - w.z0 + 1) : 1;
+  w.total = w.nS * w.nZ * w.nY * w.nX;
+  return w;
+}
+
+template <int D>
+__device__ __forceinline__ void decode_key(int64_t key, const Geom& g, int& cx, int& cy, int& cz) {
+  cx = (int)(key % g.nx);
+  int64_t r = key / g.nx;
+  cy = (int)(r % g.ny);
+  r /= g.ny;
+  cz = (D == 3) ? (int)(r % g.nz) : 0;
+}
+
+// q-th cell of the window; -1 when its slab holds nothing within reach of [tlo, thi]
+__device__ __forceinline__ int64_t window_cell(const Window& w, int q, const Geom& g,
+                                               const float2* __restrict__ slab_t, float tlo,
+                                               float thi) {
+  const int xx = q % w.nX;
+  q /= w.nX;
+  const int yy = q % w.nY;
+  q /= w.nY;
+  const int zz = q % w.nZ;
+  const int ss = w.s0 + q / w.nZ;
+  const float2 sr = slab_t[ss];
+  if (sr.x > sr.y) return -1;  // empty slab
+  const float gap = (tlo > sr.y) ? (tlo - sr.y) : ((thi < sr.x) ? (sr.x - thi) : 0.f);
+  if (!(gap <= g.epst)) return -1;
+  return (((int64_t)ss * g.nz + (w.z0 + zz)) * g.ny + (w.y0 + yy)) * g.nx + (w.x0 + xx);
+}
+
+__device__ __forceinline__ float4 shfl_f4(const float4& v, int l) {
+  return make_float4(__shfl(v.x, l), __shfl(v.y, l), __shfl(v.z, l), __shfl(v.w, l));
+}
+
+// ---------------------------------------------------------------- K5: core flags
+// Level 1, one thread per point: a point whose own cell is mutual and holds >= min_samples points
+// is core (all of them are its neighbours) — the bulk of a radar stack.  Every other point is
+// queued for level 2.
+__global__ __launch_bounds__(kBlock) void k_core_fast(const int32_t* __restrict__ skey,
+                                                     int64_t n, Geom g,
+                                                     const int32_t* __restrict__ cell_start,
+                                                     const uint8_t* __restrict__ mutual,
+                                                     uint8_t* __restrict__ core,
+                                                     int32_t* __restrict__ slow,
+                                                     int32_t* __restrict__ n_slow) {
   const int need = g.min_samples;
-  int cnt = 0;
-  // own cell first: a mutual cell holding >= min_samples points makes all of them core
-  if (need > 0 && mutual[key]) {
-    const int own = cell_start[key + 1] - cell_start[key];
-    if (own >= need) {
-      core[s] = 1;
-      return;
+  for (int64_t tile = (int64_t)blockIdx.x * kBlock * kItems; tile < n;
+       tile += (int64_t)gridDim.x * kBlock * kItems) {
+    block_append(
+        tile, n,
+        [&](int64_t s) -> bool {
+          const int32_t key = skey[s];
+          if ((int64_t)key >= g.cells || need <= 0) {  // non-finite time: no neighbours at all
+            core[s] = (need <= 0) ? 1 : 0;
+            return false;
+          }
+          if (mutual[key] && cell_start[key + 1] - cell_start[key] >= need) {
+            core[s] = 1;
+            return false;
+          }
+          return true;
+        },
+        slow, n_slow);
+  }
+}
+
+// Level 2, one wave per queued point: lanes classify up to 64 candidate cells at a time against
+// the cells' boxes (whole-cell accept adds the cell's count), then every undecided cell's points
+// are tested 64 at a time; the wave stops as soon as min_samples neighbours are seen.
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_core_slow(const float4* __restrict__ pts,
+                                                     const int32_t* __restrict__ skey, Geom g,
+                                                     const int32_t* __restrict__ cell_start,
+                                                     const float4* __restrict__ boxA,
+                                                     const float4* __restrict__ boxB,
+                                                     const float2* __restrict__ slab_t,
+                                                     const int32_t* __restrict__ slow,
+                                                     const int32_t* __restrict__ n_slow,
+                                                     uint8_t* __restrict__ core) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+  const int64_t ns = *n_slow;
+  const int need = g.min_samples;
+  for (int64_t q = w0; q < ns; q += nw) {
+    const int s = slow[q];
+    const int32_t key = skey[s];
+    const float4 p = pts[s];
+    int cx, cy, cz;
+    decode_key<D>(key, g, cx, cy, cz);
+    const Window w = make_window<D>(cx, cy, cz, (double)p.w, (double)p.w, g);
+    int cnt = 0;
+    for (int base = 0; base < w.total && cnt < need; base += 64) {
+      const int qq = base + lane;
+      int b = 0, e = 0, cls = 0;
+      if (qq < w.total) {
+        const int64_t c = window_cell(w, qq, g, slab_t, p.w, p.w);
+        if (c >= 0) {
+          b = cell_start[c];
+          e = cell_start[c + 1];
+          if (e > b) cls = classify<D>(p, boxA[c], boxB[c], g);
+        }
+      }
+      cnt += wave_sum(cls == 1 ? e - b : 0);
+      uint64_t pm = __ballot(cls == 2);
+      while (pm && cnt < need) {
+        const int l = __ffsll((unsigned long long)pm) - 1;
+        pm &= pm - 1;
+        const int bb = __shfl(b, l), ee = __shfl(e, l);
+        for (int j0 = bb; j0 < ee && cnt < need; j0 += 64) {
+          const int j = j0 + lane;
+          const bool a = (j < ee) && adjacent<D>(p, pts[j], g);
+          cnt += __popcll(__ballot(a));
+        }
+      }
     }
+    if (lane == 0) core[s] = (cnt >= need) ? 1 : 0;
   }
-  if (need > 0) {
-    for_each_cell<D>(p, key, g, cell_start, boxA, boxB, slab_t,
-                     [&](int64_t c, int b, int e, int cls) -> bool {
-                       if (cls == 1) {
-                         cnt += e - b;
-                       } else {
-                         for (int j = b; j < e; ++j) {
-                           if (adjacent<D>(p, pts[j], g)) {
-                             if (++cnt >= need) return true;
-                           }
-                         }
-                       }
-                       return cnt >= need;
-                     });
-  }
-  core[s] = (cnt >= need) ? 1 : 0;
 }
 
 // first core point (sorted index) of each cell, -1 when none
@@ -545,15 +821,18 @@ __device__ __forceinline__ int classify_cells(const float4& A1, const float4& B1
   return (dmax <= g.eps2 && tm <= g.epst) ? 1 : 2;
 }
 
-// K6a: mutual-cell x mutual-cell unions, one thread per cell A, each unordered pair once (B > A).
+// K6a: mutual-cell x mutual-cell unions, one wave per occupied cell A, lanes over the candidate
+// cells B > A of its window (each unordered pair once).
 // PARTIAL = false: only pairs the boxes prove fully adjacent (cheap, no search).
 // PARTIAL = true : undecided pairs whose roots still differ after the first pass (a kernel
 //                  boundary later, so most such pairs are already connected), searched for one
-//                  adjacent core pair with both sides culled against the other cell's box.
+//                  adjacent core pair: B's core points that can reach A's box, each tested
+//                  against A's points 64 at a time.
 template <int D, bool PARTIAL>
-__global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict__ pts,
-                                                       int64_t cells, Geom g,
+__global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict__ pts, Geom g,
                                                        const int32_t* __restrict__ cell_start,
+                                                       const int32_t* __restrict__ occ,
+                                                       const int32_t* __restrict__ n_occ,
                                                        const float4* __restrict__ boxA,
                                                        const float4* __restrict__ boxB,
                                                        const float2* __restrict__ slab_t,
@@ -562,58 +841,64 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
                                                        const uint8_t* __restrict__ mutual,
                                                        const int32_t* __restrict__ sorig,
                                                        int32_t* __restrict__ parent) {
-  for (int64_t ca = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; ca < cells;
-       ca += (int64_t)gridDim.x * blockDim.x) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+  const int64_t no = *n_occ;
+  for (int64_t q = w0; q < no; q += nw) {
+    const int ca = occ[q];
+    if ((int64_t)ca >= g.cells) continue;  // the isolated (non-finite time) cell
     const int ra = rep[ca];
     if (ra < 0 || !mutual[ca]) continue;
     const int ea = cell_start[ca + 1];
     const float4 A1 = boxA[ca], A2 = boxB[ca];
-    const int cx = (int)(ca % g.nx);
-    int64_t r = ca / g.nx;
-    const int cy = (int)(r % g.ny);
-    r /= g.ny;
-    const int cz = (D == 3) ? (int)(r % g.nz) : 0;
-    const double et = (double)g.epst;
-    const int s0 = (int)fmax(floor(((double)A2.z - et - g.ot) / g.ct) - 1.0, 0.0);
-    const int s1 = (int)fmin(floor(((double)A2.w + et - g.ot) / g.ct) + 1.0, (double)(g.nt - 1));
-    const int x0 = max(cx - 2, 0), x1 = min(cx + 2, g.nx - 1);
-    const int y0 = max(cy - 2, 0), y1 = min(cy + 2, g.ny - 1);
-    const int z0 = (D == 3) ? max(cz - 2, 0) : 0, z1 = (D == 3) ? min(cz + 2, g.nz - 1) : 0;
-    for (int sl = s0; sl <= s1; ++sl) {
-      const float2 sr = slab_t[sl];
-      if (sr.x > sr.y) continue;
-      for (int zz = z0; zz <= z1; ++zz) {
-        for (int yy = y0; yy <= y1; ++yy) {
-          const int64_t row = (((int64_t)sl * g.nz + zz) * g.ny + yy) * g.nx;
-          for (int xx = x0; xx <= x1; ++xx) {
-            const int64_t cb = row + xx;
-            if (cb <= ca) continue;
-            const int rb = rep[cb];
-            if (rb < 0 || !mutual[cb]) continue;
-            const int cls = classify_cells<D>(A1, boxA[cb], A2, boxB[cb], g);
-            if (!PARTIAL) {
-              if (cls == 1) uf_unite(parent, sorig, ra, rb);
-              continue;
+    int cx, cy, cz;
+    decode_key<D>(ca, g, cx, cy, cz);
+    const Window w = make_window<D>(cx, cy, cz, (double)A2.z, (double)A2.w, g);
+    for (int base = 0; base < w.total; base += 64) {
+      const int qq = base + lane;
+      int rb = -1, cls = 0;
+      int64_t cb = -1;
+      if (qq < w.total) {
+        cb = window_cell(w, qq, g, slab_t, A2.z, A2.w);
+        if (cb > (int64_t)ca) {
+          rb = rep[cb];
+          if (rb >= 0 && mutual[cb]) cls = classify_cells<D>(A1, boxA[cb], A2, boxB[cb], g);
+        }
+      }
+      if (!PARTIAL) {
+        if (cls == 1) uf_unite(parent, sorig, ra, rb);
+        continue;
+      }
+      const bool cand = (cls == 2) && uf_find(parent, ra) != uf_find(parent, rb);
+      uint64_t pm = __ballot(cand);
+      while (pm) {
+        const int l = __ffsll((unsigned long long)pm) - 1;
+        pm &= pm - 1;
+        const int rbl = __shfl(rb, l);
+        const int ebl = cell_start[__shfl((int)cb, l) + 1];
+        bool hit = false;
+        for (int jb0 = rbl; jb0 < ebl && !hit; jb0 += 64) {
+          const int jb = jb0 + lane;
+          float4 pb = make_float4(0.f, 0.f, 0.f, 0.f);
+          bool cb_ok = false;
+          if (jb < ebl && core[jb]) {
+            pb = pts[jb];
+            cb_ok = classify<D>(pb, A1, A2, g) != 0;
+          }
+          uint64_t bm = __ballot(cb_ok);
+          while (bm && !hit) {
+            const int lb = __ffsll((unsigned long long)bm) - 1;
+            bm &= bm - 1;
+            const float4 pq = shfl_f4(pb, lb);
+            for (int ja0 = ra; ja0 < ea && !hit; ja0 += 64) {
+              const int ja = ja0 + lane;
+              const bool adj = (ja < ea) && core[ja] && adjacent<D>(pq, pts[ja], g);
+              hit = __ballot(adj) != 0;
             }
-            if (cls != 2) continue;
-            if (uf_find(parent, ra) == uf_find(parent, rb)) continue;
-            const int eb = cell_start[cb + 1];
-            // B's core points that can reach A's box at all
-            bool hit = false;
-            for (int b = rb; b < eb && !hit; ++b) {
-              if (!core[b]) continue;
-              const float4 pb = pts[b];
-              if (classify<D>(pb, A1, A2, g) == 0) continue;
-              for (int a = ra; a < ea; ++a) {
-                if (core[a] && adjacent<D>(pb, pts[a], g)) {
-                  hit = true;
-                  break;
-                }
-              }
-            }
-            if (hit) uf_unite(parent, sorig, ra, rb);
           }
         }
+        if (hit && lane == 0) uf_unite(parent, sorig, ra, rbl);
       }
     }
   }
@@ -689,35 +974,42 @@ __global__ __launch_bounds__(kBlock) void k_fill_i32(int32_t* p, int64_t n, int3
     p[i] = v;
 }
 
-// ccmin[s] = component-min original index for core points, -1 otherwise; flags the minima.
+// ccmin[s] = component-min original index for core points, -1 otherwise; flags the minima and
+// queues the non-core points for k_label.
 __global__ __launch_bounds__(kBlock) void k_ccmin(int32_t* parent,
                                                  const uint8_t* __restrict__ core, int64_t n,
                                                  const int32_t* __restrict__ sorig,
-                                                 const int32_t* __restrict__ cmin,
                                                  int32_t* __restrict__ ccmin,
                                                  int32_t* __restrict__ is_min,
                                                  int32_t* __restrict__ nc_list,
                                                  int32_t* __restrict__ nc_count) {
-  // grid-stride with whole waves per iteration so the ballot covers 64 consecutive points
-  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n;
-       base += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t s = base + threadIdx.x;
-    const bool valid = s < n;
-    const bool nc = valid && !core[s];
-    const uint64_t bm = __ballot(nc);
-    int off = 0;
-    if ((threadIdx.x & 63) == 0 && bm) off = atomicAdd(nc_count, __popcll(bm));
-    off = __shfl(off, 0, 64);
-    if (nc) {
-      nc_list[off + rank_in_mask(bm)] = (int32_t)s;
-      ccmin[s] = -1;
-    }
-    if (!valid || nc) continue;
-    const int x = uf_find(parent, (int)s);
-    const int m = sorig[x];
-    ccmin[s] = m;
-    if (x == (int)s) is_min[m] = 1;
+  for (int64_t tile = (int64_t)blockIdx.x * kBlock * kItems; tile < n;
+       tile += (int64_t)gridDim.x * kBlock * kItems) {
+    block_append(
+        tile, n,
+        [&](int64_t s) -> bool {
+          if (!core[s]) {
+            ccmin[s] = -1;
+            return true;
+          }
+          const int x = uf_find(parent, (int)s);
+          const int m = sorig[x];
+          ccmin[s] = m;
+          if (x == (int)s) is_min[m] = 1;
+          return false;
+        },
+        nc_list, nc_count);
   }
+}
+
+// queue of the non-core points (phased / global labelling)
+__global__ __launch_bounds__(kBlock) void k_nc_list(const uint8_t* __restrict__ core, int64_t n,
+                                                   int32_t* __restrict__ nc_list,
+                                                   int32_t* __restrict__ nc_count) {
+  for (int64_t tile = (int64_t)blockIdx.x * kBlock * kItems; tile < n;
+       tile += (int64_t)gridDim.x * kBlock * kItems)
+    block_append(
+        tile, n, [&](int64_t s) -> bool { return !core[s]; }, nc_list, nc_count);
 }
 
 // K7/K8 (core points): label = id of the component minimum
@@ -733,58 +1025,96 @@ __global__ __launch_bounds__(kBlock) void k_label_core(const int32_t* __restrict
   }
 }
 
-// K7/K8 (non-core points, compacted list): min adjacent cluster id, else -1.
-template <int D>
+// K7/K8 (non-core points, queued): the smallest component key over adjacent core points, else
+// none.  One wave per point, lanes over candidate cells; the core points of a mutual cell form
+// one component (star init), so such a cell needs one adjacent core point, found 64 at a time.
+// GLOBAL = false: key = ccmin (component-min original index, local run), label = cid[key];
+// GLOBAL = true : key = srep (global representative), label = rank of key in reps.
+template <int D, bool GLOBAL>
 __global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts,
-                                                 const int32_t* __restrict__ skey, int64_t n,
-                                                 Geom g, const int32_t* __restrict__ cell_start,
+                                                 const int32_t* __restrict__ skey, Geom g,
+                                                 const int32_t* __restrict__ cell_start,
                                                  const float4* __restrict__ boxA,
                                                  const float4* __restrict__ boxB,
                                                  const float2* __restrict__ slab_t,
                                                  const int32_t* __restrict__ ccmin,
+                                                 const int64_t* __restrict__ srep,
                                                  const int32_t* __restrict__ rep,
                                                  const uint8_t* __restrict__ mutual,
                                                  const int32_t* __restrict__ sorig,
                                                  const int32_t* __restrict__ cid,
+                                                 const int64_t* __restrict__ reps, int64_t nr,
                                                  const int32_t* __restrict__ nc_list,
                                                  const int32_t* __restrict__ nc_count,
                                                  int32_t* __restrict__ labels) {
-  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= *nc_count) return;
-  const int64_t s = nc_list[q];
-  (void)n;
-  const int32_t key = skey[s];
-  int best = INT_MAX;
-  if ((int64_t)key < g.cells) {
-    const float4 p = pts[s];
-    for_each_cell<D>(p, key, g, cell_start, boxA, boxB, slab_t,
-                     [&](int64_t c, int b, int e, int cls) -> bool {
-                       const int r = rep[c];
-                       if (r < 0) return false;
-                       if (mutual[c]) {
-                         if (cls == 1) {
-                           best = min(best, ccmin[r]);
-                           return false;
-                         }
-                         if (ccmin[r] >= best) return false;  // cannot improve
-                         for (int j = r; j < e; ++j) {
-                           const int m = ccmin[j];
-                           if (m >= 0 && adjacent<D>(p, pts[j], g)) {
-                             best = min(best, m);
-                             break;
-                           }
-                         }
-                       } else {
-                         for (int j = r; j < e; ++j) {
-                           const int m = ccmin[j];
-                           if (m >= 0 && m < best && (cls == 1 || adjacent<D>(p, pts[j], g)))
-                             best = m;
-                         }
-                       }
-                       return false;
-                     });
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+  const int64_t nq = *nc_count;
+  auto keyof = [&](int j) -> int64_t { return GLOBAL ? srep[j] : (int64_t)ccmin[j]; };
+  for (int64_t q = w0; q < nq; q += nw) {
+    const int s = nc_list[q];
+    const int32_t key = skey[s];
+    int64_t best = INT64_MAX;
+    if ((int64_t)key < g.cells) {
+      const float4 p = pts[s];
+      int cx, cy, cz;
+      decode_key<D>(key, g, cx, cy, cz);
+      const Window w = make_window<D>(cx, cy, cz, (double)p.w, (double)p.w, g);
+      for (int base = 0; base < w.total; base += 64) {
+        const int qq = base + lane;
+        int b = 0, e = 0, r = -1, cls = 0, mut = 0;
+        int64_t mk = INT64_MAX;
+        if (qq < w.total) {
+          const int64_t c = window_cell(w, qq, g, slab_t, p.w, p.w);
+          if (c >= 0) {
+            b = cell_start[c];
+            e = cell_start[c + 1];
+            r = (e > b) ? rep[c] : -1;
+            if (r >= 0) {
+              cls = classify<D>(p, boxA[c], boxB[c], g);
+              mut = mutual[c];
+              if (mut) mk = keyof(r);
+            }
+          }
+        }
+        // whole mutual cells in reach: their component key directly
+        best = min(best, wave_min64((cls == 1 && mut) ? mk : INT64_MAX));
+        uint64_t pm = __ballot(cls != 0 && !(cls == 1 && mut) && (!mut || mk < best));
+        while (pm) {
+          const int l = __ffsll((unsigned long long)pm) - 1;
+          pm &= pm - 1;
+          const int rl = __shfl(r, l), el = __shfl(e, l), cl = __shfl(cls, l);
+          if (__shfl(mut, l)) {
+            const int64_t ml = __shfl(mk, l);
+            if (ml >= best) continue;
+            bool hit = false;
+            for (int j0 = rl; j0 < el && !hit; j0 += 64) {
+              const int j = j0 + lane;
+              hit = __ballot((j < el) && keyof(j) >= 0 && adjacent<D>(p, pts[j], g)) != 0;
+            }
+            if (hit) best = ml;
+          } else {
+            int64_t lb = INT64_MAX;
+            for (int j0 = rl; j0 < el; j0 += 64) {
+              const int j = j0 + lane;
+              if (j < el) {
+                const int64_t m = keyof(j);
+                if (m >= 0 && m < best && m < lb && (cl == 1 || adjacent<D>(p, pts[j], g)))
+                  lb = m;
+              }
+            }
+            best = min(best, wave_min64(lb));
+          }
+        }
+      }
+    }
+    if (lane == 0) {
+      int32_t out = -1;
+      if (best != INT64_MAX) out = GLOBAL ? rep_id(reps, nr, best) : cid[best];
+      labels[sorig[s]] = out;
+    }
   }
-  labels[sorig[s]] = (best == INT_MAX) ? -1 : cid[best];
 }
 
 // Degenerate parameters (negative/NaN eps): nobody has a neighbour, not even itself.
@@ -826,50 +1156,19 @@ __global__ void k_srep(const int64_t* __restrict__ rep, const uint8_t* __restric
        s += (int64_t)gridDim.x * blockDim.x)
     srep[s] = core[s] ? rep[sorig[s]] : -1;
 }
-__device__ __forceinline__ int32_t rep_id(const int64_t* __restrict__ reps, int64_t nr, int64_t v) {
-  int64_t lo = 0, hi = nr;
-  while (lo < hi) {
-    const int64_t m = (lo + hi) >> 1;
-    if (reps[m] < v) lo = m + 1; else hi = m;
+// Final labels of core points from global representatives (ids = rank of the representative in
+// the sorted global list); non-core points go through k_label<D, true>.
+__global__ __launch_bounds__(kBlock) void k_label_global_core(const int64_t* __restrict__ srep,
+                                                             int64_t n,
+                                                             const int32_t* __restrict__ sorig,
+                                                             const int64_t* __restrict__ reps,
+                                                             int64_t nr,
+                                                             int32_t* __restrict__ labels) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t own = srep[s];
+    if (own >= 0) labels[sorig[s]] = rep_id(reps, nr, own);
   }
-  return (lo < nr && reps[lo] == v) ? (int32_t)lo : -2;  // -2: representative missing (bug)
-}
-// Final labels from global representatives: core -> id(rep); non-core -> id(min rep over adjacent
-// core points); ids = rank of the representative in the sorted global list.
-template <int D>
-__global__ __launch_bounds__(kBlock) void k_label_global(
-    const float4* __restrict__ pts, const int32_t* __restrict__ skey, int64_t n, Geom g,
-    const int32_t* __restrict__ cell_start, const float4* __restrict__ boxA,
-    const float4* __restrict__ boxB, const float2* __restrict__ slab_t,
-    const int64_t* __restrict__ srep, const int32_t* __restrict__ rep,
-    const uint8_t* __restrict__ mutual, const int32_t* __restrict__ sorig,
-    const int64_t* __restrict__ reps, int64_t nr, int32_t* __restrict__ labels) {
-  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n) return;
-  const int64_t own = srep[s];
-  if (own >= 0) {
-    labels[sorig[s]] = rep_id(reps, nr, own);
-    return;
-  }
-  const int32_t key = skey[s];
-  int64_t best = INT64_MAX;
-  if ((int64_t)key < g.cells) {
-    const float4 p = pts[s];
-    for_each_cell<D>(p, key, g, cell_start, boxA, boxB, slab_t,
-                     [&](int64_t c, int b, int e, int cls) -> bool {
-                       const int r = rep[c];
-                       if (r < 0) return false;
-                       for (int j = r; j < e; ++j) {
-                         const int64_t m = srep[j];
-                         if (m >= 0 && m < best && (cls == 1 || adjacent<D>(p, pts[j], g))) {
-                           best = m;
-                           if (mutual[c]) break;  // one component per mutual cell
-                         }
-                       }
-                       return false;
-                     });
-  }
-  labels[sorig[s]] = (best == INT64_MAX) ? -1 : rep_id(reps, nr, best);
 }
 
 struct Timer {
@@ -918,6 +1217,7 @@ struct DbscanState {
   uint8_t *mutual = nullptr, *core = nullptr;
   float2* slab_t = nullptr;
   int32_t *parent = nullptr, *ccmin = nullptr, *cid = nullptr, *nc_list = nullptr;
+  int32_t *occ = nullptr, *hpos = nullptr;  // occupied cells (ascending), head-flag scan; n_occ = hpos[n]
   int64_t* srep = nullptr;
   int64_t* stmp = nullptr;
   Timer tm;
@@ -940,15 +1240,17 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
                              const float* t, double eps_space, double eps_time, hipStream_t st) {
   const int gb = grid_for(n, kBlock, 2048);
   // ---- bounds (one small sync); the arena is re-reserved below, so copy results out first
+  const int nbb = grid_for(n, kBlock, 1024);
   {
     Budget bb;
     bb.add<Bounds>(1);
+    bb.add<Bounds>(nbb);
     RPT_TRY(arena.reserve(bb.bytes, st));
   }
   Bounds* d_b = arena.carve_n<Bounds>(1);
-  hipLaunchKernelGGL(k_bounds_init, dim3(1), dim3(1), 0, st, d_b);
-  hipLaunchKernelGGL(k_bounds<D>, dim3(grid_for(n, kBlock, 1024)), dim3(kBlock), 0, st, x, y, z,
-                     stride, t, n, d_b);
+  Bounds* d_part = arena.carve_n<Bounds>(nbb);
+  hipLaunchKernelGGL(k_bounds<D>, dim3(nbb), dim3(kBlock), 0, st, x, y, z, stride, t, n, d_part);
+  hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(kBlock), 0, st, d_part, nbb, d_b);
   RPT_CHECK_LAUNCH();
   Bounds hb;
   RPT_HIP(hipMemcpyAsync(&hb, d_b, sizeof(Bounds), hipMemcpyDeviceToHost, st));
@@ -1023,6 +1325,8 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   bud.add<int32_t>(n + 1);  // cid
   bud.add<int32_t>(n + 1);  // non-core list (+count)
   bud.add<int64_t>(n);      // srep (global finalize)
+  bud.add<int32_t>(n + 1);  // occ
+  bud.add<int32_t>(n + 1);  // hpos
   RPT_TRY(arena.reserve(bud.bytes, st));
   (void)arena.carve_n<Bounds>(1);
   uint32_t* keys = arena.carve_n<uint32_t>(n);
@@ -1046,13 +1350,14 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   cid = arena.carve_n<int32_t>(n + 1);
   nc_list = arena.carve_n<int32_t>(n + 1);
   srep = arena.carve_n<int64_t>(n);
-  if (!srep) {
+  occ = arena.carve_n<int32_t>(n + 1);
+  hpos = arena.carve_n<int32_t>(n + 1);
+  if (!hpos) {
     set_error("internal: scratch carve overflow");
     return RPT_ENOMEM;
   }
-  RPT_HIP(hipMemsetAsync(cell_start, 0, sizeof(int32_t) * (C1 + 1), st));
   hipLaunchKernelGGL(k_keys<D>, dim3(gb), dim3(kBlock), 0, st, x, y, z, stride, t, n, g, keys,
-                     vals, cell_start);
+                     vals);
   RPT_CHECK_LAUNCH();
   int bits = 1;
   while ((int64_t(1) << bits) <= C1) ++bits;
@@ -1060,11 +1365,16 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   RPT_TRY(radix_sort_pairs(keys, vals, keys_alt, vals_alt, n, bits, rtmp, &sk, &sv, st));
   hipLaunchKernelGGL(k_gather<D>, dim3(gb), dim3(kBlock), 0, st, x, y, z, stride, t, n, sk, sv,
                      pts, sorig, skey);
+  RPT_HIP(hipMemsetAsync(cell_start, 0, sizeof(int32_t) * (C1 + 1), st));
+  RPT_HIP(hipMemsetAsync(hpos + n, 0, sizeof(int32_t), st));
+  hipLaunchKernelGGL(k_cell_runs, dim3(gb), dim3(kBlock), 0, st, skey, n, cell_start, hpos);
   RPT_CHECK_LAUNCH();
   RPT_TRY(exclusive_scan_i32(cell_start, cell_start, C1 + 1, stmp, st));
-  const int gc = grid_for(C, kBlock, 8192);
-  hipLaunchKernelGGL(k_cell_box<D>, dim3(gc), dim3(kBlock), 0, st, pts, cell_start, C, g, boxA,
-                     boxB, mutual);
+  RPT_TRY(exclusive_scan_i32(hpos, hpos, n + 1, stmp, st));
+  hipLaunchKernelGGL(k_occ_list, dim3(gb), dim3(kBlock), 0, st, skey, n, hpos, occ);
+  RPT_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_cell_box<D>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, cell_start,
+                     occ, hpos + n, g, boxA, boxB, mutual);
   RPT_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_slab_range, dim3((unsigned)nt), dim3(kBlock), 0, st, pts, cell_start,
                      (int64_t)(C / nt), (int)nt, slab_t);
@@ -1088,13 +1398,17 @@ int32_t DbscanState::build(const float* x, const float* y, const float* z, int64
 
 int32_t DbscanState::core_pass(hipStream_t st) {
   if (degenerate) return RPT_OK;
-  const unsigned gp = (unsigned)((n + kBlock - 1) / kBlock);
+  int32_t* slow = nc_list;  // the non-core queue is built later; reuse its storage
+  int32_t* n_slow = nc_list + n;
+  RPT_HIP(hipMemsetAsync(n_slow, 0, sizeof(int32_t), st));
+  hipLaunchKernelGGL(k_core_fast, dim3(tile_grid(n)), dim3(kBlock), 0, st, skey, n, g, cell_start,
+                     mutual, core, slow, n_slow);
   if (dim == 2)
-    hipLaunchKernelGGL(k_core<2>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
-                       boxA, boxB, slab_t, mutual, core);
+    hipLaunchKernelGGL(k_core_slow<2>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
+                       cell_start, boxA, boxB, slab_t, slow, n_slow, core);
   else
-    hipLaunchKernelGGL(k_core<3>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
-                       boxA, boxB, slab_t, mutual, core);
+    hipLaunchKernelGGL(k_core_slow<3>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
+                       cell_start, boxA, boxB, slab_t, slow, n_slow, core);
   RPT_CHECK_LAUNCH();
   tm.mark();
   return RPT_OK;
@@ -1104,22 +1418,28 @@ int32_t DbscanState::union_pass(hipStream_t st) {
   if (degenerate) return RPT_OK;
   const int gb = grid_for(n, kBlock, 2048);
   const int gc = grid_for(C, kBlock, 8192);
+  const int gw = wave_grid(n);
   const unsigned gp = (unsigned)((n + kBlock - 1) / kBlock);
+  const int32_t* n_occ = hpos + n;
   hipLaunchKernelGGL(k_rep, dim3(gc), dim3(kBlock), 0, st, cell_start, C, core, rep);
   hipLaunchKernelGGL(k_parent_init, dim3(gb), dim3(kBlock), 0, st, parent, n, core, skey, mutual,
                      rep, C);
   if (dim == 2) {
-    hipLaunchKernelGGL((k_union_cells<2, false>), dim3(gc), dim3(kBlock), 0, st, pts, C, g,
-                       cell_start, boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
-    hipLaunchKernelGGL((k_union_cells<2, true>), dim3(gc), dim3(kBlock), 0, st, pts, C, g,
-                       cell_start, boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
+    hipLaunchKernelGGL((k_union_cells<2, false>), dim3(gw), dim3(kBlock), 0, st, pts, g,
+                       cell_start, occ, n_occ, boxA, boxB, slab_t, core, rep, mutual, sorig,
+                       parent);
+    hipLaunchKernelGGL((k_union_cells<2, true>), dim3(gw), dim3(kBlock), 0, st, pts, g,
+                       cell_start, occ, n_occ, boxA, boxB, slab_t, core, rep, mutual, sorig,
+                       parent);
     hipLaunchKernelGGL(k_union<2>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
                        boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
   } else {
-    hipLaunchKernelGGL((k_union_cells<3, false>), dim3(gc), dim3(kBlock), 0, st, pts, C, g,
-                       cell_start, boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
-    hipLaunchKernelGGL((k_union_cells<3, true>), dim3(gc), dim3(kBlock), 0, st, pts, C, g,
-                       cell_start, boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
+    hipLaunchKernelGGL((k_union_cells<3, false>), dim3(gw), dim3(kBlock), 0, st, pts, g,
+                       cell_start, occ, n_occ, boxA, boxB, slab_t, core, rep, mutual, sorig,
+                       parent);
+    hipLaunchKernelGGL((k_union_cells<3, true>), dim3(gw), dim3(kBlock), 0, st, pts, g,
+                       cell_start, occ, n_occ, boxA, boxB, slab_t, core, rep, mutual, sorig,
+                       parent);
     hipLaunchKernelGGL(k_union<3>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
                        boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
   }
@@ -1144,23 +1464,24 @@ int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hi
     }
     return RPT_OK;
   }
-  const unsigned gp = (unsigned)((n + kBlock - 1) / kBlock);
   int32_t* nc_count = nc_list + n;
   RPT_HIP(hipMemsetAsync(cid, 0, sizeof(int32_t) * (n + 1), st));
   RPT_HIP(hipMemsetAsync(nc_count, 0, sizeof(int32_t), st));
-  hipLaunchKernelGGL(k_ccmin, dim3(gb), dim3(kBlock), 0, st, parent, core, n, sorig,
-                     (const int32_t*)nullptr, ccmin, cid, nc_list, nc_count);
+  hipLaunchKernelGGL(k_ccmin, dim3(tile_grid(n)), dim3(kBlock), 0, st, parent, core, n, sorig,
+                     ccmin, cid, nc_list, nc_count);
   RPT_CHECK_LAUNCH();
   RPT_TRY(exclusive_scan_i32(cid, cid, n + 1, stmp, st));
   hipLaunchKernelGGL(k_label_core, dim3(gb), dim3(kBlock), 0, st, ccmin, n, sorig, cid, labels);
   if (dim == 2)
-    hipLaunchKernelGGL(k_label<2>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
-                       boxA, boxB, slab_t, ccmin, rep, mutual, sorig, cid, nc_list, nc_count,
-                       labels);
+    hipLaunchKernelGGL((k_label<2, false>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
+                       cell_start, boxA, boxB, slab_t, ccmin, (const int64_t*)nullptr, rep,
+                       mutual, sorig, cid, (const int64_t*)nullptr, (int64_t)0, nc_list,
+                       nc_count, labels);
   else
-    hipLaunchKernelGGL(k_label<3>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
-                       boxA, boxB, slab_t, ccmin, rep, mutual, sorig, cid, nc_list, nc_count,
-                       labels);
+    hipLaunchKernelGGL((k_label<3, false>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
+                       cell_start, boxA, boxB, slab_t, ccmin, (const int64_t*)nullptr, rep,
+                       mutual, sorig, cid, (const int64_t*)nullptr, (int64_t)0, nc_list,
+                       nc_count, labels);
   RPT_CHECK_LAUNCH();
   tm.mark();
   if (stats) {
@@ -1194,16 +1515,21 @@ int32_t DbscanState::labels_global(const int64_t* rep_orig, const int64_t* reps,
     return RPT_ENOTSUP;
   }
   const int gb = grid_for(n, kBlock, 2048);
-  const unsigned gp = (unsigned)((n + kBlock - 1) / kBlock);
+  int32_t* nc_count = nc_list + n;
   hipLaunchKernelGGL(k_srep, dim3(gb), dim3(kBlock), 0, st, rep_orig, core, sorig, n, srep);
+  RPT_HIP(hipMemsetAsync(nc_count, 0, sizeof(int32_t), st));
+  hipLaunchKernelGGL(k_nc_list, dim3(tile_grid(n)), dim3(kBlock), 0, st, core, n, nc_list,
+                     nc_count);
+  hipLaunchKernelGGL(k_label_global_core, dim3(gb), dim3(kBlock), 0, st, srep, n, sorig, reps, nr,
+                     labels);
   if (dim == 2)
-    hipLaunchKernelGGL(k_label_global<2>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g,
-                       cell_start, boxA, boxB, slab_t, srep, rep, mutual, sorig, reps, nr,
-                       labels);
+    hipLaunchKernelGGL((k_label<2, true>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
+                       cell_start, boxA, boxB, slab_t, (const int32_t*)nullptr, srep, rep, mutual,
+                       sorig, (const int32_t*)nullptr, reps, nr, nc_list, nc_count, labels);
   else
-    hipLaunchKernelGGL(k_label_global<3>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g,
-                       cell_start, boxA, boxB, slab_t, srep, rep, mutual, sorig, reps, nr,
-                       labels);
+    hipLaunchKernelGGL((k_label<3, true>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
+                       cell_start, boxA, boxB, slab_t, (const int32_t*)nullptr, srep, rep, mutual,
+                       sorig, (const int32_t*)nullptr, reps, nr, nc_list, nc_count, labels);
   RPT_CHECK_LAUNCH();
   return RPT_OK;
 }

@@ -9,7 +9,11 @@
 //                    elements, halving split above), chunks accumulated sequentially, then a
 //                    float32 division by k.
 // Segments: a stable radix sort of (label+1, index) keeps each label's points in index order, so
-// every (label, frame) run is contiguous and ordered; one thread walks each run.
+// every (label, frame) run is contiguous and ordered.  One wave per run: lanes load 64 points at a
+// time (coalesced), the order-preserving float32 chain reads them back lane by lane from
+// registers (v_readlane), so a run of k points costs ~k dependent adds, not k memory latencies.
+// Noise (key 0) sorts first in index order, so each frame's first noise point is the head of its
+// frame within the noise run (no atomics).
 #include <climits>
 
 #include "common.h"
@@ -22,28 +26,26 @@ namespace {
 constexpr int kBlock = 256;
 
 __global__ void k_sum_keys(const int32_t* __restrict__ labels, int64_t n,
-                           uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                           const int32_t* __restrict__ pf,
-                           unsigned long long* __restrict__ first_noise) {
+                           uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t l = labels[i];
-    keys[i] = (uint32_t)(l + 1);  // noise (-1) -> 0, sorts first
+    keys[i] = (uint32_t)(labels[i] + 1);  // noise (-1) -> 0, sorts first
     vals[i] = (uint32_t)i;
-    if (l < 0) atomicMin(first_noise + pf[i], (unsigned long long)i);
   }
 }
 
-// head[p] = 1 where a (label, frame) run starts among clustered points
+// head[p] = 1 where a (label, frame) run starts among clustered points; for the noise run, the
+// first noise point of each frame is recorded.
 __global__ void k_heads(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
-                        const int32_t* __restrict__ pf, int64_t n, int32_t* __restrict__ head) {
+                        const int32_t* __restrict__ pf, int64_t n, int32_t* __restrict__ head,
+                        int64_t* __restrict__ first_noise) {
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n;
        p += (int64_t)gridDim.x * blockDim.x) {
-    int h = 0;
-    if (sk[p] != 0u) {
-      h = (p == 0) || sk[p] != sk[p - 1] || pf[sv[p]] != pf[sv[p - 1]];
-    }
-    head[p] = h;
+    const uint32_t k = sk[p], i = sv[p];
+    const int32_t f = pf[i];
+    const bool h = (p == 0) || k != sk[p - 1] || f != pf[sv[p - 1]];
+    head[p] = (k != 0u && h) ? 1 : 0;
+    if (k == 0u && h && first_noise) first_noise[f] = (int64_t)i;
   }
 }
 
@@ -125,83 +127,81 @@ __global__ void k_gather_runs(const uint32_t* __restrict__ sv, int64_t n,
   }
 }
 
-// One lane per (frame, label) run: sequential float32 sums in index order (np.mean axis 0).
-// Mean intensity: when every intensity is a non-negative integer and the running sum stays
-// below 2^24, every summation order is exact, so the sequential sum equals numpy's pairwise
-// result; otherwise numpy's chunked pairwise sum is evaluated.
-__global__ void k_summarize(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
-                            const int64_t* __restrict__ seg_start, int64_t n_seg, int64_t n,
-                            const float* __restrict__ gx, const float* __restrict__ gy,
-                            const float* __restrict__ gi, const int32_t* __restrict__ pf,
-                            int32_t* __restrict__ o_frame, int32_t* __restrict__ o_label,
-                            int64_t* __restrict__ o_count, int64_t* __restrict__ o_first,
-                            float* __restrict__ o_cx, float* __restrict__ o_cy,
-                            float* __restrict__ o_mi) {
-  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n_seg;
-       s += (int64_t)gridDim.x * blockDim.x) {
+__device__ __forceinline__ float lane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// One wave per (frame, label) run: sequential float32 sums in index order (np.mean axis 0).
+// Mean intensity: when every intensity is a non-negative integer and the total stays below 2^24,
+// every summation order is exact (integer lane sums), which equals numpy's pairwise result;
+// otherwise numpy's chunked pairwise sum is evaluated by lane 0.
+__global__ __launch_bounds__(kBlock) void k_summarize(
+    const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
+    const int64_t* __restrict__ seg_start, int64_t n_seg, int64_t n,
+    const float* __restrict__ gx, const float* __restrict__ gy, const float* __restrict__ gi,
+    const int32_t* __restrict__ pf, int32_t* __restrict__ o_frame, int32_t* __restrict__ o_label,
+    int64_t* __restrict__ o_count, int64_t* __restrict__ o_first, float* __restrict__ o_cx,
+    float* __restrict__ o_cy, float* __restrict__ o_mi) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+  for (int64_t s = w0; s < n_seg; s += nw) {
     const int64_t b = seg_start[s];
     const int64_t e = (s + 1 < n_seg) ? seg_start[s + 1] : n;
     const int64_t k = e - b;
-    float sx = gx[b], sy = gy[b];
-    float si = gi[b];
-    bool small_int = (si >= 0.f) && (si == floorf(si));
-    // batches of kU independent loads, then the order-preserving sequential adds: one memory
-    // latency per batch instead of per element
-    constexpr int kU = 32;
-    int64_t p = b + 1;
-    for (; p + kU <= e; p += kU) {
-      float bx[kU], by[kU], bi[kU];
+    float sx = gx[b], sy = gy[b];  // numpy's reduction starts from the first row
+    bool small_int = true;
+    int64_t isum = 0;
+    for (int64_t j0 = b; j0 < e; j0 += 64) {
+      const int64_t j = j0 + lane;
+      const bool in = j < e;
+      const float vx = in ? gx[j] : 0.f, vy = in ? gy[j] : 0.f, vi = in ? gi[j] : 0.f;
+      small_int = small_int && (!in || (vi >= 0.f && vi == floorf(vi) && vi < 16777216.f));
+      isum += in ? (int64_t)vi : 0;
+      const int first = (j0 == b) ? 1 : 0;
+      const int m = (int)((e - j0 < 64) ? (e - j0) : 64);
+      if (m == 64 && !first) {
 #pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        bx[u] = gx[p + u];
-        by[u] = gy[p + u];
-        bi[u] = gi[p + u];
+        for (int l = 0; l < 64; ++l) {
+          sx = sx + lane_f(vx, l);
+          sy = sy + lane_f(vy, l);
+        }
+      } else {
+        for (int l = first; l < m; ++l) {
+          sx = sx + lane_f(vx, l);
+          sy = sy + lane_f(vy, l);
+        }
       }
+    }
 #pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        sx = sx + bx[u];
-        sy = sy + by[u];
-        small_int = small_int && (bi[u] >= 0.f) && (bi[u] == floorf(bi[u]));
-        si = si + bi[u];
+    for (int off = 32; off > 0; off >>= 1) isum += __shfl_xor(isum, off);
+    const bool all_int = __all(small_int);
+    if (lane == 0) {
+      const float fk = (float)k;
+      float mi;
+      if (all_int && isum < 16777216) {
+        mi = (float)isum / fk;
+      } else {
+        float tot = 0.f;
+        for (int64_t c = 0; c < k; c += 8192) {
+          const int64_t len = (k - c < 8192) ? (k - c) : 8192;
+          tot = tot + pairwise_f32(gi, b + c, len);
+        }
+        mi = tot / fk;
       }
+      const uint32_t i0 = sv[b];
+      o_frame[s] = pf[i0];
+      o_label[s] = (int32_t)sk[b] - 1;
+      o_count[s] = k;
+      o_first[s] = i0;
+      o_cx[s] = sx / fk;
+      o_cy[s] = sy / fk;
+      o_mi[s] = mi;
     }
-    for (; p < e; ++p) {
-      sx = sx + gx[p];
-      sy = sy + gy[p];
-      const float v = gi[p];
-      small_int = small_int && (v >= 0.f) && (v == floorf(v));
-      si = si + v;
-    }
-    const float fk = (float)k;
-    float mi;
-    if (small_int && si < 16777216.f) {
-      mi = si / fk;
-    } else {
-      float tot = 0.f;
-      for (int64_t c = 0; c < k; c += 8192) {
-        const int64_t len = (k - c < 8192) ? (k - c) : 8192;
-        tot = tot + pairwise_f32(gi, b + c, len);
-      }
-      mi = tot / fk;
-    }
-    const uint32_t i0 = sv[b];
-    o_frame[s] = pf[i0];
-    o_label[s] = (int32_t)sk[b] - 1;
-    o_count[s] = k;
-    o_first[s] = i0;
-    o_cx[s] = sx / fk;
-    o_cy[s] = sy / fk;
-    o_mi[s] = mi;
   }
 }
 
-__global__ void k_noise_finish(const unsigned long long* __restrict__ fn, int n_frames,
-                               int64_t* __restrict__ out) {
-  for (int f = blockIdx.x * blockDim.x + threadIdx.x; f < n_frames; f += gridDim.x * blockDim.x)
-    out[f] = (fn[f] == ~0ull) ? -1 : (int64_t)fn[f];
-}
-
-__global__ void k_fill_u64(unsigned long long* p, int64_t n, unsigned long long v) {
+__global__ void k_fill_i64(int64_t* p, int64_t n, int64_t v) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     p[i] = v;
@@ -231,7 +231,6 @@ int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
   b.add<int64_t>(n + 1);
   b.add<int64_t>(n + 1);
   b.add<int64_t>(scan_tmp_elems(n + 1));
-  b.add<unsigned long long>(n_frames + 1);
   for (int k = 0; k < 3; ++k) b.add<float>(n + 1);
   RPT_TRY(sc.reserve(b.bytes, st));
   uint32_t* keys = sc.carve_n<uint32_t>(n + 1);
@@ -243,29 +242,26 @@ int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
   int64_t* pos = sc.carve_n<int64_t>(n + 1);
   int64_t* seg_start = sc.carve_n<int64_t>(n + 1);
   int64_t* tmp = sc.carve_n<int64_t>(scan_tmp_elems(n + 1));
-  unsigned long long* fn = sc.carve_n<unsigned long long>(n_frames + 1);
   float* gx = sc.carve_n<float>(n + 1);
   float* gy = sc.carve_n<float>(n + 1);
   float* gi = sc.carve_n<float>(n + 1);
-  if (n_frames > 0)
-    hipLaunchKernelGGL(k_fill_u64, dim3(grid_for(n_frames, 256, 64)), dim3(256), 0, st, fn,
-                       (int64_t)n_frames, ~0ull);
+  if (n_frames > 0 && frame_first_noise)
+    hipLaunchKernelGGL(k_fill_i64, dim3(grid_for(n_frames, 256, 64)), dim3(256), 0, st,
+                       frame_first_noise, (int64_t)n_frames, (int64_t)-1);
   if (n == 0) {
     *n_seg_host = 0;
-    if (n_frames > 0 && frame_first_noise)
-      hipLaunchKernelGGL(k_noise_finish, dim3(grid_for(n_frames, 256, 64)), dim3(256), 0, st,
-                         fn, n_frames, frame_first_noise);
     RPT_CHECK_LAUNCH();
     return RPT_OK;
   }
   const int g = grid_for(n, kBlock, 8192);
-  hipLaunchKernelGGL(k_sum_keys, dim3(g), dim3(kBlock), 0, st, labels, n, keys, vals, pf, fn);
+  hipLaunchKernelGGL(k_sum_keys, dim3(g), dim3(kBlock), 0, st, labels, n, keys, vals);
   RPT_CHECK_LAUNCH();
   int bits = 1;
   while ((int64_t(1) << bits) <= (int64_t)n_clusters) ++bits;
   uint32_t *sk, *sv;
   RPT_TRY(radix_sort_pairs(keys, vals, ka, va, n, bits, rtmp, &sk, &sv, st));
-  hipLaunchKernelGGL(k_heads, dim3(g), dim3(kBlock), 0, st, sk, sv, pf, n, head);
+  hipLaunchKernelGGL(k_heads, dim3(g), dim3(kBlock), 0, st, sk, sv, pf, n, head,
+                     frame_first_noise);
   RPT_HIP(hipMemsetAsync(head + n, 0, sizeof(int32_t), st));
   RPT_TRY(exclusive_scan_i32_to_i64(head, pos, n + 1, tmp, st));
   hipLaunchKernelGGL(k_seg_starts, dim3(g), dim3(kBlock), 0, st, head, pos, n, seg_start);
@@ -276,14 +272,9 @@ int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
   if (n_seg > 0) {
     hipLaunchKernelGGL(k_gather_runs, dim3(g), dim3(kBlock), 0, st, sv, n, x, y, inten, gx, gy,
                        gi);
-    hipLaunchKernelGGL(k_summarize, dim3(grid_for(n_seg, 64, 8192)), dim3(64), 0, st, sk, sv,
-                       seg_start, n_seg, n, gx, gy, gi, pf, o_frame, o_label, o_count, o_first,
-                       o_cx, o_cy, o_mi);
-    RPT_CHECK_LAUNCH();
-  }
-  if (n_frames > 0 && frame_first_noise) {
-    hipLaunchKernelGGL(k_noise_finish, dim3(grid_for(n_frames, 256, 64)), dim3(256), 0, st, fn,
-                       n_frames, frame_first_noise);
+    hipLaunchKernelGGL(k_summarize, dim3(grid_for(n_seg, kBlock / 64, 16384)), dim3(kBlock), 0,
+                       st, sk, sv, seg_start, n_seg, n, gx, gy, gi, pf, o_frame, o_label, o_count,
+                       o_first, o_cx, o_cy, o_mi);
     RPT_CHECK_LAUNCH();
   }
   *n_seg_host = n_seg;
