@@ -69,6 +69,9 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-stage hipEvent timing")
+    ap.add_argument("--sync-host", action="store_true",
+                    help="run each step's host stage (order + tracker) inline instead of "
+                         "overlapping it with the next step's device work")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -101,7 +104,7 @@ def main():
 
         ops = HipOps(dev, timing=timing)
         pipe = ShardedStackPipeline(ops, Comm(dev), cfg.gains, cfg.rows, cfg.bins, PathParams(),
-                                    timing=timing)
+                                    timing=timing, async_host=not args.sync_host)
         G = len(cfg.gains)
         pipe.set_geometry(
             tuple(torch.from_numpy(np.tile(a, F * G)).to(dev) for a in
@@ -109,13 +112,14 @@ def main():
             torch.tensor(list(cfg.gains) * F, dtype=torch.int32, device=dev))
         run = lambda: pipe.run(echo, _abi.ECHO_U8, rank * F)  # noqa: E731
     else:
-        pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), dev, timing=timing)
+        pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), dev, timing=timing,
+                                  async_host=not args.sync_host)
         pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
                           cfg.n_frames * len(cfg.gains))
         run = lambda: pipe.run(echo)  # noqa: E731
 
     for _ in range(args.warmup):
-        run()
+        run().finish()
     torch.cuda.synchronize(dev)
     if dist:
         tdist.barrier()
@@ -124,17 +128,22 @@ def main():
     stage_acc = {}
     k5_ms = []
     res = None
+    results = []
     for _ in range(args.steps):
         res = run()
-        for k, v in res.stage_ms.items():
-            stage_acc[k] = stage_acc.get(k, 0.0) + v
+        results.append(res)
         if timing:
             k5_ms.append(res.stage_ms["dbscan_core"] if not dist else ops.last_core_ms())
+    for r in results:  # host stages (order + tracker) of the last runs, in order
+        r.finish()
     torch.cuda.synchronize(dev)
     if dist:
         tdist.barrier()
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
+    for r in results:
+        for k, v in r.stage_ms.items():
+            stage_acc[k] = stage_acc.get(k, 0.0) + v
     if dist:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
@@ -152,14 +161,23 @@ def main():
     value = pts * args.steps / dt / 1e6
     ms_step = dt / args.steps * 1e3
 
+    traffic = None
+    tfile = ROOT / "profiles" / "r1" / "k5_traffic.json"
+    if tfile.exists() and not dist and args.frames == 100:
+        # PMC-measured HBM bytes per K5 launch of this same workload (tools/pmc.sh: separate
+        # FETCH_SIZE / WRITE_SIZE passes, gfx950 read correction); committed under profiles/
+        traffic = json.loads(tfile.read_text()).get("bytes_per_launch")
     roof = None
     if k5_ms:
         k5 = float(np.mean(k5_ms))
         n_in = n_core_in
         achieved = K5_BYTES_PER_POINT * n_in / (k5 * 1e-3) / 1e9
-        roof = {"kernel": "k_core (K5 neighbour count / core flag)", "bound": "hbm",
+        roof = {"kernel": "K5 = k_core_fast + k_core_slow (neighbour count / core flag)",
+                "bound": "hbm",
                 "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None if traffic is None else int(traffic),
+                "traffic_unit": "bytes per launch (PMC, profiles/r1/k5_traffic.json)",
                 "bytes_model": "17 B/point x points entering ST-DBSCAN (SURVEY.md 8d)",
                 "avg_ms": round(k5, 4), "points": n_in}
     stage = {k: round(v / args.steps, 3) for k, v in stage_acc.items()}
@@ -186,7 +204,10 @@ def main():
                                    f"eps_t 2 / min 15 + Hungarian tracking (BASELINE configs[2])",
                        "frames_per_gpu": args.frames, "points_per_step": int(pts),
                        **summary,
-                       "parallelism": f"frame-sharded x{world}" if dist else "single GPU"},
+                       "parallelism": f"frame-sharded x{world}" if dist else "single GPU",
+                       "host_stage": "inline" if args.sync_host else
+                       "overlapped: step k's order+tracker runs on a host thread during step "
+                       "k+1's device work; the timed region ends after the last one"},
             "roofline": roof, "cpu_baseline": cpu, "stage_ms": stage,
         }
         print(json.dumps(out), flush=True)

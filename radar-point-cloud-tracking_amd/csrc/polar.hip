@@ -12,6 +12,8 @@
 //   step = scale[row] / (float)bins ; r = step * (float)bin ; x = r * cos_t[row] ; y = r * sin_t[row]
 // cos_t / sin_t are inputs: numpy's float32 SIMD cos/sin are not correctly rounded, so the host
 // evaluates them exactly as the reference does (4096 values per sweep geometry).
+#include <cmath>
+
 #include "common.h"
 
 #pragma clang fp contract(off)
@@ -64,6 +66,18 @@ __device__ __forceinline__ int wave_excl_scan(int v, int* total) {
   return incl - v;
 }
 
+// Inclusive wave prefix sum with DPP (6 VALU ops, no LDS): row_shr 1/2/4/8 within 16-lane rows,
+// then row_bcast:15 / row_bcast:31 carry the row totals (GFX9-family DPP, available on gfx950).
+__device__ __forceinline__ int wave_incl_scan_dpp(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+
 // Row pass: count kept elements per row.  VEC path needs bins % (64*N) == 0 and aligned rows.
 template <class T, bool VEC>
 __global__ __launch_bounds__(kBlock) void k_row_count(const T* __restrict__ echo,
@@ -111,7 +125,11 @@ struct RowGeo {
   const float* sin_t;
 };
 
-// Row pass 2: write the kept elements whose in-file rank is a multiple of stride.
+// Row pass 2: write the kept elements whose in-file rank is a multiple of stride.  Each lane ranks
+// its kept elements, the emitted ones (bin, value) are staged in the wave's LDS slice in output
+// order, and the wave then writes them with full-width coalesced stores (a row emits only
+// ~kept/stride points, so storing from the ranking lanes directly would issue ~5 x 16 mostly
+// masked store instructions per row).
 template <class T, bool VEC>
 __global__ __launch_bounds__(kBlock) void k_row_write(
     const T* __restrict__ echo, int64_t n_rows, int rows, int bins, float thr, int stride,
@@ -119,8 +137,12 @@ __global__ __launch_bounds__(kBlock) void k_row_write(
     const int64_t* __restrict__ file_offsets, int files_per_frame, float* __restrict__ x,
     float* __restrict__ y, float* __restrict__ val, int32_t* __restrict__ gain_out,
     int32_t* __restrict__ pf_out) {
+  constexpr int CH = VEC ? 64 * Vec<T>::N : 64;  // bins per chunk
+  __shared__ uint16_t s_bin[kWavesPerBlock][CH];
+  __shared__ float s_val[kWavesPerBlock][CH];
   const int lane = threadIdx.x & 63;
-  const int64_t wave0 = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / 64;
+  const int wv = threadIdx.x / 64;
+  const int64_t wave0 = (int64_t)blockIdx.x * kWavesPerBlock + wv;
   const int64_t n_waves = (int64_t)gridDim.x * kWavesPerBlock;
   const float fb = (float)bins;
   const uint32_t ustride = (uint32_t)stride;
@@ -134,18 +156,11 @@ __global__ __launch_bounds__(kBlock) void k_row_write(
     const float ct = geo.cos_t[row], st = geo.sin_t[row];
     const int32_t g = gain ? gain[f] : 0;
     const int32_t fr = (int32_t)((uint32_t)f / (uint32_t)files_per_frame);
-    auto put = [&](int b, float v, int64_t o) {
-      const float rr = geo.ranges ? geo.ranges[row * bins + b] : step * (float)b;
-      x[o] = rr * ct;
-      y[o] = rr * st;
-      val[o] = v;
-      if (gain_out) gain_out[o] = g;
-      if (pf_out) pf_out[o] = fr;
-    };
-    if (VEC) {
-      constexpr int N = Vec<T>::N;
-      using L = typename Vec<T>::L;
-      for (int base = 0; base < bins; base += 64 * N) {
+    for (int base = 0; base < bins; base += CH) {
+      int tot;
+      if (VEC) {
+        constexpr int N = Vec<T>::N;
+        using L = typename Vec<T>::L;
         const int b0 = base + lane * N;
         const L v = *reinterpret_cast<const L*>(rp + b0);
         float fv[N];
@@ -153,19 +168,20 @@ __global__ __launch_bounds__(kBlock) void k_row_write(
         int c = 0;
 #pragma unroll
         for (int k = 0; k < N; ++k) c += (fv[k] > thr) ? 1 : 0;
-        int tot;
         const uint32_t r = rank + (uint32_t)wave_excl_scan(c, &tot);
         if (c) {
-          // kept elements with in-file rank % stride == 0 are emitted: one 32-bit division per
-          // lane, then a countdown to the next emitted rank
+          // emitted = kept elements with in-file rank % stride == 0: one 32-bit division per
+          // lane, then a countdown; slot = output index - the chunk's first output index
           const uint32_t q = r / ustride, rem = r - q * ustride;
           uint32_t skip = rem ? ustride - rem : 0u;
-          int64_t o = out0 + q + (rem ? 1 : 0);
+          int slot = (int)(q + (rem ? 1u : 0u) - (rank + ustride - 1u) / ustride);
 #pragma unroll
           for (int k = 0; k < N; ++k) {
             if (fv[k] > thr) {
               if (skip == 0u) {
-                put(b0 + k, fv[k], o++);
+                s_bin[wv][slot] = (uint16_t)(b0 + k - base);
+                s_val[wv][slot] = fv[k];
+                ++slot;
                 skip = ustride - 1u;
               } else {
                 --skip;
@@ -173,24 +189,198 @@ __global__ __launch_bounds__(kBlock) void k_row_write(
             }
           }
         }
-        rank += (uint32_t)tot;
-      }
-    } else {
-      for (int base = 0; base < bins; base += 64) {
+      } else {
         const int b = base + lane;
         const float v = (b < bins) ? to_f(rp[b]) : 0.f;
         const bool keep = (b < bins) && (v > thr);
         const uint64_t m = __ballot(keep);
+        tot = __popcll(m);
         if (keep) {
           const uint32_t r = rank + (uint32_t)rank_in_mask(m);
           const uint32_t q = r / ustride;
-          if (r - q * ustride == 0u) put(b, v, out0 + q);
+          if (r - q * ustride == 0u) {
+            const int slot = (int)(q - (rank + ustride - 1u) / ustride);
+            s_bin[wv][slot] = (uint16_t)lane;
+            s_val[wv][slot] = v;
+          }
         }
-        rank += (uint32_t)__popcll(m);
       }
+      const uint32_t first = (rank + ustride - 1u) / ustride;
+      const int n_emit = (int)((rank + (uint32_t)tot + ustride - 1u) / ustride - first);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int l = lane; l < n_emit; l += 64) {
+        const int b = base + (int)s_bin[wv][l];
+        const int64_t o = out0 + first + l;
+        const float rr = geo.ranges ? geo.ranges[row * bins + b] : step * (float)b;
+        x[o] = rr * ct;
+        y[o] = rr * st;
+        val[o] = s_val[wv][l];
+        if (gain_out) gain_out[o] = g;
+        if (pf_out) pf_out[o] = fr;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      rank += (uint32_t)tot;
     }
   }
 }
+
+// ---- u8 fast path (the radar's native sample type).  For integer samples v in [0, 255],
+// (float)v > thr  <=>  v > T  with T = floor(thr) clamped to [-1, 255] (NaN -> 255: nothing kept),
+// evaluated on 4 bytes at once (SWAR, exact per byte, no carries across bytes):
+//   T <= 127 : hi bit of ((x & 0x7f..) + (127 - T) * 0x01..) | x
+//   T >= 128 : hi bit of ((x & 0x7f..) + (255 - T) * 0x01..) & x
+__device__ __forceinline__ uint32_t gt_mask(uint32_t x, int T) {
+  if (T < 0) return 0x80808080u;
+  if (T >= 255) return 0u;
+  const uint32_t lo = x & 0x7f7f7f7fu;
+  if (T <= 127) return ((lo + (uint32_t)(127 - T) * 0x01010101u) | x) & 0x80808080u;
+  return ((lo + (uint32_t)(255 - T) * 0x01010101u) & x) & 0x80808080u;
+}
+// the 4 per-byte hi bits of a mask -> 4-bit nibble (byte k -> bit k)
+__device__ __forceinline__ uint32_t nib(uint32_t m) { return ((m >> 7) * 0x10204080u) >> 28; }
+
+// Rows per wave iteration: their loads are issued together (4 KiB in flight per wave) before any
+// row is reduced, instead of one dependent 1-KiB load per iteration.
+constexpr int kRowsPerIter = 4;
+
+__global__ __launch_bounds__(kBlock) void k_row_count_u8(const uint8_t* __restrict__ echo,
+                                                        int64_t n_rows, int bins, int T,
+                                                        int32_t* __restrict__ row_count) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave0 = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / 64;
+  const int64_t n_waves = (int64_t)gridDim.x * kWavesPerBlock;
+  const int64_t n_groups = (n_rows + kRowsPerIter - 1) / kRowsPerIter;
+  for (int64_t grp = wave0; grp < n_groups; grp += n_waves) {
+    const int64_t row0 = grp * kRowsPerIter;
+    int c[kRowsPerIter];
+#pragma unroll
+    for (int k = 0; k < kRowsPerIter; ++k) c[k] = 0;
+    for (int b0 = lane * 16; b0 < bins; b0 += 64 * 16) {
+      uint4 v[kRowsPerIter];
+#pragma unroll
+      for (int k = 0; k < kRowsPerIter; ++k)
+        v[k] = (row0 + k < n_rows) ? *reinterpret_cast<const uint4*>(echo + (row0 + k) * bins + b0)
+                                   : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+      for (int k = 0; k < kRowsPerIter; ++k)
+        c[k] += __popc(gt_mask(v[k].x, T)) + __popc(gt_mask(v[k].y, T)) +
+                __popc(gt_mask(v[k].z, T)) + __popc(gt_mask(v[k].w, T));
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+      for (int k = 0; k < kRowsPerIter; ++k) c[k] += __shfl_xor(c[k], off);
+    if (lane < kRowsPerIter) {
+      int cv = c[0];
+#pragma unroll
+      for (int k = 1; k < kRowsPerIter; ++k) cv = (lane == k) ? c[k] : cv;
+      if (row0 + lane < n_rows) row_count[row0 + lane] = cv;
+    }
+  }
+}
+
+// Same contract as k_row_write (LDS-staged emission), u8 samples, bins == 1024 (one chunk per
+// row): kRowsPerIter rows' samples are loaded before the first is ranked.
+__global__ __launch_bounds__(kBlock) void k_row_write_u8(
+    const uint8_t* __restrict__ echo, int64_t n_rows, int rows, int bins, int T, int stride,
+    RowGeo geo, const int32_t* __restrict__ gain, const int64_t* __restrict__ row_prefix,
+    const int64_t* __restrict__ file_offsets, int files_per_frame, float* __restrict__ x,
+    float* __restrict__ y, float* __restrict__ val, int32_t* __restrict__ gain_out,
+    int32_t* __restrict__ pf_out) {
+  constexpr int CH = 64 * 16;
+  __shared__ uint32_t s_stage[kWavesPerBlock][CH];  // (bin << 8) | sample
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x / 64;
+  const int64_t wave0 = (int64_t)blockIdx.x * kWavesPerBlock + wv;
+  const int64_t n_waves = (int64_t)gridDim.x * kWavesPerBlock;
+  const float fb = (float)bins;
+  const uint32_t ustride = (uint32_t)stride;
+  const int64_t n_groups = (n_rows + kRowsPerIter - 1) / kRowsPerIter;
+  const bool pow2 = (ustride & (ustride - 1u)) == 0u;
+  const uint32_t sh = (uint32_t)__builtin_ctz(ustride);
+  for (int64_t grp = wave0; grp < n_groups; grp += n_waves) {
+    // wave-uniform: lets the per-row metadata below use scalar loads / SALU
+    const int64_t row0 = (int64_t)__builtin_amdgcn_readfirstlane((int)grp) * kRowsPerIter;
+    uint4 vv[kRowsPerIter];
+#pragma unroll
+    for (int k = 0; k < kRowsPerIter; ++k)
+      vv[k] = (row0 + k < n_rows)
+                  ? *reinterpret_cast<const uint4*>(echo + (row0 + k) * CH + lane * 16)
+                  : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int kk = 0; kk < kRowsPerIter; ++kk) {
+      const int64_t row = row0 + kk;
+      if (row >= n_rows) break;
+      const uint4 v = vv[kk];
+      const int64_t f = (int64_t)((uint32_t)row / (uint32_t)rows);
+      uint32_t rank = (uint32_t)(row_prefix[row] - row_prefix[f * rows]);
+      const int64_t out0 = file_offsets[f];
+      const float step = geo.scale ? geo.scale[row] / fb : 0.f;
+      const float ct = geo.cos_t[row], st = geo.sin_t[row];
+      const int32_t g = gain ? gain[f] : 0;
+      const int32_t fr = (int32_t)((uint32_t)f / (uint32_t)files_per_frame);
+      const uint32_t m0 = gt_mask(v.x, T), m1 = gt_mask(v.y, T), m2 = gt_mask(v.z, T),
+                     m3 = gt_mask(v.w, T);
+      const int c = __popc(m0) + __popc(m1) + __popc(m2) + __popc(m3);
+      const int incl = wave_incl_scan_dpp(c);
+      const int tot = __builtin_amdgcn_readlane(incl, 63);
+      const uint32_t r = rank + (uint32_t)(incl - c);
+      const uint32_t first =
+          pow2 ? ((rank + ustride - 1u) >> sh) : (rank + ustride - 1u) / ustride;
+      if (c) {
+        uint32_t m = nib(m0) | (nib(m1) << 4) | (nib(m2) << 8) | (nib(m3) << 12);
+        const uint32_t q = pow2 ? (r >> sh) : r / ustride;
+        const uint32_t rem = r - q * ustride;
+        int slot = (int)(q + (rem ? 1u : 0u) - first);
+        // drop the kept elements before the first emitted rank, then emit every stride-th
+        for (uint32_t t = rem ? ustride - rem : 0u; t > 0u && m; --t) m &= m - 1u;
+        while (m) {
+          const int k = __builtin_ctz(m);
+          const uint32_t w = (k < 4) ? v.x : (k < 8) ? v.y : (k < 12) ? v.z : v.w;
+          const uint32_t sample = __builtin_amdgcn_ubfe(w, (uint32_t)(8 * (k & 3)), 8u);
+          s_stage[wv][slot++] = ((uint32_t)(lane * 16 + k) << 8) | sample;
+          for (uint32_t t = 0; t < ustride && m; ++t) m &= m - 1u;
+        }
+      }
+      const int n_emit =
+          (int)((pow2 ? ((rank + (uint32_t)tot + ustride - 1u) >> sh)
+                      : (rank + (uint32_t)tot + ustride - 1u) / ustride) - first);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int l = lane; l < n_emit; l += 64) {
+        const uint32_t e = s_stage[wv][l];
+        const int b = (int)(e >> 8);
+        const int64_t o = out0 + first + l;
+        const float rr = geo.ranges ? geo.ranges[row * bins + b] : step * (float)b;
+        x[o] = rr * ct;
+        y[o] = rr * st;
+        val[o] = (float)(e & 0xffu);
+        if (gain_out) gain_out[o] = g;
+        if (pf_out) pf_out[o] = fr;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+}
+
+// integer threshold of u8 samples (see gt_mask)
+inline int u8_threshold(float thr) {
+  if (!(thr == thr)) return 255;
+  const double f = std::floor((double)thr);
+  return f < -1.0 ? -1 : (f > 255.0 ? 255 : (int)f);
+}
+
+template <class T>
+constexpr bool is_u8() { return false; }
+template <>
+constexpr bool is_u8<uint8_t>() { return true; }
 
 template <class T>
 int32_t count_impl(const T* echo, int64_t n_files, int rows, int bins, float thr, int stride,
@@ -208,7 +398,11 @@ int32_t count_impl(const T* echo, int64_t n_files, int rows, int bins, float thr
   int64_t* tmp = sc.carve_n<int64_t>(scan_tmp_elems(n_rows + 1) + scan_tmp_elems(n_files + 1));
   const bool vec = (bins % (64 * Vec<T>::N) == 0) && ((uintptr_t)echo % 16 == 0);
   const int grid = grid_for(n_rows, kWavesPerBlock, 16384);
-  if (vec)
+  if (vec && is_u8<T>())
+    hipLaunchKernelGGL(k_row_count_u8, dim3(grid), dim3(kBlock), 0, st,
+                       reinterpret_cast<const uint8_t*>(echo), n_rows, bins, u8_threshold(thr),
+                       rc);
+  else if (vec)
     hipLaunchKernelGGL((k_row_count<T, true>), dim3(grid), dim3(kBlock), 0, st, echo, n_rows,
                        bins, thr, rc);
   else
@@ -243,7 +437,12 @@ int32_t write_impl(const T* echo, int64_t n_files, int rows, int bins, float thr
   }
   const bool vec = (bins % (64 * Vec<T>::N) == 0) && ((uintptr_t)echo % 16 == 0);
   const int grid = grid_for(n_rows, kWavesPerBlock, 16384);
-  if (vec)
+  if (vec && is_u8<T>() && bins == 64 * 16)
+    hipLaunchKernelGGL(k_row_write_u8, dim3(grid), dim3(kBlock), 0, st,
+                       reinterpret_cast<const uint8_t*>(echo), n_rows, rows, bins,
+                       u8_threshold(thr), stride, geo, gain, row_prefix, file_offsets, fpf, x, y,
+                       v, gout, pf);
+  else if (vec)
     hipLaunchKernelGGL((k_row_write<T, true>), dim3(grid), dim3(kBlock), 0, st, echo, n_rows,
                        rows, bins, thr, stride, geo, gain, row_prefix, file_offsets, fpf, x, y,
                        v, gout, pf);

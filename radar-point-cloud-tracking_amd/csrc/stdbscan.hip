@@ -578,29 +578,58 @@ __device__ __forceinline__ void block_append(int64_t tile0, int64_t n, P&& pred,
 }
 
 // ---------------------------------------------------------------- candidate windows
-// The cells that may hold a neighbour of point p: +-2 cells in space, the slab window of
-// [t - eps_t, t + eps_t] with +-1 slab of slack (culled per slab by its actual time range).
+// The cells that may hold a neighbour: +-2 cells in space (fixed 5-wide extents so candidate
+// decoding divides by constants; out-of-grid candidates are skipped) over the slabs whose actual
+// time range comes within eps_t of [tlo, thi] (the +-1-slab slack window is shrunk up front with
+// the per-slab time ranges).
 struct Window {
   int s0, x0, y0, z0;
-  int nS, nZ, nY, nX;
+  int nS;
   int total;
 };
 
+__device__ __forceinline__ bool slab_in_reach(const float2* __restrict__ slab_t, int s, float tlo,
+                                              float thi, float epst) {
+  const float2 sr = slab_t[s];
+  if (sr.x > sr.y) return false;  // empty slab
+  const float gap = (tlo > sr.y) ? (tlo - sr.y) : ((thi < sr.x) ? (sr.x - thi) : 0.f);
+  return gap <= epst;
+}
+
 template <int D>
-__device__ __forceinline__ Window make_window(int cx, int cy, int cz, double tlo, double thi,
-                                              const Geom& g) {
+__device__ __forceinline__ Window make_window(int cx, int cy, int cz, float tlo, float thi,
+                                              const Geom& g, const float2* __restrict__ slab_t,
+                                              int s_min = 0) {
+  constexpr int PER = (D == 3) ? 125 : 25;
   Window w;
   const double et = (double)g.epst;
-  w.s0 = (int)fmax(floor((tlo - et - g.ot) / g.ct) - 1.0, 0.0);
-  const int s1 = (int)fmin(floor((thi + et - g.ot) / g.ct) + 1.0, (double)(g.nt - 1));
-  w.x0 = max(cx - 2, 0);
-  w.y0 = max(cy - 2, 0);
-  w.z0 = (D == 3) ? max(cz - 2, 0) : 0;
-  w.nS = max(s1 - w.s0 + 1, 0);
-  w.nX = min(cx + 2, g.nx - 1) - w.x0 + 1;
-  w.nY = min(cy + 2, g.ny - 1) - w.y0 + 1;
-  w.nZ = (D == 3) ? (min(cz + 2, g.nz - 1) - w.z0 + 1) : 1;
-  w.total = w.nS * w.nZ * w.nY * w.nX;
+  int s0 = (int)fmax(floor(((double)tlo - et - g.ot) / g.ct) - 1.0, (double)s_min);
+  int s1 = (int)fmin(floor(((double)thi + et - g.ot) / g.ct) + 1.0, (double)(g.nt - 1));
+  // shrink to the slabs in reach: one lane per slab (independent loads), ballot (callers are
+  // whole waves with uniform arguments)
+  const int lane = threadIdx.x & 63;
+  int lo = -1, hi = -1;
+  for (int c = s0; c <= s1; c += 64) {
+    const bool ok = (c + lane <= s1) && slab_in_reach(slab_t, c + lane, tlo, thi, g.epst);
+    const uint64_t m = __ballot(ok);
+    if (m) {
+      if (lo < 0) lo = c + __ffsll((unsigned long long)m) - 1;
+      hi = c + 63 - __clzll((long long)m);
+    }
+  }
+  if (lo < 0) {
+    s0 = 0;
+    s1 = -1;
+  } else {
+    s0 = lo;
+    s1 = hi;
+  }
+  w.s0 = s0;
+  w.nS = max(s1 - s0 + 1, 0);
+  w.x0 = cx - 2;
+  w.y0 = cy - 2;
+  w.z0 = (D == 3) ? cz - 2 : 0;
+  w.total = w.nS * PER;
   return w;
 }
 
@@ -613,21 +642,25 @@ __device__ __forceinline__ void decode_key(int64_t key, const Geom& g, int& cx, 
   cz = (D == 3) ? (int)(r % g.nz) : 0;
 }
 
-// q-th cell of the window; -1 when its slab holds nothing within reach of [tlo, thi]
+// q-th cell of the window; -1 when outside the grid or its slab holds nothing within reach
+template <int D>
 __device__ __forceinline__ int64_t window_cell(const Window& w, int q, const Geom& g,
                                                const float2* __restrict__ slab_t, float tlo,
                                                float thi) {
-  const int xx = q % w.nX;
-  q /= w.nX;
-  const int yy = q % w.nY;
-  q /= w.nY;
-  const int zz = q % w.nZ;
-  const int ss = w.s0 + q / w.nZ;
-  const float2 sr = slab_t[ss];
-  if (sr.x > sr.y) return -1;  // empty slab
-  const float gap = (tlo > sr.y) ? (tlo - sr.y) : ((thi < sr.x) ? (sr.x - thi) : 0.f);
-  if (!(gap <= g.epst)) return -1;
-  return (((int64_t)ss * g.nz + (w.z0 + zz)) * g.ny + (w.y0 + yy)) * g.nx + (w.x0 + xx);
+  constexpr int PER = (D == 3) ? 125 : 25;
+  const int ss = q / PER;
+  int r = q - ss * PER;
+  int zz = 0;
+  if (D == 3) {
+    zz = r / 25;
+    r -= zz * 25;
+  }
+  const int yy = r / 5, xx = r - yy * 5;
+  const int x = w.x0 + xx, y = w.y0 + yy, z = w.z0 + zz;
+  if (x < 0 || x >= g.nx || y < 0 || y >= g.ny || (D == 3 && (z < 0 || z >= g.nz))) return -1;
+  const int sl = w.s0 + ss;
+  if (!slab_in_reach(slab_t, sl, tlo, thi, g.epst)) return -1;
+  return (((int64_t)sl * g.nz + z) * g.ny + y) * g.nx + x;
 }
 
 __device__ __forceinline__ float4 shfl_f4(const float4& v, int l) {
@@ -690,13 +723,13 @@ __global__ __launch_bounds__(kBlock) void k_core_slow(const float4* __restrict__
     const float4 p = pts[s];
     int cx, cy, cz;
     decode_key<D>(key, g, cx, cy, cz);
-    const Window w = make_window<D>(cx, cy, cz, (double)p.w, (double)p.w, g);
+    const Window w = make_window<D>(cx, cy, cz, p.w, p.w, g, slab_t);
     int cnt = 0;
     for (int base = 0; base < w.total && cnt < need; base += 64) {
       const int qq = base + lane;
       int b = 0, e = 0, cls = 0;
       if (qq < w.total) {
-        const int64_t c = window_cell(w, qq, g, slab_t, p.w, p.w);
+        const int64_t c = window_cell<D>(w, qq, g, slab_t, p.w, p.w);
         if (c >= 0) {
           b = cell_start[c];
           e = cell_start[c + 1];
@@ -854,13 +887,15 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
     const float4 A1 = boxA[ca], A2 = boxB[ca];
     int cx, cy, cz;
     decode_key<D>(ca, g, cx, cy, cz);
-    const Window w = make_window<D>(cx, cy, cz, (double)A2.z, (double)A2.w, g);
+    // only cells B > A: slabs from A's own on (slabs are the slowest key dimension)
+    const int sa = (int)((int64_t)ca / ((int64_t)g.nx * g.ny * g.nz));
+    const Window w = make_window<D>(cx, cy, cz, A2.z, A2.w, g, slab_t, sa);
     for (int base = 0; base < w.total; base += 64) {
       const int qq = base + lane;
       int rb = -1, cls = 0;
       int64_t cb = -1;
       if (qq < w.total) {
-        cb = window_cell(w, qq, g, slab_t, A2.z, A2.w);
+        cb = window_cell<D>(w, qq, g, slab_t, A2.z, A2.w);
         if (cb > (int64_t)ca) {
           rb = rep[cb];
           if (rb >= 0 && mutual[cb]) cls = classify_cells<D>(A1, boxA[cb], A2, boxB[cb], g);
@@ -1060,13 +1095,13 @@ __global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts
       const float4 p = pts[s];
       int cx, cy, cz;
       decode_key<D>(key, g, cx, cy, cz);
-      const Window w = make_window<D>(cx, cy, cz, (double)p.w, (double)p.w, g);
+      const Window w = make_window<D>(cx, cy, cz, p.w, p.w, g, slab_t);
       for (int base = 0; base < w.total; base += 64) {
         const int qq = base + lane;
         int b = 0, e = 0, r = -1, cls = 0, mut = 0;
         int64_t mk = INT64_MAX;
         if (qq < w.total) {
-          const int64_t c = window_cell(w, qq, g, slab_t, p.w, p.w);
+          const int64_t c = window_cell<D>(w, qq, g, slab_t, p.w, p.w);
           if (c >= 0) {
             b = cell_start[c];
             e = cell_start[c + 1];

@@ -9,9 +9,9 @@
 //                    elements, halving split above), chunks accumulated sequentially, then a
 //                    float32 division by k.
 // Segments: a stable radix sort of (label+1, index) keeps each label's points in index order, so
-// every (label, frame) run is contiguous and ordered.  One wave per run: lanes load 64 points at a
-// time (coalesced), the order-preserving float32 chain reads them back lane by lane from
-// registers (v_readlane), so a run of k points costs ~k dependent adds, not k memory latencies.
+// every (label, frame) run is contiguous and ordered.  Two waves per run (x, y): the
+// order-preserving float32 chain is fed from LDS, so a run of k points costs ~k dependent adds
+// (~4.4 cycles each), not k memory latencies.
 // Noise (key 0) sorts first in index order, so each frame's first noise point is the head of its
 // frame within the noise run (no atomics).
 #include <climits>
@@ -127,11 +127,83 @@ __global__ void k_gather_runs(const uint32_t* __restrict__ sv, int64_t n,
   }
 }
 
-__device__ __forceinline__ float lane_f(float v, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+// Order-preserving float32 sum of g[b..e) (np.add.reduce from the first element), computed by
+// one wave: lanes stage 1,024-element chunks in the wave's LDS slice (the next chunk's loads in
+// flight meanwhile) and the wave-uniform chain consumes broadcast 16-byte LDS reads issued a batch
+// ahead.  The dependent v_add_f32 (~4.4 cycles on gfx950, tools/microbench/chain.hip) is the
+// floor; a packed x/y add is no faster (8.5 cycles), so x and y run on separate waves.
+// With gi != nullptr the same chunks also load the intensities (prefetched with the coordinate),
+// accumulated per lane into isum / small_int for the mean-intensity fast path.
+__device__ __forceinline__ float seq_sum(const float* __restrict__ g, int b, int e, int lane,
+                                         float* __restrict__ sb, const float* __restrict__ gi,
+                                         int64_t& isum, bool& small_int) {
+  constexpr int kPre = 16, kChunk = 64 * kPre, V = 8;
+  float pre[kPre], pin[kPre];
+  auto load_chunk = [&](int c0) {
+#pragma unroll
+    for (int t = 0; t < kPre; ++t) {
+      const int idx = c0 + t * 64 + lane;
+      pre[t] = (idx < e) ? g[idx] : 0.f;
+      pin[t] = (gi && idx < e) ? gi[idx] : 0.f;
+    }
+  };
+  float acc = 0.f;
+  load_chunk(b);
+  for (int c0 = b; c0 < e; c0 += kChunk) {
+#pragma unroll
+    for (int t = 0; t < kPre; ++t) {
+      sb[t * 64 + lane] = pre[t];
+      const float vi = pin[t];
+      small_int = small_int && (vi >= 0.f && vi == floorf(vi) && vi < 16777216.f);
+      isum += (int64_t)vi;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (c0 + kChunk < e) load_chunk(c0 + kChunk);
+    const int m = (e - c0 < kChunk) ? (e - c0) : kChunk;
+    int i = 0;
+    if (c0 == b) {  // start from the first element, then reach a 4-aligned position
+      acc = sb[0];
+      for (i = 1; i < 4 && i < m; ++i) acc = acc + sb[i];
+    }
+    const float4* sb4 = reinterpret_cast<const float4*>(sb);
+    if (i + 8 * V <= m) {
+      float4 cur[V], nxt[V];
+#pragma unroll
+      for (int u = 0; u < V; ++u) cur[u] = sb4[i / 4 + u];
+      for (; i + 8 * V <= m; i += 4 * V) {
+#pragma unroll
+        for (int u = 0; u < V; ++u) nxt[u] = sb4[i / 4 + V + u];
+#pragma unroll
+        for (int u = 0; u < V; ++u) {
+          acc = acc + cur[u].x;
+          acc = acc + cur[u].y;
+          acc = acc + cur[u].z;
+          acc = acc + cur[u].w;
+        }
+#pragma unroll
+        for (int u = 0; u < V; ++u) cur[u] = nxt[u];
+      }
+#pragma unroll
+      for (int u = 0; u < V; ++u) {
+        acc = acc + cur[u].x;
+        acc = acc + cur[u].y;
+        acc = acc + cur[u].z;
+        acc = acc + cur[u].w;
+      }
+      i += 4 * V;
+    }
+    for (; i < m; ++i) acc = acc + sb[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  return acc;
 }
 
-// One wave per (frame, label) run: sequential float32 sums in index order (np.mean axis 0).
+// Two waves per (frame, label) run: wave 0 sums x (np.mean axis 0, sequential float32 in index
+// order) and the intensities, wave 1 sums y; they run on different SIMDs.
 // Mean intensity: when every intensity is a non-negative integer and the total stays below 2^24,
 // every summation order is exact (integer lane sums), which equals numpy's pairwise result;
 // otherwise numpy's chunked pairwise sum is evaluated by lane 0.
@@ -142,42 +214,30 @@ __global__ __launch_bounds__(kBlock) void k_summarize(
     const int32_t* __restrict__ pf, int32_t* __restrict__ o_frame, int32_t* __restrict__ o_label,
     int64_t* __restrict__ o_count, int64_t* __restrict__ o_first, float* __restrict__ o_cx,
     float* __restrict__ o_cy, float* __restrict__ o_mi) {
+  __shared__ float s_buf[kBlock / 64][1024];
   const int lane = threadIdx.x & 63;
   const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
   const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
-  for (int64_t s = w0; s < n_seg; s += nw) {
-    const int64_t b = seg_start[s];
-    const int64_t e = (s + 1 < n_seg) ? seg_start[s + 1] : n;
-    const int64_t k = e - b;
-    float sx = gx[b], sy = gy[b];  // numpy's reduction starts from the first row
+  for (int64_t w = w0; w < 2 * n_seg; w += nw) {
+    const int su = __builtin_amdgcn_readfirstlane((int)(w >> 1));
+    const int comp = __builtin_amdgcn_readfirstlane((int)(w & 1));
+    const int b = __builtin_amdgcn_readfirstlane((int)seg_start[su]);
+    const int e = __builtin_amdgcn_readfirstlane(
+        (int)((su + 1 < n_seg) ? seg_start[su + 1] : n));
+    const int k = e - b;
+    const float fk = (float)k;
     bool small_int = true;
     int64_t isum = 0;
-    for (int64_t j0 = b; j0 < e; j0 += 64) {
-      const int64_t j = j0 + lane;
-      const bool in = j < e;
-      const float vx = in ? gx[j] : 0.f, vy = in ? gy[j] : 0.f, vi = in ? gi[j] : 0.f;
-      small_int = small_int && (!in || (vi >= 0.f && vi == floorf(vi) && vi < 16777216.f));
-      isum += in ? (int64_t)vi : 0;
-      const int first = (j0 == b) ? 1 : 0;
-      const int m = (int)((e - j0 < 64) ? (e - j0) : 64);
-      if (m == 64 && !first) {
-#pragma unroll
-        for (int l = 0; l < 64; ++l) {
-          sx = sx + lane_f(vx, l);
-          sy = sy + lane_f(vy, l);
-        }
-      } else {
-        for (int l = first; l < m; ++l) {
-          sx = sx + lane_f(vx, l);
-          sy = sy + lane_f(vy, l);
-        }
-      }
+    const float sum = seq_sum(comp ? gy : gx, b, e, lane, s_buf[threadIdx.x / 64],
+                              comp ? nullptr : gi, isum, small_int);
+    if (comp) {
+      if (lane == 0) o_cy[su] = sum / fk;
+      continue;
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) isum += __shfl_xor(isum, off);
     const bool all_int = __all(small_int);
     if (lane == 0) {
-      const float fk = (float)k;
       float mi;
       if (all_int && isum < 16777216) {
         mi = (float)isum / fk;
@@ -190,13 +250,12 @@ __global__ __launch_bounds__(kBlock) void k_summarize(
         mi = tot / fk;
       }
       const uint32_t i0 = sv[b];
-      o_frame[s] = pf[i0];
-      o_label[s] = (int32_t)sk[b] - 1;
-      o_count[s] = k;
-      o_first[s] = i0;
-      o_cx[s] = sx / fk;
-      o_cy[s] = sy / fk;
-      o_mi[s] = mi;
+      o_frame[su] = pf[i0];
+      o_label[su] = (int32_t)sk[b] - 1;
+      o_count[su] = k;
+      o_first[su] = i0;
+      o_cx[su] = sum / fk;
+      o_mi[su] = mi;
     }
   }
 }
@@ -219,8 +278,8 @@ int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
     set_error("rpt_cluster_summaries: bad arguments");
     return RPT_EINVAL;
   }
-  if (n >= (int64_t(1) << 32) - 1) {
-    set_error("rpt_cluster_summaries: n exceeds the u32 index space");
+  if (n >= (int64_t(1) << 31) - 1) {
+    set_error("rpt_cluster_summaries: n exceeds the int32 index space");
     return RPT_ENOTSUP;
   }
   Scratch& sc = scratch();
@@ -272,9 +331,9 @@ int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
   if (n_seg > 0) {
     hipLaunchKernelGGL(k_gather_runs, dim3(g), dim3(kBlock), 0, st, sv, n, x, y, inten, gx, gy,
                        gi);
-    hipLaunchKernelGGL(k_summarize, dim3(grid_for(n_seg, kBlock / 64, 16384)), dim3(kBlock), 0,
-                       st, sk, sv, seg_start, n_seg, n, gx, gy, gi, pf, o_frame, o_label, o_count,
-                       o_first, o_cx, o_cy, o_mi);
+    hipLaunchKernelGGL(k_summarize, dim3(grid_for(2 * n_seg, kBlock / 64, 16384)), dim3(kBlock),
+                       0, st, sk, sv, seg_start, n_seg, n, gx, gy, gi, pf, o_frame, o_label,
+                       o_count, o_first, o_cx, o_cy, o_mi);
     RPT_CHECK_LAUNCH();
   }
   *n_seg_host = n_seg;

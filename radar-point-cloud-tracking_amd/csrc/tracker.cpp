@@ -40,7 +40,13 @@ struct PySetEmu {
   };
   std::vector<Entry> table;
   size_t mask = 7, fill = 0, used = 0;
+  std::vector<Entry> spare;
   PySetEmu() : table(8, Entry{0, 0, false}) {}
+  void reset() {
+    table.assign(8, Entry{0, 0, false});
+    mask = 7;
+    fill = used = 0;
+  }
 
   static int64_t hash_of(int32_t v) { return v == -1 ? -2 : (int64_t)v; }
 
@@ -70,10 +76,10 @@ struct PySetEmu {
   void resize(size_t minused) {
     size_t newsize = 8;
     while (newsize <= minused) newsize <<= 1;
-    std::vector<Entry> nt(newsize, Entry{0, 0, false});
+    spare.assign(newsize, Entry{0, 0, false});
     for (const Entry& e : table)
-      if (e.used) insert_clean(nt, newsize - 1, e.key, e.hash);
-    table.swap(nt);
+      if (e.used) insert_clean(spare, newsize - 1, e.key, e.hash);
+    table.swap(spare);
     mask = newsize - 1;
     fill = used;
   }
@@ -113,7 +119,8 @@ struct PySetEmu {
 }  // namespace
 
 int32_t set_order(const int32_t* keys, int32_t n, int32_t* out) {
-  PySetEmu s;
+  thread_local PySetEmu s;
+  s.reset();
   for (int32_t i = 0; i < n; ++i) s.add(keys[i]);
   int32_t m = 0;
   for (const auto& e : s.table)
@@ -140,7 +147,7 @@ int32_t order_clusters(int32_t n_frames, int64_t n_seg, const int32_t* seg_frame
   for (int64_t s = 0; s < n_seg; ++s) byf[cur[seg_frame[s]]++] = s;
   std::vector<std::pair<int64_t, int32_t>> occ;  // (first index, label)
   std::vector<int32_t> keys, ord;
-  std::vector<int64_t> lab2seg;
+  std::vector<std::pair<int32_t, int64_t>> l2s;
   for (int32_t f = 0; f < n_frames; ++f) {
     const int64_t b = cnt[f], e = cnt[f + 1];
     occ.clear();
@@ -152,8 +159,7 @@ int32_t order_clusters(int32_t n_frames, int64_t n_seg, const int32_t* seg_frame
     ord.resize(occ.size());
     const int32_t m = set_order(keys.data(), (int32_t)keys.size(), ord.data());
     // label -> segment (labels are unique within a frame)
-    std::vector<std::pair<int32_t, int64_t>> l2s;
-    l2s.reserve(e - b);
+    l2s.clear();
     for (int64_t q = b; q < e; ++q) l2s.emplace_back(seg_label[byf[q]], byf[q]);
     std::sort(l2s.begin(), l2s.end());
     for (int32_t q = 0; q < m; ++q) {
@@ -165,110 +171,161 @@ int32_t order_clusters(int32_t n_frames, int64_t n_seg, const int32_t* seg_frame
 }
 
 // ------------------------------------------------------------------ scipy LSAP
-namespace {
+// Rectangular LSAP exactly as scipy 1.15 (_lsap.c, Crouse 2016): shortest augmenting path per
+// row, remaining columns scanned from a reversed list, ties on the minimum prefer an unassigned
+// column, tall matrices solved transposed.  Scratch is kept across calls (one solver per tracker).
+struct Lsap {
+  std::vector<double> u, v, spc, tmp;
+  std::vector<int64_t> path, col4row, row4col, remaining, idx, sr_list, sc_list;
 
-int64_t augmenting_path(int64_t nc, const double* cost, std::vector<double>& u,
-                        std::vector<double>& v, std::vector<int64_t>& path,
-                        std::vector<int64_t>& row4col, std::vector<double>& spc, int64_t i,
-                        std::vector<char>& SR, std::vector<char>& SC,
-                        std::vector<int64_t>& remaining, double* p_min) {
-  double minVal = 0;
-  int64_t num_remaining = nc;
-  for (int64_t it = 0; it < nc; ++it) remaining[it] = nc - it - 1;
-  std::fill(SR.begin(), SR.end(), 0);
-  std::fill(SC.begin(), SC.end(), 0);
-  std::fill(spc.begin(), spc.end(), std::numeric_limits<double>::infinity());
-  int64_t sink = -1;
-  while (sink == -1) {
-    int64_t index = -1;
-    double lowest = std::numeric_limits<double>::infinity();
-    SR[i] = 1;
-    for (int64_t it = 0; it < num_remaining; ++it) {
-      const int64_t j = remaining[it];
-      const double r = minVal + cost[i * nc + j] - u[i] - v[j];
-      if (r < spc[j]) {
-        path[j] = i;
-        spc[j] = r;
+  // One shortest augmenting path from row i (scipy's augmenting_path).  The rows / columns it
+  // visits are recorded in sr_list / sc_list (scipy's SR / SC flags) so that the dual updates
+  // touch only those; spc is (re)initialised by the first scan, which visits every column.
+  int64_t augmenting_path(int64_t nc, const double* cost, int64_t i, double* p_min) {
+    double minVal = 0;
+    int64_t num_remaining = nc;
+    int64_t* rem = remaining.data();
+    double* sp = spc.data();
+    int64_t* pa = path.data();
+    const int64_t* r4c = row4col.data();
+    const double* vv = v.data();
+    for (int64_t it = 0; it < nc; ++it) rem[it] = nc - it - 1;
+    sr_list.clear();
+    sc_list.clear();
+    int64_t sink = -1;
+    bool first = true;
+    while (sink == -1) {
+      int64_t index = -1;
+      double lowest = std::numeric_limits<double>::infinity();
+      sr_list.push_back(i);
+      const double* row = cost + i * nc;
+      const double ui = u[i];
+      if (first) {
+        // First scan: every spc[j] is inf (the test r < spc[j] always passes) and the scan order
+        // is j = nc-1 .. 0, so it runs as contiguous (vectorisable) loops.  The sequential rule
+        // "strictly lower, or equal and the column unassigned" selects, among the columns at the
+        // minimum, the last unassigned one in scan order after the first one, else the first:
+        // with the order descending in j, that is the smallest unassigned j below the largest
+        // minimum j, else the largest minimum j.
+        const double z = minVal;  // 0.0; kept in the sum for identical rounding of -0.0
+        double mn = std::numeric_limits<double>::infinity();
+        for (int64_t j = 0; j < nc; ++j) {
+          const double r = z + row[j] - ui - vv[j];
+          sp[j] = r;
+          pa[j] = i;
+          mn = r < mn ? r : mn;
+        }
+        int64_t jmax = -1;
+        for (int64_t j = nc - 1; j >= 0; --j)
+          if (sp[j] == mn) {
+            jmax = j;
+            break;
+          }
+        int64_t jsel = jmax;
+        for (int64_t j = 0; j < jmax; ++j)
+          if (sp[j] == mn && r4c[j] == -1) {
+            jsel = j;
+            break;
+          }
+        lowest = mn;
+        index = (jmax < 0) ? -1 : nc - 1 - jsel;
+        if (mn == std::numeric_limits<double>::infinity()) index = -1;
+        first = false;
+      } else {
+        for (int64_t it = 0; it < num_remaining; ++it) {
+          const int64_t j = rem[it];
+          const double r = minVal + row[j] - ui - vv[j];
+          const bool upd = r < sp[j];
+          pa[j] = upd ? i : pa[j];
+          const double sj = upd ? r : sp[j];
+          sp[j] = sj;
+          const bool better = (sj < lowest) | ((sj == lowest) & (r4c[j] == -1));
+          lowest = better ? sj : lowest;
+          index = better ? it : index;
+        }
       }
-      if (spc[j] < lowest || (spc[j] == lowest && row4col[j] == -1)) {
-        lowest = spc[j];
-        index = it;
+      minVal = lowest;
+      if (minVal == std::numeric_limits<double>::infinity()) return -1;
+      const int64_t j = rem[index];
+      if (r4c[j] == -1)
+        sink = j;
+      else
+        i = r4c[j];
+      sc_list.push_back(j);
+      rem[index] = rem[--num_remaining];
+    }
+    *p_min = minVal;
+    return sink;
+  }
+
+  int32_t solve(const double* cost_in, int32_t nr_in, int32_t nc_in, int64_t* a, int64_t* b) {
+    int64_t nr = nr_in, nc = nc_in;
+    if (nr == 0 || nc == 0) return RPT_OK;
+    const bool transpose = nc < nr;
+    const double* cost = cost_in;
+    if (transpose) {
+      tmp.resize(nr * nc);
+      for (int64_t i = 0; i < nr; ++i)
+        for (int64_t j = 0; j < nc; ++j) tmp[j * nr + i] = cost_in[i * nc + j];
+      std::swap(nr, nc);
+      cost = tmp.data();
+    }
+    for (int64_t i = 0; i < nr * nc; ++i) {
+      if (cost[i] != cost[i] || cost[i] == -std::numeric_limits<double>::infinity()) {
+        set_error("matrix contains invalid numeric entries");
+        return RPT_EINVAL;
       }
     }
-    minVal = lowest;
-    if (minVal == std::numeric_limits<double>::infinity()) return -1;
-    const int64_t j = remaining[index];
-    if (row4col[j] == -1)
-      sink = j;
-    else
-      i = row4col[j];
-    SC[j] = 1;
-    remaining[index] = remaining[--num_remaining];
+    u.assign(nr, 0.0);
+    v.assign(nc, 0.0);
+    spc.resize(nc);
+    path.assign(nc, -1);
+    col4row.assign(nr, -1);
+    row4col.assign(nc, -1);
+    remaining.resize(nc);
+    for (int64_t cur = 0; cur < nr; ++cur) {
+      double minVal;
+      const int64_t sink = augmenting_path(nc, cost, cur, &minVal);
+      if (sink < 0) {
+        set_error("cost matrix is infeasible");
+        return RPT_EINVAL;
+      }
+      // scipy updates u over i in SR (ascending i) and v over j in SC; each entry is updated
+      // independently, so the visiting order does not change any value
+      u[cur] += minVal;
+      for (const int64_t i : sr_list)
+        if (i != cur) u[i] += minVal - spc[col4row[i]];
+      for (const int64_t j : sc_list) v[j] -= minVal - spc[j];
+      int64_t j = sink;
+      while (true) {
+        const int64_t i = path[j];
+        row4col[j] = i;
+        std::swap(col4row[i], j);
+        if (i == cur) break;
+      }
+    }
+    if (transpose) {
+      idx.resize(nr);
+      std::iota(idx.begin(), idx.end(), 0);
+      std::sort(idx.begin(), idx.end(),
+                [&](int64_t p, int64_t q) { return col4row[p] < col4row[q]; });
+      for (int64_t k = 0; k < nr; ++k) {
+        a[k] = col4row[idx[k]];
+        b[k] = idx[k];
+      }
+    } else {
+      for (int64_t k = 0; k < nr; ++k) {
+        a[k] = k;
+        b[k] = col4row[k];
+      }
+    }
+    return RPT_OK;
   }
-  *p_min = minVal;
-  return sink;
-}
-
-}  // namespace
+};
 
 int32_t lsap(const double* cost_in, int32_t nr_in, int32_t nc_in, int64_t* a, int64_t* b) {
-  int64_t nr = nr_in, nc = nc_in;
-  if (nr == 0 || nc == 0) return RPT_OK;
-  const bool transpose = nc < nr;
-  std::vector<double> tmp;
-  const double* cost = cost_in;
-  if (transpose) {
-    tmp.resize(nr * nc);
-    for (int64_t i = 0; i < nr; ++i)
-      for (int64_t j = 0; j < nc; ++j) tmp[j * nr + i] = cost_in[i * nc + j];
-    std::swap(nr, nc);
-    cost = tmp.data();
-  }
-  for (int64_t i = 0; i < nr * nc; ++i) {
-    if (cost[i] != cost[i] || cost[i] == -std::numeric_limits<double>::infinity()) {
-      set_error("matrix contains invalid numeric entries");
-      return RPT_EINVAL;
-    }
-  }
-  std::vector<double> u(nr, 0), v(nc, 0), spc(nc);
-  std::vector<int64_t> path(nc, -1), col4row(nr, -1), row4col(nc, -1), remaining(nc);
-  std::vector<char> SR(nr), SC(nc);
-  for (int64_t cur = 0; cur < nr; ++cur) {
-    double minVal;
-    const int64_t sink =
-        augmenting_path(nc, cost, u, v, path, row4col, spc, cur, SR, SC, remaining, &minVal);
-    if (sink < 0) {
-      set_error("cost matrix is infeasible");
-      return RPT_EINVAL;
-    }
-    u[cur] += minVal;
-    for (int64_t i = 0; i < nr; ++i)
-      if (SR[i] && i != cur) u[i] += minVal - spc[col4row[i]];
-    for (int64_t j = 0; j < nc; ++j)
-      if (SC[j]) v[j] -= minVal - spc[j];
-    int64_t j = sink;
-    while (true) {
-      const int64_t i = path[j];
-      row4col[j] = i;
-      std::swap(col4row[i], j);
-      if (i == cur) break;
-    }
-  }
-  if (transpose) {
-    std::vector<int64_t> idx(nr);
-    std::iota(idx.begin(), idx.end(), 0);
-    std::sort(idx.begin(), idx.end(), [&](int64_t p, int64_t q) { return col4row[p] < col4row[q]; });
-    for (int64_t k = 0; k < nr; ++k) {
-      a[k] = col4row[idx[k]];
-      b[k] = idx[k];
-    }
-  } else {
-    for (int64_t k = 0; k < nr; ++k) {
-      a[k] = k;
-      b[k] = col4row[k];
-    }
-  }
-  return RPT_OK;
+  thread_local Lsap solver;
+  return solver.solve(cost_in, nr_in, nc_in, a, b);
 }
 
 // ------------------------------------------------------------------ tracker
@@ -300,6 +357,50 @@ inline double f64_norm(double x, double y) {  // np.linalg.norm float64: ddot wi
   return std::sqrt(std::fma(y, y, x * x));
 }
 
+// Cost matrix of one frame, [k clusters][m objects]: per object the prediction in the dtype numpy
+// uses (float64 while its velocity window holds the float64 zero, float32 after), cost =
+// np.linalg.norm of the difference.  Both norms are evaluated for every entry and selected, so
+// the loop vectorises; the float64 norm's fused multiply-add must be the hardware instruction
+// for speed (libm's software fma gives the same, correctly rounded, result), hence one build for
+// AVX2+FMA hosts, dispatched at run time, and a baseline build.
+#define RPT_FILL_COSTS_BODY                                                      \
+  for (int32_t i = 0; i < k; ++i) {                                              \
+    const float fx = cx[i], fy = cy[i];                                          \
+    const double dxs = (double)fx, dys = (double)fy;                             \
+    double* row = cost + (size_t)i * m;                                          \
+    for (int32_t j = 0; j < m; ++j) {                                            \
+      const double dx = dxs - p64x[j], dy = dys - p64y[j];                       \
+      row[j] = __builtin_sqrt(__builtin_fma(dy, dy, dx * dx));                   \
+    }                                                                            \
+    for (int32_t j = 0; j < m; ++j) {                                            \
+      const float ex = fx - p32x[j], ey = fy - p32y[j];                          \
+      const float exx = ex * ex, eyy = ey * ey;                                  \
+      c32[j] = __builtin_sqrtf(exx + eyy);                                       \
+    }                                                                            \
+    for (int32_t j = 0; j < m; ++j) row[j] = is64[j] ? row[j] : (double)c32[j];  \
+  }
+
+__attribute__((target("avx2,fma"))) void fill_costs_v3(
+    int32_t k, int32_t m, const float* __restrict__ cx, const float* __restrict__ cy,
+    const uint8_t* __restrict__ is64, const double* __restrict__ p64x,
+    const double* __restrict__ p64y, const float* __restrict__ p32x,
+    const float* __restrict__ p32y, float* __restrict__ c32, double* __restrict__ cost) {
+  RPT_FILL_COSTS_BODY
+}
+void fill_costs_base(int32_t k, int32_t m, const float* __restrict__ cx,
+                     const float* __restrict__ cy, const uint8_t* __restrict__ is64,
+                     const double* __restrict__ p64x, const double* __restrict__ p64y,
+                     const float* __restrict__ p32x, const float* __restrict__ p32y,
+                     float* __restrict__ c32, double* __restrict__ cost) {
+  RPT_FILL_COSTS_BODY
+}
+#undef RPT_FILL_COSTS_BODY
+
+bool host_has_fma() {
+  static const bool v = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma");
+  return v;
+}
+
 }  // namespace
 
 struct Tracker {
@@ -307,10 +408,15 @@ struct Tracker {
   std::vector<Object> objs;  // insertion (= id) order, like the reference dict
   int64_t next_id = 1;
   int64_t current = 0;
-  // scratch
+  // scratch (kept across frames)
   std::vector<double> cost;
   std::vector<int64_t> ra, ca;
   std::vector<int> live;
+  std::vector<char> assigned;
+  std::vector<uint8_t> is64;
+  std::vector<double> p64x, p64y;
+  std::vector<float> p32x, p32y, c32;
+  Lsap solver;
 
   static void color_of(int64_t oid, int* rgb) {  // _generate_color :666-688 (float64)
     const double hue = std::fmod((double)oid * 0.618033988749895, 1.0);
@@ -434,12 +540,14 @@ struct Tracker {
     return (double)f32_norm(cx - px, cy - py);
   }
 
-  void cleanup() {
-    std::vector<Object> keep;
-    keep.reserve(objs.size());
-    for (auto& o : objs)
-      if (!(current - o.last_seen > p.max_missed_frames)) keep.push_back(std::move(o));
-    objs.swap(keep);
+  void cleanup() {  // _cleanup_lost_objects: in place, order kept (dict deletion)
+    size_t w = 0;
+    for (size_t r = 0; r < objs.size(); ++r) {
+      if (current - objs[r].last_seen > p.max_missed_frames) continue;
+      if (w != r) objs[w] = std::move(objs[r]);
+      ++w;
+    }
+    objs.erase(objs.begin() + w, objs.end());
   }
 
   int32_t update(int64_t fid, int32_t k, const float* cx, const float* cy, const int64_t* cfid) {
@@ -460,18 +568,31 @@ struct Tracker {
       return (int32_t)objs.size();
     }
     const int32_t m = (int32_t)live.size();
-    cost.assign((size_t)k * m, 0.0);
+    cost.resize((size_t)k * m);
+    is64.resize(m);
+    p64x.resize(m);
+    p64y.resize(m);
+    p32x.resize(m);
+    p32y.resize(m);
+    c32.resize(m);
     for (int32_t j = 0; j < m; ++j) {
       const Object& o = objs[live[j]];
       const Pred q = predict(o, fid - o.last_seen);  // depends on the object only
-      for (int32_t i = 0; i < k; ++i) cost[(size_t)i * m + j] = cost_pred(q, cx[i], cy[i]);
+      is64[j] = q.f64 ? 1 : 0;
+      p64x[j] = q.x;
+      p64y[j] = q.y;
+      p32x[j] = (float)q.x;
+      p32y[j] = (float)q.y;
     }
+    (host_has_fma() ? fill_costs_v3 : fill_costs_base)(k, m, cx, cy, is64.data(), p64x.data(),
+                                                         p64y.data(), p32x.data(), p32y.data(),
+                                                         c32.data(), cost.data());
     const int32_t np_ = std::min(k, m);
-    ra.assign(np_, 0);
-    ca.assign(np_, 0);
-    const int32_t ls = lsap(cost.data(), k, m, ra.data(), ca.data());
+    ra.resize(np_);
+    ca.resize(np_);
+    const int32_t ls = solver.solve(cost.data(), k, m, ra.data(), ca.data());
     if (ls != RPT_OK) return -ls;  // negative = error (counts are >= 0)
-    std::vector<char> assigned(k, 0);
+    assigned.assign(k, 0);
     for (int32_t q = 0; q < np_; ++q) {
       const int64_t i = ra[q], j = ca[q];
       if (cost[(size_t)i * m + j] <= p.max_association_distance) {

@@ -26,6 +26,7 @@ COMMON_FLAGS = [
     "-std=c++17",
     "-fPIC",
     "-ffp-contract=off",
+    "-fno-math-errno",
     f"--offload-arch={ARCH}",
     "-Wall",
     "-Wno-unused-function",

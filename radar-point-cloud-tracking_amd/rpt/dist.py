@@ -24,6 +24,7 @@ so the ranks cooperate; the result is identical to a single-device run:
 from __future__ import annotations
 
 import time
+from concurrent.futures import Future, ThreadPoolExecutor
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -167,13 +168,26 @@ class ShardResult:
     seg: Optional[Dict[str, np.ndarray]] = None  # rank 0: all segments, global frame slots
     built_global: Optional[np.ndarray] = None
     stage_ms: Dict[str, float] = field(default_factory=dict)
+    _pending: Optional[Future] = None
+
+    def finish(self) -> "ShardResult":
+        """Wait for rank 0's host stage when it runs asynchronously (async_host=True)."""
+        if self._pending is not None:
+            self.frame_order_offsets, self.frame_order, self.tracker, ms = self._pending.result()
+            if self.stage_ms:
+                self.stage_ms["tracker"] = ms
+            self._pending = None
+        return self
 
 
 class ShardedStackPipeline:
     """The path over a global stack whose frames are split across ranks (see module doc)."""
 
     def __init__(self, ops, comm: Comm, gains: Sequence[int], rows: int, bins: int,
-                 params: PathParams = None, timing: bool = False):
+                 params: PathParams = None, timing: bool = False, async_host: bool = False):
+        """async_host: rank 0's host stage (cluster order + tracker over the whole stack) runs on
+        one worker thread while the ranks go on to the next run; ShardResult.finish() waits."""
+        self._host = ThreadPoolExecutor(max_workers=1) if async_host else None
         self.ops = ops
         self.comm = comm
         self.gains = [int(g) for g in gains]
@@ -320,10 +334,18 @@ class ShardedStackPipeline:
             all_noise = np.concatenate([a.cpu().numpy() for a in g_noise]).astype(np.int64)
             built = np.concatenate([a.cpu().numpy() for a in g_built]).astype(np.int64)
             n_frames = F * W
-            fo_, order, trk = order_and_track(n_frames, built, all_seg, all_noise, p)
-            res.tracker, res.frame_order_offsets, res.frame_order = trk, fo_, order
+
+            def host_stage():
+                t0 = time.perf_counter()
+                fo_, order, trk = order_and_track(n_frames, built, all_seg, all_noise, p)
+                return fo_, order, trk, (time.perf_counter() - t0) * 1e3
+
             res.seg, res.built_global = all_seg, built
             res.n_segments = len(all_seg["frame"])
+            if self._host is not None:
+                res._pending = self._host.submit(host_stage)
+            else:
+                res.frame_order_offsets, res.frame_order, res.tracker, _ = host_stage()
         mark("tracker")
         if self.timing:
             for (a, ta), (b, tb) in zip(marks[:-1], marks[1:]):

@@ -14,6 +14,7 @@ the stream.  Host syncs per run: file offsets, grid bounds (x2), kept count, seg
 from __future__ import annotations
 
 import time
+from concurrent.futures import Future, ThreadPoolExecutor
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
 
@@ -49,19 +50,33 @@ class StackResult:
     n_clusters: int
     n_segments: int
     seg: Dict[str, np.ndarray]       # per (frame, label) summaries, host copies
-    frame_order_offsets: np.ndarray  # per built frame: its clusters in reference order
-    frame_order: np.ndarray
-    tracker: NativeTracker
+    frame_order_offsets: Optional[np.ndarray]  # per frame slot: its clusters in reference order
+    frame_order: Optional[np.ndarray]
+    tracker: Optional[NativeTracker]
     labels: Optional[torch.Tensor] = None
     points: Optional[Dict[str, torch.Tensor]] = None
     stage_ms: Dict[str, float] = field(default_factory=dict)
+    _pending: Optional[Future] = None
+
+    def finish(self) -> "StackResult":
+        """Wait for the host stage (cluster order + tracker) when it runs asynchronously."""
+        if self._pending is not None:
+            fo, order, trk, host_ms = self._pending.result()
+            self.frame_order_offsets, self.frame_order, self.tracker = fo, order, trk
+            if self.stage_ms is not None and "polar" in self.stage_ms:
+                self.stage_ms["tracker_host"] = host_ms
+            self._pending = None
+        return self
 
 
 class FrameStackPipeline:
     """Runs the path over echo [n_frames][n_gains][rows][bins] (u8 or f32) in device memory."""
 
     def __init__(self, gains: Sequence[int], rows: int, bins: int, params: PathParams = None,
-                 device=None, timing: bool = False):
+                 device=None, timing: bool = False, async_host: bool = False):
+        """async_host: the host stage (cluster order + tracker, sequential C++) of a run executes
+        on one worker thread while the caller goes on to the next run's device work; results
+        complete in submission order and StackResult.finish() waits for them."""
         self.dev = require_gpu(device)
         self.gains = [int(g) for g in gains]
         if sorted(self.gains) != self.gains:
@@ -70,6 +85,7 @@ class FrameStackPipeline:
         self.p = params or PathParams()
         self.ops = HipOps(self.dev)
         self.timing = timing
+        self._host = ThreadPoolExecutor(max_workers=1) if async_host else None
         self._geo_key = None
         self.last_stats = None
 
@@ -138,22 +154,31 @@ class FrameStackPipeline:
         mark("stdbscan")
         seg, first_noise = ops.summaries(pts, labels, n_clusters)
         mark("summaries")
-        t0 = time.perf_counter()
-        fo, order, trk = order_and_track(F, built, seg, first_noise, p)
-        host_ms = (time.perf_counter() - t0) * 1e3
+
+        def host_stage():
+            t0 = time.perf_counter()
+            fo, order, trk = order_and_track(F, built, seg, first_noise, p)
+            return fo, order, trk, (time.perf_counter() - t0) * 1e3
+
         stage_ms = {}
         if self.timing:
             torch.cuda.synchronize(self.dev)
             for (a, ea), (b, eb) in zip(ev[:-1], ev[1:]):
                 stage_ms[b] = ea.elapsed_time(eb)
-            stage_ms["tracker_host"] = host_ms
             stage_ms.update({"dbscan_grid": sts.ms_grid, "dbscan_core": sts.ms_core,
                              "dbscan_union": sts.ms_union, "dbscan_label": sts.ms_label})
         self.last_stats = sts
         res = StackResult(n_points=N, n_clustered_input=n_in, frame_ids=built,
                           n_land_cells=n_land, n_clusters=n_clusters, n_segments=len(seg["frame"]),
-                          seg=seg, frame_order_offsets=fo, frame_order=order, tracker=trk,
+                          seg=seg, frame_order_offsets=None, frame_order=None, tracker=None,
                           stage_ms=stage_ms)
+        if self._host is not None:
+            res._pending = self._host.submit(host_stage)
+        else:
+            fo, order, trk, host_ms = host_stage()
+            res.frame_order_offsets, res.frame_order, res.tracker = fo, order, trk
+            if self.timing:
+                stage_ms["tracker_host"] = host_ms
         if keep_points:
             res.labels = labels
             res.points = {"x": pts.x, "y": pts.y, "v": pts.v, "gain": pts.g, "frame": pts.pf}

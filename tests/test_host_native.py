@@ -80,6 +80,28 @@ def test_lsap_matches_scipy(i):
     np.testing.assert_array_equal(ca, cb)
 
 
+def test_lsap_tie_stress_matches_scipy():
+    """Tracking-sized rectangular problems with heavy ties, +inf entries and tall shapes: the
+    assignment must equal scipy's exactly (tie-breaking included)."""
+    from rpt.native_tracker import lsap
+
+    rng = np.random.default_rng(7)
+    for k in range(400):
+        nr, nc = int(rng.integers(1, 80)), int(rng.integers(1, 80))
+        c = rng.integers(0, 3 + k % 5, (nr, nc)).astype(np.float64)
+        if k % 3 == 0:
+            c[rng.random((nr, nc)) < 0.2] = np.inf
+        try:
+            ra, ca = linear_sum_assignment(c)
+        except ValueError:
+            with pytest.raises(ValueError):
+                lsap(c)
+            continue
+        rb, cb = lsap(c)
+        np.testing.assert_array_equal(ra, rb)
+        np.testing.assert_array_equal(ca, cb)
+
+
 def test_lsap_invalid():
     from rpt.native_tracker import lsap
 

@@ -12,6 +12,8 @@ timeout -k 10 900 python -m pytest tests -q -m gpu > gpurun_out/gpu_tests.log 2>
 rc=$?; echo "tests rc=$rc" >> gpurun_out/gpu_tests.log; ok $rc || exit $rc
 timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc=$?; echo "bench rc=$rc" >> gpurun_out/bench.err; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --sync-host --no-cpu-baseline > gpurun_out/bench_sync.json 2>> gpurun_out/bench.err
+rc=$?; echo "bench sync rc=$rc" >> gpurun_out/bench.err; [ $rc -eq 0 ] || exit $rc
 export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_$TAG" \
   -o bench -- python "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-timing \
