@@ -336,6 +336,32 @@ __device__ __forceinline__ int64_t wave_min64(int64_t v) {
   return v;
 }
 
+// Per occupied cell, its point range and bounding box in ONE record (32 B in 2-D, 48 B in 3-D), so
+// a candidate cell of a window scan costs one load; empty cells are zero (b == e).
+template <int D>
+struct CellRec;
+template <>
+struct alignas(16) CellRec<2> {
+  int b, e;
+  float x0, x1, y0, y1, t0, t1;
+};
+template <>
+struct alignas(16) CellRec<3> {
+  int b, e;
+  float x0, x1, y0, y1, z0, z1, t0, t1;
+  int pad0, pad1;
+};
+template <int D>
+__device__ __forceinline__ float4 rec_boxA(const CellRec<D>& r) {
+  return make_float4(r.x0, r.x1, r.y0, r.y1);
+}
+__device__ __forceinline__ float4 rec_boxB(const CellRec<2>& r) {
+  return make_float4(r.t0, r.t1, r.t0, r.t1);
+}
+__device__ __forceinline__ float4 rec_boxB(const CellRec<3>& r) {
+  return make_float4(r.z0, r.z1, r.t0, r.t1);
+}
+
 // Per-cell bounding boxes, one wave per occupied cell.  boxA = {xmin, xmax, ymin, ymax},
 // boxB = {zmin, zmax, tmin, tmax}.  mutual[c] = 1 when every pair of points in the cell passes
 // the neighbour test (computed conservatively from the box with the same rounding as the pair
@@ -347,7 +373,8 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ 
                                                     const int32_t* __restrict__ n_occ, Geom g,
                                                     float4* __restrict__ boxA,
                                                     float4* __restrict__ boxB,
-                                                    uint8_t* __restrict__ mutual) {
+                                                    uint8_t* __restrict__ mutual,
+                                                    CellRec<D>* __restrict__ crec) {
   const int lane = threadIdx.x & 63;
   const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
   const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
@@ -377,6 +404,20 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ 
     if (lane == 0) {
       boxA[c] = make_float4(x0, x1, y0, y1);
       boxB[c] = make_float4(z0, z1, t0, t1);
+      CellRec<D> r{};
+      r.b = b;
+      r.e = e;
+      r.x0 = x0;
+      r.x1 = x1;
+      r.y0 = y0;
+      r.y1 = y1;
+      if constexpr (D == 3) {
+        r.z0 = z0;
+        r.z1 = z1;
+      }
+      r.t0 = t0;
+      r.t1 = t1;
+      crec[c] = r;
       const double dx = (double)x1 - (double)x0;
       const double dy = (double)y1 - (double)y0;
       double d2 = dx * dx + dy * dy;
@@ -658,8 +699,9 @@ __device__ __forceinline__ int64_t window_cell(const Window& w, int q, const Geo
   const int yy = r / 5, xx = r - yy * 5;
   const int x = w.x0 + xx, y = w.y0 + yy, z = w.z0 + zz;
   if (x < 0 || x >= g.nx || y < 0 || y >= g.ny || (D == 3 && (z < 0 || z >= g.nz))) return -1;
+  // slabs between the first and last in reach are in reach unless empty (then so are their
+  // cells); the cell box's own time range is checked by classify
   const int sl = w.s0 + ss;
-  if (!slab_in_reach(slab_t, sl, tlo, thi, g.epst)) return -1;
   return (((int64_t)sl * g.nz + z) * g.ny + y) * g.nx + x;
 }
 
@@ -705,9 +747,7 @@ __global__ __launch_bounds__(kBlock) void k_core_fast(const int32_t* __restrict_
 template <int D>
 __global__ __launch_bounds__(kBlock) void k_core_slow(const float4* __restrict__ pts,
                                                      const int32_t* __restrict__ skey, Geom g,
-                                                     const int32_t* __restrict__ cell_start,
-                                                     const float4* __restrict__ boxA,
-                                                     const float4* __restrict__ boxB,
+                                                     const CellRec<D>* __restrict__ crec,
                                                      const float2* __restrict__ slab_t,
                                                      const int32_t* __restrict__ slow,
                                                      const int32_t* __restrict__ n_slow,
@@ -731,9 +771,10 @@ __global__ __launch_bounds__(kBlock) void k_core_slow(const float4* __restrict__
       if (qq < w.total) {
         const int64_t c = window_cell<D>(w, qq, g, slab_t, p.w, p.w);
         if (c >= 0) {
-          b = cell_start[c];
-          e = cell_start[c + 1];
-          if (e > b) cls = classify<D>(p, boxA[c], boxB[c], g);
+          const CellRec<D> cr = crec[c];
+          b = cr.b;
+          e = cr.e;
+          if (e > b) cls = classify<D>(p, rec_boxA<D>(cr), rec_boxB(cr), g);
         }
       }
       cnt += wave_sum(cls == 1 ? e - b : 0);
@@ -866,8 +907,7 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
                                                        const int32_t* __restrict__ cell_start,
                                                        const int32_t* __restrict__ occ,
                                                        const int32_t* __restrict__ n_occ,
-                                                       const float4* __restrict__ boxA,
-                                                       const float4* __restrict__ boxB,
+                                                       const CellRec<D>* __restrict__ crec,
                                                        const float2* __restrict__ slab_t,
                                                        const uint8_t* __restrict__ core,
                                                        const int32_t* __restrict__ rep,
@@ -883,8 +923,9 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
     if ((int64_t)ca >= g.cells) continue;  // the isolated (non-finite time) cell
     const int ra = rep[ca];
     if (ra < 0 || !mutual[ca]) continue;
-    const int ea = cell_start[ca + 1];
-    const float4 A1 = boxA[ca], A2 = boxB[ca];
+    const CellRec<D> ra_rec = crec[ca];
+    const int ea = ra_rec.e;
+    const float4 A1 = rec_boxA<D>(ra_rec), A2 = rec_boxB(ra_rec);
     int cx, cy, cz;
     decode_key<D>(ca, g, cx, cy, cz);
     // only cells B > A: slabs from A's own on (slabs are the slowest key dimension)
@@ -892,13 +933,20 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
     const Window w = make_window<D>(cx, cy, cz, A2.z, A2.w, g, slab_t, sa);
     for (int base = 0; base < w.total; base += 64) {
       const int qq = base + lane;
-      int rb = -1, cls = 0;
+      int rb = -1, cls = 0, ebv = 0;
       int64_t cb = -1;
       if (qq < w.total) {
         cb = window_cell<D>(w, qq, g, slab_t, A2.z, A2.w);
         if (cb > (int64_t)ca) {
-          rb = rep[cb];
-          if (rb >= 0 && mutual[cb]) cls = classify_cells<D>(A1, boxA[cb], A2, boxB[cb], g);
+          const CellRec<D> cr = crec[cb];
+          ebv = cr.e;
+          if (cr.e > cr.b) {
+            cls = classify_cells<D>(A1, rec_boxA<D>(cr), A2, rec_boxB(cr), g);
+            if (cls != 0) {
+              rb = rep[cb];
+              if (rb < 0 || !mutual[cb]) cls = 0;
+            }
+          }
         }
       }
       if (!PARTIAL) {
@@ -911,7 +959,7 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
         const int l = __ffsll((unsigned long long)pm) - 1;
         pm &= pm - 1;
         const int rbl = __shfl(rb, l);
-        const int ebl = cell_start[__shfl((int)cb, l) + 1];
+        const int ebl = __shfl(ebv, l);
         bool hit = false;
         for (int jb0 = rbl; jb0 < ebl && !hit; jb0 += 64) {
           const int jb = jb0 + lane;
@@ -1068,9 +1116,7 @@ __global__ __launch_bounds__(kBlock) void k_label_core(const int32_t* __restrict
 template <int D, bool GLOBAL>
 __global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts,
                                                  const int32_t* __restrict__ skey, Geom g,
-                                                 const int32_t* __restrict__ cell_start,
-                                                 const float4* __restrict__ boxA,
-                                                 const float4* __restrict__ boxB,
+                                                 const CellRec<D>* __restrict__ crec,
                                                  const float2* __restrict__ slab_t,
                                                  const int32_t* __restrict__ ccmin,
                                                  const int64_t* __restrict__ srep,
@@ -1103,13 +1149,18 @@ __global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts
         if (qq < w.total) {
           const int64_t c = window_cell<D>(w, qq, g, slab_t, p.w, p.w);
           if (c >= 0) {
-            b = cell_start[c];
-            e = cell_start[c + 1];
-            r = (e > b) ? rep[c] : -1;
-            if (r >= 0) {
-              cls = classify<D>(p, boxA[c], boxB[c], g);
-              mut = mutual[c];
-              if (mut) mk = keyof(r);
+            const CellRec<D> cr = crec[c];
+            b = cr.b;
+            e = cr.e;
+            if (e > b) cls = classify<D>(p, rec_boxA<D>(cr), rec_boxB(cr), g);
+            if (cls != 0) {
+              r = rep[c];
+              if (r < 0) {
+                cls = 0;
+              } else {
+                mut = mutual[c];
+                if (mut) mk = keyof(r);
+              }
             }
           }
         }
@@ -1253,6 +1304,11 @@ struct DbscanState {
   float2* slab_t = nullptr;
   int32_t *parent = nullptr, *ccmin = nullptr, *cid = nullptr, *nc_list = nullptr;
   int32_t *occ = nullptr, *hpos = nullptr;  // occupied cells (ascending), head-flag scan; n_occ = hpos[n]
+  void* crec = nullptr;                      // CellRec<dim>[C + 1]
+  template <int D>
+  const CellRec<D>* rec() const {
+    return static_cast<const CellRec<D>*>(crec);
+  }
   int64_t* srep = nullptr;
   int64_t* stmp = nullptr;
   Timer tm;
@@ -1362,6 +1418,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   bud.add<int64_t>(n);      // srep (global finalize)
   bud.add<int32_t>(n + 1);  // occ
   bud.add<int32_t>(n + 1);  // hpos
+  bud.add<CellRec<D>>(C1);  // crec
   RPT_TRY(arena.reserve(bud.bytes, st));
   (void)arena.carve_n<Bounds>(1);
   uint32_t* keys = arena.carve_n<uint32_t>(n);
@@ -1387,7 +1444,9 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   srep = arena.carve_n<int64_t>(n);
   occ = arena.carve_n<int32_t>(n + 1);
   hpos = arena.carve_n<int32_t>(n + 1);
-  if (!hpos) {
+  CellRec<D>* cr = arena.carve_n<CellRec<D>>(C1);
+  crec = cr;
+  if (!cr) {
     set_error("internal: scratch carve overflow");
     return RPT_ENOMEM;
   }
@@ -1408,8 +1467,9 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   RPT_TRY(exclusive_scan_i32(hpos, hpos, n + 1, stmp, st));
   hipLaunchKernelGGL(k_occ_list, dim3(gb), dim3(kBlock), 0, st, skey, n, hpos, occ);
   RPT_CHECK_LAUNCH();
+  RPT_HIP(hipMemsetAsync(cr, 0, sizeof(CellRec<D>) * C1, st));
   hipLaunchKernelGGL(k_cell_box<D>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, cell_start,
-                     occ, hpos + n, g, boxA, boxB, mutual);
+                     occ, hpos + n, g, boxA, boxB, mutual, cr);
   RPT_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_slab_range, dim3((unsigned)nt), dim3(kBlock), 0, st, pts, cell_start,
                      (int64_t)(C / nt), (int)nt, slab_t);
@@ -1440,10 +1500,10 @@ int32_t DbscanState::core_pass(hipStream_t st) {
                      mutual, core, slow, n_slow);
   if (dim == 2)
     hipLaunchKernelGGL(k_core_slow<2>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       cell_start, boxA, boxB, slab_t, slow, n_slow, core);
+                       rec<2>(), slab_t, slow, n_slow, core);
   else
     hipLaunchKernelGGL(k_core_slow<3>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       cell_start, boxA, boxB, slab_t, slow, n_slow, core);
+                       rec<3>(), slab_t, slow, n_slow, core);
   RPT_CHECK_LAUNCH();
   tm.mark();
   return RPT_OK;
@@ -1461,19 +1521,19 @@ int32_t DbscanState::union_pass(hipStream_t st) {
                      rep, C);
   if (dim == 2) {
     hipLaunchKernelGGL((k_union_cells<2, false>), dim3(gw), dim3(kBlock), 0, st, pts, g,
-                       cell_start, occ, n_occ, boxA, boxB, slab_t, core, rep, mutual, sorig,
+                       cell_start, occ, n_occ, rec<2>(), slab_t, core, rep, mutual, sorig,
                        parent);
     hipLaunchKernelGGL((k_union_cells<2, true>), dim3(gw), dim3(kBlock), 0, st, pts, g,
-                       cell_start, occ, n_occ, boxA, boxB, slab_t, core, rep, mutual, sorig,
+                       cell_start, occ, n_occ, rec<2>(), slab_t, core, rep, mutual, sorig,
                        parent);
     hipLaunchKernelGGL(k_union<2>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
                        boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
   } else {
     hipLaunchKernelGGL((k_union_cells<3, false>), dim3(gw), dim3(kBlock), 0, st, pts, g,
-                       cell_start, occ, n_occ, boxA, boxB, slab_t, core, rep, mutual, sorig,
+                       cell_start, occ, n_occ, rec<3>(), slab_t, core, rep, mutual, sorig,
                        parent);
     hipLaunchKernelGGL((k_union_cells<3, true>), dim3(gw), dim3(kBlock), 0, st, pts, g,
-                       cell_start, occ, n_occ, boxA, boxB, slab_t, core, rep, mutual, sorig,
+                       cell_start, occ, n_occ, rec<3>(), slab_t, core, rep, mutual, sorig,
                        parent);
     hipLaunchKernelGGL(k_union<3>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
                        boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
@@ -1509,12 +1569,12 @@ int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hi
   hipLaunchKernelGGL(k_label_core, dim3(gb), dim3(kBlock), 0, st, ccmin, n, sorig, cid, labels);
   if (dim == 2)
     hipLaunchKernelGGL((k_label<2, false>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       cell_start, boxA, boxB, slab_t, ccmin, (const int64_t*)nullptr, rep,
+                       rec<2>(), slab_t, ccmin, (const int64_t*)nullptr, rep,
                        mutual, sorig, cid, (const int64_t*)nullptr, (int64_t)0, nc_list,
                        nc_count, labels);
   else
     hipLaunchKernelGGL((k_label<3, false>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       cell_start, boxA, boxB, slab_t, ccmin, (const int64_t*)nullptr, rep,
+                       rec<3>(), slab_t, ccmin, (const int64_t*)nullptr, rep,
                        mutual, sorig, cid, (const int64_t*)nullptr, (int64_t)0, nc_list,
                        nc_count, labels);
   RPT_CHECK_LAUNCH();
@@ -1559,11 +1619,11 @@ int32_t DbscanState::labels_global(const int64_t* rep_orig, const int64_t* reps,
                      labels);
   if (dim == 2)
     hipLaunchKernelGGL((k_label<2, true>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       cell_start, boxA, boxB, slab_t, (const int32_t*)nullptr, srep, rep, mutual,
+                       rec<2>(), slab_t, (const int32_t*)nullptr, srep, rep, mutual,
                        sorig, (const int32_t*)nullptr, reps, nr, nc_list, nc_count, labels);
   else
     hipLaunchKernelGGL((k_label<3, true>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       cell_start, boxA, boxB, slab_t, (const int32_t*)nullptr, srep, rep, mutual,
+                       rec<3>(), slab_t, (const int32_t*)nullptr, srep, rep, mutual,
                        sorig, (const int32_t*)nullptr, reps, nr, nc_list, nc_count, labels);
   RPT_CHECK_LAUNCH();
   return RPT_OK;
