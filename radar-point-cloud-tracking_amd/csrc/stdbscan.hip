@@ -36,6 +36,7 @@
 #include <cfloat>
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 
@@ -300,16 +301,31 @@ __global__ __launch_bounds__(kBlock) void k_cell_runs(const int32_t* __restrict_
 }
 
 // pos = exclusive scan of the head flags: cell of every run head -> occ[pos]
+// (+ the occupancy bitmap: one bit per cell, small enough to stay in L2, so window scans skip
+// empty candidate cells without reading their records)
 __global__ __launch_bounds__(kBlock) void k_occ_list(const int32_t* __restrict__ skey, int64_t n,
                                                     const int32_t* __restrict__ pos,
-                                                    int32_t* __restrict__ occ) {
+                                                    int32_t* __restrict__ occ,
+                                                    uint32_t* __restrict__ occ_bits) {
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
        s += (int64_t)gridDim.x * blockDim.x)
-    if (pos[s + 1] != pos[s]) occ[pos[s]] = skey[s];
+    if (pos[s + 1] != pos[s]) {
+      const int32_t c = skey[s];
+      occ[pos[s]] = c;
+      atomicOr(occ_bits + (c >> 5), 1u << (c & 31));
+    }
+}
+
+__device__ __forceinline__ bool occupied(const uint32_t* __restrict__ bits, int64_t c) {
+  return (bits[c >> 5] >> (c & 31)) & 1u;
 }
 
 // grids of the persistent wave-per-item kernels (item counts live on the device)
-inline int wave_grid(int64_t max_items) { return grid_for(max_items, kBlock / 64, 4096); }
+inline int wave_grid(int64_t max_items) {  // a multiple of 8 blocks (XCD-aware ranges)
+  const int g = grid_for(max_items, kBlock / 64, 4096);
+  return (g + 7) & ~7;
+}
+constexpr int kDefaultUfFlags = 2;
 inline int tile_grid(int64_t n) { return grid_for(n, kBlock * 16, 2048); }
 
 __device__ __forceinline__ float wave_minf(float v) {
@@ -637,7 +653,7 @@ __device__ __forceinline__ bool slab_in_reach(const float2* __restrict__ slab_t,
   return gap <= epst;
 }
 
-template <int D>
+template <int D, bool SHRINK = true>
 __device__ __forceinline__ Window make_window(int cx, int cy, int cz, float tlo, float thi,
                                               const Geom& g, const float2* __restrict__ slab_t,
                                               int s_min = 0) {
@@ -650,7 +666,11 @@ __device__ __forceinline__ Window make_window(int cx, int cy, int cz, float tlo,
   // whole waves with uniform arguments)
   const int lane = threadIdx.x & 63;
   int lo = -1, hi = -1;
-  for (int c = s0; c <= s1; c += 64) {
+  if (!SHRINK) {  // callers that classify every candidate's time range themselves
+    lo = s0;
+    hi = s1;
+  }
+  for (int c = s0; SHRINK && c <= s1; c += 64) {
     const bool ok = (c + lane <= s1) && slab_in_reach(slab_t, c + lane, tlo, thi, g.epst);
     const uint64_t m = __ballot(ok);
     if (m) {
@@ -710,6 +730,8 @@ __device__ __forceinline__ float4 shfl_f4(const float4& v, int l) {
 }
 
 // ---------------------------------------------------------------- K5: core flags
+constexpr int kR = 4;  // candidate cells per lane per super-round of the window scans
+
 // Level 1, one thread per point: a point whose own cell is mutual and holds >= min_samples points
 // is core (all of them are its neighbours) — the bulk of a radar stack.  Every other point is
 // queued for level 2.
@@ -748,6 +770,7 @@ template <int D>
 __global__ __launch_bounds__(kBlock) void k_core_slow(const float4* __restrict__ pts,
                                                      const int32_t* __restrict__ skey, Geom g,
                                                      const CellRec<D>* __restrict__ crec,
+                                                     const uint32_t* __restrict__ occ_bits,
                                                      const float2* __restrict__ slab_t,
                                                      const int32_t* __restrict__ slow,
                                                      const int32_t* __restrict__ n_slow,
@@ -763,30 +786,47 @@ __global__ __launch_bounds__(kBlock) void k_core_slow(const float4* __restrict__
     const float4 p = pts[s];
     int cx, cy, cz;
     decode_key<D>(key, g, cx, cy, cz);
-    const Window w = make_window<D>(cx, cy, cz, p.w, p.w, g, slab_t);
+    const Window w = make_window<D, false>(cx, cy, cz, p.w, p.w, g, slab_t);
     int cnt = 0;
-    for (int base = 0; base < w.total && cnt < need; base += 64) {
-      const int qq = base + lane;
-      int b = 0, e = 0, cls = 0;
-      if (qq < w.total) {
-        const int64_t c = window_cell<D>(w, qq, g, slab_t, p.w, p.w);
-        if (c >= 0) {
-          const CellRec<D> cr = crec[c];
-          b = cr.b;
-          e = cr.e;
-          if (e > b) cls = classify<D>(p, rec_boxA<D>(cr), rec_boxB(cr), g);
+    // super-rounds of kR candidates per lane: every lane's bitmap words, then records, are
+    // loaded together (one dependent level each for up to 64*kR candidates)
+    for (int base = 0; base < w.total && cnt < need; base += 64 * kR) {
+      int64_t c[kR];
+      uint32_t wb[kR];
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        const int qq = base + r * 64 + lane;
+        c[r] = (qq < w.total) ? window_cell<D>(w, qq, g, slab_t, p.w, p.w) : -1;
+      }
+#pragma unroll
+      for (int r = 0; r < kR; ++r) wb[r] = (c[r] >= 0) ? occ_bits[c[r] >> 5] : 0u;
+      int b[kR], e[kR], cls[kR];
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        b[r] = e[r] = cls[r] = 0;
+        if (c[r] >= 0 && ((wb[r] >> (c[r] & 31)) & 1u)) {
+          const CellRec<D> cr = crec[c[r]];
+          b[r] = cr.b;
+          e[r] = cr.e;
+          cls[r] = classify<D>(p, rec_boxA<D>(cr), rec_boxB(cr), g);
         }
       }
-      cnt += wave_sum(cls == 1 ? e - b : 0);
-      uint64_t pm = __ballot(cls == 2);
-      while (pm && cnt < need) {
-        const int l = __ffsll((unsigned long long)pm) - 1;
-        pm &= pm - 1;
-        const int bb = __shfl(b, l), ee = __shfl(e, l);
-        for (int j0 = bb; j0 < ee && cnt < need; j0 += 64) {
-          const int j = j0 + lane;
-          const bool a = (j < ee) && adjacent<D>(p, pts[j], g);
-          cnt += __popcll(__ballot(a));
+      int add = 0;
+#pragma unroll
+      for (int r = 0; r < kR; ++r) add += (cls[r] == 1) ? e[r] - b[r] : 0;
+      cnt += wave_sum(add);
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        uint64_t pm = __ballot(cls[r] == 2);
+        while (pm && cnt < need) {
+          const int l = __ffsll((unsigned long long)pm) - 1;
+          pm &= pm - 1;
+          const int bb = __shfl(b[r], l), ee = __shfl(e[r], l);
+          for (int j0 = bb; j0 < ee && cnt < need; j0 += 64) {
+            const int j = j0 + lane;
+            const bool a = (j < ee) && adjacent<D>(p, pts[j], g);
+            cnt += __popcll(__ballot(a));
+          }
         }
       }
     }
@@ -820,24 +860,21 @@ __device__ __forceinline__ void uf_store(int32_t* p, int v) {
 }
 // Path-halving find.  Parents only ever decrease, so a stale read is an older ancestor and
 // every returned root was a true ancestor at some point (connectivity is never overstated).
-__device__ __forceinline__ int uf_find(int32_t* parent, int x) {
+__device__ __forceinline__ int uf_find(int32_t* parent, int x, bool halve = true) {
   while (true) {
     const int p = uf_load(parent + x);
     if (p == x) return x;
     const int gp = uf_load(parent + p);
     if (gp == p) return p;
-    uf_store(parent + x, gp);
+    if (halve) uf_store(parent + x, gp);
     x = gp;
   }
 }
-// Hook the root with the larger ORIGINAL index under the other (parents always have a smaller
-// original index): every tree's root is the component's minimum original index, which is what
-// the reference numbers clusters by — so no reduction over the component is needed.
 __device__ __forceinline__ void uf_unite(int32_t* parent, const int32_t* __restrict__ sorig,
-                                         int a, int b) {
+                                         int a, int b, bool halve = true) {
   while (true) {
-    a = uf_find(parent, a);
-    b = uf_find(parent, b);
+    a = uf_find(parent, a, halve);
+    b = uf_find(parent, b, halve);
     if (a == b) return;
     if (sorig[a] < sorig[b]) {
       const int tmp = a;
@@ -848,6 +885,24 @@ __device__ __forceinline__ void uf_unite(int32_t* parent, const int32_t* __restr
     if (old == a) return;
     a = old;
   }
+}
+
+// Tuning flags of the union kernels (rpt_set_tuning / RPT_UF_FLAGS): bit 0 = finds inside the
+// union kernels do not path-halve (agent-scope stores drop the line from the XCD's L2; k_compress
+// compresses afterwards); bit 2 = timing experiment only: skip the box-certain unites (labels
+// are then WRONG); bit 1 = XCD-aware item ranges (blockIdx % 8 = XCD under round-robin
+// placement: each XCD unions a contiguous range of cells, so its L2 keeps their parents).
+struct XcdRange {
+  int64_t first, step, end;
+};
+__device__ __forceinline__ XcdRange xcd_items(int64_t n_items, bool remap) {
+  const int64_t wpb = kBlock / 64, wave = threadIdx.x / 64;
+  if (!remap || (gridDim.x & 7)) {
+    return XcdRange{(int64_t)blockIdx.x * wpb + wave, (int64_t)gridDim.x * wpb, n_items};
+  }
+  const int64_t x = blockIdx.x & 7, lb = blockIdx.x >> 3, nbx = gridDim.x >> 3;
+  const int64_t lo = n_items * x / 8, hi = n_items * (x + 1) / 8;
+  return XcdRange{lo + lb * wpb + wave, nbx * wpb, hi};
 }
 
 // Star initialisation: every core point of a mutual cell hangs under the cell's first core point
@@ -908,80 +963,115 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
                                                        const int32_t* __restrict__ occ,
                                                        const int32_t* __restrict__ n_occ,
                                                        const CellRec<D>* __restrict__ crec,
+                                                       const uint32_t* __restrict__ occ_bits,
                                                        const float2* __restrict__ slab_t,
                                                        const uint8_t* __restrict__ core,
                                                        const int32_t* __restrict__ rep,
                                                        const uint8_t* __restrict__ mutual,
                                                        const int32_t* __restrict__ sorig,
-                                                       int32_t* __restrict__ parent) {
+                                                       int32_t* __restrict__ parent,
+                                                       int uf_flags) {
   const int lane = threadIdx.x & 63;
-  const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
-  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
-  const int64_t no = *n_occ;
-  for (int64_t q = w0; q < no; q += nw) {
+  const bool halve = !(uf_flags & 1);
+  const XcdRange xr = xcd_items(*n_occ, (uf_flags & 2) != 0);
+  for (int64_t q = xr.first; q < xr.end; q += xr.step) {
     const int ca = occ[q];
     if ((int64_t)ca >= g.cells) continue;  // the isolated (non-finite time) cell
     const int ra = rep[ca];
-    if (ra < 0 || !mutual[ca]) continue;
+    const uint8_t ma = mutual[ca];
     const CellRec<D> ra_rec = crec[ca];
+    if (ra < 0 || !ma) continue;
     const int ea = ra_rec.e;
     const float4 A1 = rec_boxA<D>(ra_rec), A2 = rec_boxB(ra_rec);
     int cx, cy, cz;
     decode_key<D>(ca, g, cx, cy, cz);
-    // only cells B > A: slabs from A's own on (slabs are the slowest key dimension)
+    // only cells B > A: slabs from A's own on (slabs are the slowest key dimension); the boxes'
+    // time ranges are checked by classify_cells, so the slab window is not shrunk first
     const int sa = (int)((int64_t)ca / ((int64_t)g.nx * g.ny * g.nz));
-    const Window w = make_window<D>(cx, cy, cz, A2.z, A2.w, g, slab_t, sa);
-    for (int base = 0; base < w.total; base += 64) {
-      const int qq = base + lane;
-      int rb = -1, cls = 0, ebv = 0;
-      int64_t cb = -1;
-      if (qq < w.total) {
-        cb = window_cell<D>(w, qq, g, slab_t, A2.z, A2.w);
-        if (cb > (int64_t)ca) {
-          const CellRec<D> cr = crec[cb];
-          ebv = cr.e;
-          if (cr.e > cr.b) {
-            cls = classify_cells<D>(A1, rec_boxA<D>(cr), A2, rec_boxB(cr), g);
-            if (cls != 0) {
-              rb = rep[cb];
-              if (rb < 0 || !mutual[cb]) cls = 0;
-            }
+    const Window w = make_window<D, false>(cx, cy, cz, A2.z, A2.w, g, slab_t, sa);
+    for (int base = 0; base < w.total; base += 64 * kR) {
+      int64_t cb[kR];
+      uint32_t wb[kR];
+#pragma unroll
+      for (int k = 0; k < kR; ++k) {
+        const int qq = base + k * 64 + lane;
+        cb[k] = (qq < w.total) ? window_cell<D>(w, qq, g, slab_t, A2.z, A2.w) : -1;
+        if (cb[k] <= (int64_t)ca) cb[k] = -1;
+      }
+#pragma unroll
+      for (int k = 0; k < kR; ++k) wb[k] = (cb[k] >= 0) ? occ_bits[cb[k] >> 5] : 0u;
+      int rb[kR], cls[kR], ebv[kR];
+#pragma unroll
+      for (int k = 0; k < kR; ++k) {
+        rb[k] = -1;
+        cls[k] = 0;
+        ebv[k] = 0;
+        if (cb[k] >= 0 && ((wb[k] >> (cb[k] & 31)) & 1u)) {
+          const CellRec<D> cr = crec[cb[k]];
+          const int r = rep[cb[k]];
+          const uint8_t m = mutual[cb[k]];
+          ebv[k] = cr.e;
+          if (r >= 0 && m) {
+            rb[k] = r;
+            cls[k] = classify_cells<D>(A1, rec_boxA<D>(cr), A2, rec_boxB(cr), g);
           }
         }
       }
       if (!PARTIAL) {
-        if (cls == 1) uf_unite(parent, sorig, ra, rb);
+        if (uf_flags & 4) continue;  // timing experiment only
+        // neighbours' roots in parallel, then ONE unite per distinct root (dense regions give
+        // a dozen box-certain neighbours that mostly share a root already)
+        const int rA = uf_find(parent, ra, halve);
+#pragma unroll
+        for (int k = 0; k < kR; ++k) {
+          const int rt = (cls[k] == 1) ? uf_find(parent, rb[k], halve) : -1;
+          bool pend = rt >= 0 && rt != rA;
+          bool mine = false;
+          uint64_t pm = __ballot(pend);
+          while (pm) {
+            const int l = __ffsll((unsigned long long)pm) - 1;
+            const int v = __shfl(rt, l);
+            mine = mine || (lane == l);
+            pend = pend && (rt != v);
+            pm = __ballot(pend);
+          }
+          if (mine) uf_unite(parent, sorig, rA, rt, halve);
+        }
         continue;
       }
-      const bool cand = (cls == 2) && uf_find(parent, ra) != uf_find(parent, rb);
-      uint64_t pm = __ballot(cand);
-      while (pm) {
-        const int l = __ffsll((unsigned long long)pm) - 1;
-        pm &= pm - 1;
-        const int rbl = __shfl(rb, l);
-        const int ebl = __shfl(ebv, l);
-        bool hit = false;
-        for (int jb0 = rbl; jb0 < ebl && !hit; jb0 += 64) {
-          const int jb = jb0 + lane;
-          float4 pb = make_float4(0.f, 0.f, 0.f, 0.f);
-          bool cb_ok = false;
-          if (jb < ebl && core[jb]) {
-            pb = pts[jb];
-            cb_ok = classify<D>(pb, A1, A2, g) != 0;
-          }
-          uint64_t bm = __ballot(cb_ok);
-          while (bm && !hit) {
-            const int lb = __ffsll((unsigned long long)bm) - 1;
-            bm &= bm - 1;
-            const float4 pq = shfl_f4(pb, lb);
-            for (int ja0 = ra; ja0 < ea && !hit; ja0 += 64) {
-              const int ja = ja0 + lane;
-              const bool adj = (ja < ea) && core[ja] && adjacent<D>(pq, pts[ja], g);
-              hit = __ballot(adj) != 0;
+#pragma unroll
+      for (int k = 0; k < kR; ++k) {
+        const bool cand =
+            (cls[k] == 2) && uf_find(parent, ra, halve) != uf_find(parent, rb[k], halve);
+        uint64_t pm = __ballot(cand);
+        while (pm) {
+          const int l = __ffsll((unsigned long long)pm) - 1;
+          pm &= pm - 1;
+          const int rbl = __shfl(rb[k], l);
+          const int ebl = __shfl(ebv[k], l);
+          bool hit = false;
+          for (int jb0 = rbl; jb0 < ebl && !hit; jb0 += 64) {
+            const int jb = jb0 + lane;
+            float4 pb = make_float4(0.f, 0.f, 0.f, 0.f);
+            bool cb_ok = false;
+            if (jb < ebl && core[jb]) {
+              pb = pts[jb];
+              cb_ok = classify<D>(pb, A1, A2, g) != 0;
+            }
+            uint64_t bm = __ballot(cb_ok);
+            while (bm && !hit) {
+              const int lb = __ffsll((unsigned long long)bm) - 1;
+              bm &= bm - 1;
+              const float4 pq = shfl_f4(pb, lb);
+              for (int ja0 = ra; ja0 < ea && !hit; ja0 += 64) {
+                const int ja = ja0 + lane;
+                const bool adj = (ja < ea) && core[ja] && adjacent<D>(pq, pts[ja], g);
+                hit = __ballot(adj) != 0;
+              }
             }
           }
+          if (hit && lane == 0) uf_unite(parent, sorig, ra, rbl, halve);
         }
-        if (hit && lane == 0) uf_unite(parent, sorig, ra, rbl);
       }
     }
   }
@@ -1117,6 +1207,7 @@ template <int D, bool GLOBAL>
 __global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts,
                                                  const int32_t* __restrict__ skey, Geom g,
                                                  const CellRec<D>* __restrict__ crec,
+                                                 const uint32_t* __restrict__ occ_bits,
                                                  const float2* __restrict__ slab_t,
                                                  const int32_t* __restrict__ ccmin,
                                                  const int64_t* __restrict__ srep,
@@ -1141,56 +1232,70 @@ __global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts
       const float4 p = pts[s];
       int cx, cy, cz;
       decode_key<D>(key, g, cx, cy, cz);
-      const Window w = make_window<D>(cx, cy, cz, p.w, p.w, g, slab_t);
-      for (int base = 0; base < w.total; base += 64) {
-        const int qq = base + lane;
-        int b = 0, e = 0, r = -1, cls = 0, mut = 0;
-        int64_t mk = INT64_MAX;
-        if (qq < w.total) {
-          const int64_t c = window_cell<D>(w, qq, g, slab_t, p.w, p.w);
-          if (c >= 0) {
-            const CellRec<D> cr = crec[c];
-            b = cr.b;
-            e = cr.e;
-            if (e > b) cls = classify<D>(p, rec_boxA<D>(cr), rec_boxB(cr), g);
-            if (cls != 0) {
-              r = rep[c];
-              if (r < 0) {
-                cls = 0;
-              } else {
-                mut = mutual[c];
-                if (mut) mk = keyof(r);
-              }
-            }
+      const Window w = make_window<D, false>(cx, cy, cz, p.w, p.w, g, slab_t);
+      for (int base = 0; base < w.total; base += 64 * kR) {
+        // super-round: bitmap words, then records + rep + mutual, loaded together per lane
+        int64_t c[kR];
+        uint32_t wb[kR];
+#pragma unroll
+        for (int k = 0; k < kR; ++k) {
+          const int qq = base + k * 64 + lane;
+          c[k] = (qq < w.total) ? window_cell<D>(w, qq, g, slab_t, p.w, p.w) : -1;
+        }
+#pragma unroll
+        for (int k = 0; k < kR; ++k) wb[k] = (c[k] >= 0) ? occ_bits[c[k] >> 5] : 0u;
+        int e[kR], r[kR], cls[kR], mut[kR];
+#pragma unroll
+        for (int k = 0; k < kR; ++k) {
+          e[k] = 0;
+          r[k] = -1;
+          cls[k] = 0;
+          mut[k] = 0;
+          if (c[k] >= 0 && ((wb[k] >> (c[k] & 31)) & 1u)) {
+            const CellRec<D> cr = crec[c[k]];
+            r[k] = rep[c[k]];
+            mut[k] = mutual[c[k]];
+            e[k] = cr.e;
+            cls[k] = (r[k] >= 0) ? classify<D>(p, rec_boxA<D>(cr), rec_boxB(cr), g) : 0;
           }
         }
+        int64_t mk[kR];
+#pragma unroll
+        for (int k = 0; k < kR; ++k) mk[k] = (cls[k] != 0 && mut[k]) ? keyof(r[k]) : INT64_MAX;
         // whole mutual cells in reach: their component key directly
-        best = min(best, wave_min64((cls == 1 && mut) ? mk : INT64_MAX));
-        uint64_t pm = __ballot(cls != 0 && !(cls == 1 && mut) && (!mut || mk < best));
-        while (pm) {
-          const int l = __ffsll((unsigned long long)pm) - 1;
-          pm &= pm - 1;
-          const int rl = __shfl(r, l), el = __shfl(e, l), cl = __shfl(cls, l);
-          if (__shfl(mut, l)) {
-            const int64_t ml = __shfl(mk, l);
-            if (ml >= best) continue;
-            bool hit = false;
-            for (int j0 = rl; j0 < el && !hit; j0 += 64) {
-              const int j = j0 + lane;
-              hit = __ballot((j < el) && keyof(j) >= 0 && adjacent<D>(p, pts[j], g)) != 0;
-            }
-            if (hit) best = ml;
-          } else {
-            int64_t lb = INT64_MAX;
-            for (int j0 = rl; j0 < el; j0 += 64) {
-              const int j = j0 + lane;
-              if (j < el) {
-                const int64_t m = keyof(j);
-                if (m >= 0 && m < best && m < lb && (cl == 1 || adjacent<D>(p, pts[j], g)))
-                  lb = m;
+        int64_t lb0 = INT64_MAX;
+#pragma unroll
+        for (int k = 0; k < kR; ++k) lb0 = min(lb0, (cls[k] == 1 && mut[k]) ? mk[k] : INT64_MAX);
+        best = min(best, wave_min64(lb0));
+#pragma unroll
+        for (int k = 0; k < kR; ++k) {
+          uint64_t pm =
+              __ballot(cls[k] != 0 && !(cls[k] == 1 && mut[k]) && (!mut[k] || mk[k] < best));
+          while (pm) {
+            const int l = __ffsll((unsigned long long)pm) - 1;
+            pm &= pm - 1;
+            const int rl = __shfl(r[k], l), el = __shfl(e[k], l), cl = __shfl(cls[k], l);
+            if (__shfl(mut[k], l)) {
+              const int64_t ml = __shfl(mk[k], l);
+              if (ml >= best) continue;
+              bool hit = false;
+              for (int j0 = rl; j0 < el && !hit; j0 += 64) {
+                const int j = j0 + lane;
+                hit = __ballot((j < el) && keyof(j) >= 0 && adjacent<D>(p, pts[j], g)) != 0;
               }
+              if (hit) best = ml;
+            } else {
+              int64_t lb = INT64_MAX;
+              for (int j0 = rl; j0 < el; j0 += 64) {
+                const int j = j0 + lane;
+                if (j < el) {
+                  const int64_t m = keyof(j);
+                  if (m >= 0 && m < best && m < lb && (cl == 1 || adjacent<D>(p, pts[j], g)))
+                    lb = m;
+                }
+              }
+              best = min(best, wave_min64(lb));
             }
-            best = min(best, wave_min64(lb));
           }
         }
       }
@@ -1305,6 +1410,8 @@ struct DbscanState {
   int32_t *parent = nullptr, *ccmin = nullptr, *cid = nullptr, *nc_list = nullptr;
   int32_t *occ = nullptr, *hpos = nullptr;  // occupied cells (ascending), head-flag scan; n_occ = hpos[n]
   void* crec = nullptr;                      // CellRec<dim>[C + 1]
+  uint32_t* occ_bits = nullptr;              // 1 bit per cell
+  int uf_flags = -1;                         // see XcdRange; -1 = read RPT_UF_FLAGS once
   template <int D>
   const CellRec<D>* rec() const {
     return static_cast<const CellRec<D>*>(crec);
@@ -1419,6 +1526,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   bud.add<int32_t>(n + 1);  // occ
   bud.add<int32_t>(n + 1);  // hpos
   bud.add<CellRec<D>>(C1);  // crec
+  bud.add<uint32_t>(C1 / 32 + 1);  // occupancy bits
   RPT_TRY(arena.reserve(bud.bytes, st));
   (void)arena.carve_n<Bounds>(1);
   uint32_t* keys = arena.carve_n<uint32_t>(n);
@@ -1446,7 +1554,8 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   hpos = arena.carve_n<int32_t>(n + 1);
   CellRec<D>* cr = arena.carve_n<CellRec<D>>(C1);
   crec = cr;
-  if (!cr) {
+  occ_bits = arena.carve_n<uint32_t>(C1 / 32 + 1);
+  if (!occ_bits) {
     set_error("internal: scratch carve overflow");
     return RPT_ENOMEM;
   }
@@ -1465,9 +1574,9 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   RPT_CHECK_LAUNCH();
   RPT_TRY(exclusive_scan_i32(cell_start, cell_start, C1 + 1, stmp, st));
   RPT_TRY(exclusive_scan_i32(hpos, hpos, n + 1, stmp, st));
-  hipLaunchKernelGGL(k_occ_list, dim3(gb), dim3(kBlock), 0, st, skey, n, hpos, occ);
+  RPT_HIP(hipMemsetAsync(occ_bits, 0, sizeof(uint32_t) * (C1 / 32 + 1), st));
+  hipLaunchKernelGGL(k_occ_list, dim3(gb), dim3(kBlock), 0, st, skey, n, hpos, occ, occ_bits);
   RPT_CHECK_LAUNCH();
-  RPT_HIP(hipMemsetAsync(cr, 0, sizeof(CellRec<D>) * C1, st));
   hipLaunchKernelGGL(k_cell_box<D>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, cell_start,
                      occ, hpos + n, g, boxA, boxB, mutual, cr);
   RPT_CHECK_LAUNCH();
@@ -1500,10 +1609,10 @@ int32_t DbscanState::core_pass(hipStream_t st) {
                      mutual, core, slow, n_slow);
   if (dim == 2)
     hipLaunchKernelGGL(k_core_slow<2>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<2>(), slab_t, slow, n_slow, core);
+                       rec<2>(), occ_bits, slab_t, slow, n_slow, core);
   else
     hipLaunchKernelGGL(k_core_slow<3>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<3>(), slab_t, slow, n_slow, core);
+                       rec<3>(), occ_bits, slab_t, slow, n_slow, core);
   RPT_CHECK_LAUNCH();
   tm.mark();
   return RPT_OK;
@@ -1511,6 +1620,10 @@ int32_t DbscanState::core_pass(hipStream_t st) {
 
 int32_t DbscanState::union_pass(hipStream_t st) {
   if (degenerate) return RPT_OK;
+  if (uf_flags < 0) {
+    const char* e = std::getenv("RPT_UF_FLAGS");
+    uf_flags = e ? std::atoi(e) : kDefaultUfFlags;
+  }
   const int gb = grid_for(n, kBlock, 2048);
   const int gc = grid_for(C, kBlock, 8192);
   const int gw = wave_grid(n);
@@ -1521,20 +1634,20 @@ int32_t DbscanState::union_pass(hipStream_t st) {
                      rep, C);
   if (dim == 2) {
     hipLaunchKernelGGL((k_union_cells<2, false>), dim3(gw), dim3(kBlock), 0, st, pts, g,
-                       cell_start, occ, n_occ, rec<2>(), slab_t, core, rep, mutual, sorig,
-                       parent);
+                       cell_start, occ, n_occ, rec<2>(), occ_bits, slab_t, core, rep, mutual, sorig,
+                       parent, uf_flags);
     hipLaunchKernelGGL((k_union_cells<2, true>), dim3(gw), dim3(kBlock), 0, st, pts, g,
-                       cell_start, occ, n_occ, rec<2>(), slab_t, core, rep, mutual, sorig,
-                       parent);
+                       cell_start, occ, n_occ, rec<2>(), occ_bits, slab_t, core, rep, mutual, sorig,
+                       parent, uf_flags);
     hipLaunchKernelGGL(k_union<2>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
                        boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
   } else {
     hipLaunchKernelGGL((k_union_cells<3, false>), dim3(gw), dim3(kBlock), 0, st, pts, g,
-                       cell_start, occ, n_occ, rec<3>(), slab_t, core, rep, mutual, sorig,
-                       parent);
+                       cell_start, occ, n_occ, rec<3>(), occ_bits, slab_t, core, rep, mutual, sorig,
+                       parent, uf_flags);
     hipLaunchKernelGGL((k_union_cells<3, true>), dim3(gw), dim3(kBlock), 0, st, pts, g,
-                       cell_start, occ, n_occ, rec<3>(), slab_t, core, rep, mutual, sorig,
-                       parent);
+                       cell_start, occ, n_occ, rec<3>(), occ_bits, slab_t, core, rep, mutual, sorig,
+                       parent, uf_flags);
     hipLaunchKernelGGL(k_union<3>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
                        boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
   }
@@ -1569,12 +1682,12 @@ int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hi
   hipLaunchKernelGGL(k_label_core, dim3(gb), dim3(kBlock), 0, st, ccmin, n, sorig, cid, labels);
   if (dim == 2)
     hipLaunchKernelGGL((k_label<2, false>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<2>(), slab_t, ccmin, (const int64_t*)nullptr, rep,
+                       rec<2>(), occ_bits, slab_t, ccmin, (const int64_t*)nullptr, rep,
                        mutual, sorig, cid, (const int64_t*)nullptr, (int64_t)0, nc_list,
                        nc_count, labels);
   else
     hipLaunchKernelGGL((k_label<3, false>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<3>(), slab_t, ccmin, (const int64_t*)nullptr, rep,
+                       rec<3>(), occ_bits, slab_t, ccmin, (const int64_t*)nullptr, rep,
                        mutual, sorig, cid, (const int64_t*)nullptr, (int64_t)0, nc_list,
                        nc_count, labels);
   RPT_CHECK_LAUNCH();
@@ -1619,11 +1732,11 @@ int32_t DbscanState::labels_global(const int64_t* rep_orig, const int64_t* reps,
                      labels);
   if (dim == 2)
     hipLaunchKernelGGL((k_label<2, true>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<2>(), slab_t, (const int32_t*)nullptr, srep, rep, mutual,
+                       rec<2>(), occ_bits, slab_t, (const int32_t*)nullptr, srep, rep, mutual,
                        sorig, (const int32_t*)nullptr, reps, nr, nc_list, nc_count, labels);
   else
     hipLaunchKernelGGL((k_label<3, true>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<3>(), slab_t, (const int32_t*)nullptr, srep, rep, mutual,
+                       rec<3>(), occ_bits, slab_t, (const int32_t*)nullptr, srep, rep, mutual,
                        sorig, (const int32_t*)nullptr, reps, nr, nc_list, nc_count, labels);
   RPT_CHECK_LAUNCH();
   return RPT_OK;
