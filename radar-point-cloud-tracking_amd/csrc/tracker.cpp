@@ -23,6 +23,8 @@
 #include <numeric>
 #include <vector>
 
+#include <immintrin.h>
+
 #include "common.h"
 
 #pragma STDC FP_CONTRACT OFF
@@ -174,9 +176,129 @@ int32_t order_clusters(int32_t n_frames, int64_t n_seg, const int32_t* seg_frame
 // Rectangular LSAP exactly as scipy 1.15 (_lsap.c, Crouse 2016): shortest augmenting path per
 // row, remaining columns scanned from a reversed list, ties on the minimum prefer an unassigned
 // column, tall matrices solved transposed.  Scratch is kept across calls (one solver per tracker).
+namespace {
+
+bool host_has_avx2() {
+  static const bool v = __builtin_cpu_supports("avx2");
+  return v;
+}
+
+// r_j = ((0 + c_j) - u_i) - v_j for every column, path_j = i; returns min_j r_j
+double first_scan_base(int64_t nc, const double* row, double ui, const double* vv, double* sp,
+                       int64_t* pa, int64_t i) {
+  double mn = std::numeric_limits<double>::infinity();
+  for (int64_t j = 0; j < nc; ++j) {
+    const double r = 0.0 + row[j] - ui - vv[j];
+    sp[j] = r;
+    pa[j] = i;
+    mn = r < mn ? r : mn;
+  }
+  return mn;
+}
+
+__attribute__((target("avx2"))) double first_scan_avx2(int64_t nc, const double* row, double ui,
+                                                       const double* vv, double* sp, int64_t* pa,
+                                                       int64_t i) {
+  const __m256d z = _mm256_setzero_pd(), uv = _mm256_set1_pd(ui);
+  const __m256i iv = _mm256_set1_epi64x(i);
+  __m256d m0 = _mm256_set1_pd(std::numeric_limits<double>::infinity()), m1 = m0;
+  int64_t j = 0;
+  for (; j + 8 <= nc; j += 8) {
+    const __m256d r0 = _mm256_sub_pd(_mm256_sub_pd(_mm256_add_pd(z, _mm256_loadu_pd(row + j)), uv),
+                                     _mm256_loadu_pd(vv + j));
+    const __m256d r1 = _mm256_sub_pd(
+        _mm256_sub_pd(_mm256_add_pd(z, _mm256_loadu_pd(row + j + 4)), uv),
+        _mm256_loadu_pd(vv + j + 4));
+    _mm256_storeu_pd(sp + j, r0);
+    _mm256_storeu_pd(sp + j + 4, r1);
+    _mm256_storeu_si256((__m256i*)(pa + j), iv);
+    _mm256_storeu_si256((__m256i*)(pa + j + 4), iv);
+    m0 = _mm256_min_pd(r0, m0);  // (r < m) ? r : m
+    m1 = _mm256_min_pd(r1, m1);
+  }
+  m0 = _mm256_min_pd(m0, m1);
+  __m128d lo = _mm_min_pd(_mm256_castpd256_pd128(m0), _mm256_extractf128_pd(m0, 1));
+  double mn = _mm_cvtsd_f64(_mm_min_sd(lo, _mm_unpackhi_pd(lo, lo)));
+  for (; j < nc; ++j) {
+    const double r = 0.0 + row[j] - ui - vv[j];
+    sp[j] = r;
+    pa[j] = i;
+    mn = r < mn ? r : mn;
+  }
+  return mn;
+}
+
+// bit j of bits = (sp[j] == mn)
+void eq_bits_base(int64_t nc, const double* sp, double mn, uint64_t* bits) {
+  for (int64_t j = 0; j < nc; ++j)
+    if (sp[j] == mn) bits[j >> 6] |= 1ull << (j & 63);
+}
+
+__attribute__((target("avx2"))) void eq_bits_avx2(int64_t nc, const double* sp, double mn,
+                                                  uint64_t* bits) {
+  const __m256d m = _mm256_set1_pd(mn);
+  for (int64_t w = 0; w * 64 < nc; ++w) {
+    const int64_t e = std::min<int64_t>(nc, w * 64 + 64);
+    uint64_t acc = 0;
+    int64_t j = w * 64;
+    for (; j + 4 <= e; j += 4)
+      acc |= (uint64_t)_mm256_movemask_pd(_mm256_cmp_pd(_mm256_loadu_pd(sp + j), m, _CMP_EQ_OQ))
+             << (j & 63);
+    for (; j < e; ++j) acc |= (uint64_t)(sp[j] == mn) << (j & 63);
+    bits[w] |= acc;
+  }
+}
+
+// One later Dijkstra scan over the remaining columns rem[0..n): r = ((mv + c_j) - u_i) - v_j,
+// spc_j = min(spc_j, r) (path_j = i where it drops); tmp[it] = the new spc of rem[it].  Returns
+// the minimum of tmp.
+__attribute__((target("avx2"))) double rest_scan_avx2(int64_t n, const int64_t* rem,
+                                                      const double* row, double mv, double ui,
+                                                      const double* vv, double* sp, int64_t* pa,
+                                                      int64_t i, double* tmp) {
+  const __m256d m = _mm256_set1_pd(mv), uv = _mm256_set1_pd(ui);
+  __m256d best = _mm256_set1_pd(std::numeric_limits<double>::infinity());
+  int64_t it = 0;
+  for (; it + 4 <= n; it += 4) {
+    const __m256i jv = _mm256_loadu_si256((const __m256i*)(rem + it));
+    const __m256d r = _mm256_sub_pd(
+        _mm256_sub_pd(_mm256_add_pd(m, _mm256_i64gather_pd(row, jv, 8)), uv),
+        _mm256_i64gather_pd(vv, jv, 8));
+    const __m256d so = _mm256_i64gather_pd(sp, jv, 8);
+    const __m256d upd = _mm256_cmp_pd(r, so, _CMP_LT_OQ);
+    const __m256d sj = _mm256_blendv_pd(so, r, upd);
+    _mm256_storeu_pd(tmp + it, sj);
+    best = _mm256_min_pd(sj, best);
+    int msk = _mm256_movemask_pd(upd);
+    while (msk) {
+      const int l = __builtin_ctz(msk);
+      const int64_t j = rem[it + l];
+      sp[j] = tmp[it + l];
+      pa[j] = i;
+      msk &= msk - 1;
+    }
+  }
+  __m128d lo = _mm_min_pd(_mm256_castpd256_pd128(best), _mm256_extractf128_pd(best, 1));
+  double mn = _mm_cvtsd_f64(_mm_min_sd(lo, _mm_unpackhi_pd(lo, lo)));
+  for (; it < n; ++it) {
+    const int64_t j = rem[it];
+    const double r = mv + row[j] - ui - vv[j];
+    if (r < sp[j]) {
+      sp[j] = r;
+      pa[j] = i;
+    }
+    tmp[it] = sp[j];
+    mn = tmp[it] < mn ? tmp[it] : mn;
+  }
+  return mn;
+}
+
+}  // namespace
+
 struct Lsap {
-  std::vector<double> u, v, spc, tmp;
+  std::vector<double> u, v, spc, tmp, scan;
   std::vector<int64_t> path, col4row, row4col, remaining, idx, sr_list, sc_list;
+  std::vector<uint64_t> eqbits;
 
   // One shortest augmenting path from row i (scipy's augmenting_path).  The rows / columns it
   // visits are recorded in sr_list / sc_list (scipy's SR / SC flags) so that the dual updates
@@ -189,7 +311,8 @@ struct Lsap {
     int64_t* pa = path.data();
     const int64_t* r4c = row4col.data();
     const double* vv = v.data();
-    for (int64_t it = 0; it < nc; ++it) rem[it] = nc - it - 1;
+    // rem (scipy's reversed list of remaining columns) is only materialised when the first scan
+    // does not reach a sink; until then rem[it] = nc - 1 - it implicitly
     sr_list.clear();
     sc_list.clear();
     int64_t sink = -1;
@@ -197,40 +320,79 @@ struct Lsap {
     while (sink == -1) {
       int64_t index = -1;
       double lowest = std::numeric_limits<double>::infinity();
+      const bool scan0 = first;
       sr_list.push_back(i);
       const double* row = cost + i * nc;
       const double ui = u[i];
       if (first) {
         // First scan: every spc[j] is inf (the test r < spc[j] always passes) and the scan order
-        // is j = nc-1 .. 0, so it runs as contiguous (vectorisable) loops.  The sequential rule
+        // is j = nc-1 .. 0, so it runs as contiguous (vectorised) loops.  The sequential rule
         // "strictly lower, or equal and the column unassigned" selects, among the columns at the
         // minimum, the last unassigned one in scan order after the first one, else the first:
         // with the order descending in j, that is the smallest unassigned j below the largest
-        // minimum j, else the largest minimum j.
-        const double z = minVal;  // 0.0; kept in the sum for identical rounding of -0.0
-        double mn = std::numeric_limits<double>::infinity();
-        for (int64_t j = 0; j < nc; ++j) {
-          const double r = z + row[j] - ui - vv[j];
-          sp[j] = r;
-          pa[j] = i;
-          mn = r < mn ? r : mn;
-        }
+        // minimum j, else the largest minimum j.  r is never -0.0 (0 + c - u - v), so a lane-wise
+        // minimum is the sequential one.
+        const double mn = (host_has_avx2() ? first_scan_avx2 : first_scan_base)(nc, row, ui, vv,
+                                                                                 sp, pa, i);
+        // columns at the minimum as a bit set (a handful of words: nc is the object count)
+        eqbits.assign((size_t)((nc + 63) >> 6), 0);
+        (host_has_avx2() ? eq_bits_avx2 : eq_bits_base)(nc, sp, mn, eqbits.data());
         int64_t jmax = -1;
-        for (int64_t j = nc - 1; j >= 0; --j)
-          if (sp[j] == mn) {
-            jmax = j;
+        for (int64_t w = (int64_t)eqbits.size() - 1; w >= 0; --w)
+          if (eqbits[w]) {
+            jmax = w * 64 + 63 - __builtin_clzll(eqbits[w]);
             break;
           }
         int64_t jsel = jmax;
-        for (int64_t j = 0; j < jmax; ++j)
-          if (sp[j] == mn && r4c[j] == -1) {
-            jsel = j;
-            break;
+        for (int64_t w = 0; w * 64 < jmax && jsel == jmax; ++w) {
+          uint64_t b = eqbits[w];
+          while (b) {
+            const int64_t j = w * 64 + __builtin_ctzll(b);
+            if (j >= jmax) break;
+            if (r4c[j] == -1) {
+              jsel = j;
+              break;
+            }
+            b &= b - 1;
           }
+        }
         lowest = mn;
         index = (jmax < 0) ? -1 : nc - 1 - jsel;
         if (mn == std::numeric_limits<double>::infinity()) index = -1;
         first = false;
+      } else if (host_has_avx2()) {
+        // Later scans: the new spc values do not depend on the scan order, so they are computed
+        // lane-parallel into tmp[it]; the sequential selection rule is then applied to the
+        // positions at the minimum: the first one, replaced by the last later one whose column
+        // is unassigned.
+        scan.resize((size_t)nc);
+        const double mn = rest_scan_avx2(num_remaining, rem, row, minVal, ui, vv, sp, pa, i,
+                                         scan.data());
+        lowest = mn;
+        index = -1;
+        if (mn != std::numeric_limits<double>::infinity()) {
+          eqbits.assign((size_t)((num_remaining + 63) >> 6), 0);
+          eq_bits_avx2(num_remaining, scan.data(), mn, eqbits.data());
+          int64_t p0 = -1;
+          for (size_t w = 0; w < eqbits.size(); ++w)
+            if (eqbits[w]) {
+              p0 = (int64_t)w * 64 + __builtin_ctzll(eqbits[w]);
+              break;
+            }
+          index = p0;
+          for (int64_t w = (int64_t)eqbits.size() - 1; w >= 0 && index == p0; --w) {
+            uint64_t b = eqbits[w];
+            while (b) {
+              const int64_t p = w * 64 + 63 - __builtin_clzll(b);
+              if (p <= p0) break;
+              if (r4c[rem[p]] == -1) {
+                index = p;
+                break;
+              }
+              b &= ~(1ull << (p & 63));
+            }
+          }
+        }
       } else {
         for (int64_t it = 0; it < num_remaining; ++it) {
           const int64_t j = rem[it];
@@ -246,13 +408,15 @@ struct Lsap {
       }
       minVal = lowest;
       if (minVal == std::numeric_limits<double>::infinity()) return -1;
-      const int64_t j = rem[index];
+      const int64_t j = scan0 ? nc - 1 - index : rem[index];
       if (r4c[j] == -1)
         sink = j;
       else
         i = r4c[j];
       sc_list.push_back(j);
-      rem[index] = rem[--num_remaining];
+      if (scan0 && sink == -1)
+        for (int64_t it = 0; it < nc; ++it) rem[it] = nc - it - 1;
+      if (sink == -1) rem[index] = rem[--num_remaining];
     }
     *p_min = minVal;
     return sink;
@@ -270,11 +434,12 @@ struct Lsap {
       std::swap(nr, nc);
       cost = tmp.data();
     }
-    for (int64_t i = 0; i < nr * nc; ++i) {
-      if (cost[i] != cost[i] || cost[i] == -std::numeric_limits<double>::infinity()) {
-        set_error("matrix contains invalid numeric entries");
-        return RPT_EINVAL;
-      }
+    bool bad = false;
+    for (int64_t i = 0; i < nr * nc; ++i)
+      bad |= (cost[i] != cost[i]) | (cost[i] == -std::numeric_limits<double>::infinity());
+    if (bad) {
+      set_error("matrix contains invalid numeric entries");
+      return RPT_EINVAL;
     }
     u.assign(nr, 0.0);
     v.assign(nc, 0.0);
@@ -346,6 +511,11 @@ struct Object {
   int64_t last_seen;
   std::vector<Vel> vel;
   int color[3];
+  // mean of the last motion_history_frames velocities, in the dtype numpy gives it (refreshed
+  // whenever vel changes; the prediction itself depends on the frame gap)
+  bool mean64;
+  double m64x, m64y;
+  float m32x, m32y;
 };
 
 inline float f32_norm(float x, float y) {  // np.linalg.norm float32: sdot without FMA
@@ -359,39 +529,40 @@ inline double f64_norm(double x, double y) {  // np.linalg.norm float64: ddot wi
 
 // Cost matrix of one frame, [k clusters][m objects]: per object the prediction in the dtype numpy
 // uses (float64 while its velocity window holds the float64 zero, float32 after), cost =
-// np.linalg.norm of the difference.  Both norms are evaluated for every entry and selected, so
-// the loop vectorises; the float64 norm's fused multiply-add must be the hardware instruction
-// for speed (libm's software fma gives the same, correctly rounded, result), hence one build for
-// AVX2+FMA hosts, dispatched at run time, and a baseline build.
-#define RPT_FILL_COSTS_BODY                                                      \
-  for (int32_t i = 0; i < k; ++i) {                                              \
-    const float fx = cx[i], fy = cy[i];                                          \
-    const double dxs = (double)fx, dys = (double)fy;                             \
-    double* row = cost + (size_t)i * m;                                          \
-    for (int32_t j = 0; j < m; ++j) {                                            \
-      const double dx = dxs - p64x[j], dy = dys - p64y[j];                       \
-      row[j] = __builtin_sqrt(__builtin_fma(dy, dy, dx * dx));                   \
-    }                                                                            \
-    for (int32_t j = 0; j < m; ++j) {                                            \
-      const float ex = fx - p32x[j], ey = fy - p32y[j];                          \
-      const float exx = ex * ex, eyy = ey * ey;                                  \
-      c32[j] = __builtin_sqrtf(exx + eyy);                                       \
-    }                                                                            \
-    for (int32_t j = 0; j < m; ++j) row[j] = is64[j] ? row[j] : (double)c32[j];  \
+// np.linalg.norm of the difference.  Every entry gets the float32 norm (8-wide), then the columns
+// listed in c64 (float64 predictions: young objects) are overwritten with the float64 norm.  The
+// float64 norm's fused multiply-add must be the hardware instruction for speed (libm's software
+// fma gives the same, correctly rounded, result), hence one build for AVX2+FMA hosts, dispatched
+// at run time, and a baseline build.
+#define RPT_FILL_COSTS_BODY                                              \
+  for (int32_t i = 0; i < k; ++i) {                                      \
+    const float fx = cx[i], fy = cy[i];                                  \
+    const double dxs = (double)fx, dys = (double)fy;                     \
+    double* row = cost + (size_t)i * m;                                  \
+    for (int32_t j = 0; j < m; ++j) {                                    \
+      const float ex = fx - p32x[j], ey = fy - p32y[j];                  \
+      const float exx = ex * ex, eyy = ey * ey;                          \
+      row[j] = (double)__builtin_sqrtf(exx + eyy);                       \
+    }                                                                    \
+    for (int32_t q = 0; q < n64; ++q) {                                  \
+      const int32_t j = c64[q];                                          \
+      const double dx = dxs - p64x[j], dy = dys - p64y[j];               \
+      row[j] = __builtin_sqrt(__builtin_fma(dy, dy, dx * dx));           \
+    }                                                                    \
   }
 
 __attribute__((target("avx2,fma"))) void fill_costs_v3(
     int32_t k, int32_t m, const float* __restrict__ cx, const float* __restrict__ cy,
-    const uint8_t* __restrict__ is64, const double* __restrict__ p64x,
+    int32_t n64, const int32_t* __restrict__ c64, const double* __restrict__ p64x,
     const double* __restrict__ p64y, const float* __restrict__ p32x,
-    const float* __restrict__ p32y, float* __restrict__ c32, double* __restrict__ cost) {
+    const float* __restrict__ p32y, double* __restrict__ cost) {
   RPT_FILL_COSTS_BODY
 }
 void fill_costs_base(int32_t k, int32_t m, const float* __restrict__ cx,
-                     const float* __restrict__ cy, const uint8_t* __restrict__ is64,
+                     const float* __restrict__ cy, int32_t n64, const int32_t* __restrict__ c64,
                      const double* __restrict__ p64x, const double* __restrict__ p64y,
                      const float* __restrict__ p32x, const float* __restrict__ p32y,
-                     float* __restrict__ c32, double* __restrict__ cost) {
+                     double* __restrict__ cost) {
   RPT_FILL_COSTS_BODY
 }
 #undef RPT_FILL_COSTS_BODY
@@ -413,9 +584,9 @@ struct Tracker {
   std::vector<int64_t> ra, ca;
   std::vector<int> live;
   std::vector<char> assigned;
-  std::vector<uint8_t> is64;
+  std::vector<int32_t> c64;
   std::vector<double> p64x, p64y;
-  std::vector<float> p32x, p32y, c32;
+  std::vector<float> p32x, p32y;
   Lsap solver;
 
   static void color_of(int64_t oid, int* rgb) {  // _generate_color :666-688 (float64)
@@ -445,6 +616,7 @@ struct Tracker {
     o.frames.push_back(fid);
     o.last_seen = fid;
     o.vel.push_back(Vel{0.f, 0.f, true});
+    refresh_mean(o);
     color_of(next_id, o.color);
     objs.push_back(std::move(o));
     ++next_id;
@@ -476,70 +648,41 @@ struct Tracker {
     bool f64;
     double x, y;  // float64 prediction (f64) or the float32 value widened
   };
-  Pred predict(const Object& o, int64_t ahead) const {
+  void refresh_mean(Object& o) const {
     const size_t H = (size_t)p.motion_history_frames;
     const size_t b = o.vel.size() > H ? o.vel.size() - H : 0;
     const size_t m = o.vel.size() - b;
     bool has64 = false;
     for (size_t k = b; k < o.vel.size(); ++k) has64 |= o.vel[k].f64_zero;
-    const float lx = o.px.back(), ly = o.py.back();
-    if (has64) {
+    o.mean64 = has64;
+    if (has64) {  // np.mean(axis=0) float64: first row then sequential adds, one division
       double sx = o.vel[b].f64_zero ? 0.0 : (double)o.vel[b].x;
       double sy = o.vel[b].f64_zero ? 0.0 : (double)o.vel[b].y;
       for (size_t k = b + 1; k < o.vel.size(); ++k) {
         sx = sx + (o.vel[k].f64_zero ? 0.0 : (double)o.vel[k].x);
         sy = sy + (o.vel[k].f64_zero ? 0.0 : (double)o.vel[k].y);
       }
-      const double mx = sx / (double)m, my = sy / (double)m;
-      return Pred{true, (double)lx + mx * (double)ahead, (double)ly + my * (double)ahead};
+      o.m64x = sx / (double)m;
+      o.m64y = sy / (double)m;
+      return;
     }
     float sx = o.vel[b].x, sy = o.vel[b].y;
     for (size_t k = b + 1; k < o.vel.size(); ++k) {
       sx = sx + o.vel[k].x;
       sy = sy + o.vel[k].y;
     }
-    const float mx = sx / (float)m, my = sy / (float)m;
-    const float px = lx + mx * (float)ahead;
-    const float py = ly + my * (float)ahead;
+    o.m32x = sx / (float)m;
+    o.m32y = sy / (float)m;
+  }
+
+  Pred predict(const Object& o, int64_t ahead) const {
+    const float lx = o.px.back(), ly = o.py.back();
+    if (o.mean64)
+      return Pred{true, (double)lx + o.m64x * (double)ahead, (double)ly + o.m64y * (double)ahead};
+    const float px = lx + o.m32x * (float)ahead;
+    const float py = ly + o.m32y * (float)ahead;
     return Pred{false, (double)px, (double)py};
   }
-  static double cost_pred(const Pred& q, float cx, float cy) {
-    if (q.f64) return f64_norm((double)cx - q.x, (double)cy - q.y);
-    return (double)f32_norm(cx - (float)q.x, cy - (float)q.y);
-  }
-
-  // cost of cluster (cx,cy) vs object prediction (:135-140, :586-587)
-  double cost_of(const Object& o, float cx, float cy, int64_t ahead) const {
-    const size_t H = (size_t)p.motion_history_frames;
-    const size_t b = o.vel.size() > H ? o.vel.size() - H : 0;
-    const size_t m = o.vel.size() - b;
-    bool has64 = false;
-    for (size_t k = b; k < o.vel.size(); ++k) has64 |= o.vel[k].f64_zero;
-    const float lx = o.px.back(), ly = o.py.back();
-    if (has64) {
-      // np.mean(axis=0) float64: first row then sequential adds, one division
-      double sx = o.vel[b].f64_zero ? 0.0 : (double)o.vel[b].x;
-      double sy = o.vel[b].f64_zero ? 0.0 : (double)o.vel[b].y;
-      for (size_t k = b + 1; k < o.vel.size(); ++k) {
-        sx = sx + (o.vel[k].f64_zero ? 0.0 : (double)o.vel[k].x);
-        sy = sy + (o.vel[k].f64_zero ? 0.0 : (double)o.vel[k].y);
-      }
-      const double mx = sx / (double)m, my = sy / (double)m;
-      const double px = (double)lx + mx * (double)ahead;
-      const double py = (double)ly + my * (double)ahead;
-      return f64_norm((double)cx - px, (double)cy - py);
-    }
-    float sx = o.vel[b].x, sy = o.vel[b].y;
-    for (size_t k = b + 1; k < o.vel.size(); ++k) {
-      sx = sx + o.vel[k].x;
-      sy = sy + o.vel[k].y;
-    }
-    const float mx = sx / (float)m, my = sy / (float)m;
-    const float px = lx + mx * (float)ahead;
-    const float py = ly + my * (float)ahead;
-    return (double)f32_norm(cx - px, cy - py);
-  }
-
   void cleanup() {  // _cleanup_lost_objects: in place, order kept (dict deletion)
     size_t w = 0;
     for (size_t r = 0; r < objs.size(); ++r) {
@@ -569,24 +712,23 @@ struct Tracker {
     }
     const int32_t m = (int32_t)live.size();
     cost.resize((size_t)k * m);
-    is64.resize(m);
+    c64.clear();
     p64x.resize(m);
     p64y.resize(m);
     p32x.resize(m);
     p32y.resize(m);
-    c32.resize(m);
     for (int32_t j = 0; j < m; ++j) {
       const Object& o = objs[live[j]];
       const Pred q = predict(o, fid - o.last_seen);  // depends on the object only
-      is64[j] = q.f64 ? 1 : 0;
+      if (q.f64) c64.push_back(j);
       p64x[j] = q.x;
       p64y[j] = q.y;
       p32x[j] = (float)q.x;
       p32y[j] = (float)q.y;
     }
-    (host_has_fma() ? fill_costs_v3 : fill_costs_base)(k, m, cx, cy, is64.data(), p64x.data(),
-                                                         p64y.data(), p32x.data(), p32y.data(),
-                                                         c32.data(), cost.data());
+    (host_has_fma() ? fill_costs_v3 : fill_costs_base)(k, m, cx, cy, (int32_t)c64.size(),
+                                                         c64.data(), p64x.data(), p64y.data(),
+                                                         p32x.data(), p32y.data(), cost.data());
     const int32_t np_ = std::min(k, m);
     ra.resize(np_);
     ca.resize(np_);
@@ -601,6 +743,7 @@ struct Tracker {
         if (fe > 0) {
           const float fef = (float)fe;
           o.vel.push_back(Vel{(cx[i] - o.px.back()) / fef, (cy[i] - o.py.back()) / fef, false});
+          refresh_mean(o);
         }
         o.px.push_back(cx[i]);
         o.py.push_back(cy[i]);

@@ -53,6 +53,7 @@ class StackResult:
     frame_order_offsets: Optional[np.ndarray]  # per frame slot: its clusters in reference order
     frame_order: Optional[np.ndarray]
     tracker: Optional[NativeTracker]
+    first_noise: Optional[np.ndarray] = None  # per frame slot: first noise point or -1
     labels: Optional[torch.Tensor] = None
     points: Optional[Dict[str, torch.Tensor]] = None
     stage_ms: Dict[str, float] = field(default_factory=dict)
@@ -171,7 +172,7 @@ class FrameStackPipeline:
         res = StackResult(n_points=N, n_clustered_input=n_in, frame_ids=built,
                           n_land_cells=n_land, n_clusters=n_clusters, n_segments=len(seg["frame"]),
                           seg=seg, frame_order_offsets=None, frame_order=None, tracker=None,
-                          stage_ms=stage_ms)
+                          stage_ms=stage_ms, first_noise=first_noise)
         if self._host is not None:
             res._pending = self._host.submit(host_stage)
         else:

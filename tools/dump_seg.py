@@ -26,6 +26,6 @@ out.mkdir(exist_ok=True)
 lab = res.labels.cpu().numpy()
 pf = res.points["frame"].cpu().numpy()
 np.savez(out / "seg.npz", built=res.frame_ids, **{"seg_" + k: v for k, v in res.seg.items()},
-         n_frames=cfg.n_frames)
+         n_frames=cfg.n_frames, first_noise=res.first_noise)
 print("segments", res.n_segments, "max count", int(res.seg["count"].max()),
       "top5", np.sort(res.seg["count"])[-5:].tolist(), "noise", int((lab < 0).sum()))
