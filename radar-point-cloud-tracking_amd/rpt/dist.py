@@ -33,7 +33,7 @@ import torch
 import torch.distributed as dist
 
 from .pipeline import PathParams
-from .stages import LAND_GRID_RESOLUTION, Points, order_and_track
+from .stages import LAND_GRID_RESOLUTION, Points, order_frames, track_ordered
 
 _MIN, _MAX, _SUM = dist.ReduceOp.MIN, dist.ReduceOp.MAX, dist.ReduceOp.SUM
 
@@ -57,6 +57,13 @@ class Comm:
         dist.all_reduce(c, op=op, group=self.group)
         return c.to(t.device)
 
+    def all_gather_fixed(self, t: torch.Tensor) -> torch.Tensor:
+        """all_gather of a 1-D tensor of the same length on every rank -> [world][len] (host)."""
+        c = self._c(t).reshape(-1)
+        out = torch.empty(self.world * c.numel(), dtype=c.dtype, device=self.cdev)
+        dist.all_gather_into_tensor(out, c, group=self.group)
+        return out.cpu().reshape(self.world, -1)
+
     def all_gather_var(self, t: torch.Tensor) -> List[torch.Tensor]:
         """all_gather of 1-D tensors of different lengths (returned on the input's device)."""
         c = self._c(t).reshape(-1)
@@ -70,6 +77,29 @@ class Comm:
         outs = [torch.empty_like(pad) for _ in range(self.world)]
         dist.all_gather(outs, pad, group=self.group)
         return [o[:k].to(t.device) for o, k in zip(outs, ns)]
+
+    def exchange_known(self, to_prev: torch.Tensor, to_next: torch.Tensor, n_from_prev: int,
+                       n_from_next: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        """exchange() when every rank already knows what its neighbours send (one P2P round):
+        returns (from_prev, from_next) with n_from_prev / n_from_next elements (empty at the
+        ends of the rank chain)."""
+        r, w = self.rank, self.world
+        dev, dt = to_prev.device, to_prev.dtype
+        bp = torch.empty(n_from_prev if r > 0 else 0, dtype=dt, device=self.cdev)
+        bn = torch.empty(n_from_next if r < w - 1 else 0, dtype=dt, device=self.cdev)
+        ops = []
+        if r > 0 and to_prev.numel():
+            ops.append(dist.P2POp(dist.isend, self._c(to_prev), r - 1, self.group))
+        if r < w - 1 and to_next.numel():
+            ops.append(dist.P2POp(dist.isend, self._c(to_next), r + 1, self.group))
+        if bp.numel():
+            ops.append(dist.P2POp(dist.irecv, bp, r - 1, self.group))
+        if bn.numel():
+            ops.append(dist.P2POp(dist.irecv, bn, r + 1, self.group))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        return bp.to(dev), bn.to(dev)
 
     def exchange(self, to_prev: Optional[torch.Tensor], to_next: Optional[torch.Tensor]
                  ) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
@@ -184,10 +214,13 @@ class ShardedStackPipeline:
     """The path over a global stack whose frames are split across ranks (see module doc)."""
 
     def __init__(self, ops, comm: Comm, gains: Sequence[int], rows: int, bins: int,
-                 params: PathParams = None, timing: bool = False, async_host: bool = False):
-        """async_host: rank 0's host stage (cluster order + tracker over the whole stack) runs on
-        one worker thread while the ranks go on to the next run; ShardResult.finish() waits."""
-        self._host = ThreadPoolExecutor(max_workers=1) if async_host else None
+                 params: PathParams = None, timing: bool = False, async_host: bool = False,
+                 host_workers: int = 2):
+        """async_host: rank 0's host stage (the tracker over the whole stack; every rank orders
+        its own frames' clusters before the gather) runs on a pool of host_workers threads while
+        the ranks go on to the next runs (runs are independent, so their trackers may overlap
+        each other too); ShardResult.finish() waits."""
+        self._host = ThreadPoolExecutor(max_workers=host_workers) if async_host else None
         self.ops = ops
         self.comm = comm
         self.gains = [int(g) for g in gains]
@@ -208,92 +241,97 @@ class ShardedStackPipeline:
         def mark(name):
             if self.timing:
                 marks.append((name, time.perf_counter()))
-        # 1. K1
+        # 1. K1; counts and bounds of every rank in one all_gather
         pts = ops.polar(echo, dt, self.rows, self.bins, self.geo, self.gain_d, p.threshold,
                         p.stride, G)
         n_local = pts.n
         built_local = np.nonzero(np.diff(pts.frame_off) > 0)[0]
-        cnts = comm.all_gather_var(torch.tensor([n_local, len(built_local)], dtype=torch.int64))
-        n_global = int(sum(int(c[0]) for c in cnts))
-        n_built = int(sum(int(c[1]) for c in cnts))
+        b = ops.bounds(pts) if n_local else np.array([np.inf, -np.inf, np.inf, -np.inf],
+                                                     np.float32)
+        info = comm.all_gather_fixed(torch.tensor(
+            [n_local, len(built_local), *b.astype(np.float64)], dtype=torch.float64)).numpy()
+        n_global = int(info[:, 0].sum())
+        n_built = int(info[:, 1].sum())
         mark("polar")
-        # 2. land filter (global grid)
+        # 2. land filter (global grid): one all_reduce of [counts | intensity sums] in float64
+        #    (integer-valued, so the sums are exact in any order)
         if p.land_filter and n_built > 10 and n_global > 0:
-            if pts.n:
-                b = ops.bounds(pts)
-            else:
-                b = np.array([np.inf, -np.inf, np.inf, -np.inf], np.float32)
-            lo = comm.all_reduce(torch.tensor([b[0], b[2]], dtype=torch.float32), _MIN).numpy()
-            hi = comm.all_reduce(torch.tensor([b[1], b[3]], dtype=torch.float32), _MAX).numpy()
-            xe = np.arange(np.float32(lo[0]), np.float32(hi[0]) + LAND_GRID_RESOLUTION,
-                           LAND_GRID_RESOLUTION)
-            ye = np.arange(np.float32(lo[1]), np.float32(hi[1]) + LAND_GRID_RESOLUTION,
-                           LAND_GRID_RESOLUTION)
+            x0, x1 = np.float32(info[:, 2].min()), np.float32(info[:, 3].max())
+            y0, y1 = np.float32(info[:, 4].min()), np.float32(info[:, 5].max())
+            xe = np.arange(x0, x1 + LAND_GRID_RESOLUTION, LAND_GRID_RESOLUTION)
+            ye = np.arange(y0, y1 + LAND_GRID_RESOLUTION, LAND_GRID_RESOLUTION)
             cnt, tot = ops.land_grid(pts, xe, ye)
-            cnt = comm.all_reduce(cnt, _SUM)
-            tot = comm.all_reduce(tot, _SUM)
+            cells = cnt.numel()
+            both = comm.all_reduce(torch.cat([cnt.to(torch.float64), tot.to(torch.float64)]),
+                                   _SUM)
+            cnt = both[:cells].to(torch.int32)
+            tot = both[cells:].contiguous()
             pts, _ = ops.land_apply(pts, cnt, tot, n_built, xe, ye)
         mark("land")
-        # 3. global numbering
-        kept = comm.all_gather_var(torch.tensor([pts.n], dtype=torch.int64))
-        kept = [int(k[0]) for k in kept]
-        P = int(sum(kept[:r]))
-        n_in_global = int(sum(kept))
-        if n_in_global == 0:
-            raise ValueError("Found array with 0 sample(s) (shape=(0, 2)) while a minimum of 1 "
-                             "is required.")
-        t_own = ops.frame_times(pts, frame0)
-        # 4. halo exchange: points of the first / last h frames
+        # 3. global numbering and halo sizes: [kept, points of the first h frames, of the last h]
         h = int(np.floor(p.eps_time)) if np.isfinite(p.eps_time) and p.eps_time >= 0 else 0
         if W > 1 and h > F:
             raise ValueError(f"each rank needs at least floor(eps_time)={h} frames")
         h = min(h, F)
         fo = pts.frame_off
-        a_first, a_last = int(fo[min(h, F)]), int(fo[F - h]) if h else pts.n
         n_own = pts.n
+        a_first, a_last = int(fo[min(h, F)]), int(fo[F - h]) if h else n_own
+        kinfo = comm.all_gather_fixed(torch.tensor([n_own, a_first, n_own - a_last],
+                                                   dtype=torch.int64)).numpy()
+        kept = kinfo[:, 0]
+        P = int(kept[:r].sum())
+        n_in_global = int(kept.sum())
+        if n_in_global == 0:
+            raise ValueError("Found array with 0 sample(s) (shape=(0, 2)) while a minimum of 1 "
+                             "is required.")
+        halo = W > 1 and h > 0
+        n_prev = int(kinfo[r - 1, 2]) if halo and r > 0 else 0      # rank r-1's last h frames
+        n_next = int(kinfo[r + 1, 1]) if halo and r < W - 1 else 0  # rank r+1's first h frames
+        t_own = ops.frame_times(pts, frame0)
+        # 4. halo exchange: points of the first / last h frames (sizes known: one P2P round)
         own_xyt = torch.stack([pts.x, pts.y, t_own]) if n_own else \
             torch.zeros((3, 0), dtype=torch.float32, device=pts.x.device)
-        send_prev = own_xyt[:, :a_first].reshape(-1) if h else None
-        send_next = own_xyt[:, a_last:].reshape(-1) if h else None
-        if W > 1 and h > 0:
-            hp, hn = comm.exchange(send_prev, send_next)
+        if halo:
+            hp, hn = comm.exchange_known(own_xyt[:, :a_first].reshape(-1),
+                                         own_xyt[:, a_last:].reshape(-1), 3 * n_prev, 3 * n_next)
+            allxyt = torch.cat([hp.reshape(3, -1), own_xyt, hn.reshape(3, -1)], dim=1)
         else:
-            hp = hn = None
-        hp = hp.reshape(3, -1) if hp is not None else own_xyt[:, :0]
-        hn = hn.reshape(3, -1) if hn is not None else own_xyt[:, :0]
-        n_prev, n_next = hp.shape[1], hn.shape[1]
-        allxyt = torch.cat([hp, own_xyt, hn], dim=1).contiguous()
+            allxyt = own_xyt
+        allxyt = allxyt.contiguous()
         base = P - n_prev
         mark("halo")
         # 5. core flags, halo flags from their owners
         X, Y, T = allxyt[0].contiguous(), allxyt[1].contiguous(), allxyt[2].contiguous()
         core = ops.dbscan_core(X, Y, T, p.eps_space, p.eps_time, p.min_samples)
-        if W > 1 and h > 0:
+        if halo:
             c_own = core[n_prev:n_prev + n_own]
-            cp, cn = comm.exchange(c_own[:a_first].contiguous(), c_own[a_last:].contiguous())
-            if cp is not None and n_prev:
+            cp, cn = comm.exchange_known(c_own[:a_first].contiguous(),
+                                         c_own[a_last:].contiguous(), n_prev, n_next)
+            if n_prev:
                 core[:n_prev] = cp
-            if cn is not None and n_next:
+            if n_next:
                 core[n_prev + n_own:] = cn
         # 6. components + equivalences across ranks
         comp = ops.dbscan_components(core)
         compg = torch.where(comp >= 0, comp.to(torch.int64) + base,
                             torch.full_like(comp, -1, dtype=torch.int64))
         pairs = np.zeros((0, 2), np.int64)
-        if W > 1 and h > 0:
+        if halo:
             g_own = compg[n_prev:n_prev + n_own]
-            op_, on_ = comm.exchange(g_own[:a_first].contiguous(), g_own[a_last:].contiguous())
-            ps = []
-            if op_ is not None and n_prev:
-                ps.append(torch.stack([compg[:n_prev], op_], 1))
-            if on_ is not None and n_next:
-                ps.append(torch.stack([compg[n_prev + n_own:], on_], 1))
-            if ps:
-                pr = torch.cat(ps).cpu().numpy()
-                pr = pr[(pr[:, 0] >= 0) & (pr[:, 1] >= 0) & (pr[:, 0] != pr[:, 1])]
-                pairs = np.unique(pr, axis=0) if len(pr) else pairs
-            allp = comm.all_gather_var(torch.from_numpy(pairs.reshape(-1).copy()))
-            pairs = np.concatenate([a.numpy() for a in allp]).reshape(-1, 2) if allp else pairs
+            op_, on_ = comm.exchange_known(g_own[:a_first].contiguous(),
+                                           g_own[a_last:].contiguous(), n_prev, n_next)
+            pr = torch.cat([torch.stack([compg[:n_prev], op_], 1),
+                            torch.stack([compg[n_prev + n_own:], on_], 1)]).cpu().numpy()
+            pr = pr[(pr[:, 0] >= 0) & (pr[:, 1] >= 0) & (pr[:, 0] != pr[:, 1])]
+            pr = np.unique(pr, axis=0) if len(pr) else pairs
+            # every rank's pair list padded to the largest possible one (halo sizes are known)
+            cap = int(max((kinfo[q - 1, 2] if q > 0 else 0) +
+                          (kinfo[q + 1, 1] if q < W - 1 else 0) for q in range(W)))
+            buf = np.zeros(1 + 2 * cap, np.int64)
+            buf[0] = len(pr)
+            buf[1:1 + 2 * len(pr)] = pr.reshape(-1)
+            allp = comm.all_gather_fixed(torch.from_numpy(buf)).numpy()
+            pairs = np.concatenate([row[1:1 + 2 * int(row[0])] for row in allp]).reshape(-1, 2)
         keys, vals = merge_equivalences(pairs)
         rep = ops.remap(comp, base, keys, vals)
         # 7. global representatives and labels
@@ -304,50 +342,66 @@ class ShardedStackPipeline:
         labels = labels_all[n_prev:n_prev + n_own]
         n_clusters = int(reps_sorted.numel())
         mark("stdbscan")
-        # 8. summaries, gathered to rank 0
+        # 8. summaries and the reference cluster order of the own frames (host, per rank), then
+        #    ONE gather of everything rank 0's tracker needs (float64 carries the int32 / int64
+        #    fields and the float32 values exactly)
         seg, first_noise = ops.summaries(pts, labels, n_clusters)
-        seg_frame_global = seg["frame"].astype(np.int64) + frame0
-        packed = np.stack([seg_frame_global, seg["label"].astype(np.int64),
-                           seg["count"].astype(np.int64), seg["first"].astype(np.int64)],
-                          1).reshape(-1)
-        fl = np.stack([seg["cx"], seg["cy"], seg["mi"]], 1).astype(np.float32).reshape(-1)
-        noise = first_noise.astype(np.int64)
-        built_g = (built_local + frame0).astype(np.int64)
-        if W > 1:
-            g_int = comm.all_gather_var(torch.from_numpy(packed.copy()))
-            g_flt = comm.all_gather_var(torch.from_numpy(fl.copy()))
-            g_noise = comm.all_gather_var(torch.from_numpy(noise.copy()))
-            g_built = comm.all_gather_var(torch.from_numpy(built_g.copy()))
-        else:
-            g_int = [torch.from_numpy(packed.copy())]
-            g_flt, g_noise, g_built = ([torch.from_numpy(fl)], [torch.from_numpy(noise)],
-                                       [torch.from_numpy(built_g)])
+        S = len(seg["frame"])
+        fo_l, order_l = order_frames(F, seg, first_noise)
+        packed = np.concatenate([
+            [S], built_local.astype(np.float64) + frame0, [-1.0] * (F - len(built_local)), fo_l,
+            order_l, seg["frame"].astype(np.float64) + frame0, seg["label"], seg["count"],
+            seg["first"], seg["cx"], seg["cy"], seg["mi"]]).astype(np.float64)
+        parts = comm.all_gather_var(torch.from_numpy(packed)) if W > 1 else \
+            [torch.from_numpy(packed)]
         mark("summaries")
         res = ShardResult(n_points_local=n_local, n_points_global=n_global,
                           n_clustered_local=n_own, n_clusters=n_clusters, labels_local=labels)
         if r == 0:
-            ints = np.concatenate([a.cpu().numpy() for a in g_int]).reshape(-1, 4)
-            flts = np.concatenate([a.cpu().numpy() for a in g_flt]).reshape(-1, 3)
-            all_seg = {"frame": ints[:, 0].astype(np.int32), "label": ints[:, 1].astype(np.int32),
-                       "count": ints[:, 2], "first": ints[:, 3],
-                       "cx": flts[:, 0].copy(), "cy": flts[:, 1].copy(), "mi": flts[:, 2].copy()}
-            all_noise = np.concatenate([a.cpu().numpy() for a in g_noise]).astype(np.int64)
-            built = np.concatenate([a.cpu().numpy() for a in g_built]).astype(np.int64)
-            n_frames = F * W
+            all_seg, built, fo_g, order_g = _unpack_parts(parts, F)
+            res.seg, res.built_global = all_seg, built
+            res.n_segments = len(all_seg["frame"])
+            res.frame_order_offsets, res.frame_order = fo_g, order_g
 
             def host_stage():
                 t0 = time.perf_counter()
-                fo_, order, trk = order_and_track(n_frames, built, all_seg, all_noise, p)
-                return fo_, order, trk, (time.perf_counter() - t0) * 1e3
+                trk = track_ordered(built - frame0, fo_g, order_g, all_seg, p, built)
+                return fo_g, order_g, trk, (time.perf_counter() - t0) * 1e3
 
-            res.seg, res.built_global = all_seg, built
-            res.n_segments = len(all_seg["frame"])
             if self._host is not None:
                 res._pending = self._host.submit(host_stage)
             else:
-                res.frame_order_offsets, res.frame_order, res.tracker, _ = host_stage()
+                res.tracker = host_stage()[2]
         mark("tracker")
         if self.timing:
             for (a, ta), (b, tb) in zip(marks[:-1], marks[1:]):
                 res.stage_ms[b] = (tb - ta) * 1e3
         return res
+
+
+def _unpack_parts(parts, F: int):
+    """Rank 0: the per-rank packed summaries (rank order = frame order) -> global seg arrays,
+    built frame ids, per-frame-slot order offsets and order (indices into the global seg)."""
+    segs = {k: [] for k in ("frame", "label", "count", "first", "cx", "cy", "mi")}
+    built, fos, orders = [], [np.zeros(1, np.int64)], []
+    s_base = 0
+    for q, t in enumerate(parts):
+        a = t.cpu().numpy()
+        S = int(a[0])
+        o = 1
+        bl = a[o:o + F]
+        o += F
+        built.append(bl[bl >= 0].astype(np.int64))
+        fo = a[o:o + F + 1].astype(np.int64)
+        o += F + 1
+        fos.append(fo[1:] + s_base)
+        orders.append(a[o:o + S].astype(np.int64) + s_base)
+        o += S
+        for k, dt in (("frame", np.int32), ("label", np.int32), ("count", np.int64),
+                      ("first", np.int64), ("cx", np.float32), ("cy", np.float32),
+                      ("mi", np.float32)):
+            segs[k].append(a[o:o + S].astype(dt))
+            o += S
+        s_base += S
+    seg = {k: np.concatenate(v) for k, v in segs.items()}
+    return seg, np.concatenate(built), np.concatenate(fos), np.concatenate(orders)

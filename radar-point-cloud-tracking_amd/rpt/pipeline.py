@@ -74,10 +74,12 @@ class FrameStackPipeline:
     """Runs the path over echo [n_frames][n_gains][rows][bins] (u8 or f32) in device memory."""
 
     def __init__(self, gains: Sequence[int], rows: int, bins: int, params: PathParams = None,
-                 device=None, timing: bool = False, async_host: bool = False):
+                 device=None, timing: bool = False, async_host: bool = False,
+                 host_workers: int = 2):
         """async_host: the host stage (cluster order + tracker, sequential C++) of a run executes
-        on one worker thread while the caller goes on to the next run's device work; results
-        complete in submission order and StackResult.finish() waits for them."""
+        on a pool of host_workers threads while the caller goes on to the next runs' device
+        work (runs are independent, so their host stages may overlap each other);
+        StackResult.finish() waits for a run's host stage."""
         self.dev = require_gpu(device)
         self.gains = [int(g) for g in gains]
         if sorted(self.gains) != self.gains:
@@ -86,7 +88,7 @@ class FrameStackPipeline:
         self.p = params or PathParams()
         self.ops = HipOps(self.dev)
         self.timing = timing
-        self._host = ThreadPoolExecutor(max_workers=1) if async_host else None
+        self._host = ThreadPoolExecutor(max_workers=host_workers) if async_host else None
         self._geo_key = None
         self.last_stats = None
 

@@ -260,12 +260,10 @@ class HipOps:
             self._dbscan = None
 
 
-def order_and_track(n_frames: int, built: np.ndarray, seg: Dict[str, np.ndarray],
-                    first_noise: np.ndarray, params, frame_ids: Optional[np.ndarray] = None):
-    """Host: per-frame reference cluster order (CPython set emulation) + the C++ tracker over the
-    built frames.  frame_ids[f] is the frame id of slot f (default: the slot)."""
-    from .native_tracker import NativeTracker
-
+def order_frames(n_frames: int, seg: Dict[str, np.ndarray], first_noise: np.ndarray):
+    """Host: per frame slot, its segments in the reference's cluster order (CPython set
+    iteration of the frame's labels, 4_temporal_object_tracker.py:519-522) -> (offsets
+    [n_frames + 1], order = indices into seg)."""
     lib = _abi.load()
     S = len(seg["frame"])
     fo = np.empty(n_frames + 1, np.int64)
@@ -277,13 +275,22 @@ def order_and_track(n_frames: int, built: np.ndarray, seg: Dict[str, np.ndarray]
         np.ascontiguousarray(first_noise, np.int64).ctypes.data_as(_abi.c_i64p),
         fo.ctypes.data_as(_abi.c_i64p), order.ctypes.data_as(_abi.c_i64p)),
         "rpt_order_clusters")
-    order = order[:S]
+    return fo, order[:S]
+
+
+def track_ordered(slots: np.ndarray, fo: np.ndarray, order: np.ndarray,
+                  seg: Dict[str, np.ndarray], params, frame_ids: Optional[np.ndarray] = None):
+    """Host: the C++ tracker over the built frame slots (ascending), each frame's clusters in
+    the order given by (fo, order); frame_ids[k] is the frame id of slots[k] (default: the
+    slot)."""
+    from .native_tracker import NativeTracker
+
     trk = NativeTracker(params.max_association_distance, params.max_missed_frames,
                         params.motion_history_frames, params.stationary_velocity_threshold)
-    built = np.asarray(built, np.int64)
-    if len(built):
-        cnts = fo[built + 1] - fo[built]
-        starts = fo[built]
+    slots = np.asarray(slots, np.int64)
+    if len(slots):
+        cnts = fo[slots + 1] - fo[slots]
+        starts = fo[slots]
         idx = np.repeat(starts - np.concatenate([[0], np.cumsum(cnts)[:-1]]), cnts) + \
             np.arange(int(cnts.sum()))
         sel = order[idx]
@@ -291,6 +298,16 @@ def order_and_track(n_frames: int, built: np.ndarray, seg: Dict[str, np.ndarray]
     else:
         sel = np.zeros(0, np.int64)
         offs = np.zeros(1, np.int64)
-    ids = built if frame_ids is None else np.asarray(frame_ids, np.int64)[built]
+    ids = slots if frame_ids is None else np.asarray(frame_ids, np.int64)
     trk.run(ids, offs, seg["cx"][sel], seg["cy"][sel])
-    return fo, order, trk
+    return trk
+
+
+def order_and_track(n_frames: int, built: np.ndarray, seg: Dict[str, np.ndarray],
+                    first_noise: np.ndarray, params, frame_ids: Optional[np.ndarray] = None):
+    """Host: per-frame reference cluster order (CPython set emulation) + the C++ tracker over the
+    built frames.  frame_ids[f] is the frame id of slot f (default: the slot)."""
+    fo, order = order_frames(n_frames, seg, first_noise)
+    built = np.asarray(built, np.int64)
+    ids = None if frame_ids is None else np.asarray(frame_ids, np.int64)[built]
+    return fo, order, track_ordered(built, fo, order, seg, params, ids)
