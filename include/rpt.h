@@ -22,6 +22,7 @@
  *   rpt_set_order                    CPython set(frame_labels) iteration order :519
  *   rpt_lsap                         scipy.optimize.linear_sum_assignment as called at :590
  *   rpt_tracker_*                    ObjectTracker :543-688 (+ TrackedObject :111-140)
+ *   rpt_stack_*                      the compute stages of run_pipeline :941-991 (K1 .. K9) in one call
  *   rpt_synth_echo                   (bench/test input generator; no reference counterpart)
  */
 #ifndef RPT_H
@@ -185,6 +186,58 @@ int32_t rpt_cluster_summaries(const int32_t* labels, const float* x, const float
                               int64_t* frame_first_noise, int64_t* n_segments_host,
                               void* stream);
 
+/* ---- native stack driver (single device) -----------------------------------------------
+ * The compute stages of run_pipeline (PointCloudWork/4_temporal_object_tracker.py:941-991) over
+ * a stack of sweeps in device memory, in ONE call: K1 (rpt_polar_count/write over
+ * n_frames*files_per_frame files, ascending gain inside a frame) -> land filter when enabled and
+ * more than 10 frames are non-empty (:954; grid edges = np.arange(min, max + res, res) as numpy
+ * evaluates it) -> rpt_stdbscan of (x, y) with times = frame slot -> rpt_cluster_summaries.
+ * Equivalent to calling those entry points in sequence; the size readbacks they need happen
+ * inside (pinned memory).  Synchronises `stream`.  An empty clustered set returns RPT_EEMPTY
+ * (sklearn's ValueError).  The handle owns its device buffers (grow-only); results stay valid
+ * until the next run on the handle. */
+/* host: the land-grid edges np.arange(lo, hi + res, res) for float32 lo/hi, as numpy 2.x
+ * evaluates it (float32 stop and length, float64 values); returns the length, writes up to cap */
+int32_t rpt_arange_edges(float lo, float hi, double res, double* out, int32_t cap);
+typedef struct rpt_stack rpt_stack;
+typedef struct rpt_stack_params {
+  int32_t n_frames, files_per_frame, rows, bins, echo_dtype;
+  float threshold;              /* INTENSITY_THRESHOLD (strict >) */
+  int32_t stride;               /* POINT_STRIDE */
+  int32_t land_filter;          /* 0 = --no-land-filter */
+  double land_resolution;       /* LAND_GRID_RESOLUTION 5.0 */
+  double land_persistence;      /* LAND_PERSISTENCE_THRESHOLD 0.8 */
+  double land_min_intensity;    /* LAND_MIN_INTENSITY 100 */
+  double eps_space, eps_time;
+  int32_t min_samples;
+  int32_t timing;               /* 1 = per-stage hipEvent times in the result */
+} rpt_stack_params;
+typedef struct rpt_stack_result {
+  int64_t n_points;             /* K1 points ("Total points", :950-951) */
+  int64_t n_clustered;          /* points entering ST-DBSCAN */
+  int64_t n_land_cells;
+  int64_t n_segments;           /* (frame, label >= 0) pairs */
+  int32_t n_built;              /* frames with at least one K1 point */
+  int32_t n_clusters;
+  double ms_polar, ms_land, ms_stdbscan, ms_summaries;  /* timing != 0 */
+  rpt_stdbscan_stats dbscan;
+} rpt_stack_result;
+rpt_stack* rpt_stack_create(void);
+void rpt_stack_destroy(rpt_stack* h);
+int32_t rpt_stack_run(rpt_stack* h, const rpt_stack_params* params, const void* echo /*dev*/,
+                      const float* scale /*dev [files*rows]*/, const float* cos_t,
+                      const float* sin_t, const int32_t* gain /*dev [files], nullable*/,
+                      rpt_stack_result* result /*host*/, void* stream);
+/* host [n_frames+1]: which 0 = K1 frame offsets, 1 = offsets of the clustered points */
+int32_t rpt_stack_frame_offsets(const rpt_stack* h, int32_t which, int64_t* out);
+/* host copies of the last run's segments (rpt_cluster_summaries layout; each nullable) and
+ * frame_first_noise [n_frames] */
+int32_t rpt_stack_segments(const rpt_stack* h, int32_t* frame, int32_t* label, int64_t* count,
+                           int64_t* first, float* cx, float* cy, float* mean_i,
+                           int64_t* frame_first_noise);
+/* device copies (each nullable, [n_clustered]) of the clustered points and their labels */
+int32_t rpt_stack_points(const rpt_stack* h, float* x, float* y, float* intensity,
+                         int32_t* gain, int32_t* point_frame, int32_t* labels, void* stream);
 /* ---- host: per-frame cluster order of the reference -----------------------------------
  * From the segments of rpt_cluster_summaries (copied to host) and frame_first_noise: for each
  * frame the segment indices in the order st_dbscan(frames) lists that frame's clusters

@@ -1,0 +1,442 @@
+// Native driver of the single-device stack path: the compute stages of run_pipeline
+// (PointCloudWork/4_temporal_object_tracker.py:941-991) over a stack of sweeps already in HBM,
+//
+//   K1 polar scatter + fusion -> land filter (> 10 built frames, :954) -> ST-DBSCAN over the
+//   stack -> per-(frame, label) summaries,
+//
+// in ONE library call.  The data-dependent sizes (points per file, land-filter bounds and kept
+// count, grid bounds, segment count) still need host readbacks, but each is a pinned-memory copy
+// and a stream sync inside C++ instead of a Python round trip per stage, and the results come
+// back in one packed copy.  Buffers are owned by the handle and grow only.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+
+namespace rpt {
+int32_t polar_count(const void* echo, int32_t dt, int64_t n_files, int32_t rows, int32_t bins,
+                    float thr, int32_t stride, int64_t* row_prefix, int64_t* file_offsets,
+                    int64_t* total_host, hipStream_t st);
+int32_t polar_write(const void* echo, int32_t dt, int64_t n_files, int32_t rows, int32_t bins,
+                    const float* scale, const float* cos_t, const float* sin_t,
+                    const int32_t* gain, float thr, int32_t stride, const int64_t* row_prefix,
+                    const int64_t* file_offsets, int32_t files_per_frame, float* x, float* y,
+                    float* v, int32_t* gout, int32_t* pf, hipStream_t st);
+int32_t frame_times(const int32_t* pf, int64_t n, const int64_t* ids, float* t, hipStream_t st);
+int32_t bounds_xy(const float* x, const float* y, int64_t n, float* out4, hipStream_t st);
+int32_t land_grid(const float* x, const float* y, const float* val, int64_t n, const double* xe,
+                  int32_t nxe, const double* ye, int32_t nye, int32_t* cnt, double* tot,
+                  hipStream_t st);
+int32_t land_mask(const int32_t* cnt, const double* tot, int64_t cells, int64_t num_frames,
+                  double pthr, double ithr, uint8_t* land, int64_t* n_land_host,
+                  hipStream_t st);
+int32_t land_filter(const float* x, const float* y, const float* v, const int32_t* g,
+                    const int32_t* pf, int64_t n, const int64_t* frame_off, int32_t n_frames,
+                    const double* xe, int32_t nxe, const double* ye, int32_t nye,
+                    const uint8_t* land, float* xo, float* yo, float* vo, int32_t* go,
+                    int32_t* pfo, int64_t* new_off, int64_t* n_kept_host, hipStream_t st);
+int32_t stdbscan(const float* x, const float* y, const float* z, int64_t stride, const float* t,
+                 int64_t n, double eps_space, double eps_time, int32_t min_samples,
+                 int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st, int dim);
+int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
+                          const float* inten, const int32_t* pf, int64_t n, int32_t n_frames,
+                          int32_t n_clusters, int32_t* o_frame, int32_t* o_label,
+                          int64_t* o_count, int64_t* o_first, float* o_cx, float* o_cy,
+                          float* o_mi, int64_t* frame_first_noise, int64_t* n_seg_host,
+                          hipStream_t st);
+
+// np.arange(lo, hi + res, res) for float32 lo/hi (numpy 2.x, NEP 50 weak Python floats): the
+// stop and the length are float32 arithmetic, element 1 is float32(lo + res), the rest are
+// float64 start + i * (e1 - e0).  Checked against numpy in tests/test_host_native.py.
+std::vector<double> arange_edges(float lo, float hi, double res) {
+  const float rf = (float)res;
+  const float stop = hi + rf;
+  const float q = (stop - lo) / rf;
+  const double len_d = std::ceil((double)q);
+  const int64_t len = (len_d > 0.0) ? (int64_t)len_d : 0;
+  std::vector<double> e((size_t)len);
+  if (len == 0) return e;
+  e[0] = (double)lo;
+  if (len == 1) return e;
+  e[1] = (double)(float)(lo + rf);
+  const double d = e[1] - e[0];
+  for (int64_t i = 2; i < len; ++i) e[(size_t)i] = e[0] + (double)i * d;
+  return e;
+}
+
+namespace {
+
+__global__ void k_count_u8(const uint8_t* __restrict__ m, int64_t n, int64_t* __restrict__ out) {
+  int64_t c = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    c += m[i] ? 1 : 0;
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd((unsigned long long*)out, (unsigned long long)c);
+}
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  // grows only between syncs of the owning stream (callers synchronise before growing)
+  int32_t ensure(size_t n, hipStream_t st) {
+    if (n <= cap && p) return RPT_OK;
+    if (p) {
+      RPT_HIP(hipStreamSynchronize(st));
+      RPT_HIP(hipFree(p));
+      p = nullptr;
+      cap = 0;
+    }
+    const size_t want = std::max<size_t>(n + n / 8 + 64, 256);
+    if (hipMalloc((void**)&p, want * sizeof(T)) != hipSuccess) {
+      p = nullptr;
+      set_error("rpt_stack: hipMalloc of %zu bytes failed", want * sizeof(T));
+      return RPT_ENOMEM;
+    }
+    cap = want;
+    return RPT_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct PinnedBuf {
+  char* p = nullptr;
+  size_t cap = 0;
+  int32_t ensure(size_t bytes, hipStream_t st) {
+    if (bytes <= cap && p) return RPT_OK;
+    if (p) {
+      RPT_HIP(hipStreamSynchronize(st));
+      RPT_HIP(hipHostFree(p));
+      p = nullptr;
+      cap = 0;
+    }
+    const size_t want = align_up(bytes + bytes / 8 + 4096, 4096);
+    if (hipHostMalloc((void**)&p, want, hipHostMallocDefault) != hipSuccess) {
+      p = nullptr;
+      set_error("rpt_stack: hipHostMalloc of %zu bytes failed", want);
+      return RPT_ENOMEM;
+    }
+    cap = want;
+    return RPT_OK;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+}  // namespace
+}  // namespace rpt
+
+using namespace rpt;
+
+struct rpt_stack {
+  DevBuf<int64_t> row_prefix, file_off, fo_d, new_off, first_noise, seg_count, seg_first, scal;
+  DevBuf<float> x, y, v, x2, y2, v2, t, seg_cx, seg_cy, seg_mi;
+  DevBuf<int32_t> g, pf, g2, pf2, labels, land_cnt, seg_frame, seg_label;
+  DevBuf<double> land_tot, edges;
+  DevBuf<uint8_t> land_mask;
+  PinnedBuf up, down;  // host staging: uploads (edges, offsets), readbacks
+  std::vector<int64_t> fo_k1, fo_in;
+  std::vector<int32_t> h_frame, h_label;
+  std::vector<int64_t> h_count, h_first, h_noise;
+  std::vector<float> h_cx, h_cy, h_mi;
+  bool land_applied = false;
+  int32_t n_frames = 0;
+  int64_t n_in = 0;
+  hipEvent_t ev[5] = {};
+  bool ev_ok = false;
+
+  ~rpt_stack() {
+    DevBuf<int64_t>* i64[] = {&row_prefix, &file_off, &fo_d, &new_off, &first_noise, &seg_count,
+                              &seg_first, &scal};
+    for (auto* b : i64) b->release();
+    DevBuf<float>* f32[] = {&x, &y, &v, &x2, &y2, &v2, &t, &seg_cx, &seg_cy, &seg_mi};
+    for (auto* b : f32) b->release();
+    DevBuf<int32_t>* i32[] = {&g, &pf, &g2, &pf2, &labels, &land_cnt, &seg_frame, &seg_label};
+    for (auto* b : i32) b->release();
+    land_tot.release();
+    edges.release();
+    land_mask.release();
+    up.release();
+    down.release();
+    if (ev_ok)
+      for (auto& e : ev) (void)hipEventDestroy(e);
+  }
+
+  int32_t run(const rpt_stack_params& p, const void* echo, const float* scale,
+              const float* cos_t, const float* sin_t, const int32_t* gain, rpt_stack_result* out,
+              hipStream_t st);
+};
+
+int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float* scale,
+                       const float* cos_t, const float* sin_t, const int32_t* gain,
+                       rpt_stack_result* out, hipStream_t st) {
+  const int32_t F = p.n_frames, G = p.files_per_frame;
+  if (F < 0 || G < 1 || p.rows <= 0 || p.bins <= 0 || p.stride < 1 || !echo || !scale ||
+      !cos_t || !sin_t) {
+    set_error("rpt_stack_run: bad arguments");
+    return RPT_EINVAL;
+  }
+  const int64_t n_files = (int64_t)F * G;
+  n_frames = F;
+  land_applied = false;
+  const bool timing = p.timing != 0;
+  if (timing && !ev_ok) {
+    for (auto& e : ev) RPT_HIP(hipEventCreate(&e));
+    ev_ok = true;
+  }
+  if (timing) RPT_HIP(hipEventRecord(ev[0], st));
+  rpt_stack_result r{};
+
+  // ---- K1: count -> per-file offsets (one readback) -> write
+  RPT_TRY(row_prefix.ensure((size_t)n_files * p.rows + 1, st));
+  RPT_TRY(file_off.ensure((size_t)n_files + 1, st));
+  RPT_TRY(down.ensure(sizeof(int64_t) * (size_t)(n_files + 2 * F + 8), st));
+  RPT_TRY(polar_count(echo, p.echo_dtype, n_files, p.rows, p.bins, p.threshold, p.stride,
+                      row_prefix.p, file_off.p, nullptr, st));
+  int64_t* hfo = reinterpret_cast<int64_t*>(down.p);
+  RPT_HIP(hipMemcpyAsync(hfo, file_off.p, sizeof(int64_t) * (n_files + 1),
+                         hipMemcpyDeviceToHost, st));
+  RPT_HIP(hipStreamSynchronize(st));
+  const int64_t N = hfo[n_files];
+  fo_k1.resize((size_t)F + 1);
+  for (int32_t f = 0; f <= F; ++f) fo_k1[(size_t)f] = hfo[(size_t)f * G];
+  r.n_points = N;
+  int32_t n_built = 0;
+  for (int32_t f = 0; f < F; ++f) n_built += (fo_k1[(size_t)f + 1] > fo_k1[(size_t)f]) ? 1 : 0;
+  r.n_built = n_built;
+  const size_t cap = (size_t)std::max<int64_t>(N, 1);
+  RPT_TRY(x.ensure(cap, st));
+  RPT_TRY(y.ensure(cap, st));
+  RPT_TRY(v.ensure(cap, st));
+  RPT_TRY(g.ensure(cap, st));
+  RPT_TRY(pf.ensure(cap, st));
+  RPT_TRY(polar_write(echo, p.echo_dtype, n_files, p.rows, p.bins, scale, cos_t, sin_t, gain,
+                      p.threshold, p.stride, row_prefix.p, file_off.p, G, x.p, y.p, v.p,
+                      gain ? g.p : nullptr, pf.p, st));
+  if (timing) RPT_HIP(hipEventRecord(ev[1], st));
+
+  // ---- land filter (global grid over the stack, :954 gate: more than 10 built frames)
+  float* cx = x.p;
+  float* cy = y.p;
+  float* cv = v.p;
+  int32_t* cg = g.p;
+  int32_t* cpf = pf.p;
+  int64_t n_in_ = N;
+  fo_in = fo_k1;
+  r.n_land_cells = 0;
+  if (p.land_filter && n_built > 10 && N > 0) {
+    float b4[4];
+    RPT_TRY(bounds_xy(x.p, y.p, N, b4, st));  // synchronises
+    const std::vector<double> xe = arange_edges(b4[0], b4[1], p.land_resolution);
+    const std::vector<double> ye = arange_edges(b4[2], b4[3], p.land_resolution);
+    const int32_t nxe = (int32_t)xe.size(), nye = (int32_t)ye.size();
+    if (nxe < 2 || nye < 2) {
+      set_error("rpt_stack_run: degenerate land grid");
+      return RPT_EINVAL;
+    }
+    const int64_t cells = (int64_t)(nxe - 1) * (nye - 1);
+    RPT_TRY(edges.ensure((size_t)(nxe + nye), st));
+    RPT_TRY(fo_d.ensure((size_t)F + 1, st));
+    RPT_TRY(up.ensure(sizeof(double) * (size_t)(nxe + nye) + sizeof(int64_t) * (size_t)(F + 1),
+                      st));
+    double* he = reinterpret_cast<double*>(up.p);
+    std::memcpy(he, xe.data(), sizeof(double) * nxe);
+    std::memcpy(he + nxe, ye.data(), sizeof(double) * nye);
+    int64_t* hf = reinterpret_cast<int64_t*>(he + nxe + nye);
+    std::memcpy(hf, fo_k1.data(), sizeof(int64_t) * (F + 1));
+    RPT_HIP(hipMemcpyAsync(edges.p, he, sizeof(double) * (nxe + nye), hipMemcpyHostToDevice, st));
+    RPT_HIP(hipMemcpyAsync(fo_d.p, hf, sizeof(int64_t) * (F + 1), hipMemcpyHostToDevice, st));
+    RPT_TRY(land_cnt.ensure((size_t)cells, st));
+    RPT_TRY(land_tot.ensure((size_t)cells, st));
+    RPT_TRY(land_mask.ensure((size_t)cells, st));
+    RPT_TRY(land_grid(x.p, y.p, v.p, N, edges.p, nxe, edges.p + nxe, nye, land_cnt.p, land_tot.p,
+                      st));
+    RPT_TRY(rpt::land_mask(land_cnt.p, land_tot.p, cells, n_built, p.land_persistence,
+                           p.land_min_intensity, land_mask.p, nullptr, st));
+    RPT_TRY(scal.ensure(4, st));
+    RPT_HIP(hipMemsetAsync(scal.p, 0, sizeof(int64_t), st));
+    hipLaunchKernelGGL(k_count_u8, dim3(grid_for(cells, 256, 64)), dim3(256), 0, st,
+                       land_mask.p, cells, scal.p);
+    RPT_CHECK_LAUNCH();
+    RPT_TRY(x2.ensure(cap, st));
+    RPT_TRY(y2.ensure(cap, st));
+    RPT_TRY(v2.ensure(cap, st));
+    RPT_TRY(g2.ensure(cap, st));
+    RPT_TRY(pf2.ensure(cap, st));
+    RPT_TRY(new_off.ensure((size_t)F + 1, st));
+    RPT_TRY(land_filter(x.p, y.p, v.p, gain ? g.p : nullptr, pf.p, N, fo_d.p, F, edges.p, nxe,
+                        edges.p + nxe, nye, land_mask.p, x2.p, y2.p, v2.p, gain ? g2.p : nullptr,
+                        pf2.p, new_off.p, nullptr, st));
+    int64_t* hn = reinterpret_cast<int64_t*>(down.p);
+    RPT_HIP(hipMemcpyAsync(hn, new_off.p, sizeof(int64_t) * (F + 1), hipMemcpyDeviceToHost, st));
+    RPT_HIP(hipMemcpyAsync(hn + F + 1, scal.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    RPT_HIP(hipStreamSynchronize(st));
+    fo_in.assign(hn, hn + F + 1);
+    n_in_ = hn[F];
+    r.n_land_cells = hn[F + 1];
+    cx = x2.p;
+    cy = y2.p;
+    cv = v2.p;
+    cg = g2.p;
+    cpf = pf2.p;
+    land_applied = true;
+  }
+  if (timing) RPT_HIP(hipEventRecord(ev[2], st));
+  n_in = n_in_;
+  r.n_clustered = n_in_;
+  if (n_in_ == 0) {
+    set_error("Found array with 0 sample(s) (shape=(0, 2)) while a minimum of 1 is required.");
+    return RPT_EEMPTY;
+  }
+
+  // ---- ST-DBSCAN over the stack (times = frame slot as float32, :460-467)
+  const size_t cap2 = (size_t)n_in_;
+  RPT_TRY(t.ensure(cap2, st));
+  RPT_TRY(labels.ensure(cap2, st));
+  RPT_TRY(frame_times(cpf, n_in_, nullptr, t.p, st));
+  rpt_stdbscan_stats sts{};
+  sts.timing = p.timing;
+  RPT_TRY(stdbscan(cx, cy, nullptr, 1, t.p, n_in_, p.eps_space, p.eps_time, p.min_samples,
+                   labels.p, &sts, st, 2));
+  r.n_clusters = sts.n_clusters;
+  r.dbscan = sts;
+  if (timing) RPT_HIP(hipEventRecord(ev[3], st));
+
+  // ---- K9 summaries (segments ordered by (label, frame)), one packed readback
+  RPT_TRY(seg_frame.ensure(cap2, st));
+  RPT_TRY(seg_label.ensure(cap2, st));
+  RPT_TRY(seg_count.ensure(cap2, st));
+  RPT_TRY(seg_first.ensure(cap2, st));
+  RPT_TRY(seg_cx.ensure(cap2, st));
+  RPT_TRY(seg_cy.ensure(cap2, st));
+  RPT_TRY(seg_mi.ensure(cap2, st));
+  RPT_TRY(first_noise.ensure((size_t)std::max(F, 1), st));
+  int64_t S = 0;
+  RPT_TRY(cluster_summaries(labels.p, cx, cy, cv, cpf, n_in_, F, sts.n_clusters, seg_frame.p,
+                            seg_label.p, seg_count.p, seg_first.p, seg_cx.p, seg_cy.p,
+                            seg_mi.p, first_noise.p, &S, st));
+  r.n_segments = S;
+  const size_t bytes = (size_t)S * (4 + 4 + 8 + 8 + 4 + 4 + 4) + (size_t)F * 8 + 64;
+  RPT_TRY(down.ensure(bytes, st));
+  char* h = down.p;
+  auto d2h = [&](void* dst, const void* src, size_t nb) -> int32_t {
+    if (nb) RPT_HIP(hipMemcpyAsync(dst, src, nb, hipMemcpyDeviceToHost, st));
+    return RPT_OK;
+  };
+  int64_t* hcount = reinterpret_cast<int64_t*>(h);
+  int64_t* hfirst = hcount + S;
+  int64_t* hnoise = hfirst + S;
+  int32_t* hframe = reinterpret_cast<int32_t*>(hnoise + F);
+  int32_t* hlabel = hframe + S;
+  float* hcx = reinterpret_cast<float*>(hlabel + S);
+  float* hcy = hcx + S;
+  float* hmi = hcy + S;
+  RPT_TRY(d2h(hcount, seg_count.p, sizeof(int64_t) * S));
+  RPT_TRY(d2h(hfirst, seg_first.p, sizeof(int64_t) * S));
+  RPT_TRY(d2h(hnoise, first_noise.p, sizeof(int64_t) * F));
+  RPT_TRY(d2h(hframe, seg_frame.p, sizeof(int32_t) * S));
+  RPT_TRY(d2h(hlabel, seg_label.p, sizeof(int32_t) * S));
+  RPT_TRY(d2h(hcx, seg_cx.p, sizeof(float) * S));
+  RPT_TRY(d2h(hcy, seg_cy.p, sizeof(float) * S));
+  RPT_TRY(d2h(hmi, seg_mi.p, sizeof(float) * S));
+  if (timing) RPT_HIP(hipEventRecord(ev[4], st));
+  RPT_HIP(hipStreamSynchronize(st));
+  h_count.assign(hcount, hcount + S);
+  h_first.assign(hfirst, hfirst + S);
+  h_noise.assign(hnoise, hnoise + F);
+  h_frame.assign(hframe, hframe + S);
+  h_label.assign(hlabel, hlabel + S);
+  h_cx.assign(hcx, hcx + S);
+  h_cy.assign(hcy, hcy + S);
+  h_mi.assign(hmi, hmi + S);
+  if (timing) {
+    float ms[4];
+    for (int k = 0; k < 4; ++k) RPT_HIP(hipEventElapsedTime(&ms[k], ev[k], ev[k + 1]));
+    r.ms_polar = ms[0];
+    r.ms_land = ms[1];
+    r.ms_stdbscan = ms[2];
+    r.ms_summaries = ms[3];
+  }
+  if (out) *out = r;
+  return RPT_OK;
+}
+
+extern "C" {
+
+int32_t rpt_arange_edges(float lo, float hi, double res, double* out, int32_t cap) {
+  const std::vector<double> e = arange_edges(lo, hi, res);
+  if (out) std::copy(e.begin(), e.begin() + std::min<size_t>(e.size(), (size_t)std::max(cap, 0)), out);
+  return (int32_t)e.size();
+}
+
+rpt_stack* rpt_stack_create(void) { return new rpt_stack(); }
+
+void rpt_stack_destroy(rpt_stack* h) { delete h; }
+
+int32_t rpt_stack_run(rpt_stack* h, const rpt_stack_params* p, const void* echo,
+                      const float* scale, const float* cos_t, const float* sin_t,
+                      const int32_t* gain, rpt_stack_result* out, void* stream) {
+  clear_error();
+  if (!h || !p) {
+    set_error("rpt_stack_run: null handle or params");
+    return RPT_EINVAL;
+  }
+  return h->run(*p, echo, scale, cos_t, sin_t, gain, out, as_stream(stream));
+}
+
+int32_t rpt_stack_frame_offsets(const rpt_stack* h, int32_t which, int64_t* out) {
+  if (!h || !out || (which != 0 && which != 1)) return RPT_EINVAL;
+  const auto& v = which == 0 ? h->fo_k1 : h->fo_in;
+  std::copy(v.begin(), v.end(), out);
+  return RPT_OK;
+}
+
+int32_t rpt_stack_segments(const rpt_stack* h, int32_t* frame, int32_t* label, int64_t* count,
+                           int64_t* first, float* cx, float* cy, float* mean_i,
+                           int64_t* frame_first_noise) {
+  if (!h) return RPT_EINVAL;
+  auto cp = [](const auto& v, auto* dst) {
+    if (dst) std::copy(v.begin(), v.end(), dst);
+  };
+  cp(h->h_frame, frame);
+  cp(h->h_label, label);
+  cp(h->h_count, count);
+  cp(h->h_first, first);
+  cp(h->h_cx, cx);
+  cp(h->h_cy, cy);
+  cp(h->h_mi, mean_i);
+  cp(h->h_noise, frame_first_noise);
+  return RPT_OK;
+}
+
+int32_t rpt_stack_points(const rpt_stack* h, float* x, float* y, float* intensity,
+                         int32_t* gain, int32_t* point_frame, int32_t* labels, void* stream) {
+  clear_error();
+  if (!h) return RPT_EINVAL;
+  const hipStream_t st = as_stream(stream);
+  const size_t n = (size_t)h->n_in;
+  auto cp = [&](void* dst, const void* src, size_t es) -> int32_t {
+    if (dst && src && n) RPT_HIP(hipMemcpyAsync(dst, src, n * es, hipMemcpyDeviceToDevice, st));
+    return RPT_OK;
+  };
+  const bool l = h->land_applied;
+  RPT_TRY(cp(x, l ? h->x2.p : h->x.p, 4));
+  RPT_TRY(cp(y, l ? h->y2.p : h->y.p, 4));
+  RPT_TRY(cp(intensity, l ? h->v2.p : h->v.p, 4));
+  RPT_TRY(cp(gain, l ? h->g2.p : h->g.p, 4));
+  RPT_TRY(cp(point_frame, l ? h->pf2.p : h->pf.p, 4));
+  RPT_TRY(cp(labels, h->labels.p, 4));
+  return RPT_OK;
+}
+
+}  // extern "C"

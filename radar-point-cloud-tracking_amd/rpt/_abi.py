@@ -85,6 +85,42 @@ class SynthParams(C.Structure):
     ]
 
 
+class StackParams(C.Structure):
+    _fields_ = [
+        ("n_frames", C.c_int32),
+        ("files_per_frame", C.c_int32),
+        ("rows", C.c_int32),
+        ("bins", C.c_int32),
+        ("echo_dtype", C.c_int32),
+        ("threshold", C.c_float),
+        ("stride", C.c_int32),
+        ("land_filter", C.c_int32),
+        ("land_resolution", C.c_double),
+        ("land_persistence", C.c_double),
+        ("land_min_intensity", C.c_double),
+        ("eps_space", C.c_double),
+        ("eps_time", C.c_double),
+        ("min_samples", C.c_int32),
+        ("timing", C.c_int32),
+    ]
+
+
+class StackResult(C.Structure):
+    _fields_ = [
+        ("n_points", C.c_int64),
+        ("n_clustered", C.c_int64),
+        ("n_land_cells", C.c_int64),
+        ("n_segments", C.c_int64),
+        ("n_built", C.c_int32),
+        ("n_clusters", C.c_int32),
+        ("ms_polar", C.c_double),
+        ("ms_land", C.c_double),
+        ("ms_stdbscan", C.c_double),
+        ("ms_summaries", C.c_double),
+        ("dbscan", StdbscanStats),
+    ]
+
+
 # (name, restype, argtypes)
 _SIGS = [
     ("rpt_version", C.c_int32, []),
@@ -127,6 +163,15 @@ _SIGS = [
     ("rpt_cluster_summaries", C.c_int32,
      [vp, vp, vp, vp, vp, C.c_int64, C.c_int32, C.c_int32, vp, vp, vp, vp, vp, vp, vp, vp,
       c_i64p, vp]),
+    ("rpt_arange_edges", C.c_int32, [C.c_float, C.c_float, C.c_double, c_f64p, C.c_int32]),
+    ("rpt_stack_create", vp, []),
+    ("rpt_stack_destroy", None, [vp]),
+    ("rpt_stack_run", C.c_int32, [vp, C.POINTER(StackParams), vp, vp, vp, vp, vp,
+                                  C.POINTER(StackResult), vp]),
+    ("rpt_stack_frame_offsets", C.c_int32, [vp, C.c_int32, c_i64p]),
+    ("rpt_stack_segments", C.c_int32, [vp, c_i32p, c_i32p, c_i64p, c_i64p, c_f32p, c_f32p, c_f32p,
+                                       c_i64p]),
+    ("rpt_stack_points", C.c_int32, [vp, vp, vp, vp, vp, vp, vp, vp]),
     ("rpt_order_clusters", C.c_int32, [C.c_int32, C.c_int64, c_i32p, c_i32p, c_i64p, c_i64p,
                                         c_i64p, c_i64p]),
     ("rpt_set_order", C.c_int32, [c_i32p, C.c_int32, c_i32p]),

@@ -8,8 +8,10 @@
   K9  per-(frame, label) summaries                           :508-536
   host C++: cluster order (CPython set), Hungarian tracker   :519, :543-688, loop :984-991
 
-Every arithmetic step runs in librpt (HIP kernels or host C++); torch provides the buffers and
-the stream.  Host syncs per run: file offsets, grid bounds (x2), kept count, segment count.
+Every arithmetic step runs in librpt (HIP kernels or host C++): the device stages are ONE native
+call (rpt_stack_run, csrc/stack.cpp) whose size readbacks (file offsets, land bounds, kept count,
+grid bounds, segment count) are pinned-memory syncs inside C++; torch provides the echo and the
+stream.
 """
 from __future__ import annotations
 
@@ -22,9 +24,10 @@ import numpy as np
 import torch
 
 from . import _abi
-from ._device import require_gpu
+from ._device import require_gpu, stream_handle
 from .native_tracker import NativeTracker
-from .stages import LAND_GRID_RESOLUTION, HipOps, order_and_track
+from .stages import (LAND_GRID_RESOLUTION, LAND_MIN_INTENSITY, LAND_PERSISTENCE_THRESHOLD,
+                     order_and_track)
 
 
 @dataclass
@@ -86,7 +89,8 @@ class FrameStackPipeline:
             raise ValueError("gains must be in ascending order (build_frame iterates sorted gains)")
         self.rows, self.bins = rows, bins
         self.p = params or PathParams()
-        self.ops = HipOps(self.dev)
+        self.lib = _abi.load()
+        self._h = self.lib.rpt_stack_create()
         self.timing = timing
         self._host = ThreadPoolExecutor(max_workers=host_workers) if async_host else None
         self._geo_key = None
@@ -120,69 +124,80 @@ class FrameStackPipeline:
         return dt
 
     def run(self, echo: torch.Tensor, keep_points: bool = False) -> StackResult:
-        p, ops = self.p, self.ops
+        """K1 -> land filter -> ST-DBSCAN -> K9 in one native call (rpt_stack_run), then the
+        host stage (cluster order + tracker) inline or on the worker pool (async_host)."""
+        p, lib = self.p, self.lib
         G = len(self.gains)
         F = echo.shape[0]
         dt = self._check(echo)
         echo = echo.contiguous()
-        ev = []
-
-        def mark(name):
-            if self.timing:
-                e = torch.cuda.Event(enable_timing=True)
-                e.record()
-                ev.append((name, e))
-        mark("start")
-        pts = ops.polar(echo, dt, self.rows, self.bins, self.geo, self.gain_d, p.threshold,
-                        p.stride, G)
-        N = pts.n
-        built = np.nonzero(np.diff(pts.frame_off) > 0)[0]   # build_frame returns None if empty
-        mark("polar")
-        n_land = 0
-        if p.land_filter and len(built) > 10 and N > 0:
-            x0, x1, y0, y1 = ops.bounds(pts)
-            xe = np.arange(x0, x1 + LAND_GRID_RESOLUTION, LAND_GRID_RESOLUTION)
-            ye = np.arange(y0, y1 + LAND_GRID_RESOLUTION, LAND_GRID_RESOLUTION)
-            cnt, tot = ops.land_grid(pts, xe, ye)
-            pts, n_land = ops.land_apply(pts, cnt, tot, len(built), xe, ye)
-        mark("land")
-        n_in = pts.n
-        if n_in == 0:
-            raise ValueError("Found array with 0 sample(s) (shape=(0, 2)) while a minimum of 1 "
-                             "is required.")
-        t = ops.frame_times(pts, 0)
-        labels, sts = ops.stdbscan(pts.x, pts.y, t, p.eps_space, p.eps_time, p.min_samples,
-                                   timing=self.timing)
-        n_clusters = int(sts.n_clusters)
-        mark("stdbscan")
-        seg, first_noise = ops.summaries(pts, labels, n_clusters)
-        mark("summaries")
+        sp = _abi.StackParams(F, G, self.rows, self.bins, dt, float(np.float32(p.threshold)),
+                              int(p.stride), 1 if p.land_filter else 0, LAND_GRID_RESOLUTION,
+                              LAND_PERSISTENCE_THRESHOLD, float(LAND_MIN_INTENSITY),
+                              float(p.eps_space), float(p.eps_time), int(p.min_samples),
+                              1 if self.timing else 0)
+        r = _abi.StackResult()
+        scale_d, cos_d, sin_d = self.geo
+        _abi.check(lib.rpt_stack_run(self._h, _abi.C.byref(sp), echo.data_ptr(),
+                                     scale_d.data_ptr(), cos_d.data_ptr(), sin_d.data_ptr(),
+                                     self.gain_d.data_ptr(), _abi.C.byref(r),
+                                     stream_handle(self.dev)), "rpt_stack_run")
+        fo = np.empty(F + 1, np.int64)
+        _abi.check(lib.rpt_stack_frame_offsets(self._h, 0, fo.ctypes.data_as(_abi.c_i64p)))
+        built = np.nonzero(np.diff(fo) > 0)[0]   # build_frame returns None if empty
+        S = int(r.n_segments)
+        seg = {"frame": np.empty(S, np.int32), "label": np.empty(S, np.int32),
+               "count": np.empty(S, np.int64), "first": np.empty(S, np.int64),
+               "cx": np.empty(S, np.float32), "cy": np.empty(S, np.float32),
+               "mi": np.empty(S, np.float32)}
+        first_noise = np.empty(F, np.int64)
+        ptr = lambda a, t: a.ctypes.data_as(t)  # noqa: E731
+        _abi.check(lib.rpt_stack_segments(
+            self._h, ptr(seg["frame"], _abi.c_i32p), ptr(seg["label"], _abi.c_i32p),
+            ptr(seg["count"], _abi.c_i64p), ptr(seg["first"], _abi.c_i64p),
+            ptr(seg["cx"], _abi.c_f32p), ptr(seg["cy"], _abi.c_f32p), ptr(seg["mi"], _abi.c_f32p),
+            ptr(first_noise, _abi.c_i64p)))
+        stage_ms = {}
+        if self.timing:
+            d = r.dbscan
+            stage_ms = {"polar": r.ms_polar, "land": r.ms_land, "stdbscan": r.ms_stdbscan,
+                        "summaries": r.ms_summaries, "dbscan_grid": d.ms_grid,
+                        "dbscan_core": d.ms_core, "dbscan_union": d.ms_union,
+                        "dbscan_label": d.ms_label}
+        self.last_stats = r.dbscan
+        res = StackResult(n_points=int(r.n_points), n_clustered_input=int(r.n_clustered),
+                          frame_ids=built, n_land_cells=int(r.n_land_cells),
+                          n_clusters=int(r.n_clusters), n_segments=S, seg=seg,
+                          frame_order_offsets=None, frame_order=None, tracker=None,
+                          stage_ms=stage_ms, first_noise=first_noise)
 
         def host_stage():
             t0 = time.perf_counter()
-            fo, order, trk = order_and_track(F, built, seg, first_noise, p)
-            return fo, order, trk, (time.perf_counter() - t0) * 1e3
+            fo_, order, trk = order_and_track(F, built, seg, first_noise, p)
+            return fo_, order, trk, (time.perf_counter() - t0) * 1e3
 
-        stage_ms = {}
-        if self.timing:
-            torch.cuda.synchronize(self.dev)
-            for (a, ea), (b, eb) in zip(ev[:-1], ev[1:]):
-                stage_ms[b] = ea.elapsed_time(eb)
-            stage_ms.update({"dbscan_grid": sts.ms_grid, "dbscan_core": sts.ms_core,
-                             "dbscan_union": sts.ms_union, "dbscan_label": sts.ms_label})
-        self.last_stats = sts
-        res = StackResult(n_points=N, n_clustered_input=n_in, frame_ids=built,
-                          n_land_cells=n_land, n_clusters=n_clusters, n_segments=len(seg["frame"]),
-                          seg=seg, frame_order_offsets=None, frame_order=None, tracker=None,
-                          stage_ms=stage_ms, first_noise=first_noise)
         if self._host is not None:
             res._pending = self._host.submit(host_stage)
         else:
-            fo, order, trk, host_ms = host_stage()
-            res.frame_order_offsets, res.frame_order, res.tracker = fo, order, trk
+            fo_, order, trk, host_ms = host_stage()
+            res.frame_order_offsets, res.frame_order, res.tracker = fo_, order, trk
             if self.timing:
                 stage_ms["tracker_host"] = host_ms
         if keep_points:
-            res.labels = labels
-            res.points = {"x": pts.x, "y": pts.y, "v": pts.v, "gain": pts.g, "frame": pts.pf}
+            n = res.n_clustered_input
+            pts = {k: torch.empty(n, dtype=dt_, device=self.dev) for k, dt_ in
+                   (("x", torch.float32), ("y", torch.float32), ("v", torch.float32),
+                    ("gain", torch.int32), ("frame", torch.int32))}
+            labels = torch.empty(n, dtype=torch.int32, device=self.dev)
+            _abi.check(lib.rpt_stack_points(self._h, pts["x"].data_ptr(), pts["y"].data_ptr(),
+                                            pts["v"].data_ptr(), pts["gain"].data_ptr(),
+                                            pts["frame"].data_ptr(), labels.data_ptr(),
+                                            stream_handle(self.dev)), "rpt_stack_points")
+            res.labels, res.points = labels, pts
         return res
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self.lib.rpt_stack_destroy(h)
+            self._h = None

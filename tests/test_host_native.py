@@ -177,3 +177,25 @@ def test_native_tracker_random_vs_oracle():
         for x, y in zip(a, b):
             np.testing.assert_array_equal(np.vstack(x.positions), np.vstack(y.positions))
             assert x.frames_seen == y.frames_seen
+
+
+def test_arange_edges_match_numpy():
+    """rpt_arange_edges (used by the native stack driver for the land grid) == np.arange(lo,
+    hi + 5.0, 5.0) on float32 bounds, incl. lengths near integral (stop - lo) / 5."""
+    from rpt import _abi
+
+    lib = _abi.load()
+    rng = np.random.default_rng(7)
+    out = np.empty(4096, np.float64)
+    for it in range(20000):
+        if it % 3 == 0:
+            a = np.float32(rng.uniform(-300, 300))
+            b = np.float32(rng.uniform(a, 400))
+        else:
+            a = np.float32(rng.uniform(-1000, 0))
+            b = np.float32(a + np.float32(rng.integers(0, 100)) * np.float32(5.0) +
+                           np.float32(rng.choice([0.0, 1e-5, -1e-5, 2.5])))
+        exp = np.arange(a, b + 5.0, 5.0)
+        n = lib.rpt_arange_edges(float(a), float(b), 5.0, out.ctypes.data_as(_abi.c_f64p), 4096)
+        assert n == len(exp)
+        np.testing.assert_array_equal(out[:n], exp)
