@@ -343,6 +343,17 @@ __device__ __forceinline__ int wave_sum(int v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
   return v;
 }
+__device__ __forceinline__ int wave_excl_sum(int v, int* total) {
+  const int lane = threadIdx.x & 63;
+  int incl = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += o;
+  }
+  *total = __shfl(incl, 63, 64);
+  return incl - v;
+}
 __device__ __forceinline__ int64_t wave_min64(int64_t v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -593,10 +604,13 @@ __device__ __forceinline__ int32_t rep_id(const int64_t* __restrict__ reps, int6
 // same-address atomics per launch otherwise serialise in L2).  Order inside a tile is
 // thread-major; consumers do not depend on the order.
 constexpr int kItems = 16;
-template <class P>
+struct AppendIndex {
+  __device__ int32_t operator()(int64_t s) const { return (int32_t)s; }
+};
+template <class P, class V = AppendIndex>
 __device__ __forceinline__ void block_append(int64_t tile0, int64_t n, P&& pred,
                                              int32_t* __restrict__ list,
-                                             int32_t* __restrict__ counter) {
+                                             int32_t* __restrict__ counter, V value = V{}) {
   __shared__ int s_wsum[kBlock / 64];
   __shared__ int s_base;
   uint32_t bits = 0;
@@ -629,7 +643,7 @@ __device__ __forceinline__ void block_append(int64_t tile0, int64_t n, P&& pred,
   while (bits) {
     const int k = __ffs(bits) - 1;
     bits &= bits - 1;
-    list[o++] = (int32_t)(tile0 + (int64_t)k * kBlock + threadIdx.x);
+    list[o++] = value(tile0 + (int64_t)k * kBlock + threadIdx.x);
   }
   __syncthreads();  // s_wsum / s_base reuse by the next tile
 }
@@ -729,41 +743,245 @@ __device__ __forceinline__ float4 shfl_f4(const float4& v, int l) {
   return make_float4(__shfl(v.x, l), __shfl(v.y, l), __shfl(v.z, l), __shfl(v.w, l));
 }
 
+// Box-box classification of two cells with the pair test's rounding (monotone bounds):
+// 0 no pair can be adjacent, 1 every pair is adjacent, 2 undecided.
+template <int D>
+__device__ __forceinline__ int classify_cells(const float4& A1, const float4& B1,
+                                              const float4& A2, const float4& B2,
+                                              const Geom& g) {
+  auto gap = [](float a0, float a1, float b0, float b1) -> float {
+    return (b0 > a1) ? (b0 - a1) : ((a0 > b1) ? (a0 - b1) : 0.f);
+  };
+  auto gapd = [](float a0, float a1, float b0, float b1) -> double {
+    return (b0 > a1) ? ((double)b0 - (double)a1) : ((a0 > b1) ? ((double)a0 - (double)b1) : 0.0);
+  };
+  const float tg = gap(A2.z, A2.w, B2.z, B2.w);
+  if (!(tg <= g.epst)) return 0;
+  const float tm = fmaxf(fabsf(B2.w - A2.z), fabsf(A2.w - B2.z));
+  const double gx = gapd(A1.x, A1.y, B1.x, B1.y), gy = gapd(A1.z, A1.w, B1.z, B1.w);
+  double dmin = gx * gx + gy * gy;
+  const double mx = fmax(fabs((double)B1.y - (double)A1.x), fabs((double)A1.y - (double)B1.x));
+  const double my = fmax(fabs((double)B1.w - (double)A1.z), fabs((double)A1.w - (double)B1.z));
+  double dmax = mx * mx + my * my;
+  if (D == 3) {
+    const double gz = gapd(A2.x, A2.y, B2.x, B2.y);
+    dmin = dmin + gz * gz;
+    const double mz = fmax(fabs((double)B2.y - (double)A2.x), fabs((double)A2.y - (double)B2.x));
+    dmax = dmax + mz * mz;
+  }
+  if (!(dmin <= g.eps2)) return 0;
+  return (dmax <= g.eps2 && tm <= g.epst) ? 1 : 2;
+}
+
 // ---------------------------------------------------------------- K5: core flags
 constexpr int kR = 4;  // candidate cells per lane per super-round of the window scans
 
-// Level 1, one thread per point: a point whose own cell is mutual and holds >= min_samples points
-// is core (all of them are its neighbours) — the bulk of a radar stack.  Every other point is
-// queued for level 2.
-__global__ __launch_bounds__(kBlock) void k_core_fast(const int32_t* __restrict__ skey,
-                                                     int64_t n, Geom g,
-                                                     const int32_t* __restrict__ cell_start,
-                                                     const uint8_t* __restrict__ mutual,
+// Level 1, one thread per occupied cell: a mutual cell (every pair adjacent) holding >=
+// min_samples points is all core — the bulk of a radar stack.  Every other cell is queued for
+// level 2 (the queue holds cell keys).  cflag (int32 per cell): 1 all core, 0 none, 2 decided
+// per point (level 4).
+__global__ __launch_bounds__(kBlock) void k_core_cell_fast(const int32_t* __restrict__ occ,
+                                                          const int32_t* __restrict__ n_occ,
+                                                          Geom g,
+                                                          const int32_t* __restrict__ cell_start,
+                                                          const uint8_t* __restrict__ mutual,
+                                                          int32_t* __restrict__ cflag,
+                                                          int32_t* __restrict__ queue,
+                                                          int32_t* __restrict__ n_queue) {
+  const int need = g.min_samples;
+  const int64_t no = *n_occ;
+  for (int64_t tile = (int64_t)blockIdx.x * kBlock * kItems; tile < no;
+       tile += (int64_t)gridDim.x * kBlock * kItems) {
+    block_append(
+        tile, no,
+        [&](int64_t q) -> bool {
+          const int32_t c = occ[q];
+          if ((int64_t)c >= g.cells || need <= 0) {  // non-finite time: no neighbours at all
+            cflag[c] = (need <= 0) ? 1 : 0;
+            return false;
+          }
+          if (mutual[c] && cell_start[c + 1] - cell_start[c] >= need) {
+            cflag[c] = 1;
+            return false;
+          }
+          return true;
+        },
+        queue, n_queue, [&](int64_t q) -> int32_t { return occ[q]; });
+  }
+}
+
+// Level 2, one wave per queued cell A: lanes classify A's candidate cells against A's box
+// (classify_cells: the pair test's rounding, monotone bounds).  Cells adjacent to every point of
+// A give a count shared by all of A's points (a lower bound, self included); cells that may hold
+// a neighbour give an upper bound.  Most sparse cells are decided here (flag 1 or 0) without
+// touching a point; the rest get flag 2.
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_core_cell_window(Geom g,
+                                                            const int32_t* __restrict__ occ,
+                                                            const CellRec<D>* __restrict__ crec,
+                                                            const uint32_t* __restrict__ occ_bits,
+                                                            const float2* __restrict__ slab_t,
+                                                            const int32_t* __restrict__ queue,
+                                                            const int32_t* __restrict__ n_queue,
+                                                            int32_t* __restrict__ cflag) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+  const int64_t nq = *n_queue;
+  const int need = g.min_samples;
+  for (int64_t q = w0; q < nq; q += nw) {
+    const int32_t ca = queue[q];
+    const CellRec<D> ra = crec[ca];
+    const float4 A1 = rec_boxA<D>(ra), A2 = rec_boxB(ra);
+    int cx, cy, cz;
+    decode_key<D>(ca, g, cx, cy, cz);
+    const Window w = make_window<D, true>(cx, cy, cz, A2.z, A2.w, g, slab_t);
+    int lo = 0, hi = 0;
+    for (int base = 0; base < w.total && lo < need; base += 64 * kR) {
+      int64_t c[kR];
+      uint32_t wb[kR];
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        const int qq = base + r * 64 + lane;
+        c[r] = (qq < w.total) ? window_cell<D>(w, qq, g, slab_t, A2.z, A2.w) : -1;
+      }
+#pragma unroll
+      for (int r = 0; r < kR; ++r) wb[r] = (c[r] >= 0) ? occ_bits[c[r] >> 5] : 0u;
+      int l = 0, h = 0;
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        if (c[r] >= 0 && ((wb[r] >> (c[r] & 31)) & 1u)) {
+          const CellRec<D> cr = crec[c[r]];
+          const int cls = classify_cells<D>(A1, rec_boxA<D>(cr), A2, rec_boxB(cr), g);
+          l += (cls == 1) ? cr.e - cr.b : 0;
+          h += (cls != 0) ? cr.e - cr.b : 0;
+        }
+      }
+      lo += wave_sum(l);
+      hi += wave_sum(h);
+    }
+    // an early exit leaves hi partial, but lo >= need already decides
+    if (lane == 0) cflag[ca] = (lo >= need) ? 1 : ((hi < need) ? 0 : 2);
+  }
+}
+
+// 2-D grids whose slab window is at most 7 slabs (R <= 3): K5 levels 1-3 in one kernel, EIGHT
+// lanes per occupied cell.  A mutual cell with >= min_samples points is all core (the bulk);
+// otherwise lane j < 2R+1 owns slab cs - R + j of the cell's window.  The window comes from the
+// cell's slab alone (R = ceil(eps_t / slab) + 1 slabs each side, pruned with the slabs' actual
+// time ranges), so a lane loads its slab's range and the occupancy words of its 5 rows together
+// with the cell's record, then the records of its (few) occupied candidates; eight cells per wave
+// keep many short dependency chains in flight.  cflag as k_core_cell_fast / _window (level 3
+// turns it into point flags).
+constexpr int kCwMaxR = 3;
+__global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
+                                                          const int32_t* __restrict__ occ,
+                                                          const int32_t* __restrict__ n_occ,
+                                                          const CellRec<2>* __restrict__ crec,
+                                                          const uint8_t* __restrict__ mutual,
+                                                          const uint32_t* __restrict__ occ_bits,
+                                                          const float2* __restrict__ slab_t,
+                                                          int32_t* __restrict__ cflag) {
+  const int64_t no = *n_occ;
+  const int need = g.min_samples;
+  const int j = threadIdx.x & 7;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t - j < no * 8;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t q = t >> 3;
+    const bool act = q < no;
+    const int32_t ca = act ? occ[q] : 0;
+    int flag = 0, b = 0, e = 0;
+    if (act && (int64_t)ca >= g.cells) {  // non-finite time: no neighbours at all
+      flag = (need <= 0) ? 1 : 0;
+    } else if (act) {
+      const int cx = ca % g.nx;
+      const int rr = ca / g.nx;
+      const int cy = rr % g.ny;
+      const int cs = rr / g.ny;
+      const int sl = cs + j - R;
+      const bool sv = j <= 2 * R && sl >= 0 && sl < g.nt;
+      const CellRec<2> ra = crec[ca];
+      const uint8_t mu = mutual[ca];
+      b = ra.b;
+      e = ra.e;
+      const float2 own = slab_t[cs];
+      float2 sr = make_float2(1.f, 0.f);
+      uint32_t m5[5] = {0u, 0u, 0u, 0u, 0u};
+      if (sv) {
+        sr = slab_t[sl];
+        const int lo_x = cx - 2 < 0 ? 2 - cx : 0;
+        const int hi_x = cx + 2 - (g.nx - 1);
+#pragma unroll
+        for (int dy = 0; dy < 5; ++dy) {
+          const int y = cy + dy - 2;
+          if (y < 0 || y >= g.ny) continue;
+          // bit dx <-> key k0 + dx (x = cx - 2 + dx); columns outside [0, nx) are cleared
+          const int64_t k0 = ((int64_t)sl * g.ny + y) * g.nx + (cx - 2);
+          const int64_t kk = k0 < 0 ? 0 : k0;
+          const int64_t w = kk >> 5;
+          const uint64_t two = (uint64_t)occ_bits[w] | ((uint64_t)occ_bits[w + 1] << 32);
+          uint32_t m =
+              (k0 < 0) ? ((uint32_t)(two << (-k0)) & 31u) : ((uint32_t)(two >> (kk & 31)) & 31u);
+          m &= ~((1u << lo_x) - 1u);
+          if (hi_x > 0) m &= (31u >> hi_x);
+          m5[dy] = m;
+        }
+      }
+      if (need <= 0 || (mu && e - b >= need)) {
+        flag = 1;
+      } else {
+        int lo = 0, hi = 0;
+        const float gap =
+            (own.x > sr.y) ? (own.x - sr.y) : ((sr.x > own.y) ? (sr.x - own.y) : 0.f);
+        if (sv && sr.x <= sr.y && gap <= g.epst) {  // this lane's slab is in reach
+          const float4 A1 = rec_boxA<2>(ra), A2 = rec_boxB(ra);
+#pragma unroll
+          for (int dy = 0; dy < 5; ++dy) {
+            uint32_t m = m5[dy];
+            const int64_t row = ((int64_t)sl * g.ny + (cy + dy - 2)) * g.nx + (cx - 2);
+            while (m) {
+              const int dx = __builtin_ctz(m);
+              m &= m - 1u;
+              const CellRec<2> cr = crec[row + dx];
+              const int cls = classify_cells<2>(A1, rec_boxA<2>(cr), A2, rec_boxB(cr), g);
+              lo += (cls == 1) ? cr.e - cr.b : 0;
+              hi += (cls != 0) ? cr.e - cr.b : 0;
+            }
+          }
+        }
+#pragma unroll
+        for (int off = 4; off > 0; off >>= 1) {
+          lo += __shfl_xor(lo, off, 8);
+          hi += __shfl_xor(hi, off, 8);
+        }
+        flag = (lo >= need) ? 1 : ((hi < need) ? 0 : 2);
+      }
+    }
+    if (act && j == 0) cflag[ca] = flag;
+  }
+}
+
+// Level 3, one thread per point: the cell's decision; points of undecided cells are queued for
+// level 4 (block-aggregated append).
+__global__ __launch_bounds__(kBlock) void k_core_fill(const int32_t* __restrict__ skey, int64_t n,
+                                                     const int32_t* __restrict__ cflag,
                                                      uint8_t* __restrict__ core,
                                                      int32_t* __restrict__ slow,
                                                      int32_t* __restrict__ n_slow) {
-  const int need = g.min_samples;
   for (int64_t tile = (int64_t)blockIdx.x * kBlock * kItems; tile < n;
        tile += (int64_t)gridDim.x * kBlock * kItems) {
     block_append(
         tile, n,
         [&](int64_t s) -> bool {
-          const int32_t key = skey[s];
-          if ((int64_t)key >= g.cells || need <= 0) {  // non-finite time: no neighbours at all
-            core[s] = (need <= 0) ? 1 : 0;
-            return false;
-          }
-          if (mutual[key] && cell_start[key + 1] - cell_start[key] >= need) {
-            core[s] = 1;
-            return false;
-          }
-          return true;
+          const int f = cflag[skey[s]];
+          core[s] = (f == 1) ? 1 : 0;
+          return f == 2;
         },
         slow, n_slow);
   }
 }
 
-// Level 2, one wave per queued point: lanes classify up to 64 candidate cells at a time against
+// Level 4, one wave per queued point: lanes classify up to 64 candidate cells at a time against
 // the cells' boxes (whole-cell accept adds the cell's count), then every undecided cell's points
 // are tested 64 at a time; the wave stops as soon as min_samples neighbours are seen.
 template <int D>
@@ -918,36 +1136,6 @@ __global__ __launch_bounds__(kBlock) void k_parent_init(int32_t* parent, int64_t
     const int32_t k = skey[s];
     parent[s] = (core[s] && (int64_t)k < cells && mutual[k]) ? rep[k] : (int32_t)s;
   }
-}
-
-// Box-box classification of two cells with the pair test's rounding (monotone bounds):
-// 0 no pair can be adjacent, 1 every pair is adjacent, 2 undecided.
-template <int D>
-__device__ __forceinline__ int classify_cells(const float4& A1, const float4& B1,
-                                              const float4& A2, const float4& B2,
-                                              const Geom& g) {
-  auto gap = [](float a0, float a1, float b0, float b1) -> float {
-    return (b0 > a1) ? (b0 - a1) : ((a0 > b1) ? (a0 - b1) : 0.f);
-  };
-  auto gapd = [](float a0, float a1, float b0, float b1) -> double {
-    return (b0 > a1) ? ((double)b0 - (double)a1) : ((a0 > b1) ? ((double)a0 - (double)b1) : 0.0);
-  };
-  const float tg = gap(A2.z, A2.w, B2.z, B2.w);
-  if (!(tg <= g.epst)) return 0;
-  const float tm = fmaxf(fabsf(B2.w - A2.z), fabsf(A2.w - B2.z));
-  const double gx = gapd(A1.x, A1.y, B1.x, B1.y), gy = gapd(A1.z, A1.w, B1.z, B1.w);
-  double dmin = gx * gx + gy * gy;
-  const double mx = fmax(fabs((double)B1.y - (double)A1.x), fabs((double)A1.y - (double)B1.x));
-  const double my = fmax(fabs((double)B1.w - (double)A1.z), fabs((double)A1.w - (double)B1.z));
-  double dmax = mx * mx + my * my;
-  if (D == 3) {
-    const double gz = gapd(A2.x, A2.y, B2.x, B2.y);
-    dmin = dmin + gz * gz;
-    const double mz = fmax(fabs((double)B2.y - (double)A2.x), fabs((double)A2.y - (double)B2.x));
-    dmax = dmax + mz * mz;
-  }
-  if (!(dmin <= g.eps2)) return 0;
-  return (dmax <= g.eps2 && tm <= g.epst) ? 1 : 2;
 }
 
 // K6a: mutual-cell x mutual-cell unions, one wave per occupied cell A, lanes over the candidate
@@ -1526,7 +1714,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   bud.add<int32_t>(n + 1);  // occ
   bud.add<int32_t>(n + 1);  // hpos
   bud.add<CellRec<D>>(C1);  // crec
-  bud.add<uint32_t>(C1 / 32 + 1);  // occupancy bits
+  bud.add<uint32_t>(C1 / 32 + 2);  // occupancy bits
   RPT_TRY(arena.reserve(bud.bytes, st));
   (void)arena.carve_n<Bounds>(1);
   uint32_t* keys = arena.carve_n<uint32_t>(n);
@@ -1554,7 +1742,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   hpos = arena.carve_n<int32_t>(n + 1);
   CellRec<D>* cr = arena.carve_n<CellRec<D>>(C1);
   crec = cr;
-  occ_bits = arena.carve_n<uint32_t>(C1 / 32 + 1);
+  occ_bits = arena.carve_n<uint32_t>(C1 / 32 + 2);  // +1: two-word window reads
   if (!occ_bits) {
     set_error("internal: scratch carve overflow");
     return RPT_ENOMEM;
@@ -1574,7 +1762,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   RPT_CHECK_LAUNCH();
   RPT_TRY(exclusive_scan_i32(cell_start, cell_start, C1 + 1, stmp, st));
   RPT_TRY(exclusive_scan_i32(hpos, hpos, n + 1, stmp, st));
-  RPT_HIP(hipMemsetAsync(occ_bits, 0, sizeof(uint32_t) * (C1 / 32 + 1), st));
+  RPT_HIP(hipMemsetAsync(occ_bits, 0, sizeof(uint32_t) * (C1 / 32 + 2), st));
   hipLaunchKernelGGL(k_occ_list, dim3(gb), dim3(kBlock), 0, st, skey, n, hpos, occ, occ_bits);
   RPT_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_cell_box<D>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, cell_start,
@@ -1602,11 +1790,33 @@ int32_t DbscanState::build(const float* x, const float* y, const float* z, int64
 
 int32_t DbscanState::core_pass(hipStream_t st) {
   if (degenerate) return RPT_OK;
-  int32_t* slow = nc_list;  // the non-core queue is built later; reuse its storage
+  // cflag lives in rep (int32 per cell, rebuilt by union_pass); the cell queue in ccmin and the
+  // point queue in nc_list (both rebuilt later), counters in cid[n] / nc_list[n]
+  int32_t* cflag = rep;
+  int32_t* cq = ccmin;
+  int32_t* n_cq = cid + n;
+  int32_t* slow = nc_list;
   int32_t* n_slow = nc_list + n;
+  const int32_t* n_occ = hpos + n;
   RPT_HIP(hipMemsetAsync(n_slow, 0, sizeof(int32_t), st));
-  hipLaunchKernelGGL(k_core_fast, dim3(tile_grid(n)), dim3(kBlock), 0, st, skey, n, g, cell_start,
-                     mutual, core, slow, n_slow);
+  // slabs each side a cell's points can reach: eps_t / slab width, +1 for the slab's extent
+  const double rs = std::ceil((double)g.epst / g.ct) + 1.0;
+  if (dim == 2 && rs <= (double)kCwMaxR && g.nz == 1) {
+    hipLaunchKernelGGL(k_core_cells_oct, dim3(grid_for(8 * n, kBlock, 8192)), dim3(kBlock), 0,
+                       st, g, (int)rs, occ, n_occ, rec<2>(), mutual, occ_bits, slab_t, cflag);
+  } else {
+    RPT_HIP(hipMemsetAsync(n_cq, 0, sizeof(int32_t), st));
+    hipLaunchKernelGGL(k_core_cell_fast, dim3(tile_grid(n)), dim3(kBlock), 0, st, occ, n_occ, g,
+                       cell_start, mutual, cflag, cq, n_cq);
+    if (dim == 2)
+      hipLaunchKernelGGL(k_core_cell_window<2>, dim3(wave_grid(n)), dim3(kBlock), 0, st, g, occ,
+                         rec<2>(), occ_bits, slab_t, cq, n_cq, cflag);
+    else
+      hipLaunchKernelGGL(k_core_cell_window<3>, dim3(wave_grid(n)), dim3(kBlock), 0, st, g, occ,
+                         rec<3>(), occ_bits, slab_t, cq, n_cq, cflag);
+  }
+  hipLaunchKernelGGL(k_core_fill, dim3(tile_grid(n)), dim3(kBlock), 0, st, skey, n, cflag, core,
+                     slow, n_slow);
   if (dim == 2)
     hipLaunchKernelGGL(k_core_slow<2>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
                        rec<2>(), occ_bits, slab_t, slow, n_slow, core);
