@@ -249,56 +249,82 @@ __attribute__((target("avx2"))) void eq_bits_avx2(int64_t nc, const double* sp, 
   }
 }
 
-// One later Dijkstra scan over the remaining columns rem[0..n): r = ((mv + c_j) - u_i) - v_j,
-// spc_j = min(spc_j, r) (path_j = i where it drops); tmp[it] = the new spc of rem[it].  Returns
-// the minimum of tmp.
-__attribute__((target("avx2"))) double rest_scan_avx2(int64_t n, const int64_t* rem,
-                                                      const double* row, double mv, double ui,
-                                                      const double* vv, double* sp, int64_t* pa,
-                                                      int64_t i, double* tmp) {
+inline double bits_all_ones() {
+  const uint64_t u = ~0ull;
+  double d;
+  std::memcpy(&d, &u, 8);
+  return d;
+}
+
+// One later Dijkstra scan over ALL columns, masked to the remaining ones (live[j] all-ones):
+// r = ((mv + c_j) - u_i) - v_j, spc_j = min(spc_j, r) with path_j = i where it drops.  Returns
+// the minimum of the remaining columns' new spc.
+__attribute__((target("avx2"))) double rest_scan_masked_avx2(int64_t nc, const double* row,
+                                                             double mv, double ui,
+                                                             const double* vv,
+                                                             const double* live, double* sp,
+                                                             int64_t* pa, int64_t i) {
   const __m256d m = _mm256_set1_pd(mv), uv = _mm256_set1_pd(ui);
-  __m256d best = _mm256_set1_pd(std::numeric_limits<double>::infinity());
-  int64_t it = 0;
-  for (; it + 4 <= n; it += 4) {
-    const __m256i jv = _mm256_loadu_si256((const __m256i*)(rem + it));
-    const __m256d r = _mm256_sub_pd(
-        _mm256_sub_pd(_mm256_add_pd(m, _mm256_i64gather_pd(row, jv, 8)), uv),
-        _mm256_i64gather_pd(vv, jv, 8));
-    const __m256d so = _mm256_i64gather_pd(sp, jv, 8);
-    const __m256d upd = _mm256_cmp_pd(r, so, _CMP_LT_OQ);
+  const __m256d inf = _mm256_set1_pd(std::numeric_limits<double>::infinity());
+  const __m256d iv = _mm256_castsi256_pd(_mm256_set1_epi64x(i));
+  __m256d best = inf;
+  int64_t j = 0;
+  for (; j + 4 <= nc; j += 4) {
+    const __m256d r = _mm256_sub_pd(_mm256_sub_pd(_mm256_add_pd(m, _mm256_loadu_pd(row + j)), uv),
+                                    _mm256_loadu_pd(vv + j));
+    const __m256d so = _mm256_loadu_pd(sp + j);
+    const __m256d lv = _mm256_loadu_pd(live + j);
+    const __m256d upd = _mm256_and_pd(_mm256_cmp_pd(r, so, _CMP_LT_OQ), lv);
     const __m256d sj = _mm256_blendv_pd(so, r, upd);
-    _mm256_storeu_pd(tmp + it, sj);
-    best = _mm256_min_pd(sj, best);
-    int msk = _mm256_movemask_pd(upd);
-    while (msk) {
-      const int l = __builtin_ctz(msk);
-      const int64_t j = rem[it + l];
-      sp[j] = tmp[it + l];
-      pa[j] = i;
-      msk &= msk - 1;
-    }
+    _mm256_storeu_pd(sp + j, sj);
+    const __m256d po = _mm256_loadu_pd(reinterpret_cast<const double*>(pa + j));
+    _mm256_storeu_pd(reinterpret_cast<double*>(pa + j), _mm256_blendv_pd(po, iv, upd));
+    best = _mm256_min_pd(_mm256_blendv_pd(inf, sj, lv), best);
   }
   __m128d lo = _mm_min_pd(_mm256_castpd256_pd128(best), _mm256_extractf128_pd(best, 1));
   double mn = _mm_cvtsd_f64(_mm_min_sd(lo, _mm_unpackhi_pd(lo, lo)));
-  for (; it < n; ++it) {
-    const int64_t j = rem[it];
+  for (; j < nc; ++j) {
+    uint64_t lb;
+    std::memcpy(&lb, live + j, 8);
+    if (!lb) continue;
     const double r = mv + row[j] - ui - vv[j];
     if (r < sp[j]) {
       sp[j] = r;
       pa[j] = i;
     }
-    tmp[it] = sp[j];
-    mn = tmp[it] < mn ? tmp[it] : mn;
+    mn = sp[j] < mn ? sp[j] : mn;
   }
   return mn;
+}
+
+// bit j of bits = (sp[j] == mn) for the remaining columns
+__attribute__((target("avx2"))) void eq_bits_live_avx2(int64_t nc, const double* sp, double mn,
+                                                       const double* live, uint64_t* bits) {
+  const __m256d m = _mm256_set1_pd(mn);
+  for (int64_t w = 0; w * 64 < nc; ++w) {
+    const int64_t e = std::min<int64_t>(nc, w * 64 + 64);
+    uint64_t acc = 0;
+    int64_t j = w * 64;
+    for (; j + 4 <= e; j += 4)
+      acc |= (uint64_t)_mm256_movemask_pd(_mm256_and_pd(
+                 _mm256_cmp_pd(_mm256_loadu_pd(sp + j), m, _CMP_EQ_OQ), _mm256_loadu_pd(live + j)))
+             << (j & 63);
+    for (; j < e; ++j) {
+      uint64_t lb;
+      std::memcpy(&lb, live + j, 8);
+      acc |= (uint64_t)(lb && sp[j] == mn) << (j & 63);
+    }
+    bits[w] |= acc;
+  }
 }
 
 }  // namespace
 
 struct Lsap {
   std::vector<double> u, v, spc, tmp, scan;
-  std::vector<int64_t> path, col4row, row4col, remaining, idx, sr_list, sc_list;
+  std::vector<int64_t> path, col4row, row4col, remaining, idx, sr_list, sc_list, pos;
   std::vector<uint64_t> eqbits;
+  std::vector<double> live;   // all-ones bit pattern: column still in rem (masked scans)
 
   // One shortest augmenting path from row i (scipy's augmenting_path).  The rows / columns it
   // visits are recorded in sr_list / sc_list (scipy's SR / SC flags) so that the dual updates
@@ -362,36 +388,31 @@ struct Lsap {
         first = false;
       } else if (host_has_avx2()) {
         // Later scans: the new spc values do not depend on the scan order, so they are computed
-        // lane-parallel into tmp[it]; the sequential selection rule is then applied to the
-        // positions at the minimum: the first one, replaced by the last later one whose column
+        // for all columns at once (contiguous, masked to the remaining ones: no gathers); the
+        // sequential selection rule is then applied by rem position: among the remaining columns
+        // at the minimum, the first in scan order, replaced by the last later one whose column
         // is unassigned.
-        scan.resize((size_t)nc);
-        const double mn = rest_scan_avx2(num_remaining, rem, row, minVal, ui, vv, sp, pa, i,
-                                         scan.data());
+        const double mn =
+            rest_scan_masked_avx2(nc, row, minVal, ui, vv, live.data(), sp, pa, i);
         lowest = mn;
         index = -1;
         if (mn != std::numeric_limits<double>::infinity()) {
-          eqbits.assign((size_t)((num_remaining + 63) >> 6), 0);
-          eq_bits_avx2(num_remaining, scan.data(), mn, eqbits.data());
-          int64_t p0 = -1;
+          eqbits.assign((size_t)((nc + 63) >> 6), 0);
+          eq_bits_live_avx2(nc, sp, mn, live.data(), eqbits.data());
+          int64_t p0 = std::numeric_limits<int64_t>::max();
           for (size_t w = 0; w < eqbits.size(); ++w)
-            if (eqbits[w]) {
-              p0 = (int64_t)w * 64 + __builtin_ctzll(eqbits[w]);
-              break;
+            for (uint64_t bb = eqbits[w]; bb; bb &= bb - 1) {
+              const int64_t pj = pos[(int64_t)w * 64 + __builtin_ctzll(bb)];
+              p0 = pj < p0 ? pj : p0;
             }
           index = p0;
-          for (int64_t w = (int64_t)eqbits.size() - 1; w >= 0 && index == p0; --w) {
-            uint64_t b = eqbits[w];
-            while (b) {
-              const int64_t p = w * 64 + 63 - __builtin_clzll(b);
-              if (p <= p0) break;
-              if (r4c[rem[p]] == -1) {
-                index = p;
-                break;
-              }
-              b &= ~(1ull << (p & 63));
+          int64_t best = -1;
+          for (size_t w = 0; w < eqbits.size(); ++w)
+            for (uint64_t bb = eqbits[w]; bb; bb &= bb - 1) {
+              const int64_t j = (int64_t)w * 64 + __builtin_ctzll(bb);
+              if (pos[j] > p0 && r4c[j] == -1 && pos[j] > best) best = pos[j];
             }
-          }
+          if (best >= 0) index = best;
         }
       } else {
         for (int64_t it = 0; it < num_remaining; ++it) {
@@ -414,9 +435,25 @@ struct Lsap {
       else
         i = r4c[j];
       sc_list.push_back(j);
-      if (scan0 && sink == -1)
+      if (scan0 && sink == -1) {
         for (int64_t it = 0; it < nc; ++it) rem[it] = nc - it - 1;
-      if (sink == -1) rem[index] = rem[--num_remaining];
+        if (host_has_avx2()) {  // rem positions and the remaining-column mask of the masked scans
+          live.assign((size_t)nc, -1.0);
+          const double ones = bits_all_ones();
+          for (int64_t c2 = 0; c2 < nc; ++c2) {
+            pos[c2] = nc - 1 - c2;
+            live[c2] = ones;
+          }
+        }
+      }
+      if (sink == -1) {
+        if (host_has_avx2()) {
+          live[j] = 0.0;
+          pos[rem[num_remaining - 1]] = index;
+          pos[j] = -1;
+        }
+        rem[index] = rem[--num_remaining];
+      }
     }
     *p_min = minVal;
     return sink;
@@ -448,6 +485,8 @@ struct Lsap {
     col4row.assign(nr, -1);
     row4col.assign(nc, -1);
     remaining.resize(nc);
+    pos.resize(nc);
+    live.resize(nc);
     for (int64_t cur = 0; cur < nr; ++cur) {
       double minVal;
       const int64_t sink = augmenting_path(nc, cost, cur, &minVal);
