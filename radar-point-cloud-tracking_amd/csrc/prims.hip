@@ -110,21 +110,6 @@ __device__ __forceinline__ int64_t block_exclusive_scan(int64_t v, int64_t* tota
   return wprefix + incl - v;
 }
 
-template <class T>
-__global__ __launch_bounds__(kScanBlock) void k_scan_reduce(const T* __restrict__ in, int64_t n,
-                                                           int64_t* __restrict__ partial) {
-  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
-  int64_t s = 0;
-#pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
-    int64_t i = base + k;
-    if (i < n) s += (int64_t)in[i];
-  }
-  int64_t tot;
-  (void)block_exclusive_scan(s, &tot);
-  if (threadIdx.x == 0) partial[blockIdx.x] = tot;
-}
-
 template <class T, class U>
 __global__ __launch_bounds__(kScanBlock) void k_scan_apply(const T* __restrict__ in, int64_t n,
                                                           const int64_t* __restrict__ partial,
@@ -148,6 +133,96 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_apply(const T* __restrict__
   }
 }
 
+// Single-pass form (decoupled look-back): tiles of kLbTile items are taken in ticket order; a
+// tile publishes its aggregate, then its inclusive prefix once its predecessors' are known.  The
+// status words are 64-bit granules {flag:2 | value:62} written and read with agent-scope relaxed
+// atomics: the data IS the flag (MI355X guide §6 Guideline 16, R2), so no fences.  Values are
+// non-negative (counts, flags) and their running total is < 2^62.  Every spin is bounded.
+constexpr int kLbItems = 16;
+constexpr int kLbTile = kScanBlock * kLbItems;  // 4096
+constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = (1ull << 62) - 1;
+
+template <class T, class U>
+__global__ __launch_bounds__(kScanBlock) void k_scan_lb(const T* __restrict__ in, int64_t n,
+                                                       U* __restrict__ out,
+                                                       uint64_t* __restrict__ status,
+                                                       uint32_t* __restrict__ ticket) {
+  __shared__ uint32_t s_tile;
+  __shared__ int64_t s_prefix;
+  if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
+  __syncthreads();
+  const int64_t tile = s_tile;
+  const int64_t base = tile * kLbTile + (int64_t)threadIdx.x * kLbItems;
+  int64_t v[kLbItems];
+  int64_t sum = 0;
+  if (base + kLbItems <= n) {
+#pragma unroll
+    for (int k = 0; k < kLbItems; ++k) {
+      v[k] = (int64_t)in[base + k];
+      sum += v[k];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kLbItems; ++k) {
+      v[k] = (base + k < n) ? (int64_t)in[base + k] : 0;
+      sum += v[k];
+    }
+  }
+  int64_t tot;
+  const int64_t excl = block_exclusive_scan(sum, &tot);
+  if (threadIdx.x < kWave) {
+    const int lane = threadIdx.x;
+    if (lane == 0)
+      __hip_atomic_store(status + tile, (tile == 0 ? kLbInc : kLbAgg) | (uint64_t)tot,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int64_t prefix = 0;
+    int64_t j = tile - 1;  // nearest predecessor not yet accounted for
+    uint32_t spins = 0;
+    while (j >= 0) {
+      const int64_t idx = j - lane;
+      const uint64_t st = (idx >= 0) ? __hip_atomic_load(status + idx, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)
+                                     : kLbInc;  // before tile 0: an inclusive zero
+      const uint64_t inc = __ballot((st >> 62) == 2u);
+      const uint64_t zero = __ballot((st >> 62) == 0u);
+      const int first_inc = inc ? __ffsll((unsigned long long)inc) - 1 : kWave;
+      const uint64_t upto = (first_inc >= kWave - 1) ? ~0ull : ((2ull << first_inc) - 1ull);
+      if (zero & upto) {  // a predecessor before the nearest inclusive one is not published yet
+        if (++spins > (1u << 24)) break;  // bounded: a lost tile gives a wrong sum, not a hang
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      int64_t part = (lane <= first_inc && idx >= 0) ? (int64_t)(st & kLbVal) : 0;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
+      prefix += part;
+      if (first_inc < kWave) break;
+      j -= kWave;
+    }
+    if (lane == 0) {
+      if (tile > 0)
+        __hip_atomic_store(status + tile, kLbInc | (uint64_t)(prefix + tot), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      s_prefix = prefix;
+    }
+  }
+  __syncthreads();
+  int64_t run = s_prefix + excl;
+  if (base + kLbItems <= n) {
+#pragma unroll
+    for (int k = 0; k < kLbItems; ++k) {
+      out[base + k] = (U)run;
+      run += v[k];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kLbItems; ++k) {
+      if (base + k < n) out[base + k] = (U)run;
+      run += v[k];
+    }
+  }
+}
+
 size_t scan_tmp_elems(int64_t n) {
   size_t total = 0;
   int64_t m = n;
@@ -159,23 +234,22 @@ size_t scan_tmp_elems(int64_t n) {
 }
 
 template <class T, class U>
-static int32_t scan_impl(const T* in, U* out, int64_t n, int64_t* tmp, hipStream_t st) {
+static int32_t scan_impl(const T* in, U* out, int64_t n, int64_t* tmp, hipStream_t stream) {
   if (n <= 0) return RPT_OK;
   const int64_t nb = (n + kScanTile - 1) / kScanTile;
   if (nb == 1) {
-    hipLaunchKernelGGL((k_scan_apply<T, U>), dim3(1), dim3(kScanBlock), 0, st, in, n,
+    hipLaunchKernelGGL((k_scan_apply<T, U>), dim3(1), dim3(kScanBlock), 0, stream, in, n,
                        (const int64_t*)nullptr, out);
     RPT_CHECK_LAUNCH();
     return RPT_OK;
   }
-  int64_t* partial = tmp;
-  int64_t* rest = tmp + nb + 64;
-  hipLaunchKernelGGL(k_scan_reduce<T>, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n,
-                     partial);
-  RPT_CHECK_LAUNCH();
-  RPT_TRY((scan_impl<int64_t, int64_t>(partial, partial, nb, rest, st)));
-  hipLaunchKernelGGL((k_scan_apply<T, U>), dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n,
-                     (const int64_t*)partial, out);
+  // one pass: status granules + ticket in tmp (scan_tmp_elems(n) >= n / 2048 + 64 words)
+  const int64_t nt = (n + kLbTile - 1) / kLbTile;
+  uint64_t* status = reinterpret_cast<uint64_t*>(tmp);
+  uint32_t* ticket = reinterpret_cast<uint32_t*>(tmp + nt);
+  RPT_HIP(hipMemsetAsync(tmp, 0, sizeof(int64_t) * (size_t)(nt + 1), stream));
+  hipLaunchKernelGGL((k_scan_lb<T, U>), dim3((unsigned)nt), dim3(kScanBlock), 0, stream, in, n,
+                     out, status, ticket);
   RPT_CHECK_LAUNCH();
   return RPT_OK;
 }

@@ -169,30 +169,55 @@ __device__ __forceinline__ float seq_sum(const float* __restrict__ g, int b, int
     }
     const float4* sb4 = reinterpret_cast<const float4*>(sb);
     if (i + 8 * V <= m) {
-      float4 cur[V], nxt[V];
+      // ping-pong register batches: the next 4V elements are read from LDS while the chain
+      // consumes the current ones (no register copies between batches)
+      float4 pa[V], pb[V];
 #pragma unroll
-      for (int u = 0; u < V; ++u) cur[u] = sb4[i / 4 + u];
-      for (; i + 8 * V <= m; i += 4 * V) {
+      for (int u = 0; u < V; ++u) pa[u] = sb4[i / 4 + u];
+      while (true) {
 #pragma unroll
-        for (int u = 0; u < V; ++u) nxt[u] = sb4[i / 4 + V + u];
+        for (int u = 0; u < V; ++u) pb[u] = sb4[i / 4 + V + u];
 #pragma unroll
         for (int u = 0; u < V; ++u) {
-          acc = acc + cur[u].x;
-          acc = acc + cur[u].y;
-          acc = acc + cur[u].z;
-          acc = acc + cur[u].w;
+          acc = acc + pa[u].x;
+          acc = acc + pa[u].y;
+          acc = acc + pa[u].z;
+          acc = acc + pa[u].w;
+        }
+        i += 4 * V;
+        if (i + 8 * V > m) {
+#pragma unroll
+          for (int u = 0; u < V; ++u) {
+            acc = acc + pb[u].x;
+            acc = acc + pb[u].y;
+            acc = acc + pb[u].z;
+            acc = acc + pb[u].w;
+          }
+          i += 4 * V;
+          break;
         }
 #pragma unroll
-        for (int u = 0; u < V; ++u) cur[u] = nxt[u];
-      }
+        for (int u = 0; u < V; ++u) pa[u] = sb4[i / 4 + V + u];
 #pragma unroll
-      for (int u = 0; u < V; ++u) {
-        acc = acc + cur[u].x;
-        acc = acc + cur[u].y;
-        acc = acc + cur[u].z;
-        acc = acc + cur[u].w;
+        for (int u = 0; u < V; ++u) {
+          acc = acc + pb[u].x;
+          acc = acc + pb[u].y;
+          acc = acc + pb[u].z;
+          acc = acc + pb[u].w;
+        }
+        i += 4 * V;
+        if (i + 8 * V > m) {
+#pragma unroll
+          for (int u = 0; u < V; ++u) {
+            acc = acc + pa[u].x;
+            acc = acc + pa[u].y;
+            acc = acc + pa[u].z;
+            acc = acc + pa[u].w;
+          }
+          i += 4 * V;
+          break;
+        }
       }
-      i += 4 * V;
     }
     for (; i < m; ++i) acc = acc + sb[i];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
 mkdir -p gpurun_out
 ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }   # 1 = test failures: keep going; else stop
-timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1
+timeout -k 10 150 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc" >> gpurun_out/smoke.log; ok $rc || exit $rc
 timeout -k 10 900 python -m pytest tests -q -m gpu > gpurun_out/gpu_tests.log 2>&1
 rc=$?; echo "tests rc=$rc" >> gpurun_out/gpu_tests.log; ok $rc || exit $rc
