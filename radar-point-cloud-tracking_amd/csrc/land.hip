@@ -113,6 +113,19 @@ __device__ __forceinline__ int count_le(const double* e, int ne, double v) {
 
 __device__ __forceinline__ int clip_idx(int c, int hi) { return c < 0 ? 0 : (c > hi ? hi : c); }
 
+// count_le for the np.arange edges of the land grid (ascending, e[i] ~ e[0] + i*d): start at the
+// arithmetic guess and step to the exact count with true edge comparisons, so the result is the
+// binary search's for any ascending edges (NaN -> 0, like count_le) in ~2 loads instead of ~7
+// dependent ones.
+__device__ __forceinline__ int count_le_arith(const double* e, int ne, double v, double inv_d) {
+  const double gd = floor((v - e[0]) * inv_d) + 1.0;
+  int g = (gd >= 0.0) ? (gd < (double)ne ? (int)gd : ne) : 0;
+  if (!(v == v)) return 0;
+  while (g < ne && e[g] <= v) ++g;
+  while (g > 0 && e[g - 1] > v) --g;
+  return g;
+}
+
 // Stage both edge arrays in LDS when they fit.
 struct Edges {
   const double* xe;
@@ -159,10 +172,11 @@ __global__ __launch_bounds__(kBlock) void k_land_grid_lds(const float* __restric
   __syncthreads();
   const double* ex = lds_e;
   const double* ey = lds_e + nxe;
+  const double idx_ = 1.0 / (ex[1] - ex[0]), idy_ = 1.0 / (ey[1] - ey[0]);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const int ix = clip_idx(count_le(ex, nxe, (double)x[i]) - 1, nxe - 2);
-    const int iy = clip_idx(count_le(ey, nye, (double)y[i]) - 1, nye - 2);
+    const int ix = clip_idx(count_le_arith(ex, nxe, (double)x[i], idx_) - 1, nxe - 2);
+    const int iy = clip_idx(count_le_arith(ey, nye, (double)y[i], idy_) - 1, nye - 2);
     const int c = ix * ny + iy;
     atomicAdd(lds_c + c, 1);
     atomicAdd(lds_t + c, (double)val[i]);
@@ -225,10 +239,11 @@ __global__ __launch_bounds__(kBlock) void k_land_keep(const float* __restrict__ 
   __shared__ double lds[kMaxEdges];
   const Edges E = stage_edges(xe, nxe, ye, nye, lds);
   const int ny = nye - 1;
+  const double idx_ = 1.0 / (E.xe[1] - E.xe[0]), idy_ = 1.0 / (E.ye[1] - E.ye[0]);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const int ix = clip_idx(count_le(E.xe, nxe, (double)x[i]) - 1, nxe - 2);
-    const int iy = clip_idx(count_le(E.ye, nye, (double)y[i]) - 1, nye - 2);
+    const int ix = clip_idx(count_le_arith(E.xe, nxe, (double)x[i], idx_) - 1, nxe - 2);
+    const int iy = clip_idx(count_le_arith(E.ye, nye, (double)y[i], idy_) - 1, nye - 2);
     keep[i] = land[(int64_t)ix * ny + iy] ? 0 : 1;
   }
 }

@@ -152,21 +152,23 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_lb(const T* __restrict__ in
   if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
   __syncthreads();
   const int64_t tile = s_tile;
-  const int64_t base = tile * kLbTile + (int64_t)threadIdx.x * kLbItems;
+  const int64_t t0 = tile * kLbTile;
+  // coalesced striped loads -> LDS -> 16 consecutive items per thread (padded rows: <= 2-way
+  // bank conflicts)
+  __shared__ int64_t s_x[kLbTile + kLbTile / kLbItems];
+  auto pad = [](int i) { return i + i / kLbItems; };
+#pragma unroll
+  for (int k = 0; k < kLbItems; ++k) {
+    const int li = k * kScanBlock + threadIdx.x;
+    s_x[pad(li)] = (t0 + li < n) ? (int64_t)in[t0 + li] : 0;
+  }
+  __syncthreads();
   int64_t v[kLbItems];
   int64_t sum = 0;
-  if (base + kLbItems <= n) {
 #pragma unroll
-    for (int k = 0; k < kLbItems; ++k) {
-      v[k] = (int64_t)in[base + k];
-      sum += v[k];
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < kLbItems; ++k) {
-      v[k] = (base + k < n) ? (int64_t)in[base + k] : 0;
-      sum += v[k];
-    }
+  for (int k = 0; k < kLbItems; ++k) {
+    v[k] = s_x[pad(threadIdx.x * kLbItems + k)];
+    sum += v[k];
   }
   int64_t tot;
   const int64_t excl = block_exclusive_scan(sum, &tot);
@@ -207,19 +209,18 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_lb(const T* __restrict__ in
     }
   }
   __syncthreads();
+  // exclusive values back through LDS, then coalesced striped stores
   int64_t run = s_prefix + excl;
-  if (base + kLbItems <= n) {
 #pragma unroll
-    for (int k = 0; k < kLbItems; ++k) {
-      out[base + k] = (U)run;
-      run += v[k];
-    }
-  } else {
+  for (int k = 0; k < kLbItems; ++k) {
+    s_x[pad(threadIdx.x * kLbItems + k)] = run;
+    run += v[k];
+  }
+  __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kLbItems; ++k) {
-      if (base + k < n) out[base + k] = (U)run;
-      run += v[k];
-    }
+  for (int k = 0; k < kLbItems; ++k) {
+    const int li = k * kScanBlock + threadIdx.x;
+    if (t0 + li < n) out[t0 + li] = (U)s_x[pad(li)];
   }
 }
 
