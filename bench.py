@@ -172,7 +172,7 @@ def main():
         k5 = float(np.mean(k5_ms))
         n_in = n_core_in
         achieved = K5_BYTES_PER_POINT * n_in / (k5 * 1e-3) / 1e9
-        roof = {"kernel": "K5 = k_core_cell_fast + k_core_cell_window + k_core_fill + k_core_slow (core flags)",
+        roof = {"kernel": "K5 = k_core_cells_oct + k_core_fill + k_core_slow (core flags)",
                 "bound": "hbm",
                 "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),

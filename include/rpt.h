@@ -53,6 +53,15 @@ int32_t rpt_device_count(void);          /* hipGetDeviceCount; 0 when no GPU    
 int32_t rpt_set_device(int32_t device);  /* hipSetDevice                               */
 void rpt_release_scratch(void);          /* free this device's scratch pool            */
 
+/* Device exclusive prefix sum (the primitive under K1's offsets, the land compaction, the grid
+ * build and the summaries): out[i] = sum of in[0..i) for i < n; with_total != 0 also writes the
+ * grand total at out[n] (out then holds n+1 values).  in == out allowed for equal dtypes.
+ * Single pass (decoupled look-back), no memset, stream-ordered.  Values are non-negative and
+ * their total is below 2^46.  Dtypes: RPT_I32->RPT_I32, RPT_I32->RPT_I64, RPT_I64->RPT_I64. */
+enum { RPT_I32 = 0, RPT_I64 = 1 };
+int32_t rpt_exclusive_scan(const void* in, int32_t in_dtype, int64_t n, void* out,
+                           int32_t out_dtype, int32_t with_total, void* stream);
+
 /* ---- K1: polar -> Cartesian scatter ---------------------------------------------
  * A batch of sweeps ("files"), each echo[rows][bins] (f32 or u8), concatenated in file
  * order (= ascending gain inside a frame, as build_frame does).  Pass 1 counts kept

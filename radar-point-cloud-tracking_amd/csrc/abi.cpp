@@ -144,6 +144,31 @@ int32_t rpt_set_device(int32_t device) {
 
 void rpt_release_scratch(void) { rpt::release_scratch_current(); }
 
+int32_t rpt_exclusive_scan(const void* in, int32_t in_dtype, int64_t n, void* out,
+                           int32_t out_dtype, int32_t with_total, void* stream) {
+  rpt::clear_error();
+  if (n < 0 || (n > 0 && (!in || !out))) {
+    rpt::set_error("rpt_exclusive_scan: bad arguments");
+    return RPT_EINVAL;
+  }
+  const hipStream_t st = rpt::as_stream(stream);
+  const auto* i32 = static_cast<const int32_t*>(in);
+  if (in_dtype == RPT_I32 && out_dtype == RPT_I32)
+    return with_total ? rpt::exclusive_scan_total_i32(i32, static_cast<int32_t*>(out), n, st)
+                      : rpt::exclusive_scan_i32(i32, static_cast<int32_t*>(out), n, nullptr, st);
+  if (in_dtype == RPT_I32 && out_dtype == RPT_I64)
+    return with_total
+               ? rpt::exclusive_scan_total_i32_to_i64(i32, static_cast<int64_t*>(out), n, st)
+               : rpt::exclusive_scan_i32_to_i64(i32, static_cast<int64_t*>(out), n, nullptr, st);
+  if (in_dtype == RPT_I64 && out_dtype == RPT_I64) {
+    const auto* i64 = static_cast<const int64_t*>(in);
+    return with_total ? rpt::exclusive_scan_total_i64(i64, static_cast<int64_t*>(out), n, st)
+                      : rpt::exclusive_scan_i64(i64, static_cast<int64_t*>(out), n, nullptr, st);
+  }
+  rpt::set_error("rpt_exclusive_scan: dtypes must be i32->i32, i32->i64 or i64->i64");
+  return RPT_ENOTSUP;
+}
+
 int32_t rpt_stdbscan(const float* x, const float* y, const float* z, int64_t stride,
                      const float* times, int64_t n, double eps_space, double eps_time,
                      int32_t min_samples, int32_t* labels, rpt_stdbscan_stats* stats,

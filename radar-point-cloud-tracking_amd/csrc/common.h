@@ -94,6 +94,28 @@ int32_t exclusive_scan_i32_to_i64(const int32_t* in, int64_t* out, int64_t n, in
 int32_t exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, int64_t* tmp,
                            hipStream_t stream);
 
+// out[0..n] = exclusive scan of in[0..n) plus the grand total at out[n] (out has n+1 entries;
+// in == out allowed): no sentinel element to clear.  Totals must stay below 2^46.
+int32_t exclusive_scan_total_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t stream);
+int32_t exclusive_scan_total_i32_to_i64(const int32_t* in, int64_t* out, int64_t n,
+                                        hipStream_t stream);
+int32_t exclusive_scan_total_i32(const int32_t* in, int32_t* out, int64_t n, hipStream_t stream);
+
+// Back-to-back copy of up to kPackMax device arrays (sizes in 4-byte words) into dst.
+constexpr int kPackMax = 10;
+struct PackList {
+  const uint32_t* src[kPackMax];
+  int64_t off[kPackMax + 1];  // word offsets in dst, off[0] = 0
+  int k = 0;
+  void add(const void* p, size_t bytes) {
+    if (k == 0) off[0] = 0;
+    src[k] = static_cast<const uint32_t*>(p);
+    off[k + 1] = off[k] + (int64_t)(bytes / 4);
+    ++k;
+  }
+};
+int32_t pack_arrays(const PackList& l, uint32_t* dst, hipStream_t st);
+
 // Stable LSD radix sort of (key,u32 value) pairs on the low `bits` bits of key.
 // Buffers: keys/vals in, keys_alt/vals_alt ping-pong; the result ends in whichever buffer the
 // returned pointer pair names (out_keys/out_vals).  tmp needs radix_tmp_elems(n) int64s.

@@ -62,16 +62,13 @@ int32_t select_roots(const int64_t* rep, int64_t base, int64_t lo, int64_t hi, i
   Budget b;
   b.add<int32_t>(m + 1);
   b.add<int64_t>(m + 1);
-  b.add<int64_t>(scan_tmp_elems(m + 1));
   RPT_TRY(sc.reserve(b.bytes, st));
   int32_t* flag = sc.carve_n<int32_t>(m + 1);
   int64_t* pos = sc.carve_n<int64_t>(m + 1);
-  int64_t* tmp = sc.carve_n<int64_t>(scan_tmp_elems(m + 1));
-  RPT_HIP(hipMemsetAsync(flag + m, 0, sizeof(int32_t), st));
   hipLaunchKernelGGL(k_root_flags, dim3(grid_for(m, 256, 4096)), dim3(256), 0, st, rep, base, lo,
                      m, flag);
   RPT_CHECK_LAUNCH();
-  RPT_TRY(exclusive_scan_i32_to_i64(flag, pos, m + 1, tmp, st));
+  RPT_TRY(exclusive_scan_total_i32_to_i64(flag, pos, m, st));
   hipLaunchKernelGGL(k_root_write, dim3(grid_for(m, 256, 4096)), dim3(256), 0, st, flag, pos,
                      base, lo, m, out);
   RPT_CHECK_LAUNCH();

@@ -358,18 +358,15 @@ int32_t land_filter(const float* x, const float* y, const float* v, const int32_
   Budget b;
   b.add<int32_t>(n + 1);
   b.add<int64_t>(n + 1);
-  b.add<int64_t>(scan_tmp_elems(n + 1));
   RPT_TRY(sc.reserve(b.bytes, st));
   int32_t* keep = sc.carve_n<int32_t>(n + 1);
   int64_t* pos = sc.carve_n<int64_t>(n + 1);
-  int64_t* tmp = sc.carve_n<int64_t>(scan_tmp_elems(n + 1));
-  RPT_HIP(hipMemsetAsync(keep + n, 0, sizeof(int32_t), st));
   if (n > 0) {
     hipLaunchKernelGGL(k_land_keep, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, st, x, y,
                        n, xe, nxe, ye, nye, land, keep);
     RPT_CHECK_LAUNCH();
   }
-  RPT_TRY(exclusive_scan_i32_to_i64(keep, pos, n + 1, tmp, st));
+  RPT_TRY(exclusive_scan_total_i32_to_i64(keep, pos, n, st));
   if (n > 0) {
     hipLaunchKernelGGL(k_land_scatter, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, st, x,
                        y, v, g, pf, n, keep, pos, xo, yo, vo, go, pfo);

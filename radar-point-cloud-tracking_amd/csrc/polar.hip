@@ -12,6 +12,7 @@
 //   step = scale[row] / (float)bins ; r = step * (float)bin ; x = r * cos_t[row] ; y = r * sin_t[row]
 // cos_t / sin_t are inputs: numpy's float32 SIMD cos/sin are not correctly rounded, so the host
 // evaluates them exactly as the reference does (4096 values per sweep geometry).
+#include <algorithm>
 #include <cmath>
 
 #include "common.h"
@@ -283,6 +284,211 @@ __global__ __launch_bounds__(kBlock) void k_row_count_u8(const uint8_t* __restri
   }
 }
 
+// Emission of one u8 row of 1024 bins whose first kept element has in-file rank `rank`: the kept
+// elements whose rank is a multiple of stride go to out0 + (their in-file emitted index).  Each
+// lane ranks its kept elements (m* = per-byte keep masks of its 16 samples, c their count, incl
+// the wave-inclusive count), the emitted (bin, sample) pairs are staged in the wave's LDS slice
+// in output order and written with full-width stores.  Outputs at or beyond cap are dropped and
+// flagged in *overflow (single-pass K1 writes into a capacity guessed from the last run).
+__device__ __forceinline__ void emit_row_u8(const uint4 v, uint32_t m0, uint32_t m1, uint32_t m2,
+                                            uint32_t m3, int c, int incl, int tot, uint32_t rank,
+                                            int64_t out0, int64_t cap, float step,
+                                            const float* __restrict__ ranges, float ct, float st,
+                                            int32_t g, int32_t fr, uint32_t ustride, bool pow2,
+                                            uint32_t sh, uint32_t* __restrict__ stage, int lane,
+                                            float* __restrict__ x, float* __restrict__ y,
+                                            float* __restrict__ val, int32_t* __restrict__ gain_out,
+                                            int32_t* __restrict__ pf_out,
+                                            uint32_t* __restrict__ overflow) {
+  const uint32_t r = rank + (uint32_t)(incl - c);
+  const uint32_t first = pow2 ? ((rank + ustride - 1u) >> sh) : (rank + ustride - 1u) / ustride;
+  if (c) {
+    uint32_t m = nib(m0) | (nib(m1) << 4) | (nib(m2) << 8) | (nib(m3) << 12);
+    const uint32_t q = pow2 ? (r >> sh) : r / ustride;
+    const uint32_t rem = r - q * ustride;
+    int slot = (int)(q + (rem ? 1u : 0u) - first);
+    // drop the kept elements before the first emitted rank, then emit every stride-th
+    for (uint32_t t = rem ? ustride - rem : 0u; t > 0u && m; --t) m &= m - 1u;
+    while (m) {
+      const int k = __builtin_ctz(m);
+      const uint32_t w = (k < 4) ? v.x : (k < 8) ? v.y : (k < 12) ? v.z : v.w;
+      const uint32_t sample = __builtin_amdgcn_ubfe(w, (uint32_t)(8 * (k & 3)), 8u);
+      stage[slot++] = ((uint32_t)(lane * 16 + k) << 8) | sample;
+      for (uint32_t t = 0; t < ustride && m; ++t) m &= m - 1u;
+    }
+  }
+  const int n_emit = (int)((pow2 ? ((rank + (uint32_t)tot + ustride - 1u) >> sh)
+                                 : (rank + (uint32_t)tot + ustride - 1u) / ustride) -
+                           first);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (int l = lane; l < n_emit; l += 64) {
+    const uint32_t e = stage[l];
+    const int b = (int)(e >> 8);
+    const int64_t o = out0 + first + l;
+    if (o >= cap) {
+      if (overflow) atomicOr(overflow, 1u);
+      continue;
+    }
+    const float rr = ranges ? ranges[b] : step * (float)b;
+    x[o] = rr * ct;
+    y[o] = rr * st;
+    val[o] = (float)(e & 0xffu);
+    if (gain_out) gain_out[o] = g;
+    if (pf_out) pf_out[o] = fr;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Single-pass K1 for u8 sweeps of 1024 bins (rows % 64 == 0): the count and write passes fused
+// with a decoupled look-back.  A block takes tiles of 64 rows (16 per wave, held in registers) in
+// ticket order (one same-address atomic per 64 KiB: they serialise in L2); it publishes the
+// tile's kept count, looks back over the earlier tiles of the same file for its in-file rank
+// (status granules {flag:2 | value:62}, agent-scope relaxed atomics: the data is the flag), takes
+// the file's output base from a second look-back over the files' emitted counts (fstat, published
+// by each file's last group), and emits.  Every wait is on a smaller ticket, so all waits end;
+// every spin is still bounded (a timeout sets *overflow and the host falls back to the two
+// passes).  file_off[f] receives the exclusive per-file output offsets (file_off[n_files] = N).
+constexpr uint64_t kK1Agg = 1ull << 62, kK1Inc = 2ull << 62, kK1Val = (1ull << 62) - 1;
+
+// Exclusive prefix of item `self` over items [first, self) of a status array of granules
+// {flag:2 | value:62} (aggregate or inclusive), one wave, 64 predecessors per round: the
+// aggregates back to the nearest inclusive.  Bounded spin; a timeout sets *err.
+__device__ __forceinline__ int64_t lookback(const uint64_t* __restrict__ status, int64_t self,
+                                            int64_t first, int lane, uint32_t* __restrict__ err) {
+  int64_t prefix = 0;
+  uint32_t spins = 0;
+  for (int64_t j = self - 1; j >= first;) {
+    const int64_t idx = j - lane;
+    const uint64_t st = (idx >= first) ? __hip_atomic_load(status + idx, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT)
+                                       : kK1Inc;  // before the range: an inclusive zero
+    const uint64_t incm = __ballot((st >> 62) == 2u);
+    const uint64_t zero = __ballot((st >> 62) == 0u);
+    const int fi = incm ? __ffsll((unsigned long long)incm) - 1 : 64;
+    const uint64_t upto = (fi >= 63) ? ~0ull : ((2ull << fi) - 1ull);
+    if (zero & upto) {
+      if (++spins > (1u << 22)) {
+        if (lane == 0) atomicOr(err, 2u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    int64_t part = (lane <= fi && idx >= first) ? (int64_t)(st & kK1Val) : 0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
+    prefix += part;
+    if (fi < 64) break;
+    j -= 64;
+  }
+  return prefix;
+}
+constexpr int kScanRowsPerWave = 16;                               // rows held in registers
+constexpr int kScanTileRows = kScanRowsPerWave * kWavesPerBlock;  // 64 rows per ticket
+__global__ __launch_bounds__(kBlock) void k_polar_scan_u8(
+    const uint8_t* __restrict__ echo, int64_t n_rows, int rows, int T, int stride, RowGeo geo,
+    const int32_t* __restrict__ gain, int files_per_frame, float* __restrict__ x,
+    float* __restrict__ y, float* __restrict__ val, int32_t* __restrict__ gain_out,
+    int32_t* __restrict__ pf_out, int64_t cap, uint64_t* __restrict__ status,
+    uint64_t* __restrict__ fstat, int64_t* __restrict__ file_off, uint32_t* __restrict__ ticket,
+    uint32_t* __restrict__ overflow) {
+  constexpr int CH = 64 * 16;
+  __shared__ uint32_t s_stage[kWavesPerBlock][CH];  // (bin << 8) | sample
+  __shared__ int64_t s_wtot[kWavesPerBlock];
+  __shared__ int64_t s_prefix, s_base;
+  __shared__ uint32_t s_tile;
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x / 64;
+  const float fb = (float)CH;
+  const uint32_t ustride = (uint32_t)stride;
+  const bool pow2 = (ustride & (ustride - 1u)) == 0u;
+  const uint32_t sh = (uint32_t)__builtin_ctz(ustride);
+  const int64_t tpf = rows / kScanTileRows;  // tiles per file
+  const int64_t n_tiles = n_rows / kScanTileRows;
+  while (true) {
+    if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const int64_t tile = s_tile;
+    if (tile >= n_tiles) break;  // uniform over the block
+    const int64_t f = tile / tpf;
+    const int64_t ti = tile - f * tpf;
+    const int64_t row0 = tile * kScanTileRows + wv * kScanRowsPerWave;
+    uint4 vv[kScanRowsPerWave];
+#pragma unroll
+    for (int k = 0; k < kScanRowsPerWave; ++k)
+      vv[k] = *reinterpret_cast<const uint4*>(echo + (row0 + k) * CH + lane * 16);
+    int tt[kScanRowsPerWave];
+    int wtot = 0;
+#pragma unroll
+    for (int k = 0; k < kScanRowsPerWave; ++k) {
+      const int c = __popc(gt_mask(vv[k].x, T)) + __popc(gt_mask(vv[k].y, T)) +
+                    __popc(gt_mask(vv[k].z, T)) + __popc(gt_mask(vv[k].w, T));
+      tt[k] = c;
+      wtot += c;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) wtot += __shfl_xor(wtot, off);
+    if (lane == 0) s_wtot[wv] = wtot;
+    __syncthreads();
+    if (wv == 0) {
+      int64_t total = 0;
+#pragma unroll
+      for (int w = 0; w < kWavesPerBlock; ++w) total += s_wtot[w];
+      // the tile's count, then its in-file prefix from the earlier tiles of the file
+      if (lane == 0)
+        __hip_atomic_store(status + tile, (ti == 0 ? kK1Inc : kK1Agg) | (uint64_t)total,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int64_t prefix = lookback(status, tile, f * tpf, lane, overflow);
+      if (lane == 0 && ti > 0)
+        __hip_atomic_store(status + tile, kK1Inc | (uint64_t)(prefix + total), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      // the file's output base: a second look-back, over the files (fstat: the file's emitted
+      // count as soon as its last tile knows it, then its inclusive base + count)
+      const int64_t fcount = (prefix + total + stride - 1) / stride;
+      if (ti == tpf - 1 && lane == 0)
+        __hip_atomic_store(fstat + f, (f == 0 ? kK1Inc : kK1Agg) | (uint64_t)fcount,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int64_t base = lookback(fstat, f, 0, lane, overflow);
+      if (ti == tpf - 1 && lane == 0) {
+        if (f > 0)
+          __hip_atomic_store(fstat + f, kK1Inc | (uint64_t)(base + fcount), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        file_off[f + 1] = base + fcount;
+        if (f == 0) file_off[0] = 0;
+      }
+      if (lane == 0) {
+        s_prefix = prefix;
+        s_base = base;
+      }
+    }
+    __syncthreads();
+    // emission, row by row (ranks continue over the block's waves in row order)
+    uint32_t rank = (uint32_t)s_prefix;
+    for (int w = 0; w < wv; ++w) rank += (uint32_t)s_wtot[w];
+    const int64_t base = s_base;
+    const int32_t g = gain ? gain[f] : 0;
+    const int32_t fr = (int32_t)((uint32_t)f / (uint32_t)files_per_frame);
+#pragma unroll
+    for (int k = 0; k < kScanRowsPerWave; ++k) {
+      const int64_t row = row0 + k;
+      const uint32_t m0 = gt_mask(vv[k].x, T), m1 = gt_mask(vv[k].y, T),
+                     m2 = gt_mask(vv[k].z, T), m3 = gt_mask(vv[k].w, T);
+      const int incl = wave_incl_scan_dpp(tt[k]);
+      const int tot = __builtin_amdgcn_readlane(incl, 63);
+      const float step = geo.scale[row] / fb;
+      emit_row_u8(vv[k], m0, m1, m2, m3, tt[k], incl, tot, rank, base, cap, step, nullptr,
+                  geo.cos_t[row], geo.sin_t[row], g, fr, ustride, pow2, sh, s_stage[wv], lane, x,
+                  y, val, gain_out, pf_out, overflow);
+      rank += (uint32_t)tot;
+    }
+    __syncthreads();  // s_tile / s_wtot reuse
+  }
+}
+
 // Same contract as k_row_write (LDS-staged emission), u8 samples, bins == 1024 (one chunk per
 // row): kRowsPerIter rows' samples are loaded before the first is ranked.
 __global__ __launch_bounds__(kBlock) void k_row_write_u8(
@@ -328,44 +534,10 @@ __global__ __launch_bounds__(kBlock) void k_row_write_u8(
       const int c = __popc(m0) + __popc(m1) + __popc(m2) + __popc(m3);
       const int incl = wave_incl_scan_dpp(c);
       const int tot = __builtin_amdgcn_readlane(incl, 63);
-      const uint32_t r = rank + (uint32_t)(incl - c);
-      const uint32_t first =
-          pow2 ? ((rank + ustride - 1u) >> sh) : (rank + ustride - 1u) / ustride;
-      if (c) {
-        uint32_t m = nib(m0) | (nib(m1) << 4) | (nib(m2) << 8) | (nib(m3) << 12);
-        const uint32_t q = pow2 ? (r >> sh) : r / ustride;
-        const uint32_t rem = r - q * ustride;
-        int slot = (int)(q + (rem ? 1u : 0u) - first);
-        // drop the kept elements before the first emitted rank, then emit every stride-th
-        for (uint32_t t = rem ? ustride - rem : 0u; t > 0u && m; --t) m &= m - 1u;
-        while (m) {
-          const int k = __builtin_ctz(m);
-          const uint32_t w = (k < 4) ? v.x : (k < 8) ? v.y : (k < 12) ? v.z : v.w;
-          const uint32_t sample = __builtin_amdgcn_ubfe(w, (uint32_t)(8 * (k & 3)), 8u);
-          s_stage[wv][slot++] = ((uint32_t)(lane * 16 + k) << 8) | sample;
-          for (uint32_t t = 0; t < ustride && m; ++t) m &= m - 1u;
-        }
-      }
-      const int n_emit =
-          (int)((pow2 ? ((rank + (uint32_t)tot + ustride - 1u) >> sh)
-                      : (rank + (uint32_t)tot + ustride - 1u) / ustride) - first);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      for (int l = lane; l < n_emit; l += 64) {
-        const uint32_t e = s_stage[wv][l];
-        const int b = (int)(e >> 8);
-        const int64_t o = out0 + first + l;
-        const float rr = geo.ranges ? geo.ranges[row * bins + b] : step * (float)b;
-        x[o] = rr * ct;
-        y[o] = rr * st;
-        val[o] = (float)(e & 0xffu);
-        if (gain_out) gain_out[o] = g;
-        if (pf_out) pf_out[o] = fr;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const float rs = geo.ranges ? 0.f : step;
+      emit_row_u8(v, m0, m1, m2, m3, c, incl, tot, rank, out0, INT64_MAX, rs,
+                  geo.ranges ? geo.ranges + row * bins : nullptr, ct, st, g, fr, ustride, pow2,
+                  sh, s_stage[wv], lane, x, y, val, gain_out, pf_out, nullptr);
     }
   }
 }
@@ -391,11 +563,9 @@ int32_t count_impl(const T* echo, int64_t n_files, int rows, int bins, float thr
   Budget b;
   b.add<int32_t>(n_rows + 1);
   b.add<int64_t>(n_files + 1);
-  b.add<int64_t>(scan_tmp_elems(n_rows + 1) + scan_tmp_elems(n_files + 1));
   RPT_TRY(sc.reserve(b.bytes, st));
   int32_t* rc = sc.carve_n<int32_t>(n_rows + 1);
   int64_t* fo = sc.carve_n<int64_t>(n_files + 1);
-  int64_t* tmp = sc.carve_n<int64_t>(scan_tmp_elems(n_rows + 1) + scan_tmp_elems(n_files + 1));
   const bool vec = (bins % (64 * Vec<T>::N) == 0) && ((uintptr_t)echo % 16 == 0);
   const int grid = grid_for(n_rows, kWavesPerBlock, 16384);
   if (vec && is_u8<T>())
@@ -409,13 +579,11 @@ int32_t count_impl(const T* echo, int64_t n_files, int rows, int bins, float thr
     hipLaunchKernelGGL((k_row_count<T, false>), dim3(grid), dim3(kBlock), 0, st, echo, n_rows,
                        bins, thr, rc);
   RPT_CHECK_LAUNCH();
-  RPT_HIP(hipMemsetAsync(rc + n_rows, 0, sizeof(int32_t), st));
-  RPT_TRY(exclusive_scan_i32_to_i64(rc, row_prefix, n_rows + 1, tmp, st));
+  RPT_TRY(exclusive_scan_total_i32_to_i64(rc, row_prefix, n_rows, st));
   hipLaunchKernelGGL(k_file_counts, dim3(grid_for(n_files, 256, 1024)), dim3(256), 0, st,
                      row_prefix, n_files, rows, stride, fo);
   RPT_CHECK_LAUNCH();
-  RPT_HIP(hipMemsetAsync(fo + n_files, 0, sizeof(int64_t), st));
-  RPT_TRY(exclusive_scan_i64(fo, file_offsets, n_files + 1, tmp, st));
+  RPT_TRY(exclusive_scan_total_i64(fo, file_offsets, n_files, st));
   if (total_host) {
     RPT_HIP(hipMemcpyAsync(total_host, file_offsets + n_files, sizeof(int64_t),
                            hipMemcpyDeviceToHost, st));
@@ -589,6 +757,43 @@ __global__ __launch_bounds__(kBlock) void k_synth(rpt_synth_params p, int64_t fr
 }  // namespace
 
 // ---------------------------------------------------------------- C-ABI bodies
+// Single-pass K1 (see k_polar_scan_u8).  Returns RPT_EINVAL when the shape does not qualify;
+// *status_host: 0 ok, bit 0 = more than cap points (outputs incomplete), bit 1 = spin timeout.
+int32_t polar_scan_u8(const uint8_t* echo, int64_t n_files, int32_t rows, int32_t bins, float thr,
+                      int32_t stride, const float* scale, const float* cos_t, const float* sin_t,
+                      const int32_t* gain, int32_t fpf, float* x, float* y, float* v,
+                      int32_t* gout, int32_t* pf, int64_t cap, int64_t* file_off,
+                      uint64_t* work, size_t work_words, hipStream_t st) {
+  const int64_t n_rows = n_files * rows;
+  if (bins != 64 * 16 || rows % kScanTileRows || n_files < 1 || stride < 1 || fpf < 1 ||
+      (uintptr_t)echo % 16 || (int64_t)rows * bins >= (int64_t(1) << 32) ||
+      n_rows >= (int64_t(1) << 31)) {
+    set_error("polar_scan_u8: shape not supported");
+    return RPT_EINVAL;
+  }
+  const int64_t n_groups = n_rows / kScanTileRows;  // tiles
+  const size_t need = (size_t)n_groups + (size_t)n_files + 1 + 2;
+  if (!work || work_words < need) {
+    set_error("polar_scan_u8: work buffer too small");
+    return RPT_EINVAL;
+  }
+  RPT_HIP(hipMemsetAsync(work, 0, need * sizeof(uint64_t), st));
+  uint64_t* status = work;
+  uint64_t* fstat = work + n_groups;
+  uint32_t* ticket = reinterpret_cast<uint32_t*>(work + n_groups + n_files + 1);
+  uint32_t* overflow = ticket + 2;
+  RowGeo geo{scale, nullptr, cos_t, sin_t};
+  int dev = 0, n_cu = 0;
+  RPT_HIP(hipGetDevice(&dev));
+  RPT_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  const int grid = (int)std::min<int64_t>((int64_t)std::max(n_cu, 1) * 4, n_groups);
+  hipLaunchKernelGGL(k_polar_scan_u8, dim3(grid), dim3(kBlock), 0, st, echo, n_rows, rows,
+                     u8_threshold(thr), stride, geo, gain, fpf, x, y, v, gout, pf, cap, status,
+                     fstat, file_off, ticket, overflow);
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
+}
+
 int32_t polar_count(const void* echo, int32_t dt, int64_t n_files, int32_t rows, int32_t bins,
                     float thr, int32_t stride, int64_t* row_prefix, int64_t* file_offsets,
                     int64_t* total_host, hipStream_t st) {

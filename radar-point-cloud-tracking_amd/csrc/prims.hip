@@ -1,8 +1,9 @@
 // Device-wide primitives used by the ST-DBSCAN grid build and the cluster summaries:
-//  * exclusive scan (int64 values) — 3-phase reduce / scan-of-partials / scan-and-add,
+//  * exclusive scan — single pass with decoupled look-back (one launch, no memset),
 //  * stable LSD radix sort of (u32 key, u32 value) pairs, 8-bit digits, wave-granular
 //    histograms so that a pass needs no block-level barriers inside the scatter loop.
 // Plus the library's error plumbing and per-device scratch pool.
+#include <algorithm>
 #include <cstdarg>
 #include <mutex>
 
@@ -110,57 +111,98 @@ __device__ __forceinline__ int64_t block_exclusive_scan(int64_t v, int64_t* tota
   return wprefix + incl - v;
 }
 
+// One-block scan of up to kScanTile outputs (same n_in / n_out contract as k_scan_lb).
 template <class T, class U>
-__global__ __launch_bounds__(kScanBlock) void k_scan_apply(const T* __restrict__ in, int64_t n,
-                                                          const int64_t* __restrict__ partial,
-                                                          U* __restrict__ out) {
-  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+__global__ __launch_bounds__(kScanBlock) void k_scan_small(const T* __restrict__ in, int64_t n_in,
+                                                          int64_t n_out, U* __restrict__ out) {
+  const int64_t base = (int64_t)threadIdx.x * kScanItems;
   int64_t vals[kScanItems];
   int64_t s = 0;
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k) {
     int64_t i = base + k;
-    vals[k] = (i < n) ? (int64_t)in[i] : 0;
+    vals[k] = (i < n_in) ? (int64_t)in[i] : 0;
     s += vals[k];
   }
   int64_t tot;
-  int64_t run = block_exclusive_scan(s, &tot) + (partial ? partial[blockIdx.x] : 0);
+  int64_t run = block_exclusive_scan(s, &tot);
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k) {
     int64_t i = base + k;
-    if (i < n) out[i] = (U)run;
+    if (i < n_out) out[i] = (U)run;
     run += vals[k];
   }
 }
 
-// Single-pass form (decoupled look-back): tiles of kLbTile items are taken in ticket order; a
-// tile publishes its aggregate, then its inclusive prefix once its predecessors' are known.  The
-// status words are 64-bit granules {flag:2 | value:62} written and read with agent-scope relaxed
-// atomics: the data IS the flag (MI355X guide §6 Guideline 16, R2), so no fences.  Values are
-// non-negative (counts, flags) and their running total is < 2^62.  Every spin is bounded.
+// Single-pass form (decoupled look-back): tiles of kLbItems x B items are taken in ticket order;
+// a tile publishes its aggregate, then its inclusive prefix once its predecessors' are known.
+// The status words are 64-bit granules {flag:2 | epoch:16 | value:46} written and read with
+// agent-scope relaxed atomics: the data IS the flag (MI355X guide §6 Guideline 16, R2), so no
+// fences.  Values are non-negative counts whose running total is < 2^46.
+//
+// No memset per scan: the status array and the ticket live in a persistent per-(device, stream)
+// ScanState.  Every launch gets a fresh epoch, and a granule of another epoch reads as "not
+// published" (the array is zeroed once per 65535 launches, before an epoch is reused); the block
+// that draws the last ticket resets the counter for the next launch on the stream.  Every spin is
+// bounded.
 constexpr int kLbItems = 16;
-constexpr int kLbTile = kScanBlock * kLbItems;  // 4096
-constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = (1ull << 62) - 1;
+constexpr int kLbBig = 1024;  // block size of the large-n kernel: 16384 items per ticket
+constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = (1ull << 46) - 1;
+constexpr int kLbEpochShift = 46;
 
-template <class T, class U>
-__global__ __launch_bounds__(kScanBlock) void k_scan_lb(const T* __restrict__ in, int64_t n,
-                                                       U* __restrict__ out,
-                                                       uint64_t* __restrict__ status,
-                                                       uint32_t* __restrict__ ticket) {
+template <int B>
+__device__ __forceinline__ int64_t block_excl_scan_b(int64_t v, int64_t* total) {
+  __shared__ int64_t wsum[B / kWave];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  int64_t incl = v;
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    int64_t o = __shfl_up(incl, off, kWave);
+    if (lane >= off) incl += o;
+  }
+  if (lane == kWave - 1) wsum[wid] = incl;
+  __syncthreads();
+  int64_t wprefix = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < B / kWave; ++w) {
+    int64_t s = wsum[w];
+    if (w < wid) wprefix += s;
+    tot += s;
+  }
+  *total = tot;
+  return wprefix + incl - v;
+}
+
+// out[i] = sum of in[0..i) for i < n_out, with in[i] read as 0 for i >= n_in (n_out <= n_in + 1:
+// n_out = n_in + 1 writes the grand total at out[n_in]).  in == out is allowed.
+template <class T, class U, int B>
+__global__ __launch_bounds__(B) void k_scan_lb(const T* __restrict__ in, int64_t n_in,
+                                               U* __restrict__ out, int64_t n_out,
+                                               uint64_t* __restrict__ status,
+                                               unsigned long long* __restrict__ ticket,
+                                               uint64_t epoch, uint32_t nt) {
+  constexpr int kTile = B * kLbItems;
   __shared__ uint32_t s_tile;
   __shared__ int64_t s_prefix;
-  if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
+  if (threadIdx.x == 0) {
+    const uint32_t t = (uint32_t)atomicAdd(ticket, 1ull);
+    // the last ticket of this launch: nobody draws again before the next launch on the stream
+    if (t == nt - 1u)
+      __hip_atomic_store(ticket, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_tile = t;
+  }
   __syncthreads();
   const int64_t tile = s_tile;
-  const int64_t t0 = tile * kLbTile;
+  const int64_t t0 = tile * kTile;
   // coalesced striped loads -> LDS -> 16 consecutive items per thread (padded rows: <= 2-way
   // bank conflicts)
-  __shared__ int64_t s_x[kLbTile + kLbTile / kLbItems];
+  __shared__ int64_t s_x[kTile + kTile / kLbItems];
   auto pad = [](int i) { return i + i / kLbItems; };
 #pragma unroll
   for (int k = 0; k < kLbItems; ++k) {
-    const int li = k * kScanBlock + threadIdx.x;
-    s_x[pad(li)] = (t0 + li < n) ? (int64_t)in[t0 + li] : 0;
+    const int li = k * B + threadIdx.x;
+    s_x[pad(li)] = (t0 + li < n_in) ? (int64_t)in[t0 + li] : 0;
   }
   __syncthreads();
   int64_t v[kLbItems];
@@ -171,20 +213,22 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_lb(const T* __restrict__ in
     sum += v[k];
   }
   int64_t tot;
-  const int64_t excl = block_exclusive_scan(sum, &tot);
+  const int64_t excl = block_excl_scan_b<B>(sum, &tot);
+  const uint64_t tag = epoch << kLbEpochShift;
   if (threadIdx.x < kWave) {
     const int lane = threadIdx.x;
     if (lane == 0)
-      __hip_atomic_store(status + tile, (tile == 0 ? kLbInc : kLbAgg) | (uint64_t)tot,
+      __hip_atomic_store(status + tile, (tile == 0 ? kLbInc : kLbAgg) | tag | (uint64_t)tot,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int64_t prefix = 0;
     int64_t j = tile - 1;  // nearest predecessor not yet accounted for
     uint32_t spins = 0;
     while (j >= 0) {
       const int64_t idx = j - lane;
-      const uint64_t st = (idx >= 0) ? __hip_atomic_load(status + idx, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT)
-                                     : kLbInc;  // before tile 0: an inclusive zero
+      uint64_t st = (idx >= 0) ? __hip_atomic_load(status + idx, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)
+                               : (kLbInc | tag);  // before tile 0: an inclusive zero
+      if (((st >> kLbEpochShift) & 0xffffu) != epoch) st = 0;  // another launch's granule
       const uint64_t inc = __ballot((st >> 62) == 2u);
       const uint64_t zero = __ballot((st >> 62) == 0u);
       const int first_inc = inc ? __ffsll((unsigned long long)inc) - 1 : kWave;
@@ -203,8 +247,8 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_lb(const T* __restrict__ in
     }
     if (lane == 0) {
       if (tile > 0)
-        __hip_atomic_store(status + tile, kLbInc | (uint64_t)(prefix + tot), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(status + tile, kLbInc | tag | (uint64_t)(prefix + tot),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_prefix = prefix;
     }
   }
@@ -219,53 +263,143 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_lb(const T* __restrict__ in
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < kLbItems; ++k) {
-    const int li = k * kScanBlock + threadIdx.x;
-    if (t0 + li < n) out[t0 + li] = (U)s_x[pad(li)];
+    const int li = k * B + threadIdx.x;
+    if (t0 + li < n_out) out[t0 + li] = (U)s_x[pad(li)];
   }
 }
 
 size_t scan_tmp_elems(int64_t n) {
-  size_t total = 0;
-  int64_t m = n;
-  while (m > kScanTile) {
-    m = (m + kScanTile - 1) / kScanTile;
-    total += (size_t)m + 64;
-  }
-  return total + 64;
+  (void)n;
+  return 64;  // the look-back state is persistent (ScanState); kept for the callers' budgets
 }
 
+namespace {
+struct ScanState {
+  uint64_t* status = nullptr;  // [cap] granules, then the ticket word
+  size_t cap = 0;
+  uint32_t epoch = 0;
+};
+std::mutex g_scan_mu;
+std::vector<std::pair<std::pair<int, hipStream_t>, ScanState*>> g_scan_states;
+
+// The look-back state of (current device, stream) with room for nt tiles, and this launch's epoch.
+int32_t scan_state(hipStream_t st, int64_t nt, ScanState** out, uint32_t* epoch) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  ScanState* s = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_scan_mu);
+    for (auto& e : g_scan_states)
+      if (e.first.first == dev && e.first.second == st) s = e.second;
+    if (!s) {
+      s = new ScanState();
+      g_scan_states.push_back({{dev, st}, s});
+    }
+  }
+  if ((size_t)nt > s->cap) {
+    if (s->status) {
+      RPT_HIP(hipStreamSynchronize(st));  // earlier scans on this stream still read it
+      RPT_HIP(hipFree(s->status));
+      s->status = nullptr;
+      s->cap = 0;
+    }
+    const size_t want = std::max<size_t>((size_t)nt + (size_t)nt / 2, 4096);
+    hipError_t e = hipMalloc(&s->status, sizeof(uint64_t) * (want + 1));
+    if (e != hipSuccess) {
+      s->status = nullptr;
+      set_error("scan state hipMalloc failed: %s", hipGetErrorString(e));
+      return RPT_ENOMEM;
+    }
+    RPT_HIP(hipMemsetAsync(s->status, 0, sizeof(uint64_t) * (want + 1), st));
+    s->cap = want;
+    s->epoch = 0;
+  }
+  if (++s->epoch > 0xffffu) {  // an epoch is about to be reused: clear every granule first
+    RPT_HIP(hipMemsetAsync(s->status, 0, sizeof(uint64_t) * s->cap, st));
+    s->epoch = 1;
+  }
+  *out = s;
+  *epoch = s->epoch;
+  return RPT_OK;
+}
+}  // namespace
+
 template <class T, class U>
-static int32_t scan_impl(const T* in, U* out, int64_t n, int64_t* tmp, hipStream_t stream) {
-  if (n <= 0) return RPT_OK;
-  const int64_t nb = (n + kScanTile - 1) / kScanTile;
+static int32_t scan_impl(const T* in, int64_t n_in, U* out, int64_t n_out, hipStream_t stream) {
+  if (n_out <= 0) return RPT_OK;
+  const int64_t nb = (n_out + kScanTile - 1) / kScanTile;
   if (nb == 1) {
-    hipLaunchKernelGGL((k_scan_apply<T, U>), dim3(1), dim3(kScanBlock), 0, stream, in, n,
-                       (const int64_t*)nullptr, out);
+    hipLaunchKernelGGL((k_scan_small<T, U>), dim3(1), dim3(kScanBlock), 0, stream, in, n_in,
+                       n_out, out);
     RPT_CHECK_LAUNCH();
     return RPT_OK;
   }
-  // one pass: status granules + ticket in tmp (scan_tmp_elems(n) >= n / 2048 + 64 words)
-  const int64_t nt = (n + kLbTile - 1) / kLbTile;
-  uint64_t* status = reinterpret_cast<uint64_t*>(tmp);
-  uint32_t* ticket = reinterpret_cast<uint32_t*>(tmp + nt);
-  RPT_HIP(hipMemsetAsync(tmp, 0, sizeof(int64_t) * (size_t)(nt + 1), stream));
-  hipLaunchKernelGGL((k_scan_lb<T, U>), dim3((unsigned)nt), dim3(kScanBlock), 0, stream, in, n,
-                     out, status, ticket);
+  const bool big = n_out > (int64_t)kLbBig * kLbItems * 64;
+  const int64_t tile = (big ? kLbBig : kScanBlock) * (int64_t)kLbItems;
+  const int64_t nt = (n_out + tile - 1) / tile;
+  if (nt >= (int64_t(1) << 31)) {
+    set_error("exclusive scan: too many tiles");
+    return RPT_ENOTSUP;
+  }
+  ScanState* s = nullptr;
+  uint32_t epoch = 0;
+  RPT_TRY(scan_state(stream, nt, &s, &epoch));
+  auto* ticket = reinterpret_cast<unsigned long long*>(s->status + s->cap);
+  if (big)
+    hipLaunchKernelGGL((k_scan_lb<T, U, kLbBig>), dim3((unsigned)nt), dim3(kLbBig), 0, stream,
+                       in, n_in, out, n_out, s->status, ticket, (uint64_t)epoch, (uint32_t)nt);
+  else
+    hipLaunchKernelGGL((k_scan_lb<T, U, kScanBlock>), dim3((unsigned)nt), dim3(kScanBlock), 0,
+                       stream, in, n_in, out, n_out, s->status, ticket, (uint64_t)epoch,
+                       (uint32_t)nt);
   RPT_CHECK_LAUNCH();
   return RPT_OK;
 }
 
 int32_t exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp,
                            hipStream_t stream) {
-  return scan_impl<int64_t, int64_t>(in, out, n, tmp, stream);
+  (void)tmp;
+  return scan_impl<int64_t, int64_t>(in, n, out, n, stream);
 }
 int32_t exclusive_scan_i32_to_i64(const int32_t* in, int64_t* out, int64_t n, int64_t* tmp,
                                   hipStream_t stream) {
-  return scan_impl<int32_t, int64_t>(in, out, n, tmp, stream);
+  (void)tmp;
+  return scan_impl<int32_t, int64_t>(in, n, out, n, stream);
 }
 int32_t exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, int64_t* tmp,
                            hipStream_t stream) {
-  return scan_impl<int32_t, int32_t>(in, out, n, tmp, stream);
+  (void)tmp;
+  return scan_impl<int32_t, int32_t>(in, n, out, n, stream);
+}
+int32_t exclusive_scan_total_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t stream) {
+  return scan_impl<int64_t, int64_t>(in, n, out, n + 1, stream);
+}
+int32_t exclusive_scan_total_i32_to_i64(const int32_t* in, int64_t* out, int64_t n,
+                                        hipStream_t stream) {
+  return scan_impl<int32_t, int64_t>(in, n, out, n + 1, stream);
+}
+int32_t exclusive_scan_total_i32(const int32_t* in, int32_t* out, int64_t n, hipStream_t stream) {
+  return scan_impl<int32_t, int32_t>(in, n, out, n + 1, stream);
+}
+
+// ------------------------------------------------------------------ packed readback
+// Copies up to kPackMax device arrays (4-byte multiples) back to back into dst, so that a
+// readback is one DMA instead of one per array (each D2H costs ~10 us of issue on the stream).
+__global__ void k_pack(PackList l, uint32_t* __restrict__ dst) {
+  const int64_t total = l.off[l.k];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int s = 0;
+    while (s + 1 < l.k && i >= l.off[s + 1]) ++s;
+    dst[i] = l.src[s][i - l.off[s]];
+  }
+}
+
+int32_t pack_arrays(const PackList& l, uint32_t* dst, hipStream_t st) {
+  if (l.k <= 0 || l.off[l.k] == 0) return RPT_OK;
+  hipLaunchKernelGGL(k_pack, dim3(grid_for(l.off[l.k], 256, 2048)), dim3(256), 0, st, l, dst);
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
 }
 
 // ------------------------------------------------------------------ radix sort

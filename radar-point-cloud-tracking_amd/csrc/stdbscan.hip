@@ -389,10 +389,11 @@ __device__ __forceinline__ float4 rec_boxB(const CellRec<3>& r) {
   return make_float4(r.z0, r.z1, r.t0, r.t1);
 }
 
-// Per-cell bounding boxes, one wave per occupied cell.  boxA = {xmin, xmax, ymin, ymax},
-// boxB = {zmin, zmax, tmin, tmax}.  mutual[c] = 1 when every pair of points in the cell passes
-// the neighbour test (computed conservatively from the box with the same rounding as the pair
-// test).
+// Per-cell bounding boxes, EIGHT lanes per occupied cell (eight cells per wave: most cells hold a
+// few dozen points, so a wave per cell would mostly wait on its loads).  boxA = {xmin, xmax,
+// ymin, ymax}, boxB = {zmin, zmax, tmin, tmax}.  mutual[c] = 1 when every pair of points in the
+// cell passes the neighbour test (computed conservatively from the box with the same rounding as
+// the pair test).
 template <int D>
 __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ pts,
                                                     const int32_t* __restrict__ cell_start,
@@ -402,33 +403,39 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ 
                                                     float4* __restrict__ boxB,
                                                     uint8_t* __restrict__ mutual,
                                                     CellRec<D>* __restrict__ crec) {
-  const int lane = threadIdx.x & 63;
-  const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
-  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+  const int j = threadIdx.x & 7;
   const int64_t no = *n_occ;
-  for (int64_t q = w0; q < no; q += nw) {
-    const int c = occ[q];
-    const int b = cell_start[c], e = cell_start[c + 1];
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t - j < no * 8;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t q = t >> 3;
+    const bool act = q < no;
+    int c = 0, b = 0, e = 0;
+    if (act) {
+      c = occ[q];
+      b = cell_start[c];
+      e = cell_start[c + 1];
+    }
     float x0 = FLT_MAX, x1 = -FLT_MAX, y0 = FLT_MAX, y1 = -FLT_MAX;
     float z0 = FLT_MAX, z1 = -FLT_MAX, t0 = FLT_MAX, t1 = -FLT_MAX;
-    for (int j = b + lane; j < e; j += 64) {
-      const float4 p = pts[j];
+    for (int s2 = b + j; s2 < e; s2 += 8) {
+      const float4 p = pts[s2];
       x0 = fminf(x0, p.x); x1 = fmaxf(x1, p.x);
       y0 = fminf(y0, p.y); y1 = fmaxf(y1, p.y);
       z0 = fminf(z0, p.z); z1 = fmaxf(z1, p.z);
       t0 = fminf(t0, p.w); t1 = fmaxf(t1, p.w);
     }
-    x0 = wave_minf(x0); x1 = wave_maxf(x1);
-    y0 = wave_minf(y0); y1 = wave_maxf(y1);
-    t0 = wave_minf(t0); t1 = wave_maxf(t1);
-    if (D == 3) {
-      z0 = wave_minf(z0);
-      z1 = wave_maxf(z1);
-    } else {
+#pragma unroll
+    for (int off = 4; off > 0; off >>= 1) {
+      x0 = fminf(x0, __shfl_xor(x0, off, 8)); x1 = fmaxf(x1, __shfl_xor(x1, off, 8));
+      y0 = fminf(y0, __shfl_xor(y0, off, 8)); y1 = fmaxf(y1, __shfl_xor(y1, off, 8));
+      z0 = fminf(z0, __shfl_xor(z0, off, 8)); z1 = fmaxf(z1, __shfl_xor(z1, off, 8));
+      t0 = fminf(t0, __shfl_xor(t0, off, 8)); t1 = fmaxf(t1, __shfl_xor(t1, off, 8));
+    }
+    if (D != 3) {
       z0 = t0;  // 2-D: pts[].z carries t (unused by the 2-D tests)
       z1 = t1;
     }
-    if (lane == 0) {
+    if (act && j == 0) {
       boxA[c] = make_float4(x0, x1, y0, y1);
       boxB[c] = make_float4(z0, z1, t0, t1);
       CellRec<D> r{};
@@ -458,21 +465,25 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ 
   }
 }
 
-// Actual time range per slab (slabs are the slowest key dimension, so each slab's points are
-// contiguous in sorted order).  One block per slab.
-__global__ __launch_bounds__(kBlock) void k_slab_range(const float4* __restrict__ pts,
+// Actual time range per slab from its occupied cells' records (slabs are the slowest key
+// dimension: a slab's cells are a contiguous range of the ascending occupied-cell list, found
+// through the head-flag scan at the slab's first point).  One block per slab.
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_slab_range(const CellRec<D>* __restrict__ crec,
+                                                      const int32_t* __restrict__ occ,
+                                                      const int32_t* __restrict__ hpos,
                                                       const int32_t* __restrict__ cell_start,
                                                       int64_t cells_per_slab, int nt,
                                                       float2* __restrict__ slab_t) {
   const int s = blockIdx.x;
   if (s >= nt) return;
-  const int b = cell_start[(int64_t)s * cells_per_slab];
-  const int e = cell_start[(int64_t)(s + 1) * cells_per_slab];
+  const int q0 = hpos[cell_start[(int64_t)s * cells_per_slab]];
+  const int q1 = hpos[cell_start[(int64_t)(s + 1) * cells_per_slab]];
   float lo = FLT_MAX, hi = -FLT_MAX;
-  for (int j = b + threadIdx.x; j < e; j += blockDim.x) {
-    const float tv = pts[j].w;
-    lo = fminf(lo, tv);
-    hi = fmaxf(hi, tv);
+  for (int q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
+    const CellRec<D> r = crec[occ[q]];
+    lo = fminf(lo, r.t0);
+    hi = fmaxf(hi, r.t1);
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -1756,20 +1767,19 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   RPT_TRY(radix_sort_pairs(keys, vals, keys_alt, vals_alt, n, bits, rtmp, &sk, &sv, st));
   hipLaunchKernelGGL(k_gather<D>, dim3(gb), dim3(kBlock), 0, st, x, y, z, stride, t, n, sk, sv,
                      pts, sorig, skey);
-  RPT_HIP(hipMemsetAsync(cell_start, 0, sizeof(int32_t) * (C1 + 1), st));
-  RPT_HIP(hipMemsetAsync(hpos + n, 0, sizeof(int32_t), st));
+  RPT_HIP(hipMemsetAsync(cell_start, 0, sizeof(int32_t) * C1, st));
   hipLaunchKernelGGL(k_cell_runs, dim3(gb), dim3(kBlock), 0, st, skey, n, cell_start, hpos);
   RPT_CHECK_LAUNCH();
-  RPT_TRY(exclusive_scan_i32(cell_start, cell_start, C1 + 1, stmp, st));
-  RPT_TRY(exclusive_scan_i32(hpos, hpos, n + 1, stmp, st));
+  RPT_TRY(exclusive_scan_total_i32(cell_start, cell_start, C1, st));
+  RPT_TRY(exclusive_scan_total_i32(hpos, hpos, n, st));
   RPT_HIP(hipMemsetAsync(occ_bits, 0, sizeof(uint32_t) * (C1 / 32 + 2), st));
   hipLaunchKernelGGL(k_occ_list, dim3(gb), dim3(kBlock), 0, st, skey, n, hpos, occ, occ_bits);
   RPT_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_cell_box<D>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, cell_start,
-                     occ, hpos + n, g, boxA, boxB, mutual, cr);
+  hipLaunchKernelGGL(k_cell_box<D>, dim3(grid_for(8 * n, kBlock, 8192)), dim3(kBlock), 0, st,
+                     pts, cell_start, occ, hpos + n, g, boxA, boxB, mutual, cr);
   RPT_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_slab_range, dim3((unsigned)nt), dim3(kBlock), 0, st, pts, cell_start,
-                     (int64_t)(C / nt), (int)nt, slab_t);
+  hipLaunchKernelGGL(k_slab_range<D>, dim3((unsigned)nt), dim3(kBlock), 0, st, cr, occ, hpos,
+                     cell_start, (int64_t)(C / nt), (int)nt, slab_t);
   RPT_CHECK_LAUNCH();
   tm.mark();
   return RPT_OK;
@@ -1883,12 +1893,12 @@ int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hi
     return RPT_OK;
   }
   int32_t* nc_count = nc_list + n;
-  RPT_HIP(hipMemsetAsync(cid, 0, sizeof(int32_t) * (n + 1), st));
+  RPT_HIP(hipMemsetAsync(cid, 0, sizeof(int32_t) * n, st));
   RPT_HIP(hipMemsetAsync(nc_count, 0, sizeof(int32_t), st));
   hipLaunchKernelGGL(k_ccmin, dim3(tile_grid(n)), dim3(kBlock), 0, st, parent, core, n, sorig,
                      ccmin, cid, nc_list, nc_count);
   RPT_CHECK_LAUNCH();
-  RPT_TRY(exclusive_scan_i32(cid, cid, n + 1, stmp, st));
+  RPT_TRY(exclusive_scan_total_i32(cid, cid, n, st));
   hipLaunchKernelGGL(k_label_core, dim3(gb), dim3(kBlock), 0, st, ccmin, n, sorig, cid, labels);
   if (dim == 2)
     hipLaunchKernelGGL((k_label<2, false>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,

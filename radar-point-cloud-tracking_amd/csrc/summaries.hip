@@ -314,7 +314,6 @@ int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
   b.add<int32_t>(n + 1);
   b.add<int64_t>(n + 1);
   b.add<int64_t>(n + 1);
-  b.add<int64_t>(scan_tmp_elems(n + 1));
   for (int k = 0; k < 3; ++k) b.add<float>(n + 1);
   RPT_TRY(sc.reserve(b.bytes, st));
   uint32_t* keys = sc.carve_n<uint32_t>(n + 1);
@@ -325,7 +324,6 @@ int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
   int32_t* head = sc.carve_n<int32_t>(n + 1);
   int64_t* pos = sc.carve_n<int64_t>(n + 1);
   int64_t* seg_start = sc.carve_n<int64_t>(n + 1);
-  int64_t* tmp = sc.carve_n<int64_t>(scan_tmp_elems(n + 1));
   float* gx = sc.carve_n<float>(n + 1);
   float* gy = sc.carve_n<float>(n + 1);
   float* gi = sc.carve_n<float>(n + 1);
@@ -346,8 +344,7 @@ int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
   RPT_TRY(radix_sort_pairs(keys, vals, ka, va, n, bits, rtmp, &sk, &sv, st));
   hipLaunchKernelGGL(k_heads, dim3(g), dim3(kBlock), 0, st, sk, sv, pf, n, head,
                      frame_first_noise);
-  RPT_HIP(hipMemsetAsync(head + n, 0, sizeof(int32_t), st));
-  RPT_TRY(exclusive_scan_i32_to_i64(head, pos, n + 1, tmp, st));
+  RPT_TRY(exclusive_scan_total_i32_to_i64(head, pos, n, st));
   hipLaunchKernelGGL(k_seg_starts, dim3(g), dim3(kBlock), 0, st, head, pos, n, seg_start);
   RPT_CHECK_LAUNCH();
   int64_t n_seg = 0;

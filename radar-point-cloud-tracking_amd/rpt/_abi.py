@@ -128,6 +128,7 @@ _SIGS = [
     ("rpt_device_count", C.c_int32, []),
     ("rpt_set_device", C.c_int32, [C.c_int32]),
     ("rpt_release_scratch", None, []),
+    ("rpt_exclusive_scan", C.c_int32, [vp, C.c_int32, C.c_int64, vp, C.c_int32, C.c_int32, vp]),
     ("rpt_polar_count", C.c_int32,
      [vp, C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_float, C.c_int32, vp, vp, c_i64p, vp]),
     ("rpt_polar_write", C.c_int32,

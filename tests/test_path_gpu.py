@@ -318,7 +318,7 @@ def _oracle_stack(echo, cfg, geo):
 
 
 @pytest.mark.parametrize("n_frames,land", [(6, True), (14, True), (14, False)])
-def test_stack_path_matches_oracle(gpu, n_frames, land):
+def test_stack_path_matches_oracle(gpu, n_frames, land, monkeypatch):
     """echo in HBM -> K1 -> land -> ST-DBSCAN -> K9 -> order -> C++ tracker, against the oracle
     run of the same stages (oracle.run_path)."""
     from rpt.pipeline import FrameStackPipeline, PathParams
@@ -330,9 +330,16 @@ def test_stack_path_matches_oracle(gpu, n_frames, land):
     pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(land_filter=land), gpu)
     pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
                       n_frames * len(cfg.gains))
-    res = pipe.run(echo_d, keep_points=True)
     frames = _oracle_stack(echo_d.cpu().numpy(), cfg, ds.geo)
     o_frames, o_labels, o_clusters, o_trk = op.run_path(frames, land=land)
+    # run 1 sizes the buffers (two-pass K1); run 2 takes the opt-in single-pass K1 (u8, 1024 bins)
+    for one_pass in ("0", "1"):
+        monkeypatch.setenv("RPT_K1_ONE_PASS", one_pass)
+        res = pipe.run(echo_d, keep_points=True)
+        _check_stack_vs_oracle(res, n_frames, frames, o_frames, o_labels, o_clusters, o_trk)
+
+
+def _check_stack_vs_oracle(res, n_frames, frames, o_frames, o_labels, o_clusters, o_trk):
     assert res.n_points == sum(len(p) for _, p, _ in frames)
     np.testing.assert_array_equal(res.labels.cpu().numpy(), o_labels)
     # per-frame cluster rows in reference order
@@ -349,6 +356,31 @@ def test_stack_path_matches_oracle(gpu, n_frames, land):
     for x, y in zip(a, b):
         np.testing.assert_array_equal(np.vstack(x.positions), np.vstack(y.positions))
         assert x.frames_seen == y.frames_seen
+
+
+def test_single_pass_k1_matches_two_pass(gpu, monkeypatch):
+    """Bench-size stack (12 frames x 3 gains x 4096 x 1024 u8): the first run of a pipeline uses
+    the two-pass K1 (count, write), the second the opt-in single-pass K1 (decoupled look-back);
+    points, labels and segments must be bit-identical."""
+    from rpt.pipeline import FrameStackPipeline, PathParams
+    from rpt.synth import DeviceSynth, SynthConfig
+
+    cfg = SynthConfig(n_frames=12)
+    ds = DeviceSynth(cfg, gpu)
+    echo = ds.echo()
+    pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), gpu)
+    pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
+                      cfg.n_frames * 3)
+    monkeypatch.setenv("RPT_K1_ONE_PASS", "0")
+    a = pipe.run(echo, keep_points=True)
+    monkeypatch.setenv("RPT_K1_ONE_PASS", "1")
+    b = pipe.run(echo, keep_points=True)
+    assert a.n_points == b.n_points and a.n_clustered_input == b.n_clustered_input
+    for k in a.points:
+        assert torch.equal(a.points[k], b.points[k]), k
+    assert torch.equal(a.labels, b.labels)
+    for k in a.seg:
+        np.testing.assert_array_equal(a.seg[k], b.seg[k])
 
 
 def test_full_size_partition_is_order_invariant(gpu):

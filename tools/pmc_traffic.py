@@ -13,7 +13,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 tag = sys.argv[1] if len(sys.argv) > 1 else "r1"
-K5 = ("k_core_fast", "k_core_slow")
+K5 = ("k_core_cells_oct", "k_core_cell_fast", "k_core_cell_window", "k_core_fill", "k_core_slow")
 
 
 def load(counter):
@@ -48,8 +48,8 @@ total = sum(r[4] for r in k5.values() if r)
 res = {"kernels": {k: (None if r is None else {"fetch_kib": r[2], "write_kib": r[3],
                                                  "bytes": r[4]}) for k, r in k5.items()},
        "bytes_per_launch": total,
-       "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch, summed over k_core_fast + "
-                  "k_core_slow; separate --pmc passes",
+       "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch, summed over the K5 kernels "
+                  "that ran (" + ", ".join(k for k, r in k5.items() if r) + "); separate --pmc passes",
        "workload": "bench.py default (100-frame stack)"}
 (out_dir / "k5_traffic.json").write_text(json.dumps(res, indent=1))
 print(json.dumps(res))
