@@ -229,320 +229,187 @@ __global__ __launch_bounds__(kBlock) void k_row_write(
   }
 }
 
-// ---- u8 fast path (the radar's native sample type).  For integer samples v in [0, 255],
-// (float)v > thr  <=>  v > T  with T = floor(thr) clamped to [-1, 255] (NaN -> 255: nothing kept),
-// evaluated on 4 bytes at once (SWAR, exact per byte, no carries across bytes):
-//   T <= 127 : hi bit of ((x & 0x7f..) + (127 - T) * 0x01..) | x
-//   T >= 128 : hi bit of ((x & 0x7f..) + (255 - T) * 0x01..) & x
-__device__ __forceinline__ uint32_t gt_mask(uint32_t x, int T) {
-  if (T < 0) return 0x80808080u;
-  if (T >= 255) return 0u;
+// ---- u8 fast path (the radar's native sample type), bins == 1024: one 16-B load per lane per
+// row.  For integer samples v in [0, 255], (float)v > thr  <=>  v > T with T = floor(thr) clamped
+// to [-1, 255] (NaN -> 255: nothing kept), evaluated on 4 bytes at once (SWAR, exact per byte,
+// no carries across bytes), K = (HI ? 255 - T : 127 - T) * 0x01010101:
+//   T <= 127 : hi bit of ((x & 0x7f..) + K) | x
+//   T >= 128 : hi bit of ((x & 0x7f..) + K) & x
+template <bool HI>
+__device__ __forceinline__ uint32_t keep_bits(uint32_t x, uint32_t K) {
   const uint32_t lo = x & 0x7f7f7f7fu;
-  if (T <= 127) return ((lo + (uint32_t)(127 - T) * 0x01010101u) | x) & 0x80808080u;
-  return ((lo + (uint32_t)(255 - T) * 0x01010101u) & x) & 0x80808080u;
+  return (HI ? ((lo + K) & x) : ((lo + K) | x)) & 0x80808080u;
 }
-// the 4 per-byte hi bits of a mask -> 4-bit nibble (byte k -> bit k)
-__device__ __forceinline__ uint32_t nib(uint32_t m) { return ((m >> 7) * 0x10204080u) >> 28; }
+// The 16 per-byte keep bits of a lane (bytes 0x80 or 0 in m0..m3) -> a 16-bit mask, sample k ->
+// bit k: two dot4 products per 8 samples (weights 1..8 and 16..128 on the 0x80 bytes) instead of
+// a multiply-gather per dword.
+__device__ __forceinline__ uint32_t mask16(uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3) {
+  const uint32_t lo = __builtin_amdgcn_udot4(
+      m0, 0x08040201u, __builtin_amdgcn_udot4(m1, 0x80402010u, 0u, false), false);
+  const uint32_t hi = __builtin_amdgcn_udot4(
+      m2, 0x08040201u, __builtin_amdgcn_udot4(m3, 0x80402010u, 0u, false), false);
+  return (lo | (hi << 8)) >> 7;
+}
 
-// Rows per wave iteration: their loads are issued together (4 KiB in flight per wave) before any
-// row is reduced, instead of one dependent 1-KiB load per iteration.
-constexpr int kRowsPerIter = 4;
+// Rows are handled in groups of kGroupRows consecutive rows of one file (the last group of a file
+// may be short): a wave issues the group's loads together (4 KiB in flight) before ranking any of
+// them.  The count pass writes one kept count per GROUP; the write pass walks the group's rows in
+// order and carries the in-file rank across them, so no per-row reduction or prefix is needed.
+constexpr int kGroupRows = 4;
 
-__global__ __launch_bounds__(kBlock) void k_row_count_u8(const uint8_t* __restrict__ echo,
-                                                        int64_t n_rows, int bins, int T,
-                                                        int32_t* __restrict__ row_count) {
+struct GroupMap {
+  uint32_t gpf;   // groups per file = ceil(rows / kGroupRows)
+  int rows;
+};
+// file, first row of the group in the stack and its row count (all wave-uniform)
+__device__ __forceinline__ void group_rows(const GroupMap& gm, uint32_t grp, uint32_t* f,
+                                           int64_t* row0, int* nr) {
+  const uint32_t ff = grp / gm.gpf;
+  const int r0 = (int)(grp - ff * gm.gpf) * kGroupRows;
+  *f = ff;
+  *row0 = (int64_t)ff * gm.rows + r0;
+  *nr = min(kGroupRows, gm.rows - r0);
+}
+
+template <bool HI>
+__global__ __launch_bounds__(kBlock) void k_group_count_u8(const uint8_t* __restrict__ echo,
+                                                          uint32_t n_groups, GroupMap gm,
+                                                          uint32_t K,
+                                                          int32_t* __restrict__ group_count) {
   const int lane = threadIdx.x & 63;
-  const int64_t wave0 = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / 64;
-  const int64_t n_waves = (int64_t)gridDim.x * kWavesPerBlock;
-  const int64_t n_groups = (n_rows + kRowsPerIter - 1) / kRowsPerIter;
-  for (int64_t grp = wave0; grp < n_groups; grp += n_waves) {
-    const int64_t row0 = grp * kRowsPerIter;
-    int c[kRowsPerIter];
+  const uint32_t wave0 = blockIdx.x * kWavesPerBlock + threadIdx.x / 64;
+  const uint32_t n_waves = gridDim.x * kWavesPerBlock;
+  for (uint32_t g0 = wave0; g0 < n_groups; g0 += n_waves) {
+    const uint32_t grp = __builtin_amdgcn_readfirstlane(g0);
+    uint32_t f;
+    int64_t row0;
+    int nr;
+    group_rows(gm, grp, &f, &row0, &nr);
+    uint4 v[kGroupRows];
 #pragma unroll
-    for (int k = 0; k < kRowsPerIter; ++k) c[k] = 0;
-    for (int b0 = lane * 16; b0 < bins; b0 += 64 * 16) {
-      uint4 v[kRowsPerIter];
+    for (int k = 0; k < kGroupRows; ++k)
+      v[k] = (k < nr) ? *reinterpret_cast<const uint4*>(echo + (row0 + k) * 1024 + lane * 16)
+                      : make_uint4(0u, 0u, 0u, 0u);
+    uint32_t c = 0;
 #pragma unroll
-      for (int k = 0; k < kRowsPerIter; ++k)
-        v[k] = (row0 + k < n_rows) ? *reinterpret_cast<const uint4*>(echo + (row0 + k) * bins + b0)
-                                   : make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-      for (int k = 0; k < kRowsPerIter; ++k)
-        c[k] += __popc(gt_mask(v[k].x, T)) + __popc(gt_mask(v[k].y, T)) +
-                __popc(gt_mask(v[k].z, T)) + __popc(gt_mask(v[k].w, T));
+    for (int k = 0; k < kGroupRows; ++k) {
+      if (k >= nr) break;  // a zero sample is kept when T = -1
+      c += __popc(keep_bits<HI>(v[k].x, K)) + __popc(keep_bits<HI>(v[k].y, K)) +
+           __popc(keep_bits<HI>(v[k].z, K)) + __popc(keep_bits<HI>(v[k].w, K));
     }
+    int s = (int)c;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1)
-#pragma unroll
-      for (int k = 0; k < kRowsPerIter; ++k) c[k] += __shfl_xor(c[k], off);
-    if (lane < kRowsPerIter) {
-      int cv = c[0];
-#pragma unroll
-      for (int k = 1; k < kRowsPerIter; ++k) cv = (lane == k) ? c[k] : cv;
-      if (row0 + lane < n_rows) row_count[row0 + lane] = cv;
-    }
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if (lane == 0) group_count[grp] = s;
   }
 }
 
-// Emission of one u8 row of 1024 bins whose first kept element has in-file rank `rank`: the kept
-// elements whose rank is a multiple of stride go to out0 + (their in-file emitted index).  Each
-// lane ranks its kept elements (m* = per-byte keep masks of its 16 samples, c their count, incl
-// the wave-inclusive count), the emitted (bin, sample) pairs are staged in the wave's LDS slice
-// in output order and written with full-width stores.  Outputs at or beyond cap are dropped and
-// flagged in *overflow (single-pass K1 writes into a capacity guessed from the last run).
-__device__ __forceinline__ void emit_row_u8(const uint4 v, uint32_t m0, uint32_t m1, uint32_t m2,
-                                            uint32_t m3, int c, int incl, int tot, uint32_t rank,
-                                            int64_t out0, int64_t cap, float step,
-                                            const float* __restrict__ ranges, float ct, float st,
-                                            int32_t g, int32_t fr, uint32_t ustride, bool pow2,
-                                            uint32_t sh, uint32_t* __restrict__ stage, int lane,
-                                            float* __restrict__ x, float* __restrict__ y,
-                                            float* __restrict__ val, int32_t* __restrict__ gain_out,
-                                            int32_t* __restrict__ pf_out,
-                                            uint32_t* __restrict__ overflow) {
-  const uint32_t r = rank + (uint32_t)(incl - c);
-  const uint32_t first = pow2 ? ((rank + ustride - 1u) >> sh) : (rank + ustride - 1u) / ustride;
-  if (c) {
-    uint32_t m = nib(m0) | (nib(m1) << 4) | (nib(m2) << 8) | (nib(m3) << 12);
-    const uint32_t q = pow2 ? (r >> sh) : r / ustride;
-    const uint32_t rem = r - q * ustride;
-    int slot = (int)(q + (rem ? 1u : 0u) - first);
-    // drop the kept elements before the first emitted rank, then emit every stride-th
-    for (uint32_t t = rem ? ustride - rem : 0u; t > 0u && m; --t) m &= m - 1u;
-    while (m) {
-      const int k = __builtin_ctz(m);
-      const uint32_t w = (k < 4) ? v.x : (k < 8) ? v.y : (k < 12) ? v.z : v.w;
-      const uint32_t sample = __builtin_amdgcn_ubfe(w, (uint32_t)(8 * (k & 3)), 8u);
-      stage[slot++] = ((uint32_t)(lane * 16 + k) << 8) | sample;
-      for (uint32_t t = 0; t < ustride && m; ++t) m &= m - 1u;
-    }
+// file_offsets input: per file ceil(kept / stride) from the group prefix
+__global__ void k_file_counts_groups(const int64_t* __restrict__ gprefix, int64_t n_files,
+                                     uint32_t gpf, int stride, int64_t* __restrict__ file_out) {
+  for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < n_files;
+       f += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t kept = gprefix[(f + 1) * gpf] - gprefix[f * gpf];
+    file_out[f] = (kept + stride - 1) / stride;
   }
-  const int n_emit = (int)((pow2 ? ((rank + (uint32_t)tot + ustride - 1u) >> sh)
-                                 : (rank + (uint32_t)tot + ustride - 1u) / ustride) -
-                           first);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  for (int l = lane; l < n_emit; l += 64) {
-    const uint32_t e = stage[l];
-    const int b = (int)(e >> 8);
-    const int64_t o = out0 + first + l;
-    if (o >= cap) {
-      if (overflow) atomicOr(overflow, 1u);
-      continue;
-    }
-    const float rr = ranges ? ranges[b] : step * (float)b;
-    x[o] = rr * ct;
-    y[o] = rr * st;
-    val[o] = (float)(e & 0xffu);
-    if (gain_out) gain_out[o] = g;
-    if (pf_out) pf_out[o] = fr;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Single-pass K1 for u8 sweeps of 1024 bins (rows % 64 == 0): the count and write passes fused
-// with a decoupled look-back.  A block takes tiles of 64 rows (16 per wave, held in registers) in
-// ticket order (one same-address atomic per 64 KiB: they serialise in L2); it publishes the
-// tile's kept count, looks back over the earlier tiles of the same file for its in-file rank
-// (status granules {flag:2 | value:62}, agent-scope relaxed atomics: the data is the flag), takes
-// the file's output base from a second look-back over the files' emitted counts (fstat, published
-// by each file's last group), and emits.  Every wait is on a smaller ticket, so all waits end;
-// every spin is still bounded (a timeout sets *overflow and the host falls back to the two
-// passes).  file_off[f] receives the exclusive per-file output offsets (file_off[n_files] = N).
-constexpr uint64_t kK1Agg = 1ull << 62, kK1Inc = 2ull << 62, kK1Val = (1ull << 62) - 1;
-
-// Exclusive prefix of item `self` over items [first, self) of a status array of granules
-// {flag:2 | value:62} (aggregate or inclusive), one wave, 64 predecessors per round: the
-// aggregates back to the nearest inclusive.  Bounded spin; a timeout sets *err.
-__device__ __forceinline__ int64_t lookback(const uint64_t* __restrict__ status, int64_t self,
-                                            int64_t first, int lane, uint32_t* __restrict__ err) {
-  int64_t prefix = 0;
-  uint32_t spins = 0;
-  for (int64_t j = self - 1; j >= first;) {
-    const int64_t idx = j - lane;
-    const uint64_t st = (idx >= first) ? __hip_atomic_load(status + idx, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT)
-                                       : kK1Inc;  // before the range: an inclusive zero
-    const uint64_t incm = __ballot((st >> 62) == 2u);
-    const uint64_t zero = __ballot((st >> 62) == 0u);
-    const int fi = incm ? __ffsll((unsigned long long)incm) - 1 : 64;
-    const uint64_t upto = (fi >= 63) ? ~0ull : ((2ull << fi) - 1ull);
-    if (zero & upto) {
-      if (++spins > (1u << 22)) {
-        if (lane == 0) atomicOr(err, 2u);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    int64_t part = (lane <= fi && idx >= first) ? (int64_t)(st & kK1Val) : 0;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
-    prefix += part;
-    if (fi < 64) break;
-    j -= 64;
-  }
-  return prefix;
-}
-constexpr int kScanRowsPerWave = 16;                               // rows held in registers
-constexpr int kScanTileRows = kScanRowsPerWave * kWavesPerBlock;  // 64 rows per ticket
-__global__ __launch_bounds__(kBlock) void k_polar_scan_u8(
-    const uint8_t* __restrict__ echo, int64_t n_rows, int rows, int T, int stride, RowGeo geo,
-    const int32_t* __restrict__ gain, int files_per_frame, float* __restrict__ x,
-    float* __restrict__ y, float* __restrict__ val, int32_t* __restrict__ gain_out,
-    int32_t* __restrict__ pf_out, int64_t cap, uint64_t* __restrict__ status,
-    uint64_t* __restrict__ fstat, int64_t* __restrict__ file_off, uint32_t* __restrict__ ticket,
-    uint32_t* __restrict__ overflow) {
-  constexpr int CH = 64 * 16;
-  __shared__ uint32_t s_stage[kWavesPerBlock][CH];  // (bin << 8) | sample
-  __shared__ int64_t s_wtot[kWavesPerBlock];
-  __shared__ int64_t s_prefix, s_base;
-  __shared__ uint32_t s_tile;
+// Write pass: the kept elements whose in-file rank is a multiple of stride.  Per row: keep mask
+// (16 bits per lane), wave-inclusive count by DPP, and each lane with kept samples walks its mask
+// (skip to the first rank that is a multiple of stride, then every stride-th) staging (bin,
+// sample) in the wave's LDS slice in output order; the row's emitted points are then written by
+// consecutive lanes (full-width stores from scalar row bases).
+template <bool HI>
+__global__ __launch_bounds__(kBlock) void k_group_write_u8(
+    const uint8_t* __restrict__ echo, uint32_t n_groups, GroupMap gm, uint32_t K, int stride,
+    const float* __restrict__ scale, const float* __restrict__ cos_t,
+    const float* __restrict__ sin_t, const int32_t* __restrict__ gain,
+    const int64_t* __restrict__ gprefix, const int64_t* __restrict__ file_offsets,
+    int files_per_frame, float* __restrict__ x, float* __restrict__ y, float* __restrict__ val,
+    int32_t* __restrict__ gain_out, int32_t* __restrict__ pf_out) {
+  __shared__ uint32_t s_stage[kWavesPerBlock][1024];  // (bin << 8) | sample
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x / 64;
-  const float fb = (float)CH;
-  const uint32_t ustride = (uint32_t)stride;
-  const bool pow2 = (ustride & (ustride - 1u)) == 0u;
-  const uint32_t sh = (uint32_t)__builtin_ctz(ustride);
-  const int64_t tpf = rows / kScanTileRows;  // tiles per file
-  const int64_t n_tiles = n_rows / kScanTileRows;
-  while (true) {
-    if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const int64_t tile = s_tile;
-    if (tile >= n_tiles) break;  // uniform over the block
-    const int64_t f = tile / tpf;
-    const int64_t ti = tile - f * tpf;
-    const int64_t row0 = tile * kScanTileRows + wv * kScanRowsPerWave;
-    uint4 vv[kScanRowsPerWave];
+  uint32_t* stage = s_stage[wv];
+  const uint32_t wave0 = blockIdx.x * kWavesPerBlock + wv;
+  const uint32_t n_waves = gridDim.x * kWavesPerBlock;
+  const uint32_t us = (uint32_t)stride;
+  const bool pow2 = (us & (us - 1u)) == 0u;
+  const uint32_t sh = (uint32_t)__builtin_ctz(us);
+  const float inv_bins = 1.0f / 1024.0f;  // exact: step = scale / 1024 == scale * 2^-10
+  for (uint32_t g0 = wave0; g0 < n_groups; g0 += n_waves) {
+    const uint32_t grp = __builtin_amdgcn_readfirstlane(g0);
+    uint32_t f;
+    int64_t row0;
+    int nr;
+    group_rows(gm, grp, &f, &row0, &nr);
+    uint4 vv[kGroupRows];
 #pragma unroll
-    for (int k = 0; k < kScanRowsPerWave; ++k)
-      vv[k] = *reinterpret_cast<const uint4*>(echo + (row0 + k) * CH + lane * 16);
-    int tt[kScanRowsPerWave];
-    int wtot = 0;
-#pragma unroll
-    for (int k = 0; k < kScanRowsPerWave; ++k) {
-      const int c = __popc(gt_mask(vv[k].x, T)) + __popc(gt_mask(vv[k].y, T)) +
-                    __popc(gt_mask(vv[k].z, T)) + __popc(gt_mask(vv[k].w, T));
-      tt[k] = c;
-      wtot += c;
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) wtot += __shfl_xor(wtot, off);
-    if (lane == 0) s_wtot[wv] = wtot;
-    __syncthreads();
-    if (wv == 0) {
-      int64_t total = 0;
-#pragma unroll
-      for (int w = 0; w < kWavesPerBlock; ++w) total += s_wtot[w];
-      // the tile's count, then its in-file prefix from the earlier tiles of the file
-      if (lane == 0)
-        __hip_atomic_store(status + tile, (ti == 0 ? kK1Inc : kK1Agg) | (uint64_t)total,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int64_t prefix = lookback(status, tile, f * tpf, lane, overflow);
-      if (lane == 0 && ti > 0)
-        __hip_atomic_store(status + tile, kK1Inc | (uint64_t)(prefix + total), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      // the file's output base: a second look-back, over the files (fstat: the file's emitted
-      // count as soon as its last tile knows it, then its inclusive base + count)
-      const int64_t fcount = (prefix + total + stride - 1) / stride;
-      if (ti == tpf - 1 && lane == 0)
-        __hip_atomic_store(fstat + f, (f == 0 ? kK1Inc : kK1Agg) | (uint64_t)fcount,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int64_t base = lookback(fstat, f, 0, lane, overflow);
-      if (ti == tpf - 1 && lane == 0) {
-        if (f > 0)
-          __hip_atomic_store(fstat + f, kK1Inc | (uint64_t)(base + fcount), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        file_off[f + 1] = base + fcount;
-        if (f == 0) file_off[0] = 0;
-      }
-      if (lane == 0) {
-        s_prefix = prefix;
-        s_base = base;
-      }
-    }
-    __syncthreads();
-    // emission, row by row (ranks continue over the block's waves in row order)
-    uint32_t rank = (uint32_t)s_prefix;
-    for (int w = 0; w < wv; ++w) rank += (uint32_t)s_wtot[w];
-    const int64_t base = s_base;
+    for (int k = 0; k < kGroupRows; ++k)
+      vv[k] = (k < nr) ? *reinterpret_cast<const uint4*>(echo + (row0 + k) * 1024 + lane * 16)
+                       : make_uint4(0u, 0u, 0u, 0u);
+    // in-file rank of the group's first kept element (< rows * 1024 < 2^32) and output base
+    uint32_t rank = (uint32_t)(gprefix[grp] - gprefix[(int64_t)f * gm.gpf]);
+    const int64_t out0 = file_offsets[f];
     const int32_t g = gain ? gain[f] : 0;
-    const int32_t fr = (int32_t)((uint32_t)f / (uint32_t)files_per_frame);
+    const int32_t fr = (int32_t)(f / (uint32_t)files_per_frame);
 #pragma unroll
-    for (int k = 0; k < kScanRowsPerWave; ++k) {
+    for (int k = 0; k < kGroupRows; ++k) {
+      if (k >= nr) break;
       const int64_t row = row0 + k;
-      const uint32_t m0 = gt_mask(vv[k].x, T), m1 = gt_mask(vv[k].y, T),
-                     m2 = gt_mask(vv[k].z, T), m3 = gt_mask(vv[k].w, T);
-      const int incl = wave_incl_scan_dpp(tt[k]);
-      const int tot = __builtin_amdgcn_readlane(incl, 63);
-      const float step = geo.scale[row] / fb;
-      emit_row_u8(vv[k], m0, m1, m2, m3, tt[k], incl, tot, rank, base, cap, step, nullptr,
-                  geo.cos_t[row], geo.sin_t[row], g, fr, ustride, pow2, sh, s_stage[wv], lane, x,
-                  y, val, gain_out, pf_out, overflow);
-      rank += (uint32_t)tot;
-    }
-    __syncthreads();  // s_tile / s_wtot reuse
-  }
-}
-
-// Same contract as k_row_write (LDS-staged emission), u8 samples, bins == 1024 (one chunk per
-// row): kRowsPerIter rows' samples are loaded before the first is ranked.
-__global__ __launch_bounds__(kBlock) void k_row_write_u8(
-    const uint8_t* __restrict__ echo, int64_t n_rows, int rows, int bins, int T, int stride,
-    RowGeo geo, const int32_t* __restrict__ gain, const int64_t* __restrict__ row_prefix,
-    const int64_t* __restrict__ file_offsets, int files_per_frame, float* __restrict__ x,
-    float* __restrict__ y, float* __restrict__ val, int32_t* __restrict__ gain_out,
-    int32_t* __restrict__ pf_out) {
-  constexpr int CH = 64 * 16;
-  __shared__ uint32_t s_stage[kWavesPerBlock][CH];  // (bin << 8) | sample
-  const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x / 64;
-  const int64_t wave0 = (int64_t)blockIdx.x * kWavesPerBlock + wv;
-  const int64_t n_waves = (int64_t)gridDim.x * kWavesPerBlock;
-  const float fb = (float)bins;
-  const uint32_t ustride = (uint32_t)stride;
-  const int64_t n_groups = (n_rows + kRowsPerIter - 1) / kRowsPerIter;
-  const bool pow2 = (ustride & (ustride - 1u)) == 0u;
-  const uint32_t sh = (uint32_t)__builtin_ctz(ustride);
-  for (int64_t grp = wave0; grp < n_groups; grp += n_waves) {
-    // wave-uniform: lets the per-row metadata below use scalar loads / SALU
-    const int64_t row0 = (int64_t)__builtin_amdgcn_readfirstlane((int)grp) * kRowsPerIter;
-    uint4 vv[kRowsPerIter];
-#pragma unroll
-    for (int k = 0; k < kRowsPerIter; ++k)
-      vv[k] = (row0 + k < n_rows)
-                  ? *reinterpret_cast<const uint4*>(echo + (row0 + k) * CH + lane * 16)
-                  : make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-    for (int kk = 0; kk < kRowsPerIter; ++kk) {
-      const int64_t row = row0 + kk;
-      if (row >= n_rows) break;
-      const uint4 v = vv[kk];
-      const int64_t f = (int64_t)((uint32_t)row / (uint32_t)rows);
-      uint32_t rank = (uint32_t)(row_prefix[row] - row_prefix[f * rows]);
-      const int64_t out0 = file_offsets[f];
-      const float step = geo.scale ? geo.scale[row] / fb : 0.f;
-      const float ct = geo.cos_t[row], st = geo.sin_t[row];
-      const int32_t g = gain ? gain[f] : 0;
-      const int32_t fr = (int32_t)((uint32_t)f / (uint32_t)files_per_frame);
-      const uint32_t m0 = gt_mask(v.x, T), m1 = gt_mask(v.y, T), m2 = gt_mask(v.z, T),
-                     m3 = gt_mask(v.w, T);
-      const int c = __popc(m0) + __popc(m1) + __popc(m2) + __popc(m3);
+      const uint4 v = vv[k];
+      uint32_t m = mask16(keep_bits<HI>(v.x, K), keep_bits<HI>(v.y, K), keep_bits<HI>(v.z, K),
+                          keep_bits<HI>(v.w, K));
+      const int c = __popc(m);
       const int incl = wave_incl_scan_dpp(c);
-      const int tot = __builtin_amdgcn_readlane(incl, 63);
-      const float rs = geo.ranges ? 0.f : step;
-      emit_row_u8(v, m0, m1, m2, m3, c, incl, tot, rank, out0, INT64_MAX, rs,
-                  geo.ranges ? geo.ranges + row * bins : nullptr, ct, st, g, fr, ustride, pow2,
-                  sh, s_stage[wv], lane, x, y, val, gain_out, pf_out, nullptr);
+      const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+      // emitted in-file indices of this row: [first, last)
+      const uint32_t first = pow2 ? ((rank + us - 1u) >> sh) : (rank + us - 1u) / us;
+      const uint32_t last = pow2 ? ((rank + tot + us - 1u) >> sh) : (rank + tot + us - 1u) / us;
+      if (last > first) {  // wave-uniform
+        if (c) {
+          const uint32_t r = rank + (uint32_t)(incl - c);
+          const uint32_t q = pow2 ? ((r + us - 1u) >> sh) : (r + us - 1u) / us;
+          int slot = (int)(q - first);
+          // drop the kept samples before the first rank that is a multiple of stride
+          for (uint32_t t = q * us - r; t > 0u && m; --t) m &= m - 1u;
+          while (m) {
+            const int kk = __builtin_ctz(m);
+            const uint32_t w = (kk < 4) ? v.x : (kk < 8) ? v.y : (kk < 12) ? v.z : v.w;
+            stage[slot++] = ((uint32_t)(lane * 16 + kk) << 8) |
+                            __builtin_amdgcn_ubfe(w, (uint32_t)(8 * (kk & 3)), 8u);
+            for (uint32_t t = 0; t < us && m; ++t) m &= m - 1u;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const float step = scale[row] * inv_bins;
+        const float ct = cos_t[row], st = sin_t[row];
+        const int n_emit = (int)(last - first);
+        const int64_t o0 = out0 + first;
+        float* xr = x + o0;
+        float* yr = y + o0;
+        float* vr = val + o0;
+        for (int l = lane; l < n_emit; l += 64) {
+          const uint32_t e = stage[l];
+          const float rr = step * (float)(e >> 8);
+          xr[l] = rr * ct;
+          yr[l] = rr * st;
+          vr[l] = (float)(e & 0xffu);
+          if (gain_out) gain_out[o0 + l] = g;
+          if (pf_out) pf_out[o0 + l] = fr;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      rank += tot;
     }
   }
 }
 
-// integer threshold of u8 samples (see gt_mask)
+// integer threshold of u8 samples (see keep_bits)
 inline int u8_threshold(float thr) {
   if (!(thr == thr)) return 255;
   const double f = std::floor((double)thr);
@@ -554,34 +421,63 @@ constexpr bool is_u8() { return false; }
 template <>
 constexpr bool is_u8<uint8_t>() { return true; }
 
+// The grouped u8 kernels take u8 sweeps of exactly 1024 bins with 16-B aligned rows; row_prefix
+// then holds the per-GROUP exclusive prefix (n_files * ceil(rows / 4) + 1 values), otherwise the
+// per-row one.  Count and write decide the same way from the same arguments.
+template <class T>
+bool grouped_u8(const T* echo, int bins) {
+  return is_u8<T>() && bins == 1024 && (uintptr_t)echo % 16 == 0;
+}
+
+inline uint32_t u8_k(int T) {
+  return (uint32_t)(T <= 127 ? 127 - T : 255 - T) * 0x01010101u;
+}
+
 template <class T>
 int32_t count_impl(const T* echo, int64_t n_files, int rows, int bins, float thr, int stride,
                    int64_t* row_prefix, int64_t* file_offsets, int64_t* total_host,
                    hipStream_t st) {
   const int64_t n_rows = n_files * rows;
+  if ((int64_t)rows * bins >= (int64_t(1) << 32) || n_rows >= (int64_t(1) << 32)) {
+    set_error("rpt_polar_count: rows*bins and n_files*rows must be < 2^32");
+    return RPT_ENOTSUP;
+  }
+  const bool grouped = grouped_u8(echo, bins);
+  const GroupMap gm{(uint32_t)((rows + kGroupRows - 1) / kGroupRows), rows};
+  const int64_t n_units = grouped ? n_files * (int64_t)gm.gpf : n_rows;
   Scratch& sc = scratch();
   Budget b;
-  b.add<int32_t>(n_rows + 1);
-  b.add<int64_t>(n_files + 1);
+  b.add<int32_t>(n_units);
+  b.add<int64_t>(n_files);
   RPT_TRY(sc.reserve(b.bytes, st));
-  int32_t* rc = sc.carve_n<int32_t>(n_rows + 1);
-  int64_t* fo = sc.carve_n<int64_t>(n_files + 1);
+  int32_t* rc = sc.carve_n<int32_t>(n_units);
+  int64_t* fo = sc.carve_n<int64_t>(n_files);
   const bool vec = (bins % (64 * Vec<T>::N) == 0) && ((uintptr_t)echo % 16 == 0);
-  const int grid = grid_for(n_rows, kWavesPerBlock, 16384);
-  if (vec && is_u8<T>())
-    hipLaunchKernelGGL(k_row_count_u8, dim3(grid), dim3(kBlock), 0, st,
-                       reinterpret_cast<const uint8_t*>(echo), n_rows, bins, u8_threshold(thr),
-                       rc);
-  else if (vec)
+  const int grid = grid_for(n_units, kWavesPerBlock, 16384);
+  if (grouped) {
+    const int T8 = u8_threshold(thr);
+    const auto* e8 = reinterpret_cast<const uint8_t*>(echo);
+    if (T8 <= 127)
+      hipLaunchKernelGGL(k_group_count_u8<false>, dim3(grid), dim3(kBlock), 0, st, e8,
+                         (uint32_t)n_units, gm, u8_k(T8), rc);
+    else
+      hipLaunchKernelGGL(k_group_count_u8<true>, dim3(grid), dim3(kBlock), 0, st, e8,
+                         (uint32_t)n_units, gm, u8_k(T8), rc);
+  } else if (vec) {
     hipLaunchKernelGGL((k_row_count<T, true>), dim3(grid), dim3(kBlock), 0, st, echo, n_rows,
                        bins, thr, rc);
-  else
+  } else {
     hipLaunchKernelGGL((k_row_count<T, false>), dim3(grid), dim3(kBlock), 0, st, echo, n_rows,
                        bins, thr, rc);
+  }
   RPT_CHECK_LAUNCH();
-  RPT_TRY(exclusive_scan_total_i32_to_i64(rc, row_prefix, n_rows, st));
-  hipLaunchKernelGGL(k_file_counts, dim3(grid_for(n_files, 256, 1024)), dim3(256), 0, st,
-                     row_prefix, n_files, rows, stride, fo);
+  RPT_TRY(exclusive_scan_total_i32_to_i64(rc, row_prefix, n_units, st));
+  if (grouped)
+    hipLaunchKernelGGL(k_file_counts_groups, dim3(grid_for(n_files, 256, 1024)), dim3(256), 0, st,
+                       row_prefix, n_files, gm.gpf, stride, fo);
+  else
+    hipLaunchKernelGGL(k_file_counts, dim3(grid_for(n_files, 256, 1024)), dim3(256), 0, st,
+                       row_prefix, n_files, rows, stride, fo);
   RPT_CHECK_LAUNCH();
   RPT_TRY(exclusive_scan_total_i64(fo, file_offsets, n_files, st));
   if (total_host) {
@@ -604,20 +500,34 @@ int32_t write_impl(const T* echo, int64_t n_files, int rows, int bins, float thr
     return RPT_ENOTSUP;
   }
   const bool vec = (bins % (64 * Vec<T>::N) == 0) && ((uintptr_t)echo % 16 == 0);
-  const int grid = grid_for(n_rows, kWavesPerBlock, 16384);
-  if (vec && is_u8<T>() && bins == 64 * 16)
-    hipLaunchKernelGGL(k_row_write_u8, dim3(grid), dim3(kBlock), 0, st,
-                       reinterpret_cast<const uint8_t*>(echo), n_rows, rows, bins,
-                       u8_threshold(thr), stride, geo, gain, row_prefix, file_offsets, fpf, x, y,
-                       v, gout, pf);
-  else if (vec)
+  if (grouped_u8(echo, bins) && geo.scale) {
+    const GroupMap gm{(uint32_t)((rows + kGroupRows - 1) / kGroupRows), rows};
+    const int64_t n_groups = n_files * (int64_t)gm.gpf;
+    const int grid = grid_for(n_groups, kWavesPerBlock, 16384);
+    const int T8 = u8_threshold(thr);
+    const auto* e8 = reinterpret_cast<const uint8_t*>(echo);
+    if (T8 <= 127)
+      hipLaunchKernelGGL(k_group_write_u8<false>, dim3(grid), dim3(kBlock), 0, st, e8,
+                         (uint32_t)n_groups, gm, u8_k(T8), stride, geo.scale, geo.cos_t,
+                         geo.sin_t, gain, row_prefix, file_offsets, fpf, x, y, v, gout, pf);
+    else
+      hipLaunchKernelGGL(k_group_write_u8<true>, dim3(grid), dim3(kBlock), 0, st, e8,
+                         (uint32_t)n_groups, gm, u8_k(T8), stride, geo.scale, geo.cos_t,
+                         geo.sin_t, gain, row_prefix, file_offsets, fpf, x, y, v, gout, pf);
+  } else if (grouped_u8(echo, bins)) {
+    set_error("rpt_polar_write: u8 sweeps take per-row scale geometry");
+    return RPT_ENOTSUP;
+  } else if (vec) {
+    const int grid = grid_for(n_rows, kWavesPerBlock, 16384);
     hipLaunchKernelGGL((k_row_write<T, true>), dim3(grid), dim3(kBlock), 0, st, echo, n_rows,
                        rows, bins, thr, stride, geo, gain, row_prefix, file_offsets, fpf, x, y,
                        v, gout, pf);
-  else
+  } else {
+    const int grid = grid_for(n_rows, kWavesPerBlock, 16384);
     hipLaunchKernelGGL((k_row_write<T, false>), dim3(grid), dim3(kBlock), 0, st, echo, n_rows,
                        rows, bins, thr, stride, geo, gain, row_prefix, file_offsets, fpf, x, y,
                        v, gout, pf);
+  }
   RPT_CHECK_LAUNCH();
   return RPT_OK;
 }
@@ -757,43 +667,6 @@ __global__ __launch_bounds__(kBlock) void k_synth(rpt_synth_params p, int64_t fr
 }  // namespace
 
 // ---------------------------------------------------------------- C-ABI bodies
-// Single-pass K1 (see k_polar_scan_u8).  Returns RPT_EINVAL when the shape does not qualify;
-// *status_host: 0 ok, bit 0 = more than cap points (outputs incomplete), bit 1 = spin timeout.
-int32_t polar_scan_u8(const uint8_t* echo, int64_t n_files, int32_t rows, int32_t bins, float thr,
-                      int32_t stride, const float* scale, const float* cos_t, const float* sin_t,
-                      const int32_t* gain, int32_t fpf, float* x, float* y, float* v,
-                      int32_t* gout, int32_t* pf, int64_t cap, int64_t* file_off,
-                      uint64_t* work, size_t work_words, hipStream_t st) {
-  const int64_t n_rows = n_files * rows;
-  if (bins != 64 * 16 || rows % kScanTileRows || n_files < 1 || stride < 1 || fpf < 1 ||
-      (uintptr_t)echo % 16 || (int64_t)rows * bins >= (int64_t(1) << 32) ||
-      n_rows >= (int64_t(1) << 31)) {
-    set_error("polar_scan_u8: shape not supported");
-    return RPT_EINVAL;
-  }
-  const int64_t n_groups = n_rows / kScanTileRows;  // tiles
-  const size_t need = (size_t)n_groups + (size_t)n_files + 1 + 2;
-  if (!work || work_words < need) {
-    set_error("polar_scan_u8: work buffer too small");
-    return RPT_EINVAL;
-  }
-  RPT_HIP(hipMemsetAsync(work, 0, need * sizeof(uint64_t), st));
-  uint64_t* status = work;
-  uint64_t* fstat = work + n_groups;
-  uint32_t* ticket = reinterpret_cast<uint32_t*>(work + n_groups + n_files + 1);
-  uint32_t* overflow = ticket + 2;
-  RowGeo geo{scale, nullptr, cos_t, sin_t};
-  int dev = 0, n_cu = 0;
-  RPT_HIP(hipGetDevice(&dev));
-  RPT_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-  const int grid = (int)std::min<int64_t>((int64_t)std::max(n_cu, 1) * 4, n_groups);
-  hipLaunchKernelGGL(k_polar_scan_u8, dim3(grid), dim3(kBlock), 0, st, echo, n_rows, rows,
-                     u8_threshold(thr), stride, geo, gain, fpf, x, y, v, gout, pf, cap, status,
-                     fstat, file_off, ticket, overflow);
-  RPT_CHECK_LAUNCH();
-  return RPT_OK;
-}
-
 int32_t polar_count(const void* echo, int32_t dt, int64_t n_files, int32_t rows, int32_t bins,
                     float thr, int32_t stride, int64_t* row_prefix, int64_t* file_offsets,
                     int64_t* total_host, hipStream_t st) {

@@ -10,7 +10,6 @@
 // back in one packed copy.  Buffers are owned by the handle and grow only.
 #include <algorithm>
 #include <cmath>
-#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -25,11 +24,6 @@ int32_t polar_write(const void* echo, int32_t dt, int64_t n_files, int32_t rows,
                     const int32_t* gain, float thr, int32_t stride, const int64_t* row_prefix,
                     const int64_t* file_offsets, int32_t files_per_frame, float* x, float* y,
                     float* v, int32_t* gout, int32_t* pf, hipStream_t st);
-int32_t polar_scan_u8(const uint8_t* echo, int64_t n_files, int32_t rows, int32_t bins, float thr,
-                      int32_t stride, const float* scale, const float* cos_t, const float* sin_t,
-                      const int32_t* gain, int32_t fpf, float* x, float* y, float* v,
-                      int32_t* gout, int32_t* pf, int64_t cap, int64_t* file_off,
-                      uint64_t* work, size_t work_words, hipStream_t st);
 int32_t frame_times(const int32_t* pf, int64_t n, const int64_t* ids, float* t, hipStream_t st);
 int32_t bounds_xy(const float* x, const float* y, int64_t n, float* out4, hipStream_t st);
 int32_t land_grid(const float* x, const float* y, const float* val, int64_t n, const double* xe,
@@ -151,8 +145,6 @@ struct rpt_stack {
   DevBuf<int32_t> g, pf, g2, pf2, labels, land_cnt, seg_frame, seg_label;
   DevBuf<double> land_tot, edges;
   DevBuf<uint8_t> land_mask;
-  DevBuf<uint64_t> k1work;   // single-pass K1 look-back state
-  int64_t k1_cap = 0;        // point capacity for single-pass K1 (from the previous runs)
   PinnedBuf up, down;  // host staging: uploads (edges, offsets), readbacks
   std::vector<int64_t> fo_k1, fo_in;
   std::vector<int32_t> h_frame, h_label;
@@ -174,7 +166,6 @@ struct rpt_stack {
     for (auto* b : i32) b->release();
     land_tot.release();
     edges.release();
-    k1work.release();
     pack_d.release();
     land_mask.release();
     up.release();
@@ -208,51 +199,16 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
   if (timing) RPT_HIP(hipEventRecord(ev[0], st));
   rpt_stack_result r{};
 
-  // ---- K1.  u8 sweeps of 1024 bins once a previous run sized the outputs: ONE pass (count and
-  // write fused, decoupled look-back) then one readback of the file offsets; otherwise (or when
-  // the points outgrow that capacity) count -> per-file offsets (one readback) -> write.
+  // ---- K1: count -> per-file offsets (one readback sizes the outputs) -> write
   RPT_TRY(file_off.ensure((size_t)n_files + 1, st));
   RPT_TRY(down.ensure(sizeof(int64_t) * (size_t)(n_files + 2 * F + 8), st));
   int64_t* hfo = reinterpret_cast<int64_t*>(down.p);
-  bool done = false;
-  // the single-pass kernel is opt-in (RPT_K1_ONE_PASS=1): its tile chain is still slower than the
-  // two streaming passes on the bench stack (profiles/r1)
-  const char* one_pass_var = std::getenv("RPT_K1_ONE_PASS");
-  const bool one_pass_env = one_pass_var && std::atoi(one_pass_var) != 0;
-  const bool one_pass = one_pass_env && p.echo_dtype == RPT_ECHO_U8 && p.bins == 1024 &&
-                        p.rows % 64 == 0 && k1_cap > 0 && (uintptr_t)echo % 16 == 0;
-  if (one_pass) {
-    const size_t words = (size_t)(n_files * p.rows / 64) + (size_t)n_files + 3;
-    RPT_TRY(k1work.ensure(words, st));
-    const size_t cap0 = (size_t)k1_cap;
-    RPT_TRY(x.ensure(cap0, st));
-    RPT_TRY(y.ensure(cap0, st));
-    RPT_TRY(v.ensure(cap0, st));
-    RPT_TRY(g.ensure(cap0, st));
-    RPT_TRY(pf.ensure(cap0, st));
-    const int64_t cap = (int64_t)std::min({x.cap, y.cap, v.cap, g.cap, pf.cap});
-    RPT_TRY(polar_scan_u8((const uint8_t*)echo, n_files, p.rows, p.bins, p.threshold, p.stride,
-                          scale, cos_t, sin_t, gain, G, x.p, y.p, v.p, gain ? g.p : nullptr,
-                          pf.p, cap, file_off.p, k1work.p, k1work.cap, st));
-    RPT_HIP(hipMemcpyAsync(hfo, file_off.p, sizeof(int64_t) * (n_files + 1),
-                           hipMemcpyDeviceToHost, st));
-    uint32_t* flag_d =
-        reinterpret_cast<uint32_t*>(k1work.p + (n_files * p.rows / 64) + n_files + 1) + 2;
-    RPT_HIP(hipMemcpyAsync(hfo + n_files + 1, flag_d, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                           st));
-    RPT_HIP(hipStreamSynchronize(st));
-    uint32_t flags = 0;
-    std::memcpy(&flags, hfo + n_files + 1, sizeof(uint32_t));
-    done = flags == 0 && hfo[n_files] <= cap;
-  }
-  if (!done) {
-    RPT_TRY(row_prefix.ensure((size_t)n_files * p.rows + 1, st));
-    RPT_TRY(polar_count(echo, p.echo_dtype, n_files, p.rows, p.bins, p.threshold, p.stride,
-                        row_prefix.p, file_off.p, nullptr, st));
-    RPT_HIP(hipMemcpyAsync(hfo, file_off.p, sizeof(int64_t) * (n_files + 1),
-                           hipMemcpyDeviceToHost, st));
-    RPT_HIP(hipStreamSynchronize(st));
-  }
+  RPT_TRY(row_prefix.ensure((size_t)n_files * p.rows + 1, st));
+  RPT_TRY(polar_count(echo, p.echo_dtype, n_files, p.rows, p.bins, p.threshold, p.stride,
+                      row_prefix.p, file_off.p, nullptr, st));
+  RPT_HIP(hipMemcpyAsync(hfo, file_off.p, sizeof(int64_t) * (n_files + 1), hipMemcpyDeviceToHost,
+                         st));
+  RPT_HIP(hipStreamSynchronize(st));
   const int64_t N = hfo[n_files];
   fo_k1.resize((size_t)F + 1);
   for (int32_t f = 0; f <= F; ++f) fo_k1[(size_t)f] = hfo[(size_t)f * G];
@@ -261,17 +217,14 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
   for (int32_t f = 0; f < F; ++f) n_built += (fo_k1[(size_t)f + 1] > fo_k1[(size_t)f]) ? 1 : 0;
   r.n_built = n_built;
   const size_t cap = (size_t)std::max<int64_t>(N, 1);
-  if (!done) {
-    RPT_TRY(x.ensure(cap, st));
-    RPT_TRY(y.ensure(cap, st));
-    RPT_TRY(v.ensure(cap, st));
-    RPT_TRY(g.ensure(cap, st));
-    RPT_TRY(pf.ensure(cap, st));
-    RPT_TRY(polar_write(echo, p.echo_dtype, n_files, p.rows, p.bins, scale, cos_t, sin_t, gain,
-                        p.threshold, p.stride, row_prefix.p, file_off.p, G, x.p, y.p, v.p,
-                        gain ? g.p : nullptr, pf.p, st));
-  }
-  k1_cap = std::max<int64_t>(k1_cap, N + N / 4 + 65536);
+  RPT_TRY(x.ensure(cap, st));
+  RPT_TRY(y.ensure(cap, st));
+  RPT_TRY(v.ensure(cap, st));
+  RPT_TRY(g.ensure(cap, st));
+  RPT_TRY(pf.ensure(cap, st));
+  RPT_TRY(polar_write(echo, p.echo_dtype, n_files, p.rows, p.bins, scale, cos_t, sin_t, gain,
+                      p.threshold, p.stride, row_prefix.p, file_off.p, G, x.p, y.p, v.p,
+                      gain ? g.p : nullptr, pf.p, st));
   if (timing) RPT_HIP(hipEventRecord(ev[1], st));
 
   // ---- land filter (global grid over the stack, :954 gate: more than 10 built frames)

@@ -318,7 +318,7 @@ def _oracle_stack(echo, cfg, geo):
 
 
 @pytest.mark.parametrize("n_frames,land", [(6, True), (14, True), (14, False)])
-def test_stack_path_matches_oracle(gpu, n_frames, land, monkeypatch):
+def test_stack_path_matches_oracle(gpu, n_frames, land):
     """echo in HBM -> K1 -> land -> ST-DBSCAN -> K9 -> order -> C++ tracker, against the oracle
     run of the same stages (oracle.run_path)."""
     from rpt.pipeline import FrameStackPipeline, PathParams
@@ -332,9 +332,8 @@ def test_stack_path_matches_oracle(gpu, n_frames, land, monkeypatch):
                       n_frames * len(cfg.gains))
     frames = _oracle_stack(echo_d.cpu().numpy(), cfg, ds.geo)
     o_frames, o_labels, o_clusters, o_trk = op.run_path(frames, land=land)
-    # run 1 sizes the buffers (two-pass K1); run 2 takes the opt-in single-pass K1 (u8, 1024 bins)
-    for one_pass in ("0", "1"):
-        monkeypatch.setenv("RPT_K1_ONE_PASS", one_pass)
+    # twice: the second run reuses the driver's buffers
+    for _ in range(2):
         res = pipe.run(echo_d, keep_points=True)
         _check_stack_vs_oracle(res, n_frames, frames, o_frames, o_labels, o_clusters, o_trk)
 
@@ -358,29 +357,31 @@ def _check_stack_vs_oracle(res, n_frames, frames, o_frames, o_labels, o_clusters
         assert x.frames_seen == y.frames_seen
 
 
-def test_single_pass_k1_matches_two_pass(gpu, monkeypatch):
-    """Bench-size stack (12 frames x 3 gains x 4096 x 1024 u8): the first run of a pipeline uses
-    the two-pass K1 (count, write), the second the opt-in single-pass K1 (decoupled look-back);
-    points, labels and segments must be bit-identical."""
-    from rpt.pipeline import FrameStackPipeline, PathParams
-    from rpt.synth import DeviceSynth, SynthConfig
-
-    cfg = SynthConfig(n_frames=12)
-    ds = DeviceSynth(cfg, gpu)
-    echo = ds.echo()
-    pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), gpu)
-    pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
-                      cfg.n_frames * 3)
-    monkeypatch.setenv("RPT_K1_ONE_PASS", "0")
-    a = pipe.run(echo, keep_points=True)
-    monkeypatch.setenv("RPT_K1_ONE_PASS", "1")
-    b = pipe.run(echo, keep_points=True)
-    assert a.n_points == b.n_points and a.n_clustered_input == b.n_clustered_input
-    for k in a.points:
-        assert torch.equal(a.points[k], b.points[k]), k
-    assert torch.equal(a.labels, b.labels)
-    for k in a.seg:
-        np.testing.assert_array_equal(a.seg[k], b.seg[k])
+def test_k1_grouped_u8_matches_generic_rows(gpu):
+    """The grouped u8 kernels (1024 bins: keep bits by SWAR + dot4 mask, group prefix) against the
+    generic per-row kernels on the same samples (a 2048-bin sweep runs the generic u8 path, and
+    its two 1024-bin halves as separate sweeps the grouped one) at thresholds on both sides of 127,
+    with short last groups (rows % 4 != 0) and strides 1, 3, 4."""
+    rng = np.random.default_rng(5)
+    for rows in (4093, 8):
+        wide = rng.integers(0, 256, (2, rows, 2048)).astype(np.uint8)
+        scale = [np.full(rows, 30.0, np.float32)] * 2
+        angle = [np.linspace(0, 359, rows).astype(np.float32)] * 2
+        for thr in (-3.0, 10.0, 127.5, 128.0, 200.0, 254.9, 255.0):
+            for stride in (1, 3, 4):
+                a = _k1(gpu, wide, scale, angle, threshold=thr, stride=stride)
+                # same samples as 1024-bin sweeps: per-row keep order is bins 0..2047 of a row
+                # in the wide layout vs two rows here, so compare kept (value) streams and counts
+                narrow = wide.reshape(2, rows * 2, 1024)
+                b = _k1(gpu, narrow, [np.repeat(sc, 2) for sc in scale],
+                        [np.repeat(an, 2) for an in angle], threshold=thr, stride=stride)
+                np.testing.assert_array_equal(a[2], b[2])  # intensities, in rank order
+                np.testing.assert_array_equal(a[5], b[5])  # file offsets
+                ref = _k1(gpu, narrow.astype(np.float32), [np.repeat(sc, 2) for sc in scale],
+                          [np.repeat(an, 2) for an in angle], threshold=thr, stride=stride,
+                          f32=True)
+                for i in range(5):
+                    np.testing.assert_array_equal(b[i], ref[i])
 
 
 def test_full_size_partition_is_order_invariant(gpu):
