@@ -152,7 +152,8 @@ constexpr int kLbEpochShift = 46;
 
 template <int B>
 __device__ __forceinline__ int64_t block_excl_scan_b(int64_t v, int64_t* total) {
-  __shared__ int64_t wsum[B / kWave];
+  constexpr int NW = B / kWave;
+  __shared__ int64_t wsum[NW];
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = threadIdx.x / kWave;
   int64_t incl = v;
@@ -163,21 +164,99 @@ __device__ __forceinline__ int64_t block_excl_scan_b(int64_t v, int64_t* total) 
   }
   if (lane == kWave - 1) wsum[wid] = incl;
   __syncthreads();
-  int64_t wprefix = 0, tot = 0;
+  // every wave scans the NW wave totals in its first lanes
+  int64_t w = lane < NW ? wsum[lane] : 0;
 #pragma unroll
-  for (int w = 0; w < B / kWave; ++w) {
-    int64_t s = wsum[w];
-    if (w < wid) wprefix += s;
-    tot += s;
+  for (int off = 1; off < NW; off <<= 1) {
+    int64_t o = __shfl_up(w, off, kWave);
+    if (lane >= off) w += o;
   }
-  *total = tot;
+  *total = __shfl(w, NW - 1, kWave);
+  const int64_t wprefix = wid ? __shfl(w, wid > 0 ? wid - 1 : 0, kWave) : 0;
   return wprefix + incl - v;
 }
 
+// 16 consecutive items of a thread, in registers, in their input type (16 or 32 VGPRs: full
+// occupancy, so a whole 8M-item scan is resident in one round).  VEC: 16-B vector accesses (the
+// thread's items are 64 B of int32 or 128 B of int64, so a wave's k-th vector access covers every
+// k-th 16-B piece of 4 / 8 KiB: the pieces of a line meet in L2 and HBM sees each line once) — no
+// LDS staging.
+template <class T, bool VEC>
+__device__ __forceinline__ void load16(const T* __restrict__ in, int64_t i0, int64_t n_in,
+                                       T (&v)[kLbItems]) {
+  if (VEC && i0 + kLbItems <= n_in) {
+    if constexpr (sizeof(T) == 4) {
+      const int4* p = reinterpret_cast<const int4*>(in + i0);
+#pragma unroll
+      for (int q = 0; q < kLbItems / 4; ++q) {
+        const int4 w = p[q];
+        v[4 * q] = w.x;
+        v[4 * q + 1] = w.y;
+        v[4 * q + 2] = w.z;
+        v[4 * q + 3] = w.w;
+      }
+    } else {
+      const longlong2* p = reinterpret_cast<const longlong2*>(in + i0);
+#pragma unroll
+      for (int q = 0; q < kLbItems / 2; ++q) {
+        const longlong2 w = p[q];
+        v[2 * q] = w.x;
+        v[2 * q + 1] = w.y;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kLbItems; ++k) v[k] = (i0 + k < n_in) ? in[i0 + k] : T(0);
+  }
+}
+
+// out[i0 + k] = run + sum of v[0..k), computed while storing
+template <class T, class U, bool VEC>
+__device__ __forceinline__ void store16(U* __restrict__ out, int64_t i0, int64_t n_out,
+                                        const T (&v)[kLbItems], int64_t run) {
+  if (VEC && i0 + kLbItems <= n_out) {
+    if constexpr (sizeof(U) == 4) {
+      int4* p = reinterpret_cast<int4*>(out + i0);
+#pragma unroll
+      for (int q = 0; q < kLbItems / 4; ++q) {
+        int4 w;
+        w.x = (int)run;
+        run += v[4 * q];
+        w.y = (int)run;
+        run += v[4 * q + 1];
+        w.z = (int)run;
+        run += v[4 * q + 2];
+        w.w = (int)run;
+        run += v[4 * q + 3];
+        p[q] = w;
+      }
+    } else {
+      longlong2* p = reinterpret_cast<longlong2*>(out + i0);
+#pragma unroll
+      for (int q = 0; q < kLbItems / 2; ++q) {
+        longlong2 w;
+        w.x = run;
+        run += v[2 * q];
+        w.y = run;
+        run += v[2 * q + 1];
+        p[q] = w;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kLbItems; ++k) {
+      if (i0 + k < n_out) out[i0 + k] = (U)run;
+      run += v[k];
+    }
+  }
+}
+
 // out[i] = sum of in[0..i) for i < n_out, with in[i] read as 0 for i >= n_in (n_out <= n_in + 1:
-// n_out = n_in + 1 writes the grand total at out[n_in]).  in == out is allowed.
-template <class T, class U, int B>
-__global__ __launch_bounds__(B) void k_scan_lb(const T* __restrict__ in, int64_t n_in,
+// n_out = n_in + 1 writes the grand total at out[n_in]).  in == out is allowed (a thread reads
+// its own 16 items before it writes them, and no other thread touches them).
+// (B = 1024: 8 waves per SIMD, i.e. two blocks per CU, 512 tiles = 8M items resident at once)
+template <class T, class U, int B, bool VEC>
+__global__ __launch_bounds__(B, B >= 1024 ? 8 : 2) void k_scan_lb(const T* __restrict__ in, int64_t n_in,
                                                U* __restrict__ out, int64_t n_out,
                                                uint64_t* __restrict__ status,
                                                unsigned long long* __restrict__ ticket,
@@ -194,24 +273,12 @@ __global__ __launch_bounds__(B) void k_scan_lb(const T* __restrict__ in, int64_t
   }
   __syncthreads();
   const int64_t tile = s_tile;
-  const int64_t t0 = tile * kTile;
-  // coalesced striped loads -> LDS -> 16 consecutive items per thread (padded rows: <= 2-way
-  // bank conflicts)
-  __shared__ int64_t s_x[kTile + kTile / kLbItems];
-  auto pad = [](int i) { return i + i / kLbItems; };
-#pragma unroll
-  for (int k = 0; k < kLbItems; ++k) {
-    const int li = k * B + threadIdx.x;
-    s_x[pad(li)] = (t0 + li < n_in) ? (int64_t)in[t0 + li] : 0;
-  }
-  __syncthreads();
-  int64_t v[kLbItems];
+  const int64_t i0 = tile * kTile + (int64_t)threadIdx.x * kLbItems;
+  T v[kLbItems];
+  load16<T, VEC>(in, i0, n_in, v);
   int64_t sum = 0;
 #pragma unroll
-  for (int k = 0; k < kLbItems; ++k) {
-    v[k] = s_x[pad(threadIdx.x * kLbItems + k)];
-    sum += v[k];
-  }
+  for (int k = 0; k < kLbItems; ++k) sum += (int64_t)v[k];
   int64_t tot;
   const int64_t excl = block_excl_scan_b<B>(sum, &tot);
   const uint64_t tag = epoch << kLbEpochShift;
@@ -253,19 +320,7 @@ __global__ __launch_bounds__(B) void k_scan_lb(const T* __restrict__ in, int64_t
     }
   }
   __syncthreads();
-  // exclusive values back through LDS, then coalesced striped stores
-  int64_t run = s_prefix + excl;
-#pragma unroll
-  for (int k = 0; k < kLbItems; ++k) {
-    s_x[pad(threadIdx.x * kLbItems + k)] = run;
-    run += v[k];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kLbItems; ++k) {
-    const int li = k * B + threadIdx.x;
-    if (t0 + li < n_out) out[t0 + li] = (U)s_x[pad(li)];
-  }
+  store16<T, U, VEC>(out, i0, n_out, v, s_prefix + excl);
 }
 
 size_t scan_tmp_elems(int64_t n) {
@@ -334,7 +389,10 @@ static int32_t scan_impl(const T* in, int64_t n_in, U* out, int64_t n_out, hipSt
     RPT_CHECK_LAUNCH();
     return RPT_OK;
   }
-  const bool big = n_out > (int64_t)kLbBig * kLbItems * 64;
+  // 1024-thread tiles for large aligned scans (fewer tickets); unaligned ones take the 256-thread
+  // kernel, whose scalar path fits its registers
+  const bool vec = (uintptr_t)in % 16 == 0 && (uintptr_t)out % 16 == 0;
+  const bool big = vec && n_out > (int64_t)kScanBlock * kLbItems * 16;
   const int64_t tile = (big ? kLbBig : kScanBlock) * (int64_t)kLbItems;
   const int64_t nt = (n_out + tile - 1) / tile;
   if (nt >= (int64_t(1) << 31)) {
@@ -345,13 +403,17 @@ static int32_t scan_impl(const T* in, int64_t n_in, U* out, int64_t n_out, hipSt
   uint32_t epoch = 0;
   RPT_TRY(scan_state(stream, nt, &s, &epoch));
   auto* ticket = reinterpret_cast<unsigned long long*>(s->status + s->cap);
+  const uint64_t ep = epoch;
+  const unsigned grid = (unsigned)nt;
   if (big)
-    hipLaunchKernelGGL((k_scan_lb<T, U, kLbBig>), dim3((unsigned)nt), dim3(kLbBig), 0, stream,
-                       in, n_in, out, n_out, s->status, ticket, (uint64_t)epoch, (uint32_t)nt);
+    hipLaunchKernelGGL((k_scan_lb<T, U, kLbBig, true>), dim3(grid), dim3(kLbBig), 0, stream, in,
+                       n_in, out, n_out, s->status, ticket, ep, (uint32_t)nt);
+  else if (vec)
+    hipLaunchKernelGGL((k_scan_lb<T, U, kScanBlock, true>), dim3(grid), dim3(kScanBlock), 0,
+                       stream, in, n_in, out, n_out, s->status, ticket, ep, (uint32_t)nt);
   else
-    hipLaunchKernelGGL((k_scan_lb<T, U, kScanBlock>), dim3((unsigned)nt), dim3(kScanBlock), 0,
-                       stream, in, n_in, out, n_out, s->status, ticket, (uint64_t)epoch,
-                       (uint32_t)nt);
+    hipLaunchKernelGGL((k_scan_lb<T, U, kScanBlock, false>), dim3(grid), dim3(kScanBlock), 0,
+                       stream, in, n_in, out, n_out, s->status, ticket, ep, (uint32_t)nt);
   RPT_CHECK_LAUNCH();
   return RPT_OK;
 }

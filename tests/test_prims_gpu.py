@@ -56,6 +56,23 @@ def test_exclusive_scan_matches_cumsum(gpu, n, dts):
         np.testing.assert_array_equal(got.astype(np.int64), _expect(a, True))
 
 
+@pytest.mark.parametrize("n", [5000, 300_001])
+def test_exclusive_scan_unaligned(gpu, n):
+    """Pointers off the 16-B grid take the scalar-access kernel."""
+    from rpt import _abi
+    from rpt._device import stream_handle
+
+    lib = _abi.load()
+    rng = np.random.default_rng(n)
+    a = rng.integers(0, 100, n).astype(np.int32)
+    t_in = torch.zeros(n + 1, dtype=torch.int32, device=gpu)
+    t_in[1:] = torch.from_numpy(a).to(gpu)
+    out = torch.zeros(n + 3, dtype=torch.int64, device=gpu)
+    _abi.check(lib.rpt_exclusive_scan(t_in[1:].data_ptr(), I32, n, out[1:].data_ptr(), I64, 1,
+                                      stream_handle(gpu)))
+    np.testing.assert_array_equal(out[1:n + 2].cpu().numpy(), _expect(a, True))
+
+
 def test_exclusive_scan_large_values_i64(gpu):
     """Running totals far beyond 32 bits (up to 2^45) survive the 46-bit status granules."""
     from rpt import _abi
