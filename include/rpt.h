@@ -73,7 +73,9 @@ int32_t rpt_exclusive_scan(const void* in, int32_t in_dtype, int64_t n, void* ou
  * cos_t/sin_t are the per-row float32 np.cos/np.sin values of the reference (input). */
 int32_t rpt_polar_count(const void* echo, int32_t echo_dtype, int64_t n_files, int32_t rows,
                         int32_t bins, float threshold, int32_t stride,
-                        int64_t* row_prefix /*dev [n_files*rows+1], kept before each row*/,
+                        int64_t* row_prefix /*dev [n_files*rows+1], work data for
+                                              rpt_polar_write: kept before each row, or before
+                                              each group of 4 rows for u8 sweeps of 1024 bins*/,
                         int64_t* file_offsets /*dev [n_files+1]*/,
                         int64_t* total_host /*host, may be NULL: then no sync*/, void* stream);
 int32_t rpt_polar_write(const void* echo, int32_t echo_dtype, int64_t n_files, int32_t rows,
