@@ -69,6 +69,9 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-stage hipEvent timing")
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="single GPU: stacks in flight at once (native handles on separate "
+                         "streams, FrameStackPipeline.submit)")
     ap.add_argument("--sync-host", action="store_true",
                     help="run each step's host stage (order + tracker) inline instead of "
                          "overlapping it with the next step's device work")
@@ -113,13 +116,16 @@ def main():
         run = lambda: pipe.run(echo, _abi.ECHO_U8, rank * F)  # noqa: E731
     else:
         pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), dev, timing=timing,
-                                  async_host=not args.sync_host)
+                                  async_host=not args.sync_host, lanes=args.lanes)
         pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
                           cfg.n_frames * len(cfg.gains))
-        run = lambda: pipe.run(echo)  # noqa: E731
+        run = lambda: pipe.submit(echo)  # noqa: E731
+
+    def resolve(r):
+        return r.result() if hasattr(r, "result") else r
 
     for _ in range(args.warmup):
-        run().finish()
+        resolve(run()).finish()
     torch.cuda.synchronize(dev)
     if dist:
         tdist.barrier()
@@ -132,8 +138,12 @@ def main():
     for _ in range(args.steps):
         res = run()
         results.append(res)
-        if timing:
-            k5_ms.append(res.stage_ms["dbscan_core"] if not dist else ops.last_core_ms())
+        if timing and dist:
+            k5_ms.append(ops.last_core_ms())
+    results = [resolve(r) for r in results]
+    if timing and not dist:
+        k5_ms = [r.stage_ms["dbscan_core"] for r in results]
+    res = results[-1]
     for r in results:  # host stages (order + tracker) of the last runs, in order
         r.finish()
     torch.cuda.synchronize(dev)
@@ -205,6 +215,7 @@ def main():
                        "frames_per_gpu": args.frames, "points_per_step": int(pts),
                        **summary,
                        "parallelism": f"frame-sharded x{world}" if dist else "single GPU",
+                       "stacks_in_flight": 1 if dist else args.lanes,
                        "host_stage": "inline" if args.sync_host else
                        "overlapped: step k's order+tracker runs on a host thread during step "
                        "k+1's device work; the timed region ends after the last one"},

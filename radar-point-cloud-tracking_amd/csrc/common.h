@@ -35,8 +35,11 @@ void clear_error();
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Waits for the work queued on st so far by polling an event (readback latency; prims.hip).
+int32_t wait_stream(hipStream_t st);
+
 // ---- scratch pool ------------------------------------------------------------------------
-// A per-device bump arena that grows on demand.  Calls reserve() once with their total
+// A bump arena per (device, stream) that grows on demand.  Calls reserve() once with their total
 // need (so no hipMalloc happens mid-call), then carve() 256-byte aligned slices.
 class Scratch {
  public:
@@ -53,7 +56,7 @@ class Scratch {
   size_t cap_ = 0;
   size_t off_ = 0;
 };
-Scratch& scratch();  // for the current device
+Scratch& scratch(hipStream_t st);  // for the current device and this stream
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // Byte budget helper: sum of aligned array sizes.

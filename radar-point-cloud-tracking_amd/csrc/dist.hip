@@ -58,7 +58,7 @@ int32_t select_roots(const int64_t* rep, int64_t base, int64_t lo, int64_t hi, i
     if (count_host) *count_host = 0;
     return RPT_OK;
   }
-  Scratch& sc = scratch();
+  Scratch& sc = scratch(st);
   Budget b;
   b.add<int32_t>(m + 1);
   b.add<int64_t>(m + 1);
@@ -73,7 +73,7 @@ int32_t select_roots(const int64_t* rep, int64_t base, int64_t lo, int64_t hi, i
                      base, lo, m, out);
   RPT_CHECK_LAUNCH();
   RPT_HIP(hipMemcpyAsync(count_host, pos + m, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-  RPT_HIP(hipStreamSynchronize(st));
+  RPT_TRY(wait_stream(st));
   return RPT_OK;
 }
 

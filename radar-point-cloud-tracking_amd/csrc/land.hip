@@ -280,7 +280,7 @@ int32_t bounds_xy(const float* x, const float* y, int64_t n, float* out4, hipStr
     return RPT_EEMPTY;
   }
   const int nb = grid_for(n, kBlock, 1024);
-  Scratch& sc = scratch();
+  Scratch& sc = scratch(st);
   Budget bud;
   bud.add<uint32_t>(4);
   bud.add<uint32_t>(4 * (int64_t)nb);
@@ -292,7 +292,7 @@ int32_t bounds_xy(const float* x, const float* y, int64_t n, float* out4, hipStr
   RPT_CHECK_LAUNCH();
   uint32_t h[4];
   RPT_HIP(hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, st));
-  RPT_HIP(hipStreamSynchronize(st));
+  RPT_TRY(wait_stream(st));
   for (int k = 0; k < 4; ++k) {
     const uint32_t u = h[k];
     const uint32_t v = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
@@ -330,7 +330,7 @@ int32_t land_grid(const float* x, const float* y, const float* val, int64_t n, c
 int32_t land_mask(const int32_t* cnt, const double* tot, int64_t cells, int64_t num_frames,
                   double pthr, double ithr, uint8_t* land, int64_t* n_land_host,
                   hipStream_t st) {
-  Scratch& sc = scratch();
+  Scratch& sc = scratch(st);
   RPT_TRY(sc.reserve(256, st));
   int32_t* d = sc.carve_n<int32_t>(1);
   RPT_HIP(hipMemsetAsync(d, 0, sizeof(int32_t), st));
@@ -343,7 +343,7 @@ int32_t land_mask(const int32_t* cnt, const double* tot, int64_t cells, int64_t 
   if (n_land_host) {
     int32_t h = 0;
     RPT_HIP(hipMemcpyAsync(&h, d, sizeof h, hipMemcpyDeviceToHost, st));
-    RPT_HIP(hipStreamSynchronize(st));
+    RPT_TRY(wait_stream(st));
     *n_land_host = h;
   }
   return RPT_OK;
@@ -354,7 +354,7 @@ int32_t land_filter(const float* x, const float* y, const float* v, const int32_
                     const double* xe, int32_t nxe, const double* ye, int32_t nye,
                     const uint8_t* land, float* xo, float* yo, float* vo, int32_t* go,
                     int32_t* pfo, int64_t* new_off, int64_t* n_kept_host, hipStream_t st) {
-  Scratch& sc = scratch();
+  Scratch& sc = scratch(st);
   Budget b;
   b.add<int32_t>(n + 1);
   b.add<int64_t>(n + 1);
@@ -379,7 +379,7 @@ int32_t land_filter(const float* x, const float* y, const float* v, const int32_
   }
   if (n_kept_host) {
     RPT_HIP(hipMemcpyAsync(n_kept_host, pos + n, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    RPT_HIP(hipStreamSynchronize(st));
+    RPT_TRY(wait_stream(st));
   }
   return RPT_OK;
 }

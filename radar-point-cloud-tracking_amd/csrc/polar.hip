@@ -445,7 +445,7 @@ int32_t count_impl(const T* echo, int64_t n_files, int rows, int bins, float thr
   const bool grouped = grouped_u8(echo, bins);
   const GroupMap gm{(uint32_t)((rows + kGroupRows - 1) / kGroupRows), rows};
   const int64_t n_units = grouped ? n_files * (int64_t)gm.gpf : n_rows;
-  Scratch& sc = scratch();
+  Scratch& sc = scratch(st);
   Budget b;
   b.add<int32_t>(n_units);
   b.add<int64_t>(n_files);
@@ -483,7 +483,7 @@ int32_t count_impl(const T* echo, int64_t n_files, int rows, int bins, float thr
   if (total_host) {
     RPT_HIP(hipMemcpyAsync(total_host, file_offsets + n_files, sizeof(int64_t),
                            hipMemcpyDeviceToHost, st));
-    RPT_HIP(hipStreamSynchronize(st));
+    RPT_TRY(wait_stream(st));
   }
   return RPT_OK;
 }

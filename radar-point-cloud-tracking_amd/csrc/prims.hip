@@ -2,7 +2,7 @@
 //  * exclusive scan — single pass with decoupled look-back (one launch, no memset),
 //  * stable LSD radix sort of (u32 key, u32 value) pairs, 8-bit digits, wave-granular
 //    histograms so that a pass needs no block-level barriers inside the scatter loop.
-// Plus the library's error plumbing and per-device scratch pool.
+// Plus the library's error plumbing and per-(device, stream) scratch pools.
 #include <algorithm>
 #include <cstdarg>
 #include <mutex>
@@ -24,6 +24,24 @@ void set_error(const char* fmt, ...) {
 }
 void clear_error() { g_last_error.clear(); }
 const char* last_error_cstr() { return g_last_error.c_str(); }
+
+// ------------------------------------------------------------------ readback wait
+// The path's size readbacks are tiny and the GPU idles until the host has launched the next
+// stage, so the wait polls an event instead of blocking in hipStreamSynchronize (whose wake-up
+// adds tens of microseconds per readback).  One cached event per (thread, device).
+int32_t wait_stream(hipStream_t st) {
+  static thread_local std::vector<hipEvent_t> evs;
+  int dev = 0;
+  RPT_HIP(hipGetDevice(&dev));
+  if ((int)evs.size() <= dev) evs.resize(dev + 1, nullptr);
+  if (!evs[dev]) RPT_HIP(hipEventCreateWithFlags(&evs[dev], hipEventDisableTiming));
+  RPT_HIP(hipEventRecord(evs[dev], st));
+  for (;;) {
+    const hipError_t e = hipEventQuery(evs[dev]);
+    if (e == hipSuccess) return RPT_OK;
+    if (e != hipErrorNotReady) RPT_HIP(e);
+  }
+}
 
 // ------------------------------------------------------------------ scratch pool
 int32_t Scratch::reserve(size_t bytes, hipStream_t stream) {
@@ -61,23 +79,26 @@ void Scratch::release() {
   cap_ = off_ = 0;
 }
 
+// One arena per (device, stream): work on different streams (concurrent stacks) never shares it.
 static std::mutex g_scratch_mu;
-static std::vector<Scratch*> g_scratch;
+static std::vector<std::pair<std::pair<int, hipStream_t>, Scratch*>> g_scratch;
 
-Scratch& scratch() {
+Scratch& scratch(hipStream_t st) {
   int dev = 0;
   (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(g_scratch_mu);
-  if ((int)g_scratch.size() <= dev) g_scratch.resize(dev + 1, nullptr);
-  if (!g_scratch[dev]) g_scratch[dev] = new Scratch();
-  return *g_scratch[dev];
+  for (auto& e : g_scratch)
+    if (e.first.first == dev && e.first.second == st) return *e.second;
+  g_scratch.push_back({{dev, st}, new Scratch()});
+  return *g_scratch.back().second;
 }
 
 void release_scratch_current() {
   int dev = 0;
   (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(g_scratch_mu);
-  if ((int)g_scratch.size() > dev && g_scratch[dev]) g_scratch[dev]->release();
+  for (auto& e : g_scratch)
+    if (e.first.first == dev) e.second->release();
 }
 
 // ------------------------------------------------------------------ exclusive scan

@@ -208,7 +208,7 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
                       row_prefix.p, file_off.p, nullptr, st));
   RPT_HIP(hipMemcpyAsync(hfo, file_off.p, sizeof(int64_t) * (n_files + 1), hipMemcpyDeviceToHost,
                          st));
-  RPT_HIP(hipStreamSynchronize(st));
+  RPT_TRY(wait_stream(st));
   const int64_t N = hfo[n_files];
   fo_k1.resize((size_t)F + 1);
   for (int32_t f = 0; f <= F; ++f) fo_k1[(size_t)f] = hfo[(size_t)f * G];
@@ -285,7 +285,7 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
     RPT_TRY(pack_d.ensure((size_t)pl.off[pl.k], st));
     RPT_TRY(pack_arrays(pl, pack_d.p, st));
     RPT_HIP(hipMemcpyAsync(hn, pack_d.p, sizeof(int64_t) * (F + 2), hipMemcpyDeviceToHost, st));
-    RPT_HIP(hipStreamSynchronize(st));
+    RPT_TRY(wait_stream(st));
     fo_in.assign(hn, hn + F + 1);
     n_in_ = hn[F];
     r.n_land_cells = hn[F + 1];
@@ -358,7 +358,7 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
     RPT_HIP(hipMemcpyAsync(h, pack_d.p, packed, hipMemcpyDeviceToHost, st));
   }
   if (timing) RPT_HIP(hipEventRecord(ev[4], st));
-  RPT_HIP(hipStreamSynchronize(st));
+  RPT_TRY(wait_stream(st));
   h_count.assign(hcount, hcount + S);
   h_first.assign(hfirst, hfirst + S);
   h_noise.assign(hnoise, hnoise + F);

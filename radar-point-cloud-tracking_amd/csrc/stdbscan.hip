@@ -1651,7 +1651,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   RPT_CHECK_LAUNCH();
   Bounds hb;
   RPT_HIP(hipMemcpyAsync(&hb, d_b, sizeof(Bounds), hipMemcpyDeviceToHost, st));
-  RPT_HIP(hipStreamSynchronize(st));
+  RPT_TRY(wait_stream(st));
   tm.mark();
   if (hb.nonfinite_xyz) {
     set_error("Input contains NaN or infinity in coordinates");
@@ -1915,7 +1915,7 @@ int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hi
   if (stats) {
     int32_t ncl = 0;
     RPT_HIP(hipMemcpyAsync(&ncl, cid + n, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    RPT_HIP(hipStreamSynchronize(st));
+    RPT_TRY(wait_stream(st));
     stats->n_points = n;
     stats->n_clusters = ncl;
     stats->n_core = -1;
@@ -1981,7 +1981,8 @@ static int32_t check_args(const float* x, const float* y, const float* z, int64_
 }
 
 static std::mutex g_state_mu;
-static std::vector<DbscanState*> g_states;  // per device, for the fused single-call path
+// per (device, stream), for the fused single-call path
+static std::vector<std::pair<std::pair<int, hipStream_t>, DbscanState*>> g_states;
 
 int32_t stdbscan(const float* x, const float* y, const float* z, int64_t stride, const float* t,
                  int64_t n, double eps_space, double eps_time, int32_t min_samples,
@@ -1996,9 +1997,13 @@ int32_t stdbscan(const float* x, const float* y, const float* z, int64_t stride,
   DbscanState* S;
   {
     std::lock_guard<std::mutex> lk(g_state_mu);
-    if ((int)g_states.size() <= dev) g_states.resize(dev + 1, nullptr);
-    if (!g_states[dev]) g_states[dev] = new DbscanState();
-    S = g_states[dev];
+    S = nullptr;
+    for (auto& e : g_states)
+      if (e.first.first == dev && e.first.second == st) S = e.second;
+    if (!S) {
+      S = new DbscanState();
+      g_states.push_back({{dev, st}, S});
+    }
   }
   RPT_TRY(S->build(x, y, z, stride, t, n, eps_space, eps_time, min_samples,
                    stats && stats->timing, st));

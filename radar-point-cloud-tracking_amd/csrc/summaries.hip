@@ -307,7 +307,7 @@ int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
     set_error("rpt_cluster_summaries: n exceeds the int32 index space");
     return RPT_ENOTSUP;
   }
-  Scratch& sc = scratch();
+  Scratch& sc = scratch(st);
   Budget b;
   for (int k = 0; k < 4; ++k) b.add<uint32_t>(n + 1);
   b.add<int64_t>(radix_tmp_elems(n));
@@ -349,7 +349,7 @@ int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
   RPT_CHECK_LAUNCH();
   int64_t n_seg = 0;
   RPT_HIP(hipMemcpyAsync(&n_seg, pos + n, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-  RPT_HIP(hipStreamSynchronize(st));
+  RPT_TRY(wait_stream(st));
   if (n_seg > 0) {
     hipLaunchKernelGGL(k_gather_runs, dim3(g), dim3(kBlock), 0, st, sv, n, x, y, inten, gx, gy,
                        gi);

@@ -78,11 +78,16 @@ class FrameStackPipeline:
 
     def __init__(self, gains: Sequence[int], rows: int, bins: int, params: PathParams = None,
                  device=None, timing: bool = False, async_host: bool = False,
-                 host_workers: int = 2):
+                 host_workers: int = 2, lanes: int = 1):
         """async_host: the host stage (cluster order + tracker, sequential C++) of a run executes
         on a pool of host_workers threads while the caller goes on to the next runs' device
         work (runs are independent, so their host stages may overlap each other);
-        StackResult.finish() waits for a run's host stage."""
+        StackResult.finish() waits for a run's host stage.
+
+        lanes > 1: submit() runs successive stacks on `lanes` native handles, each on its own
+        HIP stream and submission thread, so one stack's kernels fill the GPU while another
+        waits on a size readback or runs a latency-bound stage (the library keeps its scratch
+        and look-back state per stream)."""
         self.dev = require_gpu(device)
         self.gains = [int(g) for g in gains]
         if sorted(self.gains) != self.gains:
@@ -90,7 +95,14 @@ class FrameStackPipeline:
         self.rows, self.bins = rows, bins
         self.p = params or PathParams()
         self.lib = _abi.load()
-        self._h = self.lib.rpt_stack_create()
+        if lanes < 1:
+            raise ValueError("lanes must be >= 1")
+        self._hs = [self.lib.rpt_stack_create() for _ in range(lanes)]
+        self._h = self._hs[0]
+        self._streams = [torch.cuda.Stream(self.dev) for _ in range(lanes)] if lanes > 1 else None
+        self._lane_pool = [ThreadPoolExecutor(max_workers=1) for _ in range(lanes)] \
+            if lanes > 1 else None
+        self._next_lane = 0
         self.timing = timing
         self._host = ThreadPoolExecutor(max_workers=host_workers) if async_host else None
         self._geo_key = None
@@ -126,6 +138,23 @@ class FrameStackPipeline:
     def run(self, echo: torch.Tensor, keep_points: bool = False) -> StackResult:
         """K1 -> land filter -> ST-DBSCAN -> K9 in one native call (rpt_stack_run), then the
         host stage (cluster order + tracker) inline or on the worker pool (async_host)."""
+        return self._run_lane(self._h, stream_handle(self.dev), echo, keep_points)
+
+    def submit(self, echo: torch.Tensor, keep_points: bool = False) -> Future:
+        """Queues a run on the next lane and returns a Future of its StackResult (lanes == 1:
+        runs inline).  The echo must stay unchanged until the future is done."""
+        if self._lane_pool is None:
+            f = Future()
+            f.set_result(self.run(echo, keep_points))
+            return f
+        lane = self._next_lane
+        self._next_lane = (lane + 1) % len(self._hs)
+        s = self._streams[lane]
+        s.wait_stream(torch.cuda.current_stream(self.dev))  # the echo's producer
+        return self._lane_pool[lane].submit(self._run_lane, self._hs[lane], s.cuda_stream, echo,
+                                            keep_points)
+
+    def _run_lane(self, h, stream: int, echo: torch.Tensor, keep_points: bool) -> StackResult:
         p, lib = self.p, self.lib
         G = len(self.gains)
         F = echo.shape[0]
@@ -138,12 +167,12 @@ class FrameStackPipeline:
                               1 if self.timing else 0)
         r = _abi.StackResult()
         scale_d, cos_d, sin_d = self.geo
-        _abi.check(lib.rpt_stack_run(self._h, _abi.C.byref(sp), echo.data_ptr(),
+        _abi.check(lib.rpt_stack_run(h, _abi.C.byref(sp), echo.data_ptr(),
                                      scale_d.data_ptr(), cos_d.data_ptr(), sin_d.data_ptr(),
-                                     self.gain_d.data_ptr(), _abi.C.byref(r),
-                                     stream_handle(self.dev)), "rpt_stack_run")
+                                     self.gain_d.data_ptr(), _abi.C.byref(r), stream),
+                   "rpt_stack_run")
         fo = np.empty(F + 1, np.int64)
-        _abi.check(lib.rpt_stack_frame_offsets(self._h, 0, fo.ctypes.data_as(_abi.c_i64p)))
+        _abi.check(lib.rpt_stack_frame_offsets(h, 0, fo.ctypes.data_as(_abi.c_i64p)))
         built = np.nonzero(np.diff(fo) > 0)[0]   # build_frame returns None if empty
         S = int(r.n_segments)
         seg = {"frame": np.empty(S, np.int32), "label": np.empty(S, np.int32),
@@ -153,7 +182,7 @@ class FrameStackPipeline:
         first_noise = np.empty(F, np.int64)
         ptr = lambda a, t: a.ctypes.data_as(t)  # noqa: E731
         _abi.check(lib.rpt_stack_segments(
-            self._h, ptr(seg["frame"], _abi.c_i32p), ptr(seg["label"], _abi.c_i32p),
+            h, ptr(seg["frame"], _abi.c_i32p), ptr(seg["label"], _abi.c_i32p),
             ptr(seg["count"], _abi.c_i64p), ptr(seg["first"], _abi.c_i64p),
             ptr(seg["cx"], _abi.c_f32p), ptr(seg["cy"], _abi.c_f32p), ptr(seg["mi"], _abi.c_f32p),
             ptr(first_noise, _abi.c_i64p)))
@@ -189,15 +218,21 @@ class FrameStackPipeline:
                    (("x", torch.float32), ("y", torch.float32), ("v", torch.float32),
                     ("gain", torch.int32), ("frame", torch.int32))}
             labels = torch.empty(n, dtype=torch.int32, device=self.dev)
-            _abi.check(lib.rpt_stack_points(self._h, pts["x"].data_ptr(), pts["y"].data_ptr(),
+            if stream != stream_handle(self.dev):  # allocations above are on torch's stream
+                torch.cuda.current_stream(self.dev).synchronize()
+            _abi.check(lib.rpt_stack_points(h, pts["x"].data_ptr(), pts["y"].data_ptr(),
                                             pts["v"].data_ptr(), pts["gain"].data_ptr(),
-                                            pts["frame"].data_ptr(), labels.data_ptr(),
-                                            stream_handle(self.dev)), "rpt_stack_points")
+                                            pts["frame"].data_ptr(), labels.data_ptr(), stream),
+                       "rpt_stack_points")
+            if stream != stream_handle(self.dev):  # the caller reads them on torch's stream
+                torch.cuda.ExternalStream(stream, device=self.dev).synchronize()
             res.labels, res.points = labels, pts
         return res
 
     def __del__(self):
-        h = getattr(self, "_h", None)
-        if h:
-            self.lib.rpt_stack_destroy(h)
-            self._h = None
+        for pool in getattr(self, "_lane_pool", None) or []:
+            pool.shutdown(wait=True)
+        for h in getattr(self, "_hs", None) or []:
+            if h:
+                self.lib.rpt_stack_destroy(h)
+        self._hs, self._h = [], None

@@ -384,6 +384,37 @@ def test_k1_grouped_u8_matches_generic_rows(gpu):
                     np.testing.assert_array_equal(b[i], ref[i])
 
 
+def test_concurrent_lanes_match_single_lane(gpu):
+    """Two lanes (two native handles on two streams, submitted from two threads, the library's
+    scratch and scan state per stream) give the same results as one lane, run after run: four
+    stacks of different content alternate between the lanes."""
+    from rpt.pipeline import FrameStackPipeline, PathParams
+    from rpt.synth import DeviceSynth, SynthConfig
+
+    stacks = []
+    for k in range(4):
+        cfg = SynthConfig(n_frames=14, rows=1024, frame0=100 * k)
+        ds = DeviceSynth(cfg, gpu)
+        stacks.append(ds.echo())
+    torch.cuda.synchronize(gpu)
+    one = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), gpu)
+    two = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), gpu, lanes=2,
+                             async_host=True)
+    for p in (one, two):
+        p.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
+                       cfg.n_frames * 3)
+    ref = [one.run(e, keep_points=True) for e in stacks]
+    futs = [two.submit(e, keep_points=True) for e in stacks]
+    got = [f.result().finish() for f in futs]
+    for a, b in zip(ref, got):
+        assert a.n_points == b.n_points and a.n_clusters == b.n_clusters
+        assert torch.equal(a.labels, b.labels)
+        for k in a.seg:
+            np.testing.assert_array_equal(a.seg[k], b.seg[k])
+        oa, ob = a.tracker.objects(), b.tracker.objects()
+        assert [o.object_id for o in oa] == [o.object_id for o in ob]
+
+
 def test_full_size_partition_is_order_invariant(gpu):
     """Bench-size frames (4096x1024, 3 gains): the ST-DBSCAN partition must not depend on point
     order (size-independent property; labels renumber by first core index)."""
