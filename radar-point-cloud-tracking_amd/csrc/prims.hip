@@ -486,71 +486,100 @@ int32_t pack_arrays(const PackList& l, uint32_t* dst, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------ radix sort
+// Stable LSD radix sort with digits of up to 12 bits, so the ST-DBSCAN cell keys (≤ 24 bits)
+// take two passes and the K9 label keys (≤ 12 bits) one.  A block owns a tile of 4 waves x 1024
+// items (16 rows of 64 per wave).  Per pass: (1) per-tile digit counts (LDS atomics) written
+// digit-major as int32, (2) one exclusive scan over them = each tile's first output slot per
+// digit, (3) the scatter: the tile's items are re-counted per wave in LDS to give each wave its
+// start per digit (waves in order), then each wave ranks its rows of 64 items by ballots over the
+// digit bits and writes them.  Order inside a tile is wave, row, lane: stable.
 constexpr int kSortBlock = 256;
 constexpr int kSortRows = 16;                  // items per lane
 constexpr int kSortWaveItems = kWave * kSortRows;  // 1024 items per wave
 constexpr int kSortWavesPerBlock = kSortBlock / kWave;
+constexpr int kSortTile = kSortWaveItems * kSortWavesPerBlock;  // 4096 items per block
+constexpr int kSortMaxBits = 12;
 
-// hist[d * n_waves + w] = number of items of wave-chunk w whose digit is d.
+// hist[d * n_tiles + tile] = number of items of the tile whose digit is d.
+template <int R>
 __global__ __launch_bounds__(kSortBlock) void k_radix_hist(const uint32_t* __restrict__ keys,
-                                                          int64_t n, int shift, int64_t n_waves,
-                                                          int64_t* __restrict__ hist) {
-  __shared__ int cnt[kSortWavesPerBlock][256];
-  const int lane = threadIdx.x & (kWave - 1);
+                                                          int64_t n, int shift, int64_t n_tiles,
+                                                          int32_t* __restrict__ hist) {
+  constexpr int D = 1 << R;
+  __shared__ int cnt[kSortWavesPerBlock][D];  // one sub-histogram per wave: 4x less contention
   const int wl = threadIdx.x / kWave;
-  for (int d = lane; d < 256; d += kWave) cnt[wl][d] = 0;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  const int64_t w = (int64_t)blockIdx.x * kSortWavesPerBlock + wl;
-  if (w < n_waves) {
-    const int64_t base = w * kSortWaveItems;
+  for (int d = threadIdx.x; d < D * kSortWavesPerBlock; d += kSortBlock) (&cnt[0][0])[d] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
 #pragma unroll 4
-    for (int r = 0; r < kSortRows; ++r) {
-      int64_t i = base + (int64_t)r * kWave + lane;
-      if (i < n) atomicAdd(&cnt[wl][(keys[i] >> shift) & 255u], 1);
-    }
+  for (int r = 0; r < kSortTile / kSortBlock; ++r) {
+    const int64_t i = base + (int64_t)r * kSortBlock + threadIdx.x;
+    if (i < n) atomicAdd(&cnt[wl][(keys[i] >> shift) & (uint32_t)(D - 1)], 1);
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  if (w < n_waves)
-    for (int d = lane; d < 256; d += kWave) hist[(int64_t)d * n_waves + w] = cnt[wl][d];
+  __syncthreads();
+  for (int d = threadIdx.x; d < D; d += kSortBlock) {
+    int c = 0;
+#pragma unroll
+    for (int w = 0; w < kSortWavesPerBlock; ++w) c += cnt[w][d];
+    hist[(int64_t)d * n_tiles + blockIdx.x] = c;
+  }
 }
 
+template <int R>
 __global__ __launch_bounds__(kSortBlock) void k_radix_scatter(
     const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, int64_t n, int shift,
-    int64_t n_waves, const int64_t* __restrict__ offs, uint32_t* __restrict__ keys_out,
+    int64_t n_tiles, const int32_t* __restrict__ offs, uint32_t* __restrict__ keys_out,
     uint32_t* __restrict__ vals_out) {
-  __shared__ int64_t run[kSortWavesPerBlock][256];
+  constexpr int D = 1 << R;
+  __shared__ int32_t run[kSortWavesPerBlock][D];
   const int lane = threadIdx.x & (kWave - 1);
   const int wl = threadIdx.x / kWave;
-  const int64_t w = (int64_t)blockIdx.x * kSortWavesPerBlock + wl;
-  if (w >= n_waves) return;  // whole wave exits together
-  for (int d = lane; d < 256; d += kWave) run[wl][d] = offs[(int64_t)d * n_waves + w];
+  for (int d = lane; d < D; d += kWave) run[wl][d] = 0;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  const int64_t base = w * kSortWaveItems;
+  const int64_t base = (int64_t)blockIdx.x * kSortTile + (int64_t)wl * kSortWaveItems;
+  uint32_t k[kSortRows], v[kSortRows];
+#pragma unroll
+  for (int r = 0; r < kSortRows; ++r) {
+    const int64_t i = base + (int64_t)r * kWave + lane;
+    k[r] = i < n ? keys[i] : 0u;
+    v[r] = i < n ? vals[i] : 0u;
+  }
+#pragma unroll
+  for (int r = 0; r < kSortRows; ++r) {
+    const int64_t i = base + (int64_t)r * kWave + lane;
+    if (i < n) atomicAdd(&run[wl][(k[r] >> shift) & (uint32_t)(D - 1)], 1);
+  }
+  __syncthreads();
+  // counts -> each wave's first slot per digit: the tile's slot plus the earlier waves' counts
+  for (int d = threadIdx.x; d < D; d += kSortBlock) {
+    int32_t pos = offs[(int64_t)d * n_tiles + blockIdx.x];
+#pragma unroll
+    for (int w = 0; w < kSortWavesPerBlock; ++w) {
+      const int32_t c = run[w][d];
+      run[w][d] = pos;
+      pos += c;
+    }
+  }
+  __syncthreads();
+#pragma unroll 1
   for (int r = 0; r < kSortRows; ++r) {
     const int64_t i = base + (int64_t)r * kWave + lane;
     const bool valid = i < n;
-    uint32_t k = 0, v = 0;
-    if (valid) {
-      k = keys[i];
-      v = vals[i];
-    }
-    const uint32_t d = (k >> shift) & 255u;
+    const uint32_t d = (k[r] >> shift) & (uint32_t)(D - 1);
     uint64_t mask = __ballot(valid);
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < R; ++b) {
       const bool bit = (d >> b) & 1u;
       const uint64_t bb = __ballot(valid && bit);
       mask &= bit ? bb : ~bb;
     }
     const int rank = rank_in_mask(mask);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int64_t pos = run[wl][d] + rank;
+    const int32_t pos = run[wl][d] + rank;
     if (valid) {
-      keys_out[pos] = k;
-      vals_out[pos] = v;
+      keys_out[pos] = k[r];
+      vals_out[pos] = v[r];
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -561,9 +590,24 @@ __global__ __launch_bounds__(kSortBlock) void k_radix_scatter(
 }
 
 size_t radix_tmp_elems(int64_t n) {
-  const int64_t n_waves = (n + kSortWaveItems - 1) / kSortWaveItems;
-  const int64_t h = 256 * n_waves;
-  return (size_t)h + 64 + scan_tmp_elems(h);
+  const int64_t n_tiles = (n + kSortTile - 1) / kSortTile;
+  const int64_t h = ((int64_t)1 << kSortMaxBits) * n_tiles;  // int32 entries
+  return (size_t)(h + 1) / 2 + 64;
+}
+
+template <int R>
+static int32_t radix_pass(const uint32_t* ks, const uint32_t* vs, uint32_t* kd, uint32_t* vd,
+                          int64_t n, int shift, int32_t* hist, hipStream_t st) {
+  const int64_t n_tiles = (n + kSortTile - 1) / kSortTile;
+  const int64_t h = ((int64_t)1 << R) * n_tiles;
+  hipLaunchKernelGGL(k_radix_hist<R>, dim3((unsigned)n_tiles), dim3(kSortBlock), 0, st, ks, n,
+                     shift, n_tiles, hist);
+  RPT_CHECK_LAUNCH();
+  RPT_TRY(exclusive_scan_i32(hist, hist, h, nullptr, st));
+  hipLaunchKernelGGL(k_radix_scatter<R>, dim3((unsigned)n_tiles), dim3(kSortBlock), 0, st, ks, vs,
+                     n, shift, n_tiles, (const int32_t*)hist, kd, vd);
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
 }
 
 int32_t radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt,
@@ -572,20 +616,28 @@ int32_t radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uin
   *out_keys = keys;
   *out_vals = vals;
   if (n <= 1 || bits <= 0) return RPT_OK;
-  const int64_t n_waves = (n + kSortWaveItems - 1) / kSortWaveItems;
-  const int64_t h = 256 * n_waves;
-  int64_t* hist = tmp;
-  int64_t* scan_tmp = tmp + h + 64;
-  const unsigned blocks = (unsigned)((n_waves + kSortWavesPerBlock - 1) / kSortWavesPerBlock);
+  if (n >= (int64_t(1) << 31) || bits > 32) {
+    set_error("radix sort: n must be < 2^31 and bits <= 32");
+    return RPT_ENOTSUP;
+  }
+  // one pass up to kSortMaxBits bits (K9 label keys); wider keys (grid cells) in 8-bit digits,
+  // where the ballot ranking and the digit-major histogram stay cheapest per bit (measured:
+  // 2 x 11-12 bits cost more than 3 x 8 for the 22-bit cell keys)
+  const int passes = bits <= kSortMaxBits ? 1 : (bits + 7) / 8;
+  const int r0 = (bits + passes - 1) / passes;
+  int32_t* hist = reinterpret_cast<int32_t*>(tmp);
   uint32_t *ks = keys, *vs = vals, *kd = keys_alt, *vd = vals_alt;
-  for (int shift = 0; shift < bits; shift += 8) {
-    hipLaunchKernelGGL(k_radix_hist, dim3(blocks), dim3(kSortBlock), 0, st, ks, n, shift,
-                       n_waves, hist);
-    RPT_CHECK_LAUNCH();
-    RPT_TRY(exclusive_scan_i64(hist, hist, h, scan_tmp, st));
-    hipLaunchKernelGGL(k_radix_scatter, dim3(blocks), dim3(kSortBlock), 0, st, ks, vs, n, shift,
-                       n_waves, (const int64_t*)hist, kd, vd);
-    RPT_CHECK_LAUNCH();
+  for (int p = 0, shift = 0; p < passes; ++p) {
+    const int r = std::min(r0, bits - shift);
+    int32_t s = RPT_OK;
+    switch (r) {
+      case 1: case 2: case 3: case 4: case 5: case 6: s = radix_pass<6>(ks, vs, kd, vd, n, shift, hist, st); break;
+      case 7: case 8: s = radix_pass<8>(ks, vs, kd, vd, n, shift, hist, st); break;
+      case 9: case 10: s = radix_pass<10>(ks, vs, kd, vd, n, shift, hist, st); break;
+      default: s = radix_pass<12>(ks, vs, kd, vd, n, shift, hist, st); break;
+    }
+    if (s != RPT_OK) return s;
+    shift += r;
     std::swap(ks, kd);
     std::swap(vs, vd);
   }
