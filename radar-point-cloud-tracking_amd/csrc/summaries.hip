@@ -132,31 +132,22 @@ __global__ void k_gather_runs(const uint32_t* __restrict__ sv, int64_t n,
 // flight meanwhile) and the wave-uniform chain consumes broadcast 16-byte LDS reads issued a batch
 // ahead.  The dependent v_add_f32 (~4.4 cycles on gfx950, tools/microbench/chain.hip) is the
 // floor; a packed x/y add is no faster (8.5 cycles), so x and y run on separate waves.
-// With gi != nullptr the same chunks also load the intensities (prefetched with the coordinate),
-// accumulated per lane into isum / small_int for the mean-intensity fast path.
 __device__ __forceinline__ float seq_sum(const float* __restrict__ g, int b, int e, int lane,
-                                         float* __restrict__ sb, const float* __restrict__ gi,
-                                         int64_t& isum, bool& small_int) {
+                                         float* __restrict__ sb) {
   constexpr int kPre = 16, kChunk = 64 * kPre, V = 8;
-  float pre[kPre], pin[kPre];
+  float pre[kPre];
   auto load_chunk = [&](int c0) {
 #pragma unroll
     for (int t = 0; t < kPre; ++t) {
       const int idx = c0 + t * 64 + lane;
       pre[t] = (idx < e) ? g[idx] : 0.f;
-      pin[t] = (gi && idx < e) ? gi[idx] : 0.f;
     }
   };
   float acc = 0.f;
   load_chunk(b);
   for (int c0 = b; c0 < e; c0 += kChunk) {
 #pragma unroll
-    for (int t = 0; t < kPre; ++t) {
-      sb[t * 64 + lane] = pre[t];
-      const float vi = pin[t];
-      small_int = small_int && (vi >= 0.f && vi == floorf(vi) && vi < 16777216.f);
-      isum += (int64_t)vi;
-    }
+    for (int t = 0; t < kPre; ++t) sb[t * 64 + lane] = pre[t];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -168,7 +159,34 @@ __device__ __forceinline__ float seq_sum(const float* __restrict__ g, int b, int
       for (i = 1; i < 4 && i < m; ++i) acc = acc + sb[i];
     }
     const float4* sb4 = reinterpret_cast<const float4*>(sb);
-    if (i + 8 * V <= m) {
+    if (i == 0 && m == kChunk) {
+      // a whole chunk (the bulk of a long run): fully unrolled, three rotating batches of 16
+      // elements, each batch's LDS reads issued two batches ahead of its adds (at most 12 reads
+      // in flight, counted waits only)
+      constexpr int kB = 4, kNb = kChunk / (4 * kB);
+      float4 r[3][kB];
+#pragma unroll
+      for (int u = 0; u < kB; ++u) {
+        r[0][u] = sb4[u];
+        r[1][u] = sb4[kB + u];
+      }
+#pragma unroll
+      for (int bt = 0; bt < kNb; ++bt) {
+        if (bt + 2 < kNb) {
+#pragma unroll
+          for (int u = 0; u < kB; ++u) r[(bt + 2) % 3][u] = sb4[(bt + 2) * kB + u];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+          acc = acc + r[bt % 3][u].x;
+          acc = acc + r[bt % 3][u].y;
+          acc = acc + r[bt % 3][u].z;
+          acc = acc + r[bt % 3][u].w;
+        }
+      }
+      i = kChunk;
+    } else if (i + 8 * V <= m) {
       // ping-pong register batches: the next 4V elements are read from LDS while the chain
       // consumes the current ones (no register copies between batches)
       float4 pa[V], pb[V];
@@ -177,6 +195,7 @@ __device__ __forceinline__ float seq_sum(const float* __restrict__ g, int b, int
       while (true) {
 #pragma unroll
         for (int u = 0; u < V; ++u) pb[u] = sb4[i / 4 + V + u];
+        __builtin_amdgcn_sched_barrier(0);  // keep the next batch's reads ahead of the chain
 #pragma unroll
         for (int u = 0; u < V; ++u) {
           acc = acc + pa[u].x;
@@ -198,6 +217,7 @@ __device__ __forceinline__ float seq_sum(const float* __restrict__ g, int b, int
         }
 #pragma unroll
         for (int u = 0; u < V; ++u) pa[u] = sb4[i / 4 + V + u];
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int u = 0; u < V; ++u) {
           acc = acc + pb[u].x;
@@ -227,11 +247,46 @@ __device__ __forceinline__ float seq_sum(const float* __restrict__ g, int b, int
   return acc;
 }
 
-// Two waves per (frame, label) run: wave 0 sums x (np.mean axis 0, sequential float32 in index
-// order) and the intensities, wave 1 sums y; they run on different SIMDs.
-// Mean intensity: when every intensity is a non-negative integer and the total stays below 2^24,
-// every summation order is exact (integer lane sums), which equals numpy's pairwise result;
-// otherwise numpy's chunked pairwise sum is evaluated by lane 0.
+// Mean intensity of g[b..e) by one wave: when every intensity is a non-negative integer and the
+// total stays below 2^24, every summation order is exact (integer lane sums), which equals
+// numpy's pairwise result; otherwise numpy's chunked pairwise sum is evaluated by lane 0.
+// 32 loads per lane in flight per round.
+__device__ __forceinline__ float mean_intensity(const float* __restrict__ gi, int b, int e,
+                                                int lane) {
+  constexpr int kU = 32;
+  uint64_t isum = 0;
+  bool small_int = true;
+  for (int c0 = b; c0 < e; c0 += 64 * kU) {
+    float v[kU];
+#pragma unroll
+    for (int t = 0; t < kU; ++t) {
+      const int idx = c0 + t * 64 + lane;
+      v[t] = idx < e ? gi[idx] : 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < kU; ++t) {
+      small_int = small_int && (v[t] >= 0.f && v[t] == floorf(v[t]) && v[t] < 16777216.f);
+      isum += (uint32_t)v[t];
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) isum += __shfl_xor(isum, off);
+  const bool all_int = __all(small_int);
+  const int k = e - b;
+  const float fk = (float)k;
+  if (all_int && isum < 16777216u) return (float)isum / fk;
+  float tot = 0.f;
+  if (lane == 0)
+    for (int64_t c = 0; c < k; c += 8192) {
+      const int64_t len = (k - c < 8192) ? (k - c) : 8192;
+      tot = tot + pairwise_f32(gi, b + c, len);
+    }
+  return tot / fk;
+}
+
+// Three waves per (frame, label) run: wave 0 sums x (np.mean axis 0, sequential float32 in index
+// order), wave 1 sums y — two pure dependent-add chains on different SIMDs — and wave 2 takes
+// the mean intensity (lane-parallel), so no other work sits in the chains' instruction streams.
 __global__ __launch_bounds__(kBlock) void k_summarize(
     const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
     const int64_t* __restrict__ seg_start, int64_t n_seg, int64_t n,
@@ -243,44 +298,31 @@ __global__ __launch_bounds__(kBlock) void k_summarize(
   const int lane = threadIdx.x & 63;
   const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
   const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
-  for (int64_t w = w0; w < 2 * n_seg; w += nw) {
-    const int su = __builtin_amdgcn_readfirstlane((int)(w >> 1));
-    const int comp = __builtin_amdgcn_readfirstlane((int)(w & 1));
+  for (int64_t w = w0; w < 3 * n_seg; w += nw) {
+    const int su = __builtin_amdgcn_readfirstlane((int)(w / 3));
+    const int comp = __builtin_amdgcn_readfirstlane((int)(w - (int64_t)su * 3));
     const int b = __builtin_amdgcn_readfirstlane((int)seg_start[su]);
     const int e = __builtin_amdgcn_readfirstlane(
         (int)((su + 1 < n_seg) ? seg_start[su + 1] : n));
     const int k = e - b;
     const float fk = (float)k;
-    bool small_int = true;
-    int64_t isum = 0;
-    const float sum = seq_sum(comp ? gy : gx, b, e, lane, s_buf[threadIdx.x / 64],
-                              comp ? nullptr : gi, isum, small_int);
-    if (comp) {
-      if (lane == 0) o_cy[su] = sum / fk;
+    if (comp == 2) {
+      const float mi = mean_intensity(gi, b, e, lane);
+      if (lane == 0) o_mi[su] = mi;
       continue;
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) isum += __shfl_xor(isum, off);
-    const bool all_int = __all(small_int);
+    const float sum = seq_sum(comp ? gy : gx, b, e, lane, s_buf[threadIdx.x / 64]);
     if (lane == 0) {
-      float mi;
-      if (all_int && isum < 16777216) {
-        mi = (float)isum / fk;
+      if (comp) {
+        o_cy[su] = sum / fk;
       } else {
-        float tot = 0.f;
-        for (int64_t c = 0; c < k; c += 8192) {
-          const int64_t len = (k - c < 8192) ? (k - c) : 8192;
-          tot = tot + pairwise_f32(gi, b + c, len);
-        }
-        mi = tot / fk;
+        const uint32_t i0 = sv[b];
+        o_frame[su] = pf[i0];
+        o_label[su] = (int32_t)sk[b] - 1;
+        o_count[su] = k;
+        o_first[su] = i0;
+        o_cx[su] = sum / fk;
       }
-      const uint32_t i0 = sv[b];
-      o_frame[su] = pf[i0];
-      o_label[su] = (int32_t)sk[b] - 1;
-      o_count[su] = k;
-      o_first[su] = i0;
-      o_cx[su] = sum / fk;
-      o_mi[su] = mi;
     }
   }
 }
@@ -353,7 +395,7 @@ int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
   if (n_seg > 0) {
     hipLaunchKernelGGL(k_gather_runs, dim3(g), dim3(kBlock), 0, st, sv, n, x, y, inten, gx, gy,
                        gi);
-    hipLaunchKernelGGL(k_summarize, dim3(grid_for(2 * n_seg, kBlock / 64, 16384)), dim3(kBlock),
+    hipLaunchKernelGGL(k_summarize, dim3(grid_for(3 * n_seg, kBlock / 64, 16384)), dim3(kBlock),
                        0, st, sk, sv, seg_start, n_seg, n, gx, gy, gi, pf, o_frame, o_label,
                        o_count, o_first, o_cx, o_cy, o_mi);
     RPT_CHECK_LAUNCH();
