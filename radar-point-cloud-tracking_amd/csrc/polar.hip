@@ -70,10 +70,10 @@ __device__ __forceinline__ int wave_excl_scan(int v, int* total) {
 // Inclusive wave prefix sum with DPP (6 VALU ops, no LDS): row_shr 1/2/4/8 within 16-lane rows,
 // then row_bcast:15 / row_bcast:31 carry the row totals (GFX9-family DPP, available on gfx950).
 __device__ __forceinline__ int wave_incl_scan_dpp(int v) {
-  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
-  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
-  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
-  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);  // row_shr:8
   v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
   v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
   return v;
@@ -251,6 +251,21 @@ __device__ __forceinline__ uint32_t mask16(uint32_t m0, uint32_t m1, uint32_t m2
   return (lo | (hi << 8)) >> 7;
 }
 
+// Position of the n-th (0-based) set bit of a 16-bit mask, n < popcount: binary search on
+// popcounts of the low half, quarter, ... (v_cndmask selects, no branches).
+__device__ __forceinline__ int nth_bit16(uint32_t m, uint32_t n) {
+  int p = 0;
+  uint32_t c = __popc(m & 0xffu);
+  if (n >= c) { n -= c; p = 8; }
+  c = __popc((m >> p) & 0xfu);
+  if (n >= c) { n -= c; p += 4; }
+  c = __popc((m >> p) & 0x3u);
+  if (n >= c) { n -= c; p += 2; }
+  c = (m >> p) & 1u;
+  if (n >= c) p += 1;
+  return p;
+}
+
 // Rows are handled in groups of kGroupRows consecutive rows of one file (the last group of a file
 // may be short): a wave issues the group's loads together (4 KiB in flight) before ranking any of
 // them.  The count pass writes one kept count per GROUP; the write pass walks the group's rows in
@@ -371,14 +386,13 @@ __global__ __launch_bounds__(kBlock) void k_group_write_u8(
           const uint32_t r = rank + (uint32_t)(incl - c);
           const uint32_t q = pow2 ? ((r + us - 1u) >> sh) : (r + us - 1u) / us;
           int slot = (int)(q - first);
-          // drop the kept samples before the first rank that is a multiple of stride
-          for (uint32_t t = q * us - r; t > 0u && m; --t) m &= m - 1u;
-          while (m) {
-            const int kk = __builtin_ctz(m);
+          // the lane's emitted samples are its kept samples j = q*stride - r, + stride, ... < c;
+          // each is located in the 16-bit mask by a branch-free select (no per-bit loops)
+          for (uint32_t j = q * us - r; j < (uint32_t)c; j += us) {
+            const int kk = nth_bit16(m, j);
             const uint32_t w = (kk < 4) ? v.x : (kk < 8) ? v.y : (kk < 12) ? v.z : v.w;
             stage[slot++] = ((uint32_t)(lane * 16 + kk) << 8) |
                             __builtin_amdgcn_ubfe(w, (uint32_t)(8 * (kk & 3)), 8u);
-            for (uint32_t t = 0; t < us && m; ++t) m &= m - 1u;
           }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
