@@ -9,6 +9,8 @@
 // integer echo values of the radar path (sums < 2^53), like np.add.at's sequential order.
 #include <cstring>
 
+#include <algorithm>
+
 #include "common.h"
 
 #pragma clang fp contract(off)
@@ -146,9 +148,12 @@ __device__ __forceinline__ Edges stage_edges(const double* xe, int nxe, const do
 }
 
 // LDS-privatised form: int32 counts + f64 sums of the whole grid per block (fits when
-// cells * 12 B + edges <= ~150 KiB), flushed with one atomic per non-empty cell.
+// cells * 12 B + edges <= ~150 KiB), flushed with one atomic per non-empty cell.  One 1024-thread
+// block per CU: the per-block cost (zeroing and flushing ~10k cells) is paid 256 times, not once
+// per 256-thread block of a larger grid, and 16 waves per CU hide the LDS atomics' latency.
 constexpr int kLdsGridCells = 10240;
-__global__ __launch_bounds__(kBlock) void k_land_grid_lds(const float* __restrict__ x,
+constexpr int kGridBlock = 1024;
+__global__ __launch_bounds__(kGridBlock) void k_land_grid_lds(const float* __restrict__ x,
                                                          const float* __restrict__ y,
                                                          const float* __restrict__ val, int64_t n,
                                                          const double* __restrict__ xe, int nxe,
@@ -317,8 +322,11 @@ int32_t land_grid(const float* x, const float* y, const float* val, int64_t n, c
   if (cells <= kLdsGridCells && lds <= 150 * 1024) {
     RPT_HIP(hipFuncSetAttribute((const void*)k_land_grid_lds,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k_land_grid_lds, dim3(grid_for(n, kBlock, 512)), dim3(kBlock), lds, st, x,
-                       y, val, n, xe, nxe, ye, nye, cnt, tot);
+    int dev = 0, n_cu = 0;
+    RPT_HIP(hipGetDevice(&dev));
+    RPT_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    hipLaunchKernelGGL(k_land_grid_lds, dim3(grid_for(n, kGridBlock, std::max(n_cu, 1))),
+                       dim3(kGridBlock), lds, st, x, y, val, n, xe, nxe, ye, nye, cnt, tot);
   } else {
     hipLaunchKernelGGL(k_land_grid, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, st, x, y,
                        val, n, xe, nxe, ye, nye, cnt, tot);
