@@ -159,7 +159,8 @@ __global__ __launch_bounds__(kGridBlock) void k_land_grid_lds(const float* __res
                                                          const double* __restrict__ xe, int nxe,
                                                          const double* __restrict__ ye, int nye,
                                                          int32_t* __restrict__ cnt,
-                                                         double* __restrict__ tot) {
+                                                         double* __restrict__ tot,
+                                                         int32_t* __restrict__ cell_out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* lds_e = reinterpret_cast<double*>(smem);                    // nxe + nye edges
   const int ne = nxe + nye;
@@ -183,6 +184,7 @@ __global__ __launch_bounds__(kGridBlock) void k_land_grid_lds(const float* __res
     const int ix = clip_idx(count_le_arith(ex, nxe, (double)x[i], idx_) - 1, nxe - 2);
     const int iy = clip_idx(count_le_arith(ey, nye, (double)y[i], idy_) - 1, nye - 2);
     const int c = ix * ny + iy;
+    if (cell_out) cell_out[i] = c;
     atomicAdd(lds_c + c, 1);
     atomicAdd(lds_t + c, (double)val[i]);
   }
@@ -202,7 +204,8 @@ __global__ __launch_bounds__(kBlock) void k_land_grid(const float* __restrict__ 
                                                      const double* __restrict__ xe, int nxe,
                                                      const double* __restrict__ ye, int nye,
                                                      int32_t* __restrict__ cnt,
-                                                     double* __restrict__ tot) {
+                                                     double* __restrict__ tot,
+                                                     int32_t* __restrict__ cell_out) {
   __shared__ double lds[kMaxEdges];
   const Edges E = stage_edges(xe, nxe, ye, nye, lds);
   const int ny = nye - 1;
@@ -211,6 +214,7 @@ __global__ __launch_bounds__(kBlock) void k_land_grid(const float* __restrict__ 
     const int ix = clip_idx(count_le(E.xe, nxe, (double)x[i]) - 1, nxe - 2);
     const int iy = clip_idx(count_le(E.ye, nye, (double)y[i]) - 1, nye - 2);
     const int64_t c = (int64_t)ix * ny + iy;
+    if (cell_out) cell_out[i] = (int32_t)c;
     atomicAdd(cnt + c, 1);
     atomicAdd(tot + c, (double)val[i]);
   }
@@ -251,6 +255,16 @@ __global__ __launch_bounds__(kBlock) void k_land_keep(const float* __restrict__ 
     const int iy = clip_idx(count_le_arith(E.ye, nye, (double)y[i], idy_) - 1, nye - 2);
     keep[i] = land[(int64_t)ix * ny + iy] ? 0 : 1;
   }
+}
+
+// keep flags from the cells the grid pass stored (no edge search)
+__global__ __launch_bounds__(kBlock) void k_land_keep_cells(const int32_t* __restrict__ cell,
+                                                           int64_t n,
+                                                           const uint8_t* __restrict__ land,
+                                                           int32_t* __restrict__ keep) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    keep[i] = land[cell[i]] ? 0 : 1;
 }
 
 __global__ __launch_bounds__(kBlock) void k_land_scatter(
@@ -306,14 +320,16 @@ int32_t bounds_xy(const float* x, const float* y, int64_t n, float* out4, hipStr
   return RPT_OK;
 }
 
-int32_t land_grid(const float* x, const float* y, const float* val, int64_t n, const double* xe,
-                  int32_t nxe, const double* ye, int32_t nye, int32_t* cnt, double* tot,
-                  hipStream_t st) {
+// cell_out (nullable, [n], int32 cells < 2^31): each point's grid cell, for land_filter_cells
+int32_t land_grid_cells(const float* x, const float* y, const float* val, int64_t n,
+                        const double* xe, int32_t nxe, const double* ye, int32_t nye,
+                        int32_t* cnt, double* tot, int32_t* cell_out, hipStream_t st) {
   if (nxe < 2 || nye < 2) {
     set_error("rpt_land_grid: need at least two edges per axis");
     return RPT_EINVAL;
   }
   const int64_t cells = (int64_t)(nxe - 1) * (nye - 1);
+  if (cell_out && cells >= (int64_t(1) << 31)) cell_out = nullptr;
   RPT_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t) * cells, st));
   RPT_HIP(hipMemsetAsync(tot, 0, sizeof(double) * cells, st));
   if (n == 0) return RPT_OK;
@@ -326,13 +342,20 @@ int32_t land_grid(const float* x, const float* y, const float* val, int64_t n, c
     RPT_HIP(hipGetDevice(&dev));
     RPT_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
     hipLaunchKernelGGL(k_land_grid_lds, dim3(grid_for(n, kGridBlock, std::max(n_cu, 1))),
-                       dim3(kGridBlock), lds, st, x, y, val, n, xe, nxe, ye, nye, cnt, tot);
+                       dim3(kGridBlock), lds, st, x, y, val, n, xe, nxe, ye, nye, cnt, tot,
+                       cell_out);
   } else {
     hipLaunchKernelGGL(k_land_grid, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, st, x, y,
-                       val, n, xe, nxe, ye, nye, cnt, tot);
+                       val, n, xe, nxe, ye, nye, cnt, tot, cell_out);
   }
   RPT_CHECK_LAUNCH();
   return RPT_OK;
+}
+
+int32_t land_grid(const float* x, const float* y, const float* val, int64_t n, const double* xe,
+                  int32_t nxe, const double* ye, int32_t nye, int32_t* cnt, double* tot,
+                  hipStream_t st) {
+  return land_grid_cells(x, y, val, n, xe, nxe, ye, nye, cnt, tot, nullptr, st);
 }
 
 int32_t land_mask(const int32_t* cnt, const double* tot, int64_t cells, int64_t num_frames,
@@ -357,11 +380,13 @@ int32_t land_mask(const int32_t* cnt, const double* tot, int64_t cells, int64_t 
   return RPT_OK;
 }
 
-int32_t land_filter(const float* x, const float* y, const float* v, const int32_t* g,
-                    const int32_t* pf, int64_t n, const int64_t* frame_off, int32_t n_frames,
-                    const double* xe, int32_t nxe, const double* ye, int32_t nye,
-                    const uint8_t* land, float* xo, float* yo, float* vo, int32_t* go,
-                    int32_t* pfo, int64_t* new_off, int64_t* n_kept_host, hipStream_t st) {
+// cell (nullable): the per-point cells from land_grid_cells over the same points and edges
+int32_t land_filter_cells(const float* x, const float* y, const float* v, const int32_t* g,
+                          const int32_t* pf, int64_t n, const int64_t* frame_off,
+                          int32_t n_frames, const double* xe, int32_t nxe, const double* ye,
+                          int32_t nye, const uint8_t* land, const int32_t* cell, float* xo,
+                          float* yo, float* vo, int32_t* go, int32_t* pfo, int64_t* new_off,
+                          int64_t* n_kept_host, hipStream_t st) {
   Scratch& sc = scratch(st);
   Budget b;
   b.add<int32_t>(n + 1);
@@ -369,7 +394,11 @@ int32_t land_filter(const float* x, const float* y, const float* v, const int32_
   RPT_TRY(sc.reserve(b.bytes, st));
   int32_t* keep = sc.carve_n<int32_t>(n + 1);
   int64_t* pos = sc.carve_n<int64_t>(n + 1);
-  if (n > 0) {
+  if (n > 0 && cell) {
+    hipLaunchKernelGGL(k_land_keep_cells, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, st,
+                       cell, n, land, keep);
+    RPT_CHECK_LAUNCH();
+  } else if (n > 0) {
     hipLaunchKernelGGL(k_land_keep, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, st, x, y,
                        n, xe, nxe, ye, nye, land, keep);
     RPT_CHECK_LAUNCH();
@@ -390,6 +419,15 @@ int32_t land_filter(const float* x, const float* y, const float* v, const int32_
     RPT_TRY(wait_stream(st));
   }
   return RPT_OK;
+}
+
+int32_t land_filter(const float* x, const float* y, const float* v, const int32_t* g,
+                    const int32_t* pf, int64_t n, const int64_t* frame_off, int32_t n_frames,
+                    const double* xe, int32_t nxe, const double* ye, int32_t nye,
+                    const uint8_t* land, float* xo, float* yo, float* vo, int32_t* go,
+                    int32_t* pfo, int64_t* new_off, int64_t* n_kept_host, hipStream_t st) {
+  return land_filter_cells(x, y, v, g, pf, n, frame_off, n_frames, xe, nxe, ye, nye, land,
+                           nullptr, xo, yo, vo, go, pfo, new_off, n_kept_host, st);
 }
 
 }  // namespace rpt

@@ -26,17 +26,18 @@ int32_t polar_write(const void* echo, int32_t dt, int64_t n_files, int32_t rows,
                     float* v, int32_t* gout, int32_t* pf, hipStream_t st);
 int32_t frame_times(const int32_t* pf, int64_t n, const int64_t* ids, float* t, hipStream_t st);
 int32_t bounds_xy(const float* x, const float* y, int64_t n, float* out4, hipStream_t st);
-int32_t land_grid(const float* x, const float* y, const float* val, int64_t n, const double* xe,
-                  int32_t nxe, const double* ye, int32_t nye, int32_t* cnt, double* tot,
-                  hipStream_t st);
+int32_t land_grid_cells(const float* x, const float* y, const float* val, int64_t n,
+                        const double* xe, int32_t nxe, const double* ye, int32_t nye,
+                        int32_t* cnt, double* tot, int32_t* cell_out, hipStream_t st);
 int32_t land_mask(const int32_t* cnt, const double* tot, int64_t cells, int64_t num_frames,
                   double pthr, double ithr, uint8_t* land, int64_t* n_land_host,
                   hipStream_t st);
-int32_t land_filter(const float* x, const float* y, const float* v, const int32_t* g,
-                    const int32_t* pf, int64_t n, const int64_t* frame_off, int32_t n_frames,
-                    const double* xe, int32_t nxe, const double* ye, int32_t nye,
-                    const uint8_t* land, float* xo, float* yo, float* vo, int32_t* go,
-                    int32_t* pfo, int64_t* new_off, int64_t* n_kept_host, hipStream_t st);
+int32_t land_filter_cells(const float* x, const float* y, const float* v, const int32_t* g,
+                          const int32_t* pf, int64_t n, const int64_t* frame_off,
+                          int32_t n_frames, const double* xe, int32_t nxe, const double* ye,
+                          int32_t nye, const uint8_t* land, const int32_t* cell, float* xo,
+                          float* yo, float* vo, int32_t* go, int32_t* pfo, int64_t* new_off,
+                          int64_t* n_kept_host, hipStream_t st);
 int32_t stdbscan(const float* x, const float* y, const float* z, int64_t stride, const float* t,
                  int64_t n, double eps_space, double eps_time, int32_t min_samples,
                  int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st, int dim);
@@ -142,7 +143,7 @@ struct rpt_stack {
   DevBuf<uint32_t> pack_d;  // packed readback staging
   DevBuf<int64_t> row_prefix, file_off, fo_d, new_off, first_noise, seg_count, seg_first, scal;
   DevBuf<float> x, y, v, x2, y2, v2, t, seg_cx, seg_cy, seg_mi;
-  DevBuf<int32_t> g, pf, g2, pf2, labels, land_cnt, seg_frame, seg_label;
+  DevBuf<int32_t> g, pf, g2, pf2, labels, land_cnt, land_cell, seg_frame, seg_label;
   DevBuf<double> land_tot, edges;
   DevBuf<uint8_t> land_mask;
   PinnedBuf up, down;  // host staging: uploads (edges, offsets), readbacks
@@ -162,7 +163,8 @@ struct rpt_stack {
     for (auto* b : i64) b->release();
     DevBuf<float>* f32[] = {&x, &y, &v, &x2, &y2, &v2, &t, &seg_cx, &seg_cy, &seg_mi};
     for (auto* b : f32) b->release();
-    DevBuf<int32_t>* i32[] = {&g, &pf, &g2, &pf2, &labels, &land_cnt, &seg_frame, &seg_label};
+    DevBuf<int32_t>* i32[] = {&g,        &pf,       &g2,        &pf2,      &labels,
+                              &land_cnt, &land_cell, &seg_frame, &seg_label};
     for (auto* b : i32) b->release();
     land_tot.release();
     edges.release();
@@ -260,8 +262,9 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
     RPT_TRY(land_cnt.ensure((size_t)cells, st));
     RPT_TRY(land_tot.ensure((size_t)cells, st));
     RPT_TRY(land_mask.ensure((size_t)cells, st));
-    RPT_TRY(land_grid(x.p, y.p, v.p, N, edges.p, nxe, edges.p + nxe, nye, land_cnt.p, land_tot.p,
-                      st));
+    RPT_TRY(land_cell.ensure(cap, st));
+    RPT_TRY(land_grid_cells(x.p, y.p, v.p, N, edges.p, nxe, edges.p + nxe, nye, land_cnt.p,
+                            land_tot.p, land_cell.p, st));
     RPT_TRY(rpt::land_mask(land_cnt.p, land_tot.p, cells, n_built, p.land_persistence,
                            p.land_min_intensity, land_mask.p, nullptr, st));
     RPT_TRY(scal.ensure(4, st));
@@ -275,9 +278,9 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
     RPT_TRY(g2.ensure(cap, st));
     RPT_TRY(pf2.ensure(cap, st));
     RPT_TRY(new_off.ensure((size_t)F + 1, st));
-    RPT_TRY(land_filter(x.p, y.p, v.p, gain ? g.p : nullptr, pf.p, N, fo_d.p, F, edges.p, nxe,
-                        edges.p + nxe, nye, land_mask.p, x2.p, y2.p, v2.p, gain ? g2.p : nullptr,
-                        pf2.p, new_off.p, nullptr, st));
+    RPT_TRY(land_filter_cells(x.p, y.p, v.p, gain ? g.p : nullptr, pf.p, N, fo_d.p, F, edges.p,
+                              nxe, edges.p + nxe, nye, land_mask.p, land_cell.p, x2.p, y2.p,
+                              v2.p, gain ? g2.p : nullptr, pf2.p, new_off.p, nullptr, st));
     int64_t* hn = reinterpret_cast<int64_t*>(down.p);
     PackList pl;
     pl.add(new_off.p, sizeof(int64_t) * (F + 1));
