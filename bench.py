@@ -69,6 +69,8 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-stage hipEvent timing")
+    ap.add_argument("--sharded", action="store_true",
+                    help="run the frame-sharded (multi-GPU) pipeline even with one rank")
     ap.add_argument("--lanes", type=int, default=1,
                     help="single GPU: stacks in flight at once (native handles on separate "
                          "streams, FrameStackPipeline.submit)")
@@ -80,7 +82,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
+    # --sharded: the frame-sharded multi-GPU path even at one rank (measures its per-rank cost)
+    dist = world > 1 or args.sharded
+    if dist and "MASTER_ADDR" not in os.environ:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29533", RANK="0", WORLD_SIZE="1")
     if dist:
         import torch.distributed as tdist
 

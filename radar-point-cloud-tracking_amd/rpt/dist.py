@@ -203,7 +203,8 @@ class ShardResult:
     def finish(self) -> "ShardResult":
         """Wait for rank 0's host stage when it runs asynchronously (async_host=True)."""
         if self._pending is not None:
-            self.frame_order_offsets, self.frame_order, self.tracker, ms = self._pending.result()
+            (self.seg, self.built_global, self.frame_order_offsets, self.frame_order,
+             self.tracker, ms) = self._pending.result()
             if self.stage_ms:
                 self.stage_ms["tracker"] = ms
             self._pending = None
@@ -216,10 +217,10 @@ class ShardedStackPipeline:
     def __init__(self, ops, comm: Comm, gains: Sequence[int], rows: int, bins: int,
                  params: PathParams = None, timing: bool = False, async_host: bool = False,
                  host_workers: int = 2):
-        """async_host: rank 0's host stage (the tracker over the whole stack; every rank orders
-        its own frames' clusters before the gather) runs on a pool of host_workers threads while
-        the ranks go on to the next runs (runs are independent, so their trackers may overlap
-        each other too); ShardResult.finish() waits."""
+        """async_host: rank 0's host stage (the reference cluster order of every frame and the
+        tracker over the whole stack) runs on a pool of host_workers threads while the ranks go
+        on to the next runs (runs are independent, so their host stages may overlap each other
+        too); ShardResult.finish() waits and fills seg / frame_order / tracker."""
         self._host = ThreadPoolExecutor(max_workers=host_workers) if async_host else None
         self.ops = ops
         self.comm = comm
@@ -342,36 +343,34 @@ class ShardedStackPipeline:
         labels = labels_all[n_prev:n_prev + n_own]
         n_clusters = int(reps_sorted.numel())
         mark("stdbscan")
-        # 8. summaries and the reference cluster order of the own frames (host, per rank), then
-        #    ONE gather of everything rank 0's tracker needs (float64 carries the int32 / int64
-        #    fields and the float32 values exactly)
+        # 8. summaries of the own frames, then ONE gather of everything rank 0's host stage
+        #    needs (float64 carries the int32 / int64 fields and the float32 values exactly);
+        #    the per-frame cluster order is computed there, off every rank's critical path
         seg, first_noise = ops.summaries(pts, labels, n_clusters)
         S = len(seg["frame"])
-        fo_l, order_l = order_frames(F, seg, first_noise)
         packed = np.concatenate([
-            [S], built_local.astype(np.float64) + frame0, [-1.0] * (F - len(built_local)), fo_l,
-            order_l, seg["frame"].astype(np.float64) + frame0, seg["label"], seg["count"],
-            seg["first"], seg["cx"], seg["cy"], seg["mi"]]).astype(np.float64)
+            [S, frame0], built_local.astype(np.float64), [-1.0] * (F - len(built_local)),
+            first_noise, seg["frame"], seg["label"], seg["count"], seg["first"], seg["cx"],
+            seg["cy"], seg["mi"]]).astype(np.float64)
         parts = comm.all_gather_var(torch.from_numpy(packed)) if W > 1 else \
             [torch.from_numpy(packed)]
         mark("summaries")
         res = ShardResult(n_points_local=n_local, n_points_global=n_global,
                           n_clustered_local=n_own, n_clusters=n_clusters, labels_local=labels)
         if r == 0:
-            all_seg, built, fo_g, order_g = _unpack_parts(parts, F)
-            res.seg, res.built_global = all_seg, built
-            res.n_segments = len(all_seg["frame"])
-            res.frame_order_offsets, res.frame_order = fo_g, order_g
+            res.n_segments = int(sum(float(t[0]) for t in parts))
 
             def host_stage():
                 t0 = time.perf_counter()
+                all_seg, built, fo_g, order_g = _unpack_parts(parts, F)
                 trk = track_ordered(built - frame0, fo_g, order_g, all_seg, p, built)
-                return fo_g, order_g, trk, (time.perf_counter() - t0) * 1e3
+                return all_seg, built, fo_g, order_g, trk, (time.perf_counter() - t0) * 1e3
 
             if self._host is not None:
                 res._pending = self._host.submit(host_stage)
             else:
-                res.tracker = host_stage()[2]
+                (res.seg, res.built_global, res.frame_order_offsets, res.frame_order,
+                 res.tracker, _) = host_stage()
         mark("tracker")
         if self.timing:
             for (a, ta), (b, tb) in zip(marks[:-1], marks[1:]):
@@ -380,28 +379,33 @@ class ShardedStackPipeline:
 
 
 def _unpack_parts(parts, F: int):
-    """Rank 0: the per-rank packed summaries (rank order = frame order) -> global seg arrays,
-    built frame ids, per-frame-slot order offsets and order (indices into the global seg)."""
+    """Rank 0: the per-rank packed summaries (rank order = frame order) -> global seg arrays
+    (frame = global slot), built frame ids, and per frame slot the reference cluster order
+    (offsets + indices into the global seg), computed rank part by rank part."""
     segs = {k: [] for k in ("frame", "label", "count", "first", "cx", "cy", "mi")}
     built, fos, orders = [], [np.zeros(1, np.int64)], []
     s_base = 0
-    for q, t in enumerate(parts):
+    for t in parts:
         a = t.cpu().numpy()
-        S = int(a[0])
-        o = 1
+        S, f0 = int(a[0]), int(a[1])
+        o = 2
         bl = a[o:o + F]
         o += F
-        built.append(bl[bl >= 0].astype(np.int64))
-        fo = a[o:o + F + 1].astype(np.int64)
-        o += F + 1
-        fos.append(fo[1:] + s_base)
-        orders.append(a[o:o + S].astype(np.int64) + s_base)
-        o += S
+        built.append(bl[bl >= 0].astype(np.int64) + f0)
+        first_noise = a[o:o + F].astype(np.int64)
+        o += F
+        part = {}
         for k, dt in (("frame", np.int32), ("label", np.int32), ("count", np.int64),
                       ("first", np.int64), ("cx", np.float32), ("cy", np.float32),
                       ("mi", np.float32)):
-            segs[k].append(a[o:o + S].astype(dt))
+            part[k] = a[o:o + S].astype(dt)
             o += S
+        fo, order = order_frames(F, part, first_noise)   # frames of the part: local slots
+        fos.append(fo[1:] + s_base)
+        orders.append(order[:S] + s_base)
+        part["frame"] = part["frame"] + np.int32(f0)
+        for k in segs:
+            segs[k].append(part[k])
         s_base += S
     seg = {k: np.concatenate(v) for k, v in segs.items()}
     return seg, np.concatenate(built), np.concatenate(fos), np.concatenate(orders)
