@@ -57,6 +57,9 @@ class _Ws:
         return b[:n]
 
 
+_NP_DT = {torch.int32: np.int32, torch.int64: np.int64, torch.float32: np.float32}
+
+
 class HipOps:
     """librpt-backed stages for one device."""
 
@@ -251,8 +254,13 @@ class HipOps:
             so["cy"].data_ptr(), so["mi"].data_ptr(), ffn.data_ptr(), _abi.C.byref(nseg),
             self.st()), "rpt_cluster_summaries")
         S = int(nseg.value)
-        seg = {k: t[:S].cpu().numpy() for k, t in so.items()}
-        return seg, ffn[:F].cpu().numpy()
+        # one readback: the arrays packed on the device as float64 (exact for every field)
+        keys = list(so)
+        flat = torch.cat([so[k][:S].to(torch.float64) for k in keys] +
+                         [ffn[:F].to(torch.float64)]).cpu().numpy()
+        seg = {k: flat[i * S:(i + 1) * S].astype(_NP_DT[so[k].dtype])
+               for i, k in enumerate(keys)}
+        return seg, flat[len(keys) * S:].astype(np.int64)
 
     def close(self):
         if self._dbscan is not None:
