@@ -111,8 +111,11 @@ def main():
         from rpt.stages import HipOps
 
         ops = HipOps(dev, timing=timing)
+        # rank 0's host stage (order + tracker over N*F frames, ~6.7 us/frame) of consecutive
+        # steps runs on 4 worker threads: the steps are independent stacks
         pipe = ShardedStackPipeline(ops, Comm(dev), cfg.gains, cfg.rows, cfg.bins, PathParams(),
-                                    timing=timing, async_host=not args.sync_host)
+                                    timing=timing, async_host=not args.sync_host,
+                                    host_workers=4)
         G = len(cfg.gains)
         pipe.set_geometry(
             tuple(torch.from_numpy(np.tile(a, F * G)).to(dev) for a in
