@@ -358,6 +358,19 @@ int32_t land_grid(const float* x, const float* y, const float* val, int64_t n, c
   return land_grid_cells(x, y, val, n, xe, nxe, ye, nye, cnt, tot, nullptr, st);
 }
 
+// n_land_dev: int32 land-cell counter on the device, zeroed by the caller (no readback)
+int32_t land_mask_dev(const int32_t* cnt, const double* tot, int64_t cells, int64_t num_frames,
+                      double pthr, double ithr, uint8_t* land, int32_t* n_land_dev,
+                      hipStream_t st) {
+  const double nf = (double)(num_frames > 1 ? num_frames : 1);
+  if (cells > 0) {
+    hipLaunchKernelGGL(k_land_mask, dim3(grid_for(cells, 256, 1024)), dim3(256), 0, st, cnt, tot,
+                       cells, nf, pthr, ithr, land, n_land_dev);
+    RPT_CHECK_LAUNCH();
+  }
+  return RPT_OK;
+}
+
 int32_t land_mask(const int32_t* cnt, const double* tot, int64_t cells, int64_t num_frames,
                   double pthr, double ithr, uint8_t* land, int64_t* n_land_host,
                   hipStream_t st) {

@@ -32,6 +32,9 @@ int32_t land_grid_cells(const float* x, const float* y, const float* val, int64_
 int32_t land_mask(const int32_t* cnt, const double* tot, int64_t cells, int64_t num_frames,
                   double pthr, double ithr, uint8_t* land, int64_t* n_land_host,
                   hipStream_t st);
+int32_t land_mask_dev(const int32_t* cnt, const double* tot, int64_t cells, int64_t num_frames,
+                      double pthr, double ithr, uint8_t* land, int32_t* n_land_dev,
+                      hipStream_t st);
 int32_t land_filter_cells(const float* x, const float* y, const float* v, const int32_t* g,
                           const int32_t* pf, int64_t n, const int64_t* frame_off,
                           int32_t n_frames, const double* xe, int32_t nxe, const double* ye,
@@ -68,15 +71,6 @@ std::vector<double> arange_edges(float lo, float hi, double res) {
 }
 
 namespace {
-
-__global__ void k_count_u8(const uint8_t* __restrict__ m, int64_t n, int64_t* __restrict__ out) {
-  int64_t c = 0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x)
-    c += m[i] ? 1 : 0;
-  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
-  if ((threadIdx.x & 63) == 0 && c) atomicAdd((unsigned long long*)out, (unsigned long long)c);
-}
 
 template <class T>
 struct DevBuf {
@@ -141,7 +135,7 @@ using namespace rpt;
 
 struct rpt_stack {
   DevBuf<uint32_t> pack_d;  // packed readback staging
-  DevBuf<int64_t> row_prefix, file_off, fo_d, new_off, first_noise, seg_count, seg_first, scal;
+  DevBuf<int64_t> row_prefix, file_off, new_off, first_noise, seg_count, seg_first, scal;
   DevBuf<float> x, y, v, x2, y2, v2, t, seg_cx, seg_cy, seg_mi;
   DevBuf<int32_t> g, pf, g2, pf2, labels, land_cnt, land_cell, seg_frame, seg_label;
   DevBuf<double> land_tot, edges;
@@ -158,7 +152,7 @@ struct rpt_stack {
   bool ev_ok = false;
 
   ~rpt_stack() {
-    DevBuf<int64_t>* i64[] = {&row_prefix, &file_off, &fo_d, &new_off, &first_noise, &seg_count,
+    DevBuf<int64_t>* i64[] = {&row_prefix, &file_off, &new_off, &first_noise, &seg_count,
                               &seg_first, &scal};
     for (auto* b : i64) b->release();
     DevBuf<float>* f32[] = {&x, &y, &v, &x2, &y2, &v2, &t, &seg_cx, &seg_cy, &seg_mi};
@@ -248,37 +242,36 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
       return RPT_EINVAL;
     }
     const int64_t cells = (int64_t)(nxe - 1) * (nye - 1);
-    RPT_TRY(edges.ensure((size_t)(nxe + nye), st));
-    RPT_TRY(fo_d.ensure((size_t)F + 1, st));
-    RPT_TRY(up.ensure(sizeof(double) * (size_t)(nxe + nye) + sizeof(int64_t) * (size_t)(F + 1),
-                      st));
+    // edges and the K1 frame offsets in ONE upload: [x edges | y edges | offsets (int64)]
+    const size_t n_up = (size_t)(nxe + nye) + (size_t)F + 1;
+    RPT_TRY(edges.ensure(n_up, st));
+    RPT_TRY(up.ensure(sizeof(double) * n_up, st));
     double* he = reinterpret_cast<double*>(up.p);
     std::memcpy(he, xe.data(), sizeof(double) * nxe);
     std::memcpy(he + nxe, ye.data(), sizeof(double) * nye);
     int64_t* hf = reinterpret_cast<int64_t*>(he + nxe + nye);
     std::memcpy(hf, fo_k1.data(), sizeof(int64_t) * (F + 1));
-    RPT_HIP(hipMemcpyAsync(edges.p, he, sizeof(double) * (nxe + nye), hipMemcpyHostToDevice, st));
-    RPT_HIP(hipMemcpyAsync(fo_d.p, hf, sizeof(int64_t) * (F + 1), hipMemcpyHostToDevice, st));
+    RPT_HIP(hipMemcpyAsync(edges.p, he, sizeof(double) * n_up, hipMemcpyHostToDevice, st));
+    const int64_t* fo_dev = reinterpret_cast<const int64_t*>(edges.p + nxe + nye);
     RPT_TRY(land_cnt.ensure((size_t)cells, st));
     RPT_TRY(land_tot.ensure((size_t)cells, st));
     RPT_TRY(land_mask.ensure((size_t)cells, st));
     RPT_TRY(land_cell.ensure(cap, st));
     RPT_TRY(land_grid_cells(x.p, y.p, v.p, N, edges.p, nxe, edges.p + nxe, nye, land_cnt.p,
                             land_tot.p, land_cell.p, st));
-    RPT_TRY(rpt::land_mask(land_cnt.p, land_tot.p, cells, n_built, p.land_persistence,
-                           p.land_min_intensity, land_mask.p, nullptr, st));
+    // the land-cell count accumulates (int32) into the low half of a zeroed int64 slot
     RPT_TRY(scal.ensure(4, st));
     RPT_HIP(hipMemsetAsync(scal.p, 0, sizeof(int64_t), st));
-    hipLaunchKernelGGL(k_count_u8, dim3(grid_for(cells, 256, 64)), dim3(256), 0, st,
-                       land_mask.p, cells, scal.p);
-    RPT_CHECK_LAUNCH();
+    RPT_TRY(land_mask_dev(land_cnt.p, land_tot.p, cells, n_built, p.land_persistence,
+                          p.land_min_intensity, land_mask.p, reinterpret_cast<int32_t*>(scal.p),
+                          st));
     RPT_TRY(x2.ensure(cap, st));
     RPT_TRY(y2.ensure(cap, st));
     RPT_TRY(v2.ensure(cap, st));
     RPT_TRY(g2.ensure(cap, st));
     RPT_TRY(pf2.ensure(cap, st));
     RPT_TRY(new_off.ensure((size_t)F + 1, st));
-    RPT_TRY(land_filter_cells(x.p, y.p, v.p, gain ? g.p : nullptr, pf.p, N, fo_d.p, F, edges.p,
+    RPT_TRY(land_filter_cells(x.p, y.p, v.p, gain ? g.p : nullptr, pf.p, N, fo_dev, F, edges.p,
                               nxe, edges.p + nxe, nye, land_mask.p, land_cell.p, x2.p, y2.p,
                               v2.p, gain ? g2.p : nullptr, pf2.p, new_off.p, nullptr, st));
     int64_t* hn = reinterpret_cast<int64_t*>(down.p);
