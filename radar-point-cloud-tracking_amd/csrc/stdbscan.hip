@@ -417,12 +417,24 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ 
     }
     float x0 = FLT_MAX, x1 = -FLT_MAX, y0 = FLT_MAX, y1 = -FLT_MAX;
     float z0 = FLT_MAX, z1 = -FLT_MAX, t0 = FLT_MAX, t1 = -FLT_MAX;
-    for (int s2 = b + j; s2 < e; s2 += 8) {
-      const float4 p = pts[s2];
-      x0 = fminf(x0, p.x); x1 = fmaxf(x1, p.x);
-      y0 = fminf(y0, p.y); y1 = fmaxf(y1, p.y);
-      z0 = fminf(z0, p.z); z1 = fmaxf(z1, p.z);
-      t0 = fminf(t0, p.w); t1 = fmaxf(t1, p.w);
+    // 4 loads in flight per lane: a dense cell (hundreds of points) is otherwise a chain of
+    // dependent load round trips on its 8 lanes
+    constexpr int kU = 4;
+    for (int s0 = b + j; s0 < e; s0 += 8 * kU) {
+      float4 pp[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int s2 = s0 + 8 * u;
+        pp[u] = (s2 < e) ? pts[s2] : pts[s0];  // duplicates of a cell point leave the box as is
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const float4 p = pp[u];
+        x0 = fminf(x0, p.x); x1 = fmaxf(x1, p.x);
+        y0 = fminf(y0, p.y); y1 = fmaxf(y1, p.y);
+        z0 = fminf(z0, p.z); z1 = fmaxf(z1, p.z);
+        t0 = fminf(t0, p.w); t1 = fmaxf(t1, p.w);
+      }
     }
 #pragma unroll
     for (int off = 4; off > 0; off >>= 1) {
