@@ -417,9 +417,9 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ 
     }
     float x0 = FLT_MAX, x1 = -FLT_MAX, y0 = FLT_MAX, y1 = -FLT_MAX;
     float z0 = FLT_MAX, z1 = -FLT_MAX, t0 = FLT_MAX, t1 = -FLT_MAX;
-    // 4 loads in flight per lane: a dense cell (hundreds of points) is otherwise a chain of
+    // 8 loads in flight per lane: a dense cell (hundreds of points) is otherwise a chain of
     // dependent load round trips on its 8 lanes
-    constexpr int kU = 4;
+    constexpr int kU = 8;
     for (int s0 = b + j; s0 < e; s0 += 8 * kU) {
       float4 pp[kU];
 #pragma unroll
