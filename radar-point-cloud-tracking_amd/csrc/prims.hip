@@ -4,6 +4,7 @@
 //    histograms so that a pass needs no block-level barriers inside the scatter loop.
 // Plus the library's error plumbing and per-(device, stream) scratch pools.
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <mutex>
 
@@ -27,8 +28,8 @@ const char* last_error_cstr() { return g_last_error.c_str(); }
 
 // ------------------------------------------------------------------ readback wait
 // The path's size readbacks are tiny and the GPU idles until the host has launched the next
-// stage, so the wait polls an event instead of blocking in hipStreamSynchronize (whose wake-up
-// adds tens of microseconds per readback).  One cached event per (thread, device).
+// stage, so the wait polls an event (for up to 200 us, then it blocks) instead of blocking in
+// hipStreamSynchronize right away.  One cached event per (thread, device).
 int32_t wait_stream(hipStream_t st) {
   static thread_local std::vector<hipEvent_t> evs;
   int dev = 0;
@@ -36,11 +37,16 @@ int32_t wait_stream(hipStream_t st) {
   if ((int)evs.size() <= dev) evs.resize(dev + 1, nullptr);
   if (!evs[dev]) RPT_HIP(hipEventCreateWithFlags(&evs[dev], hipEventDisableTiming));
   RPT_HIP(hipEventRecord(evs[dev], st));
+  // poll for up to ~200 us (the readbacks of the path), then block instead of burning a core
+  const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     const hipError_t e = hipEventQuery(evs[dev]);
     if (e == hipSuccess) return RPT_OK;
     if (e != hipErrorNotReady) RPT_HIP(e);
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) break;
   }
+  RPT_HIP(hipEventSynchronize(evs[dev]));
+  return RPT_OK;
 }
 
 // ------------------------------------------------------------------ scratch pool
