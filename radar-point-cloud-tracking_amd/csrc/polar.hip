@@ -341,7 +341,7 @@ __global__ __launch_bounds__(kBlock) void k_group_write_u8(
     const float* __restrict__ sin_t, const int32_t* __restrict__ gain,
     const int64_t* __restrict__ gprefix, const int64_t* __restrict__ file_offsets,
     int files_per_frame, float* __restrict__ x, float* __restrict__ y, float* __restrict__ val,
-    int32_t* __restrict__ gain_out, int32_t* __restrict__ pf_out) {
+    int32_t* __restrict__ gain_out, int32_t* __restrict__ pf_out, int64_t cap) {
   __shared__ uint32_t s_stage[kWavesPerBlock][1024];  // (bin << 8) | sample
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x / 64;
@@ -405,7 +405,10 @@ __global__ __launch_bounds__(kBlock) void k_group_write_u8(
         float* xr = x + o0;
         float* yr = y + o0;
         float* vr = val + o0;
-        for (int l = lane; l < n_emit; l += 64) {
+        // outputs at or beyond cap are dropped: a speculative launch (sized by an earlier run)
+        // is repeated by the caller when the count says it did not fit
+        const int n_fit = (int)max((int64_t)0, min((int64_t)n_emit, cap - o0));
+        for (int l = lane; l < n_fit; l += 64) {
           const uint32_t e = stage[l];
           const float rr = step * (float)(e >> 8);
           xr[l] = rr * ct;
@@ -506,7 +509,7 @@ template <class T>
 int32_t write_impl(const T* echo, int64_t n_files, int rows, int bins, float thr, int stride,
                    RowGeo geo, const int32_t* gain, const int64_t* row_prefix,
                    const int64_t* file_offsets, int fpf, float* x, float* y, float* v,
-                   int32_t* gout, int32_t* pf, hipStream_t st) {
+                   int32_t* gout, int32_t* pf, hipStream_t st, int64_t cap = INT64_MAX) {
   const int64_t n_rows = n_files * rows;
   if ((int64_t)rows * bins >= (int64_t(1) << 32) || n_rows >= (int64_t(1) << 32) || stride < 1 ||
       fpf < 1) {
@@ -523,11 +526,14 @@ int32_t write_impl(const T* echo, int64_t n_files, int rows, int bins, float thr
     if (T8 <= 127)
       hipLaunchKernelGGL(k_group_write_u8<false>, dim3(grid), dim3(kBlock), 0, st, e8,
                          (uint32_t)n_groups, gm, u8_k(T8), stride, geo.scale, geo.cos_t,
-                         geo.sin_t, gain, row_prefix, file_offsets, fpf, x, y, v, gout, pf);
+                         geo.sin_t, gain, row_prefix, file_offsets, fpf, x, y, v, gout, pf, cap);
     else
       hipLaunchKernelGGL(k_group_write_u8<true>, dim3(grid), dim3(kBlock), 0, st, e8,
                          (uint32_t)n_groups, gm, u8_k(T8), stride, geo.scale, geo.cos_t,
-                         geo.sin_t, gain, row_prefix, file_offsets, fpf, x, y, v, gout, pf);
+                         geo.sin_t, gain, row_prefix, file_offsets, fpf, x, y, v, gout, pf, cap);
+  } else if (cap != INT64_MAX) {
+    set_error("rpt_polar_write: a capacity-bounded write needs u8 sweeps of 1024 bins");
+    return RPT_ENOTSUP;
   } else if (grouped_u8(echo, bins)) {
     set_error("rpt_polar_write: u8 sweeps take per-row scale geometry");
     return RPT_ENOTSUP;
@@ -729,6 +735,22 @@ int32_t polar_write(const void* echo, int32_t dt, int64_t n_files, int32_t rows,
                              row_prefix, file_offsets, fpf, x, y, v, gout, pf, st);
   set_error("rpt_polar_write: unknown echo dtype %d", dt);
   return RPT_EINVAL;
+}
+
+// rpt_polar_write into outputs of capacity cap (u8 sweeps of 1024 bins): points at or beyond
+// cap are dropped; the caller compares the count with cap and writes again when it overflowed.
+int32_t polar_write_cap(const uint8_t* echo, int64_t n_files, int32_t rows, float thr,
+                        int32_t stride, const float* scale, const float* cos_t,
+                        const float* sin_t, const int32_t* gain, const int64_t* row_prefix,
+                        const int64_t* file_offsets, int32_t fpf, float* x, float* y, float* v,
+                        int32_t* gout, int32_t* pf, int64_t cap, hipStream_t st) {
+  if (!grouped_u8(echo, 1024)) {
+    set_error("polar_write_cap: u8 sweeps of 1024 bins with 16-B aligned rows only");
+    return RPT_ENOTSUP;
+  }
+  RowGeo geo{scale, nullptr, cos_t, sin_t};
+  return write_impl<uint8_t>(echo, n_files, rows, 1024, thr, stride, geo, gain, row_prefix,
+                             file_offsets, fpf, x, y, v, gout, pf, st, cap);
 }
 
 int32_t sweep_to_points(const float* inten, const float* ranges, const float* cos_t,

@@ -384,6 +384,37 @@ def test_k1_grouped_u8_matches_generic_rows(gpu):
                     np.testing.assert_array_equal(b[i], ref[i])
 
 
+def test_speculative_k1_write_regrows(gpu):
+    """The stack driver queues K1's write with the capacity of the previous run; a denser stack
+    after a sparse one overflows it, and the driver must grow the buffers and write again: same
+    result as a fresh pipeline."""
+    from rpt.pipeline import FrameStackPipeline, PathParams
+    from rpt.synth import DeviceSynth, SynthConfig
+
+    sparse = SynthConfig(n_frames=12, rows=1024, clutter_density=0.002)
+    dense = SynthConfig(n_frames=12, rows=1024, clutter_density=0.03)
+    e_sparse = DeviceSynth(sparse, gpu).echo()
+    ds = DeviceSynth(dense, gpu)
+    e_dense = ds.echo()
+    torch.cuda.synchronize(gpu)
+    pipes = []
+    for _ in range(2):
+        p = FrameStackPipeline(dense.gains, dense.rows, dense.bins, PathParams(), gpu)
+        p.set_geometry(np.full(dense.rows, dense.scale, np.float32), ds.geo.cos_t,
+                       ds.geo.sin_t, dense.n_frames * 3)
+        pipes.append(p)
+    a0 = pipes[0].run(e_sparse, keep_points=True)
+    a = pipes[0].run(e_dense, keep_points=True)   # capacity from the sparse run: regrow
+    b = pipes[1].run(e_dense, keep_points=True)   # fresh
+    assert a.n_points > a0.n_points
+    assert a.n_points == b.n_points
+    for k in a.points:
+        assert torch.equal(a.points[k], b.points[k]), k
+    assert torch.equal(a.labels, b.labels)
+    for k in a.seg:
+        np.testing.assert_array_equal(a.seg[k], b.seg[k])
+
+
 def test_concurrent_lanes_match_single_lane(gpu):
     """Two lanes (two native handles on two streams, submitted from two threads, the library's
     scratch and scan state per stream) give the same results as one lane, run after run: four
