@@ -49,6 +49,18 @@ int32_t land_filter_cells(const float* x, const float* y, const float* v, const 
 int32_t stdbscan(const float* x, const float* y, const float* z, int64_t stride, const float* t,
                  int64_t n, double eps_space, double eps_time, int32_t min_samples,
                  int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st, int dim);
+int32_t stdbscan_deferred(const float* x, const float* y, const float* z, int64_t stride,
+                          const float* t, int64_t n, double eps_space, double eps_time,
+                          int32_t min_samples, int32_t* labels, rpt_stdbscan_stats* stats,
+                          hipStream_t st, int dim, const int32_t** n_clusters_dev,
+                          void** state);
+int32_t stdbscan_fill_stats(void* state, int32_t n_clusters, rpt_stdbscan_stats* stats);
+int32_t cluster_summaries_dev(const int32_t* labels, const float* x, const float* y,
+                              const float* inten, const int32_t* pf, int64_t n, int32_t n_frames,
+                              int bits, int64_t s_hint, int32_t* o_frame, int32_t* o_label,
+                              int64_t* o_count, int64_t* o_first, float* o_cx, float* o_cy,
+                              float* o_mi, int64_t* frame_first_noise,
+                              const int64_t** n_seg_dev, hipStream_t st);
 int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
                           const float* inten, const int32_t* pf, int64_t n, int32_t n_frames,
                           int32_t n_clusters, int32_t* o_frame, int32_t* o_label,
@@ -76,6 +88,58 @@ std::vector<double> arange_edges(float lo, float hi, double res) {
 }
 
 namespace {
+
+// The run's results in one readback without knowing the segment count on the host: header
+// {S, n_clusters} then arrays at offsets fixed by the capacity sc (entries >= S are not written).
+struct SegPack {
+  const int64_t* count;
+  const int64_t* first;
+  const int64_t* noise;
+  const int32_t* frame;
+  const int32_t* label;
+  const float* cx;
+  const float* cy;
+  const float* mi;
+};
+__global__ void k_pack_segs(const int64_t* __restrict__ n_seg, const int32_t* __restrict__ ncl,
+                            SegPack a, int64_t sc, int32_t F, char* __restrict__ out) {
+  const int64_t S = *n_seg;
+  const int64_t m = S < sc ? S : sc;
+  int64_t* hdr = reinterpret_cast<int64_t*>(out);
+  int64_t* count = hdr + 2;
+  int64_t* first = count + sc;
+  int64_t* noise = first + sc;
+  int32_t* frame = reinterpret_cast<int32_t*>(noise + F);
+  int32_t* label = frame + sc;
+  float* cx = reinterpret_cast<float*>(label + sc);
+  float* cy = cx + sc;
+  float* mi = cy + sc;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i0 == 0) {
+    hdr[0] = S;
+    hdr[1] = ncl ? (int64_t)*ncl : -1;
+  }
+  for (int64_t i = i0; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    count[i] = a.count[i];
+    first[i] = a.first[i];
+    frame[i] = a.frame[i];
+    label[i] = a.label[i];
+    cx[i] = a.cx[i];
+    cy[i] = a.cy[i];
+    mi[i] = a.mi[i];
+  }
+  for (int64_t i = i0; i < F; i += (int64_t)gridDim.x * blockDim.x) noise[i] = a.noise[i];
+}
+
+inline size_t seg_pack_bytes(int64_t sc, int32_t F) {
+  return 16 + (size_t)sc * (8 + 8 + 4 + 4 + 4 + 4 + 4) + (size_t)F * 8;
+}
+
+inline int radix_bits_for(int64_t v) {
+  int bits = 1;
+  while ((int64_t(1) << bits) <= v) ++bits;
+  return bits;
+}
 
 template <class T>
 struct DevBuf {
@@ -156,6 +220,8 @@ struct rpt_stack {
   hipEvent_t ev[5] = {};
   bool ev_ok = false;
   hipEvent_t ev_rb = nullptr;  // readback marker of the speculative K1 write
+  int sum_bits = 12;           // radix bits of the K9 label keys, from the previous run
+  int64_t seg_hint = 0;        // segment-count estimate from the previous run
 
   ~rpt_stack() {
     DevBuf<int64_t>* i64[] = {&row_prefix, &file_off, &new_off, &first_noise, &seg_count,
@@ -329,15 +395,19 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
   RPT_TRY(t.ensure(cap2, st));
   RPT_TRY(labels.ensure(cap2, st));
   RPT_TRY(frame_times(cpf, n_in_, nullptr, t.p, st));
+  // ST-DBSCAN and K9 without readbacks in between: the cluster count and the segment count stay
+  // on the device and come back with the results in ONE readback; the K9 sort runs with the
+  // previous run's label bits and the summarize grid with its segment count, and both are
+  // redone (rare) when the counts show they did not fit
   rpt_stdbscan_stats sts{};
   sts.timing = p.timing;
-  RPT_TRY(stdbscan(cx, cy, nullptr, 1, t.p, n_in_, p.eps_space, p.eps_time, p.min_samples,
-                   labels.p, &sts, st, 2));
-  r.n_clusters = sts.n_clusters;
-  r.dbscan = sts;
+  const int32_t* ncl_dev = nullptr;
+  void* dstate = nullptr;
+  RPT_TRY(stdbscan_deferred(cx, cy, nullptr, 1, t.p, n_in_, p.eps_space, p.eps_time,
+                            p.min_samples, labels.p, &sts, st, 2, &ncl_dev, &dstate));
   if (timing) RPT_HIP(hipEventRecord(ev[3], st));
 
-  // ---- K9 summaries (segments ordered by (label, frame)), one packed readback
+  // ---- K9 summaries (segments ordered by (label, frame))
   RPT_TRY(seg_frame.ensure(cap2, st));
   RPT_TRY(seg_label.ensure(cap2, st));
   RPT_TRY(seg_count.ensure(cap2, st));
@@ -346,40 +416,63 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
   RPT_TRY(seg_cy.ensure(cap2, st));
   RPT_TRY(seg_mi.ensure(cap2, st));
   RPT_TRY(first_noise.ensure((size_t)std::max(F, 1), st));
-  int64_t S = 0;
-  RPT_TRY(cluster_summaries(labels.p, cx, cy, cv, cpf, n_in_, F, sts.n_clusters, seg_frame.p,
-                            seg_label.p, seg_count.p, seg_first.p, seg_cx.p, seg_cy.p,
-                            seg_mi.p, first_noise.p, &S, st));
-  r.n_segments = S;
-  const size_t bytes = (size_t)S * (4 + 4 + 8 + 8 + 4 + 4 + 4) + (size_t)F * 8 + 64;
+  const int bits = ncl_dev ? sum_bits : radix_bits_for(sts.n_clusters);
+  const int64_t sc = std::min<int64_t>(
+      std::max<int64_t>(seg_hint > 0 ? seg_hint + seg_hint / 4 + 64 : 4096, 1), n_in_);
+  const int64_t* nseg_dev = nullptr;
+  RPT_TRY(cluster_summaries_dev(labels.p, cx, cy, cv, cpf, n_in_, F, bits, sc, seg_frame.p,
+                                seg_label.p, seg_count.p, seg_first.p, seg_cx.p, seg_cy.p,
+                                seg_mi.p, first_noise.p, &nseg_dev, st));
+  SegPack sp{seg_count.p, seg_first.p, first_noise.p, seg_frame.p,
+             seg_label.p, seg_cx.p,    seg_cy.p,      seg_mi.p};
+  size_t bytes = seg_pack_bytes(sc, F);
+  RPT_TRY(pack_d.ensure(bytes / 4 + 1, st));
   RPT_TRY(down.ensure(bytes, st));
-  char* h = down.p;
-  int64_t* hcount = reinterpret_cast<int64_t*>(h);
-  int64_t* hfirst = hcount + S;
-  int64_t* hnoise = hfirst + S;
-  int32_t* hframe = reinterpret_cast<int32_t*>(hnoise + F);
-  int32_t* hlabel = hframe + S;
-  float* hcx = reinterpret_cast<float*>(hlabel + S);
-  float* hcy = hcx + S;
-  float* hmi = hcy + S;
-  // the same layout packed on the device, then ONE readback
-  PackList pl;
-  pl.add(seg_count.p, sizeof(int64_t) * S);
-  pl.add(seg_first.p, sizeof(int64_t) * S);
-  pl.add(first_noise.p, sizeof(int64_t) * F);
-  pl.add(seg_frame.p, sizeof(int32_t) * S);
-  pl.add(seg_label.p, sizeof(int32_t) * S);
-  pl.add(seg_cx.p, sizeof(float) * S);
-  pl.add(seg_cy.p, sizeof(float) * S);
-  pl.add(seg_mi.p, sizeof(float) * S);
-  const size_t packed = sizeof(uint32_t) * (size_t)pl.off[pl.k];
-  if (packed) {
-    RPT_TRY(pack_d.ensure(packed / sizeof(uint32_t), st));
-    RPT_TRY(pack_arrays(pl, pack_d.p, st));
-    RPT_HIP(hipMemcpyAsync(h, pack_d.p, packed, hipMemcpyDeviceToHost, st));
-  }
+  hipLaunchKernelGGL(k_pack_segs, dim3(grid_for(std::max<int64_t>(sc, F), 256, 256)), dim3(256),
+                     0, st, nseg_dev, ncl_dev, sp, sc, F, reinterpret_cast<char*>(pack_d.p));
+  RPT_CHECK_LAUNCH();
+  RPT_HIP(hipMemcpyAsync(down.p, pack_d.p, bytes, hipMemcpyDeviceToHost, st));
   if (timing) RPT_HIP(hipEventRecord(ev[4], st));
   RPT_TRY(wait_stream(st));
+  int64_t S = reinterpret_cast<const int64_t*>(down.p)[0];
+  const int64_t ncl = ncl_dev ? reinterpret_cast<const int64_t*>(down.p)[1] : sts.n_clusters;
+  if (ncl_dev) RPT_TRY(stdbscan_fill_stats(dstate, (int32_t)ncl, &sts));
+  int64_t sc_used = sc;
+  if ((int64_t(1) << bits) <= ncl || S > sc) {
+    // the label keys needed more bits, or more segments than the readback holds: K9 again
+    // with the exact counts, then a readback of exactly S
+    if ((int64_t(1) << bits) <= ncl)
+      RPT_TRY(cluster_summaries_dev(labels.p, cx, cy, cv, cpf, n_in_, F, radix_bits_for(ncl), S,
+                                    seg_frame.p, seg_label.p, seg_count.p, seg_first.p,
+                                    seg_cx.p, seg_cy.p, seg_mi.p, first_noise.p, &nseg_dev, st));
+    sc_used = std::max<int64_t>(S, 1);
+    bytes = seg_pack_bytes(sc_used, F);
+    RPT_TRY(pack_d.ensure(bytes / 4 + 1, st));
+    RPT_TRY(down.ensure(bytes, st));
+    hipLaunchKernelGGL(k_pack_segs, dim3(grid_for(std::max<int64_t>(sc_used, F), 256, 256)),
+                       dim3(256), 0, st, nseg_dev, ncl_dev, sp, sc_used, F,
+                       reinterpret_cast<char*>(pack_d.p));
+    RPT_CHECK_LAUNCH();
+    RPT_HIP(hipMemcpyAsync(down.p, pack_d.p, bytes, hipMemcpyDeviceToHost, st));
+    RPT_TRY(wait_stream(st));
+    S = reinterpret_cast<const int64_t*>(down.p)[0];
+  }
+  // next run's guesses: one pass of up to 12 bits when the count allows, with headroom
+  const int exact = radix_bits_for(ncl);
+  sum_bits = std::max(exact, std::min(radix_bits_for(2 * ncl + 64), std::max(exact, 12)));
+  seg_hint = S;
+  r.n_clusters = (int32_t)ncl;
+  r.dbscan = sts;
+  r.n_segments = S;
+  const char* h = down.p + 16;
+  const int64_t* hcount = reinterpret_cast<const int64_t*>(h);
+  const int64_t* hfirst = hcount + sc_used;
+  const int64_t* hnoise = hfirst + sc_used;
+  const int32_t* hframe = reinterpret_cast<const int32_t*>(hnoise + F);
+  const int32_t* hlabel = hframe + sc_used;
+  const float* hcx = reinterpret_cast<const float*>(hlabel + sc_used);
+  const float* hcy = hcx + sc_used;
+  const float* hmi = hcy + sc_used;
   h_count.assign(hcount, hcount + S);
   h_first.assign(hfirst, hfirst + S);
   h_noise.assign(hnoise, hnoise + F);

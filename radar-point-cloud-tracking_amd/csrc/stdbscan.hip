@@ -1640,6 +1640,10 @@ struct DbscanState {
   int32_t core_pass(hipStream_t st);
   int32_t union_pass(hipStream_t st);
   int32_t labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st);
+  // deferred mode: labels_local leaves the cluster count on the device (cid[n]) and the timing
+  // events unread; fill_stats completes the stats once the caller has synchronised the stream
+  bool defer = false;
+  int32_t fill_stats(int32_t n_clusters, rpt_stdbscan_stats* stats);
   int32_t labels_global(const int64_t* rep_orig, const int64_t* reps, int64_t nr,
                         int32_t* labels, hipStream_t st);
 };
@@ -1924,10 +1928,18 @@ int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hi
                        nc_count, labels);
   RPT_CHECK_LAUNCH();
   tm.mark();
+  if (stats && defer) return RPT_OK;  // fill_stats after the caller's sync
   if (stats) {
     int32_t ncl = 0;
     RPT_HIP(hipMemcpyAsync(&ncl, cid + n, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     RPT_TRY(wait_stream(st));
+    RPT_TRY(fill_stats(ncl, stats));
+  }
+  return RPT_OK;
+}
+
+int32_t DbscanState::fill_stats(int32_t ncl, rpt_stdbscan_stats* stats) {
+  {
     stats->n_points = n;
     stats->n_clusters = ncl;
     stats->n_core = -1;
@@ -2022,6 +2034,49 @@ int32_t stdbscan(const float* x, const float* y, const float* z, int64_t stride,
   RPT_TRY(S->core_pass(st));
   RPT_TRY(S->union_pass(st));
   return S->labels_local(labels, stats, st);
+}
+
+// The fused path without its readbacks (the native stack driver): the cluster count stays on the
+// device at *n_clusters_dev (nullptr when the parameters are degenerate: stats is then complete)
+// and stdbscan_fill_stats completes stats after the caller has synchronised the stream.
+int32_t stdbscan_deferred(const float* x, const float* y, const float* z, int64_t stride,
+                          const float* t, int64_t n, double eps_space, double eps_time,
+                          int32_t min_samples, int32_t* labels, rpt_stdbscan_stats* stats,
+                          hipStream_t st, int dim, const int32_t** n_clusters_dev,
+                          void** state) {
+  RPT_TRY(check_args(x, y, z, stride, t, n, dim));
+  if (!labels || !stats || !n_clusters_dev || !state) {
+    set_error("stdbscan_deferred: null argument");
+    return RPT_EINVAL;
+  }
+  int dev = 0;
+  RPT_HIP(hipGetDevice(&dev));
+  DbscanState* S;
+  {
+    std::lock_guard<std::mutex> lk(g_state_mu);
+    S = nullptr;
+    for (auto& e : g_states)
+      if (e.first.first == dev && e.first.second == st) S = e.second;
+    if (!S) {
+      S = new DbscanState();
+      g_states.push_back({{dev, st}, S});
+    }
+  }
+  RPT_TRY(S->build(x, y, z, stride, t, n, eps_space, eps_time, min_samples, stats->timing != 0,
+                   st));
+  RPT_TRY(S->core_pass(st));
+  RPT_TRY(S->union_pass(st));
+  S->defer = !S->degenerate;
+  const int32_t s_ = S->labels_local(labels, stats, st);
+  *n_clusters_dev = S->defer ? S->cid + S->n : nullptr;
+  *state = S;
+  return s_;
+}
+
+int32_t stdbscan_fill_stats(void* state, int32_t n_clusters, rpt_stdbscan_stats* stats) {
+  DbscanState* S = static_cast<DbscanState*>(state);
+  S->defer = false;
+  return S->fill_stats(n_clusters, stats);
 }
 
 // ---- phased C-ABI bodies

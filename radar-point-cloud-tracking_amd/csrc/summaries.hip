@@ -16,6 +16,8 @@
 // frame within the noise run (no atomics).
 #include <climits>
 
+#include <algorithm>
+
 #include "common.h"
 
 #pragma clang fp contract(off)
@@ -289,12 +291,13 @@ __device__ __forceinline__ float mean_intensity(const float* __restrict__ gi, in
 // the mean intensity (lane-parallel), so no other work sits in the chains' instruction streams.
 __global__ __launch_bounds__(kBlock) void k_summarize(
     const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
-    const int64_t* __restrict__ seg_start, int64_t n_seg, int64_t n,
+    const int64_t* __restrict__ seg_start, const int64_t* __restrict__ n_seg_dev, int64_t n,
     const float* __restrict__ gx, const float* __restrict__ gy, const float* __restrict__ gi,
     const int32_t* __restrict__ pf, int32_t* __restrict__ o_frame, int32_t* __restrict__ o_label,
     int64_t* __restrict__ o_count, int64_t* __restrict__ o_first, float* __restrict__ o_cx,
     float* __restrict__ o_cy, float* __restrict__ o_mi) {
   __shared__ float s_buf[kBlock / 64][1024];
+  const int64_t n_seg = *n_seg_dev;  // the segment count stays on the device (no readback)
   const int lane = threadIdx.x & 63;
   const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
   const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
@@ -335,16 +338,14 @@ __global__ void k_fill_i64(int64_t* p, int64_t n, int64_t v) {
 
 }  // namespace
 
-int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
-                          const float* inten, const int32_t* pf, int64_t n, int32_t n_frames,
-                          int32_t n_clusters, int32_t* o_frame, int32_t* o_label,
-                          int64_t* o_count, int64_t* o_first, float* o_cx, float* o_cy,
-                          float* o_mi, int64_t* frame_first_noise, int64_t* n_seg_host,
-                          hipStream_t st) {
-  if (n < 0 || n_frames < 0 || n_clusters < 0 || !n_seg_host) {
-    set_error("rpt_cluster_summaries: bad arguments");
-    return RPT_EINVAL;
-  }
+// bits: radix bits of the label keys (label + 1 < 2^bits); s_hint: expected segment count (sizes
+// the summarize grid, which loops over the device count); *n_seg_dev: the count, on the device.
+static int32_t summaries_impl(const int32_t* labels, const float* x, const float* y,
+                              const float* inten, const int32_t* pf, int64_t n, int32_t n_frames,
+                              int bits, int64_t s_hint, int32_t* o_frame, int32_t* o_label,
+                              int64_t* o_count, int64_t* o_first, float* o_cx, float* o_cy,
+                              float* o_mi, int64_t* frame_first_noise,
+                              const int64_t** n_seg_dev, hipStream_t st) {
   if (n >= (int64_t(1) << 31) - 1) {
     set_error("rpt_cluster_summaries: n exceeds the int32 index space");
     return RPT_ENOTSUP;
@@ -373,35 +374,72 @@ int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
     hipLaunchKernelGGL(k_fill_i64, dim3(grid_for(n_frames, 256, 64)), dim3(256), 0, st,
                        frame_first_noise, (int64_t)n_frames, (int64_t)-1);
   if (n == 0) {
-    *n_seg_host = 0;
+    RPT_HIP(hipMemsetAsync(pos, 0, sizeof(int64_t), st));
+    *n_seg_dev = pos;
     RPT_CHECK_LAUNCH();
     return RPT_OK;
   }
   const int g = grid_for(n, kBlock, 8192);
   hipLaunchKernelGGL(k_sum_keys, dim3(g), dim3(kBlock), 0, st, labels, n, keys, vals);
   RPT_CHECK_LAUNCH();
-  int bits = 1;
-  while ((int64_t(1) << bits) <= (int64_t)n_clusters) ++bits;
   uint32_t *sk, *sv;
   RPT_TRY(radix_sort_pairs(keys, vals, ka, va, n, bits, rtmp, &sk, &sv, st));
   hipLaunchKernelGGL(k_heads, dim3(g), dim3(kBlock), 0, st, sk, sv, pf, n, head,
                      frame_first_noise);
   RPT_TRY(exclusive_scan_total_i32_to_i64(head, pos, n, st));
   hipLaunchKernelGGL(k_seg_starts, dim3(g), dim3(kBlock), 0, st, head, pos, n, seg_start);
+  hipLaunchKernelGGL(k_gather_runs, dim3(g), dim3(kBlock), 0, st, sv, n, x, y, inten, gx, gy, gi);
+  const int64_t sh = std::max<int64_t>(1, std::min<int64_t>(s_hint, n));
+  hipLaunchKernelGGL(k_summarize, dim3(grid_for(3 * sh, kBlock / 64, 16384)), dim3(kBlock), 0, st,
+                     sk, sv, seg_start, pos + n, n, gx, gy, gi, pf, o_frame, o_label, o_count,
+                     o_first, o_cx, o_cy, o_mi);
   RPT_CHECK_LAUNCH();
-  int64_t n_seg = 0;
-  RPT_HIP(hipMemcpyAsync(&n_seg, pos + n, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-  RPT_TRY(wait_stream(st));
-  if (n_seg > 0) {
-    hipLaunchKernelGGL(k_gather_runs, dim3(g), dim3(kBlock), 0, st, sv, n, x, y, inten, gx, gy,
-                       gi);
-    hipLaunchKernelGGL(k_summarize, dim3(grid_for(3 * n_seg, kBlock / 64, 16384)), dim3(kBlock),
-                       0, st, sk, sv, seg_start, n_seg, n, gx, gy, gi, pf, o_frame, o_label,
-                       o_count, o_first, o_cx, o_cy, o_mi);
-    RPT_CHECK_LAUNCH();
+  *n_seg_dev = pos + n;
+  return RPT_OK;
+}
+
+static int radix_bits_for(int64_t n_clusters) {
+  int bits = 1;
+  while ((int64_t(1) << bits) <= n_clusters) ++bits;
+  return bits;
+}
+
+int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
+                          const float* inten, const int32_t* pf, int64_t n, int32_t n_frames,
+                          int32_t n_clusters, int32_t* o_frame, int32_t* o_label,
+                          int64_t* o_count, int64_t* o_first, float* o_cx, float* o_cy,
+                          float* o_mi, int64_t* frame_first_noise, int64_t* n_seg_host,
+                          hipStream_t st) {
+  if (n < 0 || n_frames < 0 || n_clusters < 0 || !n_seg_host) {
+    set_error("rpt_cluster_summaries: bad arguments");
+    return RPT_EINVAL;
   }
+  // the summarize grid is sized for one wave per run component once the count is known
+  const int64_t* nd = nullptr;
+  RPT_TRY(summaries_impl(labels, x, y, inten, pf, n, n_frames, radix_bits_for(n_clusters),
+                         (int64_t)n_clusters * std::max(n_frames, 1) + 1, o_frame, o_label,
+                         o_count, o_first, o_cx, o_cy, o_mi, frame_first_noise, &nd, st));
+  int64_t n_seg = 0;
+  RPT_HIP(hipMemcpyAsync(&n_seg, nd, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  RPT_TRY(wait_stream(st));
   *n_seg_host = n_seg;
   return RPT_OK;
+}
+
+// No readback: the caller passes the radix bits and a segment-count estimate, and reads the
+// count (*n_seg_dev) with its other results after one sync.
+int32_t cluster_summaries_dev(const int32_t* labels, const float* x, const float* y,
+                              const float* inten, const int32_t* pf, int64_t n, int32_t n_frames,
+                              int bits, int64_t s_hint, int32_t* o_frame, int32_t* o_label,
+                              int64_t* o_count, int64_t* o_first, float* o_cx, float* o_cy,
+                              float* o_mi, int64_t* frame_first_noise,
+                              const int64_t** n_seg_dev, hipStream_t st) {
+  if (n < 0 || n_frames < 0 || bits < 1 || bits > 32 || !n_seg_dev) {
+    set_error("cluster_summaries_dev: bad arguments");
+    return RPT_EINVAL;
+  }
+  return summaries_impl(labels, x, y, inten, pf, n, n_frames, bits, s_hint, o_frame, o_label,
+                        o_count, o_first, o_cx, o_cy, o_mi, frame_first_noise, n_seg_dev, st);
 }
 
 }  // namespace rpt
