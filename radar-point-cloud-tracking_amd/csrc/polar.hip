@@ -553,7 +553,9 @@ int32_t write_impl(const T* echo, int64_t n_files, int rows, int bins, float thr
 }
 
 __global__ void k_frame_times(const int32_t* __restrict__ pf, int64_t n,
-                              const int64_t* __restrict__ ids, float* __restrict__ t) {
+                              const int64_t* __restrict__ ids, float* __restrict__ t,
+                              const int64_t* __restrict__ n_dev) {
+  if (n_dev) n = *n_dev;  // count on the device (at most the host n the grid was sized for)
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t f = pf[i];
@@ -788,7 +790,18 @@ int32_t sweep_to_points(const float* inten, const float* ranges, const float* co
 
 int32_t frame_times(const int32_t* pf, int64_t n, const int64_t* ids, float* t, hipStream_t st) {
   if (n == 0) return RPT_OK;
-  hipLaunchKernelGGL(k_frame_times, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, pf, n, ids, t);
+  hipLaunchKernelGGL(k_frame_times, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, pf, n, ids, t,
+                     (const int64_t*)nullptr);
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
+}
+
+// n_dev: the count on the device, <= n_max
+int32_t frame_times_dev(const int32_t* pf, int64_t n_max, const int64_t* n_dev, float* t,
+                        hipStream_t st) {
+  if (n_max == 0) return RPT_OK;
+  hipLaunchKernelGGL(k_frame_times, dim3(grid_for(n_max, 256, 8192)), dim3(256), 0, st, pf,
+                     n_max, (const int64_t*)nullptr, t, n_dev);
   RPT_CHECK_LAUNCH();
   return RPT_OK;
 }

@@ -53,7 +53,13 @@ int32_t stdbscan_deferred(const float* x, const float* y, const float* z, int64_
                           const float* t, int64_t n, double eps_space, double eps_time,
                           int32_t min_samples, int32_t* labels, rpt_stdbscan_stats* stats,
                           hipStream_t st, int dim, const int32_t** n_clusters_dev,
-                          void** state);
+                          void** state, const void* host_bounds);
+size_t stdbscan_bounds_bytes();
+size_t stdbscan_bounds_part_bytes(int64_t n_max);
+int32_t stdbscan_bounds_dev(const float* x, const float* y, const float* t, int64_t n_max,
+                            const int64_t* n_dev, void* out_dev, void* part_dev, hipStream_t st);
+int32_t frame_times_dev(const int32_t* pf, int64_t n_max, const int64_t* n_dev, float* t,
+                        hipStream_t st);
 int32_t stdbscan_fill_stats(void* state, int32_t n_clusters, rpt_stdbscan_stats* stats);
 int32_t cluster_summaries_dev(const int32_t* labels, const float* x, const float* y,
                               const float* inten, const int32_t* pf, int64_t n, int32_t n_frames,
@@ -209,6 +215,8 @@ struct rpt_stack {
   DevBuf<int32_t> g, pf, g2, pf2, labels, land_cnt, land_cell, seg_frame, seg_label;
   DevBuf<double> land_tot, edges;
   DevBuf<uint8_t> land_mask;
+  DevBuf<uint8_t> bnd;                 // ST-DBSCAN bounds (+ partials) of the kept points
+  std::vector<char> dbscan_bounds;     // their host copy, from the land readback
   PinnedBuf up, down;  // host staging: uploads (edges, offsets), readbacks
   std::vector<int64_t> fo_k1, fo_in;
   std::vector<int32_t> h_frame, h_label;
@@ -235,6 +243,7 @@ struct rpt_stack {
     land_tot.release();
     edges.release();
     pack_d.release();
+    bnd.release();
     land_mask.release();
     up.release();
     down.release();
@@ -365,17 +374,29 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
     RPT_TRY(land_filter_cells(x.p, y.p, v.p, gain ? g.p : nullptr, pf.p, N, fo_dev, F, edges.p,
                               nxe, edges.p + nxe, nye, land_mask.p, land_cell.p, x2.p, y2.p,
                               v2.p, gain ? g2.p : nullptr, pf2.p, new_off.p, nullptr, st));
+    // frame times and the ST-DBSCAN bounds of the kept points (their count new_off[F] stays on
+    // the device), read back with the offsets and the land-cell count: ONE round trip
+    const int64_t* kept_dev = new_off.p + F;
+    RPT_TRY(t.ensure(cap, st));
+    RPT_TRY(frame_times_dev(pf2.p, N, kept_dev, t.p, st));
+    const size_t bnd_bytes = stdbscan_bounds_bytes();
+    RPT_TRY(bnd.ensure(stdbscan_bounds_part_bytes(N) + 2 * bnd_bytes, st));
+    RPT_TRY(stdbscan_bounds_dev(x2.p, y2.p, t.p, N, kept_dev, bnd.p, bnd.p + 2 * bnd_bytes, st));
     int64_t* hn = reinterpret_cast<int64_t*>(down.p);
     PackList pl;
     pl.add(new_off.p, sizeof(int64_t) * (F + 1));
     pl.add(scal.p, sizeof(int64_t));
+    pl.add(bnd.p, bnd_bytes);
     RPT_TRY(pack_d.ensure((size_t)pl.off[pl.k], st));
     RPT_TRY(pack_arrays(pl, pack_d.p, st));
-    RPT_HIP(hipMemcpyAsync(hn, pack_d.p, sizeof(int64_t) * (F + 2), hipMemcpyDeviceToHost, st));
+    RPT_HIP(hipMemcpyAsync(hn, pack_d.p, sizeof(uint32_t) * (size_t)pl.off[pl.k],
+                           hipMemcpyDeviceToHost, st));
     RPT_TRY(wait_stream(st));
     fo_in.assign(hn, hn + F + 1);
     n_in_ = hn[F];
     r.n_land_cells = hn[F + 1];
+    dbscan_bounds.assign(reinterpret_cast<const char*>(hn + F + 2),
+                         reinterpret_cast<const char*>(hn + F + 2) + bnd_bytes);
     cx = x2.p;
     cy = y2.p;
     cv = v2.p;
@@ -392,9 +413,11 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
 
   // ---- ST-DBSCAN over the stack (times = frame slot as float32, :460-467)
   const size_t cap2 = (size_t)n_in_;
-  RPT_TRY(t.ensure(cap2, st));
   RPT_TRY(labels.ensure(cap2, st));
-  RPT_TRY(frame_times(cpf, n_in_, nullptr, t.p, st));
+  if (!land_applied) {  // with the land filter, the times and bounds came with its readback
+    RPT_TRY(t.ensure(cap2, st));
+    RPT_TRY(frame_times(cpf, n_in_, nullptr, t.p, st));
+  }
   // ST-DBSCAN and K9 without readbacks in between: the cluster count and the segment count stay
   // on the device and come back with the results in ONE readback; the K9 sort runs with the
   // previous run's label bits and the summarize grid with its segment count, and both are
@@ -404,7 +427,8 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
   const int32_t* ncl_dev = nullptr;
   void* dstate = nullptr;
   RPT_TRY(stdbscan_deferred(cx, cy, nullptr, 1, t.p, n_in_, p.eps_space, p.eps_time,
-                            p.min_samples, labels.p, &sts, st, 2, &ncl_dev, &dstate));
+                            p.min_samples, labels.p, &sts, st, 2, &ncl_dev, &dstate,
+                            land_applied ? dbscan_bounds.data() : nullptr));
   if (timing) RPT_HIP(hipEventRecord(ev[3], st));
 
   // ---- K9 summaries (segments ordered by (label, frame))

@@ -76,7 +76,9 @@ __global__ __launch_bounds__(kBlock) void k_bounds(const float* __restrict__ x,
                                                   const float* __restrict__ y,
                                                   const float* __restrict__ z, int64_t stride,
                                                   const float* __restrict__ t, int64_t n,
-                                                  Bounds* __restrict__ out) {
+                                                  Bounds* __restrict__ out,
+                                                  const int64_t* __restrict__ n_dev = nullptr) {
+  if (n_dev) n = *n_dev;  // count on the device (at most the host n the grid was sized for)
   uint32_t mn[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
   uint32_t mx[4] = {0u, 0u, 0u, 0u};
   int nonfin = 0, nonint = 0, nfin = 0;
@@ -1634,6 +1636,7 @@ struct DbscanState {
   template <int D>
   int32_t build_t(const float* x, const float* y, const float* z, int64_t stride, const float* t,
                   double eps_space, double eps_time, hipStream_t st);
+  const void* given_bounds = nullptr;  // host Bounds computed by the caller (stdbscan_bounds_dev)
   int32_t build(const float* x, const float* y, const float* z, int64_t stride, const float* t,
                 int64_t n_, double eps_space, double eps_time, int32_t ms, bool timing,
                 hipStream_t st);
@@ -1662,12 +1665,17 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   }
   Bounds* d_b = arena.carve_n<Bounds>(1);
   Bounds* d_part = arena.carve_n<Bounds>(nbb);
-  hipLaunchKernelGGL(k_bounds<D>, dim3(nbb), dim3(kBlock), 0, st, x, y, z, stride, t, n, d_part);
-  hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(kBlock), 0, st, d_part, nbb, d_b);
-  RPT_CHECK_LAUNCH();
   Bounds hb;
-  RPT_HIP(hipMemcpyAsync(&hb, d_b, sizeof(Bounds), hipMemcpyDeviceToHost, st));
-  RPT_TRY(wait_stream(st));
+  if (given_bounds) {  // the caller read them back with its own results
+    std::memcpy(&hb, given_bounds, sizeof(Bounds));
+  } else {
+    hipLaunchKernelGGL(k_bounds<D>, dim3(nbb), dim3(kBlock), 0, st, x, y, z, stride, t, n,
+                       d_part, (const int64_t*)nullptr);
+    hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(kBlock), 0, st, d_part, nbb, d_b);
+    RPT_CHECK_LAUNCH();
+    RPT_HIP(hipMemcpyAsync(&hb, d_b, sizeof(Bounds), hipMemcpyDeviceToHost, st));
+    RPT_TRY(wait_stream(st));
+  }
   tm.mark();
   if (hb.nonfinite_xyz) {
     set_error("Input contains NaN or infinity in coordinates");
@@ -2039,11 +2047,30 @@ int32_t stdbscan(const float* x, const float* y, const float* z, int64_t stride,
 // The fused path without its readbacks (the native stack driver): the cluster count stays on the
 // device at *n_clusters_dev (nullptr when the parameters are degenerate: stats is then complete)
 // and stdbscan_fill_stats completes stats after the caller has synchronised the stream.
+// Bounds of the 2-D points [0, *n_dev) (n_dev on the device, <= n_max) into out_dev
+// (stdbscan_bounds_bytes(), device): what stdbscan_deferred's build would compute, for a caller
+// that reads them back together with its own results.
+size_t stdbscan_bounds_bytes() { return sizeof(Bounds); }
+int32_t stdbscan_bounds_dev(const float* x, const float* y, const float* t, int64_t n_max,
+                            const int64_t* n_dev, void* out_dev, void* part_dev,
+                            hipStream_t st) {
+  const int nbb = grid_for(std::max<int64_t>(n_max, 1), kBlock, 1024);
+  hipLaunchKernelGGL(k_bounds<2>, dim3(nbb), dim3(kBlock), 0, st, x, y, (const float*)nullptr,
+                     (int64_t)1, t, n_max, static_cast<Bounds*>(part_dev), n_dev);
+  hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(kBlock), 0, st,
+                     static_cast<const Bounds*>(part_dev), nbb, static_cast<Bounds*>(out_dev));
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
+}
+size_t stdbscan_bounds_part_bytes(int64_t n_max) {
+  return sizeof(Bounds) * (size_t)grid_for(std::max<int64_t>(n_max, 1), kBlock, 1024);
+}
+
 int32_t stdbscan_deferred(const float* x, const float* y, const float* z, int64_t stride,
                           const float* t, int64_t n, double eps_space, double eps_time,
                           int32_t min_samples, int32_t* labels, rpt_stdbscan_stats* stats,
                           hipStream_t st, int dim, const int32_t** n_clusters_dev,
-                          void** state) {
+                          void** state, const void* host_bounds) {
   RPT_TRY(check_args(x, y, z, stride, t, n, dim));
   if (!labels || !stats || !n_clusters_dev || !state) {
     set_error("stdbscan_deferred: null argument");
@@ -2062,8 +2089,11 @@ int32_t stdbscan_deferred(const float* x, const float* y, const float* z, int64_
       g_states.push_back({{dev, st}, S});
     }
   }
-  RPT_TRY(S->build(x, y, z, stride, t, n, eps_space, eps_time, min_samples, stats->timing != 0,
-                   st));
+  S->given_bounds = host_bounds;
+  const int32_t sb = S->build(x, y, z, stride, t, n, eps_space, eps_time, min_samples,
+                              stats->timing != 0, st);
+  S->given_bounds = nullptr;
+  RPT_TRY(sb);
   RPT_TRY(S->core_pass(st));
   RPT_TRY(S->union_pass(st));
   S->defer = !S->degenerate;
