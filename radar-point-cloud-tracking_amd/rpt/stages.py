@@ -83,13 +83,12 @@ class HipOps:
         n_rows = n_files * rows
         row_prefix = ws.get(prefix + "row_prefix", n_rows + 1, torch.int64)
         file_off = ws.get(prefix + "file_off", n_files + 1, torch.int64)
-        total = _abi.C.c_int64(0)
         thr = float(np.float32(threshold))
         _abi.check(lib.rpt_polar_count(echo.data_ptr(), dt, n_files, rows, bins, thr, stride,
-                                       row_prefix.data_ptr(), file_off.data_ptr(),
-                                       _abi.C.byref(total), self.st()), "rpt_polar_count")
-        N = int(total.value)
-        foff = file_off.cpu().numpy()
+                                       row_prefix.data_ptr(), file_off.data_ptr(), None,
+                                       self.st()), "rpt_polar_count")
+        foff = file_off.cpu().numpy()   # one readback: the offsets end with the total
+        N = int(foff[-1])
         x = ws.get(prefix + "x", N, torch.float32)
         y = ws.get(prefix + "y", N, torch.float32)
         v = ws.get(prefix + "v", N, torch.float32)
@@ -123,14 +122,17 @@ class HipOps:
                                           tot.data_ptr(), self.st()), "rpt_land_grid")
         return cnt, tot
 
-    def land_apply(self, pts: Points, cnt, tot, num_frames: int, xe, ye):
+    def land_apply(self, pts: Points, cnt, tot, num_frames: int, xe, ye,
+                   want_land_cells: bool = False):
+        """Land mask + compaction; the land-cell count (a readback) only when asked for."""
         cells = cnt.numel()
         mask = self.ws.get("land_mask", cells, torch.uint8)
         nl = _abi.C.c_int64(0)
         _abi.check(self.lib.rpt_land_mask(cnt.data_ptr(), tot.data_ptr(), cells, num_frames,
                                           LAND_PERSISTENCE_THRESHOLD, float(LAND_MIN_INTENSITY),
-                                          mask.data_ptr(), _abi.C.byref(nl), self.st()),
-                   "rpt_land_mask")
+                                          mask.data_ptr(),
+                                          _abi.C.byref(nl) if want_land_cells else None,
+                                          self.st()), "rpt_land_mask")
         N, F = pts.n, len(pts.frame_off) - 1
         ws = self.ws
         out = [ws.get("x2", N, torch.float32), ws.get("y2", N, torch.float32),
@@ -138,14 +140,14 @@ class HipOps:
                ws.get("pf2", N, torch.int32)]
         fo_d = torch.from_numpy(pts.frame_off.astype(np.int64)).to(self.dev)
         nfo = ws.get("new_frame_off", F + 1, torch.int64)
-        kept = _abi.C.c_int64(0)
         _abi.check(self.lib.rpt_land_filter(
             pts.x.data_ptr(), pts.y.data_ptr(), pts.v.data_ptr(), pts.g.data_ptr(),
             pts.pf.data_ptr(), N, fo_d.data_ptr(), F, self._xe.data_ptr(), len(xe),
             self._ye.data_ptr(), len(ye), mask.data_ptr(), *[o.data_ptr() for o in out],
-            nfo.data_ptr(), _abi.C.byref(kept), self.st()), "rpt_land_filter")
-        k = int(kept.value)
-        return Points(*[o[:k] for o in out], nfo.cpu().numpy()), int(nl.value)
+            nfo.data_ptr(), None, self.st()), "rpt_land_filter")
+        nfo_h = nfo.cpu().numpy()        # one readback: the new offsets end with the kept count
+        k = int(nfo_h[-1])
+        return Points(*[o[:k] for o in out], nfo_h), int(nl.value)
 
     def frame_times(self, pts: Points, frame0: int, name="t") -> torch.Tensor:
         t = self.ws.get(name, pts.n, torch.float32)
