@@ -632,18 +632,31 @@ constexpr int kItems = 16;
 struct AppendIndex {
   __device__ int32_t operator()(int64_t s) const { return (int32_t)s; }
 };
+// Same, with this thread's predicate bits already known (bit k <-> index tile0 + k*kBlock + tid).
+template <class V = AppendIndex>
+__device__ __forceinline__ void block_append_bits(int64_t tile0, uint32_t bits,
+                                                  int32_t* __restrict__ list,
+                                                  int32_t* __restrict__ counter, V value = V{});
+
 template <class P, class V = AppendIndex>
 __device__ __forceinline__ void block_append(int64_t tile0, int64_t n, P&& pred,
                                              int32_t* __restrict__ list,
                                              int32_t* __restrict__ counter, V value = V{}) {
-  __shared__ int s_wsum[kBlock / 64];
-  __shared__ int s_base;
   uint32_t bits = 0;
 #pragma unroll
   for (int k = 0; k < kItems; ++k) {
     const int64_t s = tile0 + (int64_t)k * kBlock + threadIdx.x;
     if (s < n && pred(s)) bits |= 1u << k;
   }
+  block_append_bits(tile0, bits, list, counter, value);
+}
+
+template <class V>
+__device__ __forceinline__ void block_append_bits(int64_t tile0, uint32_t bits,
+                                                  int32_t* __restrict__ list,
+                                                  int32_t* __restrict__ counter, V value) {
+  __shared__ int s_wsum[kBlock / 64];
+  __shared__ int s_base;
   const int c = __popc(bits);
   // block exclusive scan of c
   const int lane = threadIdx.x & 63, w = threadIdx.x / 64;
@@ -906,7 +919,11 @@ __global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
                                                           const uint8_t* __restrict__ mutual,
                                                           const uint32_t* __restrict__ occ_bits,
                                                           const float2* __restrict__ slab_t,
-                                                          int32_t* __restrict__ cflag) {
+                                                          int32_t* __restrict__ cflag,
+                                                          int32_t* __restrict__ zero_counter) {
+  // the level-4 queue counter, zeroed here instead of by a memset launch (k_core_fill, the next
+  // kernel on the stream, is its first user)
+  if (blockIdx.x == 0 && threadIdx.x == 0) *zero_counter = 0;
   const int64_t no = *n_occ;
   const int need = g.min_samples;
   const int j = threadIdx.x & 7;
@@ -995,14 +1012,25 @@ __global__ __launch_bounds__(kBlock) void k_core_fill(const int32_t* __restrict_
                                                      int32_t* __restrict__ n_slow) {
   for (int64_t tile = (int64_t)blockIdx.x * kBlock * kItems; tile < n;
        tile += (int64_t)gridDim.x * kBlock * kItems) {
-    block_append(
-        tile, n,
-        [&](int64_t s) -> bool {
-          const int f = cflag[skey[s]];
-          core[s] = (f == 1) ? 1 : 0;
-          return f == 2;
-        },
-        slow, n_slow);
+    // all keys, then all cell flags, in flight together (two rounds of memory latency per tile,
+    // not two per item)
+    int32_t key[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const int64_t s = tile + (int64_t)k * kBlock + threadIdx.x;
+      key[k] = (s < n) ? skey[s] : -1;
+    }
+    int f[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) f[k] = (key[k] >= 0) ? cflag[key[k]] : 0;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const int64_t s = tile + (int64_t)k * kBlock + threadIdx.x;
+      if (s < n) core[s] = (f[k] == 1) ? 1 : 0;
+      bits |= (f[k] == 2) ? (1u << k) : 0u;
+    }
+    block_append_bits(tile, bits, slow, n_slow);
   }
 }
 
@@ -1832,13 +1860,14 @@ int32_t DbscanState::core_pass(hipStream_t st) {
   int32_t* slow = nc_list;
   int32_t* n_slow = nc_list + n;
   const int32_t* n_occ = hpos + n;
-  RPT_HIP(hipMemsetAsync(n_slow, 0, sizeof(int32_t), st));
   // slabs each side a cell's points can reach: eps_t / slab width, +1 for the slab's extent
   const double rs = std::ceil((double)g.epst / g.ct) + 1.0;
   if (dim == 2 && rs <= (double)kCwMaxR && g.nz == 1) {
     hipLaunchKernelGGL(k_core_cells_oct, dim3(grid_for(8 * n, kBlock, 8192)), dim3(kBlock), 0,
-                       st, g, (int)rs, occ, n_occ, rec<2>(), mutual, occ_bits, slab_t, cflag);
+                       st, g, (int)rs, occ, n_occ, rec<2>(), mutual, occ_bits, slab_t, cflag,
+                       n_slow);
   } else {
+    RPT_HIP(hipMemsetAsync(n_slow, 0, sizeof(int32_t), st));
     RPT_HIP(hipMemsetAsync(n_cq, 0, sizeof(int32_t), st));
     hipLaunchKernelGGL(k_core_cell_fast, dim3(tile_grid(n)), dim3(kBlock), 0, st, occ, n_occ, g,
                        cell_start, mutual, cflag, cq, n_cq);
