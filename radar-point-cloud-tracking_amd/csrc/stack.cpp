@@ -66,7 +66,7 @@ int32_t cluster_summaries_dev(const int32_t* labels, const float* x, const float
                               int bits, int64_t s_hint, int32_t* o_frame, int32_t* o_label,
                               int64_t* o_count, int64_t* o_first, float* o_cx, float* o_cy,
                               float* o_mi, int64_t* frame_first_noise,
-                              const int64_t** n_seg_dev, hipStream_t st);
+                              const int32_t** n_seg_dev, hipStream_t st);
 int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
                           const float* inten, const int32_t* pf, int64_t n, int32_t n_frames,
                           int32_t n_clusters, int32_t* o_frame, int32_t* o_label,
@@ -107,7 +107,7 @@ struct SegPack {
   const float* cy;
   const float* mi;
 };
-__global__ void k_pack_segs(const int64_t* __restrict__ n_seg, const int32_t* __restrict__ ncl,
+__global__ void k_pack_segs(const int32_t* __restrict__ n_seg, const int32_t* __restrict__ ncl,
                             SegPack a, int64_t sc, int32_t F, char* __restrict__ out) {
   const int64_t S = *n_seg;
   const int64_t m = S < sc ? S : sc;
@@ -443,7 +443,7 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
   const int bits = ncl_dev ? sum_bits : radix_bits_for(sts.n_clusters);
   const int64_t sc = std::min<int64_t>(
       std::max<int64_t>(seg_hint > 0 ? seg_hint + seg_hint / 4 + 64 : 4096, 1), n_in_);
-  const int64_t* nseg_dev = nullptr;
+  const int32_t* nseg_dev = nullptr;
   RPT_TRY(cluster_summaries_dev(labels.p, cx, cy, cv, cpf, n_in_, F, bits, sc, seg_frame.p,
                                 seg_label.p, seg_count.p, seg_first.p, seg_cx.p, seg_cy.p,
                                 seg_mi.p, first_noise.p, &nseg_dev, st));

@@ -51,7 +51,7 @@ __global__ void k_heads(const uint32_t* __restrict__ sk, const uint32_t* __restr
   }
 }
 
-__global__ void k_seg_starts(const int32_t* __restrict__ head, const int64_t* __restrict__ pos,
+__global__ void k_seg_starts(const int32_t* __restrict__ head, const int32_t* __restrict__ pos,
                              int64_t n, int64_t* __restrict__ seg_start) {
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n;
        p += (int64_t)gridDim.x * blockDim.x)
@@ -291,7 +291,7 @@ __device__ __forceinline__ float mean_intensity(const float* __restrict__ gi, in
 // the mean intensity (lane-parallel), so no other work sits in the chains' instruction streams.
 __global__ __launch_bounds__(kBlock) void k_summarize(
     const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
-    const int64_t* __restrict__ seg_start, const int64_t* __restrict__ n_seg_dev, int64_t n,
+    const int64_t* __restrict__ seg_start, const int32_t* __restrict__ n_seg_dev, int64_t n,
     const float* __restrict__ gx, const float* __restrict__ gy, const float* __restrict__ gi,
     const int32_t* __restrict__ pf, int32_t* __restrict__ o_frame, int32_t* __restrict__ o_label,
     int64_t* __restrict__ o_count, int64_t* __restrict__ o_first, float* __restrict__ o_cx,
@@ -345,7 +345,7 @@ static int32_t summaries_impl(const int32_t* labels, const float* x, const float
                               int bits, int64_t s_hint, int32_t* o_frame, int32_t* o_label,
                               int64_t* o_count, int64_t* o_first, float* o_cx, float* o_cy,
                               float* o_mi, int64_t* frame_first_noise,
-                              const int64_t** n_seg_dev, hipStream_t st) {
+                              const int32_t** n_seg_dev, hipStream_t st) {
   if (n >= (int64_t(1) << 31) - 1) {
     set_error("rpt_cluster_summaries: n exceeds the int32 index space");
     return RPT_ENOTSUP;
@@ -355,7 +355,7 @@ static int32_t summaries_impl(const int32_t* labels, const float* x, const float
   for (int k = 0; k < 4; ++k) b.add<uint32_t>(n + 1);
   b.add<int64_t>(radix_tmp_elems(n));
   b.add<int32_t>(n + 1);
-  b.add<int64_t>(n + 1);
+  b.add<int32_t>(n + 1);
   b.add<int64_t>(n + 1);
   for (int k = 0; k < 3; ++k) b.add<float>(n + 1);
   RPT_TRY(sc.reserve(b.bytes, st));
@@ -365,7 +365,7 @@ static int32_t summaries_impl(const int32_t* labels, const float* x, const float
   uint32_t* va = sc.carve_n<uint32_t>(n + 1);
   int64_t* rtmp = sc.carve_n<int64_t>(radix_tmp_elems(n));
   int32_t* head = sc.carve_n<int32_t>(n + 1);
-  int64_t* pos = sc.carve_n<int64_t>(n + 1);
+  int32_t* pos = sc.carve_n<int32_t>(n + 1);  // int32: n < 2^31 (checked above)
   int64_t* seg_start = sc.carve_n<int64_t>(n + 1);
   float* gx = sc.carve_n<float>(n + 1);
   float* gy = sc.carve_n<float>(n + 1);
@@ -374,7 +374,7 @@ static int32_t summaries_impl(const int32_t* labels, const float* x, const float
     hipLaunchKernelGGL(k_fill_i64, dim3(grid_for(n_frames, 256, 64)), dim3(256), 0, st,
                        frame_first_noise, (int64_t)n_frames, (int64_t)-1);
   if (n == 0) {
-    RPT_HIP(hipMemsetAsync(pos, 0, sizeof(int64_t), st));
+    RPT_HIP(hipMemsetAsync(pos, 0, sizeof(int32_t), st));
     *n_seg_dev = pos;
     RPT_CHECK_LAUNCH();
     return RPT_OK;
@@ -386,7 +386,7 @@ static int32_t summaries_impl(const int32_t* labels, const float* x, const float
   RPT_TRY(radix_sort_pairs(keys, vals, ka, va, n, bits, rtmp, &sk, &sv, st));
   hipLaunchKernelGGL(k_heads, dim3(g), dim3(kBlock), 0, st, sk, sv, pf, n, head,
                      frame_first_noise);
-  RPT_TRY(exclusive_scan_total_i32_to_i64(head, pos, n, st));
+  RPT_TRY(exclusive_scan_total_i32(head, pos, n, st));
   hipLaunchKernelGGL(k_seg_starts, dim3(g), dim3(kBlock), 0, st, head, pos, n, seg_start);
   hipLaunchKernelGGL(k_gather_runs, dim3(g), dim3(kBlock), 0, st, sv, n, x, y, inten, gx, gy, gi);
   const int64_t sh = std::max<int64_t>(1, std::min<int64_t>(s_hint, n));
@@ -415,12 +415,12 @@ int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
     return RPT_EINVAL;
   }
   // the summarize grid is sized for one wave per run component once the count is known
-  const int64_t* nd = nullptr;
+  const int32_t* nd = nullptr;
   RPT_TRY(summaries_impl(labels, x, y, inten, pf, n, n_frames, radix_bits_for(n_clusters),
                          (int64_t)n_clusters * std::max(n_frames, 1) + 1, o_frame, o_label,
                          o_count, o_first, o_cx, o_cy, o_mi, frame_first_noise, &nd, st));
-  int64_t n_seg = 0;
-  RPT_HIP(hipMemcpyAsync(&n_seg, nd, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  int32_t n_seg = 0;
+  RPT_HIP(hipMemcpyAsync(&n_seg, nd, sizeof(int32_t), hipMemcpyDeviceToHost, st));
   RPT_TRY(wait_stream(st));
   *n_seg_host = n_seg;
   return RPT_OK;
@@ -433,7 +433,7 @@ int32_t cluster_summaries_dev(const int32_t* labels, const float* x, const float
                               int bits, int64_t s_hint, int32_t* o_frame, int32_t* o_label,
                               int64_t* o_count, int64_t* o_first, float* o_cx, float* o_cy,
                               float* o_mi, int64_t* frame_first_noise,
-                              const int64_t** n_seg_dev, hipStream_t st) {
+                              const int32_t** n_seg_dev, hipStream_t st) {
   if (n < 0 || n_frames < 0 || bits < 1 || bits > 32 || !n_seg_dev) {
     set_error("cluster_summaries_dev: bad arguments");
     return RPT_EINVAL;
