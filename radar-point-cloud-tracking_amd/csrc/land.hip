@@ -270,7 +270,7 @@ __global__ __launch_bounds__(kBlock) void k_land_keep_cells(const int32_t* __res
 __global__ __launch_bounds__(kBlock) void k_land_scatter(
     const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ v,
     const int32_t* __restrict__ g, const int32_t* __restrict__ pf, int64_t n,
-    const int32_t* __restrict__ keep, const int64_t* __restrict__ pos, float* __restrict__ xo,
+    const int32_t* __restrict__ keep, const int32_t* __restrict__ pos, float* __restrict__ xo,
     float* __restrict__ yo, float* __restrict__ vo, int32_t* __restrict__ go,
     int32_t* __restrict__ pfo) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(kBlock) void k_land_scatter(
   }
 }
 
-__global__ void k_new_offsets(const int64_t* __restrict__ pos, const int64_t* __restrict__ off,
+__global__ void k_new_offsets(const int32_t* __restrict__ pos, const int64_t* __restrict__ off,
                               int n_frames, int64_t* __restrict__ out) {
   for (int f = blockIdx.x * blockDim.x + threadIdx.x; f <= n_frames; f += gridDim.x * blockDim.x)
     out[f] = pos[off[f]];
@@ -401,12 +401,16 @@ int32_t land_filter_cells(const float* x, const float* y, const float* v, const 
                           float* yo, float* vo, int32_t* go, int32_t* pfo, int64_t* new_off,
                           int64_t* n_kept_host, hipStream_t st) {
   Scratch& sc = scratch(st);
+  if (n >= (int64_t(1) << 31) - 1) {
+    set_error("rpt_land_filter: n exceeds the int32 index space");
+    return RPT_ENOTSUP;
+  }
   Budget b;
   b.add<int32_t>(n + 1);
-  b.add<int64_t>(n + 1);
+  b.add<int32_t>(n + 1);
   RPT_TRY(sc.reserve(b.bytes, st));
   int32_t* keep = sc.carve_n<int32_t>(n + 1);
-  int64_t* pos = sc.carve_n<int64_t>(n + 1);
+  int32_t* pos = sc.carve_n<int32_t>(n + 1);  // int32 kept positions (n < 2^31)
   if (n > 0 && cell) {
     hipLaunchKernelGGL(k_land_keep_cells, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, st,
                        cell, n, land, keep);
@@ -416,7 +420,7 @@ int32_t land_filter_cells(const float* x, const float* y, const float* v, const 
                        n, xe, nxe, ye, nye, land, keep);
     RPT_CHECK_LAUNCH();
   }
-  RPT_TRY(exclusive_scan_total_i32_to_i64(keep, pos, n, st));
+  RPT_TRY(exclusive_scan_total_i32(keep, pos, n, st));
   if (n > 0) {
     hipLaunchKernelGGL(k_land_scatter, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, st, x,
                        y, v, g, pf, n, keep, pos, xo, yo, vo, go, pfo);
@@ -428,8 +432,10 @@ int32_t land_filter_cells(const float* x, const float* y, const float* v, const 
     RPT_CHECK_LAUNCH();
   }
   if (n_kept_host) {
-    RPT_HIP(hipMemcpyAsync(n_kept_host, pos + n, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    int32_t k = 0;
+    RPT_HIP(hipMemcpyAsync(&k, pos + n, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     RPT_TRY(wait_stream(st));
+    *n_kept_host = k;
   }
   return RPT_OK;
 }
