@@ -99,12 +99,17 @@ Scratch& scratch(hipStream_t st) {
   return *g_scratch.back().second;
 }
 
+void release_scan_states(int dev);  // below, with the scan
+
 void release_scratch_current() {
   int dev = 0;
   (void)hipGetDevice(&dev);
-  std::lock_guard<std::mutex> lk(g_scratch_mu);
-  for (auto& e : g_scratch)
-    if (e.first.first == dev) e.second->release();
+  {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    for (auto& e : g_scratch)
+      if (e.first.first == dev) e.second->release();
+  }
+  release_scan_states(dev);
 }
 
 // ------------------------------------------------------------------ exclusive scan
@@ -405,6 +410,18 @@ int32_t scan_state(hipStream_t st, int64_t nt, ScanState** out, uint32_t* epoch)
   return RPT_OK;
 }
 }  // namespace
+
+// rpt_release_scratch: the look-back states of the device too (re-created, zeroed, on next use)
+void release_scan_states(int dev) {
+  std::lock_guard<std::mutex> lk(g_scan_mu);
+  for (auto& e : g_scan_states)
+    if (e.first.first == dev && e.second->status) {
+      (void)hipFree(e.second->status);
+      e.second->status = nullptr;
+      e.second->cap = 0;
+      e.second->epoch = 0;
+    }
+}
 
 template <class T, class U>
 static int32_t scan_impl(const T* in, int64_t n_in, U* out, int64_t n_out, hipStream_t stream) {

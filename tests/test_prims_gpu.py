@@ -86,6 +86,20 @@ def test_exclusive_scan_large_values_i64(gpu):
     np.testing.assert_array_equal(got, _expect(a, True))
 
 
+def test_release_scratch_between_scans(gpu):
+    """rpt_release_scratch frees the device's scratch and look-back state; the next scans
+    re-create them (zeroed) and stay exact."""
+    from rpt import _abi
+
+    lib = _abi.load()
+    rng = np.random.default_rng(21)
+    a = rng.integers(0, 9, 300_000).astype(np.int32)
+    for _ in range(3):
+        np.testing.assert_array_equal(_scan(lib, gpu, a, I32, I64, True), _expect(a, True))
+        torch.cuda.synchronize(gpu)
+        lib.rpt_release_scratch()
+
+
 def test_exclusive_scan_epoch_wrap(gpu):
     """70000 consecutive multi-tile scans on one stream (the epoch tag wraps at 65535 and the
     state is cleared then): every 5000th result and the last one stay exact."""
