@@ -38,7 +38,7 @@ extern "C" {
 #define RPT_OK 0
 #define RPT_EINVAL 1      /* bad argument (maps to ValueError)                           */
 #define RPT_ENOMEM 2      /* device allocation failed                                     */
-#define RPT_EHIP 3        /* HIP runtime error                                            */
+#define RPT_EHIP 3        /* HIP runtime error, or a device-side fault reported at a readback */
 #define RPT_EEMPTY 4      /* empty input where the reference raises (sklearn ValueError)  */
 #define RPT_ENOTSUP 5     /* input outside what the device path implements                */
 #define RPT_ENONFINITE 6  /* NaN/inf coordinates (sklearn check_array raises ValueError)  */
@@ -51,7 +51,11 @@ int32_t rpt_version(void);               /* major*10000 + minor*100 + patch     
 const char* rpt_last_error(void);        /* thread-local; "" when none                 */
 int32_t rpt_device_count(void);          /* hipGetDeviceCount; 0 when no GPU           */
 int32_t rpt_set_device(int32_t device);  /* hipSetDevice                               */
-void rpt_release_scratch(void);          /* free this device's scratch pool            */
+/* Frees the current device's scratch arenas and scan look-back states (every stream's; they are
+ * re-created on next use).  The per-stream ST-DBSCAN working sets and rpt_stack / rpt_dbscan
+ * handles are not touched.  Only valid while NO library call is in flight on this device, from
+ * any thread: a scan launched concurrently would run on freed memory. */
+void rpt_release_scratch(void);
 
 /* Device exclusive prefix sum (the primitive under K1's offsets, the land compaction, the grid
  * build and the summaries): out[i] = sum of in[0..i) for i < n; with_total != 0 also writes the
@@ -113,7 +117,7 @@ int32_t rpt_land_mask(const int32_t* count_grid, const double* intensity_grid, i
                       int64_t num_frames, double persistence_threshold, double min_intensity,
                       uint8_t* land_mask /*dev [cells]*/, int64_t* land_cells_host /*sync*/,
                       void* stream);
-/* Stable compaction of the points NOT on land.  point_frame[n] (dev, i32) is the frame slot
+/* Stable compaction of the points NOT on land (n < 2^31 - 1, else RPT_ENOTSUP: int32 positions).  point_frame[n] (dev, i32) is the frame slot
  * of each point (non-decreasing), frame_offsets[n_frames+1] (dev, int64) the frame starts;
  * new_frame_offsets[n_frames+1] (dev) receives the starts of the kept points.
  * *n_kept_host (sync). */
@@ -188,7 +192,8 @@ int32_t rpt_infer_time_from_colors(const uint8_t* colors, int64_t n, const float
  * centroid = sequential float32 sum in point order / count (np.mean axis 0);
  * mean intensity = numpy 1-D float32 mean (pairwise sums over 8192-element chunks).
  * frame_first_noise[n_frames] (dev, int64) = first point index of label -1 per frame, or -1.
- * *n_segments_host (sync).  Output arrays have capacity n. */
+ * *n_segments_host (sync).  Output arrays have capacity n.  n < 2^31 - 1 (int32 positions),
+ * else RPT_ENOTSUP. */
 int32_t rpt_cluster_summaries(const int32_t* labels, const float* x, const float* y,
                               const float* intensity, const int32_t* point_frame, int64_t n,
                               int32_t n_frames, int32_t n_clusters, int32_t* seg_frame,
@@ -204,8 +209,9 @@ int32_t rpt_cluster_summaries(const int32_t* labels, const float* x, const float
  * more than 10 frames are non-empty (:954; grid edges = np.arange(min, max + res, res) as numpy
  * evaluates it) -> rpt_stdbscan of (x, y) with times = frame slot -> rpt_cluster_summaries.
  * Equivalent to calling those entry points in sequence; the size readbacks they need happen
- * inside (pinned memory).  Synchronises `stream`.  An empty clustered set returns RPT_EEMPTY
- * (sklearn's ValueError).  The handle owns its device buffers (grow-only); results stay valid
+ * inside (pinned memory).  Synchronises `stream`.  No built frame at all gives an empty result
+ * (st_dbscan(frames) returns {}, :463-464); built frames whose points the land filter removed
+ * entirely return RPT_EEMPTY (BallTree on 0 samples: sklearn's ValueError).  The handle owns its device buffers (grow-only); results stay valid
  * until the next run on the handle. */
 /* host: the land-grid edges np.arange(lo, hi + res, res) for float32 lo/hi, as numpy 2.x
  * evaluates it (float32 stop and length, float64 values); returns the length, writes up to cap */

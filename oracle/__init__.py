@@ -8,6 +8,7 @@ Contents — a CPU restatement of the reference algorithm for every row of SURVE
 function citing the reference file:line it follows (paths relative to the reference root):
 
 * ``stdbscan``          BFS ST-DBSCAN, C (``stdbscan_oracle.c``) — 3_stdbscan_point_clouds.py:101-136
+* ``stdbscan_uf``       the same labels by the set formulation, OpenMP (large stacks)
 * ``polar_scatter``     4_temporal_object_tracker.py:200-232 arithmetic on an echo matrix
 * ``build_frames``      build_frame :312-352 concatenation
 * ``land_filter``       :359-436
@@ -53,6 +54,8 @@ def _lib():
         lib.oracle_stdbscan.restype = C.c_int32
         lib.oracle_stdbscan.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int64,
                                         C.c_double, C.c_double, C.c_int32, C.c_void_p]
+        lib.oracle_stdbscan_uf.restype = C.c_int32
+        lib.oracle_stdbscan_uf.argtypes = lib.oracle_stdbscan.argtypes
         lib.oracle_neighbour_counts.restype = C.c_int32
         lib.oracle_neighbour_counts.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int64,
                                                 C.c_double, C.c_double, C.c_void_p]
@@ -79,6 +82,22 @@ def stdbscan(coords, times, eps_space: float, eps_time: float, min_samples: int)
                                float(eps_time), int(min_samples), labels.ctypes.data)
     if r < 0:
         raise MemoryError("oracle_stdbscan failed")
+    return labels
+
+
+def stdbscan_uf(coords, times, eps_space: float, eps_time: float, min_samples: int) -> np.ndarray:
+    """The same labels by the set formulation (core counts, core-core components numbered by
+    minimum index, border = smallest adjacent id), OpenMP-parallel: the checker for stacks too
+    large for the sequential BFS.  Pinned to ``stdbscan`` by tests/test_oracle_golden.py."""
+    c, t = _prep(coords, times)
+    n = c.shape[0]
+    if n == 0:
+        raise ValueError("Found array with 0 sample(s)")
+    labels = np.empty(n, dtype=np.int32)
+    r = _lib().oracle_stdbscan_uf(c.ctypes.data, c.shape[1], t.ctypes.data, n, float(eps_space),
+                                  float(eps_time), int(min_samples), labels.ctypes.data)
+    if r < 0:
+        raise MemoryError("oracle_stdbscan_uf failed")
     return labels
 
 

@@ -125,16 +125,18 @@ def stack_coords(frames):
     return xy, t
 
 
-def run_path(frames, eps_space=8.0, eps_time=2.0, min_samples=15, land=True):
+def run_path(frames, eps_space=8.0, eps_time=2.0, min_samples=15, land=True, dbscan=None):
     """Stage order of run_pipeline :941-991 after frame building: land filter when more than 10
-    frames, ST-DBSCAN over the stack, per-frame clusters, tracker over every frame."""
+    frames, ST-DBSCAN over the stack, per-frame clusters, tracker over every frame.
+    dbscan: the labelling function (default the BFS ``stdbscan``; ``stdbscan_uf`` for stacks of
+    millions of points)."""
     from . import stdbscan
     from .tracker import Tracker
 
     if land and len(frames) > 10:
         frames = land_filter(frames)[0]
     xy, t = stack_coords(frames)
-    labels = stdbscan(xy, t, eps_space, eps_time, min_samples)
+    labels = (dbscan or stdbscan)(xy, t, eps_space, eps_time, min_samples)
     clusters = frame_clusters(frames, labels)
     trk = Tracker()
     for fid, _, _ in frames:

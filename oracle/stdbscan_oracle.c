@@ -43,6 +43,8 @@ typedef struct {
   int64_t smax;
   int64_t* gkey;   /* sorted keys */
   int64_t* gidx;   /* point index per sorted key */
+  float* gc;       /* coords of the sorted points, component-major: gc[d * n_grid + k] */
+  float* gt;       /* times of the sorted points */
   int64_t n_grid;
 } ctx_t;
 
@@ -142,7 +144,15 @@ static void build_grid(ctx_t* x) {
     ++m;
   }
   qsort(pairs, (size_t)m, 2 * sizeof(int64_t), cmp_pair);
-  for (int64_t k = 0; k < m; ++k) { x->gkey[k] = pairs[2 * k]; x->gidx[k] = pairs[2 * k + 1]; }
+  x->gc = (float*)malloc(sizeof(float) * (size_t)(m > 0 ? m : 1) * (size_t)x->dim);
+  x->gt = (float*)malloc(sizeof(float) * (size_t)(m > 0 ? m : 1));
+  for (int64_t k = 0; k < m; ++k) {
+    const int64_t i = pairs[2 * k + 1];
+    x->gkey[k] = pairs[2 * k];
+    x->gidx[k] = i;
+    for (int d = 0; d < x->dim; ++d) x->gc[(int64_t)d * m + k] = x->c[i * x->dim + d];
+    x->gt[k] = x->t[i];
+  }
   free(pairs);
   x->n_grid = m;
   x->grid = 1;
@@ -157,7 +167,54 @@ static int64_t lower_key(const ctx_t* x, int64_t key) {
   return a;
 }
 
-static int64_t neighbours_grid(const ctx_t* x, int64_t i, int64_t* buf) {
+/* candidates [p0, p1) of the sorted arrays: the predicate of adjacent(), evaluated in the same
+ * order of operations on contiguous copies (the compiler vectorises the arithmetic) */
+static int64_t scan_range(const ctx_t* x, int64_t i, int64_t p0, int64_t p1, int64_t* out) {
+  const int64_t m = x->n_grid;
+  const double eps2 = x->eps2;
+  const float epst = x->epst;
+  const float ti = x->t[i];
+  const double ax = x->c[i * x->dim];
+  const double ay = x->dim >= 2 ? (double)x->c[i * x->dim + 1] : 0.0;
+  const float* gx = x->gc;
+  const float* gy = x->gc + m;
+  const float* gt = x->gt;
+  int64_t cnt = 0;
+  if (x->dim == 2) {
+    for (int64_t p = p0; p < p1; ++p) {
+      const double dx = ax - (double)gx[p];
+      const double dy = ay - (double)gy[p];
+      const double d2 = dx * dx + dy * dy;
+      const float dt = fabsf(gt[p] - ti);
+      out[cnt] = x->gidx[p];
+      cnt += (d2 <= eps2) & (dt <= epst);
+    }
+    return cnt;
+  }
+  const double az = x->dim == 3 ? (double)x->c[i * x->dim + 2] : 0.0;
+  const float* gz = x->gc + 2 * m;
+  for (int64_t p = p0; p < p1; ++p) {
+    double d2 = 0.0;
+    if (x->dim >= 1) { const double d = ax - (double)gx[p]; d2 = d2 + d * d; }
+    if (x->dim >= 2) { const double d = ay - (double)gy[p]; d2 = d2 + d * d; }
+    if (x->dim >= 3) { const double d = az - (double)gz[p]; d2 = d2 + d * d; }
+    const float dt = fabsf(gt[p] - ti);
+    out[cnt] = x->gidx[p];
+    cnt += (d2 <= eps2) & (dt <= epst);
+  }
+  return cnt;
+}
+
+/* window of point i in grid mode: its slab +- floor(eps_t)+1 (clipped), cells +-1 per
+ * dimension; the candidates are the sorted positions [r[2k], r[2k+1]) for k < return value.
+ * r needs room for 2 * max_ranges(x) entries. */
+static int64_t max_ranges(const ctx_t* x) {
+  double dsd = floor((double)x->epst) + 1.0;
+  int64_t ds = dsd > (double)(x->smax + 1) ? x->smax + 1 : (int64_t)dsd;
+  return (2 * ds + 1) * (x->dim == 3 ? 9 : 3);
+}
+
+static int64_t grid_ranges(const ctx_t* x, int64_t i, int64_t* r) {
   float ti = x->t[i];
   int64_t slab = (int64_t)((double)ti - x->tmin);
   double dsd = floor((double)x->epst) + 1.0;
@@ -168,22 +225,31 @@ static int64_t neighbours_grid(const ctx_t* x, int64_t i, int64_t* buf) {
     lo[d] = c0[d] > 0 ? c0[d] - 1 : 0;
     hi[d] = c0[d] + 1 < x->nd[d] ? c0[d] + 1 : x->nd[d] - 1;
   }
-  int64_t cnt = 0;
+  int64_t k = 0;
   for (int64_t s = slab - ds; s <= slab + ds; ++s) {
     if (s < 0 || s > x->smax) continue;
     int64_t c[3];
     for (c[2] = (x->dim == 3 ? lo[2] : 0); c[2] <= (x->dim == 3 ? hi[2] : 0); ++c[2])
       for (c[1] = lo[1]; c[1] <= hi[1]; ++c[1]) {
         c[0] = lo[0];
-        int64_t k0 = key_of(x, s, c);
+        const int64_t k0 = key_of(x, s, c);
         c[0] = hi[0];
-        int64_t k1 = key_of(x, s, c);
-        for (int64_t p = lower_key(x, k0); p < x->n_grid && x->gkey[p] <= k1; ++p) {
-          int64_t j = x->gidx[p];
-          if (adjacent(x, i, j)) buf[cnt++] = j;
-        }
+        const int64_t k1 = key_of(x, s, c);
+        r[2 * k] = lower_key(x, k0);
+        r[2 * k + 1] = lower_key(x, k1 + 1);
+        ++k;
       }
   }
+  return k;
+}
+
+static int64_t neighbours_grid(const ctx_t* x, int64_t i, int64_t* buf) {
+  int64_t rr[2 * 7 * 9];
+  int64_t* r = max_ranges(x) <= 7 * 9 ? rr : (int64_t*)malloc(sizeof(int64_t) * 2 * (size_t)max_ranges(x));
+  const int64_t nr = grid_ranges(x, i, r);
+  int64_t cnt = 0;
+  for (int64_t k = 0; k < nr; ++k) cnt += scan_range(x, i, r[2 * k], r[2 * k + 1], buf + cnt);
+  if (r != rr) free(r);
   return cnt;
 }
 
@@ -238,6 +304,7 @@ int32_t oracle_stdbscan(const float* coords, int32_t dim, const float* times, in
     if (isfinite(x.tsorted[k])) x.n_finite = k + 1;
   }
   x.gkey = x.gidx = NULL;
+  x.gc = x.gt = NULL;
   build_grid(&x);
   for (int64_t i = 0; i < n; ++i) labels[i] = -1;
   int32_t cid = 0;
@@ -265,7 +332,7 @@ int32_t oracle_stdbscan(const float* coords, int32_t dim, const float* times, in
     ++cid;
   }
   free(x.order); free(x.tsorted); free(nb); free(nb2); free(stack); free(visited); free(inseed);
-  free(x.gkey); free(x.gidx);
+  free(x.gkey); free(x.gidx); free(x.gc); free(x.gt);
   return cid;
 }
 
@@ -289,8 +356,155 @@ int32_t oracle_neighbour_counts(const float* coords, int32_t dim, const float* t
     if (isfinite(x.tsorted[k])) x.n_finite = k + 1;
   }
   x.gkey = x.gidx = NULL;
+  x.gc = x.gt = NULL;
   build_grid(&x);
   for (int64_t i = 0; i < n; ++i) counts[i] = neighbours(&x, i, nb);
-  free(x.order); free(x.tsorted); free(nb); free(x.gkey); free(x.gidx);
+  free(x.order); free(x.tsorted); free(nb); free(x.gkey); free(x.gidx); free(x.gc);
+  free(x.gt);
   return 0;
+}
+
+/* ---------------------------------------------------------------------------------------
+ * oracle_stdbscan_uf — the same labels as oracle_stdbscan, by the set formulation the BFS
+ * computes (checked against the BFS in tests/test_oracle_golden.py):
+ *   core_i   = |{ j : adjacent(i, j) }| >= min_samples       (the BFS count, self included)
+ *   clusters = connected components of the core-core adjacency, numbered in ascending order of
+ *              their minimum index (the BFS opens cluster ids in index order);
+ *   border   = a non-core point adjacent to a core point takes the smallest adjacent cluster id
+ *              (the first cluster whose BFS reaches it); every other point is -1.
+ * OpenMP over points (lock-free union-find hooking the larger root under the smaller, so every
+ * root is its component's minimum index whatever the order).  Grid mode only (integral finite
+ * times); other inputs fall back to the BFS.  Used as the checker for stacks whose summed
+ * neighbourhood sizes (10^10 pairs at the bench's 100 frames) make the sequential BFS too slow.
+ */
+static int64_t uf_find(int64_t* par, int64_t i) {
+  for (;;) {
+    const int64_t p = __atomic_load_n(&par[i], __ATOMIC_RELAXED);
+    if (p == i) return i;
+    const int64_t gp = __atomic_load_n(&par[p], __ATOMIC_RELAXED);
+    if (gp != p) __atomic_compare_exchange_n(&par[i], (int64_t*)&p, gp, 0, __ATOMIC_RELAXED,
+                                             __ATOMIC_RELAXED);
+    i = p;
+  }
+}
+
+static void uf_unite(int64_t* par, int64_t a, int64_t b) {
+  for (;;) {
+    a = uf_find(par, a);
+    b = uf_find(par, b);
+    if (a == b) return;
+    if (a > b) { const int64_t t = a; a = b; b = t; }
+    int64_t expect = b;
+    if (__atomic_compare_exchange_n(&par[b], &expect, a, 0, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED))
+      return;
+  }
+}
+
+static int pair_ok(const ctx_t* x, int64_t i, int64_t p) {
+  const int64_t m = x->n_grid;
+  double d2 = 0.0;
+  for (int d = 0; d < x->dim; ++d) {
+    const double dd = (double)x->c[i * x->dim + d] - (double)x->gc[(int64_t)d * m + p];
+    d2 = d2 + dd * dd;
+  }
+  const float dt = fabsf(x->gt[p] - x->t[i]);
+  return (d2 <= x->eps2) & (dt <= x->epst);
+}
+
+int32_t oracle_stdbscan_uf(const float* coords, int32_t dim, const float* times, int64_t n,
+                           double eps_space, double eps_time, int32_t min_samples,
+                           int32_t* labels) {
+  ctx_t x;
+  memset(&x, 0, sizeof(x));
+  x.c = coords;
+  x.dim = dim;
+  x.t = times;
+  x.eps2 = (eps_space >= 0.0) ? eps_space * eps_space : -1.0;
+  x.epst = (float)eps_time;
+  x.n = n;
+  build_grid(&x);
+  if (!x.grid) {
+    free(x.gkey); free(x.gidx); free(x.gc); free(x.gt);
+    return oracle_stdbscan(coords, dim, times, n, eps_space, eps_time, min_samples, labels);
+  }
+  uint8_t* core = (uint8_t*)calloc((size_t)(n > 0 ? n : 1), 1);
+  int64_t* par = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+  int32_t* cid = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+  if (!core || !par || !cid) return -1;
+  const int64_t mr = max_ranges(&x);
+  /* 1. core flags: neighbour counts with early exit at min_samples */
+#pragma omp parallel
+  {
+    int64_t* r = (int64_t*)malloc(sizeof(int64_t) * 2 * (size_t)mr);
+#pragma omp for schedule(dynamic, 1024)
+    for (int64_t i = 0; i < n; ++i) {
+      par[i] = i;
+      int64_t cnt = 0;
+      if (isfinite(x.t[i]) && cnt < (int64_t)min_samples) {
+        const int64_t nr = grid_ranges(&x, i, r);
+        for (int64_t k = 0; k < nr && cnt < (int64_t)min_samples; ++k)
+          for (int64_t p = r[2 * k]; p < r[2 * k + 1]; ++p) cnt += pair_ok(&x, i, p);
+      }
+      core[i] = cnt >= (int64_t)min_samples;
+    }
+    free(r);
+  }
+  /* 2. components of the core-core adjacency: each pair once, from its lower sorted position
+   * (the candidates above q form a contiguous tail of every range) */
+  uint8_t* core_s = (uint8_t*)malloc((size_t)(x.n_grid > 0 ? x.n_grid : 1));
+  if (!core_s) return -1;
+  for (int64_t q = 0; q < x.n_grid; ++q) core_s[q] = core[x.gidx[q]];
+#pragma omp parallel
+  {
+    int64_t* r = (int64_t*)malloc(sizeof(int64_t) * 2 * (size_t)mr);
+#pragma omp for schedule(dynamic, 256)
+    for (int64_t q = 0; q < x.n_grid; ++q) {
+      if (!core_s[q]) continue;
+      const int64_t i = x.gidx[q];
+      const int64_t nr = grid_ranges(&x, i, r);
+      for (int64_t k = 0; k < nr; ++k)
+        for (int64_t p = r[2 * k] > q + 1 ? r[2 * k] : q + 1; p < r[2 * k + 1]; ++p)
+          if (core_s[p] && pair_ok(&x, i, p)) {
+            const int64_t j = x.gidx[p];
+            if (uf_find(par, j) != uf_find(par, i)) uf_unite(par, i, j);
+          }
+    }
+    free(r);
+  }
+  free(core_s);
+  /* 3. ids in ascending order of the component minimum (= the root) */
+  int32_t ncl = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    cid[i] = -1;
+    if (core[i] && uf_find(par, i) == i) cid[i] = ncl++;
+  }
+  /* 4. labels: core -> its component's id; border -> the smallest adjacent id */
+#pragma omp parallel
+  {
+    int64_t* r = (int64_t*)malloc(sizeof(int64_t) * 2 * (size_t)mr);
+#pragma omp for schedule(dynamic, 1024)
+    for (int64_t i = 0; i < n; ++i) {
+      if (core[i]) {
+        labels[i] = cid[uf_find(par, i)];
+        continue;
+      }
+      int32_t best = -1;
+      if (isfinite(x.t[i])) {
+        const int64_t nr = grid_ranges(&x, i, r);
+        for (int64_t k = 0; k < nr; ++k)
+          for (int64_t p = r[2 * k]; p < r[2 * k + 1]; ++p) {
+            const int64_t j = x.gidx[p];
+            if (core[j] && pair_ok(&x, i, p)) {
+              const int32_t c = cid[uf_find(par, j)];
+              if (best < 0 || c < best) best = c;
+            }
+          }
+      }
+      labels[i] = best;
+    }
+    free(r);
+  }
+  free(core); free(par); free(cid);
+  free(x.gkey); free(x.gidx); free(x.gc); free(x.gt);
+  return ncl;
 }

@@ -251,6 +251,10 @@ int32_t rpt_land_filter(const float* x, const float* y, const float* intensity,
                         float* intensity_out, int32_t* gain_out, int32_t* point_frame_out,
                         int64_t* new_frame_offsets, int64_t* n_kept_host, void* stream) {
   rpt::clear_error();
+  if (n >= (int64_t(1) << 31) - 1) {  // int32 kept positions
+    rpt::set_error("rpt_land_filter: n=%lld exceeds the int32 index space", (long long)n);
+    return RPT_ENOTSUP;
+  }
   return rpt::land_filter(x, y, intensity, gain, point_frame, n, frame_offsets, n_frames,
                           x_edges, nxe, y_edges, nye, land_mask, x_out, y_out, intensity_out,
                           gain_out, point_frame_out, new_frame_offsets, n_kept_host,
@@ -272,6 +276,10 @@ int32_t rpt_cluster_summaries(const int32_t* labels, const float* x, const float
                               int64_t* frame_first_noise, int64_t* n_segments_host,
                               void* stream) {
   rpt::clear_error();
+  if (n >= (int64_t(1) << 31) - 1) {  // int32 segment positions
+    rpt::set_error("rpt_cluster_summaries: n=%lld exceeds the int32 index space", (long long)n);
+    return RPT_ENOTSUP;
+  }
   return rpt::cluster_summaries(labels, x, y, intensity, point_frame, n, n_frames, n_clusters,
                                 seg_frame, seg_label, seg_count, seg_first, seg_cx, seg_cy,
                                 seg_mean_i, frame_first_noise, n_segments_host,

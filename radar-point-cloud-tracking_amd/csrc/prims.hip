@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdarg>
+#include <cstring>
 #include <mutex>
 
 #include "common.h"
@@ -30,6 +31,42 @@ const char* last_error_cstr() { return g_last_error.c_str(); }
 // The path's size readbacks are tiny and the GPU idles until the host has launched the next
 // stage, so the wait polls an event (for up to 200 us, then it blocks) instead of blocking in
 // hipStreamSynchronize right away.  One cached event per (thread, device).
+//
+// Device-side faults that must not pass silently (today: a look-back scan whose predecessor tile
+// never published within its spin bound, i.e. a wrong prefix) set a word in mapped pinned host
+// memory; every readback wait checks and clears it and fails the call with RPT_EHIP.
+static unsigned int* g_fault_host = nullptr;
+static unsigned int* g_fault_dev = nullptr;
+static std::mutex g_fault_mu;
+
+unsigned int* device_fault_word() {
+  std::lock_guard<std::mutex> lk(g_fault_mu);
+  if (!g_fault_dev) {
+    void* h = nullptr;
+    if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      return nullptr;
+    std::memset(h, 0, 64);
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+      (void)hipHostFree(h);
+      return nullptr;
+    }
+    g_fault_host = static_cast<unsigned int*>(h);
+    g_fault_dev = static_cast<unsigned int*>(d);
+  }
+  return g_fault_dev;
+}
+
+int32_t check_device_faults() {
+  if (!g_fault_host) return RPT_OK;
+  const unsigned int f = __atomic_exchange_n(g_fault_host, 0u, __ATOMIC_ACQ_REL);
+  if (f & 1u) {
+    set_error("exclusive scan: a look-back predecessor never published (prefix sums invalid)");
+    return RPT_EHIP;
+  }
+  return RPT_OK;
+}
+
 int32_t wait_stream(hipStream_t st) {
   static thread_local std::vector<hipEvent_t> evs;
   int dev = 0;
@@ -41,12 +78,12 @@ int32_t wait_stream(hipStream_t st) {
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     const hipError_t e = hipEventQuery(evs[dev]);
-    if (e == hipSuccess) return RPT_OK;
+    if (e == hipSuccess) return check_device_faults();
     if (e != hipErrorNotReady) RPT_HIP(e);
     if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) break;
   }
   RPT_HIP(hipEventSynchronize(evs[dev]));
-  return RPT_OK;
+  return check_device_faults();
 }
 
 // ------------------------------------------------------------------ scratch pool
@@ -292,7 +329,8 @@ __global__ __launch_bounds__(B, B >= 1024 ? 8 : 2) void k_scan_lb(const T* __res
                                                U* __restrict__ out, int64_t n_out,
                                                uint64_t* __restrict__ status,
                                                unsigned long long* __restrict__ ticket,
-                                               uint64_t epoch, uint32_t nt) {
+                                               uint64_t epoch, uint32_t nt,
+                                               unsigned int* __restrict__ fault) {
   constexpr int kTile = B * kLbItems;
   __shared__ uint32_t s_tile;
   __shared__ int64_t s_prefix;
@@ -333,7 +371,11 @@ __global__ __launch_bounds__(B, B >= 1024 ? 8 : 2) void k_scan_lb(const T* __res
       const int first_inc = inc ? __ffsll((unsigned long long)inc) - 1 : kWave;
       const uint64_t upto = (first_inc >= kWave - 1) ? ~0ull : ((2ull << first_inc) - 1ull);
       if (zero & upto) {  // a predecessor before the nearest inclusive one is not published yet
-        if (++spins > (1u << 24)) break;  // bounded: a lost tile gives a wrong sum, not a hang
+        if (++spins > (1u << 24)) {  // bounded: a lost tile gives a wrong sum, not a hang --
+          if (lane == 0 && fault)    // reported at the next readback wait (check_device_faults)
+            __hip_atomic_store(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
         __builtin_amdgcn_s_sleep(1);
         continue;
       }
@@ -447,17 +489,18 @@ static int32_t scan_impl(const T* in, int64_t n_in, U* out, int64_t n_out, hipSt
   uint32_t epoch = 0;
   RPT_TRY(scan_state(stream, nt, &s, &epoch));
   auto* ticket = reinterpret_cast<unsigned long long*>(s->status + s->cap);
+  unsigned int* fault = device_fault_word();
   const uint64_t ep = epoch;
   const unsigned grid = (unsigned)nt;
   if (big)
     hipLaunchKernelGGL((k_scan_lb<T, U, kLbBig, true>), dim3(grid), dim3(kLbBig), 0, stream, in,
-                       n_in, out, n_out, s->status, ticket, ep, (uint32_t)nt);
+                       n_in, out, n_out, s->status, ticket, ep, (uint32_t)nt, fault);
   else if (vec)
     hipLaunchKernelGGL((k_scan_lb<T, U, kScanBlock, true>), dim3(grid), dim3(kScanBlock), 0,
-                       stream, in, n_in, out, n_out, s->status, ticket, ep, (uint32_t)nt);
+                       stream, in, n_in, out, n_out, s->status, ticket, ep, (uint32_t)nt, fault);
   else
     hipLaunchKernelGGL((k_scan_lb<T, U, kScanBlock, false>), dim3(grid), dim3(kScanBlock), 0,
-                       stream, in, n_in, out, n_out, s->status, ticket, ep, (uint32_t)nt);
+                       stream, in, n_in, out, n_out, s->status, ticket, ep, (uint32_t)nt, fault);
   RPT_CHECK_LAUNCH();
   return RPT_OK;
 }

@@ -322,6 +322,24 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
                         gain ? g.p : nullptr, pf.p, st));
   }
   if (timing) RPT_HIP(hipEventRecord(ev[1], st));
+  if (N == 0) {
+    // no frame built: st_dbscan(frames) stacks nothing and returns {} (:463-464) -- no error,
+    // no clusters, the tracker sees no frame
+    RPT_TRY(wait_stream(st));
+    fo_in = fo_k1;
+    n_in = 0;
+    h_count.clear();
+    h_first.clear();
+    h_frame.clear();
+    h_label.clear();
+    h_cx.clear();
+    h_cy.clear();
+    h_mi.clear();
+    h_noise.assign((size_t)F, -1);
+    seg_hint = 0;
+    if (out) *out = r;
+    return RPT_OK;
+  }
 
   // ---- land filter (global grid over the stack, :954 gate: more than 10 built frames)
   float* cx = x.p;

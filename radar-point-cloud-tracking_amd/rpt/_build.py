@@ -2,7 +2,9 @@
 
 No CMake, no torch extension machinery: every ``csrc/*.hip`` / ``csrc/*.cpp`` is compiled to an
 object with ``hipcc --offload-arch=gfx950`` and linked into ``rpt/librpt.so``.  Objects are
-rebuilt only when a source or header is newer.  ``-ffp-contract=off`` is global: the parity
+rebuilt only when a source or header is newer, and all of them when the build stamp (hipcc
+version, flags, offload arch) differs from the one recorded in ``build/STAMP``.
+``-ffp-contract=off`` is global: the parity
 contract (bit-identical labels and centroids) forbids FMA contraction of the reference's
 separately rounded float operations.
 """
@@ -63,8 +65,17 @@ def _compile(src: Path, obj: Path) -> str:
     return r.stderr
 
 
+def _stamp() -> str:
+    r = subprocess.run([_hipcc(), "--version"], capture_output=True, text=True)
+    return "\n".join([r.stdout.strip(), " ".join(COMMON_FLAGS), ARCH]) + "\n"
+
+
 def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -> Path:
     BUILD.mkdir(parents=True, exist_ok=True)
+    stamp_file = BUILD / "STAMP"
+    stamp = _stamp()
+    if not stamp_file.exists() or stamp_file.read_text() != stamp:
+        force = True  # other flags, arch or compiler: objects built before are stale
     hdr_t = _headers_mtime()
     todo = []
     objs = []
@@ -84,6 +95,7 @@ def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link of librpt.so failed:\n{r.stderr}")
+    stamp_file.write_text(stamp)
     if verbose:
         print(f"[rpt build] {LIB} ({len(todo)} objects rebuilt)")
     return LIB

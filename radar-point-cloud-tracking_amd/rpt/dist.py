@@ -233,6 +233,13 @@ class ShardedStackPipeline:
         self.geo, self.gain_d = geo, gain_d
 
     def run(self, echo, dt: int, frame0: int) -> ShardResult:
+        dev = getattr(self.ops, "dev", None)
+        if dev is None or torch.device(dev).type != "cuda":  # the oracle-backed CPU test ops
+            return self._run(echo, dt, frame0)
+        with torch.cuda.device(dev):  # librpt works on the thread's current device
+            return self._run(echo, dt, frame0)
+
+    def _run(self, echo, dt: int, frame0: int) -> ShardResult:
         p, ops, comm = self.p, self.ops, self.comm
         G = len(self.gains)
         F = int(echo.shape[0])

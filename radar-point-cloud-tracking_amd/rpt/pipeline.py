@@ -155,6 +155,13 @@ class FrameStackPipeline:
                                             keep_points)
 
     def _run_lane(self, h, stream: int, echo: torch.Tensor, keep_points: bool) -> StackResult:
+        # librpt allocates and records events on the calling thread's current HIP device; lane
+        # threads (and callers whose current device differs) must run on the pipeline's
+        with torch.cuda.device(self.dev):
+            return self._run_lane_dev(h, stream, echo, keep_points)
+
+    def _run_lane_dev(self, h, stream: int, echo: torch.Tensor, keep_points: bool
+                      ) -> StackResult:
         p, lib = self.p, self.lib
         G = len(self.gains)
         F = echo.shape[0]

@@ -127,9 +127,10 @@ def st_dbscan_soa(x: torch.Tensor, y: torch.Tensor, times: torch.Tensor, eps_spa
     labels = out if out is not None else torch.empty(n, dtype=torch.int32, device=dev)
     st = _abi.StdbscanStats()
     st.timing = 1 if stats is not None else 0
-    status = _abi.load().rpt_stdbscan(ptr(x), ptr(y), ptr(z), 1, ptr(times), n,
-                                      float(eps_space), float(eps_time), int(min_samples),
-                                      labels.data_ptr(), st, stream_handle(dev))
+    with torch.cuda.device(dev):  # librpt allocates on the calling thread's current device
+        status = _abi.load().rpt_stdbscan(ptr(x), ptr(y), ptr(z), 1, ptr(times), n,
+                                          float(eps_space), float(eps_time), int(min_samples),
+                                          labels.data_ptr(), st, stream_handle(dev))
     _abi.check(status, "rpt_stdbscan")
     if stats is not None:
         stats.update(n_clusters=st.n_clusters, grid_dims=tuple(st.grid_dims),
@@ -155,9 +156,10 @@ def infer_time_from_colors(colors, gain_colors: Optional[Dict[int, Tuple[int, in
     cd = to_device(colors, torch.uint8, dev)
     pd = to_device(palette, torch.float32, dev)
     out = torch.empty(n, dtype=torch.float32, device=dev)
-    status = _abi.load().rpt_infer_time_from_colors(cd.data_ptr(), n, pd.data_ptr(),
-                                                    palette.shape[0], out.data_ptr(),
-                                                    stream_handle(dev))
+    with torch.cuda.device(dev):
+        status = _abi.load().rpt_infer_time_from_colors(cd.data_ptr(), n, pd.data_ptr(),
+                                                        palette.shape[0], out.data_ptr(),
+                                                        stream_handle(dev))
     _abi.check(status, "rpt_infer_time_from_colors")
     return out if want_torch else out.cpu().numpy()
 

@@ -47,6 +47,18 @@ class SynthConfig:
     frame0: int = 0                          # absolute index of the first frame (sharding)
 
 
+# BASELINE.json configs[4] ("dense full sweep, ~500k pts/frame"): Cartesian-uniform clutter at
+# ~4.2 kept echo cells per m^2 per sweep.  Expected points per frame ~= density * 107k (3 gains,
+# sensitivities 0.7/0.85/1.0, stride 4, 231.5 m) + ~48k target/land points.  At this density every
+# clutter point is core and ST-DBSCAN chains the whole stack into one component: a stress case
+# for the union-find and the per-(frame, label) reductions, as SURVEY.md §8(d) describes it.
+DENSE_CLUTTER_DENSITY = 4.2
+
+
+def dense_config(n_frames: int = 125, **kw) -> "SynthConfig":
+    return SynthConfig(n_frames=n_frames, clutter_density=DENSE_CLUTTER_DENSITY, **kw)
+
+
 @dataclass
 class SynthGeometry:
     angle: np.ndarray          # Angle column (float32 units of 360/8196 deg)

@@ -1,0 +1,196 @@
+"""Parity at the BASELINE.json configs' own sizes (full 4096-azimuth x 1024-bin sweeps), through
+the native stack driver (rpt_stack_run), bit-exact against the oracle:
+
+  configs[0]  one gain_40 sweep (~14k points)  — also through the package st_dbscan API
+  configs[1]  one 3-gain fused frame (~50k points)
+  12-frame full-size stack with the land filter (~570k points; BFS oracle)
+  configs[2]  the bench's own 100-frame stack (~4.4M points; union-find oracle, which is pinned
+              to the BFS by tests/test_oracle_golden.py)
+  dense       a configs[4]-density stack (clutter near 500k points per frame, one giant
+              component spanning the frames)
+
+plus the reference edge cases the stack driver must keep (4_temporal_object_tracker.py):
+an all-zero frame (build_frame returns None, the frame id gap stays, :335-336, :941-944), an
+all-zero single gain (:327-328), and the `len(frames) > 10` land gate at its boundary with an
+empty frame in the stack (:954)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from oracle import path as op
+
+from _stack_check import check_stack_vs_oracle, oracle_stack
+
+pytestmark = pytest.mark.gpu
+
+
+def _pipe(cfg, ds, dev, land=True):
+    from rpt.pipeline import FrameStackPipeline, PathParams
+
+    pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(land_filter=land), dev)
+    pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
+                      cfg.n_frames * len(cfg.gains))
+    return pipe
+
+
+def _run_and_check(dev, cfg, echo_d, ds, land=True, dbscan=None, expect_land=None):
+    frames = oracle_stack(echo_d.cpu().numpy(), cfg, ds.geo)
+    o_frames, o_labels, o_clusters, o_trk = op.run_path(frames, land=land, dbscan=dbscan)
+    res = _pipe(cfg, ds, dev, land).run(echo_d, keep_points=True)
+    check_stack_vs_oracle(res, cfg.n_frames, frames, o_frames, o_labels, o_clusters, o_trk)
+    assert list(res.frame_ids) == [fid for fid, _, _ in frames]
+    if expect_land is not None:
+        assert (res.n_land_cells > 0 or res.n_clustered_input < res.n_points) == expect_land
+    return res, frames
+
+
+def test_config0_single_gain40_sweep(gpu):
+    """configs[0]: one synthetic gain_40 sweep, eps 8 / min 15 — the stack path and the package
+    st_dbscan (3_stdbscan_point_clouds.py / clustering.py form) on its points."""
+    from rpt.processors import st_dbscan
+    from rpt.synth import DeviceSynth, SynthConfig
+
+    cfg = SynthConfig(n_frames=1, gains=(40,))
+    ds = DeviceSynth(cfg, gpu)
+    echo = ds.echo()
+    res, frames = _run_and_check(gpu, cfg, echo, ds)
+    assert 8_000 < res.n_points < 20_000
+    xy, t = op.stack_coords(frames)
+    np.testing.assert_array_equal(st_dbscan(xy, t, 8.0, 2.0, 15),
+                                  oracle.stdbscan(xy, t, 8.0, 2.0, 15))
+
+
+def test_config1_single_fused_frame(gpu):
+    """configs[1]: one 3-gain fused frame (40/50/75), ~50k points."""
+    from rpt.synth import DeviceSynth, SynthConfig
+
+    cfg = SynthConfig(n_frames=1, frame0=17)
+    ds = DeviceSynth(cfg, gpu)
+    res, _ = _run_and_check(gpu, cfg, ds.echo(), ds)
+    assert 35_000 < res.n_points < 70_000 and res.n_clusters > 5
+
+
+@pytest.mark.timeout(600)
+def test_fullsize_stack_12_frames_land(gpu):
+    """12 full-size fused frames: the land filter is on (> 10 frames); BFS oracle."""
+    from rpt.synth import DeviceSynth, SynthConfig
+
+    cfg = SynthConfig(n_frames=12)
+    ds = DeviceSynth(cfg, gpu)
+    res, _ = _run_and_check(gpu, cfg, ds.echo(), ds, expect_land=True)
+    assert res.n_points > 500_000
+
+
+@pytest.mark.timeout(1200)
+def test_config2_bench_stack_100_frames(gpu):
+    """configs[2], the bench's own workload: 100 full-size fused frames, land filter, ST-DBSCAN,
+    per-frame clusters and the tracker — labels, cluster rows and tracked objects bit-exact."""
+    from rpt.synth import DeviceSynth, SynthConfig
+
+    cfg = SynthConfig(n_frames=100)
+    ds = DeviceSynth(cfg, gpu)
+    res, _ = _run_and_check(gpu, cfg, ds.echo(), ds, dbscan=oracle.stdbscan_uf, expect_land=True)
+    assert res.n_points > 4_500_000 and res.n_clusters > 100
+
+
+@pytest.mark.timeout(900)
+def test_dense_stack_config4_density(gpu):
+    """configs[4]'s density (~500k points per frame, one component chaining every frame) on a
+    short stack; the union-find oracle."""
+    from rpt.synth import DeviceSynth, dense_config
+
+    cfg = dense_config(n_frames=4)
+    ds = DeviceSynth(cfg, gpu)
+    res, _ = _run_and_check(gpu, cfg, ds.echo(), ds, dbscan=oracle.stdbscan_uf)
+    assert res.n_points > 4 * 350_000
+
+
+# ------------------------------------------------------------------ stack-driver edge cases
+def _edge_synth(n_frames):
+    from rpt.synth import SynthConfig
+
+    return SynthConfig(n_frames=n_frames, rows=1024, n_targets=14, clutter_density=0.01)
+
+
+def test_all_zero_frame_is_dropped_with_id_gap(gpu):
+    """An all-zero frame builds no RadarFrame (:335-336): it is missing from the stack, the later
+    frame ids keep their slot (:941-944), times in ST-DBSCAN skip it, the tracker never sees it."""
+    from rpt.synth import DeviceSynth
+
+    cfg = _edge_synth(14)
+    ds = DeviceSynth(cfg, gpu)
+    echo = ds.echo()
+    echo[5].zero_()
+    res, frames = _run_and_check(gpu, cfg, echo, ds, expect_land=True)
+    assert 5 not in [fid for fid, _, _ in frames] and 5 not in list(res.frame_ids)
+    assert len(res.frame_ids) == 13
+
+
+def test_all_zero_single_gain(gpu):
+    """A gain whose sweep keeps nothing is skipped by build_frame (:327-328); the frame keeps its
+    other gains in ascending order."""
+    from rpt.synth import DeviceSynth
+
+    cfg = _edge_synth(6)
+    ds = DeviceSynth(cfg, gpu)
+    echo = ds.echo()
+    echo[2, 1].zero_()   # gain 50 of frame 2
+    echo[4, 0].zero_()   # gain 40 of frame 4
+    res, frames = _run_and_check(gpu, cfg, echo, ds)
+    g = {fid: set(np.unique(gg).tolist()) for fid, _, gg in frames}
+    assert g[2] == {40, 75} and g[4] == {50, 75}
+    assert res.points["gain"].numel() == res.n_clustered_input
+
+
+@pytest.mark.parametrize("n_frames,empty,land_on", [(11, 7, False), (12, 7, True), (11, None, True)])
+def test_land_gate_boundary_with_empty_frame(gpu, n_frames, empty, land_on):
+    """`len(frames) > 10` counts BUILT frames (:954): 11 slots with one empty frame leave 10
+    frames and no land filter; 12 slots with one empty keep 11 and filter."""
+    from rpt.synth import DeviceSynth
+
+    cfg = _edge_synth(n_frames)
+    ds = DeviceSynth(cfg, gpu)
+    echo = ds.echo()
+    if empty is not None:
+        echo[empty].zero_()
+    res, frames = _run_and_check(gpu, cfg, echo, ds, expect_land=land_on)
+    assert len(frames) == n_frames - (empty is not None)
+
+
+def test_all_frames_empty_gives_no_clusters(gpu):
+    """Every sweep empty: no frame is built, st_dbscan(frames) returns {} (:463-464) and the
+    tracker sees no frame — no error."""
+    from rpt.synth import DeviceSynth
+
+    cfg = _edge_synth(3)
+    ds = DeviceSynth(cfg, gpu)
+    echo = ds.echo()
+    echo.zero_()
+    res = _pipe(cfg, ds, gpu).run(echo, keep_points=True)
+    assert res.n_points == 0 and res.n_clusters == 0 and res.n_segments == 0
+    assert len(res.frame_ids) == 0 and len(res.tracker) == 0
+    assert res.labels.numel() == 0
+
+
+def test_everything_on_land_raises_like_sklearn(gpu):
+    """Built frames whose points the land filter removes entirely: the reference stacks empty
+    frames and BallTree raises ValueError (n = 0); the device path raises the same."""
+    from rpt.synth import DeviceSynth, SynthConfig
+
+    cfg = SynthConfig(n_frames=12, rows=1024, n_targets=0, clutter_density=0.0, land_fill=1.0)
+    ds = DeviceSynth(cfg, gpu)
+    echo = ds.echo()
+    frames = oracle_stack(echo.cpu().numpy(), cfg, ds.geo)
+    try:
+        expect = op.run_path(frames)
+    except ValueError:
+        expect = None
+    if expect is None:
+        with pytest.raises(ValueError):
+            _pipe(cfg, ds, gpu).run(echo)
+    else:  # some land-sector cells fell short of the persistence rule: compare as usual
+        res = _pipe(cfg, ds, gpu).run(echo, keep_points=True)
+        check_stack_vs_oracle(res, cfg.n_frames, frames, *expect)

@@ -199,3 +199,18 @@ def test_arange_edges_match_numpy():
         n = lib.rpt_arange_edges(float(a), float(b), 5.0, out.ctypes.data_as(_abi.c_f64p), 4096)
         assert n == len(exp)
         np.testing.assert_array_equal(out[:n], exp)
+
+
+def test_int32_index_limits_return_enotsup():
+    """rpt_land_filter / rpt_cluster_summaries use int32 positions: n >= 2^31 - 1 is refused
+    with RPT_ENOTSUP by the size check alone (no device memory is touched)."""
+    from rpt import _abi
+
+    lib = _abi.load()
+    n = (1 << 31) - 1
+    st = lib.rpt_land_filter(None, None, None, None, None, n, None, 1, None, 2, None, 2, None,
+                             None, None, None, None, None, None, None, None)
+    assert st == _abi.RPT_ENOTSUP and b"int32" in lib.rpt_last_error()
+    st = lib.rpt_cluster_summaries(None, None, None, None, None, n, 1, 1, None, None, None, None,
+                                   None, None, None, None, None, None)
+    assert st == _abi.RPT_ENOTSUP and b"int32" in lib.rpt_last_error()

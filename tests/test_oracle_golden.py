@@ -15,6 +15,41 @@ def test_stdbscan_oracle_matches_reference_labels(golden):
         eps, et, ms = g[f"c{k}_params"]
         lab = oracle.stdbscan(g[f"c{k}_coords"], g[f"c{k}_times"], eps, et, int(ms))
         np.testing.assert_array_equal(lab, g[f"c{k}_labels"], err_msg=f"case {k} {g[f'c{k}_kind']}")
+        lab = oracle.stdbscan_uf(g[f"c{k}_coords"], g[f"c{k}_times"], eps, et, int(ms))
+        np.testing.assert_array_equal(lab, g[f"c{k}_labels"], err_msg=f"uf case {k}")
+
+
+def test_stdbscan_uf_matches_bfs_on_dense_stacks():
+    """The set-formulation checker (used at full stack sizes) against the BFS oracle on dense
+    multi-frame clouds: chained clusters, border points between clusters, frame-id gaps, NaN
+    times, lattice ties, D=3."""
+    rng = np.random.default_rng(31)
+    for case in range(12):
+        F = int(rng.integers(2, 9))
+        pts, ts = [], []
+        for f in range(F):
+            if case % 4 == 1 and f == F // 2:
+                continue  # frame-id gap
+            c = rng.random((int(rng.integers(3, 10)), 2)) * 150
+            for cc in c:
+                m = int(rng.integers(5, 120))
+                pts.append(cc + rng.normal(0, rng.choice([1.0, 3.0, 6.0]), (m, 2)))
+                ts.append(np.full(m, f))
+            m = int(rng.integers(50, 400))
+            pts.append(rng.random((m, 2)) * 150)
+            ts.append(np.full(m, f))
+        xy = np.vstack(pts).astype(np.float32)
+        if case % 3 == 2:
+            xy = np.round(xy)  # lattice: exact-boundary distances
+        t = np.concatenate(ts).astype(np.float32)
+        if case % 4 == 3:
+            t[rng.random(len(t)) < 0.01] = np.nan
+        if case % 5 == 4:
+            xy = np.column_stack([xy, rng.integers(0, 30, len(xy))]).astype(np.float32)
+        eps, et, ms = float(rng.choice([3.0, 5.0, 8.0])), float(rng.choice([0.0, 1.0, 2.0])), \
+            int(rng.choice([1, 4, 10, 15]))
+        np.testing.assert_array_equal(oracle.stdbscan_uf(xy, t, eps, et, ms),
+                                      oracle.stdbscan(xy, t, eps, et, ms), err_msg=f"case {case}")
 
 
 def test_polar_oracle_matches_load_radar_csv(golden):

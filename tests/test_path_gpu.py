@@ -10,6 +10,9 @@ import torch
 import oracle
 from oracle import path as op
 
+from _stack_check import check_stack_vs_oracle as _check_stack_vs_oracle
+from _stack_check import oracle_stack as _oracle_stack
+
 pytestmark = pytest.mark.gpu
 
 
@@ -309,14 +312,6 @@ def test_mean_intensity_pairwise_chunks(gpu):
         assert float(seg["mi"][s]) == float(np.mean(p[m][:, 2]))
 
 
-def _oracle_stack(echo, cfg, geo):
-    F, G, R, B = echo.shape
-    per_frame = [{gain: op.polar_scatter(echo[f, k], np.full(R, cfg.scale, np.float32),
-                                         geo.cos_t, geo.sin_t)
-                  for k, gain in enumerate(cfg.gains)} for f in range(F)]
-    return op.build_frames(per_frame)
-
-
 @pytest.mark.parametrize("n_frames,land", [(6, True), (14, True), (14, False)])
 def test_stack_path_matches_oracle(gpu, n_frames, land):
     """echo in HBM -> K1 -> land -> ST-DBSCAN -> K9 -> order -> C++ tracker, against the oracle
@@ -336,25 +331,6 @@ def test_stack_path_matches_oracle(gpu, n_frames, land):
     for _ in range(2):
         res = pipe.run(echo_d, keep_points=True)
         _check_stack_vs_oracle(res, n_frames, frames, o_frames, o_labels, o_clusters, o_trk)
-
-
-def _check_stack_vs_oracle(res, n_frames, frames, o_frames, o_labels, o_clusters, o_trk):
-    assert res.n_points == sum(len(p) for _, p, _ in frames)
-    np.testing.assert_array_equal(res.labels.cpu().numpy(), o_labels)
-    # per-frame cluster rows in reference order
-    fo, order, seg = res.frame_order_offsets, res.frame_order, res.seg
-    got = [(f, int(seg["label"][s]), int(seg["count"][s]), seg["cx"][s], seg["cy"][s],
-            float(seg["mi"][s])) for f in range(n_frames) for s in order[fo[f]:fo[f + 1]]]
-    exp = [(fid, c[0], c[1], c[2][0], c[2][1], c[3]) for fid, _, _ in o_frames
-           for c in o_clusters.get(fid, [])]
-    assert got == exp
-    a = list(o_trk.objects.values())
-    b = res.tracker.objects()
-    assert [x.object_id for x in a] == [x.object_id for x in b]
-    assert [x.object_type for x in a] == [x.object_type for x in b]
-    for x, y in zip(a, b):
-        np.testing.assert_array_equal(np.vstack(x.positions), np.vstack(y.positions))
-        assert x.frames_seen == y.frames_seen
 
 
 def test_k1_grouped_u8_matches_generic_rows(gpu):
