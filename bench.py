@@ -7,11 +7,17 @@ land filter (> 10 frames), ST-DBSCAN over the stack, per-frame cluster summaries
 cluster order and the Hungarian tracker on the host — ending with final tracker state on the
 host.  value = points produced by K1 over the stack ("Total points", :950-951) / step time.
 
-Workload at N=1: configs[2] of BASELINE.json — 100-frame 3-gain fused stack, ST-DBSCAN +
-tracking (configs[1], one 50k-point frame, is launch-latency bound and is a parity case).
-Multi-GPU: every rank owns `--frames` contiguous frames of one global stack (weak scaling).
+Default workload: the north-star stack of BASELINE.json configs[3] — ONE 1000-frame 3-gain
+fused stack (12.6 GB of u8 echo, ~50 M points), land filter + ST-DBSCAN + tracking — strong
+scaling: at N GPUs every rank owns 1000/N contiguous frames of that same stack (rpt/dist.py), so
+the driver's N=1,2,4,8 values measure the "6x at 8 GPUs on a 1000-frame stack" target directly.
+At N=1 the whole stack runs on one MI355X (it fits: 288 GB HBM).
+  --frames F     weak scaling instead: F frames per GPU (F=100 is configs[2], round 1's line)
+  --dense        configs[4]'s density (~500k points per frame, rpt.synth.dense_config)
+  --h2d-steps K  also time K steps that first copy the echo from pinned host memory (reported
+                 as `h2d_inclusive`, never as `value`)
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--total-frames T | --frames F] [--dense]
 """
 from __future__ import annotations
 
@@ -60,12 +66,44 @@ def cpu_baseline(echo_host: np.ndarray, cfg, geo, max_seconds: float = 30.0):
     return npts, len(frames), dt
 
 
+def _cpu_model() -> str:
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _reference_measured():
+    """The reference's own sklearn/scipy path, timed in the build container by
+    tools/time_reference.py (the reference cannot travel to this box): committed numbers."""
+    f = ROOT / "profiles" / "r2" / "reference_cpu.json"
+    if not f.exists():
+        return None
+    d = json.loads(f.read_text())
+    legs = {k: {kk: v[kk] for kk in ("points", "frames", "total_s", "mpoints_per_s") if kk in v}
+            for k, v in d.get("legs", {}).items() if isinstance(v, dict)}
+    return {"source": "profiles/r2/reference_cpu.json (tools/time_reference.py)",
+            "cpu_model": d.get("cpu_model"), "threads": d.get("threads_used"), "legs": legs,
+            "note": "the reference builds one BallTree over all frames: rates fall ~1/k with k "
+                    "frames and do not extrapolate to 100-1000 frames"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=100, help="frames per GPU")
+    ap.add_argument("--total-frames", type=int, default=1000,
+                    help="frames of the one global stack, split over the ranks (strong scaling)")
+    ap.add_argument("--frames", type=int, default=None,
+                    help="frames per GPU instead (weak scaling)")
+    ap.add_argument("--dense", action="store_true", help="configs[4] density (~500k pts/frame)")
+    ap.add_argument("--h2d-steps", type=int, default=2,
+                    help="extra steps timed with the echo's H2D copy from pinned host memory "
+                         "(0 = skip)")
     ap.add_argument("--cpu-frames", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-stage hipEvent timing")
@@ -99,8 +137,17 @@ def main():
     from rpt.synth import DeviceSynth, SynthConfig
 
     _abi.load()
-    F = args.frames
-    cfg = SynthConfig(n_frames=F, frame0=rank * F)
+    if args.frames is not None:
+        F, scaling, total = args.frames, "weak", args.frames * world
+    else:
+        if args.total_frames % world:
+            raise SystemExit(f"--total-frames {args.total_frames} must divide over {world} ranks")
+        F, scaling, total = args.total_frames // world, "strong", args.total_frames
+    if args.dense:
+        from rpt.synth import dense_config
+        cfg = dense_config(n_frames=F, frame0=rank * F)
+    else:
+        cfg = SynthConfig(n_frames=F, frame0=rank * F)
     ds = DeviceSynth(cfg, dev)
     echo = ds.echo()
     torch.cuda.synchronize(dev)
@@ -179,12 +226,46 @@ def main():
     value = pts * args.steps / dt / 1e6
     ms_step = dt / args.steps * 1e3
 
-    traffic = None
-    tfile = ROOT / "profiles" / "r1" / "k5_traffic.json"
-    if tfile.exists() and not dist and args.frames == 100:
-        # PMC-measured HBM bytes per K5 launch of this same workload (tools/pmc.sh: separate
-        # FETCH_SIZE / WRITE_SIZE passes, gfx950 read correction); committed under profiles/
-        traffic = json.loads(tfile.read_text()).get("bytes_per_launch")
+    # optional leg: the same steps with the echo's H2D copy from pinned host memory inside
+    h2d = None
+    if args.h2d_steps > 0:
+        host = torch.empty(echo.shape, dtype=echo.dtype, pin_memory=True)
+        host.copy_(echo)
+        torch.cuda.synchronize(dev)
+        if dist:
+            tdist.barrier()
+        th0 = time.perf_counter()
+        hres = []
+        for _ in range(args.h2d_steps):
+            echo.copy_(host, non_blocking=True)
+            hres.append(run())
+        for r in hres:
+            resolve(r).finish()
+        torch.cuda.synchronize(dev)
+        if dist:
+            tdist.barrier()
+        dth = time.perf_counter() - th0
+        if dist:
+            t = torch.tensor([dth], dtype=torch.float64, device=dev)
+            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+            dth = float(t[0])
+        h2d = {"value": round(pts * args.h2d_steps / dth / 1e6, 3), "unit": "Mpoints/s",
+               "ms_per_step": round(dth / args.h2d_steps * 1e3, 3), "steps": args.h2d_steps,
+               "echo_bytes_per_rank": int(echo.numel() * echo.element_size()),
+               "note": "each step first copies the u8 echo from pinned host memory (PCIe), "
+                       "then runs the same path; not the headline value"}
+        del host
+
+    wkey = f"{'dense' if args.dense else 'std'}_{F}f"
+    traffic, tsrc = None, None
+    for tfile in (ROOT / "profiles" / "r2" / f"k5_traffic_{wkey}.json",
+                  ROOT / "profiles" / "r1" / "k5_traffic.json"):
+        if tfile.exists() and not dist and (tfile.parent.name == "r2" or wkey == "std_100f"):
+            # PMC-measured HBM bytes per K5 launch of this same workload (tools/pmc.sh: separate
+            # FETCH_SIZE / WRITE_SIZE passes, gfx950 read correction); committed under profiles/
+            traffic = json.loads(tfile.read_text()).get("bytes_per_launch")
+            tsrc = str(tfile.relative_to(ROOT))
+            break
     roof = None
     if k5_ms:
         k5 = float(np.mean(k5_ms))
@@ -195,39 +276,51 @@ def main():
                 "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None if traffic is None else int(traffic),
-                "traffic_unit": "bytes per launch (PMC, profiles/r1/k5_traffic.json)",
+                "traffic_unit": f"bytes per launch (PMC, {tsrc})" if tsrc else None,
                 "bytes_model": "17 B/point x points entering ST-DBSCAN (SURVEY.md 8d)",
                 "avg_ms": round(k5, 4), "points": n_in}
     stage = {k: round(v / args.steps, 3) for k, v in stage_acc.items()}
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and not dist:
-        cf = min(args.cpu_frames, args.frames)
+        cf = min(args.cpu_frames, F)
         eh = echo[:cf].cpu().numpy()
         npts, nfr, cdt = cpu_baseline(eh, cfg, ds.geo)
         cpu = {"value": round(npts / cdt / 1e6, 5), "unit": "Mpoints/s", "cores": 1,
                "kind": "port",
-               "sample": f"first {nfr} frames of the same stack ({npts} points): oracle numpy "
-                         f"polar scatter + C BFS ST-DBSCAN + numpy/scipy tracker, 1 thread, "
-                         f"{cdt:.1f} s"}
+               "what": "oracle grid-BFS port: oracle/ C grid-indexed BFS restatement of st_dbscan "
+                       "+ numpy polar/land + Python tracker, 1 thread -- NOT the reference's "
+                       "BallTree path (that one is reference_measured)",
+               "cpu_model": _cpu_model(),
+               "sample": f"first {nfr} frames of the same stack ({npts} points), {cdt:.1f} s",
+               "reference_measured": _reference_measured()}
     if rank == 0:
+        what = "dense (configs[4] density, ~500k pts/frame)" if args.dense else \
+            "3-gain fused"
+        if scaling == "strong":
+            wl = (f"ONE {total}-frame {what} stack (4096 az x 1024 echo u8) split over {world} "
+                  f"GPU(s), {F} frames each; land filter + ST-DBSCAN eps 8 / eps_t 2 / min 15 + "
+                  f"Hungarian tracking (BASELINE configs[3]"
+                  f"{' / configs[4]' if args.dense else ''}, strong scaling)")
+        else:
+            wl = (f"{F}-frame {what} stack per GPU (4096 az x 1024 echo u8), land filter + "
+                  f"ST-DBSCAN eps 8 / eps_t 2 / min 15 + Hungarian tracking "
+                  f"(BASELINE configs[2] at F=100, weak scaling)")
         out = {
             "metric": "Mpoints/s clustered+tracked, 1024-echo synthetic frames; 1/2/4/8-GPU scaling",
             "value": round(value, 3), "unit": "Mpoints/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8 echo / f32 geometry / f64 distance",
+            "scaling": scaling, "vs_baseline": None,
+            "dtype": "u8 echo / f32 geometry / f64 distance",
             "data": "synthetic (device-generated, seeded)",
-            "config": {"workload": f"{args.frames}-frame 3-gain fused stack per GPU "
-                                   f"(4096 az x 1024 echo u8), land filter + ST-DBSCAN eps 8 / "
-                                   f"eps_t 2 / min 15 + Hungarian tracking (BASELINE configs[2])",
-                       "frames_per_gpu": args.frames, "points_per_step": int(pts),
-                       **summary,
+            "config": {"workload": wl, "total_frames": total, "frames_per_gpu": F,
+                       "points_per_step": int(pts), **summary,
                        "parallelism": f"frame-sharded x{world}" if dist else "single GPU",
                        "stacks_in_flight": 1 if dist else args.lanes,
                        "host_stage": "inline" if args.sync_host else
                        "overlapped: step k's order+tracker runs on a host thread during step "
                        "k+1's device work; the timed region ends after the last one"},
-            "roofline": roof, "cpu_baseline": cpu, "stage_ms": stage,
+            "roofline": roof, "cpu_baseline": cpu, "h2d_inclusive": h2d, "stage_ms": stage,
         }
         print(json.dumps(out), flush=True)
     if dist:

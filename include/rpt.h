@@ -23,6 +23,8 @@
  *   rpt_lsap                         scipy.optimize.linear_sum_assignment as called at :590
  *   rpt_tracker_*                    ObjectTracker :543-688 (+ TrackedObject :111-140)
  *   rpt_stack_*                      the compute stages of run_pipeline :941-991 (K1 .. K9) in one call
+ *   rpt_fuse_gains_max               fuse_gains_max PointCloudWork/5_gain_fusion_ply_builder.py:222-273
+ *   rpt_csv_*                        pd.read_csv + fillna/to_numpy of load_radar_csv :189-211
  *   rpt_synth_echo                   (bench/test input generator; no reference counterpart)
  */
 #ifndef RPT_H
@@ -186,6 +188,16 @@ int32_t rpt_select_roots(const int64_t* rep, int64_t base, int64_t lo, int64_t h
 int32_t rpt_infer_time_from_colors(const uint8_t* colors, int64_t n, const float* palette,
                                    int32_t n_pal, float* times_out, void* stream);
 
+/* ---- max-intensity gain fusion (5_gain_fusion_ply_builder.py fuse_gains_max :222-273) ------
+ * Points x, y, intensity (dev, float32 [n], intensities > 0: the loader's threshold) on a
+ * grid_resolution grid anchored at the float32 minima: per cell the maximum intensity; occupied
+ * cells in np.where(valid.T) order (y-major, then x) as float64 cell centres
+ * (x_min + ix * res) + res / 2 and float32 maxima.  Outputs (dev) need capacity n (one cell per
+ * point at most).  *n_out_host: the cell count (sync).  n = 0 gives 0 cells. */
+int32_t rpt_fuse_gains_max(const float* x, const float* y, const float* intensity, int64_t n,
+                           double grid_resolution, double* out_x, double* out_y,
+                           float* out_intensity, int64_t* n_out_host, void* stream);
+
 /* ---- K9: per-(frame, label) cluster summaries ---------------------------------------
  * point_frame[n] (dev, i32, non-decreasing frame slot per point), labels[n] from
  * rpt_stdbscan.  Segment s = one (frame, label>=0) pair, ordered by (label, frame).
@@ -311,6 +323,26 @@ int32_t rpt_tracker_object_info(const rpt_tracker* t, int32_t idx, rpt_object_in
  * (exact widening of the f32 values; velocity 0 is the f64 zero).  Buffers sized from info. */
 int32_t rpt_tracker_object_history(const rpt_tracker* t, int32_t idx, float* px, float* py,
                                    int64_t* frames, double* vx, double* vy);
+
+/* ---- host: radar CSV ingest ---------------------------------------------------------------
+ * The file half of load_radar_csv (PointCloudWork/4_temporal_object_tracker.py:189-211;
+ * radar_pipeline/core/loaders.py:46-101): pd.read_csv(header=None, names=Status, Scale, Range,
+ * Gain, Angle, Echo_0..Echo_{bins-1}, skiprows=1), echo fillna(0) -> float32, Scale/Angle ->
+ * float32, parsed by n_threads host threads (<= 0: all cores), one file per task.
+ * rpt_csv_count_rows: rows_out[i] = data rows of file i (blank lines skipped), -1 unreadable.
+ * rpt_csv_parse_sweeps: file i -> echo + i*rows_cap*bins (u8 or f32 per echo_dtype), scale/angle
+ * + i*rows_cap (float32; NaN where pandas reads NaN), gain_col[i] = the Gain value when every row
+ * holds the same one, else NaN; rows past the
+ * file's end are zero.  status_out[i]: 0 ok, 1 unreadable or more fields than names (read_csv
+ * raises: the reference returns an empty sweep), 2 no data row (df.empty: empty sweep), 3 a value
+ * that is not an integer in 0..255 with echo_dtype u8 (parse again as f32), 4 a non-numeric value
+ * (the reference's to_numpy(float32) raises ValueError). */
+int32_t rpt_csv_count_rows(const char* const* paths, int32_t n_files, int64_t* rows_out,
+                           int32_t n_threads);
+int32_t rpt_csv_parse_sweeps(const char* const* paths, int32_t n_files, int32_t rows_cap,
+                             int32_t bins, int32_t echo_dtype, void* echo /*host*/,
+                             float* scale, float* angle, float* gain_col, int32_t* status_out,
+                             int32_t n_threads);
 
 /* ---- synthetic input (bench / parity tests) -----------------------------------------
  * Deterministic u8 echo [n_frames][n_gains][rows][bins] from integer hashes; see

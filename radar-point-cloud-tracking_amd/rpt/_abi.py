@@ -185,6 +185,12 @@ _SIGS = [
     ("rpt_tracker_object_info", C.c_int32, [vp, C.c_int32, C.POINTER(ObjectInfo)]),
     ("rpt_tracker_object_history", C.c_int32, [vp, C.c_int32, c_f32p, c_f32p, c_i64p, c_f64p,
                                                 c_f64p]),
+    ("rpt_fuse_gains_max", C.c_int32,
+     [vp, vp, vp, C.c_int64, C.c_double, vp, vp, vp, c_i64p, vp]),
+    ("rpt_csv_count_rows", C.c_int32, [C.POINTER(C.c_char_p), C.c_int32, c_i64p, C.c_int32]),
+    ("rpt_csv_parse_sweeps", C.c_int32,
+     [C.POINTER(C.c_char_p), C.c_int32, C.c_int32, C.c_int32, C.c_int32, vp, c_f32p, c_f32p,
+      c_f32p, c_i32p, C.c_int32]),
     ("rpt_synth_echo", C.c_int32,
      [C.POINTER(SynthParams), C.c_int64, C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp]),
 ]

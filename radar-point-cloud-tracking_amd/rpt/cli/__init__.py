@@ -1,0 +1,3 @@
+"""Command-line drop-ins: ``rpt.cli.tracker`` (PointCloudWork/4_temporal_object_tracker.py),
+``rpt.cli.stdbscan_ply`` (PointCloudWork/3_stdbscan_point_clouds.py) and ``rpt.cli.main``
+(the ``radar-pipeline`` click group's ``cluster`` command)."""

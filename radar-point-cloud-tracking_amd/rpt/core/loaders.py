@@ -1,9 +1,9 @@
 """Drop-in for ``radar_pipeline.core.loaders`` containers and loaders
 (radar-pipeline/src/radar_pipeline/core/loaders.py:15-101, :149-220).
 
-The containers are the boundary types of the path.  The CSV/PLY parsers are host text I/O
-("next"): they keep the reference's pandas / ASCII semantics here and
-are not part of the timed device path.
+The containers are the boundary types of the path.  load_radar_csv parses with librpt's native
+CSV reader (csrc/csv.cpp; pandas read_csv semantics, checked against pandas
+in tests/test_csv_ingest.py); the PLY reader keeps the reference's ASCII semantics.
 """
 from __future__ import annotations
 
@@ -46,26 +46,32 @@ class PointCloud:
 
 
 def load_radar_csv(path: Path, config: Optional[RadarConfig] = None) -> RadarSweep:
-    """loaders.py:46-101 (pandas C parser, like the reference)."""
-    import pandas as pd
+    """loaders.py:46-101: pd.read_csv(names=Status..Echo_n, skiprows=1) semantics through the
+    native parser; an empty CSV raises ValueError, a malformed one raises like read_csv."""
+    from .ingest import STATUS_EMPTY, STATUS_NON_NUMERIC, STATUS_OK, read_sweeps
 
     if config is None:
         config = RadarConfig()
-    cols = ["Status", "Scale", "Range", "Gain", "Angle"] + [
-        f"Echo_{i}" for i in range(config.num_echo_columns)]
-    df = pd.read_csv(path, header=None, names=cols, skiprows=1, engine="c")
-    if df.empty:
+    path = Path(path)
+    if not path.exists():
+        raise FileNotFoundError(f"[Errno 2] No such file or directory: '{path}'")
+    b = read_sweeps([path], bins=config.num_echo_columns)
+    st = int(b.status[0])
+    if st == STATUS_EMPTY:
         raise ValueError(f"CSV is empty: {path}")
-    angles_rad = np.deg2rad(df["Angle"].to_numpy(np.float32) * config.angle_scale)
-    echo = df.iloc[:, 5:].fillna(0).to_numpy(np.float32)
-    scale = df["Scale"].to_numpy(np.float32)
+    if st == STATUS_NON_NUMERIC:
+        raise ValueError(f"could not convert string to float in {path}")
+    if st != STATUS_OK:
+        raise ValueError(f"Error tokenizing data in {path}")
+    n = int(b.rows[0])
+    angles_rad = np.deg2rad(b.angle[0, :n] * config.angle_scale)
+    echo = b.echo[0, :n].astype(np.float32)
+    scale = b.scale[0, :n].copy()
     ranges = (scale[:, None] / echo.shape[1]) * np.arange(echo.shape[1], dtype=np.float32)
-    gain = None
-    gains = df["Gain"].unique()
-    if len(gains) == 1:
-        gain = int(gains[0])
+    g = float(b.gain[0])
+    gain = int(g) if np.isfinite(g) else None
     return RadarSweep(angles_rad=angles_rad, ranges=ranges, intensities=echo, scale=scale,
-                      gain=gain, source_path=Path(path))
+                      gain=gain, source_path=path)
 
 
 def load_ply(path: Path) -> PointCloud:

@@ -18,7 +18,13 @@ are reproducible.  Outputs (all in tests/golden/):
   g4_clusters.npz   st_dbscan(frames) per-frame Cluster lists in reference order (:443-536)
   g5_tracker.npz    ObjectTracker.update sequences (:543-688)
   g6_pipeline.npz   run_pipeline (:893-1038) CSV outputs on a 12-frame synthetic CSV stack
+  g7_ply.npz        3_stdbscan_point_clouds.process_one (:174-193) and radar_pipeline
+                    process_ply_clustering (processors/clustering.py:157-208) on synthetic PLY
+                    stacks (labels CSV text + stdout)
+  g8_fuse_max.npz   5_gain_fusion_ply_builder.fuse_gains_max (:222-273) on small CSV frames
   meta.json         library versions / CPU of the generating run
+
+    python tests/golden/make_golden.py [g7 g8 ...]   # only the named fixtures
 """
 from __future__ import annotations
 
@@ -375,6 +381,93 @@ def g6_pipeline(trk, tmp: Path):
     np.savez_compressed(OUT / "g6_pipeline.npz", **rec)
 
 
+def synth_ply(path: Path, seed: int, n_blobs: int = 8, with_color: bool = True):
+    """ASCII PLY stack like 2_build_point_clouds.py writes (x y z [red green blue]); z is an
+    intensity-like height, the colour is the gain tint (40/50/75) with a few off-palette ones."""
+    rng = np.random.default_rng(seed)
+    pal = np.array([(0, 114, 255), (0, 200, 83), (255, 87, 34)], np.int64)
+    pts, cols = [], []
+    for b in range(n_blobs):
+        c = rng.random(3) * [200, 200, 40]
+        m = int(rng.integers(30, 150))
+        pts.append(c + rng.normal(0, [2.0, 2.0, 1.0], (m, 3)))
+        cols.append(pal[rng.integers(0, 3, m)])
+    m = 400
+    pts.append(rng.random((m, 3)) * [220, 220, 40])
+    cols.append(rng.integers(0, 256, (m, 3)))
+    xyz = np.vstack(pts)
+    rgb = np.vstack(cols)
+    head = ["ply", "format ascii 1.0", f"element vertex {len(xyz)}", "property float x",
+            "property float y", "property float z"]
+    if with_color:
+        head += ["property uchar red", "property uchar green", "property uchar blue"]
+    head.append("end_header")
+    lines = []
+    for (x, y, z), (r, g, bl) in zip(xyz, rgb):
+        lines.append(f"{x:.4f} {y:.4f} {z:.4f}" + (f" {r} {g} {bl}" if with_color else ""))
+    path.write_text("\n".join(head + lines) + "\n")
+    return path
+
+
+def g7_ply(ref3, tmp: Path):
+    from radar_pipeline.processors.clustering import process_ply_clustering
+
+    rec = {}
+    for k, (seed, col) in enumerate(((707, True), (708, True), (709, False))):
+        d = tmp / f"c{k}"
+        d.mkdir(parents=True)
+        ply = synth_ply(d / "stack.ply", seed, with_color=col)
+        buf = io.StringIO()
+        with redirect_stdout(buf):
+            ref3.process_one(ply, "stack_dbscan", eps=ref3.EPS_SPACE,
+                             min_samples=ref3.MIN_SAMPLES, max_points=ref3.MAX_POINTS)
+        rec[f"c{k}_script_stdout"] = np.array(buf.getvalue())
+        rec[f"c{k}_script_csv"] = np.array((d / "stack_dbscan_labels.csv").read_text())
+        if col:  # the package loader needs RGB for infer_time_from_colors
+            out = d / "pkg"
+            out.mkdir()
+            buf = io.StringIO()
+            with redirect_stdout(buf):
+                csv_path, _ = process_ply_clustering(ply, out)
+            rec[f"c{k}_pkg_stdout"] = np.array(buf.getvalue())
+            rec[f"c{k}_pkg_csv"] = np.array(csv_path.read_text())
+    rec["n_cases"] = np.int64(3)
+    np.savez_compressed(OUT / "g7_ply.npz", **rec)
+
+
+def synth_fuse_frames(root: Path, F: int = 2, rows: int = 256, seed: int = 808):
+    """Small CSV frames (3 gains) for fuse_gains_max (regenerated by the tests)."""
+    rng = np.random.default_rng(seed)
+    angles = np.sort(rng.choice(8196, rows, replace=False))
+    frames = []
+    for f in range(F):
+        ff = {}
+        for k, g in enumerate((40, 50, 75)):
+            echo = np.zeros((rows, 1024), np.int64)
+            m = rng.random((rows, 1024)) < 0.05
+            echo[m] = rng.integers(0, 256, m.sum())
+            d = root / f"gain_{g}"
+            d.mkdir(parents=True, exist_ok=True)
+            p = d / f"20250813_1426{10 + 3 * f:02d}_{100 * k:03d}.csv"
+            write_csv(p, 1, np.full(rows, [231.5, 115.75, 463.0][f % 3]), 0, g, angles, echo)
+            ff[g] = p
+        frames.append(ff)
+    return frames
+
+
+def g8_fuse_max(tmp: Path):
+    fuse = _load("ref_fusion5", REF / "PointCloudWork" / "5_gain_fusion_ply_builder.py")
+    frames = synth_fuse_frames(tmp / "fuse")
+    rec = {}
+    for f, ff in enumerate(frames):
+        for res in (1.0, 2.5):
+            x, y, i = fuse.fuse_gains_max(ff, grid_resolution=res)
+            key = f"f{f}_r{str(res).replace('.', '_')}"
+            rec[key + "_x"], rec[key + "_y"], rec[key + "_i"] = x, y, i
+    rec["n_frames"] = np.int64(len(frames))
+    np.savez_compressed(OUT / "g8_fuse_max.npz", **rec)
+
+
 def main():
     if not REF.exists():
         raise SystemExit("make_golden.py must run where /root/reference exists (build container)")
@@ -383,19 +476,36 @@ def main():
     trk = _load("ref_tracker4", REF / "PointCloudWork" / "4_temporal_object_tracker.py")
     ref3 = _load("ref_stdbscan3", REF / "PointCloudWork" / "3_stdbscan_point_clouds.py")
     from radar_pipeline.core import loaders as rp_loaders, transforms as rp_transforms
+    only = set(sys.argv[1:])
+    want = lambda name: not only or name in only  # noqa: E731
+    n = None
     with tempfile.TemporaryDirectory() as td:
         tmp = Path(td)
-        g1_polar(trk, rp_loaders, rp_transforms, tmp / "g1")
-        n = g2_stdbscan(ref3)
-        g3_land(trk)
-        g4_clusters(trk)
-        g5_tracker(trk)
-        g6_pipeline(trk, tmp / "g6")
+        if want("g1"):
+            g1_polar(trk, rp_loaders, rp_transforms, tmp / "g1")
+        if want("g2"):
+            n = g2_stdbscan(ref3)
+        if want("g3"):
+            g3_land(trk)
+        if want("g4"):
+            g4_clusters(trk)
+        if want("g5"):
+            g5_tracker(trk)
+        if want("g6"):
+            g6_pipeline(trk, tmp / "g6")
+        if want("g7"):
+            g7_ply(ref3, tmp / "g7")
+        if want("g8"):
+            g8_fuse_max(tmp / "g8")
     import scipy
     import sklearn
-    meta = {"numpy": np.__version__, "scipy": scipy.__version__, "sklearn": sklearn.__version__,
-            "python": platform.python_version(), "cpu": platform.processor() or platform.machine(),
-            "g2_cases": n}
+    mp = OUT / "meta.json"
+    meta = json.loads(mp.read_text()) if mp.exists() else {}
+    meta.update({"numpy": np.__version__, "scipy": scipy.__version__,
+                 "sklearn": sklearn.__version__, "python": platform.python_version(),
+                 "cpu": platform.processor() or platform.machine()})
+    if n is not None:
+        meta["g2_cases"] = n
     (OUT / "meta.json").write_text(json.dumps(meta, indent=1) + "\n")
     for p in sorted(OUT.glob("*.npz")):
         print(f"{p.name}: {p.stat().st_size / 1024:.1f} KiB")

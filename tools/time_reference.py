@@ -1,0 +1,168 @@
+#!/usr/bin/env python3
+"""Times THE REFERENCE ITSELF (the sklearn/scipy CPU path) in the build container, on the bench's
+own synthetic inputs, and writes profiles/r2/reference_cpu.json (bench.py reports it as
+`cpu_baseline.reference_measured`).  The reference never travels to the GPU box; only the JSON
+written here does.
+
+    PYTHONDONTWRITEBYTECODE=1 python tools/time_reference.py [--budget-s 600]
+
+Legs (SURVEY.md §8(d) "reference CPU baseline"):
+  csv_build_frame  build_frame (:312-352) on one frame's three 4096x1029 CSVs (pandas parse +
+                   numpy polar arithmetic), i.e. the reference's real-file cost per frame
+  configs[0]       3_stdbscan_point_clouds.st_dbscan (:101-136) on one synthetic gain_40 sweep
+                   (eps 8 / eps_t 2 / min 15), and 4_temporal_object_tracker st_dbscan + tracker
+  configs[1]       4_temporal_object_tracker st_dbscan (:443-536) + ObjectTracker (:543-688) on one
+                   fused frame
+  prefix_k         the same on the first k frames of the bench's 100-frame stack (configs[2]) for
+                   k = 2, 3, ... while a run stays within the budget; the reference builds one
+                   spatial BallTree over ALL frames (:474-475), so its time and memory grow
+                   ~k^2 per point: these rates are NOT extrapolable to 100 or 1000 frames.
+Points are built by the oracle's restatement of load_radar_csv's arithmetic (pinned bit-exact
+to the reference by tests/test_oracle_golden.py) so no CSV round trip sits inside the timed
+clustering legs.  One process, one thread (the reference is single-threaded on this path).
+"""
+from __future__ import annotations
+
+import argparse
+import importlib.util
+import json
+import os
+import platform
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+REF = Path("/root/reference")
+ROOT = Path(__file__).resolve().parents[1]
+for _p in (str(ROOT / "radar-point-cloud-tracking_amd"), str(ROOT), str(ROOT / "tests" / "golden")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+sys.dont_write_bytecode = True
+
+import numpy as np  # noqa: E402
+
+
+def _load(name: str, path: Path):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _cpu_model() -> str:
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def _frames(trk, echo, cfg, geo, fid0=0):
+    from oracle import path as op
+
+    R = cfg.rows
+    per_frame = [{g: op.polar_scatter(echo[f, k], np.full(R, cfg.scale, np.float32),
+                                      geo.cos_t, geo.sin_t) for k, g in enumerate(cfg.gains)}
+                 for f in range(echo.shape[0])]
+    return [trk.RadarFrame(timestamp=None, timestamp_ms=(fid0 + fid) * 3000, frame_id=fid0 + fid,
+                           points=p, gains=g) for fid, p, g in op.build_frames(per_frame)]
+
+
+def _cluster_track(trk, frames):
+    t0 = time.perf_counter()
+    cbf = trk.st_dbscan(frames, trk.EPS_SPACE, trk.EPS_TIME, trk.MIN_SAMPLES)
+    t1 = time.perf_counter()
+    tr = trk.ObjectTracker()
+    for fr in frames:
+        tr.update(cbf.get(fr.frame_id, []), fr.frame_id)
+    t2 = time.perf_counter()
+    n = sum(f.num_points for f in frames)
+    return {"points": n, "frames": len(frames), "st_dbscan_s": round(t1 - t0, 3),
+            "tracker_s": round(t2 - t1, 3), "total_s": round(t2 - t0, 3),
+            "mpoints_per_s": round(n / (t2 - t0) / 1e6, 6),
+            "clusters": sum(len(v) for v in cbf.values()), "objects": len(tr.objects)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--budget-s", type=float, default=600.0)
+    ap.add_argument("--max-prefix", type=int, default=6)
+    ap.add_argument("--out", default=str(ROOT / "profiles" / "r2" / "reference_cpu.json"))
+    args = ap.parse_args()
+    if not REF.exists():
+        raise SystemExit("time_reference.py must run where /root/reference exists (build container)")
+    os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
+    trk = _load("ref_tracker4", REF / "PointCloudWork" / "4_temporal_object_tracker.py")
+    ref3 = _load("ref_stdbscan3", REF / "PointCloudWork" / "3_stdbscan_point_clouds.py")
+    from make_golden import write_csv
+    from rpt.synth import SynthConfig, make_geometry, numpy_echo
+
+    out = {"what": "the reference CPU path itself (PointCloudWork/*.py, sklearn BallTree + scipy "
+                   "LSAP), one thread, in the build container",
+           "cpu_model": _cpu_model(), "cpu_count": os.cpu_count(), "threads_used": 1,
+           "numpy": np.__version__, "python": platform.python_version(), "legs": {}}
+    legs = out["legs"]
+
+    def save():
+        Path(args.out).parent.mkdir(parents=True, exist_ok=True)
+        Path(args.out).write_text(json.dumps(out, indent=1) + "\n")
+
+    # --- configs[0]: one gain_40 sweep
+    cfg = SynthConfig(n_frames=1, gains=(40,))
+    geo = make_geometry(cfg)
+    echo = numpy_echo(cfg, geo)
+    frames = _frames(trk, echo, cfg, geo)
+    xy = frames[0].points[:, :2].astype(np.float32)
+    t0 = time.perf_counter()
+    ref3.st_dbscan(xy, np.zeros(len(xy), np.float32), eps_space=8.0, eps_time=2.0, min_samples=15)
+    dt = time.perf_counter() - t0
+    legs["configs0_3_stdbscan"] = {"points": len(xy), "total_s": round(dt, 3),
+                                   "mpoints_per_s": round(len(xy) / dt / 1e6, 6)}
+    legs["configs0_tracker_path"] = _cluster_track(trk, frames)
+    print("configs[0]", legs["configs0_3_stdbscan"], legs["configs0_tracker_path"], flush=True)
+    save()
+
+    # --- CSV ingest of one full frame (3 gains), the reference's load_radar_csv + build_frame
+    cfg = SynthConfig(n_frames=100)
+    geo = make_geometry(cfg)
+    e1 = numpy_echo(cfg, geo, frames=range(0, 1))
+    with tempfile.TemporaryDirectory() as td:
+        files = {}
+        for k, g in enumerate(cfg.gains):
+            d = Path(td) / f"gain_{g}"
+            d.mkdir()
+            p = d / f"20250813_142602_{100 * k:03d}.csv"
+            write_csv(p, 1, np.full(cfg.rows, cfg.scale), 0, g, geo.angle.astype(np.int64), e1[0, k])
+            files[g] = p
+        t0 = time.perf_counter()
+        fr = trk.build_frame(files, 0)
+        dt = time.perf_counter() - t0
+    legs["csv_build_frame"] = {"points": int(fr.num_points), "files": 3, "rows": cfg.rows,
+                               "total_s": round(dt, 3)}
+    print("csv build_frame", legs["csv_build_frame"], flush=True)
+
+    # --- configs[1]: one fused frame; then prefixes of the bench stack
+    legs["configs1_fused_frame"] = _cluster_track(trk, _frames(trk, e1, cfg, geo))
+    print("configs[1]", legs["configs1_fused_frame"], flush=True)
+    save()
+    last = legs["configs1_fused_frame"]["total_s"]
+    for k in range(2, args.max_prefix + 1):
+        # time grows ~k^2 (spatial BallTree over all frames, :474-475): stop before the budget
+        if last * (k / (k - 1)) ** 2 > args.budget_s:
+            legs[f"prefix_{k}_skipped"] = f"projected {last * (k / (k - 1)) ** 2:.0f} s > budget"
+            break
+        e = numpy_echo(cfg, geo, frames=range(0, k))
+        r = _cluster_track(trk, _frames(trk, e, cfg, geo))
+        legs[f"prefix_{k}"] = r
+        last = r["total_s"]
+        print(f"prefix {k}", r, flush=True)
+        save()
+    save()
+
+
+if __name__ == "__main__":
+    main()
