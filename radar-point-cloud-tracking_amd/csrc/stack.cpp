@@ -10,6 +10,7 @@
 // back in one packed copy.  Buffers are owned by the handle and grow only.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -18,17 +19,19 @@
 namespace rpt {
 int32_t polar_count(const void* echo, int32_t dt, int64_t n_files, int32_t rows, int32_t bins,
                     float thr, int32_t stride, int64_t* row_prefix, int64_t* file_offsets,
-                    int64_t* total_host, hipStream_t st);
+                    int64_t* total_host, hipStream_t st, uint64_t* masks);
 int32_t polar_write_cap(const uint8_t* echo, int64_t n_files, int32_t rows, float thr,
                         int32_t stride, const float* scale, const float* cos_t,
                         const float* sin_t, const int32_t* gain, const int64_t* row_prefix,
                         const int64_t* file_offsets, int32_t fpf, float* x, float* y, float* v,
-                        int32_t* gout, int32_t* pf, int64_t cap, hipStream_t st);
+                        int32_t* gout, int32_t* pf, int64_t cap, hipStream_t st,
+                        const uint64_t* masks);
 int32_t polar_write(const void* echo, int32_t dt, int64_t n_files, int32_t rows, int32_t bins,
                     const float* scale, const float* cos_t, const float* sin_t,
                     const int32_t* gain, float thr, int32_t stride, const int64_t* row_prefix,
                     const int64_t* file_offsets, int32_t files_per_frame, float* x, float* y,
-                    float* v, int32_t* gout, int32_t* pf, hipStream_t st);
+                    float* v, int32_t* gout, int32_t* pf, hipStream_t st, const uint64_t* masks);
+int64_t polar_mask_words(int64_t n_files, int32_t rows);
 int32_t frame_times(const int32_t* pf, int64_t n, const int64_t* ids, float* t, hipStream_t st);
 int32_t bounds_xy(const float* x, const float* y, int64_t n, float* out4, hipStream_t st);
 int32_t land_grid_cells(const float* x, const float* y, const float* val, int64_t n,
@@ -215,6 +218,8 @@ struct rpt_stack {
   DevBuf<int32_t> g, pf, g2, pf2, labels, land_cnt, land_cell, seg_frame, seg_label;
   DevBuf<double> land_tot, edges;
   DevBuf<uint8_t> land_mask;
+  DevBuf<uint64_t> masks;              // K1 keep masks (count pass -> write pass)
+  int k1_masks = -1;                   // RPT_K1_MASKS, read once
   DevBuf<uint8_t> bnd;                 // ST-DBSCAN bounds (+ partials) of the kept points
   std::vector<char> dbscan_bounds;     // their host copy, from the land readback
   PinnedBuf up, down;  // host staging: uploads (edges, offsets), readbacks
@@ -282,15 +287,28 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
   RPT_TRY(down.ensure(sizeof(int64_t) * (size_t)(n_files + 2 * F + 8), st));
   int64_t* hfo = reinterpret_cast<int64_t*>(down.p);
   RPT_TRY(row_prefix.ensure((size_t)n_files * p.rows + 1, st));
+  // u8 sweeps of 1024 bins, RPT_K1_MASKS=1: the count pass keeps the keep masks (1/8 of the echo)
+  // for the write pass, which then reads the echo only where it emits.  Off by default: the
+  // write pass is latency-bound, not bandwidth-bound, so it gained less (-0.5 ms at 1000 frames)
+  // than the mask stores cost the count pass (+0.3-0.6 ms) (profiles/r2/ab_k5_k1.md)
+  const bool grouped = p.echo_dtype == RPT_ECHO_U8 && p.bins == 1024 &&
+                       (uintptr_t)echo % 16 == 0;
+  if (k1_masks < 0) {
+    const char* e = std::getenv("RPT_K1_MASKS");
+    k1_masks = (e && std::atoi(e) != 0) ? 1 : 0;
+  }
+  uint64_t* mk = nullptr;
+  if (grouped && k1_masks) {
+    RPT_TRY(masks.ensure((size_t)polar_mask_words(n_files, p.rows), st));
+    mk = masks.p;
+  }
   RPT_TRY(polar_count(echo, p.echo_dtype, n_files, p.rows, p.bins, p.threshold, p.stride,
-                      row_prefix.p, file_off.p, nullptr, st));
+                      row_prefix.p, file_off.p, nullptr, st, mk));
   RPT_HIP(hipMemcpyAsync(hfo, file_off.p, sizeof(int64_t) * (n_files + 1), hipMemcpyDeviceToHost,
                          st));
   // u8 sweeps of 1024 bins, outputs sized by an earlier run: the write is queued right behind
   // the readback (capacity-bounded) instead of after the host has seen the count; when the
   // count exceeds the capacity the buffers grow and the write runs again
-  const bool grouped = p.echo_dtype == RPT_ECHO_U8 && p.bins == 1024 &&
-                       (uintptr_t)echo % 16 == 0;
   int64_t spec_cap = -1;
   if (grouped && x.p && y.p && v.p && g.p && pf.p) {
     spec_cap = (int64_t)std::min({x.cap, y.cap, v.cap, g.cap, pf.cap});
@@ -298,7 +316,7 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
     RPT_HIP(hipEventRecord(ev_rb, st));
     RPT_TRY(polar_write_cap((const uint8_t*)echo, n_files, p.rows, p.threshold, p.stride, scale,
                             cos_t, sin_t, gain, row_prefix.p, file_off.p, G, x.p, y.p, v.p,
-                            gain ? g.p : nullptr, pf.p, spec_cap, st));
+                            gain ? g.p : nullptr, pf.p, spec_cap, st, mk));
     RPT_HIP(hipEventSynchronize(ev_rb));  // the readback only; the write keeps running
   } else {
     RPT_TRY(wait_stream(st));
@@ -319,7 +337,7 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
     RPT_TRY(pf.ensure(cap, st));
     RPT_TRY(polar_write(echo, p.echo_dtype, n_files, p.rows, p.bins, scale, cos_t, sin_t, gain,
                         p.threshold, p.stride, row_prefix.p, file_off.p, G, x.p, y.p, v.p,
-                        gain ? g.p : nullptr, pf.p, st));
+                        gain ? g.p : nullptr, pf.p, st, mk));
   }
   if (timing) RPT_HIP(hipEventRecord(ev[1], st));
   if (N == 0) {

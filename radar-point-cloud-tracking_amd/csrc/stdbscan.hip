@@ -903,6 +903,21 @@ __global__ __launch_bounds__(kBlock) void k_core_cell_window(Geom g,
   }
 }
 
+// core flags v of the points [b, e) of one cell, by `lanes` lanes (j = this lane's index): bytes at
+// the unaligned ends, dwords inside (cells list their points contiguously in sorted order)
+__device__ __forceinline__ void write_cell_flags(uint8_t* __restrict__ core, int b, int e, int j,
+                                                 int lanes, uint8_t v) {
+  const int wb = (b + 3) & ~3, we = e & ~3;
+  if (wb >= we) {
+    for (int s = b + j; s < e; s += lanes) core[s] = v;
+    return;
+  }
+  for (int s = b + j; s < wb; s += lanes) core[s] = v;
+  const uint32_t vv = v ? 0x01010101u : 0u;
+  for (int w = wb + 4 * j; w < we; w += 4 * lanes) *reinterpret_cast<uint32_t*>(core + w) = vv;
+  for (int s = we + j; s < e; s += lanes) core[s] = v;
+}
+
 // 2-D grids whose slab window is at most 7 slabs (R <= 3): K5 levels 1-3 in one kernel, EIGHT
 // lanes per occupied cell.  A mutual cell with >= min_samples points is all core (the bulk);
 // otherwise lane j < 2R+1 owns slab cs - R + j of the cell's window.  The window comes from the
@@ -920,10 +935,11 @@ __global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
                                                           const uint32_t* __restrict__ occ_bits,
                                                           const float2* __restrict__ slab_t,
                                                           int32_t* __restrict__ cflag,
-                                                          int32_t* __restrict__ zero_counter) {
-  // the level-4 queue counter, zeroed here instead of by a memset launch (k_core_fill, the next
-  // kernel on the stream, is its first user)
-  if (blockIdx.x == 0 && threadIdx.x == 0) *zero_counter = 0;
+                                                          int32_t* __restrict__ zero_counter,
+                                                          uint8_t* __restrict__ core) {
+  // legacy pipeline: the level-4 queue counter, zeroed here instead of by a memset launch
+  // (k_core_fill, the next kernel on the stream, is its first user)
+  if (zero_counter && blockIdx.x == 0 && threadIdx.x == 0) *zero_counter = 0;
   const int64_t no = *n_occ;
   const int need = g.min_samples;
   const int j = threadIdx.x & 7;
@@ -935,6 +951,9 @@ __global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
     int flag = 0, b = 0, e = 0;
     if (act && (int64_t)ca >= g.cells) {  // non-finite time: no neighbours at all
       flag = (need <= 0) ? 1 : 0;
+      const CellRec<2> ri = crec[ca];
+      b = ri.b;
+      e = ri.e;
     } else if (act) {
       const int cx = ca % g.nx;
       const int rr = ca / g.nx;
@@ -979,15 +998,20 @@ __global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
           const float4 A1 = rec_boxA<2>(ra), A2 = rec_boxB(ra);
 #pragma unroll
           for (int dy = 0; dy < 5; ++dy) {
-            uint32_t m = m5[dy];
+            const uint32_t m = m5[dy];
+            if (!m) continue;
             const int64_t row = ((int64_t)sl * g.ny + (cy + dy - 2)) * g.nx + (cx - 2);
-            while (m) {
-              const int dx = __builtin_ctz(m);
-              m &= m - 1u;
-              const CellRec<2> cr = crec[row + dx];
-              const int cls = classify_cells<2>(A1, rec_boxA<2>(cr), A2, rec_boxB(cr), g);
-              lo += (cls == 1) ? cr.e - cr.b : 0;
-              hi += (cls != 0) ? cr.e - cr.b : 0;
+            // the row's (up to 5) candidate records in flight together, then classified
+            CellRec<2> cr[5];
+#pragma unroll
+            for (int dx = 0; dx < 5; ++dx)
+              if ((m >> dx) & 1u) cr[dx] = crec[row + dx];
+#pragma unroll
+            for (int dx = 0; dx < 5; ++dx) {
+              if (!((m >> dx) & 1u)) continue;
+              const int cls = classify_cells<2>(A1, rec_boxA<2>(cr[dx]), A2, rec_boxB(cr[dx]), g);
+              lo += (cls == 1) ? cr[dx].e - cr[dx].b : 0;
+              hi += (cls != 0) ? cr[dx].e - cr[dx].b : 0;
             }
           }
         }
@@ -1000,11 +1024,15 @@ __global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
       }
     }
     if (act && j == 0) cflag[ca] = flag;
+    // decided cells write their points' flags here (the undecided ones are k_core_slow_cells')
+    if (core && act && flag != 2) write_cell_flags(core, b, e, j, 8, (uint8_t)flag);
   }
 }
 
 // Level 3, one thread per point: the cell's decision; points of undecided cells are queued for
-// level 4 (block-aggregated append).
+// level 4 (block-aggregated append; QUEUE = false: the undecided cells are left to
+// k_core_slow_cells).
+template <bool QUEUE>
 __global__ __launch_bounds__(kBlock) void k_core_fill(const int32_t* __restrict__ skey, int64_t n,
                                                      const int32_t* __restrict__ cflag,
                                                      uint8_t* __restrict__ core,
@@ -1030,7 +1058,7 @@ __global__ __launch_bounds__(kBlock) void k_core_fill(const int32_t* __restrict_
       if (s < n) core[s] = (f[k] == 1) ? 1 : 0;
       bits |= (f[k] == 2) ? (1u << k) : 0u;
     }
-    block_append_bits(tile, bits, slow, n_slow);
+    if (QUEUE) block_append_bits(tile, bits, slow, n_slow);
   }
 }
 
@@ -1102,6 +1130,158 @@ __global__ __launch_bounds__(kBlock) void k_core_slow(const float4* __restrict__
       }
     }
     if (lane == 0) core[s] = (cnt >= need) ? 1 : 0;
+  }
+}
+
+// Level 4 by cells: waves stride over the occupied cells (no queue: a cell flag read per occupied
+// cell replaces the per-point fill + append), and every undecided cell (flag 2) is
+// settled by its wave: the cell's candidate window, box-classified against the CELL once, stays
+// in registers (up to 64*kR candidate cells) while the wave walks the cell's points -- per point
+// a box test per candidate (whole-cell accept adds the count), then the undecided candidates'
+// points 64 at a time, stopping at min_samples.  Windows larger than 64*kR cells fall back to the
+// per-point window walk of k_core_slow.
+template <int D>
+__device__ __forceinline__ int core_count_point(const float4& p, int32_t key,
+                                                const float4* __restrict__ pts, const Geom& g,
+                                                const CellRec<D>* __restrict__ crec,
+                                                const uint32_t* __restrict__ occ_bits,
+                                                const float2* __restrict__ slab_t) {
+  const int lane = threadIdx.x & 63;
+  const int need = g.min_samples;
+  int cx, cy, cz;
+  decode_key<D>(key, g, cx, cy, cz);
+  const Window w = make_window<D, false>(cx, cy, cz, p.w, p.w, g, slab_t);
+  int cnt = 0;
+  for (int base = 0; base < w.total && cnt < need; base += 64 * kR) {
+    int64_t c[kR];
+    uint32_t wb[kR];
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const int qq = base + r * 64 + lane;
+      c[r] = (qq < w.total) ? window_cell<D>(w, qq, g, slab_t, p.w, p.w) : -1;
+    }
+#pragma unroll
+    for (int r = 0; r < kR; ++r) wb[r] = (c[r] >= 0) ? occ_bits[c[r] >> 5] : 0u;
+    int b[kR], e[kR], cls[kR];
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      b[r] = e[r] = cls[r] = 0;
+      if (c[r] >= 0 && ((wb[r] >> (c[r] & 31)) & 1u)) {
+        const CellRec<D> cr = crec[c[r]];
+        b[r] = cr.b;
+        e[r] = cr.e;
+        cls[r] = classify<D>(p, rec_boxA<D>(cr), rec_boxB(cr), g);
+      }
+    }
+    int add = 0;
+#pragma unroll
+    for (int r = 0; r < kR; ++r) add += (cls[r] == 1) ? e[r] - b[r] : 0;
+    cnt += wave_sum(add);
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      uint64_t pm = __ballot(cls[r] == 2);
+      while (pm && cnt < need) {
+        const int l = __ffsll((unsigned long long)pm) - 1;
+        pm &= pm - 1;
+        const int bb = __shfl(b[r], l), ee = __shfl(e[r], l);
+        for (int j0 = bb; j0 < ee && cnt < need; j0 += 64) {
+          const int j = j0 + lane;
+          cnt += __popcll(__ballot((j < ee) && adjacent<D>(p, pts[j], g)));
+        }
+      }
+    }
+  }
+  return cnt;
+}
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_core_slow_cells(const float4* __restrict__ pts, Geom g,
+                                                           const CellRec<D>* __restrict__ crec,
+                                                           const uint32_t* __restrict__ occ_bits,
+                                                           const float2* __restrict__ slab_t,
+                                                           const int32_t* __restrict__ occ,
+                                                           const int32_t* __restrict__ n_occ,
+                                                           const int32_t* __restrict__ cflag,
+                                                           uint8_t* __restrict__ core) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+  const int64_t no = *n_occ;
+  const int need = g.min_samples;
+  // lane l of wave w looks at occupied cell w + l*nw (+ 64*nw per round): undecided cells are
+  // spatially clustered, i.e. consecutive in the occupied list, and this spreads them over all
+  // waves instead of handing a cluster of them to one wave
+  for (int64_t q0 = w0; q0 < no; q0 += nw * 64) {
+    const int64_t q = q0 + (int64_t)lane * nw;
+    const int32_t cq = (q < no) ? occ[q] : -1;
+    uint64_t um = __ballot(cq >= 0 && (int64_t)cq < g.cells && cflag[cq] == 2);
+    while (um) {
+      const int l = __ffsll((unsigned long long)um) - 1;
+      um &= um - 1;
+      const int32_t ca = __builtin_amdgcn_readlane(cq, l);
+      const CellRec<D> ra = crec[ca];
+      const float4 A1 = rec_boxA<D>(ra), A2 = rec_boxB(ra);
+      int cx, cy, cz;
+      decode_key<D>(ca, g, cx, cy, cz);
+      const Window w = make_window<D, true>(cx, cy, cz, A2.z, A2.w, g, slab_t);
+      if (w.total > 64 * kR) {  // wide windows: the per-point walk
+        for (int s = ra.b; s < ra.e; ++s) {
+          const int cnt = core_count_point<D>(pts[s], ca, pts, g, crec, occ_bits, slab_t);
+          if (lane == 0) core[s] = (cnt >= need) ? 1 : 0;
+        }
+        continue;
+      }
+      // the window's candidate cells that may hold a neighbour of SOME point of the cell
+      float4 cA[kR], cB[kR];
+      int cb[kR], ce[kR];
+      int64_t c[kR];
+      uint32_t wb[kR];
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        const int qq = r * 64 + lane;
+        c[r] = (qq < w.total) ? window_cell<D>(w, qq, g, slab_t, A2.z, A2.w) : -1;
+      }
+#pragma unroll
+      for (int r = 0; r < kR; ++r) wb[r] = (c[r] >= 0) ? occ_bits[c[r] >> 5] : 0u;
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        cb[r] = ce[r] = 0;
+        cA[r] = cB[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (c[r] >= 0 && ((wb[r] >> (c[r] & 31)) & 1u)) {
+          const CellRec<D> cr = crec[c[r]];
+          if (classify_cells<D>(A1, rec_boxA<D>(cr), A2, rec_boxB(cr), g) != 0) {
+            cb[r] = cr.b;
+            ce[r] = cr.e;
+            cA[r] = rec_boxA<D>(cr);
+            cB[r] = rec_boxB(cr);
+          }
+        }
+      }
+      for (int s = ra.b; s < ra.e; ++s) {
+        const float4 p = pts[s];
+        int cls[kR];
+#pragma unroll
+        for (int r = 0; r < kR; ++r) cls[r] = (ce[r] > cb[r]) ? classify<D>(p, cA[r], cB[r], g) : 0;
+        int add = 0;
+#pragma unroll
+        for (int r = 0; r < kR; ++r) add += (cls[r] == 1) ? ce[r] - cb[r] : 0;
+        int cnt = wave_sum(add);
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+          uint64_t pm = __ballot(cls[r] == 2);
+          while (pm && cnt < need) {
+            const int l2 = __ffsll((unsigned long long)pm) - 1;
+            pm &= pm - 1;
+            const int bb = __shfl(cb[r], l2), ee = __shfl(ce[r], l2);
+            for (int j0 = bb; j0 < ee && cnt < need; j0 += 64) {
+              const int j = j0 + lane;
+              cnt += __popcll(__ballot((j < ee) && adjacent<D>(p, pts[j], g)));
+            }
+          }
+        }
+        if (lane == 0) core[s] = (cnt >= need) ? 1 : 0;
+      }
+    }
   }
 }
 
@@ -1653,6 +1833,8 @@ struct DbscanState {
   void* crec = nullptr;                      // CellRec<dim>[C + 1]
   uint32_t* occ_bits = nullptr;              // 1 bit per cell
   int uf_flags = -1;                         // see XcdRange; -1 = read RPT_UF_FLAGS once
+  int k5_legacy = -1;                        // 1: round-1 K5 (fill + point queue); RPT_K5_MODE
+  int k5_fill = 0;
   template <int D>
   const CellRec<D>* rec() const {
     return static_cast<const CellRec<D>*>(crec);
@@ -1860,12 +2042,57 @@ int32_t DbscanState::core_pass(hipStream_t st) {
   int32_t* slow = nc_list;
   int32_t* n_slow = nc_list + n;
   const int32_t* n_occ = hpos + n;
+  if (k5_legacy < 0) {  // RPT_K5_MODE: 0 round-1 queue pipeline, 1 cells write point flags,
+                        // 2 cells + point-flag fill (no queue); both 1/2 end in k_core_slow_cells
+    // default 0: the folded variants measured no faster on the 100- and 1000-frame stacks
+    // (profiles/r2/ab_k5_k1.md): the per-point flag writes moved into the cell kernel cost what
+    // the fill pass cost, and the cell-wise slow pass balances worse than the point queue
+    const char* e = std::getenv("RPT_K5_MODE");
+    k5_legacy = e ? std::atoi(e) : 0;
+    k5_legacy = (k5_legacy == 0) ? 1 : 0;
+    k5_fill = (e && std::atoi(e) == 2) ? 1 : 0;
+  }
   // slabs each side a cell's points can reach: eps_t / slab width, +1 for the slab's extent
   const double rs = std::ceil((double)g.epst / g.ct) + 1.0;
-  if (dim == 2 && rs <= (double)kCwMaxR && g.nz == 1) {
+  const bool oct = dim == 2 && rs <= (double)kCwMaxR && g.nz == 1;
+  if (!k5_legacy) {
+    // cells decide (and write their points' flags) in one pass; the undecided cells' points are
+    // settled by k_core_slow_cells, which walks the occupied cells itself (no queue, no fill)
+    if (oct) {
+      hipLaunchKernelGGL(k_core_cells_oct, dim3(grid_for(8 * n, kBlock, 8192)), dim3(kBlock), 0,
+                         st, g, (int)rs, occ, n_occ, rec<2>(), mutual, occ_bits, slab_t, cflag,
+                         (int32_t*)nullptr, k5_fill ? (uint8_t*)nullptr : core);
+      if (k5_fill)
+        hipLaunchKernelGGL(k_core_fill<false>, dim3(tile_grid(n)), dim3(kBlock), 0, st, skey, n,
+                           cflag, core, slow, n_slow);
+    } else {
+      RPT_HIP(hipMemsetAsync(n_cq, 0, sizeof(int32_t), st));
+      hipLaunchKernelGGL(k_core_cell_fast, dim3(tile_grid(n)), dim3(kBlock), 0, st, occ, n_occ,
+                         g, cell_start, mutual, cflag, cq, n_cq);
+      if (dim == 2)
+        hipLaunchKernelGGL(k_core_cell_window<2>, dim3(wave_grid(n)), dim3(kBlock), 0, st, g,
+                           occ, rec<2>(), occ_bits, slab_t, cq, n_cq, cflag);
+      else
+        hipLaunchKernelGGL(k_core_cell_window<3>, dim3(wave_grid(n)), dim3(kBlock), 0, st, g,
+                           occ, rec<3>(), occ_bits, slab_t, cq, n_cq, cflag);
+      hipLaunchKernelGGL(k_core_fill<false>, dim3(tile_grid(n)), dim3(kBlock), 0, st, skey, n,
+                         cflag, core, slow, n_slow);
+    }
+    const int gs = wave_grid(n);
+    if (dim == 2)
+      hipLaunchKernelGGL(k_core_slow_cells<2>, dim3(gs), dim3(kBlock), 0, st, pts, g, rec<2>(),
+                         occ_bits, slab_t, occ, n_occ, cflag, core);
+    else
+      hipLaunchKernelGGL(k_core_slow_cells<3>, dim3(gs), dim3(kBlock), 0, st, pts, g, rec<3>(),
+                         occ_bits, slab_t, occ, n_occ, cflag, core);
+    RPT_CHECK_LAUNCH();
+    tm.mark();
+    return RPT_OK;
+  }
+  if (oct) {
     hipLaunchKernelGGL(k_core_cells_oct, dim3(grid_for(8 * n, kBlock, 8192)), dim3(kBlock), 0,
                        st, g, (int)rs, occ, n_occ, rec<2>(), mutual, occ_bits, slab_t, cflag,
-                       n_slow);
+                       n_slow, (uint8_t*)nullptr);
   } else {
     RPT_HIP(hipMemsetAsync(n_slow, 0, sizeof(int32_t), st));
     RPT_HIP(hipMemsetAsync(n_cq, 0, sizeof(int32_t), st));
@@ -1878,8 +2105,8 @@ int32_t DbscanState::core_pass(hipStream_t st) {
       hipLaunchKernelGGL(k_core_cell_window<3>, dim3(wave_grid(n)), dim3(kBlock), 0, st, g, occ,
                          rec<3>(), occ_bits, slab_t, cq, n_cq, cflag);
   }
-  hipLaunchKernelGGL(k_core_fill, dim3(tile_grid(n)), dim3(kBlock), 0, st, skey, n, cflag, core,
-                     slow, n_slow);
+  hipLaunchKernelGGL(k_core_fill<true>, dim3(tile_grid(n)), dim3(kBlock), 0, st, skey, n, cflag,
+                     core, slow, n_slow);
   if (dim == 2)
     hipLaunchKernelGGL(k_core_slow<2>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
                        rec<2>(), occ_bits, slab_t, slow, n_slow, core);

@@ -16,8 +16,9 @@ from _stack_check import oracle_stack as _oracle_stack
 pytestmark = pytest.mark.gpu
 
 
-def _k1(dev, echo, scale, angle, gains=(0,), threshold=10.0, stride=4, f32=False):
-    """Run rpt_polar_count/write on a batch of equally shaped sweeps."""
+def _k1(dev, echo, scale, angle, gains=(0,), threshold=10.0, stride=4, f32=False, masked=False):
+    """Run rpt_polar_count/write (or their keep-mask variants) on a batch of equally shaped
+    sweeps."""
     from rpt import _abi
     from rpt._device import stream_handle
     from rpt.core.transforms import trig_tables
@@ -41,17 +42,27 @@ def _k1(dev, echo, scale, angle, gains=(0,), threshold=10.0, stride=4, f32=False
     tot = _abi.C.c_int64(0)
     dt = _abi.ECHO_F32 if f32 else _abi.ECHO_U8
     st = stream_handle(dev)
-    _abi.check(lib.rpt_polar_count(ed.data_ptr(), dt, nf, rows, bins, threshold, stride,
-                                   rp.data_ptr(), fo.data_ptr(), _abi.C.byref(tot), st))
+    mk = torch.zeros(max(int(lib.rpt_polar_mask_words(nf, rows)), 1), dtype=torch.int64,
+                     device=dev) if masked else None
+    if masked:
+        _abi.check(lib.rpt_polar_count_masked(ed.data_ptr(), dt, nf, rows, bins, threshold,
+                                              stride, rp.data_ptr(), fo.data_ptr(),
+                                              _abi.C.byref(tot), mk.data_ptr(), st))
+    else:
+        _abi.check(lib.rpt_polar_count(ed.data_ptr(), dt, nf, rows, bins, threshold, stride,
+                                       rp.data_ptr(), fo.data_ptr(), _abi.C.byref(tot), st))
     n = tot.value
     x = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
     y, v = torch.empty_like(x), torch.empty_like(x)
     g = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
     pf = torch.empty_like(g)
-    _abi.check(lib.rpt_polar_write(ed.data_ptr(), dt, nf, rows, bins, sc.data_ptr(),
-                                   cd.data_ptr(), sd.data_ptr(), gd.data_ptr(), threshold, stride,
-                                   rp.data_ptr(), fo.data_ptr(), len(gains), x.data_ptr(),
-                                   y.data_ptr(), v.data_ptr(), g.data_ptr(), pf.data_ptr(), st))
+    args = (ed.data_ptr(), dt, nf, rows, bins, sc.data_ptr(), cd.data_ptr(), sd.data_ptr(),
+            gd.data_ptr(), threshold, stride, rp.data_ptr(), fo.data_ptr(), len(gains),
+            x.data_ptr(), y.data_ptr(), v.data_ptr(), g.data_ptr(), pf.data_ptr())
+    if masked:
+        _abi.check(lib.rpt_polar_write_masked(*args, mk.data_ptr(), st))
+    else:
+        _abi.check(lib.rpt_polar_write(*args, st))
     return (x[:n].cpu().numpy(), y[:n].cpu().numpy(), v[:n].cpu().numpy(), g[:n].cpu().numpy(),
             pf[:n].cpu().numpy(), fo.cpu().numpy())
 
@@ -358,6 +369,25 @@ def test_k1_grouped_u8_matches_generic_rows(gpu):
                           f32=True)
                 for i in range(5):
                     np.testing.assert_array_equal(b[i], ref[i])
+
+
+def test_k1_keep_masks_match_two_full_reads(gpu):
+    """The keep-mask K1 (count pass stores 64-bit masks per lane and group, write pass reads the
+    masks and only the 16-B echo chunks that emit) against the two-full-read kernels: thresholds
+    on both sides of 127 and at the ends, strides 1/3/4/7, short last groups, dense and sparse."""
+    rng = np.random.default_rng(17)
+    for rows, p in ((4096, 0.02), (1023, 0.5), (6, 1.0)):
+        echo = np.where(rng.random((3, rows, 1024)) < p, rng.integers(0, 256, (3, rows, 1024)),
+                        0).astype(np.uint8)
+        scale = [np.full(rows, 231.5, np.float32)] * 3
+        angle = [np.linspace(0, 8000, rows).astype(np.float32)] * 3
+        for thr in (-3.0, 10.0, 127.5, 200.0, 255.0):
+            for stride in (1, 3, 4, 7):
+                a = _k1(gpu, echo, scale, angle, gains=(40, 50, 75), threshold=thr, stride=stride)
+                b = _k1(gpu, echo, scale, angle, gains=(40, 50, 75), threshold=thr, stride=stride,
+                        masked=True)
+                for i in range(6):
+                    np.testing.assert_array_equal(a[i], b[i])
 
 
 def test_speculative_k1_write_regrows(gpu):
