@@ -109,6 +109,9 @@ def main():
     ap.add_argument("--no-timing", action="store_true", help="skip per-stage hipEvent timing")
     ap.add_argument("--sharded", action="store_true",
                     help="run the frame-sharded (multi-GPU) pipeline even with one rank")
+    ap.add_argument("--python-shard", action="store_true",
+                    help="sharded runs: ShardedStackPipeline (HipOps stages composed in Python) "
+                         "instead of the native shard driver")
     ap.add_argument("--lanes", type=int, default=1,
                     help="single GPU: stacks in flight at once (native handles on separate "
                          "streams, FrameStackPipeline.submit)")
@@ -153,22 +156,32 @@ def main():
     torch.cuda.synchronize(dev)
     timing = not args.no_timing
     if dist:
-        # frame-sharded global stack: rank r owns frames [r*F, (r+1)*F) (rpt/dist.py)
-        from rpt.dist import Comm, ShardedStackPipeline
-        from rpt.stages import HipOps
+        # frame-sharded global stack: rank r owns frames [r*F, (r+1)*F) (rpt/dist.py); every
+        # per-rank stage in librpt's shard driver (--python-shard: the HipOps-composed variant)
+        from rpt.dist import Comm, NativeShardPipeline, ShardedStackPipeline
 
-        ops = HipOps(dev, timing=timing)
-        # rank 0's host stage (order + tracker over N*F frames, ~6.7 us/frame) of consecutive
+        # rank 0's host stage (order + tracker over N*F frames, ~6 us/frame) of consecutive
         # steps runs on 4 worker threads: the steps are independent stacks
-        pipe = ShardedStackPipeline(ops, Comm(dev), cfg.gains, cfg.rows, cfg.bins, PathParams(),
-                                    timing=timing, async_host=not args.sync_host,
-                                    host_workers=4)
-        G = len(cfg.gains)
-        pipe.set_geometry(
-            tuple(torch.from_numpy(np.tile(a, F * G)).to(dev) for a in
-                  (np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t)),
-            torch.tensor(list(cfg.gains) * F, dtype=torch.int32, device=dev))
-        run = lambda: pipe.run(echo, _abi.ECHO_U8, rank * F)  # noqa: E731
+        if args.python_shard:
+            from rpt.stages import HipOps
+
+            ops = HipOps(dev, timing=timing)
+            pipe = ShardedStackPipeline(ops, Comm(dev), cfg.gains, cfg.rows, cfg.bins,
+                                        PathParams(), timing=timing,
+                                        async_host=not args.sync_host, host_workers=4)
+            G = len(cfg.gains)
+            pipe.set_geometry(
+                tuple(torch.from_numpy(np.tile(a, F * G)).to(dev) for a in
+                      (np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t)),
+                torch.tensor(list(cfg.gains) * F, dtype=torch.int32, device=dev))
+            run = lambda: pipe.run(echo, _abi.ECHO_U8, rank * F)  # noqa: E731
+        else:
+            ops = pipe = NativeShardPipeline(Comm(dev), cfg.gains, cfg.rows, cfg.bins,
+                                             PathParams(), timing=timing,
+                                             async_host=not args.sync_host, host_workers=4)
+            pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t,
+                              ds.geo.sin_t, cfg.n_frames * len(cfg.gains))
+            run = lambda: pipe.run(echo, rank * F)  # noqa: E731
     else:
         pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), dev, timing=timing,
                                   async_host=not args.sync_host, lanes=args.lanes)
@@ -267,6 +280,7 @@ def main():
             tsrc = str(tfile.relative_to(ROOT))
             break
     roof = None
+    k5_ms = [v for v in k5_ms if v is not None]
     if k5_ms:
         k5 = float(np.mean(k5_ms))
         n_in = n_core_in
@@ -315,7 +329,9 @@ def main():
             "data": "synthetic (device-generated, seeded)",
             "config": {"workload": wl, "total_frames": total, "frames_per_gpu": F,
                        "points_per_step": int(pts), **summary,
-                       "parallelism": f"frame-sharded x{world}" if dist else "single GPU",
+                       "parallelism": (f"frame-sharded x{world}"
+                                       f"{' (python stages)' if args.python_shard else ''}")
+                       if dist else "single GPU",
                        "stacks_in_flight": 1 if dist else args.lanes,
                        "host_stage": "inline" if args.sync_host else
                        "overlapped: step k's order+tracker runs on a host thread during step "

@@ -23,6 +23,7 @@
  *   rpt_lsap                         scipy.optimize.linear_sum_assignment as called at :590
  *   rpt_tracker_*                    ObjectTracker :543-688 (+ TrackedObject :111-140)
  *   rpt_stack_*                      the compute stages of run_pipeline :941-991 (K1 .. K9) in one call
+ *   rpt_shard_*                      the same stages over a frame range of a multi-GPU stack
  *   rpt_fuse_gains_max               fuse_gains_max PointCloudWork/5_gain_fusion_ply_builder.py:222-273
  *   rpt_csv_*                        pd.read_csv + fillna/to_numpy of load_radar_csv :189-211
  *   rpt_synth_echo                   (bench/test input generator; no reference counterpart)
@@ -284,6 +285,77 @@ int32_t rpt_stack_segments(const rpt_stack* h, int32_t* frame, int32_t* label, i
 /* device copies (each nullable, [n_clustered]) of the clustered points and their labels */
 int32_t rpt_stack_points(const rpt_stack* h, float* x, float* y, float* intensity,
                          int32_t* gain, int32_t* point_frame, int32_t* labels, void* stream);
+/* ---- frame-sharded multi-GPU driver ----------------------------------------
+ * One rank's phases of ONE global stack whose contiguous frame ranges are spread over ranks; the
+ * caller runs the collectives between phases (rpt/dist.py: torch.distributed over RCCL / gloo) on
+ * buffers it owns.  Results equal rpt_stack_run over the whole stack.  Sequence per step:
+ *   polar -> [all_gather info] -> land_grid -> [all_reduce grid] -> land_apply ->
+ *   [all_gather kept/head/tail; halo x,y,t P2P] -> core -> [halo core P2P] -> components ->
+ *   [halo component P2P] -> pairs -> [all_gather pairs; rpt_merge_equivalences] -> roots ->
+ *   [all_gather roots] -> finish -> segments (rank 0 runs the host order + tracker) */
+typedef struct rpt_shard rpt_shard;
+typedef struct rpt_shard_info {
+  int64_t n_points;       /* K1 points of this rank's frames */
+  int32_t n_built;        /* of them, frames with at least one point */
+  int32_t pad0;
+  float bounds[4];        /* min x, max x, min y, max y of the K1 points (+inf/-inf: none) */
+  int64_t n_kept;         /* points after the land filter */
+  int64_t n_head, n_tail; /* kept points of the first / last halo_frames frames */
+  int64_t n_land_cells;
+} rpt_shard_info;
+rpt_shard* rpt_shard_create(void);
+void rpt_shard_destroy(rpt_shard* h);
+/* K1 over the rank's frames (rpt_stack_params as for rpt_stack_run) + bounds; synchronises */
+int32_t rpt_shard_polar(rpt_shard* h, const rpt_stack_params* params, const void* echo,
+                        const float* scale, const float* cos_t, const float* sin_t,
+                        const int32_t* gain, rpt_shard_info* info, void* stream);
+/* land-grid cells for the GLOBAL bounds (host; (len(x edges)-1) * (len(y edges)-1), 0 if < 2) */
+int64_t rpt_shard_land_cells(const float* global_bounds, double resolution);
+/* this rank's land grid over the global edges into grid (dev float64 [2*cells]: counts | sums) */
+int32_t rpt_shard_land_grid(rpt_shard* h, const float* global_bounds, double* grid, int64_t cells,
+                            void* stream);
+/* land mask from the all-reduced grid (NULL: no land filter) with the GLOBAL built-frame count,
+ * compaction, and the kept points as float32 x/y/t (dev, capacity n_points) with t = frame0 + frame
+ * slot; n_kept / n_head / n_tail / n_land_cells in info; synchronises */
+int32_t rpt_shard_land_apply(rpt_shard* h, const double* grid, int64_t cells,
+                             int32_t n_built_global, int32_t halo_frames, int64_t frame0,
+                             float* x_out, float* y_out, float* t_out, rpt_shard_info* info,
+                             void* stream);
+/* core flags (dev u8 [n]) of [prev halo | own | next halo] (dev float32 x/y/t [n], n > 0) */
+int32_t rpt_shard_core(rpt_shard* h, const float* x, const float* y, const float* t, int64_t n,
+                       uint8_t* core, void* stream);
+/* duration of the last core-flag pass (params.timing != 0; synchronises), -1 if not timed */
+double rpt_shard_core_ms(rpt_shard* h);
+/* components with the halo flags replaced by their owners': comp (dev int64 [n]) = base +
+ * component-minimum local index, -1 for non-core (base = global index of point 0) */
+int32_t rpt_shard_components(rpt_shard* h, const uint8_t* core, int64_t base, int64_t* comp,
+                             void* stream);
+/* equivalence pairs between the halo points' components (comp[0, n_prev), comp[n - n_next, n))
+ * and their owners' (owner_prev / owner_next, dev int64): pairs (dev int64 [1 + 2*cap]) = count,
+ * then (min, max) pairs; no sync */
+int32_t rpt_shard_pairs(rpt_shard* h, const int64_t* comp, int64_t n_prev,
+                        const int64_t* owner_prev, int64_t n_next, const int64_t* owner_next,
+                        int64_t* pairs, int64_t cap, void* stream);
+/* host: union of equivalence pairs [n_pairs][2] -> sorted distinct ids (keys_out) and each
+ * id's class minimum (reps_out), up to cap; returns the number of ids */
+int64_t rpt_merge_equivalences(const int64_t* pairs, int64_t n_pairs, int64_t* keys_out,
+                               int64_t* reps_out, int64_t cap);
+/* representatives (keys/vals host, sorted) and the global roots among own points
+ * [n_prev, n_prev + n_own) into roots (dev int64, capacity n_own); *n_roots (sync) */
+int32_t rpt_shard_roots(rpt_shard* h, const int64_t* keys, const int64_t* vals, int64_t n_keys,
+                        int64_t base, int64_t n_prev, int64_t n_own, int64_t* roots,
+                        int64_t* n_roots, void* stream);
+/* labels from every rank's roots (dev int64, ascending) + K9 summaries of the own points;
+ * *n_segments (sync); the segments then via rpt_shard_segments (local frame slots) */
+int32_t rpt_shard_finish(rpt_shard* h, const int64_t* reps_sorted, int64_t n_reps,
+                         int64_t* n_segments, void* stream);
+int32_t rpt_shard_segments(const rpt_shard* h, int32_t* frame, int32_t* label, int64_t* count,
+                           int64_t* first, float* cx, float* cy, float* mean_i,
+                           int64_t* frame_first_noise);
+/* labels (dev int32 [n_kept]) of the own kept points of the last rpt_shard_finish; no sync */
+int32_t rpt_shard_labels(const rpt_shard* h, int32_t* out, void* stream);
+int32_t rpt_shard_frame_offsets(const rpt_shard* h, int32_t which, int64_t* out);
+
 /* ---- host: per-frame cluster order of the reference -----------------------------------
  * From the segments of rpt_cluster_summaries (copied to host) and frame_first_noise: for each
  * frame the segment indices in the order st_dbscan(frames) lists that frame's clusters

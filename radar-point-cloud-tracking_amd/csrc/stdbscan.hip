@@ -1623,7 +1623,8 @@ __global__ __launch_bounds__(kBlock) void k_label_core(const int32_t* __restrict
 // none.  One wave per point, lanes over candidate cells; the core points of a mutual cell form
 // one component (star init), so such a cell needs one adjacent core point, found 64 at a time.
 // GLOBAL = false: key = ccmin (component-min original index, local run), label = cid[key];
-// GLOBAL = true : key = srep (global representative), label = rank of key in reps.
+// GLOBAL = true : key = slab (the core point's final label: labels are ranks of the sorted global
+//                 representatives, so the smallest label is the smallest representative).
 template <int D, bool GLOBAL>
 __global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts,
                                                  const int32_t* __restrict__ skey, Geom g,
@@ -1631,12 +1632,11 @@ __global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts
                                                  const uint32_t* __restrict__ occ_bits,
                                                  const float2* __restrict__ slab_t,
                                                  const int32_t* __restrict__ ccmin,
-                                                 const int64_t* __restrict__ srep,
+                                                 const int32_t* __restrict__ slab,
                                                  const int32_t* __restrict__ rep,
                                                  const uint8_t* __restrict__ mutual,
                                                  const int32_t* __restrict__ sorig,
                                                  const int32_t* __restrict__ cid,
-                                                 const int64_t* __restrict__ reps, int64_t nr,
                                                  const int32_t* __restrict__ nc_list,
                                                  const int32_t* __restrict__ nc_count,
                                                  int32_t* __restrict__ labels) {
@@ -1644,7 +1644,7 @@ __global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts
   const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
   const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
   const int64_t nq = *nc_count;
-  auto keyof = [&](int j) -> int64_t { return GLOBAL ? srep[j] : (int64_t)ccmin[j]; };
+  auto keyof = [&](int j) -> int64_t { return GLOBAL ? (int64_t)slab[j] : (int64_t)ccmin[j]; };
   for (int64_t q = w0; q < nq; q += nw) {
     const int s = nc_list[q];
     const int32_t key = skey[s];
@@ -1723,7 +1723,7 @@ __global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts
     }
     if (lane == 0) {
       int32_t out = -1;
-      if (best != INT64_MAX) out = GLOBAL ? rep_id(reps, nr, best) : cid[best];
+      if (best != INT64_MAX) out = GLOBAL ? (int32_t)best : cid[best];
       labels[sorig[s]] = out;
     }
   }
@@ -1761,25 +1761,50 @@ __global__ void k_comp_out(int32_t* parent, const uint8_t* __restrict__ core,
        s += (int64_t)gridDim.x * blockDim.x)
     comp[sorig[s]] = core[s] ? sorig[uf_find(parent, (int)s)] : -1;
 }
-// srep[s] = rep[sorig[s]] for core points (global representative), -1 otherwise
-__global__ void k_srep(const int64_t* __restrict__ rep, const uint8_t* __restrict__ core,
-                       const int32_t* __restrict__ sorig, int64_t n, int64_t* __restrict__ srep) {
-  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
-       s += (int64_t)gridDim.x * blockDim.x)
-    srep[s] = core[s] ? rep[sorig[s]] : -1;
+// Global labelling, core points: ccmin[s] = component-min original index; each component's
+// label = rank of its global representative (rep[min], from the equivalence merge) among the
+// sorted representatives -- one binary search per component, at its root; non-core queued.
+__global__ __launch_bounds__(kBlock) void k_ccmin_global(int32_t* parent,
+                                                        const uint8_t* __restrict__ core,
+                                                        int64_t n,
+                                                        const int32_t* __restrict__ sorig,
+                                                        const int64_t* __restrict__ rep,
+                                                        const int64_t* __restrict__ reps,
+                                                        int64_t nr, int32_t* __restrict__ ccmin,
+                                                        int32_t* __restrict__ gl,
+                                                        int32_t* __restrict__ nc_list,
+                                                        int32_t* __restrict__ nc_count) {
+  for (int64_t tile = (int64_t)blockIdx.x * kBlock * kItems; tile < n;
+       tile += (int64_t)gridDim.x * kBlock * kItems) {
+    block_append(
+        tile, n,
+        [&](int64_t s) -> bool {
+          if (!core[s]) return true;
+          const int x = uf_find(parent, (int)s);
+          const int m = sorig[x];
+          ccmin[s] = m;
+          if (x == (int)s) gl[m] = rep_id(reps, nr, rep[m]);
+          return false;
+        },
+        nc_list, nc_count);
+  }
 }
-// Final labels of core points from global representatives (ids = rank of the representative in
-// the sorted global list); non-core points go through k_label<D, true>.
-__global__ __launch_bounds__(kBlock) void k_label_global_core(const int64_t* __restrict__ srep,
-                                                             int64_t n,
+// slab[s] = final label of core point s (-1 for non-core); core labels written out
+__global__ __launch_bounds__(kBlock) void k_label_global_core(const uint8_t* __restrict__ core,
+                                                             const int32_t* __restrict__ ccmin,
+                                                             const int32_t* __restrict__ gl,
                                                              const int32_t* __restrict__ sorig,
-                                                             const int64_t* __restrict__ reps,
-                                                             int64_t nr,
+                                                             int64_t n,
+                                                             int32_t* __restrict__ slab,
                                                              int32_t* __restrict__ labels) {
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
        s += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t own = srep[s];
-    if (own >= 0) labels[sorig[s]] = rep_id(reps, nr, own);
+    int32_t l = -1;
+    if (core[s]) {
+      l = gl[ccmin[s]];
+      labels[sorig[s]] = l;
+    }
+    slab[s] = l;
   }
 }
 
@@ -1839,7 +1864,7 @@ struct DbscanState {
   const CellRec<D>* rec() const {
     return static_cast<const CellRec<D>*>(crec);
   }
-  int64_t* srep = nullptr;
+  int32_t* slab = nullptr;   // per sorted point: final label of core points (global path)
   int64_t* stmp = nullptr;
   Timer tm;
 
@@ -1955,7 +1980,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   bud.add<int32_t>(n);      // ccmin
   bud.add<int32_t>(n + 1);  // cid
   bud.add<int32_t>(n + 1);  // non-core list (+count)
-  bud.add<int64_t>(n);      // srep (global finalize)
+  bud.add<int32_t>(n);      // slab (global finalize)
   bud.add<int32_t>(n + 1);  // occ
   bud.add<int32_t>(n + 1);  // hpos
   bud.add<CellRec<D>>(C1);  // crec
@@ -1982,7 +2007,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   ccmin = arena.carve_n<int32_t>(n);
   cid = arena.carve_n<int32_t>(n + 1);
   nc_list = arena.carve_n<int32_t>(n + 1);
-  srep = arena.carve_n<int64_t>(n);
+  slab = arena.carve_n<int32_t>(n);
   occ = arena.carve_n<int32_t>(n + 1);
   hpos = arena.carve_n<int32_t>(n + 1);
   CellRec<D>* cr = arena.carve_n<CellRec<D>>(C1);
@@ -2182,14 +2207,12 @@ int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hi
   hipLaunchKernelGGL(k_label_core, dim3(gb), dim3(kBlock), 0, st, ccmin, n, sorig, cid, labels);
   if (dim == 2)
     hipLaunchKernelGGL((k_label<2, false>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<2>(), occ_bits, slab_t, ccmin, (const int64_t*)nullptr, rep,
-                       mutual, sorig, cid, (const int64_t*)nullptr, (int64_t)0, nc_list,
-                       nc_count, labels);
+                       rec<2>(), occ_bits, slab_t, ccmin, (const int32_t*)nullptr, rep,
+                       mutual, sorig, cid, nc_list, nc_count, labels);
   else
     hipLaunchKernelGGL((k_label<3, false>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<3>(), occ_bits, slab_t, ccmin, (const int64_t*)nullptr, rep,
-                       mutual, sorig, cid, (const int64_t*)nullptr, (int64_t)0, nc_list,
-                       nc_count, labels);
+                       rec<3>(), occ_bits, slab_t, ccmin, (const int32_t*)nullptr, rep,
+                       mutual, sorig, cid, nc_list, nc_count, labels);
   RPT_CHECK_LAUNCH();
   tm.mark();
   if (stats && defer) return RPT_OK;  // fill_stats after the caller's sync
@@ -2232,20 +2255,19 @@ int32_t DbscanState::labels_global(const int64_t* rep_orig, const int64_t* reps,
   }
   const int gb = grid_for(n, kBlock, 2048);
   int32_t* nc_count = nc_list + n;
-  hipLaunchKernelGGL(k_srep, dim3(gb), dim3(kBlock), 0, st, rep_orig, core, sorig, n, srep);
   RPT_HIP(hipMemsetAsync(nc_count, 0, sizeof(int32_t), st));
-  hipLaunchKernelGGL(k_nc_list, dim3(tile_grid(n)), dim3(kBlock), 0, st, core, n, nc_list,
-                     nc_count);
-  hipLaunchKernelGGL(k_label_global_core, dim3(gb), dim3(kBlock), 0, st, srep, n, sorig, reps, nr,
-                     labels);
+  hipLaunchKernelGGL(k_ccmin_global, dim3(tile_grid(n)), dim3(kBlock), 0, st, parent, core, n,
+                     sorig, rep_orig, reps, nr, ccmin, cid, nc_list, nc_count);
+  hipLaunchKernelGGL(k_label_global_core, dim3(gb), dim3(kBlock), 0, st, core, ccmin, cid, sorig,
+                     n, slab, labels);
   if (dim == 2)
     hipLaunchKernelGGL((k_label<2, true>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<2>(), occ_bits, slab_t, (const int32_t*)nullptr, srep, rep, mutual,
-                       sorig, (const int32_t*)nullptr, reps, nr, nc_list, nc_count, labels);
+                       rec<2>(), occ_bits, slab_t, (const int32_t*)nullptr, slab, rep, mutual,
+                       sorig, (const int32_t*)nullptr, nc_list, nc_count, labels);
   else
     hipLaunchKernelGGL((k_label<3, true>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<3>(), occ_bits, slab_t, (const int32_t*)nullptr, srep, rep, mutual,
-                       sorig, (const int32_t*)nullptr, reps, nr, nc_list, nc_count, labels);
+                       rec<3>(), occ_bits, slab_t, (const int32_t*)nullptr, slab, rep, mutual,
+                       sorig, (const int32_t*)nullptr, nc_list, nc_count, labels);
   RPT_CHECK_LAUNCH();
   return RPT_OK;
 }

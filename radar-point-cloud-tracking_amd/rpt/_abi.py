@@ -121,6 +121,19 @@ class StackResult(C.Structure):
     ]
 
 
+class ShardInfo(C.Structure):
+    _fields_ = [
+        ("n_points", C.c_int64),
+        ("n_built", C.c_int32),
+        ("pad0", C.c_int32),
+        ("bounds", C.c_float * 4),
+        ("n_kept", C.c_int64),
+        ("n_head", C.c_int64),
+        ("n_tail", C.c_int64),
+        ("n_land_cells", C.c_int64),
+    ]
+
+
 # (name, restype, argtypes)
 _SIGS = [
     ("rpt_version", C.c_int32, []),
@@ -180,6 +193,26 @@ _SIGS = [
     ("rpt_stack_segments", C.c_int32, [vp, c_i32p, c_i32p, c_i64p, c_i64p, c_f32p, c_f32p, c_f32p,
                                        c_i64p]),
     ("rpt_stack_points", C.c_int32, [vp, vp, vp, vp, vp, vp, vp, vp]),
+    ("rpt_shard_create", vp, []),
+    ("rpt_shard_destroy", None, [vp]),
+    ("rpt_shard_polar", C.c_int32, [vp, C.POINTER(StackParams), vp, vp, vp, vp, vp,
+                                    C.POINTER(ShardInfo), vp]),
+    ("rpt_shard_land_cells", C.c_int64, [c_f32p, C.c_double]),
+    ("rpt_shard_land_grid", C.c_int32, [vp, c_f32p, vp, C.c_int64, vp]),
+    ("rpt_shard_land_apply", C.c_int32, [vp, vp, C.c_int64, C.c_int32, C.c_int32, C.c_int64, vp,
+                                         vp, vp, C.POINTER(ShardInfo), vp]),
+    ("rpt_shard_core", C.c_int32, [vp, vp, vp, vp, C.c_int64, vp, vp]),
+    ("rpt_shard_core_ms", C.c_double, [vp]),
+    ("rpt_shard_components", C.c_int32, [vp, vp, C.c_int64, vp, vp]),
+    ("rpt_shard_pairs", C.c_int32, [vp, vp, C.c_int64, vp, C.c_int64, vp, vp, C.c_int64, vp]),
+    ("rpt_merge_equivalences", C.c_int64, [c_i64p, C.c_int64, c_i64p, c_i64p, C.c_int64]),
+    ("rpt_shard_roots", C.c_int32, [vp, c_i64p, c_i64p, C.c_int64, C.c_int64, C.c_int64,
+                                    C.c_int64, vp, c_i64p, vp]),
+    ("rpt_shard_finish", C.c_int32, [vp, vp, C.c_int64, c_i64p, vp]),
+    ("rpt_shard_segments", C.c_int32, [vp, c_i32p, c_i32p, c_i64p, c_i64p, c_f32p, c_f32p,
+                                       c_f32p, c_i64p]),
+    ("rpt_shard_labels", C.c_int32, [vp, vp, vp]),
+    ("rpt_shard_frame_offsets", C.c_int32, [vp, C.c_int32, c_i64p]),
     ("rpt_order_clusters", C.c_int32, [C.c_int32, C.c_int64, c_i32p, c_i32p, c_i64p, c_i64p,
                                         c_i64p, c_i64p]),
     ("rpt_set_order", C.c_int32, [c_i32p, C.c_int32, c_i32p]),

@@ -52,13 +52,19 @@ class Comm:
     def _c(self, t: torch.Tensor) -> torch.Tensor:
         return t.to(self.cdev).contiguous()
 
+    # a one-member group's collectives are the identity: no device round trip at world 1
+
     def all_reduce(self, t: torch.Tensor, op) -> torch.Tensor:
+        if self.world == 1:
+            return t
         c = self._c(t).clone()
         dist.all_reduce(c, op=op, group=self.group)
         return c.to(t.device)
 
     def all_gather_fixed(self, t: torch.Tensor) -> torch.Tensor:
         """all_gather of a 1-D tensor of the same length on every rank -> [world][len] (host)."""
+        if self.world == 1:
+            return t.reshape(1, -1).cpu()
         c = self._c(t).reshape(-1)
         out = torch.empty(self.world * c.numel(), dtype=c.dtype, device=self.cdev)
         dist.all_gather_into_tensor(out, c, group=self.group)
@@ -66,6 +72,8 @@ class Comm:
 
     def all_gather_var(self, t: torch.Tensor) -> List[torch.Tensor]:
         """all_gather of 1-D tensors of different lengths (returned on the input's device)."""
+        if self.world == 1:
+            return [t.reshape(-1)]
         c = self._c(t).reshape(-1)
         n = torch.tensor([c.numel()], dtype=torch.int64, device=self.cdev)
         ns = [torch.zeros_like(n) for _ in range(self.world)]
@@ -416,3 +424,280 @@ def _unpack_parts(parts, F: int):
         s_base += S
     seg = {k: np.concatenate(v) for k, v in segs.items()}
     return seg, np.concatenate(built), np.concatenate(fos), np.concatenate(orders)
+
+
+class NativeShardPipeline:
+    """The frame-sharded path with every per-rank stage in librpt's shard driver (rpt_shard_*,
+    csrc/stack.cpp): one native call per phase, each at most one packed readback; the
+    collectives between phases (torch.distributed: RCCL over xGMI, or gloo) move tensors this
+    class owns.  Same protocol and results as ShardedStackPipeline (module doc), which stays as
+    the CPU-testable restatement (tests/test_dist_cpu.py)."""
+
+    def __init__(self, comm: Comm, gains: Sequence[int], rows: int, bins: int,
+                 params: PathParams = None, timing: bool = False, async_host: bool = False,
+                 host_workers: int = 2):
+        from . import _abi
+        from .stages import _Ws
+
+        self.comm = comm
+        self.dev = comm.dev
+        self.gains = [int(g) for g in gains]
+        self.rows, self.bins = rows, bins
+        self.p = params or PathParams()
+        self.timing = timing
+        self.lib = _abi.load()
+        self._abi = _abi
+        self.h = self.lib.rpt_shard_create()
+        self.ws = _Ws(self.dev)
+        self._host = ThreadPoolExecutor(max_workers=host_workers) if async_host else None
+        self.core_points = 0
+        self._n_own = 0
+        self._core_ms = False
+
+    def set_geometry(self, scale, cos_t, sin_t, n_files: int):
+        def rep(a):
+            a = np.ascontiguousarray(a, dtype=np.float32)
+            if a.size == self.rows:
+                a = np.tile(a, n_files)
+            return torch.from_numpy(a).to(self.dev)
+        self.geo = (rep(scale), rep(cos_t), rep(sin_t))
+        self.gain_d = torch.tensor(self.gains * (n_files // len(self.gains)), dtype=torch.int32,
+                                   device=self.dev)
+
+    def last_core_ms(self) -> Optional[float]:
+        """hipEvent duration of the last run's core-flag pass (timing=True), else None."""
+        if not self._core_ms:
+            return None
+        ms = float(self.lib.rpt_shard_core_ms(self.h))
+        return ms if ms >= 0 else None
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            self.lib.rpt_shard_destroy(h)
+            self.h = None
+
+    def run(self, echo: torch.Tensor, frame0: int) -> ShardResult:
+        with torch.cuda.device(self.dev):
+            return self._run(echo, frame0)
+
+    def _run(self, echo: torch.Tensor, frame0: int) -> ShardResult:
+        from ._device import stream_handle
+        from .stages import LAND_MIN_INTENSITY, LAND_PERSISTENCE_THRESHOLD
+
+        A, lib, comm, p, ws = self._abi, self.lib, self.comm, self.p, self.ws
+        C_ = A.C
+        G = len(self.gains)
+        F = int(echo.shape[0])
+        W, r = comm.world, comm.rank
+        st = stream_handle(self.dev)
+        marks = [("start", time.perf_counter())]
+
+        def mark(name):
+            if self.timing:
+                marks.append((name, time.perf_counter()))
+
+        def chk(status, what):
+            A.check(status, what)
+
+        dt = {torch.uint8: A.ECHO_U8, torch.float32: A.ECHO_F32}[echo.dtype]
+        echo = echo.contiguous()
+        sp = A.StackParams(F, G, self.rows, self.bins, dt, float(np.float32(p.threshold)),
+                           int(p.stride), 1 if p.land_filter else 0, LAND_GRID_RESOLUTION,
+                           LAND_PERSISTENCE_THRESHOLD, float(LAND_MIN_INTENSITY),
+                           float(p.eps_space), float(p.eps_time), int(p.min_samples),
+                           1 if self.timing else 0)
+        info = A.ShardInfo()
+        scale_d, cos_d, sin_d = self.geo
+        # 1. K1 + bounds (one readback), then every rank's counts / bounds
+        chk(lib.rpt_shard_polar(self.h, C_.byref(sp), echo.data_ptr(), scale_d.data_ptr(),
+                                cos_d.data_ptr(), sin_d.data_ptr(), self.gain_d.data_ptr(),
+                                C_.byref(info), st), "rpt_shard_polar")
+        n_points = int(info.n_points)
+        allinfo = comm.all_gather_fixed(torch.tensor(
+            [n_points, info.n_built, *[float(b) for b in info.bounds]],
+            dtype=torch.float64)).numpy()
+        n_global = int(allinfo[:, 0].sum())
+        n_built = int(allinfo[:, 1].sum())
+        mark("polar")
+        # 2. land grid over the global bounds, all-reduced (integer-valued float64: exact)
+        grid, cells = None, 0
+        if p.land_filter and n_built > 10 and n_global > 0:
+            gb = np.array([allinfo[:, 2].min(), allinfo[:, 3].max(), allinfo[:, 4].min(),
+                           allinfo[:, 5].max()], np.float32)
+            gbp = gb.ctypes.data_as(A.c_f32p)
+            cells = int(lib.rpt_shard_land_cells(gbp, LAND_GRID_RESOLUTION))
+            if cells <= 0:
+                raise ValueError("degenerate land grid")
+            grid = ws.get("grid", 2 * cells, torch.float64)
+            chk(lib.rpt_shard_land_grid(self.h, gbp, grid.data_ptr(), cells, st),
+                "rpt_shard_land_grid")
+            grid = comm.all_reduce(grid, _SUM)
+        # 3. mask + compaction; own x / y / t land between room for the two halos
+        h = int(np.floor(p.eps_time)) if np.isfinite(p.eps_time) and p.eps_time >= 0 else 0
+        if W > 1 and h > F:
+            raise ValueError(f"each rank needs at least floor(eps_time)={h} frames")
+        halo = W > 1 and h > 0
+        cap_prev = int(allinfo[r - 1, 0]) if halo and r > 0 else 0
+        cap_next = int(allinfo[r + 1, 0]) if halo and r < W - 1 else 0
+        cap = cap_prev + n_points + cap_next
+        xyt = ws.get("xyt", 3 * max(cap, 1), torch.float32)
+        X, Y, T = xyt[:cap], xyt[cap:2 * cap], xyt[2 * cap:3 * cap]
+        off = cap_prev
+        chk(lib.rpt_shard_land_apply(self.h, grid.data_ptr() if grid is not None else None,
+                                     cells, n_built, h, int(frame0), X[off:].data_ptr(),
+                                     Y[off:].data_ptr(), T[off:].data_ptr(), C_.byref(info), st),
+            "rpt_shard_land_apply")
+        n_own, n_head, n_tail = int(info.n_kept), int(info.n_head), int(info.n_tail)
+        kinfo = comm.all_gather_fixed(torch.tensor([n_own, n_head, n_tail],
+                                                   dtype=torch.int64)).numpy()
+        kept = kinfo[:, 0]
+        P = int(kept[:r].sum())
+        n_in_global = int(kept.sum())
+        mark("land")
+        if n_in_global == 0:
+            if n_built > 0:  # BallTree on 0 samples (sklearn ValueError)
+                raise ValueError("Found array with 0 sample(s) (shape=(0, 2)) while a minimum "
+                                 "of 1 is required.")
+        n_prev = int(kinfo[r - 1, 2]) if halo and r > 0 else 0
+        n_next = int(kinfo[r + 1, 1]) if halo and r < W - 1 else 0
+        # 4. halo: x / y / t of the first / last h frames to the neighbours (sizes known)
+        if halo:
+            def pack(a, b):
+                return torch.cat([X[off + a:off + b], Y[off + a:off + b], T[off + a:off + b]])
+            hp, hn = comm.exchange_known(pack(0, n_head), pack(n_own - n_tail, n_own),
+                                         3 * n_prev, 3 * n_next)
+            if n_prev:
+                X[off - n_prev:off] = hp[:n_prev]
+                Y[off - n_prev:off] = hp[n_prev:2 * n_prev]
+                T[off - n_prev:off] = hp[2 * n_prev:]
+            if n_next:
+                e = off + n_own
+                X[e:e + n_next] = hn[:n_next]
+                Y[e:e + n_next] = hn[n_next:2 * n_next]
+                T[e:e + n_next] = hn[2 * n_next:]
+        lo = off - n_prev
+        n_tot = n_prev + n_own + n_next
+        base = P - n_prev
+        mark("halo")
+        # 5. core flags; the halo points' flags from their owners
+        core = ws.get("core", max(n_tot, 1), torch.uint8)
+        self._core_ms = False
+        if n_tot:
+            chk(lib.rpt_shard_core(self.h, X[lo:].data_ptr(), Y[lo:].data_ptr(),
+                                   T[lo:].data_ptr(), n_tot, core.data_ptr(), st),
+                "rpt_shard_core")
+            self._core_ms = self.timing   # read (synchronising) by last_core_ms()
+        self.core_points = n_tot
+        if halo:
+            c_own = core[n_prev:n_prev + n_own]
+            cp, cn = comm.exchange_known(c_own[:n_head].contiguous(),
+                                         c_own[n_own - n_tail:].contiguous(), n_prev, n_next)
+            if n_prev:
+                core[:n_prev] = cp
+            if n_next:
+                core[n_prev + n_own:n_tot] = cn
+        # 6. components; equivalences across ranks from the halo points' owners
+        comp = ws.get("comp", max(n_tot, 1), torch.int64)
+        if n_tot:
+            chk(lib.rpt_shard_components(self.h, core.data_ptr(), base, comp.data_ptr(), st),
+                "rpt_shard_components")
+        pairs = np.zeros(0, np.int64)
+        if halo:
+            g_own = comp[n_prev:n_prev + n_own]
+            op_, on_ = comm.exchange_known(g_own[:n_head].contiguous(),
+                                           g_own[n_own - n_tail:].contiguous(), n_prev, n_next)
+            pcap = n_prev + n_next
+            pb = ws.get("pairs", 1 + 2 * max(pcap, 1), torch.int64)
+            if n_tot:
+                chk(lib.rpt_shard_pairs(self.h, comp.data_ptr(), n_prev, op_.data_ptr(), n_next,
+                                        on_.data_ptr(), pb.data_ptr(), pcap, st),
+                    "rpt_shard_pairs")
+            else:
+                pb[0] = 0
+            cnts = comm.all_gather_fixed(pb[:1]).numpy().reshape(-1)
+            m = int(cnts.max()) if len(cnts) else 0
+            if m > 0:
+                allp = comm.all_gather_fixed(pb[1:1 + 2 * m].contiguous()).numpy()
+                pairs = np.concatenate([row[:2 * int(c)] for row, c in zip(allp, cnts)])
+        npair = len(pairs) // 2
+        pairs = np.ascontiguousarray(pairs, np.int64)
+        nk = int(lib.rpt_merge_equivalences(pairs.ctypes.data_as(A.c_i64p), npair, None, None, 0))
+        keys = np.empty(max(nk, 1), np.int64)
+        vals = np.empty(max(nk, 1), np.int64)
+        lib.rpt_merge_equivalences(pairs.ctypes.data_as(A.c_i64p), npair,
+                                   keys.ctypes.data_as(A.c_i64p), vals.ctypes.data_as(A.c_i64p),
+                                   nk)
+        # 7. representatives this rank owns, every rank's (ascending in rank order)
+        roots = ws.get("roots", max(n_own, 1), torch.int64)
+        nr = C_.c_int64(0)
+        if n_tot:
+            chk(lib.rpt_shard_roots(self.h, keys.ctypes.data_as(A.c_i64p),
+                                    vals.ctypes.data_as(A.c_i64p), nk, base, n_prev, n_own,
+                                    roots.data_ptr(), C_.byref(nr), st), "rpt_shard_roots")
+        all_roots = comm.all_gather_var(roots[:int(nr.value)]) if W > 1 else \
+            [roots[:int(nr.value)]]
+        reps = torch.cat([a.to(self.dev) for a in all_roots]).contiguous()
+        n_clusters = int(reps.numel())
+        # 8. labels + K9 of the own frames (one readback)
+        nseg = C_.c_int64(0)
+        if n_tot:
+            chk(lib.rpt_shard_finish(self.h, reps.data_ptr(), n_clusters, C_.byref(nseg), st),
+                "rpt_shard_finish")
+        S = int(nseg.value)
+        seg = {"frame": np.empty(S, np.int32), "label": np.empty(S, np.int32),
+               "count": np.empty(S, np.int64), "first": np.empty(S, np.int64),
+               "cx": np.empty(S, np.float32), "cy": np.empty(S, np.float32),
+               "mi": np.empty(S, np.float32)}
+        first_noise = np.full(F, -1, np.int64)
+        if n_tot:
+            ptr = lambda a, t: a.ctypes.data_as(t)  # noqa: E731
+            chk(lib.rpt_shard_segments(
+                self.h, ptr(seg["frame"], A.c_i32p), ptr(seg["label"], A.c_i32p),
+                ptr(seg["count"], A.c_i64p), ptr(seg["first"], A.c_i64p),
+                ptr(seg["cx"], A.c_f32p), ptr(seg["cy"], A.c_f32p), ptr(seg["mi"], A.c_f32p),
+                ptr(first_noise, A.c_i64p)), "rpt_shard_segments")
+        fo = np.empty(F + 1, np.int64)
+        chk(lib.rpt_shard_frame_offsets(self.h, 0, fo.ctypes.data_as(A.c_i64p)),
+            "rpt_shard_frame_offsets")
+        built_local = np.nonzero(np.diff(fo) > 0)[0]
+        packed = np.concatenate([
+            [S, frame0], built_local.astype(np.float64), [-1.0] * (F - len(built_local)),
+            first_noise, seg["frame"], seg["label"], seg["count"], seg["first"], seg["cx"],
+            seg["cy"], seg["mi"]]).astype(np.float64)
+        parts = comm.all_gather_var(torch.from_numpy(packed)) if W > 1 else \
+            [torch.from_numpy(packed)]
+        mark("stdbscan")
+        self._n_own = n_own if n_tot else 0
+        labels = None
+        res = ShardResult(n_points_local=n_points, n_points_global=n_global,
+                          n_clustered_local=n_own, n_clusters=n_clusters, labels_local=labels)
+        if r == 0:
+            res.n_segments = int(sum(float(t[0]) for t in parts))
+
+            def host_stage():
+                t0 = time.perf_counter()
+                all_seg, built, fo_g, order_g = _unpack_parts(parts, F)
+                trk = track_ordered(built - frame0, fo_g, order_g, all_seg, p, built)
+                return all_seg, built, fo_g, order_g, trk, (time.perf_counter() - t0) * 1e3
+
+            if self._host is not None:
+                res._pending = self._host.submit(host_stage)
+            else:
+                (res.seg, res.built_global, res.frame_order_offsets, res.frame_order,
+                 res.tracker, _) = host_stage()
+        mark("summaries")
+        if self.timing:
+            for (a, ta), (b, tb) in zip(marks[:-1], marks[1:]):
+                res.stage_ms[b] = (tb - ta) * 1e3
+        return res
+
+    def labels_local(self) -> torch.Tensor:
+        """Labels (device int32, a copy) of this rank's kept points of the last run."""
+        from ._device import stream_handle
+        out = torch.empty(self._n_own, dtype=torch.int32, device=self.dev)
+        if self._n_own:
+            self._abi.check(self.lib.rpt_shard_labels(self.h, out.data_ptr(),
+                                                      stream_handle(self.dev)),
+                            "rpt_shard_labels")
+        return out

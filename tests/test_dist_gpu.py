@@ -1,5 +1,5 @@
-"""Frame-sharded path on the GPU: 2 ranks (gloo, sharing cuda:0 on a one-GPU box) run
-rpt.dist.ShardedStackPipeline over librpt; rank 0 compares with the single-GPU
+"""Frame-sharded path on the GPU: 2 or 3 ranks (gloo, sharing cuda:0 on a one-GPU box) run
+rpt.dist.NativeShardPipeline (librpt's rpt_shard_* driver) or ShardedStackPipeline over librpt; rank 0 compares with the single-GPU
 FrameStackPipeline (labels, per-frame cluster rows in reference order, tracked objects).
 The ranks are started by torch.distributed.run as child processes (tools/dist_check.py)."""
 from __future__ import annotations
@@ -24,14 +24,15 @@ def _free_port():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,frames", [(2, 14)])
-def test_sharded_gpu_matches_single_gpu(world, frames):
+@pytest.mark.parametrize("world,frames,impl", [(2, 14, "native"), (3, 6, "native"),
+                                               (2, 14, "python")])
+def test_sharded_gpu_matches_single_gpu(world, frames, impl):
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={world}", "--master-addr=127.0.0.1",
            f"--master-port={_free_port()}", str(ROOT / "tools" / "dist_check.py"),
-           "--backend", "gloo", "--frames", str(frames)]
+           "--backend", "gloo", "--frames", str(frames), "--impl", impl]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-4000:]

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Multi-rank check of the frame-sharded path on GPU(s): every rank runs rpt.dist's
-ShardedStackPipeline on its frame range; rank 0 also runs the single-GPU FrameStackPipeline over
+NativeShardPipeline (or, --impl python, ShardedStackPipeline) on its frame range; rank 0 also runs the single-GPU FrameStackPipeline over
 the whole stack and asserts identical labels, per-frame cluster rows and tracked objects.
 
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \
@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--backend", default="gloo")
     ap.add_argument("--frames", type=int, default=14, help="frames per rank")
     ap.add_argument("--rows", type=int, default=4096)
+    ap.add_argument("--impl", default="native", choices=("native", "python"),
+                    help="native: NativeShardPipeline (librpt shard driver); python: "
+                         "ShardedStackPipeline over HipOps")
     args = ap.parse_args()
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
@@ -42,7 +45,7 @@ def main():
         dist.init_process_group("gloo")
 
     from rpt import _abi
-    from rpt.dist import Comm, ShardedStackPipeline
+    from rpt.dist import Comm, NativeShardPipeline, ShardedStackPipeline
     from rpt.pipeline import FrameStackPipeline, PathParams
     from rpt.stages import HipOps
     from rpt.synth import DeviceSynth, SynthConfig
@@ -51,13 +54,21 @@ def main():
     cfg = SynthConfig(n_frames=F, rows=args.rows, frame0=rank * F)
     ds = DeviceSynth(cfg, dev)
     echo = ds.echo()
-    ops = HipOps(dev)
-    pipe = ShardedStackPipeline(ops, Comm(dev), cfg.gains, cfg.rows, cfg.bins, PathParams())
-    geo = tuple(torch.from_numpy(np.tile(a, F * 3)).to(dev) for a in
-                (np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t))
-    pipe.set_geometry(geo, torch.tensor(list(cfg.gains) * F, dtype=torch.int32, device=dev))
-    res = pipe.run(echo, _abi.ECHO_U8, rank * F)
-    labels = Comm(dev).all_gather_var(res.labels_local.to(torch.int64))
+    if args.impl == "native":
+        pipe = NativeShardPipeline(Comm(dev), cfg.gains, cfg.rows, cfg.bins, PathParams())
+        pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
+                          F * 3)
+        res = pipe.run(echo, rank * F)
+        mine = pipe.labels_local()
+    else:
+        ops = HipOps(dev)
+        pipe = ShardedStackPipeline(ops, Comm(dev), cfg.gains, cfg.rows, cfg.bins, PathParams())
+        geo = tuple(torch.from_numpy(np.tile(a, F * 3)).to(dev) for a in
+                    (np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t))
+        pipe.set_geometry(geo, torch.tensor(list(cfg.gains) * F, dtype=torch.int32, device=dev))
+        res = pipe.run(echo, _abi.ECHO_U8, rank * F)
+        mine = res.labels_local
+    labels = Comm(dev).all_gather_var(mine.to(torch.int64))
     ok = True
     if rank == 0:
         full = SynthConfig(n_frames=F * world, rows=args.rows)
@@ -77,7 +88,7 @@ def main():
         a, b = res.tracker.objects(), ref.tracker.objects()
         ok &= [o.object_id for o in a] == [o.object_id for o in b]
         ok &= all(np.array_equal(np.vstack(x.positions), np.vstack(y.positions)) for x, y in zip(a, b))
-        print(f"[dist_check] world={world} backend={args.backend} points={res.n_points_global} "
+        print(f"[dist_check] world={world} backend={args.backend} impl={args.impl} points={res.n_points_global} "
               f"clusters={res.n_clusters} segments={res.n_segments} objects={len(a)} "
               f"labels_equal={np.array_equal(got, exp)} ok={ok}", flush=True)
     flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
