@@ -94,22 +94,24 @@ int32_t rpt_polar_write(const void* echo, int32_t echo_dtype, int64_t n_files, i
                         float* x, float* y, float* intensity, int32_t* gain_out /*nullable*/,
                         int32_t* point_frame_out /*nullable: file / files_per_frame*/,
                         void* stream);
-/* Same two passes with the keep masks kept between them (u8 sweeps of 1024 bins with 16-B aligned
- * rows; other sweeps ignore the masks): the count pass stores one 64-bit word per 64 lanes x group
- * of 4 rows (rpt_polar_mask_words(n_files, rows) words, 1/8 of the echo), the write pass reads
- * them plus only the 16-B echo chunks holding an emitted sample instead of the whole echo. */
-int64_t rpt_polar_mask_words(int64_t n_files, int32_t rows);
-int32_t rpt_polar_count_masked(const void* echo, int32_t echo_dtype, int64_t n_files,
+/* Same two passes with the kept samples staged between them (u8 sweeps of 1024 bins with 16-B
+ * aligned rows; other sweeps ignore the buffer): for every group of 4 rows that keeps at most 128
+ * samples the count pass stores them as 32-bit (row, bin, sample) entries in the group's slot of
+ * entries (dev, rpt_polar_stage_words(n_files, rows) words), and the write pass reads those
+ * instead of the group's echo -- one read of the echo for sparse sweeps (what rpt_stack_run
+ * does).  Same outputs as rpt_polar_count + rpt_polar_write. */
+int64_t rpt_polar_stage_words(int64_t n_files, int32_t rows);
+int32_t rpt_polar_count_staged(const void* echo, int32_t echo_dtype, int64_t n_files,
                                int32_t rows, int32_t bins, float threshold, int32_t stride,
                                int64_t* row_prefix, int64_t* file_offsets, int64_t* total_host,
-                               uint64_t* keep_masks /*dev*/, void* stream);
-int32_t rpt_polar_write_masked(const void* echo, int32_t echo_dtype, int64_t n_files,
+                               uint32_t* entries /*dev*/, void* stream);
+int32_t rpt_polar_write_staged(const void* echo, int32_t echo_dtype, int64_t n_files,
                                int32_t rows, int32_t bins, const float* scale, const float* cos_t,
                                const float* sin_t, const int32_t* gain, float threshold,
                                int32_t stride, const int64_t* row_prefix,
                                const int64_t* file_offsets, int32_t files_per_frame, float* x,
                                float* y, float* intensity, int32_t* gain_out,
-                               int32_t* point_frame_out, const uint64_t* keep_masks /*dev*/,
+                               int32_t* point_frame_out, const uint32_t* entries /*dev*/,
                                void* stream);
 /* times_out[i] = (float)frame_ids[point_frame[i]] (frame_ids dev int64 per frame slot; NULL =
  * the slot itself): the float32 frame_ids stack of 4_temporal_object_tracker.py:460-467. */

@@ -14,13 +14,13 @@ int32_t stdbscan(const float* x, const float* y, const float* z, int64_t stride,
                  int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st, int dim);
 int32_t polar_count(const void* echo, int32_t dt, int64_t n_files, int32_t rows, int32_t bins,
                     float thr, int32_t stride, int64_t* row_prefix, int64_t* file_offsets,
-                    int64_t* total_host, hipStream_t st, uint64_t* masks);
+                    int64_t* total_host, hipStream_t st, uint32_t* entries);
 int32_t polar_write(const void* echo, int32_t dt, int64_t n_files, int32_t rows, int32_t bins,
                     const float* scale, const float* cos_t, const float* sin_t,
                     const int32_t* gain, float thr, int32_t stride, const int64_t* row_prefix,
                     const int64_t* file_offsets, int32_t files_per_frame, float* x, float* y,
-                    float* v, int32_t* gout, int32_t* pf, hipStream_t st, const uint64_t* masks);
-int64_t polar_mask_words(int64_t n_files, int32_t rows);
+                    float* v, int32_t* gout, int32_t* pf, hipStream_t st, const uint32_t* entries);
+int64_t polar_stage_words(int64_t n_files, int32_t rows);
 int32_t frame_times(const int32_t* pf, int64_t n, const int64_t* ids, float* t, hipStream_t st);
 int32_t sweep_to_points(const float* inten, const float* ranges, const float* cos_t,
                         const float* sin_t, int32_t rows, int32_t bins, float thr,
@@ -188,17 +188,17 @@ int32_t rpt_polar_count(const void* echo, int32_t echo_dtype, int64_t n_files, i
                           file_offsets, total_host, rpt::as_stream(stream), nullptr);
 }
 
-int64_t rpt_polar_mask_words(int64_t n_files, int32_t rows) {
-  return (n_files > 0 && rows > 0) ? rpt::polar_mask_words(n_files, rows) : 0;
+int64_t rpt_polar_stage_words(int64_t n_files, int32_t rows) {
+  return (n_files > 0 && rows > 0) ? rpt::polar_stage_words(n_files, rows) : 0;
 }
 
-int32_t rpt_polar_count_masked(const void* echo, int32_t echo_dtype, int64_t n_files,
+int32_t rpt_polar_count_staged(const void* echo, int32_t echo_dtype, int64_t n_files,
                                int32_t rows, int32_t bins, float threshold, int32_t stride,
                                int64_t* row_prefix, int64_t* file_offsets, int64_t* total_host,
-                               uint64_t* keep_masks, void* stream) {
+                               uint32_t* entries, void* stream) {
   rpt::clear_error();
   return rpt::polar_count(echo, echo_dtype, n_files, rows, bins, threshold, stride, row_prefix,
-                          file_offsets, total_host, rpt::as_stream(stream), keep_masks);
+                          file_offsets, total_host, rpt::as_stream(stream), entries);
 }
 
 int32_t rpt_polar_write(const void* echo, int32_t echo_dtype, int64_t n_files, int32_t rows,
@@ -213,19 +213,19 @@ int32_t rpt_polar_write(const void* echo, int32_t echo_dtype, int64_t n_files, i
                           intensity, gain_out, point_frame_out, rpt::as_stream(stream), nullptr);
 }
 
-int32_t rpt_polar_write_masked(const void* echo, int32_t echo_dtype, int64_t n_files,
+int32_t rpt_polar_write_staged(const void* echo, int32_t echo_dtype, int64_t n_files,
                                int32_t rows, int32_t bins, const float* scale, const float* cos_t,
                                const float* sin_t, const int32_t* gain, float threshold,
                                int32_t stride, const int64_t* row_prefix,
                                const int64_t* file_offsets, int32_t files_per_frame, float* x,
                                float* y, float* intensity, int32_t* gain_out,
-                               int32_t* point_frame_out, const uint64_t* keep_masks,
+                               int32_t* point_frame_out, const uint32_t* entries,
                                void* stream) {
   rpt::clear_error();
   return rpt::polar_write(echo, echo_dtype, n_files, rows, bins, scale, cos_t, sin_t, gain,
                           threshold, stride, row_prefix, file_offsets, files_per_frame, x, y,
                           intensity, gain_out, point_frame_out, rpt::as_stream(stream),
-                          keep_masks);
+                          entries);
 }
 
 int32_t rpt_frame_times(const int32_t* point_frame, int64_t n, const int64_t* frame_ids,

@@ -38,6 +38,7 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 // Waits for the work queued on st so far by polling an event (readback latency; prims.hip).
 int32_t wait_stream(hipStream_t st);  // also reports device faults (check_device_faults)
 int32_t check_device_faults();
+unsigned int* device_fault_word();  // mapped pinned fault word for bounded device spins
 
 // ---- scratch pool ------------------------------------------------------------------------
 // A bump arena per (device, stream) that grows on demand.  Calls reserve() once with their total

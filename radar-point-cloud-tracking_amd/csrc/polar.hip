@@ -286,16 +286,68 @@ __device__ __forceinline__ void group_rows(const GroupMap& gm, uint32_t grp, uin
   *nr = min(kGroupRows, gm.rows - r0);
 }
 
-// masks (nullable): the count pass also stores every lane's 16-bit keep masks of the group's
-// rows as ONE 64-bit word per lane (row k in bits 16k..16k+15; 512 B per group, 1/8 of the echo),
-// so the write pass reads the masks and only the 16-B echo chunks that hold an emitted sample
-// instead of the whole echo a second time.
-template <bool HI>
+// Kept samples of a group by in-group rank.  A wave leaves its group's per-row inclusive lane
+// counts, keep masks and sample bytes in its LDS slice; the kept sample of in-group rank i is then
+// found by any lane: row from the row bases (scalar compares), lane by a 6-step binary search of
+// the row's inclusive counts, bit by nth_bit16 of that lane's mask.  Work goes to the OUTPUT slots
+// (consecutive lanes, full-width stores) instead of walking each input lane's mask bits, so a
+// dense lane no longer holds its whole wave in a divergent loop.
+struct GroupLds {
+  int incl[kGroupRows][64];
+  uint32_t mask[kGroupRows][64];
+  uint32_t bytes[kGroupRows][256];  // the group's 4 KiB of samples
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void group_to_lds(GroupLds& L, int lane, const uint32_t (&m)[kGroupRows],
+                                             const int (&incl)[kGroupRows],
+                                             const uint4 (&vv)[kGroupRows]) {
+#pragma unroll
+  for (int k = 0; k < kGroupRows; ++k) {
+    L.incl[k][lane] = incl[k];
+    L.mask[k][lane] = m[k];
+    *reinterpret_cast<uint4*>(&L.bytes[k][lane * 4]) = vv[k];
+  }
+  wave_lds_sync();
+}
+
+// (row << 18) | (bin << 8) | sample of the kept sample of in-group rank i (i < rb[kGroupRows];
+// rb[k] = kept samples of the rows before row k)
+__device__ __forceinline__ uint32_t kept_entry(const GroupLds& L,
+                                               const uint32_t (&rb)[kGroupRows + 1], uint32_t i) {
+  const int k = (i >= rb[1]) + (i >= rb[2]) + (i >= rb[3]);
+  const int ir = (int)(i - rb[k]);
+  const int* inc = L.incl[k];
+  int lo = 0;  // lanes whose inclusive count is <= ir
+#pragma unroll
+  for (int step = 32; step > 0; step >>= 1)
+    if (inc[lo + step - 1] <= ir) lo += step;
+  const uint32_t msk = L.mask[k][lo];
+  const int j = ir - (inc[lo] - __popc(msk));
+  const int bit = nth_bit16(msk, (uint32_t)j);
+  const int bin = lo * 16 + bit;
+  const uint32_t w = L.bytes[k][bin >> 2];
+  return ((uint32_t)k << 18) | ((uint32_t)bin << 8) | __builtin_amdgcn_ubfe(w, 8u * (bin & 3), 8u);
+}
+
+// Staged kept samples (nullable): when a group keeps at most kStageSlots samples the count pass
+// also stores them in in-group rank order, as kept_entry() words, in the group's slot of
+// kStageSlots words; the write pass then reads those instead of the group's 4 KiB of echo (one
+// read of the echo for the whole K1).  A group that keeps more (dense sweeps) is read from the
+// echo again by the write pass.
+constexpr int kStageSlots = 256;
+
+template <bool HI, bool STAGE>
 __global__ __launch_bounds__(kBlock) void k_group_count_u8(const uint8_t* __restrict__ echo,
                                                           uint32_t n_groups, GroupMap gm,
                                                           uint32_t K,
                                                           int32_t* __restrict__ group_count,
-                                                          uint64_t* __restrict__ masks) {
+                                                          uint32_t* __restrict__ entries) {
   const int lane = threadIdx.x & 63;
   const uint32_t wave0 = blockIdx.x * kWavesPerBlock + threadIdx.x / 64;
   const uint32_t n_waves = gridDim.x * kWavesPerBlock;
@@ -310,30 +362,46 @@ __global__ __launch_bounds__(kBlock) void k_group_count_u8(const uint8_t* __rest
     for (int k = 0; k < kGroupRows; ++k)
       v[k] = (k < nr) ? *reinterpret_cast<const uint4*>(echo + (row0 + k) * 1024 + lane * 16)
                       : make_uint4(0u, 0u, 0u, 0u);
-    uint32_t c = 0;
-    if (masks) {
-      uint64_t mw = 0;
+    if constexpr (STAGE) {
+      __shared__ GroupLds s_lds[kWavesPerBlock];
+      GroupLds& L = s_lds[threadIdx.x / 64];
+      uint32_t m[kGroupRows];
+      int c[kGroupRows], incl[kGroupRows];
 #pragma unroll
       for (int k = 0; k < kGroupRows; ++k) {
-        if (k >= nr) break;  // a zero sample is kept when T = -1
-        const uint32_t m = mask16(keep_bits<HI>(v[k].x, K), keep_bits<HI>(v[k].y, K),
-                                  keep_bits<HI>(v[k].z, K), keep_bits<HI>(v[k].w, K));
-        c += __popc(m);
-        mw |= (uint64_t)m << (16 * k);
+        m[k] = (k < nr) ? mask16(keep_bits<HI>(v[k].x, K), keep_bits<HI>(v[k].y, K),
+                                 keep_bits<HI>(v[k].z, K), keep_bits<HI>(v[k].w, K))
+                        : 0u;  // a zero sample is kept when T = -1: rows past nr keep nothing
+        c[k] = __popc(m[k]);
+        incl[k] = wave_incl_scan_dpp(c[k]);
       }
-      masks[(int64_t)grp * 64 + lane] = mw;
+      uint32_t rb[kGroupRows + 1];
+      rb[0] = 0;
+#pragma unroll
+      for (int k = 0; k < kGroupRows; ++k)
+        rb[k + 1] = rb[k] + (uint32_t)__builtin_amdgcn_readlane(incl[k], 63);
+      const uint32_t total = rb[kGroupRows];
+      if (total != 0u && total <= (uint32_t)kStageSlots) {  // wave-uniform
+        group_to_lds(L, lane, m, incl, v);
+        uint32_t* e = entries + (int64_t)grp * kStageSlots;
+        for (uint32_t i = (uint32_t)lane; i < total; i += 64u) e[i] = kept_entry(L, rb, i);
+        wave_lds_sync();  // the slice is rewritten by the next group
+      }
+      if (lane == 0) group_count[grp] = (int32_t)total;
+      continue;
     } else {
+      uint32_t c = 0;
 #pragma unroll
       for (int k = 0; k < kGroupRows; ++k) {
         if (k >= nr) break;  // a zero sample is kept when T = -1
         c += __popc(keep_bits<HI>(v[k].x, K)) + __popc(keep_bits<HI>(v[k].y, K)) +
              __popc(keep_bits<HI>(v[k].z, K)) + __popc(keep_bits<HI>(v[k].w, K));
       }
-    }
-    int s = (int)c;
+      int s = (int)c;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    if (lane == 0) group_count[grp] = s;
+      for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+      if (lane == 0) group_count[grp] = s;
+    }
   }
 }
 
@@ -347,14 +415,13 @@ __global__ void k_file_counts_groups(const int64_t* __restrict__ gprefix, int64_
   }
 }
 
-// Write pass: the kept elements whose in-file rank is a multiple of stride.  Per row: keep mask
-// (16 bits per lane), wave-inclusive count by DPP, and each lane with kept samples walks its mask
-// (skip to the first rank that is a multiple of stride, then every stride-th) staging (bin,
-// sample) in the wave's LDS slice in output order; the row's emitted points are then written by
-// consecutive lanes (full-width stores from scalar row bases).
-// MASKED: the keep masks come from the count pass (one 64-bit word per lane and group); the echo
-// is read only as the 16-B chunk of a lane that emits a sample of the row.
-template <bool HI, bool MASKED>
+// Write pass: the kept samples whose in-file rank is a multiple of stride.  The group's emitted
+// outputs [first, last) (in-file indices: ceil(rank / stride) ...) go to consecutive lanes; output
+// o is the kept sample of in-group rank o * stride - rank, found with kept_entry() from the
+// group's LDS slice (or, STAGED, read from the count pass's slot when the group was staged:
+// no echo read at all).  Outputs at or beyond cap are dropped: a speculative launch (sized by an
+// earlier run) is repeated by the caller when the count says it did not fit.
+template <bool HI, bool STAGED>
 __global__ __launch_bounds__(kBlock) void k_group_write_u8(
     const uint8_t* __restrict__ echo, uint32_t n_groups, GroupMap gm, uint32_t K, int stride,
     const float* __restrict__ scale, const float* __restrict__ cos_t,
@@ -362,12 +429,11 @@ __global__ __launch_bounds__(kBlock) void k_group_write_u8(
     const int64_t* __restrict__ gprefix, const int64_t* __restrict__ file_offsets,
     int files_per_frame, float* __restrict__ x, float* __restrict__ y, float* __restrict__ val,
     int32_t* __restrict__ gain_out, int32_t* __restrict__ pf_out, int64_t cap,
-    const uint64_t* __restrict__ masks) {
-  __shared__ uint32_t s_stage[kWavesPerBlock][1024];  // (bin << 8) | sample
+    const uint32_t* __restrict__ entries) {
+  __shared__ GroupLds s_lds[kWavesPerBlock];
   const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x / 64;
-  uint32_t* stage = s_stage[wv];
-  const uint32_t wave0 = blockIdx.x * kWavesPerBlock + wv;
+  GroupLds& L = s_lds[threadIdx.x / 64];
+  const uint32_t wave0 = blockIdx.x * kWavesPerBlock + threadIdx.x / 64;
   const uint32_t n_waves = gridDim.x * kWavesPerBlock;
   const uint32_t us = (uint32_t)stride;
   const bool pow2 = (us & (us - 1u)) == 0u;
@@ -379,121 +445,55 @@ __global__ __launch_bounds__(kBlock) void k_group_write_u8(
     int64_t row0;
     int nr;
     group_rows(gm, grp, &f, &row0, &nr);
-    // everything the group reads from memory is issued up front (the LDS fences of the emission
-    // below would otherwise keep the compiler from hoisting these loads into earlier rows)
-    uint4 vv[kGroupRows];
-    uint64_t mw = 0;
-    if (MASKED) {
-      mw = masks[(int64_t)grp * 64 + lane];
-    } else {
+    // in-file rank of the group's first kept sample (< rows * 1024 < 2^32), its kept count, the
+    // group's emitted outputs [first, last) and the file's output base
+    const int64_t gp0 = gprefix[grp];
+    const uint32_t rank = (uint32_t)(gp0 - gprefix[(int64_t)f * gm.gpf]);
+    const uint32_t total = (uint32_t)(gprefix[grp + 1] - gp0);
+    const uint32_t first = pow2 ? ((rank + us - 1u) >> sh) : (rank + us - 1u) / us;
+    const uint32_t last = pow2 ? ((rank + total + us - 1u) >> sh) : (rank + total + us - 1u) / us;
+    if (last == first) continue;  // wave-uniform: nothing emitted
+    const int64_t out0 = file_offsets[f];
+    const int32_t g = gain ? gain[f] : 0;
+    const int32_t fr = (int32_t)(f / (uint32_t)files_per_frame);
+    const bool staged = STAGED && total <= (uint32_t)kStageSlots;
+    uint32_t rb[kGroupRows + 1];
+    if (!staged) {
+      uint4 vv[kGroupRows];
 #pragma unroll
       for (int k = 0; k < kGroupRows; ++k)
         vv[k] = (k < nr) ? *reinterpret_cast<const uint4*>(echo + (row0 + k) * 1024 + lane * 16)
                          : make_uint4(0u, 0u, 0u, 0u);
-    }
-    float stp[kGroupRows], ctv[kGroupRows], stv[kGroupRows];
+      uint32_t m[kGroupRows];
+      int incl[kGroupRows];
 #pragma unroll
-    for (int k = 0; k < kGroupRows; ++k) {
-      const int64_t row = row0 + (k < nr ? k : 0);
-      stp[k] = scale[row] * inv_bins;
-      ctv[k] = cos_t[row];
-      stv[k] = sin_t[row];
-    }
-    // in-file rank of the group's first kept element (< rows * 1024 < 2^32) and output base
-    uint32_t rank = (uint32_t)(gprefix[grp] - gprefix[(int64_t)f * gm.gpf]);
-    const int64_t out0 = file_offsets[f];
-    const int32_t g = gain ? gain[f] : 0;
-    const int32_t fr = (int32_t)(f / (uint32_t)files_per_frame);
-    // masks, counts and wave scans of all rows first (independent chains, interleaved)
-    uint32_t m[kGroupRows];
-    int c[kGroupRows], incl[kGroupRows];
-#pragma unroll
-    for (int k = 0; k < kGroupRows; ++k) {
-      if (MASKED)
-        m[k] = (k < nr) ? (uint32_t)(mw >> (16 * k)) & 0xffffu : 0u;
-      else
+      for (int k = 0; k < kGroupRows; ++k) {
         m[k] = (k < nr) ? mask16(keep_bits<HI>(vv[k].x, K), keep_bits<HI>(vv[k].y, K),
                                  keep_bits<HI>(vv[k].z, K), keep_bits<HI>(vv[k].w, K))
                         : 0u;
-      c[k] = __popc(m[k]);
-      incl[k] = wave_incl_scan_dpp(c[k]);
-    }
-    uint32_t rk[kGroupRows + 1];
-    rk[0] = rank;
-#pragma unroll
-    for (int k = 0; k < kGroupRows; ++k)
-      rk[k + 1] = rk[k] + (uint32_t)__builtin_amdgcn_readlane(incl[k], 63);
-    if (MASKED) {
-      // the 16-B echo chunks of the lanes that emit in a row, all loads in flight together
-#pragma unroll
-      for (int k = 0; k < kGroupRows; ++k) {
-        const uint32_t r = rk[k] + (uint32_t)(incl[k] - c[k]);
-        const uint32_t q = pow2 ? ((r + us - 1u) >> sh) : (r + us - 1u) / us;
-        vv[k] = (c[k] && q * us - r < (uint32_t)c[k])
-                    ? *reinterpret_cast<const uint4*>(echo + (row0 + k) * 1024 + lane * 16)
-                    : make_uint4(0u, 0u, 0u, 0u);
+        incl[k] = wave_incl_scan_dpp(__popc(m[k]));
       }
-    }
-    // emission: the group's rows stage (row, bin, sample) in output order in the wave's LDS slice
-    // and are flushed together (their outputs are contiguous: same file, consecutive rows) -- one
-    // fence pair and one store loop per group instead of per row, unless the slice fills up
-    const uint32_t first0 = pow2 ? ((rk[0] + us - 1u) >> sh) : (rk[0] + us - 1u) / us;
-    uint32_t flushed = first0;  // output index (in-file) of the first unflushed staged entry
-    auto flush = [&](uint32_t upto) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const int n_emit = (int)(upto - flushed);
-      const int64_t o0 = out0 + flushed;
-      // outputs at or beyond cap are dropped: a speculative launch (sized by an earlier run)
-      // is repeated by the caller when the count says it did not fit
-      const int n_fit = (int)max((int64_t)0, min((int64_t)n_emit, cap - o0));
-      for (int l = lane; l < n_fit; l += 64) {
-        const uint32_t e = stage[l];
-        const int k = (int)(e >> 18);
-        const float step = (k == 0) ? stp[0] : (k == 1) ? stp[1] : (k == 2) ? stp[2] : stp[3];
-        const float ct = (k == 0) ? ctv[0] : (k == 1) ? ctv[1] : (k == 2) ? ctv[2] : ctv[3];
-        const float st = (k == 0) ? stv[0] : (k == 1) ? stv[1] : (k == 2) ? stv[2] : stv[3];
-        const float rr = step * (float)((e >> 8) & 1023u);
-        x[o0 + l] = rr * ct;
-        y[o0 + l] = rr * st;
-        val[o0 + l] = (float)(e & 0xffu);
-        if (gain_out) gain_out[o0 + l] = g;
-        if (pf_out) pf_out[o0 + l] = fr;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      flushed = upto;
-    };
+      rb[0] = 0;
 #pragma unroll
-    for (int k = 0; k < kGroupRows; ++k) {
-      if (k >= nr) break;
-      const uint32_t rnk = rk[k], tot = rk[k + 1] - rk[k];
-      // emitted in-file indices of this row: [first, last)
-      const uint32_t first = pow2 ? ((rnk + us - 1u) >> sh) : (rnk + us - 1u) / us;
-      const uint32_t last = pow2 ? ((rnk + tot + us - 1u) >> sh) : (rnk + tot + us - 1u) / us;
-      if (last > first) {  // wave-uniform
-        if (last - flushed > 1024u) flush(first);  // the slice cannot take this row as well
-        if (c[k]) {
-          const uint32_t r = rnk + (uint32_t)(incl[k] - c[k]);
-          const uint32_t q = pow2 ? ((r + us - 1u) >> sh) : (r + us - 1u) / us;
-          int slot = (int)(q - flushed);
-          const uint4 v = vv[k];
-          // the lane's emitted samples are its kept samples j = q*stride - r, + stride, ... < c;
-          // each is located in the 16-bit mask by a branch-free select (no per-bit loops)
-          for (uint32_t j = q * us - r; j < (uint32_t)c[k]; j += us) {
-            const int kk = nth_bit16(m[k], j);
-            const uint32_t w = (kk < 4) ? v.x : (kk < 8) ? v.y : (kk < 12) ? v.z : v.w;
-            stage[slot++] = ((uint32_t)k << 18) | ((uint32_t)(lane * 16 + kk) << 8) |
-                            __builtin_amdgcn_ubfe(w, (uint32_t)(8 * (kk & 3)), 8u);
-          }
-        }
-      }
+      for (int k = 0; k < kGroupRows; ++k)
+        rb[k + 1] = rb[k] + (uint32_t)__builtin_amdgcn_readlane(incl[k], 63);
+      group_to_lds(L, lane, m, incl, vv);
     }
-    const uint32_t last_all = pow2 ? ((rk[kGroupRows] + us - 1u) >> sh)
-                                   : (rk[kGroupRows] + us - 1u) / us;
-    if (last_all > flushed) flush(last_all);
+    const uint32_t* e = entries + (int64_t)grp * kStageSlots;
+    for (uint32_t o = first + (uint32_t)lane; o < last; o += 64u) {
+      const int64_t oo = out0 + o;
+      if (oo >= cap) break;
+      const uint32_t i = o * us - rank;  // in-group kept rank
+      const uint32_t ent = staged ? e[i] : kept_entry(L, rb, i);
+      const int64_t row = row0 + (ent >> 18);
+      const float rr = scale[row] * inv_bins * (float)((ent >> 8) & 1023u);
+      x[oo] = rr * cos_t[row];
+      y[oo] = rr * sin_t[row];
+      val[oo] = (float)(ent & 0xffu);
+      if (gain_out) gain_out[oo] = g;
+      if (pf_out) pf_out[oo] = fr;
+    }
+    if (!staged) wave_lds_sync();  // the slice is rewritten by the next group
   }
 }
 
@@ -524,7 +524,7 @@ inline uint32_t u8_k(int T) {
 template <class T>
 int32_t count_impl(const T* echo, int64_t n_files, int rows, int bins, float thr, int stride,
                    int64_t* row_prefix, int64_t* file_offsets, int64_t* total_host,
-                   hipStream_t st, uint64_t* masks = nullptr) {
+                   hipStream_t st, uint32_t* entries = nullptr) {
   const int64_t n_rows = n_files * rows;
   if ((int64_t)rows * bins >= (int64_t(1) << 32) || n_rows >= (int64_t(1) << 32)) {
     set_error("rpt_polar_count: rows*bins and n_files*rows must be < 2^32");
@@ -545,12 +545,20 @@ int32_t count_impl(const T* echo, int64_t n_files, int rows, int bins, float thr
   if (grouped) {
     const int T8 = u8_threshold(thr);
     const auto* e8 = reinterpret_cast<const uint8_t*>(echo);
-    if (T8 <= 127)
-      hipLaunchKernelGGL(k_group_count_u8<false>, dim3(grid), dim3(kBlock), 0, st, e8,
-                         (uint32_t)n_units, gm, u8_k(T8), rc, masks);
-    else
-      hipLaunchKernelGGL(k_group_count_u8<true>, dim3(grid), dim3(kBlock), 0, st, e8,
-                         (uint32_t)n_units, gm, u8_k(T8), rc, masks);
+#define RPT_K1C(HI, S)                                                                    \
+  hipLaunchKernelGGL((k_group_count_u8<HI, S>), dim3(grid), dim3(kBlock), 0, st, e8,        \
+                     (uint32_t)n_units, gm, u8_k(T8), rc, entries)
+    if (entries) {
+      if (T8 <= 127)
+        RPT_K1C(false, true);
+      else
+        RPT_K1C(true, true);
+    } else if (T8 <= 127) {
+      RPT_K1C(false, false);
+    } else {
+      RPT_K1C(true, false);
+    }
+#undef RPT_K1C
   } else if (vec) {
     hipLaunchKernelGGL((k_row_count<T, true>), dim3(grid), dim3(kBlock), 0, st, echo, n_rows,
                        bins, thr, rc);
@@ -581,7 +589,7 @@ int32_t write_impl(const T* echo, int64_t n_files, int rows, int bins, float thr
                    RowGeo geo, const int32_t* gain, const int64_t* row_prefix,
                    const int64_t* file_offsets, int fpf, float* x, float* y, float* v,
                    int32_t* gout, int32_t* pf, hipStream_t st, int64_t cap = INT64_MAX,
-                   const uint64_t* masks = nullptr) {
+                   const uint32_t* entries = nullptr) {
   const int64_t n_rows = n_files * rows;
   if ((int64_t)rows * bins >= (int64_t(1) << 32) || n_rows >= (int64_t(1) << 32) || stride < 1 ||
       fpf < 1) {
@@ -598,9 +606,12 @@ int32_t write_impl(const T* echo, int64_t n_files, int rows, int bins, float thr
 #define RPT_K1W(HI, M)                                                                       \
   hipLaunchKernelGGL((k_group_write_u8<HI, M>), dim3(grid), dim3(kBlock), 0, st, e8,          \
                      (uint32_t)n_groups, gm, u8_k(T8), stride, geo.scale, geo.cos_t, geo.sin_t, \
-                     gain, row_prefix, file_offsets, fpf, x, y, v, gout, pf, cap, masks)
-    if (masks) {  // the keep masks of the count pass (the threshold is already applied)
-      RPT_K1W(false, true);
+                     gain, row_prefix, file_offsets, fpf, x, y, v, gout, pf, cap, entries)
+    if (entries) {
+      if (T8 <= 127)
+        RPT_K1W(false, true);
+      else
+        RPT_K1W(true, true);
     } else if (T8 <= 127) {
       RPT_K1W(false, false);
     } else {
@@ -765,14 +776,14 @@ __global__ __launch_bounds__(kBlock) void k_synth(rpt_synth_params p, int64_t fr
 }  // namespace
 
 // ---------------------------------------------------------------- C-ABI bodies
-// words of the keep masks of rpt_polar_count / _write (u8 sweeps of 1024 bins; else 0)
-int64_t polar_mask_words(int64_t n_files, int32_t rows) {
-  return n_files * (int64_t)((rows + kGroupRows - 1) / kGroupRows) * 64;
+// words of the staged kept entries of rpt_polar_count / _write (u8 sweeps of 1024 bins; else 0)
+int64_t polar_stage_words(int64_t n_files, int32_t rows) {
+  return n_files * (int64_t)((rows + kGroupRows - 1) / kGroupRows) * kStageSlots;
 }
 
 int32_t polar_count(const void* echo, int32_t dt, int64_t n_files, int32_t rows, int32_t bins,
                     float thr, int32_t stride, int64_t* row_prefix, int64_t* file_offsets,
-                    int64_t* total_host, hipStream_t st, uint64_t* masks) {
+                    int64_t* total_host, hipStream_t st, uint32_t* entries) {
   if (!echo || n_files < 0 || rows <= 0 || bins <= 0 || stride < 1 || !row_prefix ||
       !file_offsets) {
     set_error("rpt_polar_count: bad arguments");
@@ -787,7 +798,7 @@ int32_t polar_count(const void* echo, int32_t dt, int64_t n_files, int32_t rows,
   if (dt == RPT_ECHO_U8)
     return count_impl<uint8_t>((const uint8_t*)echo, n_files, rows, bins, thr, stride,
                                row_prefix, file_offsets, total_host, st,
-                               grouped_u8((const uint8_t*)echo, bins) ? masks : nullptr);
+                               grouped_u8((const uint8_t*)echo, bins) ? entries : nullptr);
   if (dt == RPT_ECHO_F32)
     return count_impl<float>((const float*)echo, n_files, rows, bins, thr, stride, row_prefix,
                              file_offsets, total_host, st);
@@ -799,7 +810,7 @@ int32_t polar_write(const void* echo, int32_t dt, int64_t n_files, int32_t rows,
                     const float* scale, const float* cos_t, const float* sin_t,
                     const int32_t* gain, float thr, int32_t stride, const int64_t* row_prefix,
                     const int64_t* file_offsets, int32_t fpf, float* x, float* y, float* v,
-                    int32_t* gout, int32_t* pf, hipStream_t st, const uint64_t* masks) {
+                    int32_t* gout, int32_t* pf, hipStream_t st, const uint32_t* entries) {
   if (n_files == 0) return RPT_OK;
   if (fpf < 1) {
     set_error("rpt_polar_write: files_per_frame must be >= 1");
@@ -814,7 +825,7 @@ int32_t polar_write(const void* echo, int32_t dt, int64_t n_files, int32_t rows,
   if (dt == RPT_ECHO_U8)
     return write_impl<uint8_t>((const uint8_t*)echo, n_files, rows, bins, thr, stride, geo, gain,
                                row_prefix, file_offsets, fpf, x, y, v, gout, pf, st, INT64_MAX,
-                               grouped_u8((const uint8_t*)echo, bins) ? masks : nullptr);
+                               grouped_u8((const uint8_t*)echo, bins) ? entries : nullptr);
   if (dt == RPT_ECHO_F32)
     return write_impl<float>((const float*)echo, n_files, rows, bins, thr, stride, geo, gain,
                              row_prefix, file_offsets, fpf, x, y, v, gout, pf, st);
@@ -829,14 +840,14 @@ int32_t polar_write_cap(const uint8_t* echo, int64_t n_files, int32_t rows, floa
                         const float* sin_t, const int32_t* gain, const int64_t* row_prefix,
                         const int64_t* file_offsets, int32_t fpf, float* x, float* y, float* v,
                         int32_t* gout, int32_t* pf, int64_t cap, hipStream_t st,
-                        const uint64_t* masks) {
+                        const uint32_t* entries) {
   if (!grouped_u8(echo, 1024)) {
     set_error("polar_write_cap: u8 sweeps of 1024 bins with 16-B aligned rows only");
     return RPT_ENOTSUP;
   }
   RowGeo geo{scale, nullptr, cos_t, sin_t};
   return write_impl<uint8_t>(echo, n_files, rows, 1024, thr, stride, geo, gain, row_prefix,
-                             file_offsets, fpf, x, y, v, gout, pf, st, cap, masks);
+                             file_offsets, fpf, x, y, v, gout, pf, st, cap, entries);
 }
 
 int32_t sweep_to_points(const float* inten, const float* ranges, const float* cos_t,

@@ -19,19 +19,19 @@
 namespace rpt {
 int32_t polar_count(const void* echo, int32_t dt, int64_t n_files, int32_t rows, int32_t bins,
                     float thr, int32_t stride, int64_t* row_prefix, int64_t* file_offsets,
-                    int64_t* total_host, hipStream_t st, uint64_t* masks);
+                    int64_t* total_host, hipStream_t st, uint32_t* entries);
 int32_t polar_write_cap(const uint8_t* echo, int64_t n_files, int32_t rows, float thr,
                         int32_t stride, const float* scale, const float* cos_t,
                         const float* sin_t, const int32_t* gain, const int64_t* row_prefix,
                         const int64_t* file_offsets, int32_t fpf, float* x, float* y, float* v,
                         int32_t* gout, int32_t* pf, int64_t cap, hipStream_t st,
-                        const uint64_t* masks);
+                        const uint32_t* entries);
 int32_t polar_write(const void* echo, int32_t dt, int64_t n_files, int32_t rows, int32_t bins,
                     const float* scale, const float* cos_t, const float* sin_t,
                     const int32_t* gain, float thr, int32_t stride, const int64_t* row_prefix,
                     const int64_t* file_offsets, int32_t files_per_frame, float* x, float* y,
-                    float* v, int32_t* gout, int32_t* pf, hipStream_t st, const uint64_t* masks);
-int64_t polar_mask_words(int64_t n_files, int32_t rows);
+                    float* v, int32_t* gout, int32_t* pf, hipStream_t st, const uint32_t* entries);
+int64_t polar_stage_words(int64_t n_files, int32_t rows);
 int32_t frame_times(const int32_t* pf, int64_t n, const int64_t* ids, float* t, hipStream_t st);
 int32_t bounds_xy(const float* x, const float* y, int64_t n, float* out4, hipStream_t st);
 int32_t land_grid_cells(const float* x, const float* y, const float* val, int64_t n,
@@ -234,8 +234,8 @@ struct rpt_stack {
   DevBuf<int32_t> g, pf, g2, pf2, labels, land_cnt, land_cell, seg_frame, seg_label;
   DevBuf<double> land_tot, edges;
   DevBuf<uint8_t> land_mask;
-  DevBuf<uint64_t> masks;              // K1 keep masks (count pass -> write pass)
-  int k1_masks = -1;                   // RPT_K1_MASKS, read once
+  DevBuf<uint32_t> k1_stage;           // K1 staged kept samples (count pass -> write pass)
+  int k1_staged = -1;                  // RPT_K1_STAGE (default on), read once
   DevBuf<uint8_t> bnd;                 // ST-DBSCAN bounds (+ partials) of the kept points
   std::vector<char> dbscan_bounds;     // their host copy, from the land readback
   PinnedBuf up, down;  // host staging: uploads (edges, offsets), readbacks
@@ -266,6 +266,7 @@ struct rpt_stack {
     pack_d.release();
     bnd.release();
     land_mask.release();
+    k1_stage.release();
     up.release();
     down.release();
     if (ev_ok)
@@ -303,20 +304,19 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
   RPT_TRY(down.ensure(sizeof(int64_t) * (size_t)(n_files + 2 * F + 8), st));
   int64_t* hfo = reinterpret_cast<int64_t*>(down.p);
   RPT_TRY(row_prefix.ensure((size_t)n_files * p.rows + 1, st));
-  // u8 sweeps of 1024 bins, RPT_K1_MASKS=1: the count pass keeps the keep masks (1/8 of the echo)
-  // for the write pass, which then reads the echo only where it emits.  Off by default: the
-  // write pass is latency-bound, not bandwidth-bound, so it gained less (-0.5 ms at 1000 frames)
-  // than the mask stores cost the count pass (+0.3-0.6 ms) (profiles/r2/ab_k5_k1.md)
+  // u8 sweeps of 1024 bins: the count pass stages the kept samples of every group that keeps at
+  // most 128 of them (the sparse radar case) and the write pass reads those instead of the echo,
+  // so K1 reads the echo once (RPT_K1_STAGE=0: two full reads)
   const bool grouped = p.echo_dtype == RPT_ECHO_U8 && p.bins == 1024 &&
                        (uintptr_t)echo % 16 == 0;
-  if (k1_masks < 0) {
-    const char* e = std::getenv("RPT_K1_MASKS");
-    k1_masks = (e && std::atoi(e) != 0) ? 1 : 0;
+  if (k1_staged < 0) {
+    const char* e = std::getenv("RPT_K1_STAGE");
+    k1_staged = (e && std::atoi(e) == 0) ? 0 : 1;
   }
-  uint64_t* mk = nullptr;
-  if (grouped && k1_masks) {
-    RPT_TRY(masks.ensure((size_t)polar_mask_words(n_files, p.rows), st));
-    mk = masks.p;
+  uint32_t* mk = nullptr;
+  if (grouped && k1_staged) {
+    RPT_TRY(k1_stage.ensure((size_t)polar_stage_words(n_files, p.rows), st));
+    mk = k1_stage.p;
   }
   RPT_TRY(polar_count(echo, p.echo_dtype, n_files, p.rows, p.bins, p.threshold, p.stride,
                       row_prefix.p, file_off.p, nullptr, st, mk));
@@ -854,10 +854,19 @@ int32_t rpt_shard_polar(rpt_shard* h, const rpt_stack_params* p, const void* ech
   RPT_TRY(h->bnd.ensure(8, st));
   const size_t down_bytes = sizeof(int64_t) * (size_t)(n_files + 2) + 16;
   RPT_TRY(S.down.ensure(down_bytes, st));
-  RPT_TRY(polar_count(echo, p->echo_dtype, n_files, p->rows, p->bins, p->threshold, p->stride,
-                      S.row_prefix.p, S.file_off.p, nullptr, st, nullptr));
   const bool grouped = p->echo_dtype == RPT_ECHO_U8 && p->bins == 1024 &&
                        (uintptr_t)echo % 16 == 0;
+  if (S.k1_staged < 0) {
+    const char* e = std::getenv("RPT_K1_STAGE");
+    S.k1_staged = (e && std::atoi(e) == 0) ? 0 : 1;
+  }
+  uint32_t* mk = nullptr;  // staged kept samples, as in rpt_stack_run
+  if (grouped && S.k1_staged) {
+    RPT_TRY(S.k1_stage.ensure((size_t)polar_stage_words(n_files, p->rows), st));
+    mk = S.k1_stage.p;
+  }
+  RPT_TRY(polar_count(echo, p->echo_dtype, n_files, p->rows, p->bins, p->threshold, p->stride,
+                      S.row_prefix.p, S.file_off.p, nullptr, st, mk));
   int64_t spec_cap = -1;
   const int64_t* n_dev = S.file_off.p + n_files;
   if (grouped && S.x.p && S.y.p && S.v.p && S.g.p && S.pf.p) {
@@ -866,8 +875,7 @@ int32_t rpt_shard_polar(rpt_shard* h, const rpt_stack_params* p, const void* ech
     spec_cap = (int64_t)std::min({S.x.cap, S.y.cap, S.v.cap, S.g.cap, S.pf.cap});
     RPT_TRY(polar_write_cap((const uint8_t*)echo, n_files, p->rows, p->threshold, p->stride,
                             scale, cos_t, sin_t, gain, S.row_prefix.p, S.file_off.p, G, S.x.p,
-                            S.y.p, S.v.p, gain ? S.g.p : nullptr, S.pf.p, spec_cap, st,
-                            nullptr));
+                            S.y.p, S.v.p, gain ? S.g.p : nullptr, S.pf.p, spec_cap, st, mk));
     hipLaunchKernelGGL(k_init_bounds, dim3(1), dim3(64), 0, st, h->bnd.p);
     hipLaunchKernelGGL(k_xy_bounds_part, dim3(grid_for(std::max<int64_t>(spec_cap, 1), 256, 512)),
                        dim3(256), 0, st, S.x.p, S.y.p, spec_cap, n_dev, h->bnd.p);
@@ -891,7 +899,7 @@ int32_t rpt_shard_polar(rpt_shard* h, const rpt_stack_params* p, const void* ech
     RPT_TRY(S.pf.ensure(cap, st));
     RPT_TRY(polar_write(echo, p->echo_dtype, n_files, p->rows, p->bins, scale, cos_t, sin_t, gain,
                         p->threshold, p->stride, S.row_prefix.p, S.file_off.p, G, S.x.p, S.y.p,
-                        S.v.p, gain ? S.g.p : nullptr, S.pf.p, st, nullptr));
+                        S.v.p, gain ? S.g.p : nullptr, S.pf.p, st, mk));
     hipLaunchKernelGGL(k_init_bounds, dim3(1), dim3(64), 0, st, h->bnd.p);
     hipLaunchKernelGGL(k_xy_bounds_part, dim3(grid_for(std::max<int64_t>(N, 1), 256, 512)),
                        dim3(256), 0, st, S.x.p, S.y.p, N, (const int64_t*)nullptr, h->bnd.p);

@@ -147,11 +147,11 @@ _SIGS = [
     ("rpt_polar_write", C.c_int32,
      [vp, C.c_int32, C.c_int64, C.c_int32, C.c_int32, vp, vp, vp, vp, C.c_float, C.c_int32, vp,
       vp, C.c_int32, vp, vp, vp, vp, vp, vp]),
-    ("rpt_polar_mask_words", C.c_int64, [C.c_int64, C.c_int32]),
-    ("rpt_polar_count_masked", C.c_int32,
+    ("rpt_polar_stage_words", C.c_int64, [C.c_int64, C.c_int32]),
+    ("rpt_polar_count_staged", C.c_int32,
      [vp, C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_float, C.c_int32, vp, vp, c_i64p, vp,
       vp]),
-    ("rpt_polar_write_masked", C.c_int32,
+    ("rpt_polar_write_staged", C.c_int32,
      [vp, C.c_int32, C.c_int64, C.c_int32, C.c_int32, vp, vp, vp, vp, C.c_float, C.c_int32, vp,
       vp, C.c_int32, vp, vp, vp, vp, vp, vp, vp]),
     ("rpt_frame_times", C.c_int32, [vp, C.c_int64, vp, vp, vp]),

@@ -16,8 +16,8 @@ from _stack_check import oracle_stack as _oracle_stack
 pytestmark = pytest.mark.gpu
 
 
-def _k1(dev, echo, scale, angle, gains=(0,), threshold=10.0, stride=4, f32=False, masked=False):
-    """Run rpt_polar_count/write (or their keep-mask variants) on a batch of equally shaped
+def _k1(dev, echo, scale, angle, gains=(0,), threshold=10.0, stride=4, f32=False, staged=False):
+    """Run rpt_polar_count/write (or their staged-entry variants) on a batch of equally shaped
     sweeps."""
     from rpt import _abi
     from rpt._device import stream_handle
@@ -42,10 +42,10 @@ def _k1(dev, echo, scale, angle, gains=(0,), threshold=10.0, stride=4, f32=False
     tot = _abi.C.c_int64(0)
     dt = _abi.ECHO_F32 if f32 else _abi.ECHO_U8
     st = stream_handle(dev)
-    mk = torch.zeros(max(int(lib.rpt_polar_mask_words(nf, rows)), 1), dtype=torch.int64,
-                     device=dev) if masked else None
-    if masked:
-        _abi.check(lib.rpt_polar_count_masked(ed.data_ptr(), dt, nf, rows, bins, threshold,
+    mk = torch.zeros(max(int(lib.rpt_polar_stage_words(nf, rows)), 1), dtype=torch.int32,
+                     device=dev) if staged else None
+    if staged:
+        _abi.check(lib.rpt_polar_count_staged(ed.data_ptr(), dt, nf, rows, bins, threshold,
                                               stride, rp.data_ptr(), fo.data_ptr(),
                                               _abi.C.byref(tot), mk.data_ptr(), st))
     else:
@@ -59,8 +59,8 @@ def _k1(dev, echo, scale, angle, gains=(0,), threshold=10.0, stride=4, f32=False
     args = (ed.data_ptr(), dt, nf, rows, bins, sc.data_ptr(), cd.data_ptr(), sd.data_ptr(),
             gd.data_ptr(), threshold, stride, rp.data_ptr(), fo.data_ptr(), len(gains),
             x.data_ptr(), y.data_ptr(), v.data_ptr(), g.data_ptr(), pf.data_ptr())
-    if masked:
-        _abi.check(lib.rpt_polar_write_masked(*args, mk.data_ptr(), st))
+    if staged:
+        _abi.check(lib.rpt_polar_write_staged(*args, mk.data_ptr(), st))
     else:
         _abi.check(lib.rpt_polar_write(*args, st))
     return (x[:n].cpu().numpy(), y[:n].cpu().numpy(), v[:n].cpu().numpy(), g[:n].cpu().numpy(),
@@ -371,21 +371,24 @@ def test_k1_grouped_u8_matches_generic_rows(gpu):
                     np.testing.assert_array_equal(b[i], ref[i])
 
 
-def test_k1_keep_masks_match_two_full_reads(gpu):
-    """The keep-mask K1 (count pass stores 64-bit masks per lane and group, write pass reads the
-    masks and only the 16-B echo chunks that emit) against the two-full-read kernels: thresholds
-    on both sides of 127 and at the ends, strides 1/3/4/7, short last groups, dense and sparse."""
+def test_k1_staged_entries_match_two_full_reads(gpu):
+    """The staged K1 (the count pass stores the kept samples of every group keeping <= 128 of
+    them, the write pass reads those instead of the echo; denser groups read the echo again)
+    against the two-full-read kernels: thresholds on both sides of 127 and at the ends, strides
+    1/3/4/7, short last groups, an empty file between others, and densities from all-staged to
+    none-staged with mixed groups in between."""
     rng = np.random.default_rng(17)
-    for rows, p in ((4096, 0.02), (1023, 0.5), (6, 1.0)):
-        echo = np.where(rng.random((3, rows, 1024)) < p, rng.integers(0, 256, (3, rows, 1024)),
+    for rows, p in ((4096, 0.02), (1023, 0.5), (6, 1.0), (37, 0.0), (512, 0.03)):
+        echo = np.where(rng.random((6, rows, 1024)) < p, rng.integers(0, 256, (6, rows, 1024)),
                         0).astype(np.uint8)
-        scale = [np.full(rows, 231.5, np.float32)] * 3
-        angle = [np.linspace(0, 8000, rows).astype(np.float32)] * 3
+        echo[2] = 0
+        scale = [np.full(rows, 231.5, np.float32)] * 6
+        angle = [np.linspace(0, 8000, rows).astype(np.float32)] * 6
         for thr in (-3.0, 10.0, 127.5, 200.0, 255.0):
             for stride in (1, 3, 4, 7):
                 a = _k1(gpu, echo, scale, angle, gains=(40, 50, 75), threshold=thr, stride=stride)
                 b = _k1(gpu, echo, scale, angle, gains=(40, 50, 75), threshold=thr, stride=stride,
-                        masked=True)
+                        staged=True)
                 for i in range(6):
                     np.testing.assert_array_equal(a[i], b[i])
 
