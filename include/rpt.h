@@ -172,6 +172,25 @@ int32_t rpt_stdbscan(const float* x, const float* y, const float* z, int64_t str
                      const float* times, int64_t n, double eps_space, double eps_time,
                      int32_t min_samples, int32_t* labels, rpt_stdbscan_stats* stats,
                      void* stream);
+/* Denoise variant (replaces st_dbscan of PointCloudWorkF/stdbscan_denoising_pipeline.py:264-369;
+ * 2-D, x / y / times dev float32 [n]): core = >= min_samples neighbours (itself included, same
+ * test as rpt_stdbscan) spanning >= min_frames distinct int32(times) frames; clusters numbered by
+ * their minimum core index; a non-core point takes the smallest cluster m adjacent to it through a
+ * core point with (its index > m, or it is a neighbour of core point m) -- the FIFO expansion's
+ * result, :340-367.  n == 0 is not an error (no labels written).  RPT_ENOTSUP when
+ * eps_time > 30 with min_frames >= 2.  Synchronises. */
+/* pandas DataFrame.groupby(labels).mean() of float32 x / y / intensity columns (pandas 2.x
+ * group_mean: float32 Kahan-compensated sum in row order, / (float)count), for labels in
+ * [0, n_labels) (noise -1 and labels >= n_labels ignored): count (dev int64) and the three means
+ * (dev float32), each [n_labels]; the cluster table of stdbscan_denoising_pipeline.py:997-1012.
+ * Synchronises. */
+int32_t rpt_label_means(const int32_t* labels, const float* x, const float* y,
+                        const float* intensity, int64_t n, int64_t n_labels, int64_t* count,
+                        float* mean_x, float* mean_y, float* mean_intensity, void* stream);
+int32_t rpt_stdbscan_denoise(const float* x, const float* y, const float* times, int64_t n,
+                             double eps_space, double eps_time, int32_t min_samples,
+                             int32_t min_frames, int32_t* labels, rpt_stdbscan_stats* stats,
+                             void* stream);
 
 /* ---- phased ST-DBSCAN (frame-sharded multi-GPU) -------------------------------------
  * The fused rpt_stdbscan split into phases so ranks can exchange halo data between them:

@@ -9,6 +9,7 @@ function citing the reference file:line it follows (paths relative to the refere
 
 * ``stdbscan``          BFS ST-DBSCAN, C (``stdbscan_oracle.c``) — 3_stdbscan_point_clouds.py:101-136
 * ``stdbscan_uf``       the same labels by the set formulation, OpenMP (large stacks)
+* ``stdbscan_denoise``  the denoise variant, C — PointCloudWorkF/stdbscan_denoising_pipeline.py:264-369
 * ``polar_scatter``     4_temporal_object_tracker.py:200-232 arithmetic on an echo matrix
 * ``build_frames``      build_frame :312-352 concatenation
 * ``land_filter``       :359-436
@@ -56,6 +57,9 @@ def _lib():
                                         C.c_double, C.c_double, C.c_int32, C.c_void_p]
         lib.oracle_stdbscan_uf.restype = C.c_int32
         lib.oracle_stdbscan_uf.argtypes = lib.oracle_stdbscan.argtypes
+        lib.oracle_stdbscan_denoise.restype = C.c_int32
+        lib.oracle_stdbscan_denoise.argtypes = lib.oracle_stdbscan.argtypes[:7] + [
+            C.c_int32, C.c_void_p]
         lib.oracle_neighbour_counts.restype = C.c_int32
         lib.oracle_neighbour_counts.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int64,
                                                 C.c_double, C.c_double, C.c_void_p]
@@ -98,6 +102,23 @@ def stdbscan_uf(coords, times, eps_space: float, eps_time: float, min_samples: i
                                   float(eps_time), int(min_samples), labels.ctypes.data)
     if r < 0:
         raise MemoryError("oracle_stdbscan_uf failed")
+    return labels
+
+
+def stdbscan_denoise(coords, times, eps_space: float, eps_time: float, min_samples: int,
+                     min_frames: int = 2) -> np.ndarray:
+    """Labels of the denoise variant (PointCloudWorkF/stdbscan_denoising_pipeline.py:264-369:
+    min_frames core condition, FIFO expansion), the reference's loop restated in C."""
+    c, t = _prep(coords, times)
+    n = c.shape[0]
+    labels = np.empty(n, dtype=np.int32)
+    if n == 0:
+        return labels
+    r = _lib().oracle_stdbscan_denoise(c.ctypes.data, c.shape[1], t.ctypes.data, n,
+                                       float(eps_space), float(eps_time), int(min_samples),
+                                       int(min_frames), labels.ctypes.data)
+    if r < 0:
+        raise MemoryError("oracle_stdbscan_denoise failed")
     return labels
 
 

@@ -508,3 +508,103 @@ int32_t oracle_stdbscan_uf(const float* coords, int32_t dim, const float* times,
   free(x.gkey); free(x.gidx); free(x.gc); free(x.gt);
   return ncl;
 }
+
+/* ---- denoise variant: PointCloudWorkF/stdbscan_denoising_pipeline.py:264-369, restated as the
+ * reference's own loop.  Same neighbour predicate as above (BallTree query_radius over float32
+ * coords, float32 time filter :317-321).  Differences from oracle_stdbscan:
+ *   - core (:308-315): len(neighbours) >= min_samples AND the neighbours' int32(times) frames
+ *     (astype truncation, :305) number >= min_frames;
+ *   - expansion (:340-367): FIFO queue seeded with ALL neighbours of the seed (visited or not),
+ *     a popped unvisited core point appends its neighbours that are neither visited nor already
+ *     queued in this cluster (in_queue, reset per cluster, :357-367); every popped point still
+ *     labelled -1 takes the cluster id.
+ * n == 0 returns 0 clusters (the reference returns an empty array, :286-287). */
+static int cmp_i32(const void* a, const void* b) {
+  const int32_t x = *(const int32_t*)a, y = *(const int32_t*)b;
+  return (x > y) - (x < y);
+}
+
+static int32_t np_int32(float v) {
+  /* numpy float32 -> int32 astype on x86-64: truncation; NaN / out of range -> INT32_MIN */
+  if (!(v == v) || v >= 2147483648.0f || v < -2147483648.0f) return INT32_MIN;
+  return (int32_t)v;
+}
+
+static int denoise_core(const ctx_t* x, const int64_t* nb, int64_t cnt, int32_t min_samples,
+                        int32_t min_frames, int32_t* fbuf) {
+  if (cnt < (int64_t)min_samples) return 0;
+  for (int64_t k = 0; k < cnt; ++k) fbuf[k] = np_int32(x->t[nb[k]]);
+  qsort(fbuf, (size_t)cnt, sizeof(int32_t), cmp_i32);
+  int64_t uniq = cnt > 0 ? 1 : 0;
+  for (int64_t k = 1; k < cnt; ++k) uniq += fbuf[k] != fbuf[k - 1];
+  return uniq >= (int64_t)min_frames;
+}
+
+int32_t oracle_stdbscan_denoise(const float* coords, int32_t dim, const float* times, int64_t n,
+                                double eps_space, double eps_time, int32_t min_samples,
+                                int32_t min_frames, int32_t* labels) {
+  if (n <= 0) return 0;
+  ctx_t x;
+  x.c = coords;
+  x.dim = dim;
+  x.t = times;
+  x.eps2 = eps_space * eps_space;
+  if (!(eps_space >= 0.0)) x.eps2 = -1.0;
+  x.epst = (float)eps_time;
+  x.n = n;
+  x.order = (int64_t*)malloc(sizeof(int64_t) * (size_t)n);
+  x.tsorted = (float*)malloc(sizeof(float) * (size_t)n);
+  int64_t* nb = (int64_t*)malloc(sizeof(int64_t) * (size_t)n);
+  int64_t* nb2 = (int64_t*)malloc(sizeof(int64_t) * (size_t)n);
+  int32_t* fbuf = (int32_t*)malloc(sizeof(int32_t) * (size_t)n);
+  int64_t* queue = (int64_t*)malloc(sizeof(int64_t) * (size_t)(2 * n + 1));
+  uint8_t* visited = (uint8_t*)calloc((size_t)n, 1);
+  uint8_t* in_queue = (uint8_t*)calloc((size_t)n, 1);
+  if (!x.order || !x.tsorted || !nb || !nb2 || !fbuf || !queue || !visited || !in_queue)
+    return -1;
+  for (int64_t i = 0; i < n; ++i) x.order[i] = i;
+  g_t_for_sort = times;
+  qsort(x.order, (size_t)n, sizeof(int64_t), cmp_time);
+  x.n_finite = 0;
+  for (int64_t k = 0; k < n; ++k) {
+    x.tsorted[k] = times[x.order[k]];
+    if (isfinite(x.tsorted[k])) x.n_finite = k + 1;
+  }
+  x.gkey = x.gidx = NULL;
+  x.gc = x.gt = NULL;
+  build_grid(&x);
+  for (int64_t i = 0; i < n; ++i) labels[i] = -1;
+  int32_t cid = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    if (visited[i]) continue;
+    visited[i] = 1;
+    const int64_t cnt = neighbours(&x, i, nb);
+    if (!denoise_core(&x, nb, cnt, min_samples, min_frames, fbuf)) continue;
+    labels[i] = cid;
+    int64_t head = 0, tail = 0;
+    for (int64_t k = 0; k < cnt; ++k) {
+      queue[tail++] = nb[k];
+      in_queue[nb[k]] = 1;
+    }
+    while (head < tail) {
+      const int64_t pt = queue[head++];
+      if (!visited[pt]) {
+        visited[pt] = 1;
+        const int64_t c2 = neighbours(&x, pt, nb2);
+        if (denoise_core(&x, nb2, c2, min_samples, min_frames, fbuf))
+          for (int64_t k = 0; k < c2; ++k)
+            if (!visited[nb2[k]] && !in_queue[nb2[k]]) {
+              queue[tail++] = nb2[k];
+              in_queue[nb2[k]] = 1;
+            }
+      }
+      if (labels[pt] == -1) labels[pt] = cid;
+    }
+    for (int64_t k = 0; k < tail; ++k) in_queue[queue[k]] = 0; /* in_queue[:] = False */
+    ++cid;
+  }
+  free(x.order); free(x.tsorted); free(nb); free(nb2); free(fbuf); free(queue);
+  free(visited); free(in_queue);
+  free(x.gkey); free(x.gidx); free(x.gc); free(x.gt);
+  return cid;
+}

@@ -9,6 +9,13 @@
 namespace rpt {
 const char* last_error_cstr();
 void release_scratch_current();
+int32_t label_means(const int32_t* labels, const float* x, const float* y, const float* inten,
+                    int64_t n, int64_t n_labels, int64_t* o_count, float* o_x, float* o_y,
+                    float* o_v, hipStream_t st);
+int32_t stdbscan_denoise(const float* x, const float* y, const float* t, int64_t n,
+                         double eps_space, double eps_time, int32_t min_samples,
+                         int32_t min_frames, int32_t* labels, rpt_stdbscan_stats* stats,
+                         hipStream_t st);
 int32_t stdbscan(const float* x, const float* y, const float* z, int64_t stride, const float* t,
                  int64_t n, double eps_space, double eps_time, int32_t min_samples,
                  int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st, int dim);
@@ -178,6 +185,27 @@ int32_t rpt_stdbscan(const float* x, const float* y, const float* z, int64_t str
   const int dim = z ? 3 : 2;
   return rpt::stdbscan(x, y, z, stride, times, n, eps_space, eps_time, min_samples, labels,
                        stats, rpt::as_stream(stream), dim);
+}
+
+int32_t rpt_label_means(const int32_t* labels, const float* x, const float* y,
+                        const float* intensity, int64_t n, int64_t n_labels, int64_t* count,
+                        float* mean_x, float* mean_y, float* mean_intensity, void* stream) {
+  rpt::clear_error();
+  return rpt::label_means(labels, x, y, intensity, n, n_labels, count, mean_x, mean_y,
+                          mean_intensity, rpt::as_stream(stream));
+}
+
+int32_t rpt_stdbscan_denoise(const float* x, const float* y, const float* times, int64_t n,
+                             double eps_space, double eps_time, int32_t min_samples,
+                             int32_t min_frames, int32_t* labels, rpt_stdbscan_stats* stats,
+                             void* stream) {
+  rpt::clear_error();
+  if (n < 0) {
+    rpt::set_error("rpt_stdbscan_denoise: n < 0");
+    return RPT_EINVAL;
+  }
+  return rpt::stdbscan_denoise(x, y, times, n, eps_space, eps_time, min_samples, min_frames,
+                               labels, stats, rpt::as_stream(stream));
 }
 
 int32_t rpt_polar_count(const void* echo, int32_t echo_dtype, int64_t n_files, int32_t rows,

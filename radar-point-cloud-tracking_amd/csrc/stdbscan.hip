@@ -1808,6 +1808,227 @@ __global__ __launch_bounds__(kBlock) void k_label_global_core(const uint8_t* __r
   }
 }
 
+// ---------------------------------------------------------------- denoise variant (O8)
+// PointCloudWorkF/stdbscan_denoising_pipeline.py:264-369.  A point is core when it has
+// >= min_samples space-time neighbours (itself included, as K5) AND those neighbours span
+// >= min_frames distinct int32(t) frames (:308-315); clusters are expanded with a FIFO queue that
+// never re-queues a visited point (:346-363).  The component structure is K6's; only the core
+// condition and the border rule differ (see k_label_fifo).
+//
+// Frames, cell level (every finite t integral: a slab is one frame): a cell whose column (same
+// x, y) holds, in >= min_frames - 1 other slabs, a cell every point of which is a neighbour of
+// every point of this cell (box test) has all its core points frame-complete.
+__global__ __launch_bounds__(kBlock) void k_frames_cells(Geom g, int R,
+                                                        const int32_t* __restrict__ occ,
+                                                        const int32_t* __restrict__ n_occ,
+                                                        const CellRec<2>* __restrict__ crec,
+                                                        const uint32_t* __restrict__ occ_bits,
+                                                        int min_frames,
+                                                        uint8_t* __restrict__ fok) {
+  const int64_t no = *n_occ;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < no;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t ca = occ[q];
+    if ((int64_t)ca >= g.cells) continue;  // non-finite time: settled per point
+    const int cx = ca % g.nx;
+    const int rr = ca / g.nx;
+    const int cy = rr % g.ny;
+    const int cs = rr / g.ny;
+    const CellRec<2> ra = crec[ca];
+    const float4 A1 = rec_boxA<2>(ra), B1 = rec_boxB(ra);
+    int frames = 1;  // the cell's own
+    const int s0 = max(cs - R, 0), s1 = min(cs + R, g.nt - 1);
+    for (int sl = s0; sl <= s1 && frames < min_frames; ++sl) {
+      if (sl == cs) continue;
+      const int64_t c = ((int64_t)sl * g.ny + cy) * g.nx + cx;
+      if (!((occ_bits[c >> 5] >> (c & 31)) & 1u)) continue;
+      const CellRec<2> rc = crec[c];
+      frames += (classify_cells<2>(A1, B1, rec_boxA<2>(rc), rec_boxB(rc), g) == 1) ? 1 : 0;
+    }
+    fok[ca] = frames >= min_frames ? 1 : 0;
+  }
+}
+
+// Queue of the core points whose frame count is still open; points of the isolated cell
+// (non-finite t: no neighbour, 0 frames) are settled here.
+__global__ __launch_bounds__(kBlock) void k_frames_queue(const int32_t* __restrict__ skey,
+                                                        int64_t n, int64_t cells,
+                                                        const uint8_t* __restrict__ fok,
+                                                        int min_frames, int refine,
+                                                        uint8_t* __restrict__ core,
+                                                        int32_t* __restrict__ list,
+                                                        int32_t* __restrict__ count) {
+  for (int64_t tile = (int64_t)blockIdx.x * kBlock * kItems; tile < n;
+       tile += (int64_t)gridDim.x * kBlock * kItems)
+    block_append(
+        tile, n,
+        [&](int64_t s) -> bool {
+          if (!core[s]) return false;
+          const int32_t key = skey[s];
+          if ((int64_t)key >= cells) {
+            core[s] = (min_frames <= 0) ? 1 : 0;
+            return false;
+          }
+          return refine && !(fok && fok[key]);
+        },
+        list, count);
+}
+
+// Frame count of one queued core point per wave: the int32(t) offsets (within +-31 of its own:
+// |dt| <= eps_t <= 30, checked by the host) of its neighbours as a 64-bit set, scanned cell by
+// cell until min_frames distinct frames are seen.
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_frames_points(const float4* __restrict__ pts,
+                                                         const int32_t* __restrict__ skey, Geom g,
+                                                         const CellRec<D>* __restrict__ crec,
+                                                         const uint32_t* __restrict__ occ_bits,
+                                                         const float2* __restrict__ slab_t,
+                                                         int integral, int min_frames,
+                                                         const int32_t* __restrict__ list,
+                                                         const int32_t* __restrict__ count,
+                                                         uint8_t* __restrict__ core) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+  const int64_t nq = *count;
+  for (int64_t q = w0; q < nq; q += nw) {
+    const int s = list[q];
+    const float4 p = pts[s];
+    const int own = (int)p.w;  // numpy astype(int32): truncation toward zero
+    int cx, cy, cz;
+    decode_key<D>(skey[s], g, cx, cy, cz);
+    const Window w = make_window<D, false>(cx, cy, cz, p.w, p.w, g, slab_t);
+    uint64_t seen = 0;
+    for (int base = 0; base < w.total && __popcll(seen) < min_frames; base += 64) {
+      const int qq = base + lane;
+      const int64_t c = (qq < w.total) ? window_cell<D>(w, qq, g, slab_t, p.w, p.w) : -1;
+      int b = 0, e = 0, cls = 0;
+      if (c >= 0 && ((occ_bits[c >> 5] >> (c & 31)) & 1u)) {
+        const CellRec<D> cr = crec[c];
+        b = cr.b;
+        e = cr.e;
+        cls = classify<D>(p, rec_boxA<D>(cr), rec_boxB(cr), g);
+      }
+      uint64_t pm = __ballot(cls != 0);
+      while (pm && __popcll(seen) < min_frames) {
+        const int l = __ffsll((unsigned long long)pm) - 1;
+        pm &= pm - 1;
+        const int bb = __shfl(b, l), cl = __shfl(cls, l);
+        // a whole-cell hit in frame-id data is one frame: its first point says which
+        const int ee = (cl == 1 && integral) ? bb + 1 : __shfl(e, l);
+        for (int j0 = bb; j0 < ee && __popcll(seen) < min_frames; j0 += 64) {
+          const int j = j0 + lane;
+          uint64_t bit = 0;
+          if (j < ee) {
+            const float4 pj = pts[j];
+            if (cl == 1 || adjacent<D>(p, pj, g))  // |t| >= 2^31 (saturating casts): clamped
+              bit = 1ull << min(max((int)pj.w - own + 32, 0), 63);
+          }
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1)
+            bit |= (uint64_t)__shfl_xor((unsigned long long)bit, off);
+          seen |= bit;
+        }
+      }
+    }
+    if (lane == 0) core[s] = (__popcll(seen) >= min_frames) ? 1 : 0;
+  }
+}
+
+// spos[orig] = sorted position
+__global__ void k_inverse_perm(const int32_t* __restrict__ sorig, int64_t n,
+                               int32_t* __restrict__ spos) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x)
+    spos[sorig[s]] = (int32_t)s;
+}
+
+// Border labels of the FIFO expansion (:340-367).  Clusters are drained one after another in
+// seed order, the seed being the component's minimum core index m (what ccmin holds).  A non-core
+// point p (original index P) is popped by cluster m -- and keeps the first such label -- iff it is
+// adjacent to a core point of m and either P > m (still unvisited when m's cores expand) or p is a
+// neighbour of the seed itself (the seed's neighbour list is queued whole, visited or not, :343).
+// Every qualifying m < P beats every m > P, so the first kind is a plain minimum and the second is
+// resolved smallest-first with one seed test per distinct m.  One wave per non-core point.
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_label_fifo(const float4* __restrict__ pts,
+                                                      const int32_t* __restrict__ skey, Geom g,
+                                                      const CellRec<D>* __restrict__ crec,
+                                                      const uint32_t* __restrict__ occ_bits,
+                                                      const float2* __restrict__ slab_t,
+                                                      const int32_t* __restrict__ ccmin,
+                                                      const int32_t* __restrict__ rep,
+                                                      const int32_t* __restrict__ sorig,
+                                                      const int32_t* __restrict__ spos,
+                                                      const int32_t* __restrict__ cid,
+                                                      const int32_t* __restrict__ nc_list,
+                                                      const int32_t* __restrict__ nc_count,
+                                                      int32_t* __restrict__ labels) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+  const int64_t nq = *nc_count;
+  for (int64_t q = w0; q < nq; q += nw) {
+    const int s = nc_list[q];
+    const int P = sorig[s];
+    const int32_t key = skey[s];
+    int best_lt = INT_MAX, best_gt = INT_MAX;
+    if ((int64_t)key < g.cells) {
+      const float4 p = pts[s];
+      int cx, cy, cz;
+      decode_key<D>(key, g, cx, cy, cz);
+      const Window w = make_window<D, false>(cx, cy, cz, p.w, p.w, g, slab_t);
+      for (int base = 0; base < w.total; base += 64) {
+        const int qq = base + lane;
+        const int64_t c = (qq < w.total) ? window_cell<D>(w, qq, g, slab_t, p.w, p.w) : -1;
+        int b = 0, e = 0, cls = 0;
+        if (c >= 0 && ((occ_bits[c >> 5] >> (c & 31)) & 1u) && rep[c] >= 0) {
+          const CellRec<D> cr = crec[c];
+          b = cr.b;
+          e = cr.e;
+          cls = classify<D>(p, rec_boxA<D>(cr), rec_boxB(cr), g);
+        }
+        uint64_t pm = __ballot(cls != 0);
+        while (pm) {
+          const int l = __ffsll((unsigned long long)pm) - 1;
+          pm &= pm - 1;
+          const int bb = __shfl(b, l), ee = __shfl(e, l), cl = __shfl(cls, l);
+          for (int j0 = bb; j0 < ee; j0 += 64) {
+            const int j = j0 + lane;
+            int m = -1;
+            if (j < ee) {
+              m = ccmin[j];
+              if (m >= 0 && cl != 1 && !adjacent<D>(p, pts[j], g)) m = -1;
+            }
+            int lt = (m >= 0 && m < P) ? m : INT_MAX;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) lt = min(lt, __shfl_xor(lt, off));
+            best_lt = min(best_lt, lt);
+            if (best_lt != INT_MAX) continue;  // a smaller qualifying cluster is known
+            // m > P: the smallest not yet rejected whose seed is a neighbour of p
+            int cand = (m > P && m < best_gt) ? m : INT_MAX;
+            while (true) {
+              int mm = cand;
+#pragma unroll
+              for (int off = 32; off > 0; off >>= 1) mm = min(mm, __shfl_xor(mm, off));
+              if (mm == INT_MAX) break;
+              if (adjacent<D>(p, pts[spos[mm]], g)) {
+                best_gt = mm;
+                break;
+              }
+              if (cand == mm) cand = INT_MAX;
+            }
+          }
+        }
+      }
+    }
+    if (lane == 0) {
+      const int best = (best_lt != INT_MAX) ? best_lt : best_gt;
+      labels[P] = (best != INT_MAX) ? cid[best] : -1;
+    }
+  }
+}
+
 struct Timer {
   bool on = false;
   hipStream_t st{};
@@ -1865,6 +2086,8 @@ struct DbscanState {
     return static_cast<const CellRec<D>*>(crec);
   }
   int32_t* slab = nullptr;   // per sorted point: final label of core points (global path)
+  uint8_t* fok = nullptr;    // per cell: frame condition met by every core point (denoise)
+  bool integral_t = false;   // every finite t integral (slab = one frame id)
   int64_t* stmp = nullptr;
   Timer tm;
 
@@ -1884,6 +2107,9 @@ struct DbscanState {
   int32_t fill_stats(int32_t n_clusters, rpt_stdbscan_stats* stats);
   int32_t labels_global(const int64_t* rep_orig, const int64_t* reps, int64_t nr,
                         int32_t* labels, hipStream_t st);
+  // denoise variant: the min_frames core condition, then the FIFO border labels
+  int32_t frames_pass(int32_t min_frames, hipStream_t st);
+  int32_t labels_fifo(int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st);
 };
 
 template <int D>
@@ -1927,6 +2153,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
     hi[k] = (double)ord2f(hb.mx[k]);
   }
   if (hb.n_finite_t == 0) lo[3] = hi[3] = 0.0;
+  integral_t = !hb.nonintegral_t;
   const double margin = 1.0 + 1.0 / 1048576.0;  // 2^-20
   double cs = (eps_space > 0.0 ? eps_space * 0.5 : 1.0) * margin;
   double ct = !hb.nonintegral_t ? 1.0 : (epst > 0.f ? (double)epst : 1.0) * margin;
@@ -1980,7 +2207,8 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   bud.add<int32_t>(n);      // ccmin
   bud.add<int32_t>(n + 1);  // cid
   bud.add<int32_t>(n + 1);  // non-core list (+count)
-  bud.add<int32_t>(n);      // slab (global finalize)
+  bud.add<int32_t>(n);      // slab (global finalize; denoise: orig -> sorted)
+  bud.add<uint8_t>(C1);     // fok (denoise)
   bud.add<int32_t>(n + 1);  // occ
   bud.add<int32_t>(n + 1);  // hpos
   bud.add<CellRec<D>>(C1);  // crec
@@ -2008,6 +2236,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   cid = arena.carve_n<int32_t>(n + 1);
   nc_list = arena.carve_n<int32_t>(n + 1);
   slab = arena.carve_n<int32_t>(n);
+  fok = arena.carve_n<uint8_t>(C1);
   occ = arena.carve_n<int32_t>(n + 1);
   hpos = arena.carve_n<int32_t>(n + 1);
   CellRec<D>* cr = arena.carve_n<CellRec<D>>(C1);
@@ -2272,6 +2501,65 @@ int32_t DbscanState::labels_global(const int64_t* rep_orig, const int64_t* reps,
   return RPT_OK;
 }
 
+int32_t DbscanState::frames_pass(int32_t min_frames, hipStream_t st) {
+  if (degenerate || min_frames < 1) return RPT_OK;  // <= 0: every core point qualifies
+  const bool refine = min_frames >= 2;
+  int32_t* list = nc_list;  // free until labels_fifo rebuilds it
+  int32_t* count = nc_list + n;
+  const int32_t* n_occ = hpos + n;
+  const bool cells = refine && integral_t && dim == 2 && g.nz == 1;
+  if (cells) {
+    const int R = (int)std::min<double>(std::floor((double)g.epst / g.ct), 64.0);
+    hipLaunchKernelGGL(k_frames_cells, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, st, g, R,
+                       occ, n_occ, rec<2>(), occ_bits, min_frames, fok);
+  }
+  RPT_HIP(hipMemsetAsync(count, 0, sizeof(int32_t), st));
+  hipLaunchKernelGGL(k_frames_queue, dim3(tile_grid(n)), dim3(kBlock), 0, st, skey, n, C,
+                     cells ? (const uint8_t*)fok : (const uint8_t*)nullptr, (int)min_frames,
+                     refine ? 1 : 0, core, list, count);
+  if (refine) {
+    if (dim == 2)
+      hipLaunchKernelGGL(k_frames_points<2>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
+                         rec<2>(), occ_bits, slab_t, integral_t ? 1 : 0, (int)min_frames, list,
+                         count, core);
+    else
+      hipLaunchKernelGGL(k_frames_points<3>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
+                         rec<3>(), occ_bits, slab_t, integral_t ? 1 : 0, (int)min_frames, list,
+                         count, core);
+  }
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
+}
+
+int32_t DbscanState::labels_fifo(int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st) {
+  const int gb = grid_for(n, kBlock, 2048);
+  int32_t* nc_count = nc_list + n;
+  int32_t* spos = slab;
+  RPT_HIP(hipMemsetAsync(cid, 0, sizeof(int32_t) * n, st));
+  RPT_HIP(hipMemsetAsync(nc_count, 0, sizeof(int32_t), st));
+  hipLaunchKernelGGL(k_ccmin, dim3(tile_grid(n)), dim3(kBlock), 0, st, parent, core, n, sorig,
+                     ccmin, cid, nc_list, nc_count);
+  hipLaunchKernelGGL(k_inverse_perm, dim3(gb), dim3(kBlock), 0, st, sorig, n, spos);
+  RPT_CHECK_LAUNCH();
+  RPT_TRY(exclusive_scan_total_i32(cid, cid, n, st));
+  hipLaunchKernelGGL(k_label_core, dim3(gb), dim3(kBlock), 0, st, ccmin, n, sorig, cid, labels);
+  if (dim == 2)
+    hipLaunchKernelGGL((k_label_fifo<2>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
+                       rec<2>(), occ_bits, slab_t, ccmin, rep, sorig, spos, cid, nc_list,
+                       nc_count, labels);
+  else
+    hipLaunchKernelGGL((k_label_fifo<3>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
+                       rec<3>(), occ_bits, slab_t, ccmin, rep, sorig, spos, cid, nc_list,
+                       nc_count, labels);
+  RPT_CHECK_LAUNCH();
+  tm.mark();
+  int32_t ncl = 0;
+  RPT_HIP(hipMemcpyAsync(&ncl, cid + n, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  RPT_TRY(wait_stream(st));
+  if (stats) RPT_TRY(fill_stats(ncl, stats));
+  return RPT_OK;
+}
+
 static int32_t check_args(const float* x, const float* y, const float* z, int64_t stride,
                           const float* t, int64_t n, int dim) {
   if (n <= 0) {
@@ -2320,6 +2608,59 @@ int32_t stdbscan(const float* x, const float* y, const float* z, int64_t stride,
   RPT_TRY(S->core_pass(st));
   RPT_TRY(S->union_pass(st));
   return S->labels_local(labels, stats, st);
+}
+
+// Denoise variant (PointCloudWorkF/stdbscan_denoising_pipeline.py:264-369), 2-D.
+int32_t stdbscan_denoise(const float* x, const float* y, const float* t, int64_t n,
+                         double eps_space, double eps_time, int32_t min_samples,
+                         int32_t min_frames, int32_t* labels, rpt_stdbscan_stats* stats,
+                         hipStream_t st) {
+  if (n == 0) {  // the reference returns an empty label array (:286-287), no error
+    if (stats) *stats = rpt_stdbscan_stats{};
+    return RPT_OK;
+  }
+  RPT_TRY(check_args(x, y, nullptr, 1, t, n, 2));
+  if (!labels) {
+    set_error("rpt_stdbscan_denoise: null labels");
+    return RPT_EINVAL;
+  }
+  if (min_frames >= 2 && !((float)eps_time <= 30.0f) && (float)eps_time == (float)eps_time) {
+    set_error("rpt_stdbscan_denoise: eps_time > 30 with min_frames >= 2 is not supported");
+    return RPT_ENOTSUP;
+  }
+  int dev = 0;
+  RPT_HIP(hipGetDevice(&dev));
+  DbscanState* S;
+  {
+    std::lock_guard<std::mutex> lk(g_state_mu);
+    S = nullptr;
+    for (auto& e : g_states)
+      if (e.first.first == dev && e.first.second == st) S = e.second;
+    if (!S) {
+      S = new DbscanState();
+      g_states.push_back({{dev, st}, S});
+    }
+  }
+  RPT_TRY(S->build(x, y, nullptr, 1, t, n, eps_space, eps_time, min_samples,
+                   stats && stats->timing, st));
+  if (S->degenerate) {
+    // no pair passes (not even (i, i)): core iff 0 >= min_samples and 0 >= min_frames, each its
+    // own cluster in index order
+    const bool single = min_samples <= 0 && min_frames <= 0;
+    hipLaunchKernelGGL(k_isolated_labels, dim3(grid_for(n, kBlock, 2048)), dim3(kBlock), 0, st,
+                       labels, n, single ? 1 : 0);
+    RPT_CHECK_LAUNCH();
+    if (stats) {
+      stats->n_points = n;
+      stats->n_core = single ? n : 0;
+      stats->n_clusters = single ? (int32_t)n : 0;
+    }
+    return wait_stream(st);
+  }
+  RPT_TRY(S->core_pass(st));
+  RPT_TRY(S->frames_pass(min_frames, st));
+  RPT_TRY(S->union_pass(st));
+  return S->labels_fifo(labels, stats, st);
 }
 
 // The fused path without its readbacks (the native stack driver): the cluster count stays on the

@@ -330,6 +330,83 @@ __global__ __launch_bounds__(kBlock) void k_summarize(
   }
 }
 
+// pandas groupby(...).mean() of float32 columns (pandas/_libs/groupby.pyx group_mean, pandas
+// 2.x): per group, in row order, a float32 Kahan-compensated sum (y = v - c; t = s + y;
+// c = (t - s) - y; c = 0 if NaN; s = t), then s / (float)count.  One wave per run: lanes stage
+// chunks in LDS, lane 0 runs the dependent chain.
+__device__ __forceinline__ float kahan_mean(const float* __restrict__ g, int b, int e, int lane,
+                                            float* __restrict__ sb) {
+  constexpr int kPre = 16, kChunk = 64 * kPre;
+  float s = 0.f, c = 0.f;
+  for (int c0 = b; c0 < e; c0 += kChunk) {
+#pragma unroll
+    for (int t = 0; t < kPre; ++t) {
+      const int idx = c0 + t * 64 + lane;
+      sb[t * 64 + lane] = (idx < e) ? g[idx] : 0.f;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int m = (e - c0 < kChunk) ? (e - c0) : kChunk;
+    if (lane == 0)
+      for (int i = 0; i < m; ++i) {
+        const float y = sb[i] - c;
+        const float t = s + y;
+        c = (t - s) - y;
+        if (c != c) c = 0.f;
+        s = t;
+      }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  return s / (float)(e - b);
+}
+
+// head[p] = 1 where a label run starts among clustered points (noise, key 0, excluded)
+__global__ void k_label_heads(const uint32_t* __restrict__ sk, int64_t n,
+                              int32_t* __restrict__ head) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t k = sk[p];
+    head[p] = (k != 0u && (p == 0 || k != sk[p - 1])) ? 1 : 0;
+  }
+}
+
+// Three waves per label run: x, y, intensity group means; outputs indexed by label.
+__global__ __launch_bounds__(kBlock) void k_label_means(
+    const uint32_t* __restrict__ sk, const int64_t* __restrict__ seg_start,
+    const int32_t* __restrict__ n_seg_dev, int64_t n, const float* __restrict__ gx,
+    const float* __restrict__ gy, const float* __restrict__ gi, int64_t n_labels,
+    int64_t* __restrict__ o_count, float* __restrict__ o_x, float* __restrict__ o_y,
+    float* __restrict__ o_v) {
+  __shared__ float s_buf[kBlock / 64][1024];
+  const int64_t n_seg = *n_seg_dev;
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+  for (int64_t w = w0; w < 3 * n_seg; w += nw) {
+    const int su = __builtin_amdgcn_readfirstlane((int)(w / 3));
+    const int comp = __builtin_amdgcn_readfirstlane((int)(w - (int64_t)su * 3));
+    const int b = __builtin_amdgcn_readfirstlane((int)seg_start[su]);
+    const int e = __builtin_amdgcn_readfirstlane(
+        (int)((su + 1 < n_seg) ? seg_start[su + 1] : n));
+    const int64_t lab = (int64_t)sk[b] - 1;
+    const float m = kahan_mean(comp == 0 ? gx : (comp == 1 ? gy : gi), b, e, lane,
+                               s_buf[threadIdx.x / 64]);
+    if (lane == 0 && lab < n_labels) {
+      if (comp == 0) {
+        o_x[lab] = m;
+        o_count[lab] = e - b;
+      } else if (comp == 1) {
+        o_y[lab] = m;
+      } else {
+        o_v[lab] = m;
+      }
+    }
+  }
+}
+
 __global__ void k_fill_i64(int64_t* p, int64_t n, int64_t v) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -440,6 +517,65 @@ int32_t cluster_summaries_dev(const int32_t* labels, const float* x, const float
   }
   return summaries_impl(labels, x, y, inten, pf, n, n_frames, bits, s_hint, o_frame, o_label,
                         o_count, o_first, o_cx, o_cy, o_mi, frame_first_noise, n_seg_dev, st);
+}
+
+// Per-label pandas group means (count, x, y, intensity) of labels in [0, n_labels); labels
+// without points keep count 0.  Synchronises once.
+int32_t label_means(const int32_t* labels, const float* x, const float* y, const float* inten,
+                    int64_t n, int64_t n_labels, int64_t* o_count, float* o_x, float* o_y,
+                    float* o_v, hipStream_t st) {
+  if (n < 0 || n_labels < 0 || (n > 0 && (!labels || !x || !y || !inten)) ||
+      (n_labels > 0 && (!o_count || !o_x || !o_y || !o_v))) {
+    set_error("rpt_label_means: bad arguments");
+    return RPT_EINVAL;
+  }
+  if (n >= (int64_t(1) << 31) - 1 || n_labels >= (int64_t(1) << 31) - 1) {
+    set_error("rpt_label_means: n exceeds the int32 index space");
+    return RPT_ENOTSUP;
+  }
+  if (n_labels > 0) {
+    RPT_HIP(hipMemsetAsync(o_count, 0, sizeof(int64_t) * (size_t)n_labels, st));
+    RPT_HIP(hipMemsetAsync(o_x, 0, sizeof(float) * (size_t)n_labels, st));
+    RPT_HIP(hipMemsetAsync(o_y, 0, sizeof(float) * (size_t)n_labels, st));
+    RPT_HIP(hipMemsetAsync(o_v, 0, sizeof(float) * (size_t)n_labels, st));
+  }
+  if (n == 0) return wait_stream(st);
+  Scratch& sc = scratch(st);
+  Budget b;
+  for (int k = 0; k < 4; ++k) b.add<uint32_t>(n + 1);
+  b.add<int64_t>(radix_tmp_elems(n));
+  b.add<int32_t>(n + 1);
+  b.add<int32_t>(n + 1);
+  b.add<int64_t>(n + 1);
+  for (int k = 0; k < 3; ++k) b.add<float>(n + 1);
+  RPT_TRY(sc.reserve(b.bytes, st));
+  uint32_t* keys = sc.carve_n<uint32_t>(n + 1);
+  uint32_t* vals = sc.carve_n<uint32_t>(n + 1);
+  uint32_t* ka = sc.carve_n<uint32_t>(n + 1);
+  uint32_t* va = sc.carve_n<uint32_t>(n + 1);
+  int64_t* rtmp = sc.carve_n<int64_t>(radix_tmp_elems(n));
+  int32_t* head = sc.carve_n<int32_t>(n + 1);
+  int32_t* pos = sc.carve_n<int32_t>(n + 1);
+  int64_t* seg_start = sc.carve_n<int64_t>(n + 1);
+  float* gx = sc.carve_n<float>(n + 1);
+  float* gy = sc.carve_n<float>(n + 1);
+  float* gi = sc.carve_n<float>(n + 1);
+  const int g = grid_for(n, kBlock, 8192);
+  hipLaunchKernelGGL(k_sum_keys, dim3(g), dim3(kBlock), 0, st, labels, n, keys, vals);
+  RPT_CHECK_LAUNCH();
+  int bits = 1;
+  while ((int64_t(1) << bits) <= n_labels + 1) ++bits;
+  uint32_t *sk, *sv;
+  RPT_TRY(radix_sort_pairs(keys, vals, ka, va, n, bits, rtmp, &sk, &sv, st));
+  hipLaunchKernelGGL(k_label_heads, dim3(g), dim3(kBlock), 0, st, sk, n, head);
+  RPT_TRY(exclusive_scan_total_i32(head, pos, n, st));
+  hipLaunchKernelGGL(k_seg_starts, dim3(g), dim3(kBlock), 0, st, head, pos, n, seg_start);
+  hipLaunchKernelGGL(k_gather_runs, dim3(g), dim3(kBlock), 0, st, sv, n, x, y, inten, gx, gy, gi);
+  hipLaunchKernelGGL(k_label_means, dim3(grid_for(3 * (n_labels + 1), kBlock / 64, 16384)),
+                     dim3(kBlock), 0, st, sk, seg_start, pos + n, n, gx, gy, gi, n_labels,
+                     o_count, o_x, o_y, o_v);
+  RPT_CHECK_LAUNCH();
+  return wait_stream(st);
 }
 
 }  // namespace rpt

@@ -170,6 +170,11 @@ _SIGS = [
     ("rpt_stdbscan", C.c_int32,
      [vp, vp, vp, C.c_int64, vp, C.c_int64, C.c_double, C.c_double, C.c_int32, vp,
       C.POINTER(StdbscanStats), vp]),
+    ("rpt_label_means", C.c_int32,
+     [vp, vp, vp, vp, C.c_int64, C.c_int64, vp, vp, vp, vp, vp]),
+    ("rpt_stdbscan_denoise", C.c_int32,
+     [vp, vp, vp, C.c_int64, C.c_double, C.c_double, C.c_int32, C.c_int32, vp,
+      C.POINTER(StdbscanStats), vp]),
     ("rpt_infer_time_from_colors", C.c_int32, [vp, C.c_int64, vp, C.c_int32, vp, vp]),
     ("rpt_dbscan_create", vp, []),
     ("rpt_dbscan_destroy", None, [vp]),

@@ -22,6 +22,11 @@ are reproducible.  Outputs (all in tests/golden/):
                     process_ply_clustering (processors/clustering.py:157-208) on synthetic PLY
                     stacks (labels CSV text + stdout)
   g8_fuse_max.npz   5_gain_fusion_ply_builder.fuse_gains_max (:222-273) on small CSV frames
+  g9_denoise.npz    PointCloudWorkF/stdbscan_denoising_pipeline.st_dbscan (:264-369: min_frames
+                    core condition, FIFO expansion) on blob / lattice / float-time clouds
+  g10_denoise_pipeline.npz
+                    stdbscan_denoising_pipeline.run_pipeline (:862-1046, no_viz) on a synthetic
+                    CSV stack: stdout, both binary PLYs, denoising_stats.csv, clusters.csv
   meta.json         library versions / CPU of the generating run
 
     python tests/golden/make_golden.py [g7 g8 ...]   # only the named fixtures
@@ -468,6 +473,91 @@ def g8_fuse_max(tmp: Path):
     np.savez_compressed(OUT / "g8_fuse_max.npz", **rec)
 
 
+def _denoise_cases():
+    """(name, coords f32 [n,2], times f32 [n], eps_space, eps_time, min_samples, min_frames)."""
+    rng = np.random.default_rng(909)
+    cases = []
+
+    def blobs(n_frames, n_blobs, per, spread, drift, noise, skip=()):
+        xs, ts = [], []
+        centers = rng.random((n_blobs, 2)) * 120.0
+        for f in range(n_frames):
+            if f in skip:
+                continue
+            for b in range(n_blobs):
+                if rng.random() < 0.25:  # a blob missing from a frame: single-frame neighbours
+                    continue
+                c = centers[b] + drift * f
+                k = rng.integers(per // 2, per + 1)
+                xs.append(c + rng.normal(0, spread, (k, 2)))
+                ts.append(np.full(k, f, np.float32))
+            k = rng.integers(0, noise + 1)
+            xs.append(rng.random((k, 2)) * 140.0)
+            ts.append(np.full(k, f, np.float32))
+        xy = np.vstack(xs).astype(np.float32)
+        t = np.concatenate(ts).astype(np.float32)
+        perm = rng.permutation(len(t)) if rng.random() < 0.5 else np.arange(len(t))
+        return xy[perm], t[perm]
+
+    for i, (eps, et, ms, mf) in enumerate([(8.0, 2.0, 15, 2), (6.0, 1.0, 8, 2), (5.0, 2.0, 6, 3),
+                                          (8.0, 0.0, 10, 1), (7.0, 2.5, 12, 2), (4.0, 1.0, 4, 2),
+                                          (9.0, 3.0, 20, 4), (6.0, 2.0, 5, 1)]):
+        xy, t = blobs(6 + i, 7, 30, 2.5 + 0.3 * i, rng.normal(0, 0.8, 2), 25,
+                      skip=(2,) if i % 3 == 0 else ())
+        cases.append((f"blobs{i}", xy, t, eps, et, ms, mf))
+    # dense single-frame blobs next to multi-frame ones (the min_frames condition decides)
+    xy1, t1 = blobs(1, 5, 60, 1.5, np.zeros(2), 10)
+    xy2, t2 = blobs(4, 4, 20, 2.0, np.zeros(2), 10)
+    xy2 = xy2 + 200.0
+    cases.append(("single_vs_multi", np.vstack([xy1, xy2]), np.concatenate([t1, t2 + 10]),
+                  6.0, 2.0, 8, 2))
+    # lattice: many equal distances, border points shared by several clusters
+    g = np.stack(np.meshgrid(np.arange(14), np.arange(14)), -1).reshape(-1, 2).astype(np.float32)
+    xy = np.vstack([g * 2.0 + f * 0.5 for f in range(3)]).astype(np.float32)
+    t = np.repeat(np.arange(3, dtype=np.float32), len(g))
+    cases.append(("lattice", xy, t, 2.0, 1.0, 5, 2))
+    # float times (not frame ids): int32 truncation decides the frames
+    xy, t = blobs(5, 6, 25, 2.0, np.zeros(2), 15)
+    t = (t * 0.7 + rng.random(len(t)).astype(np.float32) * 0.6).astype(np.float32)
+    cases.append(("float_time", xy, t, 6.0, 1.2, 8, 2))
+    # a NaN time (never a neighbour) and an empty cloud
+    xy, t = blobs(3, 3, 20, 2.0, np.zeros(2), 5)
+    t = t.copy()
+    t[::37] = np.nan
+    cases.append(("nan_time", xy, t, 6.0, 2.0, 6, 2))
+    cases.append(("empty", np.zeros((0, 2), np.float32), np.zeros(0, np.float32), 8.0, 2.0, 15, 2))
+    return cases
+
+
+def g9_denoise(den):
+    rec = {}
+    names = []
+    for name, xy, t, eps, et, ms, mf in _denoise_cases():
+        lab = den.st_dbscan(xy.astype(np.float32), t.astype(np.float32), eps, et, ms, mf)
+        rec[f"{name}_xy"], rec[f"{name}_t"] = xy.astype(np.float32), t.astype(np.float32)
+        rec[f"{name}_labels"] = np.asarray(lab, np.int32)
+        rec[f"{name}_params"] = np.array([eps, et, ms, mf], np.float64)
+        names.append(name)
+    rec["names"] = np.array(names)
+    np.savez_compressed(OUT / "g9_denoise.npz", **rec)
+    return len(names)
+
+
+def g10_denoise_pipeline(den, tmp: Path):
+    data = synth_csv_stack(tmp / "stack")
+    out = tmp / "out"
+    buf = io.StringIO()
+    with redirect_stdout(buf):
+        den.run_pipeline(data, out, eps_space=8.0, eps_time=2.0, min_samples=15, min_frames=2,
+                         max_frames=0, no_viz=True, parallel=False)
+    rec = {"stdout": np.array(buf.getvalue())}
+    for name in ("denoised_point_cloud.ply", "raw_point_cloud.ply"):
+        rec[name.replace(".", "_")] = np.frombuffer((out / name).read_bytes(), np.uint8)
+    for name in ("denoising_stats.csv", "clusters.csv"):
+        rec[name.replace(".", "_")] = np.array((out / name).read_text())
+    np.savez_compressed(OUT / "g10_denoise_pipeline.npz", **rec)
+
+
 def main():
     if not REF.exists():
         raise SystemExit("make_golden.py must run where /root/reference exists (build container)")
@@ -497,6 +587,12 @@ def main():
             g7_ply(ref3, tmp / "g7")
         if want("g8"):
             g8_fuse_max(tmp / "g8")
+        if want("g9") or want("g10"):
+            den = _load("ref_denoise", REF / "PointCloudWorkF" / "stdbscan_denoising_pipeline.py")
+            if want("g9"):
+                g9_denoise(den)
+            if want("g10"):
+                g10_denoise_pipeline(den, tmp / "g10")
     import scipy
     import sklearn
     mp = OUT / "meta.json"

@@ -1,0 +1,120 @@
+"""Denoise mode (PointCloudWorkF/stdbscan_denoising_pipeline.py) on the
+GPU: rpt_stdbscan_denoise against the reference's own labels (g9) and against the C oracle on
+synthetic radar stacks; rpt_label_means against pandas' group mean; the pipeline drop-in against
+the reference's run_pipeline outputs (g10: stdout, both binary PLYs, both CSVs), byte-identical."""
+from __future__ import annotations
+
+import contextlib
+import io
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+
+
+def test_denoise_labels_match_reference(gpu, golden):
+    from rpt.denoise import st_dbscan
+
+    g = golden("g9_denoise.npz")
+    for name in g["names"]:
+        eps, et, ms, mf = g[f"{name}_params"]
+        lab = st_dbscan(g[f"{name}_xy"], g[f"{name}_t"], eps, et, int(ms), int(mf), device=gpu)
+        np.testing.assert_array_equal(lab, g[f"{name}_labels"], err_msg=str(name))
+
+
+@pytest.mark.parametrize("min_frames,eps_time", [(2, 2.0), (3, 2.0), (1, 1.0), (2, 1.0)])
+def test_denoise_matches_oracle_on_radar_stack(gpu, min_frames, eps_time):
+    """Points of a synthetic radar stack (K1, no land filter) clustered by the device denoise
+    path and by the oracle's FIFO restatement; frames as times, one missing frame id."""
+    from rpt.denoise import st_dbscan
+    from rpt.pipeline import FrameStackPipeline, PathParams
+    from rpt.synth import DeviceSynth, SynthConfig
+
+    cfg = SynthConfig(n_frames=6, rows=1024, n_targets=20, clutter_density=0.01)
+    ds = DeviceSynth(cfg, gpu)
+    pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(land_filter=False), gpu)
+    pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
+                      cfg.n_frames * len(cfg.gains))
+    res = pipe.run(ds.echo(), keep_points=True)
+    xy = torch.stack([res.points["x"], res.points["y"]], 1)
+    t = res.points["frame"].to(torch.float32)
+    t = torch.where(t >= 3, t + 1, t)  # a gap in the frame ids
+    lab = st_dbscan(xy, t, 8.0, eps_time, 15, min_frames).cpu().numpy()
+    ref = oracle.stdbscan_denoise(xy.cpu().numpy(), t.cpu().numpy(), 8.0, eps_time, 15,
+                                  min_frames)
+    assert (ref >= 0).sum() > 1000
+    np.testing.assert_array_equal(lab, ref)
+
+
+def test_denoise_float_times_and_edges(gpu):
+    from rpt.denoise import st_dbscan
+
+    rng = np.random.default_rng(3)
+    xy = (rng.random((3000, 2)) * 60).astype(np.float32)
+    t = (rng.integers(0, 6, 3000) + rng.random(3000) * 0.8).astype(np.float32)
+    for et, ms, mf in ((1.5, 6, 2), (0.5, 4, 2), (2.0, 10, 3), (2.0, 0, 0)):
+        np.testing.assert_array_equal(st_dbscan(xy, t, 5.0, et, ms, mf, device=gpu),
+                                      oracle.stdbscan_denoise(xy, t, 5.0, et, ms, mf))
+    # empty input: no labels, no error (:286-287)
+    assert st_dbscan(np.zeros((0, 2), np.float32), np.zeros(0, np.float32), 8.0, 2.0, 15,
+                     2, device=gpu).shape == (0,)
+    # no pair passes: all noise, or singletons when nothing is required
+    assert (st_dbscan(xy, t, -1.0, 2.0, 3, 2, device=gpu) == -1).all()
+    np.testing.assert_array_equal(st_dbscan(xy, t, -1.0, 2.0, 0, 0, device=gpu),
+                                  np.arange(3000, dtype=np.int32))
+    with pytest.raises(NotImplementedError):
+        st_dbscan(xy, t, 5.0, 40.0, 5, 2, device=gpu)
+
+
+def test_label_means_match_pandas_group_mean(gpu):
+    """rpt_label_means = pandas groupby mean of float32 columns (Kahan-compensated float32)."""
+    import pandas as pd
+
+    from rpt.denoise import cluster_table
+
+    rng = np.random.default_rng(8)
+    n = 200_000
+    lab = rng.integers(-1, 300, n).astype(np.int32)
+    lab[rng.random(n) < 0.2] = 7  # one large group
+    x = (rng.normal(0, 1, n) * 150 + 30).astype(np.float32)
+    y = (rng.random(n) * 1e4).astype(np.float32)
+    v = (rng.random(n) * 255).astype(np.float32)
+    keep = lab >= 0
+    ref = pd.DataFrame({"cluster_id": lab[keep], "x": x[keep], "y": y[keep],
+                        "intensity": v[keep]}).groupby("cluster_id").agg(
+        num_points=("x", "count"), centroid_x=("x", "mean"), centroid_y=("y", "mean"),
+        mean_intensity=("intensity", "mean")).reset_index()
+    T = lambda a: torch.from_numpy(a).to(gpu)  # noqa: E731
+    got = cluster_table(T(lab), T(x), T(y), T(v), int(lab.max()) + 1)
+    assert ref.to_csv(index=False) == got.to_csv(index=False)
+
+
+def test_denoise_pipeline_matches_reference_outputs(tmp_path, golden):
+    sys.path.insert(0, str(GOLDEN))
+    from make_golden import synth_csv_stack
+
+    from rpt.denoise import run_pipeline
+
+    g = golden("g10_denoise_pipeline.npz")
+    data = synth_csv_stack(tmp_path / "stack")
+    out = tmp_path / "out"
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        run_pipeline(data, out, eps_space=8.0, eps_time=2.0, min_samples=15, min_frames=2,
+                     max_frames=0, no_viz=True, parallel=False)
+    ref_out = str(g["stdout"])
+    ref_dir = [l for l in ref_out.splitlines() if l.startswith("Results saved to: ")][0]
+    ref_dir = ref_dir[len("Results saved to: "):]
+    assert buf.getvalue().replace(str(out), "<OUT>") == ref_out.replace(ref_dir, "<OUT>")
+    for name in ("denoised_point_cloud.ply", "raw_point_cloud.ply"):
+        assert (out / name).read_bytes() == bytes(g[name.replace(".", "_")]), name
+    for name in ("denoising_stats.csv", "clusters.csv"):
+        assert (out / name).read_text() == str(g[name.replace(".", "_")]), name

@@ -159,3 +159,68 @@ def test_tracker_oracle_matches_reference(golden):
         np.testing.assert_array_equal([isinstance(o.average_velocity, np.float32) for o in objs],
                                       g[f"s{s}_obj_avgv_f32"])
         np.testing.assert_array_equal([o.color for o in objs], g[f"s{s}_obj_color"])
+
+
+def test_denoise_oracle_matches_reference(golden):
+    """oracle.stdbscan_denoise against PointCloudWorkF st_dbscan run in the build container
+    (g9: blobs with missing frames, single- vs multi-frame blobs, lattice, float times, a NaN
+    time, an empty cloud; min_frames 1-4)."""
+    g = golden("g9_denoise.npz")
+    for name in g["names"]:
+        eps, et, ms, mf = g[f"{name}_params"]
+        lab = oracle.stdbscan_denoise(g[f"{name}_xy"], g[f"{name}_t"], eps, et, int(ms), int(mf))
+        np.testing.assert_array_equal(lab, g[f"{name}_labels"], err_msg=str(name))
+
+
+def _denoise_sets(xy, t, eps, et, ms, mf):
+    """The set formulation the device path computes (csrc/stdbscan.hip k_frames_* and
+    k_label_fifo), brute force: core = count >= ms and >= mf distinct int32(t) frames among the
+    neighbours; components of core points numbered by minimum index; a non-core point p takes
+    the smallest component m adjacent through a core point with p > m or p adjacent to m."""
+    n = len(t)
+    x64 = xy.astype(np.float64)
+    d2 = (x64[:, None, 0] - x64[None, :, 0]) ** 2 + (x64[:, None, 1] - x64[None, :, 1]) ** 2
+    with np.errstate(invalid="ignore"):
+        adj = (d2 <= eps * eps) & (np.abs(t[:, None] - t[None, :]) <= np.float32(et))
+    with np.errstate(invalid="ignore"):
+        fr = t.astype(np.int32)
+    core = np.array([adj[i].sum() >= ms and len(np.unique(fr[adj[i]])) >= mf for i in range(n)],
+                    bool) if n else np.zeros(0, bool)
+    comp = np.full(n, -1)
+    for i in range(n):
+        if core[i] and comp[i] < 0:
+            stack, comp[i] = [i], i
+            while stack:
+                a = stack.pop()
+                for b in np.nonzero(adj[a] & core)[0]:
+                    if comp[b] < 0:
+                        comp[b] = i
+                        stack.append(b)
+    mins = sorted(set(comp[core].tolist()))
+    cid = {m: k for k, m in enumerate(mins)}
+    lab = np.full(n, -1, np.int32)
+    for i in range(n):
+        if core[i]:
+            lab[i] = cid[comp[i]]
+        else:
+            ms_ = [m for m in set(comp[adj[i] & core].tolist()) if i > m or adj[i, m]]
+            if ms_:
+                lab[i] = cid[min(ms_)]
+    return lab
+
+
+def test_denoise_set_formulation_matches_fifo_oracle():
+    """The order-free formulation of the FIFO expansion (what the GPU computes) equals the
+    sequential restatement on random clouds with many shared border points."""
+    rng = np.random.default_rng(41)
+    for k in range(30):
+        n = int(rng.integers(50, 500))
+        xy = (rng.random((n, 2)) * rng.uniform(20, 80)).astype(np.float32)
+        t = rng.integers(0, 5, n).astype(np.float32)
+        if k % 5 == 4:
+            t = (t + rng.random(n) * 0.9).astype(np.float32)
+        eps, et = float(rng.uniform(2, 8)), float(rng.choice([0.0, 1.0, 1.5, 2.0]))
+        ms, mf = int(rng.integers(1, 12)), int(rng.integers(0, 4))
+        a = oracle.stdbscan_denoise(xy, t, eps, et, ms, mf)
+        b = _denoise_sets(xy, t, eps, et, ms, mf)
+        np.testing.assert_array_equal(a, b, err_msg=f"case {k}")
