@@ -24,7 +24,7 @@
 //   k_cell_box    per occupied cell: bounding box in space and time, "mutual" flag
 //                 (box diagonal within eps and time span within eps_t: every pair adjacent)
 //   k_core        neighbour count with early exit at min_samples; whole-cell accept/reject
-//   k_rep         first core point of each cell
+//   k_rep         the minimum-original-index core point of each cell
 //   k_union       core-core union-find (min-index hooking); one edge per mutual cell suffices
 //   k_compress    root of every point
 //   k_cmin        minimum original index per component
@@ -68,7 +68,7 @@ struct Bounds {
   int32_t nonfinite_xyz;  // any NaN/inf coordinate
   int32_t nonintegral_t;  // any finite t with t != floor(t) or |t| >= 2^24
   int32_t n_finite_t;
-  int32_t pad;
+  int32_t t_descends;     // some t[i] < t[i-1]: the points are not in time order
 };
 
 template <int D>
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(kBlock) void k_bounds(const float* __restrict__ x,
   if (n_dev) n = *n_dev;  // count on the device (at most the host n the grid was sized for)
   uint32_t mn[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
   uint32_t mx[4] = {0u, 0u, 0u, 0u};
-  int nonfin = 0, nonint = 0, nfin = 0;
+  int nonfin = 0, nonint = 0, nfin = 0, desc = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     float v[4];
@@ -103,6 +103,7 @@ __global__ __launch_bounds__(kBlock) void k_bounds(const float* __restrict__ x,
       mx[3] = max(mx[3], o);
       if (v[3] != floorf(v[3]) || fabsf(v[3]) >= 16777216.f) nonint = 1;
     }
+    if (i > 0 && !(t[i - 1] <= v[3])) desc = 1;  // NaN counts as out of order
   }
   // wave reduce, then one partial per block
 #pragma unroll
@@ -115,9 +116,10 @@ __global__ __launch_bounds__(kBlock) void k_bounds(const float* __restrict__ x,
     nonfin |= __shfl_xor(nonfin, off);
     nonint |= __shfl_xor(nonint, off);
     nfin += __shfl_xor(nfin, off);
+    desc |= __shfl_xor(desc, off);
   }
   __shared__ uint32_t smn[kBlock / 64][4], smx[kBlock / 64][4];
-  __shared__ int sfl[kBlock / 64][3];
+  __shared__ int sfl[kBlock / 64][4];
   const int w = threadIdx.x / 64;
   if ((threadIdx.x & 63) == 0) {
     for (int k = 0; k < 4; ++k) {
@@ -127,6 +129,7 @@ __global__ __launch_bounds__(kBlock) void k_bounds(const float* __restrict__ x,
     sfl[w][0] = nonfin;
     sfl[w][1] = nonint;
     sfl[w][2] = nfin;
+    sfl[w][3] = desc;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -138,6 +141,7 @@ __global__ __launch_bounds__(kBlock) void k_bounds(const float* __restrict__ x,
       nonfin |= sfl[v][0];
       nonint |= sfl[v][1];
       nfin += sfl[v][2];
+      desc |= sfl[v][3];
     }
     // per-block partial, reduced by k_bounds_final (no same-address atomics)
     Bounds& o = out[blockIdx.x];
@@ -148,7 +152,7 @@ __global__ __launch_bounds__(kBlock) void k_bounds(const float* __restrict__ x,
     o.nonfinite_xyz = nonfin;
     o.nonintegral_t = nonint;
     o.n_finite_t = nfin;
-    o.pad = 0;
+    o.t_descends = desc;
   }
 }
 
@@ -156,7 +160,7 @@ __global__ __launch_bounds__(kBlock) void k_bounds_final(const Bounds* __restric
                                                         Bounds* __restrict__ out) {
   uint32_t mn[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
   uint32_t mx[4] = {0u, 0u, 0u, 0u};
-  int nonfin = 0, nonint = 0, nfin = 0;
+  int nonfin = 0, nonint = 0, nfin = 0, desc = 0;
   for (int b = threadIdx.x; b < nb; b += blockDim.x) {
     const Bounds& p = part[b];
     for (int k = 0; k < 4; ++k) {
@@ -166,6 +170,7 @@ __global__ __launch_bounds__(kBlock) void k_bounds_final(const Bounds* __restric
     nonfin |= p.nonfinite_xyz;
     nonint |= p.nonintegral_t;
     nfin += p.n_finite_t;
+    desc |= p.t_descends;
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -177,6 +182,7 @@ __global__ __launch_bounds__(kBlock) void k_bounds_final(const Bounds* __restric
     nonfin |= __shfl_xor(nonfin, off);
     nonint |= __shfl_xor(nonint, off);
     nfin += __shfl_xor(nfin, off);
+    desc |= __shfl_xor(desc, off);
   }
   __shared__ Bounds sb[kBlock / 64];
   const int w = threadIdx.x / 64;
@@ -188,6 +194,7 @@ __global__ __launch_bounds__(kBlock) void k_bounds_final(const Bounds* __restric
     sb[w].nonfinite_xyz = nonfin;
     sb[w].nonintegral_t = nonint;
     sb[w].n_finite_t = nfin;
+    sb[w].t_descends = desc;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -199,6 +206,7 @@ __global__ __launch_bounds__(kBlock) void k_bounds_final(const Bounds* __restric
       nonfin |= sb[v].nonfinite_xyz;
       nonint |= sb[v].nonintegral_t;
       nfin += sb[v].n_finite_t;
+      desc |= sb[v].t_descends;
     }
     for (int k = 0; k < 4; ++k) {
       out->mn[k] = mn[k];
@@ -207,7 +215,7 @@ __global__ __launch_bounds__(kBlock) void k_bounds_final(const Bounds* __restric
     out->nonfinite_xyz = nonfin;
     out->nonintegral_t = nonint;
     out->n_finite_t = nfin;
-    out->pad = 0;
+    out->t_descends = desc;
   }
 }
 
@@ -316,6 +324,97 @@ __global__ __launch_bounds__(kBlock) void k_occ_list(const int32_t* __restrict__
       occ[pos[s]] = c;
       atomicOr(occ_bits + (c >> 5), 1u << (c & 31));
     }
+}
+
+// ---- K4 for time-ordered 2-D input (the stack path: points come frame-major from K1 / the land
+// filter, and a slab is a frame): the cell sort is a counting sort of each slab's points by their
+// (y, x) cell, one 1024-thread block per slab with the slab's cell histogram in LDS.  It replaces
+// keys + three radix passes + the gather + the cell-count pass: two reads of x / y (/ t) and one
+// scattered write of the sorted records per point, and the dense cell_start rows come out of the
+// histogram scan directly.  Order inside a cell is arrival order: nothing downstream depends on
+// it (roots are minimum ORIGINAL indices, counts and minima are order-free).
+constexpr int kBucketBlock = 1024;
+constexpr int kBucketCells = 16384;  // per-slab cells held in LDS (64 KiB)
+
+// slab_lo[s] = first point of slab s (points ordered by slab), slab_lo[nt] = n
+__global__ void k_slab_lo(const float* __restrict__ t, int64_t n, Geom g,
+                          int32_t* __restrict__ slab_lo) {
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s <= g.nt; s += gridDim.x * blockDim.x) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const int64_t m = (lo + hi) >> 1;
+      if (slab_of(t[m], g) < s) lo = m + 1; else hi = m;
+    }
+    slab_lo[s] = (int32_t)(s == g.nt ? n : lo);
+  }
+}
+
+__global__ __launch_bounds__(kBucketBlock) void k_slab_bucket(
+    const float* __restrict__ x, const float* __restrict__ y, int64_t stride,
+    const float* __restrict__ t, Geom g, const int32_t* __restrict__ slab_lo,
+    float4* __restrict__ pts, int32_t* __restrict__ sorig, int32_t* __restrict__ skey,
+    int32_t* __restrict__ cell_start) {
+  __shared__ int32_t hist[kBucketCells];
+  __shared__ int32_t wsum[kBucketBlock / 64];
+  const int s = blockIdx.x;
+  const int P = g.nx * g.ny;
+  const int lo = slab_lo[s], hi = slab_lo[s + 1];
+  for (int c = threadIdx.x; c < P; c += kBucketBlock) hist[c] = 0;
+  __syncthreads();
+  auto cell = [&](int64_t i) {
+    return cell_of((double)y[i * stride], g.oy, g.cs, g.ny) * g.nx +
+           cell_of((double)x[i * stride], g.ox, g.cs, g.nx);
+  };
+  for (int i = lo + threadIdx.x; i < hi; i += kBucketBlock) atomicAdd(&hist[cell(i)], 1);
+  __syncthreads();
+  // exclusive scan of hist[0, P): each thread a contiguous run, then the block's run sums
+  const int per = (P + kBucketBlock - 1) / kBucketBlock;
+  const int c0 = threadIdx.x * per, c1 = min(c0 + per, P);
+  int run = 0;
+  for (int c = c0; c < c1; ++c) run += hist[c];
+  const int lane = threadIdx.x & 63, w = threadIdx.x / 64;
+  int incl = run;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += o;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int before = 0;
+  for (int v = 0; v < w; ++v) before += wsum[v];
+  int acc = before + incl - run;
+  for (int c = c0; c < c1; ++c) {
+    const int h = hist[c];
+    hist[c] = acc;
+    cell_start[(int64_t)s * P + c] = lo + acc;
+    acc += h;
+  }
+  __syncthreads();
+  for (int i = lo + threadIdx.x; i < hi; i += kBucketBlock) {
+    const int c = cell(i);
+    const int dst = lo + atomicAdd(&hist[c], 1);
+    float4 p;
+    p.x = x[(int64_t)i * stride];
+    p.y = y[(int64_t)i * stride];
+    p.w = t[i];
+    p.z = p.w;
+    pts[dst] = p;
+    sorig[dst] = i;
+    skey[dst] = s * P + c;
+  }
+  if (s == g.nt - 1 && threadIdx.x == 0) {  // the isolated cell (empty here) and the end
+    cell_start[g.cells] = hi;
+    cell_start[g.cells + 1] = hi;
+  }
+}
+
+// run-head flags of the sorted keys (the occupied-cell list is their scan)
+__global__ __launch_bounds__(kBlock) void k_key_heads(const int32_t* __restrict__ skey, int64_t n,
+                                                     int32_t* __restrict__ head) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x)
+    head[s] = (s == 0 || skey[s - 1] != skey[s]) ? 1 : 0;
 }
 
 __device__ __forceinline__ bool occupied(const uint32_t* __restrict__ bits, int64_t c) {
@@ -1285,20 +1384,44 @@ __global__ __launch_bounds__(kBlock) void k_core_slow_cells(const float4* __rest
   }
 }
 
-// first core point (sorted index) of each cell, -1 when none
-__global__ __launch_bounds__(kBlock) void k_rep(const int32_t* __restrict__ cell_start,
-                                               int64_t cells, const uint8_t* __restrict__ core,
+// The core point (sorted index) of each cell with the smallest ORIGINAL index, -1 when none:
+// the star init hangs a mutual cell's core points under it, which keeps every union-find root
+// its component's minimum original index whatever the order inside the cell (the slab-bucket
+// K4 does not keep input order inside a cell).  Two coalesced passes over the sorted points:
+// a segmented wave minimum per cell run (runs are contiguous), one atomicMin per (wave, cell)
+// run, then the point holding the minimum writes itself.
+__global__ __launch_bounds__(kBlock) void k_cell_min_orig(const int32_t* __restrict__ skey,
+                                                         const uint8_t* __restrict__ core,
+                                                         const int32_t* __restrict__ sorig,
+                                                         int64_t n, int64_t cells,
+                                                         int32_t* __restrict__ cell_min) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t s0 = (int64_t)blockIdx.x * blockDim.x; s0 < n;
+       s0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = s0 + threadIdx.x;
+    const int key = (s < n) ? skey[s] : -1;
+    int v = (s < n && core[s] && (int64_t)key < cells) ? sorig[s] : INT_MAX;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {  // sorted keys: equal at distance off = same run
+      const int ov = __shfl_up(v, off, 64);
+      const int ok = __shfl_up(key, off, 64);
+      if (lane >= off && ok == key) v = min(v, ov);
+    }
+    const int next = __shfl_down(key, 1, 64);
+    if ((lane == 63 || next != key) && key >= 0 && v != INT_MAX) atomicMin(cell_min + key, v);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_rep(const int32_t* __restrict__ skey,
+                                               const uint8_t* __restrict__ core,
+                                               const int32_t* __restrict__ sorig, int64_t n,
+                                               int64_t cells,
+                                               const int32_t* __restrict__ cell_min,
                                                int32_t* __restrict__ rep) {
-  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < cells;
-       c += (int64_t)gridDim.x * blockDim.x) {
-    const int b = cell_start[c], e = cell_start[c + 1];
-    int r = -1;
-    for (int j = b; j < e; ++j)
-      if (core[j]) {
-        r = j;
-        break;
-      }
-    rep[c] = r;
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    const int key = skey[s];
+    if (core[s] && (int64_t)key < cells && sorig[s] == cell_min[key]) rep[key] = (int32_t)s;
   }
 }
 
@@ -1356,8 +1479,8 @@ __device__ __forceinline__ XcdRange xcd_items(int64_t n_items, bool remap) {
   return XcdRange{lo + lb * wpb + wave, nbx * wpb, hi};
 }
 
-// Star initialisation: every core point of a mutual cell hangs under the cell's first core point
-// (its minimum original index: cells list points in index order), other points are roots.
+// Star initialisation: every core point of a mutual cell hangs under the cell's core point of
+// minimum original index (k_rep), other points are roots.
 __global__ __launch_bounds__(kBlock) void k_parent_init(int32_t* parent, int64_t n,
                                                        const uint8_t* __restrict__ core,
                                                        const int32_t* __restrict__ skey,
@@ -1402,7 +1525,7 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
     const uint8_t ma = mutual[ca];
     const CellRec<D> ra_rec = crec[ca];
     if (ra < 0 || !ma) continue;
-    const int ea = ra_rec.e;
+    const int ba = ra_rec.b, ea = ra_rec.e;  // core points anywhere in [b, e): scans start at b
     const float4 A1 = rec_boxA<D>(ra_rec), A2 = rec_boxB(ra_rec);
     int cx, cy, cz;
     decode_key<D>(ca, g, cx, cy, cz);
@@ -1421,17 +1544,19 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
       }
 #pragma unroll
       for (int k = 0; k < kR; ++k) wb[k] = (cb[k] >= 0) ? occ_bits[cb[k] >> 5] : 0u;
-      int rb[kR], cls[kR], ebv[kR];
+      int rb[kR], cls[kR], ebv[kR], bbv[kR];
 #pragma unroll
       for (int k = 0; k < kR; ++k) {
         rb[k] = -1;
         cls[k] = 0;
         ebv[k] = 0;
+        bbv[k] = 0;
         if (cb[k] >= 0 && ((wb[k] >> (cb[k] & 31)) & 1u)) {
           const CellRec<D> cr = crec[cb[k]];
           const int r = rep[cb[k]];
           const uint8_t m = mutual[cb[k]];
           ebv[k] = cr.e;
+          bbv[k] = cr.b;
           if (r >= 0 && m) {
             rb[k] = r;
             cls[k] = classify_cells<D>(A1, rec_boxA<D>(cr), A2, rec_boxB(cr), g);
@@ -1470,8 +1595,9 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
           pm &= pm - 1;
           const int rbl = __shfl(rb[k], l);
           const int ebl = __shfl(ebv[k], l);
+          const int bbl = __shfl(bbv[k], l);
           bool hit = false;
-          for (int jb0 = rbl; jb0 < ebl && !hit; jb0 += 64) {
+          for (int jb0 = bbl; jb0 < ebl && !hit; jb0 += 64) {
             const int jb = jb0 + lane;
             float4 pb = make_float4(0.f, 0.f, 0.f, 0.f);
             bool cb_ok = false;
@@ -1484,7 +1610,7 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
               const int lb = __ffsll((unsigned long long)bm) - 1;
               bm &= bm - 1;
               const float4 pq = shfl_f4(pb, lb);
-              for (int ja0 = ra; ja0 < ea && !hit; ja0 += 64) {
+              for (int ja0 = ba; ja0 < ea && !hit; ja0 += 64) {
                 const int ja = ja0 + lane;
                 const bool adj = (ja < ea) && core[ja] && adjacent<D>(pq, pts[ja], g);
                 hit = __ballot(adj) != 0;
@@ -1533,7 +1659,7 @@ __global__ __launch_bounds__(kBlock) void k_union(const float4* __restrict__ pts
                          return false;
                        }
                        if (uf_find(parent, si) == uf_find(parent, r)) return false;
-                       for (int j = r; j < e; ++j) {
+                       for (int j = b; j < e; ++j) {
                          if (core[j] && adjacent<D>(p, pts[j], g)) {
                            uf_unite(parent, sorig, si, j);
                            break;
@@ -1665,9 +1791,10 @@ __global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts
         }
 #pragma unroll
         for (int k = 0; k < kR; ++k) wb[k] = (c[k] >= 0) ? occ_bits[c[k] >> 5] : 0u;
-        int e[kR], r[kR], cls[kR], mut[kR];
+        int bg[kR], e[kR], r[kR], cls[kR], mut[kR];
 #pragma unroll
         for (int k = 0; k < kR; ++k) {
+          bg[k] = 0;
           e[k] = 0;
           r[k] = -1;
           cls[k] = 0;
@@ -1676,6 +1803,7 @@ __global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts
             const CellRec<D> cr = crec[c[k]];
             r[k] = rep[c[k]];
             mut[k] = mutual[c[k]];
+            bg[k] = cr.b;
             e[k] = cr.e;
             cls[k] = (r[k] >= 0) ? classify<D>(p, rec_boxA<D>(cr), rec_boxB(cr), g) : 0;
           }
@@ -1695,19 +1823,19 @@ __global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts
           while (pm) {
             const int l = __ffsll((unsigned long long)pm) - 1;
             pm &= pm - 1;
-            const int rl = __shfl(r[k], l), el = __shfl(e[k], l), cl = __shfl(cls[k], l);
+            const int bl = __shfl(bg[k], l), el = __shfl(e[k], l), cl = __shfl(cls[k], l);
             if (__shfl(mut[k], l)) {
               const int64_t ml = __shfl(mk[k], l);
               if (ml >= best) continue;
               bool hit = false;
-              for (int j0 = rl; j0 < el && !hit; j0 += 64) {
+              for (int j0 = bl; j0 < el && !hit; j0 += 64) {
                 const int j = j0 + lane;
                 hit = __ballot((j < el) && keyof(j) >= 0 && adjacent<D>(p, pts[j], g)) != 0;
               }
               if (hit) best = ml;
             } else {
               int64_t lb = INT64_MAX;
-              for (int j0 = rl; j0 < el; j0 += 64) {
+              for (int j0 = bl; j0 < el; j0 += 64) {
                 const int j = j0 + lane;
                 if (j < el) {
                   const int64_t m = keyof(j);
@@ -2081,11 +2209,13 @@ struct DbscanState {
   int uf_flags = -1;                         // see XcdRange; -1 = read RPT_UF_FLAGS once
   int k5_legacy = -1;                        // 1: round-1 K5 (fill + point queue); RPT_K5_MODE
   int k5_fill = 0;
+  int bucket_mode = -1;                      // RPT_K4_BUCKET (default 1): slab-bucket K4
   template <int D>
   const CellRec<D>* rec() const {
     return static_cast<const CellRec<D>*>(crec);
   }
   int32_t* slab = nullptr;   // per sorted point: final label of core points (global path)
+  int32_t* cell_min = nullptr;  // per cell: minimum original index of its core points (k_rep)
   uint8_t* fok = nullptr;    // per cell: frame condition met by every core point (denoise)
   bool integral_t = false;   // every finite t integral (slab = one frame id)
   int64_t* stmp = nullptr;
@@ -2209,10 +2339,12 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   bud.add<int32_t>(n + 1);  // non-core list (+count)
   bud.add<int32_t>(n);      // slab (global finalize; denoise: orig -> sorted)
   bud.add<uint8_t>(C1);     // fok (denoise)
+  bud.add<int32_t>(C1);     // cell_min
   bud.add<int32_t>(n + 1);  // occ
   bud.add<int32_t>(n + 1);  // hpos
   bud.add<CellRec<D>>(C1);  // crec
   bud.add<uint32_t>(C1 / 32 + 2);  // occupancy bits
+  bud.add<int32_t>(nt + 1);        // slab_lo (slab-bucket path)
   RPT_TRY(arena.reserve(bud.bytes, st));
   (void)arena.carve_n<Bounds>(1);
   uint32_t* keys = arena.carve_n<uint32_t>(n);
@@ -2237,28 +2369,46 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   nc_list = arena.carve_n<int32_t>(n + 1);
   slab = arena.carve_n<int32_t>(n);
   fok = arena.carve_n<uint8_t>(C1);
+  cell_min = arena.carve_n<int32_t>(C1);
   occ = arena.carve_n<int32_t>(n + 1);
   hpos = arena.carve_n<int32_t>(n + 1);
   CellRec<D>* cr = arena.carve_n<CellRec<D>>(C1);
   crec = cr;
   occ_bits = arena.carve_n<uint32_t>(C1 / 32 + 2);  // +1: two-word window reads
-  if (!occ_bits) {
+  int32_t* slab_lo = arena.carve_n<int32_t>(nt + 1);
+  if (!slab_lo) {
     set_error("internal: scratch carve overflow");
     return RPT_ENOMEM;
   }
-  hipLaunchKernelGGL(k_keys<D>, dim3(gb), dim3(kBlock), 0, st, x, y, z, stride, t, n, g, keys,
-                     vals);
-  RPT_CHECK_LAUNCH();
-  int bits = 1;
-  while ((int64_t(1) << bits) <= C1) ++bits;
-  uint32_t *sk, *sv;
-  RPT_TRY(radix_sort_pairs(keys, vals, keys_alt, vals_alt, n, bits, rtmp, &sk, &sv, st));
-  hipLaunchKernelGGL(k_gather<D>, dim3(gb), dim3(kBlock), 0, st, x, y, z, stride, t, n, sk, sv,
-                     pts, sorig, skey);
-  RPT_HIP(hipMemsetAsync(cell_start, 0, sizeof(int32_t) * C1, st));
-  hipLaunchKernelGGL(k_cell_runs, dim3(gb), dim3(kBlock), 0, st, skey, n, cell_start, hpos);
-  RPT_CHECK_LAUNCH();
-  RPT_TRY(exclusive_scan_total_i32(cell_start, cell_start, C1, st));
+  if (bucket_mode < 0) {
+    const char* e = std::getenv("RPT_K4_BUCKET");
+    bucket_mode = (e && std::atoi(e) == 0) ? 0 : 1;
+  }
+  // time-ordered finite 2-D points with a slab's cells fitting LDS: per-slab counting sort
+  const bool bucket = bucket_mode && D == 2 && hb.n_finite_t == n && !hb.t_descends &&
+                      (int64_t)nx * ny <= kBucketCells && nt < (int64_t(1) << 31);
+  if (bucket) {
+    hipLaunchKernelGGL(k_slab_lo, dim3(grid_for(nt + 1, kBlock, 1024)), dim3(kBlock), 0, st, t, n,
+                       g, slab_lo);
+    hipLaunchKernelGGL(k_slab_bucket, dim3((unsigned)nt), dim3(kBucketBlock), 0, st, x, y, stride,
+                       t, g, slab_lo, pts, sorig, skey, cell_start);
+    hipLaunchKernelGGL(k_key_heads, dim3(gb), dim3(kBlock), 0, st, skey, n, hpos);
+    RPT_CHECK_LAUNCH();
+  } else {
+    hipLaunchKernelGGL(k_keys<D>, dim3(gb), dim3(kBlock), 0, st, x, y, z, stride, t, n, g, keys,
+                       vals);
+    RPT_CHECK_LAUNCH();
+    int bits = 1;
+    while ((int64_t(1) << bits) <= C1) ++bits;
+    uint32_t *sk, *sv;
+    RPT_TRY(radix_sort_pairs(keys, vals, keys_alt, vals_alt, n, bits, rtmp, &sk, &sv, st));
+    hipLaunchKernelGGL(k_gather<D>, dim3(gb), dim3(kBlock), 0, st, x, y, z, stride, t, n, sk, sv,
+                       pts, sorig, skey);
+    RPT_HIP(hipMemsetAsync(cell_start, 0, sizeof(int32_t) * C1, st));
+    hipLaunchKernelGGL(k_cell_runs, dim3(gb), dim3(kBlock), 0, st, skey, n, cell_start, hpos);
+    RPT_CHECK_LAUNCH();
+    RPT_TRY(exclusive_scan_total_i32(cell_start, cell_start, C1, st));
+  }
   RPT_TRY(exclusive_scan_total_i32(hpos, hpos, n, st));
   RPT_HIP(hipMemsetAsync(occ_bits, 0, sizeof(uint32_t) * (C1 / 32 + 2), st));
   hipLaunchKernelGGL(k_occ_list, dim3(gb), dim3(kBlock), 0, st, skey, n, hpos, occ, occ_bits);
@@ -2383,7 +2533,12 @@ int32_t DbscanState::union_pass(hipStream_t st) {
   const int gw = wave_grid(n);
   const unsigned gp = (unsigned)((n + kBlock - 1) / kBlock);
   const int32_t* n_occ = hpos + n;
-  hipLaunchKernelGGL(k_rep, dim3(gc), dim3(kBlock), 0, st, cell_start, C, core, rep);
+  hipLaunchKernelGGL(k_fill_i32, dim3(gc), dim3(kBlock), 0, st, cell_min, C, INT_MAX);
+  RPT_HIP(hipMemsetAsync(rep, 0xFF, sizeof(int32_t) * (size_t)C, st));
+  hipLaunchKernelGGL(k_cell_min_orig, dim3(gb), dim3(kBlock), 0, st, skey, core, sorig, n, C,
+                     cell_min);
+  hipLaunchKernelGGL(k_rep, dim3(gb), dim3(kBlock), 0, st, skey, core, sorig, n, C, cell_min,
+                     rep);
   hipLaunchKernelGGL(k_parent_init, dim3(gb), dim3(kBlock), 0, st, parent, n, core, skey, mutual,
                      rep, C);
   if (dim == 2) {
