@@ -1745,9 +1745,36 @@ __global__ __launch_bounds__(kBlock) void k_label_core(const int32_t* __restrict
   }
 }
 
+// Per cell, the smallest component key among its core points (INT_MAX: none) -- the same
+// segmented wave minimum over the sorted points as k_cell_min_orig.
+__global__ __launch_bounds__(kBlock) void k_cell_min_key(const int32_t* __restrict__ skey,
+                                                        const int32_t* __restrict__ key_of,
+                                                        int64_t n, int64_t cells,
+                                                        int32_t* __restrict__ cell_key) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t s0 = (int64_t)blockIdx.x * blockDim.x; s0 < n;
+       s0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = s0 + threadIdx.x;
+    const int key = (s < n) ? skey[s] : -1;
+    const int kv = (s < n) ? key_of[s] : -1;
+    int v = (kv >= 0 && (int64_t)key < cells) ? kv : INT_MAX;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int ov = __shfl_up(v, off, 64);
+      const int ok = __shfl_up(key, off, 64);
+      if (lane >= off && ok == key) v = min(v, ov);
+    }
+    const int next = __shfl_down(key, 1, 64);
+    if ((lane == 63 || next != key) && key >= 0 && v != INT_MAX) atomicMin(cell_key + key, v);
+  }
+}
+
 // K7/K8 (non-core points, queued): the smallest component key over adjacent core points, else
-// none.  One wave per point, lanes over candidate cells; the core points of a mutual cell form
-// one component (star init), so such a cell needs one adjacent core point, found 64 at a time.
+// none.  One wave per point, one lane per candidate cell of its window.  A cell whose box is
+// wholly adjacent contributes its smallest key (cell_key) with no point read; the others are
+// resolved in increasing cell_key order and only while that key can still beat the best so far:
+// a mutual cell (one component) needs one adjacent core point, any other cell the smallest key
+// among its adjacent core points.
 // GLOBAL = false: key = ccmin (component-min original index, local run), label = cid[key];
 // GLOBAL = true : key = slab (the core point's final label: labels are ranks of the sorted global
 //                 representatives, so the smallest label is the smallest representative).
@@ -1757,9 +1784,8 @@ __global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts
                                                  const CellRec<D>* __restrict__ crec,
                                                  const uint32_t* __restrict__ occ_bits,
                                                  const float2* __restrict__ slab_t,
-                                                 const int32_t* __restrict__ ccmin,
-                                                 const int32_t* __restrict__ slab,
-                                                 const int32_t* __restrict__ rep,
+                                                 const int32_t* __restrict__ key_of,
+                                                 const int32_t* __restrict__ cell_key,
                                                  const uint8_t* __restrict__ mutual,
                                                  const int32_t* __restrict__ sorig,
                                                  const int32_t* __restrict__ cid,
@@ -1770,88 +1796,99 @@ __global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts
   const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
   const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
   const int64_t nq = *nc_count;
-  auto keyof = [&](int j) -> int64_t { return GLOBAL ? (int64_t)slab[j] : (int64_t)ccmin[j]; };
   for (int64_t q = w0; q < nq; q += nw) {
     const int s = nc_list[q];
     const int32_t key = skey[s];
-    int64_t best = INT64_MAX;
+    int best = INT_MAX;
     if ((int64_t)key < g.cells) {
       const float4 p = pts[s];
       int cx, cy, cz;
       decode_key<D>(key, g, cx, cy, cz);
       const Window w = make_window<D, false>(cx, cy, cz, p.w, p.w, g, slab_t);
+      // super-rounds of kR candidates per lane, loads of one kind issued together: the cells'
+      // smallest keys (empty cells hold INT_MAX, so no occupancy lookup), then the records of
+      // the cells with core points -- two dependent rounds per super-round
       for (int base = 0; base < w.total; base += 64 * kR) {
-        // super-round: bitmap words, then records + rep + mutual, loaded together per lane
         int64_t c[kR];
-        uint32_t wb[kR];
+        int ck[kR], cb[kR], ce[kR], cls[kR], mu[kR];
 #pragma unroll
         for (int k = 0; k < kR; ++k) {
           const int qq = base + k * 64 + lane;
           c[k] = (qq < w.total) ? window_cell<D>(w, qq, g, slab_t, p.w, p.w) : -1;
         }
 #pragma unroll
-        for (int k = 0; k < kR; ++k) wb[k] = (c[k] >= 0) ? occ_bits[c[k] >> 5] : 0u;
-        int bg[kR], e[kR], r[kR], cls[kR], mut[kR];
+        for (int k = 0; k < kR; ++k) ck[k] = (c[k] >= 0) ? cell_key[c[k]] : INT_MAX;
+        int v = INT_MAX;
 #pragma unroll
         for (int k = 0; k < kR; ++k) {
-          bg[k] = 0;
-          e[k] = 0;
-          r[k] = -1;
-          cls[k] = 0;
-          mut[k] = 0;
-          if (c[k] >= 0 && ((wb[k] >> (c[k] & 31)) & 1u)) {
+          cb[k] = ce[k] = cls[k] = mu[k] = 0;
+          if (ck[k] != INT_MAX) {
             const CellRec<D> cr = crec[c[k]];
-            r[k] = rep[c[k]];
-            mut[k] = mutual[c[k]];
-            bg[k] = cr.b;
-            e[k] = cr.e;
-            cls[k] = (r[k] >= 0) ? classify<D>(p, rec_boxA<D>(cr), rec_boxB(cr), g) : 0;
+            cb[k] = cr.b;
+            ce[k] = cr.e;
+            mu[k] = mutual[c[k]];
+            cls[k] = classify<D>(p, rec_boxA<D>(cr), rec_boxB(cr), g);
+            if (cls[k] == 1) v = min(v, ck[k]);
           }
         }
-        int64_t mk[kR];
 #pragma unroll
-        for (int k = 0; k < kR; ++k) mk[k] = (cls[k] != 0 && mut[k]) ? keyof(r[k]) : INT64_MAX;
-        // whole mutual cells in reach: their component key directly
-        int64_t lb0 = INT64_MAX;
+        for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off));
+        best = min(best, v);
+        // the partially reachable cells, smallest key first, while a key can still win
+        uint32_t pend = 0;
 #pragma unroll
-        for (int k = 0; k < kR; ++k) lb0 = min(lb0, (cls[k] == 1 && mut[k]) ? mk[k] : INT64_MAX);
-        best = min(best, wave_min64(lb0));
+        for (int k = 0; k < kR; ++k) pend |= (cls[k] == 2) ? (1u << k) : 0u;
+        while (true) {
+          int mine = INT_MAX, mk = -1;
 #pragma unroll
-        for (int k = 0; k < kR; ++k) {
-          uint64_t pm =
-              __ballot(cls[k] != 0 && !(cls[k] == 1 && mut[k]) && (!mut[k] || mk[k] < best));
-          while (pm) {
-            const int l = __ffsll((unsigned long long)pm) - 1;
-            pm &= pm - 1;
-            const int bl = __shfl(bg[k], l), el = __shfl(e[k], l), cl = __shfl(cls[k], l);
-            if (__shfl(mut[k], l)) {
-              const int64_t ml = __shfl(mk[k], l);
-              if (ml >= best) continue;
-              bool hit = false;
-              for (int j0 = bl; j0 < el && !hit; j0 += 64) {
-                const int j = j0 + lane;
-                hit = __ballot((j < el) && keyof(j) >= 0 && adjacent<D>(p, pts[j], g)) != 0;
-              }
-              if (hit) best = ml;
-            } else {
-              int64_t lb = INT64_MAX;
-              for (int j0 = bl; j0 < el; j0 += 64) {
-                const int j = j0 + lane;
-                if (j < el) {
-                  const int64_t m = keyof(j);
-                  if (m >= 0 && m < best && m < lb && (cl == 1 || adjacent<D>(p, pts[j], g)))
-                    lb = m;
-                }
-              }
-              best = min(best, wave_min64(lb));
+          for (int k = 0; k < kR; ++k)
+            if (((pend >> k) & 1u) && ck[k] < best && ck[k] < mine) {
+              mine = ck[k];
+              mk = k;
             }
+          int mm = mine;
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1) mm = min(mm, __shfl_xor(mm, off));
+          if (mm == INT_MAX) break;
+          const uint64_t at = __ballot(mine == mm);
+          const int l = __ffsll((unsigned long long)at) - 1;
+          const int kl = __shfl(mk, l);
+          int bsel = 0, esel = 0, msel = 0;
+#pragma unroll
+          for (int k = 0; k < kR; ++k)
+            if (k == kl) {
+              bsel = cb[k];
+              esel = ce[k];
+              msel = mu[k];
+            }
+          if (lane == l) pend &= ~(1u << kl);
+          const int bl = __shfl(bsel, l), el = __shfl(esel, l);
+          if (__shfl(msel, l)) {  // one component: a single adjacent core point decides
+            bool hit = false;
+            for (int j0 = bl; j0 < el && !hit; j0 += 64) {
+              const int j = j0 + lane;
+              hit = __ballot((j < el) && key_of[j] >= 0 && adjacent<D>(p, pts[j], g)) != 0;
+            }
+            if (hit) best = mm;
+          } else {
+            int lb = INT_MAX;
+            for (int j0 = bl; j0 < el; j0 += 64) {
+              const int j = j0 + lane;
+              if (j < el) {
+                const int m = key_of[j];
+                if (m >= 0 && m < best && m < lb && adjacent<D>(p, pts[j], g)) lb = m;
+              }
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) lb = min(lb, __shfl_xor(lb, off));
+            best = min(best, lb);
           }
         }
       }
     }
     if (lane == 0) {
       int32_t out = -1;
-      if (best != INT64_MAX) out = GLOBAL ? (int32_t)best : cid[best];
+      if (best != INT_MAX) out = GLOBAL ? best : cid[best];
       labels[sorig[s]] = out;
     }
   }
@@ -2589,14 +2626,17 @@ int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hi
   RPT_CHECK_LAUNCH();
   RPT_TRY(exclusive_scan_total_i32(cid, cid, n, st));
   hipLaunchKernelGGL(k_label_core, dim3(gb), dim3(kBlock), 0, st, ccmin, n, sorig, cid, labels);
+  const int gc = grid_for(C, kBlock, 8192);
+  hipLaunchKernelGGL(k_fill_i32, dim3(gc), dim3(kBlock), 0, st, cell_min, C, INT_MAX);
+  hipLaunchKernelGGL(k_cell_min_key, dim3(gb), dim3(kBlock), 0, st, skey, ccmin, n, C, cell_min);
   if (dim == 2)
     hipLaunchKernelGGL((k_label<2, false>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<2>(), occ_bits, slab_t, ccmin, (const int32_t*)nullptr, rep,
-                       mutual, sorig, cid, nc_list, nc_count, labels);
+                       rec<2>(), occ_bits, slab_t, ccmin, cell_min, mutual, sorig, cid, nc_list,
+                       nc_count, labels);
   else
     hipLaunchKernelGGL((k_label<3, false>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<3>(), occ_bits, slab_t, ccmin, (const int32_t*)nullptr, rep,
-                       mutual, sorig, cid, nc_list, nc_count, labels);
+                       rec<3>(), occ_bits, slab_t, ccmin, cell_min, mutual, sorig, cid, nc_list,
+                       nc_count, labels);
   RPT_CHECK_LAUNCH();
   tm.mark();
   if (stats && defer) return RPT_OK;  // fill_stats after the caller's sync
@@ -2644,14 +2684,17 @@ int32_t DbscanState::labels_global(const int64_t* rep_orig, const int64_t* reps,
                      sorig, rep_orig, reps, nr, ccmin, cid, nc_list, nc_count);
   hipLaunchKernelGGL(k_label_global_core, dim3(gb), dim3(kBlock), 0, st, core, ccmin, cid, sorig,
                      n, slab, labels);
+  const int gc = grid_for(C, kBlock, 8192);
+  hipLaunchKernelGGL(k_fill_i32, dim3(gc), dim3(kBlock), 0, st, cell_min, C, INT_MAX);
+  hipLaunchKernelGGL(k_cell_min_key, dim3(gb), dim3(kBlock), 0, st, skey, slab, n, C, cell_min);
   if (dim == 2)
     hipLaunchKernelGGL((k_label<2, true>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<2>(), occ_bits, slab_t, (const int32_t*)nullptr, slab, rep, mutual,
-                       sorig, (const int32_t*)nullptr, nc_list, nc_count, labels);
+                       rec<2>(), occ_bits, slab_t, slab, cell_min, mutual, sorig,
+                       (const int32_t*)nullptr, nc_list, nc_count, labels);
   else
     hipLaunchKernelGGL((k_label<3, true>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<3>(), occ_bits, slab_t, (const int32_t*)nullptr, slab, rep, mutual,
-                       sorig, (const int32_t*)nullptr, nc_list, nc_count, labels);
+                       rec<3>(), occ_bits, slab_t, slab, cell_min, mutual, sorig,
+                       (const int32_t*)nullptr, nc_list, nc_count, labels);
   RPT_CHECK_LAUNCH();
   return RPT_OK;
 }
