@@ -13,4 +13,4 @@ for C in FETCH_SIZE WRITE_SIZE; do
     > "gpurun_out/pmc_$C.log" 2>&1
   rc=$?; echo "pmc $C rc=$rc" >> "gpurun_out/pmc_$C.log"; [ $rc -eq 0 ] || exit $rc
 done
-python tools/pmc_traffic.py "$TAG"
+python tools/pmc_traffic.py "$TAG" "${2:-k5_traffic.json}" "${3:-bench.py default workload}"

@@ -3,7 +3,7 @@
 tools/pmc.sh: bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 per launch (FETCH_SIZE is in KiB and
 reads half of the bytes of wide coalesced reads on gfx950, MI355X_MICROARCH.md §HBM; the factor is
 calibrated for 16-B/lane streams, so for K5's narrower gathers it is an approximation).
-Writes profiles/<tag>/k5_traffic.json and a per-kernel summary CSV."""
+Writes profiles/<tag>/<name> (default k5_traffic.json) and a per-kernel summary CSV."""
 import csv
 import glob
 import json
@@ -13,6 +13,8 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 tag = sys.argv[1] if len(sys.argv) > 1 else "r1"
+out_name = sys.argv[2] if len(sys.argv) > 2 else "k5_traffic.json"
+workload = sys.argv[3] if len(sys.argv) > 3 else "bench.py default (100-frame stack)"
 K5 = ("k_core_cells_oct", "k_core_cell_fast", "k_core_cell_window", "k_core_fill", "k_core_slow")
 
 
@@ -50,6 +52,6 @@ res = {"kernels": {k: (None if r is None else {"fetch_kib": r[2], "write_kib": r
        "bytes_per_launch": total,
        "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch, summed over the K5 kernels "
                   "that ran (" + ", ".join(k for k, r in k5.items() if r) + "); separate --pmc passes",
-       "workload": "bench.py default (100-frame stack)"}
-(out_dir / "k5_traffic.json").write_text(json.dumps(res, indent=1))
+       "workload": workload}
+(out_dir / out_name).write_text(json.dumps(res, indent=1))
 print(json.dumps(res))
