@@ -239,7 +239,9 @@ int32_t rpt_fuse_gains_max(const float* x, const float* y, const float* intensit
 
 /* ---- K9: per-(frame, label) cluster summaries ---------------------------------------
  * point_frame[n] (dev, i32, non-decreasing frame slot per point), labels[n] from
- * rpt_stdbscan.  Segment s = one (frame, label>=0) pair, ordered by (label, frame).
+ * rpt_stdbscan.  Segment s = one (frame, label>=0) pair; the order of segments is unspecified
+ * (frame-major when n_clusters < 8192 and frames average <= 2^18 points, label-major otherwise):
+ * rpt_order_clusters buckets them.
  * centroid = sequential float32 sum in point order / count (np.mean axis 0);
  * mean intensity = numpy 1-D float32 mean (pairwise sums over 8192-element chunks).
  * frame_first_noise[n_frames] (dev, int64) = first point index of label -1 per frame, or -1.

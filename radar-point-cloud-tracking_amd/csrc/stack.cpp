@@ -69,7 +69,8 @@ int32_t cluster_summaries_dev(const int32_t* labels, const float* x, const float
                               int bits, int64_t s_hint, int32_t* o_frame, int32_t* o_label,
                               int64_t* o_count, int64_t* o_first, float* o_cx, float* o_cy,
                               float* o_mi, int64_t* frame_first_noise,
-                              const int32_t** n_seg_dev, hipStream_t st);
+                              const int32_t** n_seg_dev, bool force_radix, bool* radix_used,
+                              hipStream_t st);
 int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
                           const float* inten, const int32_t* pf, int64_t n, int32_t n_frames,
                           int32_t n_clusters, int32_t* o_frame, int32_t* o_label,
@@ -250,6 +251,7 @@ struct rpt_stack {
   bool ev_ok = false;
   hipEvent_t ev_rb = nullptr;  // readback marker of the speculative K1 write
   int sum_bits = 12;           // radix bits of the K9 label keys, from the previous run
+  bool k9_radix = false;       // a frame held more labels than K9's frame sort takes
   int64_t seg_hint = 0;        // segment-count estimate from the previous run
 
   ~rpt_stack() {
@@ -483,7 +485,7 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
                             land_applied ? dbscan_bounds.data() : nullptr));
   if (timing) RPT_HIP(hipEventRecord(ev[3], st));
 
-  // ---- K9 summaries (segments ordered by (label, frame))
+  // ---- K9 summaries (per-(frame, label) segments)
   RPT_TRY(seg_frame.ensure(cap2, st));
   RPT_TRY(seg_label.ensure(cap2, st));
   RPT_TRY(seg_count.ensure(cap2, st));
@@ -496,9 +498,10 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
   const int64_t sc = std::min<int64_t>(
       std::max<int64_t>(seg_hint > 0 ? seg_hint + seg_hint / 4 + 64 : 4096, 1), n_in_);
   const int32_t* nseg_dev = nullptr;
+  bool radix_used = false;
   RPT_TRY(cluster_summaries_dev(labels.p, cx, cy, cv, cpf, n_in_, F, bits, sc, seg_frame.p,
                                 seg_label.p, seg_count.p, seg_first.p, seg_cx.p, seg_cy.p,
-                                seg_mi.p, first_noise.p, &nseg_dev, st));
+                                seg_mi.p, first_noise.p, &nseg_dev, k9_radix, &radix_used, st));
   SegPack sp{seg_count.p, seg_first.p, first_noise.p, seg_frame.p,
              seg_label.p, seg_cx.p,    seg_cy.p,      seg_mi.p};
   size_t bytes = seg_pack_bytes(sc, F);
@@ -514,24 +517,33 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
   const int64_t ncl = ncl_dev ? reinterpret_cast<const int64_t*>(down.p)[1] : sts.n_clusters;
   if (ncl_dev) RPT_TRY(stdbscan_fill_stats(dstate, (int32_t)ncl, &sts));
   int64_t sc_used = sc;
-  if ((int64_t(1) << bits) <= ncl || S > sc) {
-    // the label keys needed more bits, or more segments than the readback holds: K9 again
-    // with the exact counts, then a readback of exactly S
-    if ((int64_t(1) << bits) <= ncl)
-      RPT_TRY(cluster_summaries_dev(labels.p, cx, cy, cv, cpf, n_in_, F, radix_bits_for(ncl), S,
-                                    seg_frame.p, seg_label.p, seg_count.p, seg_first.p,
-                                    seg_cx.p, seg_cy.p, seg_mi.p, first_noise.p, &nseg_dev, st));
-    sc_used = std::max<int64_t>(S, 1);
-    bytes = seg_pack_bytes(sc_used, F);
-    RPT_TRY(pack_d.ensure(bytes / 4 + 1, st));
-    RPT_TRY(down.ensure(bytes, st));
-    hipLaunchKernelGGL(k_pack_segs, dim3(grid_for(std::max<int64_t>(sc_used, F), 256, 256)),
-                       dim3(256), 0, st, nseg_dev, ncl_dev, sp, sc_used, F,
-                       reinterpret_cast<char*>(pack_d.p));
-    RPT_CHECK_LAUNCH();
-    RPT_HIP(hipMemcpyAsync(down.p, pack_d.p, bytes, hipMemcpyDeviceToHost, st));
-    RPT_TRY(wait_stream(st));
-    S = reinterpret_cast<const int64_t*>(down.p)[0];
+  // K9 again when the frame sort met a frame with too many labels (S = -1: the radix path, from
+  // now on) or the radix path's label keys needed more bits; then the readback repeats until it
+  // holds every segment (a redo changes the count)
+  const bool bits_short = radix_used && (int64_t(1) << bits) <= ncl;
+  if (S < 0 || bits_short || S > sc) {
+    const bool rerun = S < 0 || bits_short;
+    if (S < 0) k9_radix = true;
+    if (rerun)
+      RPT_TRY(cluster_summaries_dev(labels.p, cx, cy, cv, cpf, n_in_, F, radix_bits_for(ncl),
+                                    std::max<int64_t>(S, sc), seg_frame.p, seg_label.p,
+                                    seg_count.p, seg_first.p, seg_cx.p, seg_cy.p, seg_mi.p,
+                                    first_noise.p, &nseg_dev, k9_radix, nullptr, st));
+    sc_used = rerun ? sc : std::max<int64_t>(S, 1);
+    for (int pass = 0; pass < 2; ++pass) {
+      bytes = seg_pack_bytes(sc_used, F);
+      RPT_TRY(pack_d.ensure(bytes / 4 + 1, st));
+      RPT_TRY(down.ensure(bytes, st));
+      hipLaunchKernelGGL(k_pack_segs, dim3(grid_for(std::max<int64_t>(sc_used, F), 256, 256)),
+                         dim3(256), 0, st, nseg_dev, ncl_dev, sp, sc_used, F,
+                         reinterpret_cast<char*>(pack_d.p));
+      RPT_CHECK_LAUNCH();
+      RPT_HIP(hipMemcpyAsync(down.p, pack_d.p, bytes, hipMemcpyDeviceToHost, st));
+      RPT_TRY(wait_stream(st));
+      S = reinterpret_cast<const int64_t*>(down.p)[0];
+      if (S <= sc_used) break;
+      sc_used = S;
+    }
   }
   // next run's guesses: one pass of up to 12 bits when the count allows, with headroom
   const int exact = radix_bits_for(ncl);
@@ -1189,15 +1201,20 @@ int32_t rpt_shard_finish(rpt_shard* h, const int64_t* reps_sorted, int64_t n_rep
   int64_t Sg = 0;
   if (K > 0) {
     const int32_t* nseg_dev = nullptr;
-    RPT_TRY(cluster_summaries_dev(lab, x, y, v, pf, K, F, bits, K, S.seg_frame.p, S.seg_label.p,
-                                  S.seg_count.p, S.seg_first.p, S.seg_cx.p, S.seg_cy.p,
-                                  S.seg_mi.p, S.first_noise.p, &nseg_dev, st));
+    auto k9 = [&]() {
+      return cluster_summaries_dev(lab, x, y, v, pf, K, F, bits, K, S.seg_frame.p, S.seg_label.p,
+                                   S.seg_count.p, S.seg_first.p, S.seg_cx.p, S.seg_cy.p,
+                                   S.seg_mi.p, S.first_noise.p, &nseg_dev, S.k9_radix, nullptr,
+                                   st);
+    };
+    RPT_TRY(k9());
     SegPack sp{S.seg_count.p, S.seg_first.p, S.first_noise.p, S.seg_frame.p,
                S.seg_label.p, S.seg_cx.p,    S.seg_cy.p,      S.seg_mi.p};
-    // readback sized by the previous run's segment count (+ headroom); again when it overflows
+    // readback sized by the previous run's segment count (+ headroom); again when it overflows,
+    // and after a redo on the radix path when a frame held too many labels (count -1)
     int64_t sc = std::min<int64_t>(std::max<int64_t>(S.seg_hint > 0 ? S.seg_hint + S.seg_hint / 4 + 64
                                                                    : 4096, 1), K);
-    for (int pass = 0; pass < 2; ++pass) {
+    for (int pass = 0; pass < 3; ++pass) {
       const size_t bytes = seg_pack_bytes(sc, F);
       RPT_TRY(S.pack_d.ensure(bytes / 4 + 1, st));
       RPT_TRY(S.down.ensure(bytes, st));
@@ -1208,6 +1225,11 @@ int32_t rpt_shard_finish(rpt_shard* h, const int64_t* reps_sorted, int64_t n_rep
       RPT_HIP(hipMemcpyAsync(S.down.p, S.pack_d.p, bytes, hipMemcpyDeviceToHost, st));
       RPT_TRY(wait_stream(st));
       Sg = reinterpret_cast<const int64_t*>(S.down.p)[0];
+      if (Sg < 0 && !S.k9_radix) {
+        S.k9_radix = true;
+        RPT_TRY(k9());
+        continue;
+      }
       if (Sg <= sc) break;
       sc = Sg;
     }

@@ -8,13 +8,17 @@
 //                    each chunk summed pairwise (numpy pairwise_sum: 8 accumulators up to 128
 //                    elements, halving split above), chunks accumulated sequentially, then a
 //                    float32 division by k.
-// Segments: a stable radix sort of (label+1, index) keeps each label's points in index order, so
-// every (label, frame) run is contiguous and ordered.  Two waves per run (x, y): the
+// Segments: a stable per-frame counting sort (one 8-wave block per frame, labels hashed to LDS
+// slots; up to kFsMaxKeys labels per frame) or, beyond that, a stable radix sort of (label+1,
+// index) keeps each label's points in index order, so every (frame, label) run is contiguous and
+// ordered; segments come frame-major (hash order inside a frame) from the counting sort,
+// label-major from the radix sort (consumers bucket them by frame, tracker.cpp order_clusters).  Two waves per run (x, y): the
 // order-preserving float32 chain is fed from LDS, so a run of k points costs ~k dependent adds
 // (~4.4 cycles each), not k memory latencies.
-// Noise (key 0) sorts first in index order, so each frame's first noise point is the head of its
-// frame within the noise run (no atomics).
+// Radix path: noise (key 0) sorts first in index order, so each frame's first noise point is the
+// head of its frame within the noise run (no atomics).
 #include <climits>
+#include <cstdlib>
 
 #include <algorithm>
 
@@ -289,6 +293,10 @@ __device__ __forceinline__ float mean_intensity(const float* __restrict__ gi, in
 // Three waves per (frame, label) run: wave 0 sums x (np.mean axis 0, sequential float32 in index
 // order), wave 1 sums y — two pure dependent-add chains on different SIMDs — and wave 2 takes
 // the mean intensity (lane-parallel), so no other work sits in the chains' instruction streams.
+// META: the frame sort already wrote frame/label/count/first and o_count gives each run's length
+// (runs are not adjacent: noise slots sit between frames); otherwise runs tile [0, n) and the
+// metadata comes from the sorted keys.
+template <bool META>
 __global__ __launch_bounds__(kBlock) void k_summarize(
     const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
     const int64_t* __restrict__ seg_start, const int32_t* __restrict__ n_seg_dev, int64_t n,
@@ -306,7 +314,7 @@ __global__ __launch_bounds__(kBlock) void k_summarize(
     const int comp = __builtin_amdgcn_readfirstlane((int)(w - (int64_t)su * 3));
     const int b = __builtin_amdgcn_readfirstlane((int)seg_start[su]);
     const int e = __builtin_amdgcn_readfirstlane(
-        (int)((su + 1 < n_seg) ? seg_start[su + 1] : n));
+        META ? (int)(b + o_count[su]) : (int)((su + 1 < n_seg) ? seg_start[su + 1] : n));
     const int k = e - b;
     const float fk = (float)k;
     if (comp == 2) {
@@ -318,6 +326,8 @@ __global__ __launch_bounds__(kBlock) void k_summarize(
     if (lane == 0) {
       if (comp) {
         o_cy[su] = sum / fk;
+      } else if (META) {
+        o_cx[su] = sum / fk;
       } else {
         const uint32_t i0 = sv[b];
         o_frame[su] = pf[i0];
@@ -407,6 +417,285 @@ __global__ __launch_bounds__(kBlock) void k_label_means(
   }
 }
 
+// ---- per-frame counting sort (point_frame non-decreasing) ----------------------------------
+// One 8-wave block per frame.  Each wave owns a contiguous part of the frame's points; the frame's
+// clustered labels get LDS hash slots (at most kFsMaxKeys distinct labels per frame, else the
+// frame reports an overflow and the caller redoes K9 on the radix path), counted per (wave, slot),
+// scanned into frame-local offsets and per-wave cursors, and the points scattered stably — a
+// (frame, label) run is then contiguous and in index order, as the radix path gives.  Noise is
+// not scattered; each frame's first noise point is the first one of its lowest wave.
+constexpr int kFsWaves = 8, kFsSlots = 1024, kFsMaxKeys = kFsSlots / 2;
+
+struct FsLds {
+  int keys[kFsSlots];               // label + 1 per slot, or -1
+  uint32_t cnt[kFsWaves][kFsSlots]; // per-wave counts, then per-wave cursors
+  int off[kFsSlots];                // run start (frame-local) per slot
+  uint32_t wsum[2][kFsWaves];
+  int fnoise[kFsWaves];
+  int nkeys, overflow;
+};
+
+__device__ __forceinline__ uint32_t fs_hash(int v) {
+  return ((uint32_t)v * 2654435761u) >> (32 - 10);
+}
+
+__device__ int fs_insert(FsLds& L, int v) {
+  uint32_t s = fs_hash(v);
+  for (int probe = 0; probe < kFsSlots; ++probe) {
+    const int k = __atomic_load_n(&L.keys[s], __ATOMIC_RELAXED);
+    if (k == v) return (int)s;
+    if (k == -1) {
+      const int old = atomicCAS(&L.keys[s], -1, v);
+      if (old == -1) {
+        if (atomicAdd(&L.nkeys, 1) >= kFsMaxKeys) L.overflow = 1;
+        return (int)s;
+      }
+      if (old == v) return (int)s;
+    }
+    s = (s + 1) & (kFsSlots - 1);
+  }
+  L.overflow = 1;
+  return -1;
+}
+
+__device__ __forceinline__ int fs_find(const FsLds& L, int v) {
+  uint32_t s = fs_hash(v);
+  for (int probe = 0; probe < kFsSlots; ++probe) {
+    const int k = L.keys[s];
+    if (k == v) return (int)s;
+    if (k == -1) return -1;
+    s = (s + 1) & (kFsSlots - 1);
+  }
+  return -1;
+}
+
+// Lanes with equal keys in this 64-point step: the lowest such lane (leader), the lane's rank
+// among them and their number.  One ballot per distinct key, scalar loop.
+__device__ __forceinline__ void wave_group(int v, bool valid, int lane, int& leader, int& rank,
+                                           int& cnt) {
+  uint64_t rem = __ballot(valid);
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  leader = -1;
+  rank = 0;
+  cnt = 0;
+  while (rem) {
+    const int l = __builtin_ctzll(rem);
+    const int u = __builtin_amdgcn_readlane(v, l);
+    const bool mine = valid && v == u;
+    const uint64_t m = __ballot(mine);
+    if (mine) {
+      leader = l;
+      rank = __popcll(m & lt);
+      cnt = __popcll(m);
+    }
+    rem &= ~m;
+  }
+}
+
+__device__ __forceinline__ int64_t lower_bound_i32(const int32_t* __restrict__ a, int64_t n,
+                                                   int32_t key) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < key)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t o = __shfl_up(x, off);
+    if (lane >= off) x += o;
+  }
+  return x;
+}
+
+// Per segment q of the frame the frame-local lists at [lo + q] get the run's start position,
+// length and label; tmp_first[start] gets the run's first point index.
+__global__ __launch_bounds__(kFsWaves * 64) void k_frame_sort(
+    const int32_t* __restrict__ labels, const int32_t* __restrict__ pf, int64_t n,
+    const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ inten,
+    float* __restrict__ gx, float* __restrict__ gy, float* __restrict__ gi,
+    int32_t* __restrict__ fstart, int32_t* __restrict__ tmp_start, int32_t* __restrict__ tmp_len,
+    int32_t* __restrict__ tmp_label, int32_t* __restrict__ tmp_first,
+    int32_t* __restrict__ nseg_f, int64_t* __restrict__ first_noise,
+    int32_t* __restrict__ overflow) {
+  __shared__ FsLds L;
+  const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lo = __builtin_amdgcn_readfirstlane((int)lower_bound_i32(pf, n, f));
+  const int hi = __builtin_amdgcn_readfirstlane((int)lower_bound_i32(pf, n, f + 1));
+  for (int s = tid; s < kFsSlots; s += kFsWaves * 64) {
+    L.keys[s] = -1;
+#pragma unroll
+    for (int q = 0; q < kFsWaves; ++q) L.cnt[q][s] = 0u;
+  }
+  if (tid == 0) {
+    L.nkeys = 0;
+    L.overflow = 0;
+    fstart[f] = lo;
+  }
+  __syncthreads();
+  // this wave's chunks of 64 points
+  const int nch = (hi - lo + 63) / 64, cpw = (nch + kFsWaves - 1) / kFsWaves;
+  const int cb0 = w * cpw, cb1 = min(nch, cb0 + cpw);
+  // pass 1: counts per (wave, slot), one LDS update per distinct label per step (its leader)
+  int wfn = INT_MAX;
+  constexpr int U1 = 8;
+  for (int cb = cb0; cb < cb1; cb += U1) {
+    int lab[U1];
+#pragma unroll
+    for (int u = 0; u < U1; ++u) {
+      const int i = lo + (cb + u) * 64 + lane;
+      lab[u] = (cb + u < cb1 && i < hi) ? labels[i] : -2;
+    }
+#pragma unroll
+    for (int u = 0; u < U1; ++u) {
+      const int v = lab[u] + 1;
+      if (wfn == INT_MAX) {
+        const uint64_t m0 = __ballot(v == 0);
+        if (m0) wfn = lo + (cb + u) * 64 + __builtin_ctzll(m0);
+      }
+      const bool valid = v >= 1;
+      int leader, rank, cm;
+      wave_group(v, valid, lane, leader, rank, cm);
+      if (valid && lane == leader) {
+        const int s = fs_insert(L, v);
+        if (s >= 0) L.cnt[w][s] += (uint32_t)cm;
+      }
+    }
+  }
+  if (lane == 0) L.fnoise[w] = wfn;
+  __syncthreads();
+  if (L.overflow) {
+    if (tid == 0) {
+      nseg_f[f] = 0;
+      atomicExch(overflow, 1);
+    }
+    return;
+  }
+  if (tid == 0 && first_noise) {
+    int m = INT_MAX;
+#pragma unroll
+    for (int q = 0; q < kFsWaves; ++q) m = min(m, L.fnoise[q]);
+    if (m != INT_MAX) first_noise[f] = m;
+  }
+  // scan: two slots per thread; run offsets and segment slots in slot order
+  const int s0 = 2 * tid, s1 = s0 + 1;
+  uint32_t t0 = 0, t1 = 0;
+#pragma unroll
+  for (int q = 0; q < kFsWaves; ++q) {
+    t0 += L.cnt[q][s0];
+    t1 += L.cnt[q][s1];
+  }
+  const uint32_t a = t0 + t1, pcount = (t0 != 0u) + (t1 != 0u);
+  const uint32_t ia = wave_incl_scan(a, lane), ip = wave_incl_scan(pcount, lane);
+  if (lane == 63) {
+    L.wsum[0][w] = ia;
+    L.wsum[1][w] = ip;
+  }
+  __syncthreads();
+  uint32_t pa = 0, pp = 0, ta = 0, tp = 0;
+#pragma unroll
+  for (int q = 0; q < kFsWaves; ++q) {
+    if (q < w) {
+      pa += L.wsum[0][q];
+      pp += L.wsum[1][q];
+    }
+    ta += L.wsum[0][q];
+    tp += L.wsum[1][q];
+  }
+  const uint32_t eo = pa + ia - a, eq = pp + ip - pcount;
+  auto emit = [&](int s, uint32_t t, uint32_t o, uint32_t q) {
+    if (t == 0u) return;
+    L.off[s] = (int)o;
+    tmp_start[lo + q] = lo + (int)o;
+    tmp_len[lo + q] = (int)t;
+    tmp_label[lo + q] = L.keys[s] - 1;
+    uint32_t run = o;
+#pragma unroll
+    for (int r = 0; r < kFsWaves; ++r) {
+      const uint32_t c = L.cnt[r][s];
+      L.cnt[r][s] = run;
+      run += c;
+    }
+  };
+  emit(s0, t0, eo, eq);
+  emit(s1, t1, eo + t0, eq + (t0 != 0u));
+  if (tid == 0) nseg_f[f] = (int)tp;
+  (void)ta;
+  __syncthreads();
+  // pass 2: stable scatter through the per-wave cursors
+  constexpr int U2 = 4;
+  for (int cb = cb0; cb < cb1; cb += U2) {
+    int lab[U2];
+    float px[U2], py[U2], pv[U2];
+#pragma unroll
+    for (int u = 0; u < U2; ++u) {
+      const int i = lo + (cb + u) * 64 + lane;
+      const bool in = cb + u < cb1 && i < hi;
+      lab[u] = in ? labels[i] : -2;
+      px[u] = in ? x[i] : 0.f;
+      py[u] = in ? y[i] : 0.f;
+      pv[u] = in ? inten[i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U2; ++u) {
+      const int i = lo + (cb + u) * 64 + lane;
+      const int v = lab[u] + 1;
+      const bool valid = v >= 1;
+      int leader, rank, cm;
+      wave_group(v, valid, lane, leader, rank, cm);
+      int base = 0;
+      if (valid && lane == leader) {
+        const int s = fs_find(L, v);
+        base = (int)L.cnt[w][s];
+        L.cnt[w][s] = (uint32_t)(base + cm);
+        if (base == L.off[s]) tmp_first[lo + base] = i;
+      }
+      base = __shfl(base, leader < 0 ? lane : leader);
+      if (valid) {
+        const int p = lo + base + rank;
+        gx[p] = px[u];
+        gy[p] = py[u];
+        gi[p] = pv[u];
+      }
+    }
+  }
+}
+
+__global__ void k_seg_total_fix(const int32_t* __restrict__ overflow, int32_t* __restrict__ total) {
+  if (threadIdx.x == 0 && *overflow) *total = -1;
+}
+
+// Frame-local segment lists -> the global frame-major list (one wave per frame).
+__global__ void k_seg_compact(int32_t F, const int32_t* __restrict__ fstart,
+                              const int32_t* __restrict__ nseg_f, const int32_t* __restrict__ base,
+                              const int32_t* __restrict__ tmp_start,
+                              const int32_t* __restrict__ tmp_len,
+                              const int32_t* __restrict__ tmp_label,
+                              const int32_t* __restrict__ tmp_first, int32_t* __restrict__ o_frame,
+                              int32_t* __restrict__ o_label, int64_t* __restrict__ o_count,
+                              int64_t* __restrict__ o_first, int64_t* __restrict__ seg_start) {
+  const int lane = threadIdx.x & 63;
+  const int w0 = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  const int nw = gridDim.x * (blockDim.x / 64);
+  for (int f = w0; f < F; f += nw) {
+    const int lo = fstart[f], m = nseg_f[f], b = base[f];
+    for (int q = lane; q < m; q += 64) {
+      const int s = tmp_start[lo + q];
+      o_frame[b + q] = f;
+      o_label[b + q] = tmp_label[lo + q];
+      o_count[b + q] = tmp_len[lo + q];
+      o_first[b + q] = tmp_first[s];
+      seg_start[b + q] = s;
+    }
+  }
+}
+
 __global__ void k_fill_i64(int64_t* p, int64_t n, int64_t v) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -422,12 +711,63 @@ static int32_t summaries_impl(const int32_t* labels, const float* x, const float
                               int bits, int64_t s_hint, int32_t* o_frame, int32_t* o_label,
                               int64_t* o_count, int64_t* o_first, float* o_cx, float* o_cy,
                               float* o_mi, int64_t* frame_first_noise,
-                              const int32_t** n_seg_dev, hipStream_t st) {
+                              const int32_t** n_seg_dev, bool force_radix, bool* radix_used,
+                              hipStream_t st) {
   if (n >= (int64_t(1) << 31) - 1) {
     set_error("rpt_cluster_summaries: n exceeds the int32 index space");
     return RPT_ENOTSUP;
   }
   Scratch& sc = scratch(st);
+  if (n_frames > 0 && frame_first_noise)
+    hipLaunchKernelGGL(k_fill_i64, dim3(grid_for(n_frames, 256, 64)), dim3(256), 0, st,
+                       frame_first_noise, (int64_t)n_frames, (int64_t)-1);
+  const int64_t sh = std::max<int64_t>(1, std::min<int64_t>(s_hint, n));
+  // per-frame counting sort unless forced off (RPT_K9_RADIX=1, or a redo after a frame held more
+  // than kFsMaxKeys labels) or frames are huge (one 8-wave block per frame)
+  static const bool env_radix = [] {
+    const char* e = std::getenv("RPT_K9_RADIX");
+    return e && e[0] == '1';
+  }();
+  const bool frame_sort = !force_radix && !env_radix && n_frames > 0 && n > 0 &&
+                          n / n_frames <= (int64_t(1) << 20);
+  if (radix_used) *radix_used = !frame_sort;
+  if (frame_sort) {
+    Budget b;
+    for (int k = 0; k < 3; ++k) b.add<float>(n + 1);
+    for (int k = 0; k < 4; ++k) b.add<int32_t>(n + 1);
+    b.add<int64_t>(n + 1);
+    for (int k = 0; k < 3; ++k) b.add<int32_t>((int64_t)n_frames + 1);
+    b.add<int32_t>(1);
+    RPT_TRY(sc.reserve(b.bytes, st));
+    float* gx = sc.carve_n<float>(n + 1);
+    float* gy = sc.carve_n<float>(n + 1);
+    float* gi = sc.carve_n<float>(n + 1);
+    int32_t* tstart = sc.carve_n<int32_t>(n + 1);
+    int32_t* tlen = sc.carve_n<int32_t>(n + 1);
+    int32_t* tlabel = sc.carve_n<int32_t>(n + 1);
+    int32_t* tfirst = sc.carve_n<int32_t>(n + 1);
+    int64_t* seg_start = sc.carve_n<int64_t>(n + 1);
+    int32_t* fstart = sc.carve_n<int32_t>((int64_t)n_frames + 1);
+    int32_t* nseg_f = sc.carve_n<int32_t>((int64_t)n_frames + 1);
+    int32_t* base = sc.carve_n<int32_t>((int64_t)n_frames + 1);
+    int32_t* ovf = sc.carve_n<int32_t>(1);
+    RPT_HIP(hipMemsetAsync(ovf, 0, sizeof(int32_t), st));
+    hipLaunchKernelGGL(k_frame_sort, dim3(n_frames), dim3(kFsWaves * 64), 0, st, labels, pf, n,
+                       x, y, inten, gx, gy, gi, fstart, tstart, tlen, tlabel, tfirst, nseg_f,
+                       frame_first_noise, ovf);
+    RPT_CHECK_LAUNCH();
+    RPT_TRY(exclusive_scan_total_i32(nseg_f, base, n_frames, st));
+    hipLaunchKernelGGL(k_seg_compact, dim3(grid_for(n_frames, 4, 1024)), dim3(256), 0, st,
+                       n_frames, fstart, nseg_f, base, tstart, tlen, tlabel, tfirst, o_frame,
+                       o_label, o_count, o_first, seg_start);
+    hipLaunchKernelGGL(k_seg_total_fix, dim3(1), dim3(64), 0, st, ovf, base + n_frames);
+    hipLaunchKernelGGL(k_summarize<true>, dim3(grid_for(3 * sh, kBlock / 64, 16384)),
+                       dim3(kBlock), 0, st, nullptr, nullptr, seg_start, base + n_frames, n, gx,
+                       gy, gi, pf, o_frame, o_label, o_count, o_first, o_cx, o_cy, o_mi);
+    RPT_CHECK_LAUNCH();
+    *n_seg_dev = base + n_frames;
+    return RPT_OK;
+  }
   Budget b;
   for (int k = 0; k < 4; ++k) b.add<uint32_t>(n + 1);
   b.add<int64_t>(radix_tmp_elems(n));
@@ -447,9 +787,6 @@ static int32_t summaries_impl(const int32_t* labels, const float* x, const float
   float* gx = sc.carve_n<float>(n + 1);
   float* gy = sc.carve_n<float>(n + 1);
   float* gi = sc.carve_n<float>(n + 1);
-  if (n_frames > 0 && frame_first_noise)
-    hipLaunchKernelGGL(k_fill_i64, dim3(grid_for(n_frames, 256, 64)), dim3(256), 0, st,
-                       frame_first_noise, (int64_t)n_frames, (int64_t)-1);
   if (n == 0) {
     RPT_HIP(hipMemsetAsync(pos, 0, sizeof(int32_t), st));
     *n_seg_dev = pos;
@@ -466,8 +803,7 @@ static int32_t summaries_impl(const int32_t* labels, const float* x, const float
   RPT_TRY(exclusive_scan_total_i32(head, pos, n, st));
   hipLaunchKernelGGL(k_seg_starts, dim3(g), dim3(kBlock), 0, st, head, pos, n, seg_start);
   hipLaunchKernelGGL(k_gather_runs, dim3(g), dim3(kBlock), 0, st, sv, n, x, y, inten, gx, gy, gi);
-  const int64_t sh = std::max<int64_t>(1, std::min<int64_t>(s_hint, n));
-  hipLaunchKernelGGL(k_summarize, dim3(grid_for(3 * sh, kBlock / 64, 16384)), dim3(kBlock), 0, st,
+  hipLaunchKernelGGL(k_summarize<false>, dim3(grid_for(3 * sh, kBlock / 64, 16384)), dim3(kBlock), 0, st,
                      sk, sv, seg_start, pos + n, n, gx, gy, gi, pf, o_frame, o_label, o_count,
                      o_first, o_cx, o_cy, o_mi);
   RPT_CHECK_LAUNCH();
@@ -491,32 +827,41 @@ int32_t cluster_summaries(const int32_t* labels, const float* x, const float* y,
     set_error("rpt_cluster_summaries: bad arguments");
     return RPT_EINVAL;
   }
-  // the summarize grid is sized for one wave per run component once the count is known
+  // the summarize grid is sized for one wave per run component once the count is known; a
+  // frame with more than kFsMaxKeys labels sends K9 to the radix path
   const int32_t* nd = nullptr;
-  RPT_TRY(summaries_impl(labels, x, y, inten, pf, n, n_frames, radix_bits_for(n_clusters),
-                         (int64_t)n_clusters * std::max(n_frames, 1) + 1, o_frame, o_label,
-                         o_count, o_first, o_cx, o_cy, o_mi, frame_first_noise, &nd, st));
   int32_t n_seg = 0;
-  RPT_HIP(hipMemcpyAsync(&n_seg, nd, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-  RPT_TRY(wait_stream(st));
+  for (int pass = 0; pass < 2; ++pass) {
+    RPT_TRY(summaries_impl(labels, x, y, inten, pf, n, n_frames, radix_bits_for(n_clusters),
+                           (int64_t)n_clusters * std::max(n_frames, 1) + 1, o_frame, o_label,
+                           o_count, o_first, o_cx, o_cy, o_mi, frame_first_noise, &nd, pass == 1,
+                           nullptr, st));
+    RPT_HIP(hipMemcpyAsync(&n_seg, nd, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    RPT_TRY(wait_stream(st));
+    if (n_seg >= 0) break;
+  }
   *n_seg_host = n_seg;
   return RPT_OK;
 }
 
 // No readback: the caller passes the radix bits and a segment-count estimate, and reads the
-// count (*n_seg_dev) with its other results after one sync.
+// count (*n_seg_dev) with its other results after one sync.  A count of -1 means a frame held
+// more labels than the frame sort takes: redo with force_radix.  *radix_used tells whether the
+// label bits mattered (radix path) — the frame sort takes any labels.
 int32_t cluster_summaries_dev(const int32_t* labels, const float* x, const float* y,
                               const float* inten, const int32_t* pf, int64_t n, int32_t n_frames,
                               int bits, int64_t s_hint, int32_t* o_frame, int32_t* o_label,
                               int64_t* o_count, int64_t* o_first, float* o_cx, float* o_cy,
                               float* o_mi, int64_t* frame_first_noise,
-                              const int32_t** n_seg_dev, hipStream_t st) {
+                              const int32_t** n_seg_dev, bool force_radix, bool* radix_used,
+                              hipStream_t st) {
   if (n < 0 || n_frames < 0 || bits < 1 || bits > 32 || !n_seg_dev) {
     set_error("cluster_summaries_dev: bad arguments");
     return RPT_EINVAL;
   }
   return summaries_impl(labels, x, y, inten, pf, n, n_frames, bits, s_hint, o_frame, o_label,
-                        o_count, o_first, o_cx, o_cy, o_mi, frame_first_noise, n_seg_dev, st);
+                        o_count, o_first, o_cx, o_cy, o_mi, frame_first_noise, n_seg_dev,
+                        force_radix, radix_used, st);
 }
 
 // Per-label pandas group means (count, x, y, intensity) of labels in [0, n_labels); labels

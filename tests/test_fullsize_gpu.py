@@ -108,6 +108,34 @@ def test_dense_stack_config4_density(gpu):
     assert res.n_points > 4 * 350_000
 
 
+@pytest.mark.timeout(600)
+def test_first_run_with_more_clusters_than_guessed(gpu):
+    """A fresh driver guesses 12 label bits for K9; a 1000-frame stack has > 4,096 clusters, so
+    the first run redoes K9 (whose segment count then changes) and re-reads the segments.  The
+    first run must equal the second (no redo) and account for every clustered point."""
+    from rpt.synth import DeviceSynth, SynthConfig
+
+    cfg = SynthConfig(n_frames=1000)
+    ds = DeviceSynth(cfg, gpu)
+    echo = ds.echo()
+    pipe = _pipe(cfg, ds, gpu)
+    r1 = pipe.run(echo, keep_points=True).finish()
+    lab = r1.labels.cpu().numpy()
+    pf = r1.points["frame"].cpu().numpy()
+    r2 = pipe.run(echo).finish()
+    assert r1.n_clusters > 4096 and r1.n_clusters == r2.n_clusters
+    assert r1.n_segments == r2.n_segments == len(r1.seg["frame"])
+    k1 = np.lexsort((r1.seg["label"], r1.seg["frame"]))
+    k2 = np.lexsort((r2.seg["label"], r2.seg["frame"]))
+    for key in r1.seg:
+        np.testing.assert_array_equal(r1.seg[key][k1], r2.seg[key][k2], err_msg=key)
+    assert r1.seg["count"].sum() == (lab >= 0).sum()
+    keys = pf[lab >= 0].astype(np.int64) << 32 | lab[lab >= 0].astype(np.int64)
+    assert len(np.unique(keys)) == r1.n_segments
+    np.testing.assert_array_equal(r1.frame_order_offsets, r2.frame_order_offsets)
+    assert len(r1.tracker.objects()) == len(r2.tracker.objects())
+
+
 # ------------------------------------------------------------------ stack-driver edge cases
 def _edge_synth(n_frames):
     from rpt.synth import SynthConfig

@@ -3,6 +3,8 @@ pinned oracle: K1 polar scatter + fusion, synthetic echo, land filter, cluster s
 reference cluster order, and the whole stack -> tracker path."""
 from __future__ import annotations
 
+import sys
+
 import numpy as np
 import pytest
 import torch
@@ -321,6 +323,73 @@ def test_mean_intensity_pairwise_chunks(gpu):
         c = np.mean(p[m][:, :2], axis=0)
         assert seg["cx"][s] == c[0] and seg["cy"][s] == c[1]
         assert float(seg["mi"][s]) == float(np.mean(p[m][:, 2]))
+
+
+def _radix_summaries_in_child(frames, lab, ncl):
+    """_summaries_device in a child process with RPT_K9_RADIX=1 (read once per process)."""
+    import os
+    import subprocess
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as d:
+        np.savez(os.path.join(d, "in.npz"), lab=lab, ncl=ncl,
+                 **{f"p{k}": p for k, (_, p, _) in enumerate(frames)})
+        code = (
+            "import sys, numpy as np, torch\n"
+            f"sys.path[:0] = {sys.path!r}\n"
+            "from test_path_gpu import _summaries_device\n"
+            f"g = np.load({os.path.join(d, 'in.npz')!r})\n"
+            f"frames = [(k, g[f'p{{k}}'], None) for k in range({len(frames)})]\n"
+            "seg, fo, order = _summaries_device(torch.device('cuda:0'), frames, g['lab'],"
+            " int(g['ncl']))\n"
+            f"np.savez({os.path.join(d, 'out.npz')!r}, fo=fo, order=order,"
+            " **{'s_' + k: v for k, v in seg.items()})\n")
+        env = dict(os.environ, RPT_K9_RADIX="1")
+        subprocess.run([sys.executable, "-c", code], check=True, env=env, timeout=240,
+                       cwd=os.path.dirname(os.path.abspath(__file__)))
+        o = np.load(os.path.join(d, "out.npz"))
+        seg = {k[2:]: o[k] for k in o.files if k.startswith("s_")}
+        return seg, o["fo"], o["order"]
+
+
+@pytest.mark.parametrize("crowded", [False, True])
+def test_summaries_frame_sort_matches_radix_path(gpu, crowded):
+    """K9's per-frame counting sort and its radix path (RPT_K9_RADIX=1, in a child process) give
+    the same segments — frame-major vs label-major — on frames of ragged sizes, empty frames,
+    noise-only frames and runs interleaved point by point; `crowded` adds a frame with more
+    labels than the frame sort takes (the sync entry point then redoes K9 on the radix path)."""
+    rng = np.random.default_rng(21)
+    sizes = [0, 1, 63, 64, 65, 3000, 0, 517, 20000, 5, 0] + ([6000] if crowded else [])
+    frames = []
+    labs = []
+    for k, m in enumerate(sizes):
+        p = np.column_stack([rng.normal(0, 50, m), rng.normal(0, 50, m),
+                             rng.integers(0, 255, m)]).astype(np.float32)
+        lab = rng.integers(-1, 3000 if k == 11 else 40 + k, m).astype(np.int32)
+        if k == 9:
+            lab[:] = -1
+        frames.append((k, p, None))
+        labs.append(lab)
+    lab = np.concatenate(labs)
+    ncl = int(lab.max()) + 1
+    a = _summaries_device(gpu, frames, lab, ncl)
+    b = _radix_summaries_in_child(frames, lab, ncl)
+    ka = np.lexsort((a[0]["label"], a[0]["frame"]))
+    kb = np.lexsort((b[0]["label"], b[0]["frame"]))
+    assert np.all(np.diff(a[0]["frame"]) >= 0) != crowded  # frame-major unless redone
+    for key in a[0]:
+        np.testing.assert_array_equal(a[0][key][ka], b[0][key][kb], err_msg=key)
+    np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(a[0]["label"][a[2]], b[0]["label"][b[2]])
+    pf = np.concatenate([np.full(m, k, np.int32) for k, m in enumerate(sizes)])
+    pts = np.vstack([p for _, p, _ in frames])
+    for s in range(len(a[0]["label"])):
+        m = (pf == a[0]["frame"][s]) & (lab == a[0]["label"][s])
+        assert a[0]["count"][s] == m.sum()
+        assert a[0]["first"][s] == np.nonzero(m)[0][0]
+        c = np.mean(pts[m][:, :2], axis=0)
+        assert a[0]["cx"][s] == c[0] and a[0]["cy"][s] == c[1]
+    assert len(a[0]["label"]) == len({(f, l) for f, l in zip(pf, lab) if l >= 0})
 
 
 @pytest.mark.parametrize("n_frames,land", [(6, True), (14, True), (14, False)])
