@@ -229,6 +229,10 @@ struct Geom {
   double eps2;            // eps_space^2 (float64)
   float epst;             // float32(eps_time)
   int min_samples;
+  // float32 box-bound screen (classify_cells<D, true>): a float32 squared box distance <= e2lo
+  // (> e2hi) is <= (>) eps2 in the float64 bound too (margins 1e-5 >> the float32 rounding);
+  // e2lo = -1 / e2hi = inf disable it (eps2 outside [1e-20, 1e30])
+  float e2lo, e2hi;
 };
 
 __device__ __forceinline__ int cell_of(double v, double o, double cs, int n) {
@@ -620,6 +624,7 @@ __global__ __launch_bounds__(kBlock) void k_slab_range(const CellRec<D>* __restr
 }
 
 // ---------------------------------------------------------------- neighbour predicates
+
 // Exact pair test (see file header).
 template <int D>
 __device__ __forceinline__ bool adjacent(const float4& a, const float4& b, const Geom& g) {
@@ -882,7 +887,9 @@ __device__ __forceinline__ float4 shfl_f4(const float4& v, int l) {
 
 // Box-box classification of two cells with the pair test's rounding (monotone bounds):
 // 0 no pair can be adjacent, 1 every pair is adjacent, 2 undecided.
-template <int D>
+// SCREEN: float32 bounds first, float64 only near the threshold (Geom::e2lo / e2hi) -- faster
+// in the K5 cell pass; the union kernels measured slower with it (their loops schedule worse).
+template <int D, bool SCREEN = false>
 __device__ __forceinline__ int classify_cells(const float4& A1, const float4& B1,
                                               const float4& A2, const float4& B2,
                                               const Geom& g) {
@@ -895,6 +902,16 @@ __device__ __forceinline__ int classify_cells(const float4& A1, const float4& B1
   const float tg = gap(A2.z, A2.w, B2.z, B2.w);
   if (!(tg <= g.epst)) return 0;
   const float tm = fmaxf(fabsf(B2.w - A2.z), fabsf(A2.w - B2.z));
+  if (D == 2 && SCREEN) {
+    const float fx = gap(A1.x, A1.y, B1.x, B1.y), fy = gap(A1.z, A1.w, B1.z, B1.w);
+    const float fmn = fx * fx + fy * fy;
+    const float ux = fmaxf(fabsf(B1.y - A1.x), fabsf(A1.y - B1.x));
+    const float uy = fmaxf(fabsf(B1.w - A1.z), fabsf(A1.w - B1.z));
+    const float fmx = ux * ux + uy * uy;
+    if (fmn > g.e2hi) return 0;
+    if (fmx <= g.e2lo) return (tm <= g.epst) ? 1 : 2;
+    if (fmn <= g.e2lo && fmx > g.e2hi) return 2;
+  }
   const double gx = gapd(A1.x, A1.y, B1.x, B1.y), gy = gapd(A1.z, A1.w, B1.z, B1.w);
   double dmin = gx * gx + gy * gy;
   const double mx = fmax(fabs((double)B1.y - (double)A1.x), fabs((double)A1.y - (double)B1.x));
@@ -908,6 +925,19 @@ __device__ __forceinline__ int classify_cells(const float4& A1, const float4& B1
   }
   if (!(dmin <= g.eps2)) return 0;
   return (dmax <= g.eps2 && tm <= g.epst) ? 1 : 2;
+}
+
+struct XcdRange {
+  int64_t first, step, end;
+};
+__device__ __forceinline__ XcdRange xcd_items(int64_t n_items, bool remap) {
+  const int64_t wpb = kBlock / 64, wave = threadIdx.x / 64;
+  if (!remap || (gridDim.x & 7)) {
+    return XcdRange{(int64_t)blockIdx.x * wpb + wave, (int64_t)gridDim.x * wpb, n_items};
+  }
+  const int64_t x = blockIdx.x & 7, lb = blockIdx.x >> 3, nbx = gridDim.x >> 3;
+  const int64_t lo = n_items * x / 8, hi = n_items * (x + 1) / 8;
+  return XcdRange{lo + lb * wpb + wave, nbx * wpb, hi};
 }
 
 // ---------------------------------------------------------------- K5: core flags
@@ -1035,17 +1065,22 @@ __global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
                                                           const float2* __restrict__ slab_t,
                                                           int32_t* __restrict__ cflag,
                                                           int32_t* __restrict__ zero_counter,
-                                                          uint8_t* __restrict__ core) {
+                                                          uint8_t* __restrict__ core, int exp) {
   // legacy pipeline: the level-4 queue counter, zeroed here instead of by a memset launch
   // (k_core_fill, the next kernel on the stream, is its first user)
   if (zero_counter && blockIdx.x == 0 && threadIdx.x == 0) *zero_counter = 0;
   const int64_t no = *n_occ;
   const int need = g.min_samples;
   const int j = threadIdx.x & 7;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t - j < no * 8;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t q = t >> 3;
-    const bool act = q < no;
+  // XCD-aware cell ranges (grid a multiple of 8): blocks sharing an XCD take one contiguous
+  // eighth of the (slab-major) occupied cells, so the neighbouring slabs' records they read stay
+  // in that XCD's L2 instead of being fetched by all eight
+  const int64_t cpb = blockDim.x / 8;
+  const int64_t xg = blockIdx.x & 7, nbx = gridDim.x >> 3;
+  const int64_t qlo = no * xg / 8, qhi = no * (xg + 1) / 8;
+  for (int64_t q0 = qlo + (int64_t)(blockIdx.x >> 3) * cpb; q0 < qhi; q0 += nbx * cpb) {
+    const int64_t q = q0 + threadIdx.x / 8;
+    const bool act = q < qhi;
     const int32_t ca = act ? occ[q] : 0;
     int flag = 0, b = 0, e = 0;
     if (act && (int64_t)ca >= g.cells) {  // non-finite time: no neighbours at all
@@ -1087,18 +1122,25 @@ __global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
           m5[dy] = m;
         }
       }
+      const float gap =
+          (own.x > sr.y) ? (own.x - sr.y) : ((sr.x > own.y) ? (sr.x - own.y) : 0.f);
+      const bool reach = sv && sr.x <= sr.y && gap <= g.epst;  // this lane's slab is in reach
       if (need <= 0 || (mu && e - b >= need)) {
         flag = 1;
+      } else if (exp) {  // timing experiment only (RPT_K5_EXP): flags are WRONG
+        flag = 2;
       } else {
         int lo = 0, hi = 0;
-        const float gap =
-            (own.x > sr.y) ? (own.x - sr.y) : ((sr.x > own.y) ? (sr.x - own.y) : 0.f);
-        if (sv && sr.x <= sr.y && gap <= g.epst) {  // this lane's slab is in reach
-          const float4 A1 = rec_boxA<2>(ra), A2 = rec_boxB(ra);
+        const float4 A1 = rec_boxA<2>(ra), A2 = rec_boxB(ra);
+        // rows nearest first (the cell's own row, then +-1, then +-2); the eight lanes stop as
+        // soon as the adjacent-to-every-point count reaches min_samples (most cells: after the
+        // own row), saving the outer rows' record round trips
+        bool decided = false;
 #pragma unroll
-          for (int dy = 0; dy < 5; ++dy) {
-            const uint32_t m = m5[dy];
-            if (!m) continue;
+        for (int k = 0; k < 5; ++k) {
+          const int dy = (k == 0) ? 2 : ((k & 1) ? 2 - (k + 1) / 2 : 2 + k / 2);
+          const uint32_t m = reach ? m5[dy] : 0u;
+          if (m) {
             const int64_t row = ((int64_t)sl * g.ny + (cy + dy - 2)) * g.nx + (cx - 2);
             // the row's (up to 5) candidate records in flight together, then classified
             CellRec<2> cr[5];
@@ -1108,18 +1150,32 @@ __global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
 #pragma unroll
             for (int dx = 0; dx < 5; ++dx) {
               if (!((m >> dx) & 1u)) continue;
-              const int cls = classify_cells<2>(A1, rec_boxA<2>(cr[dx]), A2, rec_boxB(cr[dx]), g);
+              const int cls =
+                  classify_cells<2, true>(A1, rec_boxA<2>(cr[dx]), A2, rec_boxB(cr[dx]), g);
               lo += (cls == 1) ? cr[dx].e - cr[dx].b : 0;
               hi += (cls != 0) ? cr[dx].e - cr[dx].b : 0;
             }
           }
-        }
+          if (k == 0 || k == 2) {
+            int ls = lo;
 #pragma unroll
-        for (int off = 4; off > 0; off >>= 1) {
-          lo += __shfl_xor(lo, off, 8);
-          hi += __shfl_xor(hi, off, 8);
+            for (int off = 4; off > 0; off >>= 1) ls += __shfl_xor(ls, off, 8);
+            if (ls >= need) {
+              decided = true;
+              break;
+            }
+          }
         }
-        flag = (lo >= need) ? 1 : ((hi < need) ? 0 : 2);
+        if (decided) {
+          flag = 1;
+        } else {
+#pragma unroll
+          for (int off = 4; off > 0; off >>= 1) {
+            lo += __shfl_xor(lo, off, 8);
+            hi += __shfl_xor(hi, off, 8);
+          }
+          flag = (lo >= need) ? 1 : ((hi < need) ? 0 : 2);
+        }
       }
     }
     if (act && j == 0) cflag[ca] = flag;
@@ -1174,11 +1230,10 @@ __global__ __launch_bounds__(kBlock) void k_core_slow(const float4* __restrict__
                                                      const int32_t* __restrict__ n_slow,
                                                      uint8_t* __restrict__ core) {
   const int lane = threadIdx.x & 63;
-  const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
-  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
-  const int64_t ns = *n_slow;
   const int need = g.min_samples;
-  for (int64_t q = w0; q < ns; q += nw) {
+  // XCD-aware ranges of the (cell-ordered) queue: neighbouring points' windows share an L2
+  const XcdRange xr = xcd_items(*n_slow, true);
+  for (int64_t q = xr.first; q < xr.end; q += xr.step) {
     const int s = slow[q];
     const int32_t key = skey[s];
     const float4 p = pts[s];
@@ -1466,19 +1521,6 @@ __device__ __forceinline__ void uf_unite(int32_t* parent, const int32_t* __restr
 // compresses afterwards); bit 2 = timing experiment only: skip the box-certain unites (labels
 // are then WRONG); bit 1 = XCD-aware item ranges (blockIdx % 8 = XCD under round-robin
 // placement: each XCD unions a contiguous range of cells, so its L2 keeps their parents).
-struct XcdRange {
-  int64_t first, step, end;
-};
-__device__ __forceinline__ XcdRange xcd_items(int64_t n_items, bool remap) {
-  const int64_t wpb = kBlock / 64, wave = threadIdx.x / 64;
-  if (!remap || (gridDim.x & 7)) {
-    return XcdRange{(int64_t)blockIdx.x * wpb + wave, (int64_t)gridDim.x * wpb, n_items};
-  }
-  const int64_t x = blockIdx.x & 7, lb = blockIdx.x >> 3, nbx = gridDim.x >> 3;
-  const int64_t lo = n_items * x / 8, hi = n_items * (x + 1) / 8;
-  return XcdRange{lo + lb * wpb + wave, nbx * wpb, hi};
-}
-
 // Star initialisation: every core point of a mutual cell hangs under the cell's core point of
 // minimum original index (k_rep), other points are roots.
 __global__ __launch_bounds__(kBlock) void k_parent_init(int32_t* parent, int64_t n,
@@ -1793,10 +1835,9 @@ __global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts
                                                  const int32_t* __restrict__ nc_count,
                                                  int32_t* __restrict__ labels) {
   const int lane = threadIdx.x & 63;
-  const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
-  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
-  const int64_t nq = *nc_count;
-  for (int64_t q = w0; q < nq; q += nw) {
+  // XCD-aware ranges of the (cell-ordered) queue: neighbouring points' windows share an L2
+  const XcdRange xr = xcd_items(*nc_count, true);
+  for (int64_t q = xr.first; q < xr.end; q += xr.step) {
     const int s = nc_list[q];
     const int32_t key = skey[s];
     int best = INT_MAX;
@@ -2246,6 +2287,7 @@ struct DbscanState {
   int uf_flags = -1;                         // see XcdRange; -1 = read RPT_UF_FLAGS once
   int k5_legacy = -1;                        // 1: round-1 K5 (fill + point queue); RPT_K5_MODE
   int k5_fill = 0;
+  int k5_exp = 0;                            // timing experiments only (RPT_K5_EXP)
   int bucket_mode = -1;                      // RPT_K4_BUCKET (default 1): slab-bucket K4
   template <int D>
   const CellRec<D>* rec() const {
@@ -2313,6 +2355,13 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   g = Geom{};
   g.eps2 = eps_space * eps_space;
   g.epst = epst;
+  static const bool screen_on = [] {
+    const char* e = std::getenv("RPT_F32_SCREEN");
+    return !(e && e[0] == '0');
+  }();
+  const bool screen = screen_on && g.eps2 >= 1e-20 && g.eps2 <= 1e30;
+  g.e2lo = screen ? (float)(g.eps2 * (1.0 - 1e-5)) : -1.0f;
+  g.e2hi = screen ? (float)(g.eps2 * (1.0 + 1e-5)) : INFINITY;
   g.min_samples = min_samples;
   double lo[4], hi[4];
   for (int k = 0; k < 4; ++k) {
@@ -2488,6 +2537,8 @@ int32_t DbscanState::core_pass(hipStream_t st) {
     // default 0: the folded variants measured no faster on the 100- and 1000-frame stacks
     // (profiles/r2/ab_k5_k1.md): the per-point flag writes moved into the cell kernel cost what
     // the fill pass cost, and the cell-wise slow pass balances worse than the point queue
+    const char* x = std::getenv("RPT_K5_EXP");
+    k5_exp = x ? std::atoi(x) : 0;
     const char* e = std::getenv("RPT_K5_MODE");
     k5_legacy = e ? std::atoi(e) : 0;
     k5_legacy = (k5_legacy == 0) ? 1 : 0;
@@ -2500,9 +2551,9 @@ int32_t DbscanState::core_pass(hipStream_t st) {
     // cells decide (and write their points' flags) in one pass; the undecided cells' points are
     // settled by k_core_slow_cells, which walks the occupied cells itself (no queue, no fill)
     if (oct) {
-      hipLaunchKernelGGL(k_core_cells_oct, dim3(grid_for(8 * n, kBlock, 8192)), dim3(kBlock), 0,
+      hipLaunchKernelGGL(k_core_cells_oct, dim3((grid_for(8 * n, kBlock, 8192) + 7) & ~7), dim3(kBlock), 0,
                          st, g, (int)rs, occ, n_occ, rec<2>(), mutual, occ_bits, slab_t, cflag,
-                         (int32_t*)nullptr, k5_fill ? (uint8_t*)nullptr : core);
+                         (int32_t*)nullptr, k5_fill ? (uint8_t*)nullptr : core, k5_exp);
       if (k5_fill)
         hipLaunchKernelGGL(k_core_fill<false>, dim3(tile_grid(n)), dim3(kBlock), 0, st, skey, n,
                            cflag, core, slow, n_slow);
@@ -2531,9 +2582,9 @@ int32_t DbscanState::core_pass(hipStream_t st) {
     return RPT_OK;
   }
   if (oct) {
-    hipLaunchKernelGGL(k_core_cells_oct, dim3(grid_for(8 * n, kBlock, 8192)), dim3(kBlock), 0,
+    hipLaunchKernelGGL(k_core_cells_oct, dim3((grid_for(8 * n, kBlock, 8192) + 7) & ~7), dim3(kBlock), 0,
                        st, g, (int)rs, occ, n_occ, rec<2>(), mutual, occ_bits, slab_t, cflag,
-                       n_slow, (uint8_t*)nullptr);
+                       n_slow, (uint8_t*)nullptr, k5_exp);
   } else {
     RPT_HIP(hipMemsetAsync(n_slow, 0, sizeof(int32_t), st));
     RPT_HIP(hipMemsetAsync(n_cq, 0, sizeof(int32_t), st));
