@@ -108,6 +108,17 @@ int32_t exclusive_scan_total_i32(const int32_t* in, int32_t* out, int64_t n, hip
 
 // Back-to-back copy of up to kPackMax device arrays (sizes in 4-byte words) into dst.
 constexpr int kPackMax = 10;
+// Point-set bounds of the ST-DBSCAN grid build (k_bounds in stdbscan.hip; also produced by the
+// fused land compaction, land.hip): ordered-u32 (sign-flipped float bits) minima / maxima.
+struct Bounds {
+  uint32_t mn[4];   // ordered-u32 minima of x, y, z, t (t over finite values only)
+  uint32_t mx[4];
+  int32_t nonfinite_xyz;  // any NaN/inf coordinate
+  int32_t nonintegral_t;  // any finite t with t != floor(t) or |t| >= 2^24
+  int32_t n_finite_t;
+  int32_t t_descends;     // some t[i] < t[i-1]: the points are not in time order
+};
+
 struct PackList {
   const uint32_t* src[kPackMax];
   int64_t off[kPackMax + 1];  // word offsets in dst, off[0] = 0

@@ -7,6 +7,7 @@
 // edge array staged in LDS, so no floating-point re-derivation of the edges can disagree.
 // Counts are int32 atomics (order-free); intensity sums are float64 atomics, exact for the
 // integer echo values of the radar path (sums < 2^53), like np.add.at's sequential order.
+#include <climits>
 #include <cstring>
 
 #include <algorithm>
@@ -291,6 +292,233 @@ __global__ void k_new_offsets(const int32_t* __restrict__ pos, const int64_t* __
     out[f] = pos[off[f]];
 }
 
+
+// ---- fused compaction of the stack driver (filter_land_from_frame, :426-436, over the stack) --
+// Tiles of kCompTile points; item k of thread t is point tile*kCompTile + k*kCompBlock + t, so
+// loads and (kept-order) stores are coalesced.  Pass 1 counts each tile's kept points (cell not
+// land) from the cells the grid pass stored; after a scan of the tile counts, pass 2 recomputes
+// the flags, ranks them (ballots + a 64-entry scan of the per-(item, wave) counts) and writes the
+// kept points in order with their times (float32 frame slots, :460-467) and a per-tile partial of
+// the ST-DBSCAN bounds -- the keep / position arrays, their full-length scan, the frame-time
+// pass and the bounds pass of the separate kernels are gone.
+constexpr int kCompBlock = 256, kCompItems = 16, kCompTile = kCompBlock * kCompItems;
+
+struct BoundsPart {
+  uint32_t mnx, mxx, mny, mxy;
+  int32_t mnf, mxf, flags, pad;  // flags: 1 non-finite x/y, 2 frame slots descend
+};
+
+__device__ __forceinline__ bool kept_at(const int32_t* __restrict__ cell,
+                                        const uint8_t* __restrict__ land, int64_t i, int64_t n) {
+  return i < n && !land[cell[i]];
+}
+
+__global__ __launch_bounds__(kCompBlock) void k_land_tile_counts(const int32_t* __restrict__ cell,
+                                                                int64_t n,
+                                                                const uint8_t* __restrict__ land,
+                                                                int32_t* __restrict__ tile_cnt) {
+  const int64_t i0 = (int64_t)blockIdx.x * kCompTile + threadIdx.x;
+  int32_t cl[kCompItems];
+#pragma unroll
+  for (int k = 0; k < kCompItems; ++k) {
+    const int64_t i = i0 + (int64_t)k * kCompBlock;
+    cl[k] = (i < n) ? cell[i] : -1;
+  }
+  int c = 0;
+#pragma unroll
+  for (int k = 0; k < kCompItems; ++k) c += (cl[k] >= 0 && !land[cl[k]]) ? 1 : 0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+  __shared__ int ws[kCompBlock / 64];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x / 64] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+#pragma unroll
+    for (int w = 0; w < kCompBlock / 64; ++w) t += ws[w];
+    tile_cnt[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(kCompBlock) void k_land_compact(
+    const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ v,
+    const int32_t* __restrict__ g, const int32_t* __restrict__ pf, int64_t n,
+    const int32_t* __restrict__ cell, const uint8_t* __restrict__ land,
+    const int32_t* __restrict__ tile_base, float* __restrict__ xo, float* __restrict__ yo,
+    float* __restrict__ vo, int32_t* __restrict__ go, int32_t* __restrict__ pfo,
+    float* __restrict__ to, BoundsPart* __restrict__ part) {
+  constexpr int NW = kCompBlock / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x / 64;
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const int64_t i0 = (int64_t)blockIdx.x * kCompTile + threadIdx.x;
+  int32_t cl[kCompItems];
+#pragma unroll
+  for (int k = 0; k < kCompItems; ++k) {
+    const int64_t i = i0 + (int64_t)k * kCompBlock;
+    cl[k] = (i < n) ? cell[i] : -1;
+  }
+  uint32_t km = 0;
+#pragma unroll
+  for (int k = 0; k < kCompItems; ++k) km |= (cl[k] >= 0 && !land[cl[k]]) ? (1u << k) : 0u;
+  __shared__ int cw[kCompItems * NW];  // per (item k, wave) counts, then their exclusive scan
+#pragma unroll
+  for (int k = 0; k < kCompItems; ++k) {
+    const uint64_t bk = __ballot((km >> k) & 1u);
+    if (lane == 0) cw[k * NW + w] = __popcll(bk);
+  }
+  __syncthreads();
+  static_assert(kCompItems * NW == 64, "one wave scans the per-(item, wave) counts");
+  if (w == 0) {
+    const int c = cw[lane];
+    int incl = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int o = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += o;
+    }
+    cw[lane] = incl - c;
+  }
+  __syncthreads();
+  const int64_t tb = tile_base[blockIdx.x];
+  uint32_t mnx = 0xffffffffu, mxx = 0u, mny = 0xffffffffu, mxy = 0u;
+  int mnf = INT_MAX, mxf = INT_MIN, flags = 0;
+#pragma unroll 4
+  for (int k = 0; k < kCompItems; ++k) {
+    const int64_t i = i0 + (int64_t)k * kCompBlock;
+    const bool kp = (km >> k) & 1u;
+    const uint64_t bk = __ballot(kp);
+    if (i < n) {
+      const int f = pf[i];
+      // input order; the kept points descend only if the input does
+      if (i > 0 && f < pf[i - 1]) flags |= 2;
+      if (kp) {
+        const int64_t o = tb + cw[k * NW + w] + __popcll(bk & lt);
+        const float px = x[i], py = y[i];
+        xo[o] = px;
+        yo[o] = py;
+        vo[o] = v[i];
+        if (go) go[o] = g[i];
+        pfo[o] = f;
+        to[o] = (float)f;
+        if (!isfinite(px) || !isfinite(py)) flags |= 1;
+        const uint32_t a = f2ord(px), b = f2ord(py);
+        mnx = min(mnx, a);
+        mxx = max(mxx, a);
+        mny = min(mny, b);
+        mxy = max(mxy, b);
+        mnf = min(mnf, f);
+        mxf = max(mxf, f);
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    mnx = min(mnx, (uint32_t)__shfl_xor((int)mnx, off));
+    mxx = max(mxx, (uint32_t)__shfl_xor((int)mxx, off));
+    mny = min(mny, (uint32_t)__shfl_xor((int)mny, off));
+    mxy = max(mxy, (uint32_t)__shfl_xor((int)mxy, off));
+    mnf = min(mnf, __shfl_xor(mnf, off));
+    mxf = max(mxf, __shfl_xor(mxf, off));
+    flags |= __shfl_xor(flags, off);
+  }
+  __shared__ BoundsPart wp[NW];
+  if (lane == 0) wp[w] = BoundsPart{mnx, mxx, mny, mxy, mnf, mxf, flags, 0};
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    BoundsPart r = wp[0];
+    for (int q = 1; q < NW; ++q) {
+      r.mnx = min(r.mnx, wp[q].mnx);
+      r.mxx = max(r.mxx, wp[q].mxx);
+      r.mny = min(r.mny, wp[q].mny);
+      r.mxy = max(r.mxy, wp[q].mxy);
+      r.mnf = min(r.mnf, wp[q].mnf);
+      r.mxf = max(r.mxf, wp[q].mxf);
+      r.flags |= wp[q].flags;
+    }
+    part[blockIdx.x] = r;
+  }
+}
+
+// new_off[f] = first kept point of frame slot >= f (the kept frame slots ascend), new_off[F] =
+// kept count: one binary search per frame slot
+__global__ void k_land_new_off(const int32_t* __restrict__ n_kept_dev,
+                               const int32_t* __restrict__ pfo, int n_frames,
+                               int64_t* __restrict__ new_off) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f > n_frames) return;
+  const int64_t nk = *n_kept_dev;
+  int64_t lo = 0, hi = nk;
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (pfo[m] < f)
+      lo = m + 1;
+    else
+      hi = m;
+  }
+  new_off[f] = (f == n_frames) ? nk : lo;
+}
+
+// the tiles' partials -> Bounds (what k_bounds<2> gives for the kept points with t = frame
+// slot: z = 0, every t finite and integral below 2^24)
+__global__ __launch_bounds__(kBlock) void k_land_compact_final(
+    const BoundsPart* __restrict__ part, int nt, const int32_t* __restrict__ n_kept_dev,
+    Bounds* __restrict__ out) {
+  const int64_t nk = *n_kept_dev;
+  uint32_t mnx = 0xffffffffu, mxx = 0u, mny = 0xffffffffu, mxy = 0u;
+  int mnf = INT_MAX, mxf = INT_MIN, flags = 0;
+  for (int b = threadIdx.x; b < nt; b += blockDim.x) {
+    const BoundsPart p = part[b];
+    mnx = min(mnx, p.mnx);
+    mxx = max(mxx, p.mxx);
+    mny = min(mny, p.mny);
+    mxy = max(mxy, p.mxy);
+    mnf = min(mnf, p.mnf);
+    mxf = max(mxf, p.mxf);
+    flags |= p.flags;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    mnx = min(mnx, (uint32_t)__shfl_xor((int)mnx, off));
+    mxx = max(mxx, (uint32_t)__shfl_xor((int)mxx, off));
+    mny = min(mny, (uint32_t)__shfl_xor((int)mny, off));
+    mxy = max(mxy, (uint32_t)__shfl_xor((int)mxy, off));
+    mnf = min(mnf, __shfl_xor(mnf, off));
+    mxf = max(mxf, __shfl_xor(mxf, off));
+    flags |= __shfl_xor(flags, off);
+  }
+  __shared__ BoundsPart wp[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) wp[threadIdx.x / 64] = BoundsPart{mnx, mxx, mny, mxy, mnf, mxf, flags, 0};
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    BoundsPart r = wp[0];
+    for (int q = 1; q < kBlock / 64; ++q) {
+      r.mnx = min(r.mnx, wp[q].mnx);
+      r.mxx = max(r.mxx, wp[q].mxx);
+      r.mny = min(r.mny, wp[q].mny);
+      r.mxy = max(r.mxy, wp[q].mxy);
+      r.mnf = min(r.mnf, wp[q].mnf);
+      r.mxf = max(r.mxf, wp[q].mxf);
+      r.flags |= wp[q].flags;
+    }
+    Bounds b;
+    const uint32_t z = f2ord(0.f);
+    const bool any = nk > 0;
+    b.mn[0] = r.mnx;
+    b.mx[0] = r.mxx;
+    b.mn[1] = r.mny;
+    b.mx[1] = r.mxy;
+    b.mn[2] = any ? z : 0xffffffffu;
+    b.mx[2] = any ? z : 0u;
+    b.mn[3] = any ? f2ord((float)r.mnf) : 0xffffffffu;
+    b.mx[3] = any ? f2ord((float)r.mxf) : 0u;
+    b.nonfinite_xyz = (r.flags & 1) ? 1 : 0;
+    b.nonintegral_t = (any && (r.mxf >= 16777216 || r.mnf <= -16777216)) ? 1 : 0;
+    b.n_finite_t = (int32_t)nk;
+    b.t_descends = (r.flags & 2) ? 1 : 0;
+    *out = b;
+  }
+}
+
 }  // namespace
 
 int32_t bounds_xy(const float* x, const float* y, int64_t n, float* out4, hipStream_t st) {
@@ -437,6 +665,44 @@ int32_t land_filter_cells(const float* x, const float* y, const float* v, const 
     RPT_TRY(wait_stream(st));
     *n_kept_host = k;
   }
+  return RPT_OK;
+}
+
+// The stack driver's land compaction (see k_land_compact): kept points of [0, n) -- cells from
+// land_grid_cells, land flags from land_mask_dev -- into xo / yo / vo / go (nullable) / pfo and
+// their times to (float32 frame slot), new_off[n_frames + 1] (device: first kept point per
+// frame slot, kept count last) and the kept points' ST-DBSCAN bounds (*bounds_out, device).
+// pf must be non-decreasing (the stack's frame-major order).  No synchronisation.
+int32_t land_compact_dev(const float* x, const float* y, const float* v, const int32_t* g,
+                         const int32_t* pf, int64_t n, const int32_t* cell, const uint8_t* land,
+                         int32_t n_frames, float* xo, float* yo, float* vo, int32_t* go,
+                         int32_t* pfo, float* to, int64_t* new_off, Bounds* bounds_out,
+                         hipStream_t st) {
+  if (n < 0 || n >= (int64_t(1) << 31) - 1 || n_frames < 0) {
+    set_error("land_compact_dev: bad sizes");
+    return RPT_EINVAL;
+  }
+  const int64_t nt = std::max<int64_t>((n + kCompTile - 1) / kCompTile, 1);
+  Scratch& sc = scratch(st);
+  Budget bud;
+  bud.add<int32_t>(nt + 1);
+  bud.add<int32_t>(nt + 1);
+  bud.add<BoundsPart>(nt);
+  RPT_TRY(sc.reserve(bud.bytes, st));
+  int32_t* cnt = sc.carve_n<int32_t>(nt + 1);
+  int32_t* base = sc.carve_n<int32_t>(nt + 1);
+  BoundsPart* part = sc.carve_n<BoundsPart>(nt);
+  hipLaunchKernelGGL(k_land_tile_counts, dim3((unsigned)nt), dim3(kCompBlock), 0, st, cell, n,
+                     land, cnt);
+  RPT_CHECK_LAUNCH();
+  RPT_TRY(exclusive_scan_total_i32(cnt, base, nt, st));
+  hipLaunchKernelGGL(k_land_compact, dim3((unsigned)nt), dim3(kCompBlock), 0, st, x, y, v, g, pf,
+                     n, cell, land, base, xo, yo, vo, go, pfo, to, part);
+  hipLaunchKernelGGL(k_land_new_off, dim3((n_frames + 64) / 64), dim3(64), 0, st, base + nt, pfo,
+                     n_frames, new_off);
+  hipLaunchKernelGGL(k_land_compact_final, dim3(1), dim3(kBlock), 0, st, part, (int)nt,
+                     base + nt, bounds_out);
+  RPT_CHECK_LAUNCH();
   return RPT_OK;
 }
 

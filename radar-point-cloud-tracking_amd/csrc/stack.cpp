@@ -49,6 +49,11 @@ int32_t land_filter_cells(const float* x, const float* y, const float* v, const 
                           int32_t nye, const uint8_t* land, const int32_t* cell, float* xo,
                           float* yo, float* vo, int32_t* go, int32_t* pfo, int64_t* new_off,
                           int64_t* n_kept_host, hipStream_t st);
+int32_t land_compact_dev(const float* x, const float* y, const float* v, const int32_t* g,
+                         const int32_t* pf, int64_t n, const int32_t* cell, const uint8_t* land,
+                         int32_t n_frames, float* xo, float* yo, float* vo, int32_t* go,
+                         int32_t* pfo, float* to, int64_t* new_off, Bounds* bounds_out,
+                         hipStream_t st);
 int32_t stdbscan(const float* x, const float* y, const float* z, int64_t stride, const float* t,
                  int64_t n, double eps_space, double eps_time, int32_t min_samples,
                  int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st, int dim);
@@ -425,17 +430,16 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
     RPT_TRY(g2.ensure(cap, st));
     RPT_TRY(pf2.ensure(cap, st));
     RPT_TRY(new_off.ensure((size_t)F + 1, st));
-    RPT_TRY(land_filter_cells(x.p, y.p, v.p, gain ? g.p : nullptr, pf.p, N, fo_dev, F, edges.p,
-                              nxe, edges.p + nxe, nye, land_mask.p, land_cell.p, x2.p, y2.p,
-                              v2.p, gain ? g2.p : nullptr, pf2.p, new_off.p, nullptr, st));
-    // frame times and the ST-DBSCAN bounds of the kept points (their count new_off[F] stays on
-    // the device), read back with the offsets and the land-cell count: ONE round trip
-    const int64_t* kept_dev = new_off.p + F;
+    // one fused compaction: the kept points in order, their frame times and their ST-DBSCAN
+    // bounds (the kept count new_off[F] stays on the device), read back with the offsets and the
+    // land-cell count: ONE round trip
+    (void)fo_dev;
     RPT_TRY(t.ensure(cap, st));
-    RPT_TRY(frame_times_dev(pf2.p, N, kept_dev, t.p, st));
     const size_t bnd_bytes = stdbscan_bounds_bytes();
-    RPT_TRY(bnd.ensure(stdbscan_bounds_part_bytes(N) + 2 * bnd_bytes, st));
-    RPT_TRY(stdbscan_bounds_dev(x2.p, y2.p, t.p, N, kept_dev, bnd.p, bnd.p + 2 * bnd_bytes, st));
+    RPT_TRY(bnd.ensure(2 * bnd_bytes, st));
+    RPT_TRY(land_compact_dev(x.p, y.p, v.p, gain ? g.p : nullptr, pf.p, N, land_cell.p,
+                             land_mask.p, F, x2.p, y2.p, v2.p, gain ? g2.p : nullptr, pf2.p, t.p,
+                             new_off.p, reinterpret_cast<Bounds*>(bnd.p), st));
     int64_t* hn = reinterpret_cast<int64_t*>(down.p);
     PackList pl;
     pl.add(new_off.p, sizeof(int64_t) * (F + 1));

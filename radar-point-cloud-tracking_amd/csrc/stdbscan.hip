@@ -62,14 +62,6 @@ inline float ord2f(uint32_t u) {  // host side
   return f;
 }
 
-struct Bounds {
-  uint32_t mn[4];   // ordered-u32 minima of x, y, z, t (t over finite values only)
-  uint32_t mx[4];
-  int32_t nonfinite_xyz;  // any NaN/inf coordinate
-  int32_t nonintegral_t;  // any finite t with t != floor(t) or |t| >= 2^24
-  int32_t n_finite_t;
-  int32_t t_descends;     // some t[i] < t[i-1]: the points are not in time order
-};
 
 template <int D>
 __global__ __launch_bounds__(kBlock) void k_bounds(const float* __restrict__ x,
