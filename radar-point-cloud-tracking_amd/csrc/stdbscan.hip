@@ -349,9 +349,10 @@ __global__ __launch_bounds__(kBucketBlock) void k_slab_bucket(
     const float* __restrict__ x, const float* __restrict__ y, int64_t stride,
     const float* __restrict__ t, Geom g, const int32_t* __restrict__ slab_lo,
     float4* __restrict__ pts, int32_t* __restrict__ sorig, int32_t* __restrict__ skey,
-    int32_t* __restrict__ cell_start) {
+    int32_t* __restrict__ cell_start, int32_t* __restrict__ occ_tmp,
+    int32_t* __restrict__ slab_occ, uint32_t* __restrict__ occ_bits) {
   __shared__ int32_t hist[kBucketCells];
-  __shared__ int32_t wsum[kBucketBlock / 64];
+  __shared__ int32_t wsum[kBucketBlock / 64], wocc[kBucketBlock / 64];
   const int s = blockIdx.x;
   const int P = g.nx * g.ny;
   const int lo = slab_lo[s], hi = slab_lo[s + 1];
@@ -366,26 +367,60 @@ __global__ __launch_bounds__(kBucketBlock) void k_slab_bucket(
   // exclusive scan of hist[0, P): each thread a contiguous run, then the block's run sums
   const int per = (P + kBucketBlock - 1) / kBucketBlock;
   const int c0 = threadIdx.x * per, c1 = min(c0 + per, P);
-  int run = 0;
-  for (int c = c0; c < c1; ++c) run += hist[c];
+  int run = 0, orun = 0;
+  for (int c = c0; c < c1; ++c) {
+    const int h = hist[c];
+    run += h;
+    orun += (h > 0) ? 1 : 0;
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x / 64;
-  int incl = run;
+  int incl = run, oincl = orun;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
     const int o = __shfl_up(incl, off, 64);
-    if (lane >= off) incl += o;
+    const int oo = __shfl_up(oincl, off, 64);
+    if (lane >= off) {
+      incl += o;
+      oincl += oo;
+    }
   }
-  if (lane == 63) wsum[w] = incl;
+  if (lane == 63) {
+    wsum[w] = incl;
+    wocc[w] = oincl;
+  }
   __syncthreads();
-  int before = 0;
-  for (int v = 0; v < w; ++v) before += wsum[v];
+  int before = 0, obefore = 0, otot = 0;
+  for (int v = 0; v < kBucketBlock / 64; ++v) {
+    if (v < w) {
+      before += wsum[v];
+      obefore += wocc[v];
+    }
+    otot += wocc[v];
+  }
   int acc = before + incl - run;
+  // the slab's occupied cells, ascending, at the front of its point range (a slab has no more
+  // occupied cells than points), and their occupancy bits (one atomicOr per word of this run)
+  int oacc = lo + obefore + oincl - orun;
+  uint32_t word = 0xffffffffu, mask = 0u;
   for (int c = c0; c < c1; ++c) {
     const int h = hist[c];
     hist[c] = acc;
     cell_start[(int64_t)s * P + c] = lo + acc;
     acc += h;
+    if (h > 0) {
+      const int64_t key = (int64_t)s * P + c;
+      occ_tmp[oacc++] = (int32_t)key;
+      const uint32_t wd = (uint32_t)(key >> 5);
+      if (wd != word) {
+        if (mask) atomicOr(occ_bits + word, mask);
+        word = wd;
+        mask = 0u;
+      }
+      mask |= 1u << (key & 31);
+    }
   }
+  if (mask) atomicOr(occ_bits + word, mask);
+  if (threadIdx.x == 0) slab_occ[s] = otot;
   __syncthreads();
   for (int i = lo + threadIdx.x; i < hi; i += kBucketBlock) {
     const int c = cell(i);
@@ -403,6 +438,16 @@ __global__ __launch_bounds__(kBucketBlock) void k_slab_bucket(
     cell_start[g.cells] = hi;
     cell_start[g.cells + 1] = hi;
   }
+}
+
+// the slabs' occupied-cell runs (k_slab_bucket, at each slab's point offset) -> the ascending list
+__global__ __launch_bounds__(kBlock) void k_occ_gather(const int32_t* __restrict__ occ_tmp,
+                                                      const int32_t* __restrict__ slab_lo,
+                                                      const int32_t* __restrict__ occ_base,
+                                                      int32_t* __restrict__ occ) {
+  const int s = blockIdx.x;
+  const int b = occ_base[s], m = occ_base[s + 1] - b, lo = slab_lo[s];
+  for (int j = threadIdx.x; j < m; j += blockDim.x) occ[b + j] = occ_tmp[lo + j];
 }
 
 // run-head flags of the sorted keys (the occupied-cell list is their scan)
@@ -583,11 +628,12 @@ __global__ __launch_bounds__(kBlock) void k_slab_range(const CellRec<D>* __restr
                                                       const int32_t* __restrict__ hpos,
                                                       const int32_t* __restrict__ cell_start,
                                                       int64_t cells_per_slab, int nt,
-                                                      float2* __restrict__ slab_t) {
+                                                      float2* __restrict__ slab_t,
+                                                      const int32_t* __restrict__ occ_base) {
   const int s = blockIdx.x;
   if (s >= nt) return;
-  const int q0 = hpos[cell_start[(int64_t)s * cells_per_slab]];
-  const int q1 = hpos[cell_start[(int64_t)(s + 1) * cells_per_slab]];
+  const int q0 = occ_base ? occ_base[s] : hpos[cell_start[(int64_t)s * cells_per_slab]];
+  const int q1 = occ_base ? occ_base[s + 1] : hpos[cell_start[(int64_t)(s + 1) * cells_per_slab]];
   float lo = FLT_MAX, hi = -FLT_MAX;
   for (int q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
     const CellRec<D> r = crec[occ[q]];
@@ -2273,7 +2319,8 @@ struct DbscanState {
   uint8_t *mutual = nullptr, *core = nullptr;
   float2* slab_t = nullptr;
   int32_t *parent = nullptr, *ccmin = nullptr, *cid = nullptr, *nc_list = nullptr;
-  int32_t *occ = nullptr, *hpos = nullptr;  // occupied cells (ascending), head-flag scan; n_occ = hpos[n]
+  int32_t *occ = nullptr, *hpos = nullptr;  // occupied cells (ascending), head-flag scan
+  const int32_t* n_occ_dev = nullptr;        // the occupied-cell count (hpos[n] or the slab scan's)
   void* crec = nullptr;                      // CellRec<dim>[C + 1]
   uint32_t* occ_bits = nullptr;              // 1 bit per cell
   int uf_flags = -1;                         // see XcdRange; -1 = read RPT_UF_FLAGS once
@@ -2423,6 +2470,8 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   bud.add<CellRec<D>>(C1);  // crec
   bud.add<uint32_t>(C1 / 32 + 2);  // occupancy bits
   bud.add<int32_t>(nt + 1);        // slab_lo (slab-bucket path)
+  bud.add<int32_t>(nt + 1);        // slab_occ (slab-bucket path)
+  bud.add<int32_t>(nt + 1);        // occ_base (slab-bucket path)
   RPT_TRY(arena.reserve(bud.bytes, st));
   (void)arena.carve_n<Bounds>(1);
   uint32_t* keys = arena.carve_n<uint32_t>(n);
@@ -2454,6 +2503,8 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   crec = cr;
   occ_bits = arena.carve_n<uint32_t>(C1 / 32 + 2);  // +1: two-word window reads
   int32_t* slab_lo = arena.carve_n<int32_t>(nt + 1);
+  int32_t* slab_occ = arena.carve_n<int32_t>(nt + 1);
+  int32_t* occ_base = arena.carve_n<int32_t>(nt + 1);
   if (!slab_lo) {
     set_error("internal: scratch carve overflow");
     return RPT_ENOMEM;
@@ -2468,10 +2519,17 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   if (bucket) {
     hipLaunchKernelGGL(k_slab_lo, dim3(grid_for(nt + 1, kBlock, 1024)), dim3(kBlock), 0, st, t, n,
                        g, slab_lo);
+    RPT_HIP(hipMemsetAsync(occ_bits, 0, sizeof(uint32_t) * (C1 / 32 + 2), st));
+    // the slabs write their occupied cells (ascending) into hpos at their point offsets, the
+    // occupancy bits and their counts; one scan over the slabs and a gather give the list
     hipLaunchKernelGGL(k_slab_bucket, dim3((unsigned)nt), dim3(kBucketBlock), 0, st, x, y, stride,
-                       t, g, slab_lo, pts, sorig, skey, cell_start);
-    hipLaunchKernelGGL(k_key_heads, dim3(gb), dim3(kBlock), 0, st, skey, n, hpos);
+                       t, g, slab_lo, pts, sorig, skey, cell_start, hpos, slab_occ, occ_bits);
     RPT_CHECK_LAUNCH();
+    RPT_TRY(exclusive_scan_total_i32(slab_occ, occ_base, nt, st));
+    hipLaunchKernelGGL(k_occ_gather, dim3((unsigned)nt), dim3(kBlock), 0, st, hpos, slab_lo,
+                       occ_base, occ);
+    RPT_CHECK_LAUNCH();
+    n_occ_dev = occ_base + nt;
   } else {
     hipLaunchKernelGGL(k_keys<D>, dim3(gb), dim3(kBlock), 0, st, x, y, z, stride, t, n, g, keys,
                        vals);
@@ -2486,16 +2544,17 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
     hipLaunchKernelGGL(k_cell_runs, dim3(gb), dim3(kBlock), 0, st, skey, n, cell_start, hpos);
     RPT_CHECK_LAUNCH();
     RPT_TRY(exclusive_scan_total_i32(cell_start, cell_start, C1, st));
+    RPT_TRY(exclusive_scan_total_i32(hpos, hpos, n, st));
+    RPT_HIP(hipMemsetAsync(occ_bits, 0, sizeof(uint32_t) * (C1 / 32 + 2), st));
+    hipLaunchKernelGGL(k_occ_list, dim3(gb), dim3(kBlock), 0, st, skey, n, hpos, occ, occ_bits);
+    RPT_CHECK_LAUNCH();
+    n_occ_dev = hpos + n;
   }
-  RPT_TRY(exclusive_scan_total_i32(hpos, hpos, n, st));
-  RPT_HIP(hipMemsetAsync(occ_bits, 0, sizeof(uint32_t) * (C1 / 32 + 2), st));
-  hipLaunchKernelGGL(k_occ_list, dim3(gb), dim3(kBlock), 0, st, skey, n, hpos, occ, occ_bits);
-  RPT_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_cell_box<D>, dim3(grid_for(8 * n, kBlock, 8192)), dim3(kBlock), 0, st,
-                     pts, cell_start, occ, hpos + n, g, boxA, boxB, mutual, cr);
+                     pts, cell_start, occ, n_occ_dev, g, boxA, boxB, mutual, cr);
   RPT_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_slab_range<D>, dim3((unsigned)nt), dim3(kBlock), 0, st, cr, occ, hpos,
-                     cell_start, (int64_t)(C / nt), (int)nt, slab_t);
+                     cell_start, (int64_t)(C / nt), (int)nt, slab_t, bucket ? occ_base : nullptr);
   RPT_CHECK_LAUNCH();
   tm.mark();
   return RPT_OK;
@@ -2523,7 +2582,7 @@ int32_t DbscanState::core_pass(hipStream_t st) {
   int32_t* n_cq = cid + n;
   int32_t* slow = nc_list;
   int32_t* n_slow = nc_list + n;
-  const int32_t* n_occ = hpos + n;
+  const int32_t* n_occ = n_occ_dev;
   if (k5_legacy < 0) {  // RPT_K5_MODE: 0 round-1 queue pipeline, 1 cells write point flags,
                         // 2 cells + point-flag fill (no queue); both 1/2 end in k_core_slow_cells
     // default 0: the folded variants measured no faster on the 100- and 1000-frame stacks
@@ -2612,7 +2671,7 @@ int32_t DbscanState::union_pass(hipStream_t st) {
   const int gc = grid_for(C, kBlock, 8192);
   const int gw = wave_grid(n);
   const unsigned gp = (unsigned)((n + kBlock - 1) / kBlock);
-  const int32_t* n_occ = hpos + n;
+  const int32_t* n_occ = n_occ_dev;
   hipLaunchKernelGGL(k_fill_i32, dim3(gc), dim3(kBlock), 0, st, cell_min, C, INT_MAX);
   RPT_HIP(hipMemsetAsync(rep, 0xFF, sizeof(int32_t) * (size_t)C, st));
   hipLaunchKernelGGL(k_cell_min_orig, dim3(gb), dim3(kBlock), 0, st, skey, core, sorig, n, C,
@@ -2747,7 +2806,7 @@ int32_t DbscanState::frames_pass(int32_t min_frames, hipStream_t st) {
   const bool refine = min_frames >= 2;
   int32_t* list = nc_list;  // free until labels_fifo rebuilds it
   int32_t* count = nc_list + n;
-  const int32_t* n_occ = hpos + n;
+  const int32_t* n_occ = n_occ_dev;
   const bool cells = refine && integral_t && dim == 2 && g.nz == 1;
   if (cells) {
     const int R = (int)std::min<double>(std::floor((double)g.epst / g.ct), 64.0);
