@@ -24,7 +24,7 @@
 //   k_cell_box    per occupied cell: bounding box in space and time, "mutual" flag
 //                 (box diagonal within eps and time span within eps_t: every pair adjacent)
 //   k_core        neighbour count with early exit at min_samples; whole-cell accept/reject
-//   k_rep         the minimum-original-index core point of each cell
+//   k_cell_min_pair  the minimum-original-index core point of each cell (star init)
 //   k_union       core-core union-find (min-index hooking); one edge per mutual cell suffices
 //   k_compress    root of every point
 //   k_cmin        minimum original index per component
@@ -448,14 +448,6 @@ __global__ __launch_bounds__(kBlock) void k_occ_gather(const int32_t* __restrict
   const int s = blockIdx.x;
   const int b = occ_base[s], m = occ_base[s + 1] - b, lo = slab_lo[s];
   for (int j = threadIdx.x; j < m; j += blockDim.x) occ[b + j] = occ_tmp[lo + j];
-}
-
-// run-head flags of the sorted keys (the occupied-cell list is their scan)
-__global__ __launch_bounds__(kBlock) void k_key_heads(const int32_t* __restrict__ skey, int64_t n,
-                                                     int32_t* __restrict__ head) {
-  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
-       s += (int64_t)gridDim.x * blockDim.x)
-    head[s] = (s == 0 || skey[s - 1] != skey[s]) ? 1 : 0;
 }
 
 __device__ __forceinline__ bool occupied(const uint32_t* __restrict__ bits, int64_t c) {
@@ -965,6 +957,12 @@ __device__ __forceinline__ int classify_cells(const float4& A1, const float4& B1
   return (dmax <= g.eps2 && tm <= g.epst) ? 1 : 2;
 }
 
+// Tuning flags of the union kernels (rpt_set_tuning / RPT_UF_FLAGS): bit 0 = finds inside the
+// union kernels do not path-halve (agent-scope stores drop the line from the XCD's L2; k_compress
+// compresses afterwards); bit 2 = timing experiment only: skip the box-certain unites (labels
+// are then WRONG); bit 1 = XCD-aware item ranges (blockIdx % 8 = XCD under round-robin
+// placement: each XCD unions a contiguous range of cells, so its L2 keeps their parents).
+// XcdRange is also the item split of the K5 / K7 queue kernels.
 struct XcdRange {
   int64_t first, step, end;
 };
@@ -1477,44 +1475,53 @@ __global__ __launch_bounds__(kBlock) void k_core_slow_cells(const float4* __rest
   }
 }
 
-// The core point (sorted index) of each cell with the smallest ORIGINAL index, -1 when none:
-// the star init hangs a mutual cell's core points under it, which keeps every union-find root
-// its component's minimum original index whatever the order inside the cell (the slab-bucket
-// K4 does not keep input order inside a cell).  Two coalesced passes over the sorted points:
-// a segmented wave minimum per cell run (runs are contiguous), one atomicMin per (wave, cell)
-// run, then the point holding the minimum writes itself.
-__global__ __launch_bounds__(kBlock) void k_cell_min_orig(const int32_t* __restrict__ skey,
+// Per cell the smallest (original index << 32 | sorted index) over its core points (segmented
+// wave minimum over the sorted points, one atomicMin per run): the core point with the smallest
+// ORIGINAL index is the cell's representative, which keeps every union-find root its component's
+// minimum original index whatever the order inside the cell (the slab-bucket K4 does not keep
+// index order), and the star initialisation reads it directly.
+__global__ __launch_bounds__(kBlock) void k_cell_min_pair(const int32_t* __restrict__ skey,
                                                          const uint8_t* __restrict__ core,
                                                          const int32_t* __restrict__ sorig,
                                                          int64_t n, int64_t cells,
-                                                         int32_t* __restrict__ cell_min) {
+                                                         unsigned long long* __restrict__ cmin) {
   const int lane = threadIdx.x & 63;
   for (int64_t s0 = (int64_t)blockIdx.x * blockDim.x; s0 < n;
        s0 += (int64_t)gridDim.x * blockDim.x) {
     const int64_t s = s0 + threadIdx.x;
     const int key = (s < n) ? skey[s] : -1;
-    int v = (s < n && core[s] && (int64_t)key < cells) ? sorig[s] : INT_MAX;
+    uint64_t v = (s < n && core[s] && (int64_t)key < cells)
+                     ? (((uint64_t)(uint32_t)sorig[s] << 32) | (uint32_t)s)
+                     : ~0ull;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {  // sorted keys: equal at distance off = same run
-      const int ov = __shfl_up(v, off, 64);
+      const uint32_t olo = (uint32_t)__shfl_up((int)(uint32_t)v, off, 64);
+      const uint32_t ohi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), off, 64);
       const int ok = __shfl_up(key, off, 64);
-      if (lane >= off && ok == key) v = min(v, ov);
+      if (lane >= off && ok == key) v = min(v, ((uint64_t)ohi << 32) | olo);
     }
     const int next = __shfl_down(key, 1, 64);
-    if ((lane == 63 || next != key) && key >= 0 && v != INT_MAX) atomicMin(cell_min + key, v);
+    if ((lane == 63 || next != key) && key >= 0 && v != ~0ull)
+      atomicMin(cmin + key, (unsigned long long)v);
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_rep(const int32_t* __restrict__ skey,
-                                               const uint8_t* __restrict__ core,
-                                               const int32_t* __restrict__ sorig, int64_t n,
-                                               int64_t cells,
-                                               const int32_t* __restrict__ cell_min,
-                                               int32_t* __restrict__ rep) {
+// Star initialisation from k_cell_min_pair: core points of a mutual cell under the cell's
+// representative, other points roots; the representative records itself in rep.
+__global__ __launch_bounds__(kBlock) void k_parent_init_pair(
+    int32_t* __restrict__ parent, int64_t n, const uint8_t* __restrict__ core,
+    const int32_t* __restrict__ skey, const uint8_t* __restrict__ mutual,
+    const unsigned long long* __restrict__ cmin, int64_t cells, int32_t* __restrict__ rep) {
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
        s += (int64_t)gridDim.x * blockDim.x) {
-    const int key = skey[s];
-    if (core[s] && (int64_t)key < cells && sorig[s] == cell_min[key]) rep[key] = (int32_t)s;
+    const int32_t k = skey[s];
+    int32_t p = (int32_t)s;
+    if (core[s] && (int64_t)k < cells) {
+      const int32_t r = (int32_t)(uint32_t)cmin[k];
+      if (r == (int32_t)s) rep[k] = r;
+      if (mutual[k]) p = r;
+    }
+    parent[s] = p;
   }
 }
 
@@ -1551,26 +1558,6 @@ __device__ __forceinline__ void uf_unite(int32_t* parent, const int32_t* __restr
     const int old = atomicCAS(parent + a, a, b);
     if (old == a) return;
     a = old;
-  }
-}
-
-// Tuning flags of the union kernels (rpt_set_tuning / RPT_UF_FLAGS): bit 0 = finds inside the
-// union kernels do not path-halve (agent-scope stores drop the line from the XCD's L2; k_compress
-// compresses afterwards); bit 2 = timing experiment only: skip the box-certain unites (labels
-// are then WRONG); bit 1 = XCD-aware item ranges (blockIdx % 8 = XCD under round-robin
-// placement: each XCD unions a contiguous range of cells, so its L2 keeps their parents).
-// Star initialisation: every core point of a mutual cell hangs under the cell's core point of
-// minimum original index (k_rep), other points are roots.
-__global__ __launch_bounds__(kBlock) void k_parent_init(int32_t* parent, int64_t n,
-                                                       const uint8_t* __restrict__ core,
-                                                       const int32_t* __restrict__ skey,
-                                                       const uint8_t* __restrict__ mutual,
-                                                       const int32_t* __restrict__ rep,
-                                                       int64_t cells) {
-  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
-       s += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t k = skey[s];
-    parent[s] = (core[s] && (int64_t)k < cells && mutual[k]) ? rep[k] : (int32_t)s;
   }
 }
 
@@ -1826,7 +1813,7 @@ __global__ __launch_bounds__(kBlock) void k_label_core(const int32_t* __restrict
 }
 
 // Per cell, the smallest component key among its core points (INT_MAX: none) -- the same
-// segmented wave minimum over the sorted points as k_cell_min_orig.
+// segmented wave minimum over the sorted points as k_cell_min_pair.
 __global__ __launch_bounds__(kBlock) void k_cell_min_key(const int32_t* __restrict__ skey,
                                                         const int32_t* __restrict__ key_of,
                                                         int64_t n, int64_t cells,
@@ -2321,6 +2308,7 @@ struct DbscanState {
   int32_t *parent = nullptr, *ccmin = nullptr, *cid = nullptr, *nc_list = nullptr;
   int32_t *occ = nullptr, *hpos = nullptr;  // occupied cells (ascending), head-flag scan
   const int32_t* n_occ_dev = nullptr;        // the occupied-cell count (hpos[n] or the slab scan's)
+  uint64_t* cell_min_pair = nullptr;         // per cell (min core original index, its sorted index)
   void* crec = nullptr;                      // CellRec<dim>[C + 1]
   uint32_t* occ_bits = nullptr;              // 1 bit per cell
   int uf_flags = -1;                         // see XcdRange; -1 = read RPT_UF_FLAGS once
@@ -2333,7 +2321,7 @@ struct DbscanState {
     return static_cast<const CellRec<D>*>(crec);
   }
   int32_t* slab = nullptr;   // per sorted point: final label of core points (global path)
-  int32_t* cell_min = nullptr;  // per cell: minimum original index of its core points (k_rep)
+  int32_t* cell_min = nullptr;  // per cell: smallest component key (label pass)
   uint8_t* fok = nullptr;    // per cell: frame condition met by every core point (denoise)
   bool integral_t = false;   // every finite t integral (slab = one frame id)
   int64_t* stmp = nullptr;
@@ -2465,6 +2453,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   bud.add<int32_t>(n);      // slab (global finalize; denoise: orig -> sorted)
   bud.add<uint8_t>(C1);     // fok (denoise)
   bud.add<int32_t>(C1);     // cell_min
+  bud.add<uint64_t>(C1);    // cell_min_pair (union star initialisation)
   bud.add<int32_t>(n + 1);  // occ
   bud.add<int32_t>(n + 1);  // hpos
   bud.add<CellRec<D>>(C1);  // crec
@@ -2497,6 +2486,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   slab = arena.carve_n<int32_t>(n);
   fok = arena.carve_n<uint8_t>(C1);
   cell_min = arena.carve_n<int32_t>(C1);
+  cell_min_pair = arena.carve_n<uint64_t>(C1);
   occ = arena.carve_n<int32_t>(n + 1);
   hpos = arena.carve_n<int32_t>(n + 1);
   CellRec<D>* cr = arena.carve_n<CellRec<D>>(C1);
@@ -2672,14 +2662,15 @@ int32_t DbscanState::union_pass(hipStream_t st) {
   const int gw = wave_grid(n);
   const unsigned gp = (unsigned)((n + kBlock - 1) / kBlock);
   const int32_t* n_occ = n_occ_dev;
-  hipLaunchKernelGGL(k_fill_i32, dim3(gc), dim3(kBlock), 0, st, cell_min, C, INT_MAX);
+  (void)gc;
+  // per-cell (min original index, sorted index) of the core points, one u64 per cell
+  auto* cmin = reinterpret_cast<unsigned long long*>(cell_min_pair);
   RPT_HIP(hipMemsetAsync(rep, 0xFF, sizeof(int32_t) * (size_t)C, st));
-  hipLaunchKernelGGL(k_cell_min_orig, dim3(gb), dim3(kBlock), 0, st, skey, core, sorig, n, C,
-                     cell_min);
-  hipLaunchKernelGGL(k_rep, dim3(gb), dim3(kBlock), 0, st, skey, core, sorig, n, C, cell_min,
-                     rep);
-  hipLaunchKernelGGL(k_parent_init, dim3(gb), dim3(kBlock), 0, st, parent, n, core, skey, mutual,
-                     rep, C);
+  RPT_HIP(hipMemsetAsync(cmin, 0xFF, sizeof(unsigned long long) * (size_t)C, st));
+  hipLaunchKernelGGL(k_cell_min_pair, dim3(gb), dim3(kBlock), 0, st, skey, core, sorig, n, C,
+                     cmin);
+  hipLaunchKernelGGL(k_parent_init_pair, dim3(gb), dim3(kBlock), 0, st, parent, n, core, skey,
+                     mutual, cmin, C, rep);
   if (dim == 2) {
     hipLaunchKernelGGL((k_union_cells<2, false>), dim3(gw), dim3(kBlock), 0, st, pts, g,
                        cell_start, occ, n_occ, rec<2>(), occ_bits, slab_t, core, rep, mutual, sorig,
