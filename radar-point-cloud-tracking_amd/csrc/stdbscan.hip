@@ -216,6 +216,7 @@ struct Geom {
   double ox, oy, oz, ot;  // origins (minima)
   double cs;              // spatial cell side
   double ct;              // time slab width
+  double inv_cs, inv_ct;  // their float64 reciprocals (cell_of)
   int nx, ny, nz, nt;
   int64_t cells;          // nx*ny*nz*nt (an extra "isolated" cell C holds non-finite t)
   double eps2;            // eps_space^2 (float64)
@@ -227,13 +228,17 @@ struct Geom {
   float e2lo, e2hi;
 };
 
-__device__ __forceinline__ int cell_of(double v, double o, double cs, int n) {
-  double q = floor((v - o) / cs);
+// cell index floor((v - o) / side) as a multiply by the host's float64 reciprocal (a float64
+// divide per coordinate dominated the grid build); every kernel assigns cells through this one
+// function, so assignments stay consistent, and the 2^-20 margin on the side keeps every
+// neighbour within +-2 cells whatever the last-bit rounding
+__device__ __forceinline__ int cell_of(double v, double o, double inv, int n) {
+  double q = floor((v - o) * inv);
   int c = (q < 0.0) ? 0 : (q >= (double)n ? n - 1 : (int)q);
   return c;
 }
 __device__ __forceinline__ int slab_of(float t, const Geom& g) {
-  return cell_of((double)t, g.ot, g.ct, g.nt);
+  return cell_of((double)t, g.ot, g.inv_ct, g.nt);
 }
 
 template <int D>
@@ -250,9 +255,9 @@ __global__ __launch_bounds__(kBlock) void k_keys(const float* __restrict__ x,
     if (!isfinite(ti)) {
       key = (uint32_t)g.cells;  // isolated: matches nothing, not even itself
     } else {
-      const int cx = cell_of((double)x[i * stride], g.ox, g.cs, g.nx);
-      const int cy = cell_of((double)y[i * stride], g.oy, g.cs, g.ny);
-      const int cz = (D == 3) ? cell_of((double)z[i * stride], g.oz, g.cs, g.nz) : 0;
+      const int cx = cell_of((double)x[i * stride], g.ox, g.inv_cs, g.nx);
+      const int cy = cell_of((double)y[i * stride], g.oy, g.inv_cs, g.ny);
+      const int cz = (D == 3) ? cell_of((double)z[i * stride], g.oz, g.inv_cs, g.nz) : 0;
       const int s = slab_of(ti, g);
       key = (uint32_t)((((int64_t)s * g.nz + cz) * g.ny + cy) * g.nx + cx);
     }
@@ -331,6 +336,7 @@ __global__ __launch_bounds__(kBlock) void k_occ_list(const int32_t* __restrict__
 // it (roots are minimum ORIGINAL indices, counts and minima are order-free).
 constexpr int kBucketBlock = 1024;
 constexpr int kBucketCells = 16384;  // per-slab cells held in LDS (64 KiB)
+constexpr int kBucketU = 4;          // points per thread per round (loads in flight together)
 
 // slab_lo[s] = first point of slab s (points ordered by slab), slab_lo[nt] = n
 __global__ void k_slab_lo(const float* __restrict__ t, int64_t n, Geom g,
@@ -358,11 +364,42 @@ __global__ __launch_bounds__(kBucketBlock) void k_slab_bucket(
   const int lo = slab_lo[s], hi = slab_lo[s + 1];
   for (int c = threadIdx.x; c < P; c += kBucketBlock) hist[c] = 0;
   __syncthreads();
-  auto cell = [&](int64_t i) {
-    return cell_of((double)y[i * stride], g.oy, g.cs, g.ny) * g.nx +
-           cell_of((double)x[i * stride], g.ox, g.cs, g.nx);
+  // consecutive points (along a ray) often share a cell: a run of equal cells in a wave takes
+  // ONE LDS atomic (by its head lane) instead of one per point
+  const int ln = threadIdx.x & 63;
+  auto runs = [&](int c, bool v, int& rank, int& len, int& head) {
+    const int up = __shfl_up(c, 1, 64), dn = __shfl_down(c, 1, 64);
+    const uint64_t hm = __ballot(v && (ln == 0 || up != c));
+    const uint64_t lm = __ballot(v && (ln == 63 || dn != c));
+    const uint64_t below = (ln == 63) ? ~0ull : ((2ull << ln) - 1ull);
+    head = 63 - __builtin_clzll(hm & below | 1ull);  // hm has a bit at or below ln when v
+    const int last = ln + __builtin_ctzll((lm >> ln) | (1ull << (63 - ln)));
+    rank = ln - head;
+    len = last - head + 1;
   };
-  for (int i = lo + threadIdx.x; i < hi; i += kBucketBlock) atomicAdd(&hist[cell(i)], 1);
+  // kBucketU points per thread per round, their loads issued together
+  auto cell_xy = [&](float px, float py) {
+    return cell_of((double)py, g.oy, g.inv_cs, g.ny) * g.nx +
+           cell_of((double)px, g.ox, g.inv_cs, g.nx);
+  };
+  for (int i0 = lo; i0 < hi; i0 += kBucketBlock * kBucketU) {
+    float px[kBucketU], py[kBucketU];
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u) {
+      const int i = i0 + u * kBucketBlock + threadIdx.x;
+      px[u] = (i < hi) ? x[(int64_t)i * stride] : 0.f;
+      py[u] = (i < hi) ? y[(int64_t)i * stride] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u) {
+      const int i = i0 + u * kBucketBlock + threadIdx.x;
+      const bool v = i < hi;
+      const int c = v ? cell_xy(px[u], py[u]) : -1;
+      int rank, len, head;
+      runs(c, v, rank, len, head);
+      if (v && rank == 0) atomicAdd(&hist[c], len);
+    }
+  }
   __syncthreads();
   // exclusive scan of hist[0, P): each thread a contiguous run, then the block's run sums
   const int per = (P + kBucketBlock - 1) / kBucketBlock;
@@ -422,17 +459,31 @@ __global__ __launch_bounds__(kBucketBlock) void k_slab_bucket(
   if (mask) atomicOr(occ_bits + word, mask);
   if (threadIdx.x == 0) slab_occ[s] = otot;
   __syncthreads();
-  for (int i = lo + threadIdx.x; i < hi; i += kBucketBlock) {
-    const int c = cell(i);
-    const int dst = lo + atomicAdd(&hist[c], 1);
-    float4 p;
-    p.x = x[(int64_t)i * stride];
-    p.y = y[(int64_t)i * stride];
-    p.w = t[i];
-    p.z = p.w;
-    pts[dst] = p;
-    sorig[dst] = i;
-    skey[dst] = s * P + c;
+  for (int i0 = lo; i0 < hi; i0 += kBucketBlock * kBucketU) {
+    float px[kBucketU], py[kBucketU], pt[kBucketU];
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u) {
+      const int i = i0 + u * kBucketBlock + threadIdx.x;
+      px[u] = (i < hi) ? x[(int64_t)i * stride] : 0.f;
+      py[u] = (i < hi) ? y[(int64_t)i * stride] : 0.f;
+      pt[u] = (i < hi) ? t[i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u) {
+      const int i = i0 + u * kBucketBlock + threadIdx.x;
+      const bool v = i < hi;
+      const int c = v ? cell_xy(px[u], py[u]) : -1;
+      int rank, len, head;
+      runs(c, v, rank, len, head);
+      int base = (v && rank == 0) ? atomicAdd(&hist[c], len) : 0;
+      base = __shfl(base, head, 64);
+      if (v) {
+        const int dst = lo + base + rank;
+        pts[dst] = make_float4(px[u], py[u], pt[u], pt[u]);
+        sorig[dst] = i;
+        skey[dst] = s * P + c;
+      }
+    }
   }
   if (s == g.nt - 1 && threadIdx.x == 0) {  // the isolated cell (empty here) and the end
     cell_start[g.cells] = hi;
@@ -719,8 +770,8 @@ __device__ __forceinline__ void for_each_cell(const float4& p, int32_t key, cons
   const int cs = (D == 3) ? (r / g.nz) : r;
   // conservative slab window (+-1 slack), culled by each slab's actual time range
   const double tp = (double)p.w, et = (double)g.epst;
-  int s0 = (int)fmax(floor((tp - et - g.ot) / g.ct) - 1.0, 0.0);
-  int s1 = (int)fmin(floor((tp + et - g.ot) / g.ct) + 1.0, (double)(g.nt - 1));
+  int s0 = (int)fmax(floor((tp - et - g.ot) * g.inv_ct) - 1.0, 0.0);
+  int s1 = (int)fmin(floor((tp + et - g.ot) * g.inv_ct) + 1.0, (double)(g.nt - 1));
   const int x0 = max(cx - 2, 0), x1 = min(cx + 2, g.nx - 1);
   const int y0 = max(cy - 2, 0), y1 = min(cy + 2, g.ny - 1);
   const int z0 = (D == 3) ? max(cz - 2, 0) : 0, z1 = (D == 3) ? min(cz + 2, g.nz - 1) : 0;
@@ -846,8 +897,8 @@ __device__ __forceinline__ Window make_window(int cx, int cy, int cz, float tlo,
   constexpr int PER = (D == 3) ? 125 : 25;
   Window w;
   const double et = (double)g.epst;
-  int s0 = (int)fmax(floor(((double)tlo - et - g.ot) / g.ct) - 1.0, (double)s_min);
-  int s1 = (int)fmin(floor(((double)thi + et - g.ot) / g.ct) + 1.0, (double)(g.nt - 1));
+  int s0 = (int)fmax(floor(((double)tlo - et - g.ot) * g.inv_ct) - 1.0, (double)s_min);
+  int s1 = (int)fmin(floor(((double)thi + et - g.ot) * g.inv_ct) + 1.0, (double)(g.nt - 1));
   // shrink to the slabs in reach: one lane per slab (independent loads), ballot (callers are
   // whole waves with uniform arguments)
   const int lane = threadIdx.x & 63;
@@ -882,11 +933,13 @@ __device__ __forceinline__ Window make_window(int cx, int cy, int cz, float tlo,
 
 template <int D>
 __device__ __forceinline__ void decode_key(int64_t key, const Geom& g, int& cx, int& cy, int& cz) {
-  cx = (int)(key % g.nx);
-  int64_t r = key / g.nx;
-  cy = (int)(r % g.ny);
+  // keys of real cells are < 2^30 (cmax): 32-bit divisions, not the 64-bit ones' call sequence
+  const int k = (int)key;
+  cx = k % g.nx;
+  int r = k / g.nx;
+  cy = r % g.ny;
   r /= g.ny;
-  cz = (D == 3) ? (int)(r % g.nz) : 0;
+  cz = (D == 3) ? (r % g.nz) : 0;
 }
 
 // q-th cell of the window; -1 when outside the grid or its slab holds nothing within reach
@@ -1147,12 +1200,13 @@ __global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
           const int y = cy + dy - 2;
           if (y < 0 || y >= g.ny) continue;
           // bit dx <-> key k0 + dx (x = cx - 2 + dx); columns outside [0, nx) are cleared
-          const int64_t k0 = ((int64_t)sl * g.ny + y) * g.nx + (cx - 2);
-          const int64_t kk = k0 < 0 ? 0 : k0;
-          const int64_t w = kk >> 5;
-          const uint64_t two = (uint64_t)occ_bits[w] | ((uint64_t)occ_bits[w + 1] << 32);
-          uint32_t m =
-              (k0 < 0) ? ((uint32_t)(two << (-k0)) & 31u) : ((uint32_t)(two >> (kk & 31)) & 31u);
+          // (int32 keys: cells < 2^30)
+          const int k0 = (sl * g.ny + y) * g.nx + (cx - 2);
+          const int kk = k0 < 0 ? 0 : k0;
+          const int w = kk >> 5;
+          const uint32_t lo_w = occ_bits[w], hi_w = occ_bits[w + 1];
+          uint32_t m = (k0 < 0) ? ((lo_w << (-k0)) & 31u)
+                                : (__builtin_amdgcn_alignbit(hi_w, lo_w, (uint32_t)(kk & 31)) & 31u);
           m &= ~((1u << lo_x) - 1u);
           if (hi_x > 0) m &= (31u >> hi_x);
           m5[dy] = m;
@@ -1177,7 +1231,7 @@ __global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
           const int dy = (k == 0) ? 2 : ((k & 1) ? 2 - (k + 1) / 2 : 2 + k / 2);
           const uint32_t m = reach ? m5[dy] : 0u;
           if (m) {
-            const int64_t row = ((int64_t)sl * g.ny + (cy + dy - 2)) * g.nx + (cx - 2);
+            const int row = (sl * g.ny + (cy + dy - 2)) * g.nx + (cx - 2);
             // the row's (up to 5) candidate records in flight together, then classified
             CellRec<2> cr[5];
 #pragma unroll
@@ -2424,6 +2478,8 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   g.ot = lo[3];
   g.cs = cs;
   g.ct = ct;
+  g.inv_cs = 1.0 / cs;
+  g.inv_ct = 1.0 / ct;
   g.nx = (int)nx;
   g.ny = (int)ny;
   g.nz = (int)nz;
@@ -2585,8 +2641,11 @@ int32_t DbscanState::core_pass(hipStream_t st) {
     k5_legacy = (k5_legacy == 0) ? 1 : 0;
     k5_fill = (e && std::atoi(e) == 2) ? 1 : 0;
   }
-  // slabs each side a cell's points can reach: eps_t / slab width, +1 for the slab's extent
-  const double rs = std::ceil((double)g.epst / g.ct) + 1.0;
+  // slabs each side a cell's points can reach: eps_t / slab width, +1 for the slab's extent;
+  // integral times with integral slab widths: a slab holds whole time values, so ceil(floor(eps_t)
+  // / width) slabs each side hold every time within eps_t
+  const double rs = integral_t ? std::ceil(std::floor((double)g.epst) / g.ct)
+                               : std::ceil((double)g.epst / g.ct) + 1.0;
   const bool oct = dim == 2 && rs <= (double)kCwMaxR && g.nz == 1;
   if (!k5_legacy) {
     // cells decide (and write their points' flags) in one pass; the undecided cells' points are
