@@ -270,7 +270,7 @@ __device__ __forceinline__ int nth_bit16(uint32_t m, uint32_t n) {
 // may be short): a wave issues the group's loads together (4 KiB in flight) before ranking any of
 // them.  The count pass writes one kept count per GROUP; the write pass walks the group's rows in
 // order and carries the in-file rank across them, so no per-row reduction or prefix is needed.
-constexpr int kGroupRows = 4;
+constexpr int kGroupRows = 4;  // k_group_write_u8 selects the rows' geometry among 4
 
 struct GroupMap {
   uint32_t gpf;   // groups per file = ceil(rows / kGroupRows)
@@ -445,6 +445,21 @@ __global__ __launch_bounds__(kBlock) void k_group_write_u8(
     int64_t row0;
     int nr;
     group_rows(gm, grp, &f, &row0, &nr);
+    // the group's rows' geometry, loaded by lanes 0..3 together with the prefix reads (one
+    // dependent load level less per output: ent -> row -> geometry becomes a lane shuffle)
+    float g_sc = 0.f, g_c = 0.f, g_s = 0.f;
+    if (lane < nr) {
+      g_sc = scale[row0 + lane];
+      g_c = cos_t[row0 + lane];
+      g_s = sin_t[row0 + lane];
+    }
+    float r_sc[kGroupRows], r_c[kGroupRows], r_s[kGroupRows];  // wave-uniform (readlane)
+#pragma unroll
+    for (int k = 0; k < kGroupRows; ++k) {
+      r_sc[k] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, g_sc), k));
+      r_c[k] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, g_c), k));
+      r_s[k] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, g_s), k));
+    }
     // in-file rank of the group's first kept sample (< rows * 1024 < 2^32), its kept count, the
     // group's emitted outputs [first, last) and the file's output base
     const int64_t gp0 = gprefix[grp];
@@ -485,10 +500,13 @@ __global__ __launch_bounds__(kBlock) void k_group_write_u8(
       if (oo >= cap) break;
       const uint32_t i = o * us - rank;  // in-group kept rank
       const uint32_t ent = staged ? e[i] : kept_entry(L, rb, i);
-      const int64_t row = row0 + (ent >> 18);
-      const float rr = scale[row] * inv_bins * (float)((ent >> 8) & 1023u);
-      x[oo] = rr * cos_t[row];
-      y[oo] = rr * sin_t[row];
+      const int rk = (int)(ent >> 18);
+      const float sc = rk == 0 ? r_sc[0] : (rk == 1 ? r_sc[1] : (rk == 2 ? r_sc[2] : r_sc[3]));
+      const float cc = rk == 0 ? r_c[0] : (rk == 1 ? r_c[1] : (rk == 2 ? r_c[2] : r_c[3]));
+      const float ss = rk == 0 ? r_s[0] : (rk == 1 ? r_s[1] : (rk == 2 ? r_s[2] : r_s[3]));
+      const float rr = sc * inv_bins * (float)((ent >> 8) & 1023u);
+      x[oo] = rr * cc;
+      y[oo] = rr * ss;
       val[oo] = (float)(ent & 0xffu);
       if (gain_out) gain_out[oo] = g;
       if (pf_out) pf_out[oo] = fr;

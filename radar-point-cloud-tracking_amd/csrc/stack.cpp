@@ -43,12 +43,6 @@ int32_t land_mask(const int32_t* cnt, const double* tot, int64_t cells, int64_t 
 int32_t land_mask_dev(const int32_t* cnt, const double* tot, int64_t cells, int64_t num_frames,
                       double pthr, double ithr, uint8_t* land, int32_t* n_land_dev,
                       hipStream_t st);
-int32_t land_filter_cells(const float* x, const float* y, const float* v, const int32_t* g,
-                          const int32_t* pf, int64_t n, const int64_t* frame_off,
-                          int32_t n_frames, const double* xe, int32_t nxe, const double* ye,
-                          int32_t nye, const uint8_t* land, const int32_t* cell, float* xo,
-                          float* yo, float* vo, int32_t* go, int32_t* pfo, int64_t* new_off,
-                          int64_t* n_kept_host, hipStream_t st);
 int32_t land_compact_dev(const float* x, const float* y, const float* v, const int32_t* g,
                          const int32_t* pf, int64_t n, const int32_t* cell, const uint8_t* land,
                          int32_t n_frames, float* xo, float* yo, float* vo, int32_t* go,
@@ -1013,7 +1007,6 @@ int32_t rpt_shard_land_apply(rpt_shard* h, const double* grid, int64_t cells,
   RPT_TRY(S.down.ensure(sizeof(int64_t) * (size_t)(F + 4), st));
   hn = reinterpret_cast<int64_t*>(S.down.p);
   if (h->land) {
-    const int32_t nxe = (int32_t)h->xe.size(), nye = (int32_t)h->ye.size();
     RPT_TRY(S.land_cnt.ensure((size_t)cells, st));
     RPT_TRY(S.land_mask.ensure((size_t)cells, st));
     hipLaunchKernelGGL(k_f64_to_cnt, dim3(grid_for(cells, 256, 1024)), dim3(256), 0, st, grid,
@@ -1029,12 +1022,13 @@ int32_t rpt_shard_land_apply(rpt_shard* h, const double* grid, int64_t cells,
     RPT_TRY(S.v2.ensure(cap, st));
     RPT_TRY(S.g2.ensure(cap, st));
     RPT_TRY(S.pf2.ensure(cap, st));
-    const int64_t* fo_dev = reinterpret_cast<const int64_t*>(S.edges.p + nxe + nye);
-    if (N > 0)
-      RPT_TRY(land_filter_cells(S.x.p, S.y.p, S.v.p, S.g.p, S.pf.p, N, fo_dev, F, S.edges.p, nxe,
-                                S.edges.p + nxe, nye, S.land_mask.p, S.land_cell.p, S.x2.p,
-                                S.y2.p, S.v2.p, S.g2.p, S.pf2.p, S.new_off.p, nullptr, st));
-    else
+    if (N > 0) {  // the fused compaction (kept points in order, new frame offsets)
+      RPT_TRY(S.t.ensure(cap, st));
+      RPT_TRY(S.bnd.ensure(2 * sizeof(Bounds), st));
+      RPT_TRY(land_compact_dev(S.x.p, S.y.p, S.v.p, S.g.p, S.pf.p, N, S.land_cell.p,
+                               S.land_mask.p, F, S.x2.p, S.y2.p, S.v2.p, S.g2.p, S.pf2.p, S.t.p,
+                               S.new_off.p, reinterpret_cast<Bounds*>(S.bnd.p), st));
+    } else
       RPT_HIP(hipMemsetAsync(S.new_off.p, 0, sizeof(int64_t) * (F + 1), st));
     RPT_HIP(hipMemcpyAsync(hn, S.new_off.p, sizeof(int64_t) * (F + 1), hipMemcpyDeviceToHost,
                            st));
