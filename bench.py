@@ -16,6 +16,9 @@ At N=1 the whole stack runs on one MI355X (it fits: 288 GB HBM).
   --dense        configs[4]'s density (~500k points per frame, rpt.synth.dense_config)
   --h2d-steps K  also time K steps that first copy the echo from pinned host memory (reported
                  as `h2d_inclusive`, never as `value`)
+After the timed region (N=1, timing on), K5 is also timed on the configs[4] per-GPU share (125
+dense frames), where SURVEY.md §8(d) sets the 0.40 roofline target: `roofline_configs4_share`
+(`--no-dense-k5` skips it).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--total-frames T | --frames F] [--dense]
 """
@@ -107,6 +110,8 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-stage hipEvent timing")
+    ap.add_argument("--no-dense-k5", action="store_true",
+                    help="skip the K5 roofline leg at the configs[4] per-GPU share")
     ap.add_argument("--sharded", action="store_true",
                     help="run the frame-sharded (multi-GPU) pipeline even with one rank")
     ap.add_argument("--python-shard", action="store_true",
@@ -295,6 +300,28 @@ def main():
                 "avg_ms": round(k5, 4), "points": n_in}
     stage = {k: round(v / args.steps, 3) for k, v in stage_acc.items()}
 
+    # K5 again at the size SURVEY 8(d) sets its 0.40 target for: the configs[4] per-GPU share
+    # (125 dense frames, ~61 M points), after the timed region; hipEvents as above
+    roof_c4 = None
+    if rank == 0 and not dist and not args.dense and timing and not args.no_dense_k5:
+        from rpt.synth import dense_config
+        dcfg = dense_config(n_frames=125)
+        dds = DeviceSynth(dcfg, dev)
+        decho = dds.echo()
+        dpipe = FrameStackPipeline(dcfg.gains, dcfg.rows, dcfg.bins, PathParams(), dev,
+                                   timing=True)
+        dpipe.set_geometry(np.full(dcfg.rows, dcfg.scale, np.float32), dds.geo.cos_t,
+                           dds.geo.sin_t, dcfg.n_frames * len(dcfg.gains))
+        dres = [dpipe.run(decho).finish() for _ in range(4)][1:]  # one warm-up run
+        dk5 = float(np.mean([r.stage_ms["dbscan_core"] for r in dres]))
+        dn = dres[-1].n_clustered_input
+        dach = K5_BYTES_PER_POINT * dn / (dk5 * 1e-3) / 1e9
+        roof_c4 = {"workload": "configs[4] per-GPU share: 125 dense frames (~500k pts/frame)",
+                   "achieved": round(dach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": round(dach / HBM_PEAK_GBS, 4), "avg_ms": round(dk5, 4),
+                   "points": dn, "runs": len(dres)}
+        del dpipe, decho, dds
+
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and not dist:
         cf = min(args.cpu_frames, F)
@@ -336,7 +363,8 @@ def main():
                        "host_stage": "inline" if args.sync_host else
                        "overlapped: step k's order+tracker runs on a host thread during step "
                        "k+1's device work; the timed region ends after the last one"},
-            "roofline": roof, "cpu_baseline": cpu, "h2d_inclusive": h2d, "stage_ms": stage,
+            "roofline": roof, "roofline_configs4_share": roof_c4, "cpu_baseline": cpu,
+            "h2d_inclusive": h2d, "stage_ms": stage,
         }
         print(json.dumps(out), flush=True)
     if dist:
