@@ -16,6 +16,10 @@ At N=1 the whole stack runs on one MI355X (it fits: 288 GB HBM).
   --dense        configs[4]'s density (~500k points per frame, rpt.synth.dense_config)
   --h2d-steps K  also time K steps that first copy the echo from pinned host memory (reported
                  as `h2d_inclusive`, never as `value`)
+At N=1 two stacks are in flight by default (`--lanes 2`: native handles on two streams; step
+k+1's device work runs while step k's host stage and readbacks finish, and the two stacks'
+latency-bound kernels share the CUs); `one_stack_in_flight` repeats the steps strictly one after
+another, and K5's roofline is taken from that leg (K5 alone on the GPU).
 After the timed region (N=1, timing on), K5 is also timed on the configs[4] per-GPU share (125
 dense frames), where SURVEY.md §8(d) sets the 0.40 roofline target: `roofline_configs4_share`
 (`--no-dense-k5` skips it).
@@ -117,9 +121,9 @@ def main():
     ap.add_argument("--python-shard", action="store_true",
                     help="sharded runs: ShardedStackPipeline (HipOps stages composed in Python) "
                          "instead of the native shard driver")
-    ap.add_argument("--lanes", type=int, default=1,
+    ap.add_argument("--lanes", type=int, default=2,
                     help="single GPU: stacks in flight at once (native handles on separate "
-                         "streams, FrameStackPipeline.submit)")
+                         "streams, FrameStackPipeline.submit); 1 = strictly one after another")
     ap.add_argument("--sync-host", action="store_true",
                     help="run each step's host stage (order + tracker) inline instead of "
                          "overlapping it with the next step's device work")
@@ -244,6 +248,37 @@ def main():
     value = pts * args.steps / dt / 1e6
     ms_step = dt / args.steps * 1e3
 
+    # one stack in flight (lanes = 1): the same steps strictly one after another.  K5's roofline
+    # is taken here, where its kernels have the GPU to themselves (with two stacks in flight the
+    # other stack's kernels share the CUs and stretch every event-timed stage)
+    seq = None
+    if not dist and args.lanes > 1:
+        spipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), dev, timing=timing,
+                                   async_host=not args.sync_host, lanes=1)
+        spipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t,
+                           ds.geo.sin_t, cfg.n_frames * len(cfg.gains))
+        for _ in range(max(args.warmup, 1)):
+            resolve(spipe.submit(echo)).finish()
+        torch.cuda.synchronize(dev)
+        ts0 = time.perf_counter()
+        sres = [resolve(spipe.submit(echo)) for _ in range(args.steps)]
+        for r in sres:
+            r.finish()
+        torch.cuda.synchronize(dev)
+        dts = time.perf_counter() - ts0
+        seq = {"value": round(pts * args.steps / dts / 1e6, 3), "unit": "Mpoints/s",
+               "ms_per_step": round(dts / args.steps * 1e3, 3), "steps": args.steps,
+               "note": "same workload, one stack in flight (lanes=1)"}
+        if timing:
+            k5_ms = [r.stage_ms["dbscan_core"] for r in sres]
+            # per-stage times from this leg too: with two stacks in flight every event-timed
+            # stage also contains the other stack's interleaved kernels
+            stage_acc = {}
+            for r in sres:
+                for k, v in r.stage_ms.items():
+                    stage_acc[k] = stage_acc.get(k, 0.0) + v
+        del spipe
+
     # optional leg: the same steps with the echo's H2D copy from pinned host memory inside
     h2d = None
     if args.h2d_steps > 0:
@@ -291,6 +326,7 @@ def main():
         n_in = n_core_in
         achieved = K5_BYTES_PER_POINT * n_in / (k5 * 1e-3) / 1e9
         roof = {"kernel": "K5 = k_core_cells_oct + k_core_fill + k_core_slow (core flags)",
+                "measured_in": "one-stack-in-flight leg" if seq is not None else "timed steps",
                 "bound": "hbm",
                 "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -363,8 +399,10 @@ def main():
                        "host_stage": "inline" if args.sync_host else
                        "overlapped: step k's order+tracker runs on a host thread during step "
                        "k+1's device work; the timed region ends after the last one"},
+            "one_stack_in_flight": seq,
             "roofline": roof, "roofline_configs4_share": roof_c4, "cpu_baseline": cpu,
             "h2d_inclusive": h2d, "stage_ms": stage,
+            "stage_ms_from": "one_stack_in_flight" if seq is not None else "timed steps",
         }
         print(json.dumps(out), flush=True)
     if dist:
