@@ -184,6 +184,17 @@ def main():
                       (np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t)),
                 torch.tensor(list(cfg.gains) * F, dtype=torch.int32, device=dev))
             run = lambda: pipe.run(echo, _abi.ECHO_U8, rank * F)  # noqa: E731
+        elif args.lanes > 1:
+            # several stacks in flight (rpt.dist.ShardLanes: per lane a process group, stream and
+            # thread); K5 and the stage times come from the one-stack-in-flight leg below
+            from rpt.dist import ShardLanes
+
+            lanes_ = ShardLanes(dev, args.lanes, cfg.gains, cfg.rows, cfg.bins, PathParams(),
+                                timing=timing, async_host=not args.sync_host, host_workers=4)
+            lanes_.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t,
+                                ds.geo.sin_t, cfg.n_frames * len(cfg.gains))
+            ops = lanes_.pipes[0]
+            run = lambda: lanes_.submit(echo, rank * F)  # noqa: E731
         else:
             ops = pipe = NativeShardPipeline(Comm(dev), cfg.gains, cfg.rows, cfg.bins,
                                              PathParams(), timing=timing,
@@ -212,10 +223,11 @@ def main():
     k5_ms = []
     res = None
     results = []
+    sharded_lanes = dist and not args.python_shard and args.lanes > 1
     for _ in range(args.steps):
         res = run()
         results.append(res)
-        if timing and dist:
+        if timing and dist and not sharded_lanes:
             k5_ms.append(ops.last_core_ms())
     results = [resolve(r) for r in results]
     if timing and not dist:
@@ -252,6 +264,33 @@ def main():
     # is taken here, where its kernels have the GPU to themselves (with two stacks in flight the
     # other stack's kernels share the CUs and stretch every event-timed stage)
     seq = None
+    if sharded_lanes:  # every rank: lane 0's pipeline, one stack at a time
+        for _ in range(max(args.warmup, 1)):
+            ops.run(echo, rank * F).finish()
+        torch.cuda.synchronize(dev)
+        tdist.barrier()
+        ts0 = time.perf_counter()
+        sres = []
+        k5_ms = []
+        for _ in range(args.steps):
+            sres.append(ops.run(echo, rank * F))
+            if timing:
+                k5_ms.append(ops.last_core_ms())
+        for r in sres:
+            r.finish()
+        torch.cuda.synchronize(dev)
+        tdist.barrier()
+        t = torch.tensor([time.perf_counter() - ts0], dtype=torch.float64, device=dev)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dts = float(t[0])
+        seq = {"value": round(pts * args.steps / dts / 1e6, 3), "unit": "Mpoints/s",
+               "ms_per_step": round(dts / args.steps * 1e3, 3), "steps": args.steps,
+               "note": "same workload, one stack in flight per rank"}
+        if timing:
+            stage_acc = {}
+            for r in sres:
+                for k, v in r.stage_ms.items():
+                    stage_acc[k] = stage_acc.get(k, 0.0) + v
     if not dist and args.lanes > 1:
         spipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), dev, timing=timing,
                                    async_host=not args.sync_host, lanes=1)
@@ -395,7 +434,7 @@ def main():
                        "parallelism": (f"frame-sharded x{world}"
                                        f"{' (python stages)' if args.python_shard else ''}")
                        if dist else "single GPU",
-                       "stacks_in_flight": 1 if dist else args.lanes,
+                       "stacks_in_flight": 1 if args.python_shard else args.lanes,
                        "host_stage": "inline" if args.sync_host else
                        "overlapped: step k's order+tracker runs on a host thread during step "
                        "k+1's device work; the timed region ends after the last one"},

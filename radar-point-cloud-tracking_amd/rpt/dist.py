@@ -701,3 +701,51 @@ class NativeShardPipeline:
                                                       stream_handle(self.dev)),
                             "rpt_shard_labels")
         return out
+
+
+class ShardLanes:
+    """Several stacks in flight on the frame-sharded path: lane i owns a NativeShardPipeline
+    with its own process group (its own RCCL communicator, so one lane's collectives never
+    interleave with another's), its own HIP stream and one worker thread.  submit() hands the
+    stacks to the lanes in turn; every rank submits the same sequence, so each lane's collectives
+    pair up across ranks.  Step k+1's device work then runs while step k waits on collectives,
+    readbacks or its host stage -- the sharded form of FrameStackPipeline(lanes=...)."""
+
+    def __init__(self, dev: torch.device, lanes: int, gains: Sequence[int], rows: int,
+                 bins: int, params: PathParams = None, timing: bool = False,
+                 async_host: bool = False, host_workers: int = 2):
+        if lanes < 1:
+            raise ValueError("lanes must be >= 1")
+        self.dev = dev
+        world = dist.get_world_size()
+        groups = [None] + [dist.new_group(list(range(world))) for _ in range(lanes - 1)]
+        self.pipes = [NativeShardPipeline(Comm(dev, g), gains, rows, bins, params, timing=timing,
+                                          async_host=async_host, host_workers=host_workers)
+                      for g in groups]
+        self.streams = [torch.cuda.Stream(dev) for _ in range(lanes)] if lanes > 1 else [None]
+        self.pools = [ThreadPoolExecutor(max_workers=1) for _ in range(lanes)]
+        self._next = 0
+
+    def set_geometry(self, scale, cos_t, sin_t, n_files: int):
+        for p in self.pipes:
+            p.set_geometry(scale, cos_t, sin_t, n_files)
+
+    def submit(self, echo: torch.Tensor, frame0: int) -> Future:
+        """Runs the next lane on (echo, frame0); Future of its ShardResult (call finish())."""
+        li = self._next
+        self._next = (li + 1) % len(self.pipes)
+        pipe, s = self.pipes[li], self.streams[li]
+
+        def work():
+            with torch.cuda.device(self.dev):
+                if s is None:
+                    return pipe.run(echo, frame0)
+                s.wait_stream(torch.cuda.default_stream(self.dev))  # the echo is ready
+                with torch.cuda.stream(s):
+                    return pipe.run(echo, frame0)
+
+        return self.pools[li].submit(work)
+
+    def close(self):
+        for p in self.pools:
+            p.shutdown(wait=True)

@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--backend", default="gloo")
     ap.add_argument("--frames", type=int, default=14, help="frames per rank")
     ap.add_argument("--rows", type=int, default=4096)
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="native: stacks in flight (rpt.dist.ShardLanes); every lane's result "
+                         "is checked")
     ap.add_argument("--impl", default="native", choices=("native", "python"),
                     help="native: NativeShardPipeline (librpt shard driver); python: "
                          "ShardedStackPipeline over HipOps")
@@ -46,7 +49,7 @@ def main():
 
     from rpt import _abi
     from rpt.dist import Comm, NativeShardPipeline, ShardedStackPipeline
-    from rpt.pipeline import FrameStackPipeline, PathParams
+    from rpt.pipeline import PathParams
     from rpt.stages import HipOps
     from rpt.synth import DeviceSynth, SynthConfig
 
@@ -54,12 +57,25 @@ def main():
     cfg = SynthConfig(n_frames=F, rows=args.rows, frame0=rank * F)
     ds = DeviceSynth(cfg, dev)
     echo = ds.echo()
-    if args.impl == "native":
+    runs = []  # (result, this rank's labels) per checked run
+    if args.impl == "native" and args.lanes > 1:
+        from rpt.dist import ShardLanes
+
+        lanes = ShardLanes(dev, args.lanes, cfg.gains, cfg.rows, cfg.bins, PathParams())
+        lanes.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t,
+                           ds.geo.sin_t, F * 3)
+        futs = [lanes.submit(echo, rank * F) for _ in range(2 * args.lanes)]
+        outs = [f.result().finish() for f in futs]
+        torch.cuda.synchronize(dev)
+        for k, r in enumerate(outs[-args.lanes:]):  # the last run of every lane
+            runs.append((r, lanes.pipes[(len(outs) - args.lanes + k) % args.lanes].labels_local()))
+        lanes.close()
+    elif args.impl == "native":
         pipe = NativeShardPipeline(Comm(dev), cfg.gains, cfg.rows, cfg.bins, PathParams())
         pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
                           F * 3)
         res = pipe.run(echo, rank * F)
-        mine = pipe.labels_local()
+        runs.append((res, pipe.labels_local()))
     else:
         ops = HipOps(dev)
         pipe = ShardedStackPipeline(ops, Comm(dev), cfg.gains, cfg.rows, cfg.bins, PathParams())
@@ -67,8 +83,22 @@ def main():
                     (np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t))
         pipe.set_geometry(geo, torch.tensor(list(cfg.gains) * F, dtype=torch.int32, device=dev))
         res = pipe.run(echo, _abi.ECHO_U8, rank * F)
-        mine = res.labels_local
-    labels = Comm(dev).all_gather_var(mine.to(torch.int64))
+        runs.append((res, res.labels_local))
+    ok = True
+    for res, mine in runs:
+        ok &= check(res, Comm(dev).all_gather_var(mine.to(torch.int64)), rank, world, args, dev)
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    flag = Comm(dev).all_reduce(flag, dist.ReduceOp.MIN)
+    dist.destroy_process_group()
+    sys.exit(0 if int(flag.item()) == 1 else 1)
+
+
+def check(res, labels, rank, world, args, dev):
+    """Rank 0: the sharded run against the single-GPU pipeline over the whole stack."""
+    from rpt.pipeline import FrameStackPipeline, PathParams
+    from rpt.synth import DeviceSynth, SynthConfig
+
+    F = args.frames
     ok = True
     if rank == 0:
         full = SynthConfig(n_frames=F * world, rows=args.rows)
@@ -90,11 +120,8 @@ def main():
         ok &= all(np.array_equal(np.vstack(x.positions), np.vstack(y.positions)) for x, y in zip(a, b))
         print(f"[dist_check] world={world} backend={args.backend} impl={args.impl} points={res.n_points_global} "
               f"clusters={res.n_clusters} segments={res.n_segments} objects={len(a)} "
-              f"labels_equal={np.array_equal(got, exp)} ok={ok}", flush=True)
-    flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
-    flag = Comm(dev).all_reduce(flag, dist.ReduceOp.MIN)
-    dist.destroy_process_group()
-    sys.exit(0 if int(flag.item()) == 1 else 1)
+              f"labels_equal={np.array_equal(got, exp)} lanes={args.lanes} ok={ok}", flush=True)
+    return ok
 
 
 if __name__ == "__main__":
