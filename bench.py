@@ -121,9 +121,12 @@ def main():
     ap.add_argument("--python-shard", action="store_true",
                     help="sharded runs: ShardedStackPipeline (HipOps stages composed in Python) "
                          "instead of the native shard driver")
-    ap.add_argument("--lanes", type=int, default=2,
-                    help="single GPU: stacks in flight at once (native handles on separate "
-                         "streams, FrameStackPipeline.submit); 1 = strictly one after another")
+    ap.add_argument("--lanes", type=int, default=None,
+                    help="stacks in flight at once (default 2 on one GPU: native handles on "
+                         "separate streams; 1 with N>1 ranks, where a lane is also a process "
+                         "group -- rpt.dist.ShardLanes -- and several RCCL communicators "
+                         "sharing a rank's hardware queues can order their kernels differently "
+                         "on different GPUs); 1 = strictly one after another")
     ap.add_argument("--sync-host", action="store_true",
                     help="run each step's host stage (order + tracker) inline instead of "
                          "overlapping it with the next step's device work")
@@ -131,6 +134,8 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if args.lanes is None:
+        args.lanes = 2 if world == 1 and not args.sharded else 1
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # --sharded: the frame-sharded multi-GPU path even at one rank (measures its per-rank cost)
     dist = world > 1 or args.sharded
