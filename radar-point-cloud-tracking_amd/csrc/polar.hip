@@ -14,6 +14,7 @@
 // evaluates them exactly as the reference does (4096 values per sweep geometry).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -363,8 +364,6 @@ __global__ __launch_bounds__(kBlock) void k_group_count_u8(const uint8_t* __rest
       v[k] = (k < nr) ? *reinterpret_cast<const uint4*>(echo + (row0 + k) * 1024 + lane * 16)
                       : make_uint4(0u, 0u, 0u, 0u);
     if constexpr (STAGE) {
-      __shared__ GroupLds s_lds[kWavesPerBlock];
-      GroupLds& L = s_lds[threadIdx.x / 64];
       uint32_t m[kGroupRows];
       int c[kGroupRows], incl[kGroupRows];
 #pragma unroll
@@ -382,10 +381,14 @@ __global__ __launch_bounds__(kBlock) void k_group_count_u8(const uint8_t* __rest
         rb[k + 1] = rb[k] + (uint32_t)__builtin_amdgcn_readlane(incl[k], 63);
       const uint32_t total = rb[kGroupRows];
       if (total != 0u && total <= (uint32_t)kStageSlots) {  // wave-uniform
-        group_to_lds(L, lane, m, incl, v);
         uint32_t* e = entries + (int64_t)grp * kStageSlots;
-        for (uint32_t i = (uint32_t)lane; i < total; i += 64u) e[i] = kept_entry(L, rb, i);
-        wave_lds_sync();  // the slice is rewritten by the next group
+        {
+          __shared__ GroupLds s_lds[kWavesPerBlock];
+          GroupLds& L = s_lds[threadIdx.x / 64];
+          group_to_lds(L, lane, m, incl, v);
+          for (uint32_t i = (uint32_t)lane; i < total; i += 64u) e[i] = kept_entry(L, rb, i);
+          wave_lds_sync();  // the slice is rewritten by the next group
+        }
       }
       if (lane == 0) group_count[grp] = (int32_t)total;
       continue;
@@ -421,7 +424,9 @@ __global__ void k_file_counts_groups(const int64_t* __restrict__ gprefix, int64_
 // group's LDS slice (or, STAGED, read from the count pass's slot when the group was staged:
 // no echo read at all).  Outputs at or beyond cap are dropped: a speculative launch (sized by an
 // earlier run) is repeated by the caller when the count says it did not fit.
-template <bool HI, bool STAGED>
+// LIST: the groups are the first *list_n entries of list (the unstaged groups of the expand
+// write below), not 0 .. n_groups-1.
+template <bool HI, bool STAGED, bool LIST = false>
 __global__ __launch_bounds__(kBlock) void k_group_write_u8(
     const uint8_t* __restrict__ echo, uint32_t n_groups, GroupMap gm, uint32_t K, int stride,
     const float* __restrict__ scale, const float* __restrict__ cos_t,
@@ -429,7 +434,8 @@ __global__ __launch_bounds__(kBlock) void k_group_write_u8(
     const int64_t* __restrict__ gprefix, const int64_t* __restrict__ file_offsets,
     int files_per_frame, float* __restrict__ x, float* __restrict__ y, float* __restrict__ val,
     int32_t* __restrict__ gain_out, int32_t* __restrict__ pf_out, int64_t cap,
-    const uint32_t* __restrict__ entries) {
+    const uint32_t* __restrict__ entries, const uint32_t* __restrict__ list = nullptr,
+    const uint32_t* __restrict__ list_n = nullptr) {
   __shared__ GroupLds s_lds[kWavesPerBlock];
   const int lane = threadIdx.x & 63;
   GroupLds& L = s_lds[threadIdx.x / 64];
@@ -439,8 +445,9 @@ __global__ __launch_bounds__(kBlock) void k_group_write_u8(
   const bool pow2 = (us & (us - 1u)) == 0u;
   const uint32_t sh = (uint32_t)__builtin_ctz(us);
   const float inv_bins = 1.0f / 1024.0f;  // exact: step = scale / 1024 == scale * 2^-10
-  for (uint32_t g0 = wave0; g0 < n_groups; g0 += n_waves) {
-    const uint32_t grp = __builtin_amdgcn_readfirstlane(g0);
+  const uint32_t n_items = LIST ? *list_n : n_groups;
+  for (uint32_t g0 = wave0; g0 < n_items; g0 += n_waves) {
+    const uint32_t grp = __builtin_amdgcn_readfirstlane(LIST ? list[g0] : g0);
     uint32_t f;
     int64_t row0;
     int nr;
@@ -515,6 +522,222 @@ __global__ __launch_bounds__(kBlock) void k_group_write_u8(
   }
 }
 
+// ---- expand write: output slots to threads (staged groups)
+// The wave-per-group write above walks 3 M groups of ~16 outputs each with a dependent
+// prefix -> entry -> store chain per group; its time is that chain times the groups per wave
+// slot.  Here the outputs themselves are spread over the threads: per group one 64-bit word
+//   bits 0..39  gs    = global index of the group's first emitted output
+//   bits 40..62 phase = in-group kept rank of that output (first * stride - rank < stride)
+//   bit 63      the group emits outputs but kept > kStageSlots samples (not staged): its
+//               outputs are written by k_group_write_u8<.., LIST> over the list of such groups
+// and a block walks a contiguous range of 1024-output tiles, finding each output's group by a
+// binary search of an LDS window of those words (gs is non-decreasing in the group index).
+constexpr int kGsBits = 40;
+constexpr uint64_t kGsMask = (1ull << kGsBits) - 1ull;
+constexpr uint64_t kUnstaged = 1ull << 63;
+constexpr int kTileOut = 1024;  // outputs per block tile, 4 per thread
+constexpr int kOutPerThread = kTileOut / kBlock;
+static_assert(kOutPerThread == 4, "k_expand_write stores a thread's outputs as one 16-B vector");
+constexpr int kWin = 1024;  // groups in the LDS window
+
+__global__ __launch_bounds__(kBlock) void k_group_starts(const int64_t* __restrict__ gprefix,
+                                                        const int64_t* __restrict__ file_offsets,
+                                                        uint32_t n_groups, uint32_t gpf,
+                                                        uint32_t stride,
+                                                        uint64_t* __restrict__ gword,
+                                                        uint32_t* __restrict__ list,
+                                                        uint32_t* __restrict__ list_n) {
+  __shared__ uint32_t s_n, s_base;
+  for (uint32_t b0 = blockIdx.x * kBlock; b0 < n_groups; b0 += gridDim.x * kBlock) {
+    if (threadIdx.x == 0) s_n = 0u;
+    __syncthreads();
+    const uint32_t g = b0 + threadIdx.x;
+    bool un = false;
+    uint32_t slot = 0u;
+    if (g < n_groups) {
+      const uint32_t f = g / gpf;
+      const int64_t p0 = gprefix[g];
+      const uint64_t rank = (uint64_t)(p0 - gprefix[(int64_t)f * gpf]);
+      const uint64_t total = (uint64_t)(gprefix[g + 1] - p0);
+      const uint64_t first = (rank + stride - 1u) / stride;
+      const uint64_t last = (rank + total + stride - 1u) / stride;
+      const uint64_t gs = (uint64_t)file_offsets[f] + first;
+      const uint64_t phase = first * stride - rank;
+      un = last > first && total > (uint64_t)kStageSlots;
+      gword[g] = gs | (phase << kGsBits) | (un ? kUnstaged : 0ull);
+      if (un) slot = atomicAdd(&s_n, 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && s_n) s_base = atomicAdd(list_n, s_n);
+    __syncthreads();
+    if (un) list[s_base + slot] = g;
+  }
+}
+
+// largest g in [lo, hi) with gs(g) <= O, given gs(lo) <= O: one wave, 64-ary search
+__device__ uint32_t wave_find_group(const uint64_t* __restrict__ gword, uint32_t lo, uint32_t hi,
+                                    uint64_t O) {
+  const uint32_t lane = threadIdx.x & 63u;
+  while (hi - lo > 1u) {
+    const uint32_t step = (hi - lo + 63u) / 64u;
+    const uint32_t idx = lo + lane * step;
+    const bool le = idx < hi && (gword[idx] & kGsMask) <= O;  // a prefix of the lanes
+    const uint64_t m = __ballot(le);
+    const uint32_t top = 63u - (uint32_t)__clzll((long long)m);
+    lo = __builtin_amdgcn_readfirstlane(lo + top * step);
+    hi = min(hi, lo + step);
+  }
+  return lo;
+}
+
+// same, one thread (the rare outputs beyond the LDS window)
+__device__ uint32_t thread_find_group(const uint64_t* __restrict__ gword, uint32_t lo,
+                                      uint32_t hi, uint64_t O) {
+  while (hi - lo > 1u) {
+    const uint32_t mid = lo + (hi - lo) / 2u;
+    if ((gword[mid] & kGsMask) <= O)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+// largest j < wn with s_win[j].gs <= O (s_win[0].gs <= O)
+__device__ __forceinline__ uint32_t lds_find(const uint64_t* s_win, uint32_t wn, uint64_t O) {
+  uint32_t lo = 0u;
+#pragma unroll
+  for (uint32_t step = kWin / 2; step > 0u; step >>= 1)
+    if (lo + step < wn && (s_win[lo + step] & kGsMask) <= O) lo += step;
+  return lo;
+}
+
+// VEC: every output array is 16-B aligned (float4 / int4 stores of a thread's 4 outputs)
+template <bool VEC>
+__global__ __launch_bounds__(kBlock) void k_expand_write(
+    const uint64_t* __restrict__ gword, uint32_t n_groups, GroupMap gm, uint32_t stride,
+    const float* __restrict__ scale, const float* __restrict__ cos_t,
+    const float* __restrict__ sin_t, const int32_t* __restrict__ gain,
+    const int64_t* __restrict__ total_out, int files_per_frame, float* __restrict__ x,
+    float* __restrict__ y, float* __restrict__ val, int32_t* __restrict__ gain_out,
+    int32_t* __restrict__ pf_out, int64_t cap, const uint32_t* __restrict__ entries) {
+  __shared__ uint64_t s_win[kWin];
+  __shared__ uint32_t s_glo;
+  const int64_t total = min(*total_out, cap);
+  const int64_t n_tiles = (total + kTileOut - 1) / kTileOut;
+  const int64_t t0 = n_tiles * blockIdx.x / gridDim.x;
+  const int64_t t1 = n_tiles * (blockIdx.x + 1) / gridDim.x;
+  if (t0 >= t1) return;  // block-uniform
+  if (threadIdx.x < 64) {
+    const uint32_t g = wave_find_group(gword, 0u, n_groups, (uint64_t)t0 * kTileOut);
+    if (threadIdx.x == 0) s_glo = g;
+  }
+  __syncthreads();
+  const float inv_bins = 1.0f / 1024.0f;  // exact: step = scale / 1024 == scale * 2^-10
+  for (int64_t t = t0; t < t1; ++t) {
+    const uint32_t glo = s_glo;
+    const uint32_t wn = min((uint32_t)kWin, n_groups - glo);
+    for (uint32_t j = threadIdx.x; j < (uint32_t)kWin; j += kBlock)
+      s_win[j] = j < wn ? gword[glo + j] : ~0ull;
+    __syncthreads();
+    const bool truncated = glo + wn < n_groups;
+    const uint64_t O0 = (uint64_t)t * kTileOut;
+    // phase A: this thread's kOutPerThread consecutive outputs: the first one's group by the LDS
+    // search, the others by stepping over group starts (empty groups share their successor's)
+    auto word = [&](uint32_t g) -> uint64_t {
+      return (g - glo < wn) ? s_win[g - glo] : gword[g];
+    };
+    auto next_gs = [&](uint32_t g) -> uint64_t {
+      return g + 1u < n_groups ? (word(g + 1u) & kGsMask) : ~0ull;
+    };
+    const uint64_t Ob = O0 + (uint64_t)threadIdx.x * kOutPerThread;
+    uint32_t grp[kOutPerThread], idx[kOutPerThread];
+    bool ok[kOutPerThread];
+    if ((int64_t)Ob < total) {
+      const uint32_t j = lds_find(s_win, wn, Ob);
+      uint32_t g = (j == wn - 1u && truncated) ? thread_find_group(gword, glo + j, n_groups, Ob)
+                                               : glo + j;
+      uint64_t w = word(g), nx = next_gs(g);
+#pragma unroll
+      for (int k = 0; k < kOutPerThread; ++k) {
+        const uint64_t O = Ob + k;
+        const bool in = (int64_t)O < total;
+        while (in && O >= nx) {
+          ++g;
+          w = word(g);
+          nx = next_gs(g);
+        }
+        ok[k] = in && !(w & kUnstaged);
+        grp[k] = g;
+        idx[k] = (uint32_t)((O - (w & kGsMask)) * stride + ((w & ~kUnstaged) >> kGsBits));
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kOutPerThread; ++k) {
+        ok[k] = false;
+        grp[k] = glo;
+        idx[k] = 0u;
+      }
+    }
+    // the next tile's first group (thread 0), before the window is rewritten
+    if (threadIdx.x == 0 && t + 1 < t1) {
+      const uint64_t On = O0 + kTileOut;
+      const uint32_t j = lds_find(s_win, wn, On);
+      s_glo = (j == wn - 1u && truncated) ? thread_find_group(gword, glo + j, n_groups, On)
+                                          : glo + j;
+    }
+    // phase B: the staged entries, then the rows' geometry, then the stores
+    uint32_t ent[kOutPerThread];
+#pragma unroll
+    for (int k = 0; k < kOutPerThread; ++k)
+      ent[k] = ok[k] ? entries[(int64_t)grp[k] * kStageSlots + idx[k]] : 0u;
+    float sc[kOutPerThread], cc[kOutPerThread], ss[kOutPerThread];
+    uint32_t fl[kOutPerThread];
+#pragma unroll
+    for (int k = 0; k < kOutPerThread; ++k) {
+      const uint32_t f = grp[k] / gm.gpf;
+      fl[k] = f;
+      const int64_t row = (int64_t)f * gm.rows +
+                          (int64_t)(grp[k] - f * gm.gpf) * kGroupRows + (ent[k] >> 18);
+      sc[k] = ok[k] ? scale[row] : 0.f;
+      cc[k] = ok[k] ? cos_t[row] : 0.f;
+      ss[k] = ok[k] ? sin_t[row] : 0.f;
+    }
+    float ox[kOutPerThread], oy[kOutPerThread], ov[kOutPerThread];
+    int32_t og[kOutPerThread], op[kOutPerThread];
+    bool all_ok = true;
+#pragma unroll
+    for (int k = 0; k < kOutPerThread; ++k) {
+      const float rr = sc[k] * inv_bins * (float)((ent[k] >> 8) & 1023u);
+      ox[k] = rr * cc[k];
+      oy[k] = rr * ss[k];
+      ov[k] = (float)(ent[k] & 0xffu);
+      og[k] = gain ? gain[fl[k]] : 0;
+      op[k] = (int32_t)(fl[k] / (uint32_t)files_per_frame);
+      all_ok = all_ok && ok[k];
+    }
+    if (VEC && all_ok) {  // 16-B stores (the common case)
+      *reinterpret_cast<float4*>(x + Ob) = make_float4(ox[0], ox[1], ox[2], ox[3]);
+      *reinterpret_cast<float4*>(y + Ob) = make_float4(oy[0], oy[1], oy[2], oy[3]);
+      *reinterpret_cast<float4*>(val + Ob) = make_float4(ov[0], ov[1], ov[2], ov[3]);
+      if (gain_out) *reinterpret_cast<int4*>(gain_out + Ob) = make_int4(og[0], og[1], og[2], og[3]);
+      if (pf_out) *reinterpret_cast<int4*>(pf_out + Ob) = make_int4(op[0], op[1], op[2], op[3]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < kOutPerThread; ++k) {
+        if (!ok[k]) continue;
+        const uint64_t oo = Ob + k;
+        x[oo] = ox[k];
+        y[oo] = oy[k];
+        val[oo] = ov[k];
+        if (gain_out) gain_out[oo] = og[k];
+        if (pf_out) pf_out[oo] = op[k];
+      }
+    }
+    __syncthreads();  // s_win and s_glo of the next tile
+  }
+}
+
 // integer threshold of u8 samples (see keep_bits)
 inline int u8_threshold(float thr) {
   if (!(thr == thr)) return 255;
@@ -537,6 +760,17 @@ bool grouped_u8(const T* echo, int bins) {
 
 inline uint32_t u8_k(int T) {
   return (uint32_t)(T <= 127 ? 127 - T : 255 - T) * 0x01010101u;
+}
+
+// k_expand_write: a persistent grid (8 blocks per CU of the 256; each walks a contiguous tile
+// range).  RPT_K1_EXPAND=0 keeps the wave-per-group write for A/B runs.
+constexpr int kExpandBlocks = 2048;
+inline bool expand_write_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("RPT_K1_EXPAND");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
 }
 
 template <class T>
@@ -621,6 +855,51 @@ int32_t write_impl(const T* echo, int64_t n_files, int rows, int bins, float thr
     const int grid = grid_for(n_groups, kWavesPerBlock, 16384);
     const int T8 = u8_threshold(thr);
     const auto* e8 = reinterpret_cast<const uint8_t*>(echo);
+    if (entries && expand_write_enabled() && stride < (1 << 23) &&
+        n_files * (int64_t)rows * 1024 < (int64_t(1) << kGsBits)) {
+      // staged entries: outputs to threads (k_expand_write); the few unstaged groups listed by
+      // k_group_starts are written by the wave-per-group kernel
+      Scratch& sc = scratch(st);
+      Budget b;
+      b.add<uint64_t>(n_groups);
+      b.add<uint32_t>(n_groups);
+      b.add<uint32_t>(1);
+      RPT_TRY(sc.reserve(b.bytes, st));
+      uint64_t* gword = sc.carve_n<uint64_t>(n_groups);
+      uint32_t* list = sc.carve_n<uint32_t>(n_groups);
+      uint32_t* list_n = sc.carve_n<uint32_t>(1);
+      RPT_HIP(hipMemsetAsync(list_n, 0, sizeof(uint32_t), st));
+      hipLaunchKernelGGL(k_group_starts, dim3(grid_for(n_groups, kBlock, 4096)), dim3(kBlock), 0,
+                         st, row_prefix, file_offsets, (uint32_t)n_groups, gm.gpf,
+                         (uint32_t)stride, gword, list, list_n);
+      RPT_CHECK_LAUNCH();
+      auto al16 = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
+      const bool vec4 = al16(x) && al16(y) && al16(v) && (!gout || al16(gout)) && (!pf || al16(pf));
+      if (vec4)
+        hipLaunchKernelGGL(k_expand_write<true>, dim3(kExpandBlocks), dim3(kBlock), 0, st, gword,
+                           (uint32_t)n_groups, gm, (uint32_t)stride, geo.scale, geo.cos_t,
+                           geo.sin_t, gain, file_offsets + n_files, fpf, x, y, v, gout, pf, cap,
+                           entries);
+      else
+        hipLaunchKernelGGL(k_expand_write<false>, dim3(kExpandBlocks), dim3(kBlock), 0, st,
+                           gword, (uint32_t)n_groups, gm, (uint32_t)stride, geo.scale, geo.cos_t,
+                           geo.sin_t, gain, file_offsets + n_files, fpf, x, y, v, gout, pf, cap,
+                           entries);
+      RPT_CHECK_LAUNCH();
+      const int lgrid = std::min(grid, 2048);
+#define RPT_K1L(HI)                                                                            \
+  hipLaunchKernelGGL((k_group_write_u8<HI, false, true>), dim3(lgrid), dim3(kBlock), 0, st, e8, \
+                     (uint32_t)n_groups, gm, u8_k(T8), stride, geo.scale, geo.cos_t, geo.sin_t,  \
+                     gain, row_prefix, file_offsets, fpf, x, y, v, gout, pf, cap, entries, list, \
+                     list_n)
+      if (T8 <= 127)
+        RPT_K1L(false);
+      else
+        RPT_K1L(true);
+#undef RPT_K1L
+      RPT_CHECK_LAUNCH();
+      return RPT_OK;
+    }
 #define RPT_K1W(HI, M)                                                                       \
   hipLaunchKernelGGL((k_group_write_u8<HI, M>), dim3(grid), dim3(kBlock), 0, st, e8,          \
                      (uint32_t)n_groups, gm, u8_k(T8), stride, geo.scale, geo.cos_t, geo.sin_t, \

@@ -445,9 +445,10 @@ def test_k1_staged_entries_match_two_full_reads(gpu):
     them, the write pass reads those instead of the echo; denser groups read the echo again)
     against the two-full-read kernels: thresholds on both sides of 127 and at the ends, strides
     1/3/4/7, short last groups, an empty file between others, and densities from all-staged to
-    none-staged with mixed groups in between."""
+    none-staged with mixed groups in between, and a nearly empty stack whose 1024-output tiles
+    span more groups than the expand write's LDS window (its global-search fallback)."""
     rng = np.random.default_rng(17)
-    for rows, p in ((4096, 0.02), (1023, 0.5), (6, 1.0), (37, 0.0), (512, 0.03)):
+    for rows, p in ((4096, 0.02), (1023, 0.5), (6, 1.0), (37, 0.0), (512, 0.03), (4096, 2e-5)):
         echo = np.where(rng.random((6, rows, 1024)) < p, rng.integers(0, 256, (6, rows, 1024)),
                         0).astype(np.uint8)
         echo[2] = 0
