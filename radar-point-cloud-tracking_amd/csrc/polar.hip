@@ -293,9 +293,9 @@ __device__ __forceinline__ void group_rows(const GroupMap& gm, uint32_t grp, uin
 // the row's inclusive counts, bit by nth_bit16 of that lane's mask.  Work goes to the OUTPUT slots
 // (consecutive lanes, full-width stores) instead of walking each input lane's mask bits, so a
 // dense lane no longer holds its whole wave in a divergent loop.
-struct GroupLds {
-  int incl[kGroupRows][64];
-  uint32_t mask[kGroupRows][64];
+struct GroupLds {  // 5 KiB per wave: 8 waves per SIMD fit the LDS (u16 counts and masks)
+  uint16_t incl[kGroupRows][64];  // <= 1024
+  uint16_t mask[kGroupRows][64];
   uint32_t bytes[kGroupRows][256];  // the group's 4 KiB of samples
 };
 
@@ -310,8 +310,8 @@ __device__ __forceinline__ void group_to_lds(GroupLds& L, int lane, const uint32
                                              const uint4 (&vv)[kGroupRows]) {
 #pragma unroll
   for (int k = 0; k < kGroupRows; ++k) {
-    L.incl[k][lane] = incl[k];
-    L.mask[k][lane] = m[k];
+    L.incl[k][lane] = (uint16_t)incl[k];
+    L.mask[k][lane] = (uint16_t)m[k];
     *reinterpret_cast<uint4*>(&L.bytes[k][lane * 4]) = vv[k];
   }
   wave_lds_sync();
@@ -323,13 +323,13 @@ __device__ __forceinline__ uint32_t kept_entry(const GroupLds& L,
                                                const uint32_t (&rb)[kGroupRows + 1], uint32_t i) {
   const int k = (i >= rb[1]) + (i >= rb[2]) + (i >= rb[3]);
   const int ir = (int)(i - rb[k]);
-  const int* inc = L.incl[k];
+  const uint16_t* inc = L.incl[k];
   int lo = 0;  // lanes whose inclusive count is <= ir
 #pragma unroll
   for (int step = 32; step > 0; step >>= 1)
     if (inc[lo + step - 1] <= ir) lo += step;
   const uint32_t msk = L.mask[k][lo];
-  const int j = ir - (inc[lo] - __popc(msk));
+  const int j = ir - ((int)inc[lo] - __popc(msk));
   const int bit = nth_bit16(msk, (uint32_t)j);
   const int bin = lo * 16 + bit;
   const uint32_t w = L.bytes[k][bin >> 2];
@@ -382,13 +382,11 @@ __global__ __launch_bounds__(kBlock) void k_group_count_u8(const uint8_t* __rest
       const uint32_t total = rb[kGroupRows];
       if (total != 0u && total <= (uint32_t)kStageSlots) {  // wave-uniform
         uint32_t* e = entries + (int64_t)grp * kStageSlots;
-        {
-          __shared__ GroupLds s_lds[kWavesPerBlock];
-          GroupLds& L = s_lds[threadIdx.x / 64];
-          group_to_lds(L, lane, m, incl, v);
-          for (uint32_t i = (uint32_t)lane; i < total; i += 64u) e[i] = kept_entry(L, rb, i);
-          wave_lds_sync();  // the slice is rewritten by the next group
-        }
+        __shared__ GroupLds s_lds[kWavesPerBlock];
+        GroupLds& L = s_lds[threadIdx.x / 64];
+        group_to_lds(L, lane, m, incl, v);
+        for (uint32_t i = (uint32_t)lane; i < total; i += 64u) e[i] = kept_entry(L, rb, i);
+        wave_lds_sync();  // the slice is rewritten by the next group
       }
       if (lane == 0) group_count[grp] = (int32_t)total;
       continue;
