@@ -8,6 +8,7 @@
 // Counts are int32 atomics (order-free); intensity sums are float64 atomics, exact for the
 // integer echo values of the radar path (sums < 2^53), like np.add.at's sequential order.
 #include <climits>
+#include <cstdlib>
 #include <cstring>
 
 #include <algorithm>
@@ -195,6 +196,63 @@ __global__ __launch_bounds__(kGridBlock) void k_land_grid_lds(const float* __res
     if (k) {
       atomicAdd(cnt + c, k);
       atomicAdd(tot + c, lds_t[c]);
+    }
+  }
+}
+
+// Same, for intensities that are integers in [0, 255] (u8 echo samples): one packed u64 LDS
+// atomic per point, count << 40 | sum (a block's per-cell count < 2^24 and sum < 2^40, checked by
+// the caller), instead of an int32 and a float64 atomic.  Integer sums below 2^53 are exact in any
+// order, so the float64 grid equals the unpacked kernel's.
+constexpr int kPackShift = 40;
+__global__ __launch_bounds__(kGridBlock) void k_land_grid_lds_u8(
+    const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ val,
+    int64_t n, const double* __restrict__ xe, int nxe, const double* __restrict__ ye, int nye,
+    int32_t* __restrict__ cnt, double* __restrict__ tot, int32_t* __restrict__ cell_out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* lds_e = reinterpret_cast<double*>(smem);  // nxe + nye edges
+  const int ne = nxe + nye;
+  const int ne_al = (ne + 1) & ~1;
+  unsigned long long* lds_p = reinterpret_cast<unsigned long long*>(lds_e + ne_al);
+  const int ny = nye - 1;
+  const int cells = (nxe - 1) * ny;
+  for (int i = threadIdx.x; i < nxe; i += blockDim.x) lds_e[i] = xe[i];
+  for (int i = threadIdx.x; i < nye; i += blockDim.x) lds_e[nxe + i] = ye[i];
+  for (int c = threadIdx.x; c < cells; c += blockDim.x) lds_p[c] = 0ull;
+  __syncthreads();
+  const double* ex = lds_e;
+  const double* ey = lds_e + nxe;
+  const double idx_ = 1.0 / (ex[1] - ex[0]), idy_ = 1.0 / (ey[1] - ey[0]);
+  // one 1024-thread block per CU: kU points per thread per round, loads issued together (16
+  // waves alone keep too few bytes in flight)
+  constexpr int kU = 8;
+  const int64_t chunk = (int64_t)kGridBlock * kU;
+  for (int64_t b0 = (int64_t)blockIdx.x * chunk; b0 < n; b0 += (int64_t)gridDim.x * chunk) {
+    float px[kU], py[kU], pv[kU];
+#pragma unroll
+    for (int k = 0; k < kU; ++k) {
+      const int64_t i = b0 + (int64_t)k * kGridBlock + threadIdx.x;
+      px[k] = i < n ? x[i] : 0.f;
+      py[k] = i < n ? y[i] : 0.f;
+      pv[k] = i < n ? val[i] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < kU; ++k) {
+      const int64_t i = b0 + (int64_t)k * kGridBlock + threadIdx.x;
+      if (i >= n) break;
+      const int ix = clip_idx(count_le_arith(ex, nxe, (double)px[k], idx_) - 1, nxe - 2);
+      const int iy = clip_idx(count_le_arith(ey, nye, (double)py[k], idy_) - 1, nye - 2);
+      const int c = ix * ny + iy;
+      if (cell_out) cell_out[i] = c;
+      atomicAdd(lds_p + c, (1ull << kPackShift) | (unsigned long long)(uint32_t)pv[k]);
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < cells; c += blockDim.x) {
+    const unsigned long long v = lds_p[c];
+    if (v) {
+      atomicAdd(cnt + c, (int32_t)(v >> kPackShift));
+      atomicAdd(tot + c, (double)(v & ((1ull << kPackShift) - 1ull)));
     }
   }
 }
@@ -548,10 +606,21 @@ int32_t bounds_xy(const float* x, const float* y, int64_t n, float* out4, hipStr
   return RPT_OK;
 }
 
+// RPT_LAND_U8=0: the int32 + float64 atomics kernel also for u8 points (A/B)
+static bool land_u8_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("RPT_LAND_U8");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+
 // cell_out (nullable, [n], int32 cells < 2^31): each point's grid cell, for land_filter_cells
+// u8_vals: every val is an integer in [0, 255] (points of a u8 echo; packed-atomic kernel)
 int32_t land_grid_cells(const float* x, const float* y, const float* val, int64_t n,
                         const double* xe, int32_t nxe, const double* ye, int32_t nye,
-                        int32_t* cnt, double* tot, int32_t* cell_out, hipStream_t st) {
+                        int32_t* cnt, double* tot, int32_t* cell_out, hipStream_t st,
+                        int32_t u8_vals) {
   if (nxe < 2 || nye < 2) {
     set_error("rpt_land_grid: need at least two edges per axis");
     return RPT_EINVAL;
@@ -563,13 +632,21 @@ int32_t land_grid_cells(const float* x, const float* y, const float* val, int64_
   if (n == 0) return RPT_OK;
   const int64_t ne_al = ((int64_t)nxe + nye + 1) & ~int64_t(1);
   const size_t lds = (size_t)ne_al * 8 + (size_t)cells * 12;
-  if (cells <= kLdsGridCells && lds <= 150 * 1024) {
+  const size_t lds_u8 = (size_t)ne_al * 8 + (size_t)cells * 8;
+  int dev = 0, n_cu = 0;
+  RPT_HIP(hipGetDevice(&dev));
+  RPT_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  const int gb = grid_for(n, kGridBlock, std::max(n_cu, 1));
+  if (u8_vals && lds_u8 <= 150 * 1024 && (n + gb - 1) / gb < (int64_t(1) << 24) &&
+      land_u8_enabled()) {
+    RPT_HIP(hipFuncSetAttribute((const void*)k_land_grid_lds_u8,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_u8));
+    hipLaunchKernelGGL(k_land_grid_lds_u8, dim3(gb), dim3(kGridBlock), lds_u8, st, x, y, val, n,
+                       xe, nxe, ye, nye, cnt, tot, cell_out);
+  } else if (cells <= kLdsGridCells && lds <= 150 * 1024) {
     RPT_HIP(hipFuncSetAttribute((const void*)k_land_grid_lds,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    int dev = 0, n_cu = 0;
-    RPT_HIP(hipGetDevice(&dev));
-    RPT_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-    hipLaunchKernelGGL(k_land_grid_lds, dim3(grid_for(n, kGridBlock, std::max(n_cu, 1))),
+    hipLaunchKernelGGL(k_land_grid_lds, dim3(gb),
                        dim3(kGridBlock), lds, st, x, y, val, n, xe, nxe, ye, nye, cnt, tot,
                        cell_out);
   } else {
@@ -583,7 +660,7 @@ int32_t land_grid_cells(const float* x, const float* y, const float* val, int64_
 int32_t land_grid(const float* x, const float* y, const float* val, int64_t n, const double* xe,
                   int32_t nxe, const double* ye, int32_t nye, int32_t* cnt, double* tot,
                   hipStream_t st) {
-  return land_grid_cells(x, y, val, n, xe, nxe, ye, nye, cnt, tot, nullptr, st);
+  return land_grid_cells(x, y, val, n, xe, nxe, ye, nye, cnt, tot, nullptr, st, 0);
 }
 
 // n_land_dev: int32 land-cell counter on the device, zeroed by the caller (no readback)

@@ -36,7 +36,8 @@ int32_t frame_times(const int32_t* pf, int64_t n, const int64_t* ids, float* t, 
 int32_t bounds_xy(const float* x, const float* y, int64_t n, float* out4, hipStream_t st);
 int32_t land_grid_cells(const float* x, const float* y, const float* val, int64_t n,
                         const double* xe, int32_t nxe, const double* ye, int32_t nye,
-                        int32_t* cnt, double* tot, int32_t* cell_out, hipStream_t st);
+                        int32_t* cnt, double* tot, int32_t* cell_out, hipStream_t st,
+                        int32_t u8_vals);
 int32_t land_mask(const int32_t* cnt, const double* tot, int64_t cells, int64_t num_frames,
                   double pthr, double ithr, uint8_t* land, int64_t* n_land_host,
                   hipStream_t st);
@@ -411,7 +412,7 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
     RPT_TRY(land_mask.ensure((size_t)cells, st));
     RPT_TRY(land_cell.ensure(cap, st));
     RPT_TRY(land_grid_cells(x.p, y.p, v.p, N, edges.p, nxe, edges.p + nxe, nye, land_cnt.p,
-                            land_tot.p, land_cell.p, st));
+                            land_tot.p, land_cell.p, st, p.echo_dtype == RPT_ECHO_U8 ? 1 : 0));
     // the land-cell count accumulates (int32) into the low half of a zeroed int64 slot
     RPT_TRY(scal.ensure(4, st));
     RPT_HIP(hipMemsetAsync(scal.p, 0, sizeof(int64_t), st));
@@ -976,7 +977,8 @@ int32_t rpt_shard_land_grid(rpt_shard* h, const float* gbounds, double* grid, in
   RPT_TRY(S.land_cnt.ensure((size_t)cells, st));
   RPT_TRY(S.land_cell.ensure(cap, st));
   RPT_TRY(land_grid_cells(S.x.p, S.y.p, S.v.p, h->n_points, S.edges.p, nxe, S.edges.p + nxe,
-                          nye, S.land_cnt.p, grid + cells, S.land_cell.p, st));
+                          nye, S.land_cnt.p, grid + cells, S.land_cell.p, st,
+                          h->p.echo_dtype == RPT_ECHO_U8 ? 1 : 0));
   hipLaunchKernelGGL(k_cnt_to_f64, dim3(grid_for(cells, 256, 1024)), dim3(256), 0, st,
                      S.land_cnt.p, cells, grid);
   RPT_CHECK_LAUNCH();
