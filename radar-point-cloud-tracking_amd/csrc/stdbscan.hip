@@ -1033,6 +1033,9 @@ __device__ __forceinline__ XcdRange xcd_items(int64_t n_items, bool remap) {
 
 // ---------------------------------------------------------------- K5: core flags
 constexpr int kR = 4;  // candidate cells per lane per super-round of the window scans
+static_assert(kR >= 2, "the union passes' candidate masks cover two 64-position rounds");
+// k_union_cells: the top bit of a cell's candidate mask = "not recorded, enumerate the window"
+constexpr uint32_t kPmaskFull = 0x80000000u;
 
 // Level 1, one thread per occupied cell: a mutual cell (every pair adjacent) holding >=
 // min_samples points is all core — the bulk of a radar stack.  Every other cell is queued for
@@ -1637,7 +1640,8 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
                                                        const uint8_t* __restrict__ mutual,
                                                        const int32_t* __restrict__ sorig,
                                                        int32_t* __restrict__ parent,
-                                                       int uf_flags) {
+                                                       int uf_flags,
+                                                       uint4* __restrict__ pmask = nullptr) {
   const int lane = threadIdx.x & 63;
   const bool halve = !(uf_flags & 1);
   const XcdRange xr = xcd_items(*n_occ, (uf_flags & 2) != 0);
@@ -1656,9 +1660,33 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
     // time ranges are checked by classify_cells, so the slab window is not shrunk first
     const int sa = (int)((int64_t)ca / ((int64_t)g.nx * g.ny * g.nz));
     const Window w = make_window<D, false>(cx, cy, cz, A2.z, A2.w, g, slab_t, sa);
+    // PARTIAL with the first pass's mask of this cell's undecided candidates (window positions
+    // < 127): only those are visited, no enumeration or classification of the window again
+    uint4 pm = make_uint4(0u, 0u, 0u, kPmaskFull);
+    if (PARTIAL && pmask) pm = pmask[q];
+    const bool listed = PARTIAL && !(pm.w & kPmaskFull);
     for (int base = 0; base < w.total; base += 64 * kR) {
       int64_t cb[kR];
       uint32_t wb[kR];
+      int rb[kR], cls[kR], ebv[kR], bbv[kR];
+      if (listed) {
+#pragma unroll
+        for (int k = 0; k < kR; ++k) {
+          rb[k] = -1;
+          cls[k] = 0;
+          ebv[k] = 0;
+          bbv[k] = 0;
+          const uint32_t word = k == 0 ? (lane < 32 ? pm.x : pm.y) : (lane < 32 ? pm.z : pm.w);
+          if (k < 2 && ((word >> (lane & 31)) & 1u)) {
+            const int64_t c = window_cell<D>(w, k * 64 + lane, g, slab_t, A2.z, A2.w);
+            const CellRec<D> cr = crec[c];
+            rb[k] = rep[c];
+            ebv[k] = cr.e;
+            bbv[k] = cr.b;
+            cls[k] = 2;
+          }
+        }
+      } else {
 #pragma unroll
       for (int k = 0; k < kR; ++k) {
         const int qq = base + k * 64 + lane;
@@ -1667,7 +1695,6 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
       }
 #pragma unroll
       for (int k = 0; k < kR; ++k) wb[k] = (cb[k] >= 0) ? occ_bits[cb[k] >> 5] : 0u;
-      int rb[kR], cls[kR], ebv[kR], bbv[kR];
 #pragma unroll
       for (int k = 0; k < kR; ++k) {
         rb[k] = -1;
@@ -1686,7 +1713,16 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
           }
         }
       }
+      }
       if (!PARTIAL) {
+        if (pmask && base == 0) {  // the undecided candidates for the second pass
+          const uint64_t m0 = __ballot(cls[0] == 2), m1 = __ballot(cls[1] == 2);
+          if (lane == 0)
+            pmask[q] = (w.total < 128)
+                           ? make_uint4((uint32_t)m0, (uint32_t)(m0 >> 32), (uint32_t)m1,
+                                        (uint32_t)(m1 >> 32) & ~kPmaskFull)
+                           : make_uint4(0u, 0u, 0u, kPmaskFull);
+        }
         if (uf_flags & 4) continue;  // timing experiment only
         // neighbours' roots in parallel, then ONE unite per distinct root (dense regions give
         // a dozen box-certain neighbours that mostly share a root already)
@@ -2367,6 +2403,9 @@ struct DbscanState {
   uint64_t* cell_min_pair = nullptr;         // per cell (min core original index, its sorted index)
   void* crec = nullptr;                      // CellRec<dim>[C + 1]
   uint32_t* occ_bits = nullptr;              // 1 bit per cell
+  uint4* pmask = nullptr;  // union passes' undecided-candidate masks per occupied cell (aliases
+                           // the grid build's radix key buffers, dead after the build)
+  int union_list = -1;     // RPT_UNION_LIST=0: the second union pass enumerates every window
   int uf_flags = -1;                         // see XcdRange; -1 = read RPT_UF_FLAGS once
   int k5_legacy = -1;                        // 1: round-1 K5 (fill + point queue); RPT_K5_MODE
   int k5_fill = 0;
@@ -2535,6 +2574,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   uint32_t* vals = arena.carve_n<uint32_t>(n);
   uint32_t* keys_alt = arena.carve_n<uint32_t>(n);
   uint32_t* vals_alt = arena.carve_n<uint32_t>(n);
+  pmask = reinterpret_cast<uint4*>(keys);  // 4 x n u32, contiguous: room for n_occ <= n masks
   int64_t* rtmp = arena.carve_n<int64_t>(radix_tmp_elems(n));
   pts = arena.carve_n<float4>(n);
   sorig = arena.carve_n<int32_t>(n);
@@ -2742,13 +2782,18 @@ int32_t DbscanState::union_pass(hipStream_t st) {
                      cmin);
   hipLaunchKernelGGL(k_parent_init_pair, dim3(gb), dim3(kBlock), 0, st, parent, n, core, skey,
                      mutual, cmin, C, rep);
+  if (union_list < 0) {
+    const char* e = std::getenv("RPT_UNION_LIST");
+    union_list = (e && std::atoi(e) == 0) ? 0 : 1;
+  }
   if (dim == 2) {
+    uint4* pm = union_list ? pmask : nullptr;
     hipLaunchKernelGGL((k_union_cells<2, false>), dim3(gw), dim3(kBlock), 0, st, pts, g,
                        cell_start, occ, n_occ, rec<2>(), occ_bits, slab_t, core, rep, mutual, sorig,
-                       parent, uf_flags);
+                       parent, uf_flags, pm);
     hipLaunchKernelGGL((k_union_cells<2, true>), dim3(gw), dim3(kBlock), 0, st, pts, g,
                        cell_start, occ, n_occ, rec<2>(), occ_bits, slab_t, core, rep, mutual, sorig,
-                       parent, uf_flags);
+                       parent, uf_flags, pm);
     hipLaunchKernelGGL(k_union<2>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
                        boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
   } else {
