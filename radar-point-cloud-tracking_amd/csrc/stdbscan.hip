@@ -2406,6 +2406,7 @@ struct DbscanState {
   uint4* pmask = nullptr;  // union passes' undecided-candidate masks per occupied cell (aliases
                            // the grid build's radix key buffers, dead after the build)
   int union_list = -1;     // RPT_UNION_LIST=0: the second union pass enumerates every window
+  int uf_compress = -1;    // RPT_UF_COMPRESS=1: a compression pass closes the union stage
   int uf_flags = -1;                         // see XcdRange; -1 = read RPT_UF_FLAGS once
   int k5_legacy = -1;                        // 1: round-1 K5 (fill + point queue); RPT_K5_MODE
   int k5_fill = 0;
@@ -2807,8 +2808,15 @@ int32_t DbscanState::union_pass(hipStream_t st) {
                        boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
   }
   RPT_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_compress, dim3(gb), dim3(kBlock), 0, st, parent, core, n, sorig,
-                     (int32_t*)nullptr);
+  // every later reader walks to the root with path halving (k_ccmin, k_comp_out, ...), so a
+  // separate compression pass only moves that work; RPT_UF_COMPRESS=1 keeps it (A/B)
+  if (uf_compress < 0) {
+    const char* e = std::getenv("RPT_UF_COMPRESS");
+    uf_compress = (e && std::atoi(e) == 1) ? 1 : 0;
+  }
+  if (uf_compress)
+    hipLaunchKernelGGL(k_compress, dim3(gb), dim3(kBlock), 0, st, parent, core, n, sorig,
+                       (int32_t*)nullptr);
   RPT_CHECK_LAUNCH();
   tm.mark();
   return RPT_OK;
