@@ -1853,13 +1853,32 @@ __global__ __launch_bounds__(kBlock) void k_fill_i32(int32_t* p, int64_t n, int3
     p[i] = v;
 }
 
+// Cluster id of a component minimum m = its rank among the minima: one bit per original index
+// (set by k_ccmin) and an exclusive scan of the words' popcounts (total = cluster count at
+// pref[words]): n/32 words to clear and scan instead of an n-length flag array.
+struct MinRank {
+  const uint32_t* bits;
+  const int32_t* pref;
+  __device__ __forceinline__ int32_t operator[](int32_t m) const {
+    const uint32_t w = bits[m >> 5];
+    return pref[m >> 5] + __popc(w & ((1u << (m & 31)) - 1u));
+  }
+};
+
+__global__ void k_word_popc(const uint32_t* __restrict__ bits, int64_t words,
+                            int32_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = __popc(bits[i]);
+}
+
 // ccmin[s] = component-min original index for core points, -1 otherwise; flags the minima and
 // queues the non-core points for k_label.
 __global__ __launch_bounds__(kBlock) void k_ccmin(int32_t* parent,
                                                  const uint8_t* __restrict__ core, int64_t n,
                                                  const int32_t* __restrict__ sorig,
                                                  int32_t* __restrict__ ccmin,
-                                                 int32_t* __restrict__ is_min,
+                                                 uint32_t* __restrict__ min_bits,
                                                  int32_t* __restrict__ nc_list,
                                                  int32_t* __restrict__ nc_count) {
   for (int64_t tile = (int64_t)blockIdx.x * kBlock * kItems; tile < n;
@@ -1874,7 +1893,7 @@ __global__ __launch_bounds__(kBlock) void k_ccmin(int32_t* parent,
           const int x = uf_find(parent, (int)s);
           const int m = sorig[x];
           ccmin[s] = m;
-          if (x == (int)s) is_min[m] = 1;
+          if (x == (int)s) atomicOr(min_bits + (m >> 5), 1u << (m & 31));
           return false;
         },
         nc_list, nc_count);
@@ -1895,7 +1914,7 @@ __global__ __launch_bounds__(kBlock) void k_nc_list(const uint8_t* __restrict__ 
 __global__ __launch_bounds__(kBlock) void k_label_core(const int32_t* __restrict__ ccmin,
                                                       int64_t n,
                                                       const int32_t* __restrict__ sorig,
-                                                      const int32_t* __restrict__ cid,
+                                                      MinRank cid,
                                                       int32_t* __restrict__ labels) {
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
        s += (int64_t)gridDim.x * blockDim.x) {
@@ -1947,7 +1966,7 @@ __global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts
                                                  const int32_t* __restrict__ cell_key,
                                                  const uint8_t* __restrict__ mutual,
                                                  const int32_t* __restrict__ sorig,
-                                                 const int32_t* __restrict__ cid,
+                                                 MinRank cid,
                                                  const int32_t* __restrict__ nc_list,
                                                  const int32_t* __restrict__ nc_count,
                                                  int32_t* __restrict__ labels) {
@@ -2283,7 +2302,7 @@ __global__ __launch_bounds__(kBlock) void k_label_fifo(const float4* __restrict_
                                                       const int32_t* __restrict__ rep,
                                                       const int32_t* __restrict__ sorig,
                                                       const int32_t* __restrict__ spos,
-                                                      const int32_t* __restrict__ cid,
+                                                      MinRank cid,
                                                       const int32_t* __restrict__ nc_list,
                                                       const int32_t* __restrict__ nc_count,
                                                       int32_t* __restrict__ labels) {
@@ -2407,6 +2426,11 @@ struct DbscanState {
                            // the grid build's radix key buffers, dead after the build)
   int union_list = -1;     // RPT_UNION_LIST=0: the second union pass enumerates every window
   int uf_compress = -1;    // RPT_UF_COMPRESS=1: a compression pass closes the union stage
+  uint32_t* min_bits = nullptr;  // component minima, 1 bit per original index (MinRank)
+  int32_t* min_pref = nullptr;   // exclusive popcount prefix of min_bits' words (+ total)
+  int64_t min_words() const { return n / 32 + 1; }
+  int32_t* n_clusters_ptr() const { return min_pref + min_words(); }
+  int32_t cluster_ids(hipStream_t st);
   int uf_flags = -1;                         // see XcdRange; -1 = read RPT_UF_FLAGS once
   int k5_legacy = -1;                        // 1: round-1 K5 (fill + point queue); RPT_K5_MODE
   int k5_fill = 0;
@@ -2562,6 +2586,8 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   bud.add<uint8_t>(C1);     // fok (denoise)
   bud.add<int32_t>(C1);     // cell_min
   bud.add<uint64_t>(C1);    // cell_min_pair (union star initialisation)
+  bud.add<uint32_t>(n / 32 + 1);  // min_bits
+  bud.add<int32_t>(n / 32 + 2);   // min_pref
   bud.add<int32_t>(n + 1);  // occ
   bud.add<int32_t>(n + 1);  // hpos
   bud.add<CellRec<D>>(C1);  // crec
@@ -2596,6 +2622,8 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   fok = arena.carve_n<uint8_t>(C1);
   cell_min = arena.carve_n<int32_t>(C1);
   cell_min_pair = arena.carve_n<uint64_t>(C1);
+  min_bits = arena.carve_n<uint32_t>(n / 32 + 1);
+  min_pref = arena.carve_n<int32_t>(n / 32 + 2);
   occ = arena.carve_n<int32_t>(n + 1);
   hpos = arena.carve_n<int32_t>(n + 1);
   CellRec<D>* cr = arena.carve_n<CellRec<D>>(C1);
@@ -2822,6 +2850,18 @@ int32_t DbscanState::union_pass(hipStream_t st) {
   return RPT_OK;
 }
 
+// component minima (k_ccmin; also queues the non-core points) -> MinRank prefix and cluster count
+int32_t DbscanState::cluster_ids(hipStream_t st) {
+  const int64_t W = min_words();
+  RPT_HIP(hipMemsetAsync(min_bits, 0, sizeof(uint32_t) * W, st));
+  hipLaunchKernelGGL(k_ccmin, dim3(tile_grid(n)), dim3(kBlock), 0, st, parent, core, n, sorig,
+                     ccmin, min_bits, nc_list, nc_list + n);
+  hipLaunchKernelGGL(k_word_popc, dim3(grid_for(W, kBlock, 2048)), dim3(kBlock), 0, st, min_bits,
+                     W, min_pref);
+  RPT_CHECK_LAUNCH();
+  return exclusive_scan_total_i32(min_pref, min_pref, W, st);
+}
+
 int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st) {
   const int gb = grid_for(n, kBlock, 2048);
   if (degenerate) {
@@ -2836,30 +2876,27 @@ int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hi
     return RPT_OK;
   }
   int32_t* nc_count = nc_list + n;
-  RPT_HIP(hipMemsetAsync(cid, 0, sizeof(int32_t) * n, st));
   RPT_HIP(hipMemsetAsync(nc_count, 0, sizeof(int32_t), st));
-  hipLaunchKernelGGL(k_ccmin, dim3(tile_grid(n)), dim3(kBlock), 0, st, parent, core, n, sorig,
-                     ccmin, cid, nc_list, nc_count);
-  RPT_CHECK_LAUNCH();
-  RPT_TRY(exclusive_scan_total_i32(cid, cid, n, st));
-  hipLaunchKernelGGL(k_label_core, dim3(gb), dim3(kBlock), 0, st, ccmin, n, sorig, cid, labels);
+  RPT_TRY(cluster_ids(st));
+  const MinRank mr{min_bits, min_pref};
+  hipLaunchKernelGGL(k_label_core, dim3(gb), dim3(kBlock), 0, st, ccmin, n, sorig, mr, labels);
   const int gc = grid_for(C, kBlock, 8192);
   hipLaunchKernelGGL(k_fill_i32, dim3(gc), dim3(kBlock), 0, st, cell_min, C, INT_MAX);
   hipLaunchKernelGGL(k_cell_min_key, dim3(gb), dim3(kBlock), 0, st, skey, ccmin, n, C, cell_min);
   if (dim == 2)
     hipLaunchKernelGGL((k_label<2, false>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<2>(), occ_bits, slab_t, ccmin, cell_min, mutual, sorig, cid, nc_list,
+                       rec<2>(), occ_bits, slab_t, ccmin, cell_min, mutual, sorig, mr, nc_list,
                        nc_count, labels);
   else
     hipLaunchKernelGGL((k_label<3, false>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<3>(), occ_bits, slab_t, ccmin, cell_min, mutual, sorig, cid, nc_list,
+                       rec<3>(), occ_bits, slab_t, ccmin, cell_min, mutual, sorig, mr, nc_list,
                        nc_count, labels);
   RPT_CHECK_LAUNCH();
   tm.mark();
   if (stats && defer) return RPT_OK;  // fill_stats after the caller's sync
   if (stats) {
     int32_t ncl = 0;
-    RPT_HIP(hipMemcpyAsync(&ncl, cid + n, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    RPT_HIP(hipMemcpyAsync(&ncl, n_clusters_ptr(), sizeof(int32_t), hipMemcpyDeviceToHost, st));
     RPT_TRY(wait_stream(st));
     RPT_TRY(fill_stats(ncl, stats));
   }
@@ -2907,11 +2944,11 @@ int32_t DbscanState::labels_global(const int64_t* rep_orig, const int64_t* reps,
   if (dim == 2)
     hipLaunchKernelGGL((k_label<2, true>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
                        rec<2>(), occ_bits, slab_t, slab, cell_min, mutual, sorig,
-                       (const int32_t*)nullptr, nc_list, nc_count, labels);
+                       MinRank{nullptr, nullptr}, nc_list, nc_count, labels);
   else
     hipLaunchKernelGGL((k_label<3, true>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
                        rec<3>(), occ_bits, slab_t, slab, cell_min, mutual, sorig,
-                       (const int32_t*)nullptr, nc_list, nc_count, labels);
+                       MinRank{nullptr, nullptr}, nc_list, nc_count, labels);
   RPT_CHECK_LAUNCH();
   return RPT_OK;
 }
@@ -2950,26 +2987,24 @@ int32_t DbscanState::labels_fifo(int32_t* labels, rpt_stdbscan_stats* stats, hip
   const int gb = grid_for(n, kBlock, 2048);
   int32_t* nc_count = nc_list + n;
   int32_t* spos = slab;
-  RPT_HIP(hipMemsetAsync(cid, 0, sizeof(int32_t) * n, st));
   RPT_HIP(hipMemsetAsync(nc_count, 0, sizeof(int32_t), st));
-  hipLaunchKernelGGL(k_ccmin, dim3(tile_grid(n)), dim3(kBlock), 0, st, parent, core, n, sorig,
-                     ccmin, cid, nc_list, nc_count);
+  RPT_TRY(cluster_ids(st));
   hipLaunchKernelGGL(k_inverse_perm, dim3(gb), dim3(kBlock), 0, st, sorig, n, spos);
   RPT_CHECK_LAUNCH();
-  RPT_TRY(exclusive_scan_total_i32(cid, cid, n, st));
-  hipLaunchKernelGGL(k_label_core, dim3(gb), dim3(kBlock), 0, st, ccmin, n, sorig, cid, labels);
+  const MinRank mr{min_bits, min_pref};
+  hipLaunchKernelGGL(k_label_core, dim3(gb), dim3(kBlock), 0, st, ccmin, n, sorig, mr, labels);
   if (dim == 2)
     hipLaunchKernelGGL((k_label_fifo<2>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<2>(), occ_bits, slab_t, ccmin, rep, sorig, spos, cid, nc_list,
+                       rec<2>(), occ_bits, slab_t, ccmin, rep, sorig, spos, mr, nc_list,
                        nc_count, labels);
   else
     hipLaunchKernelGGL((k_label_fifo<3>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<3>(), occ_bits, slab_t, ccmin, rep, sorig, spos, cid, nc_list,
+                       rec<3>(), occ_bits, slab_t, ccmin, rep, sorig, spos, mr, nc_list,
                        nc_count, labels);
   RPT_CHECK_LAUNCH();
   tm.mark();
   int32_t ncl = 0;
-  RPT_HIP(hipMemcpyAsync(&ncl, cid + n, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  RPT_HIP(hipMemcpyAsync(&ncl, n_clusters_ptr(), sizeof(int32_t), hipMemcpyDeviceToHost, st));
   RPT_TRY(wait_stream(st));
   if (stats) RPT_TRY(fill_stats(ncl, stats));
   return RPT_OK;
@@ -3132,7 +3167,7 @@ int32_t stdbscan_deferred(const float* x, const float* y, const float* z, int64_
   RPT_TRY(S->union_pass(st));
   S->defer = !S->degenerate;
   const int32_t s_ = S->labels_local(labels, stats, st);
-  *n_clusters_dev = S->defer ? S->cid + S->n : nullptr;
+  *n_clusters_dev = S->defer ? S->n_clusters_ptr() : nullptr;
   *state = S;
   return s_;
 }
