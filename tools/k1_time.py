@@ -34,7 +34,7 @@ st = stream_handle(dev)
 loaded = [C.CDLL(lp) for lp in libs]
 lib0 = _abi.load()
 words = int(lib0.rpt_polar_stage_words(nf, rows))
-mk = torch.empty(words, dtype=torch.int32, device=dev)
+mk = torch.zeros(words, dtype=torch.int32, device=dev)  # zero: diagnostic builds may skip it
 rp = torch.empty(nf * ((rows + 3) // 4) + 1, dtype=torch.int64, device=dev)
 fo = torch.empty(nf + 1, dtype=torch.int64, device=dev)
 tot = C.c_int64(0)
