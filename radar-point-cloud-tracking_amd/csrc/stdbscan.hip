@@ -1565,6 +1565,25 @@ __global__ __launch_bounds__(kBlock) void k_cell_min_pair(const int32_t* __restr
   }
 }
 
+// rep = -1 and the (min original, sorted) pair = all-ones for the occupied cells only: every
+// reader of rep / the pairs looks at occupied cells (occ list, occupancy bits or non-empty
+// cell_start ranges), so the dense C-cell grid needs no clear.
+__global__ __launch_bounds__(kBlock) void k_init_occ_cells(const int32_t* __restrict__ occ,
+                                                          const int32_t* __restrict__ n_occ,
+                                                          int64_t cells,
+                                                          int32_t* __restrict__ rep,
+                                                          unsigned long long* __restrict__ cmin) {
+  const int64_t m = *n_occ;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t c = occ[q];
+    if ((int64_t)c < cells) {
+      rep[c] = -1;
+      cmin[c] = ~0ull;
+    }
+  }
+}
+
 // Star initialisation from k_cell_min_pair: core points of a mutual cell under the cell's
 // representative, other points roots; the representative records itself in rep.
 __global__ __launch_bounds__(kBlock) void k_parent_init_pair(
@@ -2805,8 +2824,7 @@ int32_t DbscanState::union_pass(hipStream_t st) {
   (void)gc;
   // per-cell (min original index, sorted index) of the core points, one u64 per cell
   auto* cmin = reinterpret_cast<unsigned long long*>(cell_min_pair);
-  RPT_HIP(hipMemsetAsync(rep, 0xFF, sizeof(int32_t) * (size_t)C, st));
-  RPT_HIP(hipMemsetAsync(cmin, 0xFF, sizeof(unsigned long long) * (size_t)C, st));
+  hipLaunchKernelGGL(k_init_occ_cells, dim3(gb), dim3(kBlock), 0, st, occ, n_occ, C, rep, cmin);
   hipLaunchKernelGGL(k_cell_min_pair, dim3(gb), dim3(kBlock), 0, st, skey, core, sorig, n, C,
                      cmin);
   hipLaunchKernelGGL(k_parent_init_pair, dim3(gb), dim3(kBlock), 0, st, parent, n, core, skey,
