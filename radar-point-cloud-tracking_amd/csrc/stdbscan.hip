@@ -1316,7 +1316,8 @@ __global__ __launch_bounds__(kBlock) void k_core_fill(const int32_t* __restrict_
 // the cells' boxes (whole-cell accept adds the cell's count), then every undecided cell's points
 // are tested 64 at a time; the wave stops as soon as min_samples neighbours are seen.
 template <int D>
-__global__ __launch_bounds__(kBlock) void k_core_slow(const float4* __restrict__ pts,
+// 8 waves/SIMD (64 VGPRs, one spill; 72 gave 7): -3 % on the latency-bound queue pass
+__global__ __launch_bounds__(kBlock, 8) void k_core_slow(const float4* __restrict__ pts,
                                                      const int32_t* __restrict__ skey, Geom g,
                                                      const CellRec<D>* __restrict__ crec,
                                                      const uint32_t* __restrict__ occ_bits,
@@ -1976,7 +1977,8 @@ __global__ __launch_bounds__(kBlock) void k_cell_min_key(const int32_t* __restri
 // GLOBAL = true : key = slab (the core point's final label: labels are ranks of the sorted global
 //                 representatives, so the smallest label is the smallest representative).
 template <int D, bool GLOBAL>
-__global__ __launch_bounds__(kBlock) void k_label(const float4* __restrict__ pts,
+// 7 waves/SIMD (72 VGPRs, one spill): 80 VGPRs left it at 6 and latency-bound (-2 %)
+__global__ __launch_bounds__(kBlock, 7) void k_label(const float4* __restrict__ pts,
                                                  const int32_t* __restrict__ skey, Geom g,
                                                  const CellRec<D>* __restrict__ crec,
                                                  const uint32_t* __restrict__ occ_bits,
