@@ -419,13 +419,15 @@ __global__ __launch_bounds__(kBlock) void k_label_means(
 }
 
 // ---- per-frame counting sort (point_frame non-decreasing) ----------------------------------
-// One 8-wave block per frame.  Each wave owns a contiguous part of the frame's points; the frame's
+// One 16-wave block per frame (8 waves: the frame's chunk chain per wave set the time at 125 frames).  Each wave owns a contiguous part of the frame's points; the frame's
 // clustered labels get LDS hash slots (at most kFsMaxKeys distinct labels per frame, else the
 // frame reports an overflow and the caller redoes K9 on the radix path), counted per (wave, slot),
 // scanned into frame-local offsets and per-wave cursors, and the points scattered stably — a
 // (frame, label) run is then contiguous and in index order, as the radix path gives.  Noise is
 // not scattered; each frame's first noise point is the first one of its lowest wave.
-constexpr int kFsWaves = 8, kFsSlots = 1024, kFsMaxKeys = kFsSlots / 2;
+constexpr int kFsWaves = 16, kFsSlots = 1024, kFsMaxKeys = kFsSlots / 2;
+constexpr int kFsSpt = kFsSlots / (kFsWaves * 64);  // scan slots per thread
+static_assert(kFsSpt >= 1 && kFsSpt * kFsWaves * 64 == kFsSlots, "frame sort slot split");
 
 struct FsLds {
   int keys[kFsSlots];               // label + 1 per slot, or -1
@@ -584,15 +586,19 @@ __global__ __launch_bounds__(kFsWaves * 64) void k_frame_sort(
     for (int q = 0; q < kFsWaves; ++q) m = min(m, L.fnoise[q]);
     if (m != INT_MAX) first_noise[f] = m;
   }
-  // scan: two slots per thread; run offsets and segment slots in slot order
-  const int s0 = 2 * tid, s1 = s0 + 1;
-  uint32_t t0 = 0, t1 = 0;
+  // scan: kFsSpt consecutive slots per thread; run offsets and segment slots in slot order
+  uint32_t tt[kFsSpt];
+  uint32_t a = 0u, pcount = 0u;
 #pragma unroll
-  for (int q = 0; q < kFsWaves; ++q) {
-    t0 += L.cnt[q][s0];
-    t1 += L.cnt[q][s1];
+  for (int j = 0; j < kFsSpt; ++j) {
+    const int sj = kFsSpt * tid + j;
+    uint32_t t = 0u;
+#pragma unroll
+    for (int q = 0; q < kFsWaves; ++q) t += L.cnt[q][sj];
+    tt[j] = t;
+    a += t;
+    pcount += (t != 0u);
   }
-  const uint32_t a = t0 + t1, pcount = (t0 != 0u) + (t1 != 0u);
   const uint32_t ia = wave_incl_scan(a, lane), ip = wave_incl_scan(pcount, lane);
   if (lane == 63) {
     L.wsum[0][w] = ia;
@@ -624,8 +630,15 @@ __global__ __launch_bounds__(kFsWaves * 64) void k_frame_sort(
       run += c;
     }
   };
-  emit(s0, t0, eo, eq);
-  emit(s1, t1, eo + t0, eq + (t0 != 0u));
+  {
+    uint32_t o = eo, q = eq;
+#pragma unroll
+    for (int j = 0; j < kFsSpt; ++j) {
+      emit(kFsSpt * tid + j, tt[j], o, q);
+      o += tt[j];
+      q += (tt[j] != 0u);
+    }
+  }
   if (tid == 0) nseg_f[f] = (int)tp;
   (void)ta;
   __syncthreads();
