@@ -16,9 +16,10 @@ At N=1 the whole stack runs on one MI355X (it fits: 288 GB HBM).
   --dense        configs[4]'s density (~500k points per frame, rpt.synth.dense_config)
   --h2d-steps K  also time K steps that first copy the echo from pinned host memory (reported
                  as `h2d_inclusive`, never as `value`)
-At N=1 two stacks are in flight by default (`--lanes 2`: native handles on two streams; step
-k+1's device work runs while step k's host stage and readbacks finish, and the two stacks'
-latency-bound kernels share the CUs); `one_stack_in_flight` repeats the steps strictly one after
+At N=1 three stacks are in flight by default (`--lanes 3`: native handles on three streams;
+step k+1's device work runs while step k's host stage and readbacks finish, and the stacks'
+latency-bound kernels share the CUs; 3 measured +4-5 % over 2 in interleaved same-box runs, 4
+no better); `one_stack_in_flight` repeats the steps strictly one after
 another, and K5's roofline is taken from that leg (K5 alone on the GPU).
 After the timed region (N=1, timing on), K5 is also timed on the configs[4] per-GPU share (125
 dense frames), where SURVEY.md §8(d) sets the 0.40 roofline target: `roofline_configs4_share`
@@ -122,7 +123,7 @@ def main():
                     help="sharded runs: ShardedStackPipeline (HipOps stages composed in Python) "
                          "instead of the native shard driver")
     ap.add_argument("--lanes", type=int, default=None,
-                    help="stacks in flight at once (default 2 on one GPU: native handles on "
+                    help="stacks in flight at once (default 3 on one GPU: native handles on "
                          "separate streams; 1 with N>1 ranks, where a lane is also a process "
                          "group -- rpt.dist.ShardLanes -- and several RCCL communicators "
                          "sharing a rank's hardware queues can order their kernels differently "
@@ -135,7 +136,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if args.lanes is None:
-        args.lanes = 2 if world == 1 and not args.sharded else 1
+        args.lanes = 3 if world == 1 and not args.sharded else 1
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # --sharded: the frame-sharded multi-GPU path even at one rank (measures its per-rank cost)
     dist = world > 1 or args.sharded
