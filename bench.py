@@ -128,6 +128,8 @@ def main():
                          "group -- rpt.dist.ShardLanes -- and several RCCL communicators "
                          "sharing a rank's hardware queues can order their kernels differently "
                          "on different GPUs); 1 = strictly one after another")
+    ap.add_argument("--no-one-stack", action="store_true",
+                    help="skip the one-stack-in-flight leg (and so K5's roofline)")
     ap.add_argument("--sync-host", action="store_true",
                     help="run each step's host stage (order + tracker) inline instead of "
                          "overlapping it with the next step's device work")
@@ -297,7 +299,7 @@ def main():
             for r in sres:
                 for k, v in r.stage_ms.items():
                     stage_acc[k] = stage_acc.get(k, 0.0) + v
-    if not dist and args.lanes > 1:
+    if not dist and args.lanes > 1 and not args.no_one_stack:
         spipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), dev, timing=timing,
                                    async_host=not args.sync_host, lanes=1)
         spipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t,
