@@ -359,7 +359,9 @@ __global__ __launch_bounds__(kBucketBlock) void k_slab_bucket(
     float4* __restrict__ pts, int32_t* __restrict__ sorig, int32_t* __restrict__ skey,
     int32_t* __restrict__ cell_start, int32_t* __restrict__ occ_tmp,
     int32_t* __restrict__ slab_occ, uint32_t* __restrict__ occ_bits) {
-  __shared__ int32_t hist[kBucketCells];
+  // the slab's nx * ny cell counts, sized at launch (a 463-m sweep at cells of 5.6 m: 27 KiB, so
+  // several slabs share a CU instead of one 64-KiB histogram each)
+  extern __shared__ int32_t hist[];
   __shared__ int32_t wsum[kBucketBlock / 64], wocc[kBucketBlock / 64];
   const int s = blockIdx.x;
   const int P = g.nx * g.ny;
@@ -2670,8 +2672,12 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
     RPT_HIP(hipMemsetAsync(occ_bits, 0, sizeof(uint32_t) * (C1 / 32 + 2), st));
     // the slabs write their occupied cells (ascending) into hpos at their point offsets, the
     // occupancy bits and their counts; one scan over the slabs and a gather give the list
-    hipLaunchKernelGGL(k_slab_bucket, dim3((unsigned)nt), dim3(kBucketBlock), 0, st, x, y, stride,
-                       t, g, slab_lo, pts, sorig, skey, cell_start, hpos, slab_occ, occ_bits);
+    const size_t hist_bytes = sizeof(int32_t) * (size_t)nx * ny;
+    RPT_HIP(hipFuncSetAttribute((const void*)k_slab_bucket,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)hist_bytes));
+    hipLaunchKernelGGL(k_slab_bucket, dim3((unsigned)nt), dim3(kBucketBlock), hist_bytes, st, x,
+                       y, stride, t, g, slab_lo, pts, sorig, skey, cell_start, hpos, slab_occ,
+                       occ_bits);
     RPT_CHECK_LAUNCH();
     RPT_TRY(exclusive_scan_total_i32(slab_occ, occ_base, nt, st));
     hipLaunchKernelGGL(k_occ_gather, dim3((unsigned)nt), dim3(kBlock), 0, st, hpos, slab_lo,
