@@ -1038,6 +1038,14 @@ constexpr int kR = 4;  // candidate cells per lane per super-round of the window
 static_assert(kR >= 2, "the union passes' candidate masks cover two 64-position rounds");
 // k_union_cells: the top bit of a cell's candidate mask = "not recorded, enumerate the window"
 constexpr uint32_t kPmaskFull = 0x80000000u;
+// RPT_CELL_ROOTS=0: k_ccmin walks every core point's parent chain (A/B)
+static bool cell_roots_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("RPT_CELL_ROOTS");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
 
 // Level 1, one thread per occupied cell: a mutual cell (every pair adjacent) holding >=
 // min_samples points is all core — the bulk of a radar stack.  Every other cell is queued for
@@ -1896,13 +1904,38 @@ __global__ void k_word_popc(const uint32_t* __restrict__ bits, int64_t words,
 
 // ccmin[s] = component-min original index for core points, -1 otherwise; flags the minima and
 // queues the non-core points for k_label.
+// Root of every occupied mutual cell's core points (its representative's root): the core points
+// of a mutual cell all hang under the representative (star init), so k_ccmin takes their root
+// from here -- one cached per-cell read instead of a parent chain per point.
+__global__ __launch_bounds__(kBlock) void k_cell_roots(int32_t* parent,
+                                                      const int32_t* __restrict__ occ,
+                                                      const int32_t* __restrict__ n_occ,
+                                                      int64_t cells,
+                                                      const uint8_t* __restrict__ mutual,
+                                                      const int32_t* __restrict__ rep,
+                                                      int32_t* __restrict__ cell_root) {
+  const int64_t m = *n_occ;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t c = occ[q];
+    if ((int64_t)c >= cells || !mutual[c]) continue;
+    const int r = rep[c];
+    if (r >= 0) cell_root[c] = uf_find(parent, r);
+  }
+}
+
+// cell_root (nullable): k_cell_roots' output, read for core points of mutual cells (skey, mutual)
 __global__ __launch_bounds__(kBlock) void k_ccmin(int32_t* parent,
                                                  const uint8_t* __restrict__ core, int64_t n,
                                                  const int32_t* __restrict__ sorig,
                                                  int32_t* __restrict__ ccmin,
                                                  uint32_t* __restrict__ min_bits,
                                                  int32_t* __restrict__ nc_list,
-                                                 int32_t* __restrict__ nc_count) {
+                                                 int32_t* __restrict__ nc_count,
+                                                 const int32_t* __restrict__ skey = nullptr,
+                                                 const uint8_t* __restrict__ mutual = nullptr,
+                                                 const int32_t* __restrict__ cell_root = nullptr,
+                                                 int64_t cells = 0) {
   for (int64_t tile = (int64_t)blockIdx.x * kBlock * kItems; tile < n;
        tile += (int64_t)gridDim.x * kBlock * kItems) {
     block_append(
@@ -1912,7 +1945,12 @@ __global__ __launch_bounds__(kBlock) void k_ccmin(int32_t* parent,
             ccmin[s] = -1;
             return true;
           }
-          const int x = uf_find(parent, (int)s);
+          int x;
+          const int32_t key = cell_root ? skey[s] : -1;
+          if (cell_root && (int64_t)key < cells && key >= 0 && mutual[key])
+            x = cell_root[key];
+          else
+            x = uf_find(parent, (int)s);
           const int m = sorig[x];
           ccmin[s] = m;
           if (x == (int)s) atomicOr(min_bits + (m >> 5), 1u << (m & 31));
@@ -2880,8 +2918,14 @@ int32_t DbscanState::union_pass(hipStream_t st) {
 int32_t DbscanState::cluster_ids(hipStream_t st) {
   const int64_t W = min_words();
   RPT_HIP(hipMemsetAsync(min_bits, 0, sizeof(uint32_t) * W, st));
+  // per-cell roots of the mutual cells into cell_min (re-filled before k_cell_min_key)
+  const bool cr = cell_roots_enabled();
+  if (cr)
+    hipLaunchKernelGGL(k_cell_roots, dim3(grid_for(n, kBlock, 2048)), dim3(kBlock), 0, st, parent,
+                       occ, n_occ_dev, C, mutual, rep, cell_min);
   hipLaunchKernelGGL(k_ccmin, dim3(tile_grid(n)), dim3(kBlock), 0, st, parent, core, n, sorig,
-                     ccmin, min_bits, nc_list, nc_list + n);
+                     ccmin, min_bits, nc_list, nc_list + n, skey, mutual,
+                     cr ? (const int32_t*)cell_min : nullptr, C);
   hipLaunchKernelGGL(k_word_popc, dim3(grid_for(W, kBlock, 2048)), dim3(kBlock), 0, st, min_bits,
                      W, min_pref);
   RPT_CHECK_LAUNCH();
