@@ -86,6 +86,31 @@ class Comm:
         dist.all_gather(outs, pad, group=self.group)
         return [o[:k].to(t.device) for o, k in zip(outs, ns)]
 
+    def all_gather_capped(self, t: torch.Tensor, cap: int) -> Tuple[List[torch.Tensor], int]:
+        """all_gather_var in ONE collective when every rank's length fits cap: each rank sends
+        [length | first min(length, cap) elements] padded to 1 + cap (the length as the dtype:
+        exact below 2^53), everyone reads the lengths from the same gathered block, and only when
+        some length exceeds cap do all ranks (consistently) fall back to the two-round form.
+        Returns (pieces on the input's device, longest length)."""
+        if self.world == 1:
+            t = t.reshape(-1)
+            return [t], int(t.numel())
+        c = self._c(t).reshape(-1)
+        n = int(c.numel())
+        buf = torch.zeros(1 + cap, dtype=c.dtype, device=self.cdev)
+        buf[0] = n
+        k = min(n, cap)
+        if k:
+            buf[1:1 + k] = c[:k]
+        out = torch.empty(self.world * (1 + cap), dtype=c.dtype, device=self.cdev)
+        dist.all_gather_into_tensor(out, buf, group=self.group)
+        out = out.reshape(self.world, 1 + cap)
+        lens = [int(v) for v in out[:, 0].cpu().tolist()]
+        m = max(lens) if lens else 0
+        if m > cap:
+            return self.all_gather_var(t), m
+        return [out[r, 1:1 + lens[r]].to(t.device) for r in range(self.world)], m
+
     def exchange_known(self, to_prev: torch.Tensor, to_next: torch.Tensor, n_from_prev: int,
                        n_from_next: int) -> Tuple[torch.Tensor, torch.Tensor]:
         """exchange() when every rank already knows what its neighbours send (one P2P round):
@@ -453,6 +478,9 @@ class NativeShardPipeline:
         self.core_points = 0
         self._n_own = 0
         self._core_ms = False
+        # capacities of the one-collective gathers (grown from what earlier steps needed; a step
+        # that exceeds one falls back to the two-round gather, consistently on every rank)
+        self._cap_pairs, self._cap_roots, self._cap_parts = 4096, 4096, 65536
 
     def set_geometry(self, scale, cos_t, sin_t, n_files: int):
         def rep(a):
@@ -615,11 +643,9 @@ class NativeShardPipeline:
                     "rpt_shard_pairs")
             else:
                 pb[0] = 0
-            cnts = comm.all_gather_fixed(pb[:1]).numpy().reshape(-1)
-            m = int(cnts.max()) if len(cnts) else 0
-            if m > 0:
-                allp = comm.all_gather_fixed(pb[1:1 + 2 * m].contiguous()).numpy()
-                pairs = np.concatenate([row[:2 * int(c)] for row, c in zip(allp, cnts)])
+            # [pair count | pairs]: one gather of the first 1 + cap words carries every rank's
+            # count and (when they fit) its pairs; a larger count sends the rest in a second round
+            pairs = self._gather_pairs(comm, pb, 2 * max(pcap, 1))
         npair = len(pairs) // 2
         pairs = np.ascontiguousarray(pairs, np.int64)
         nk = int(lib.rpt_merge_equivalences(pairs.ctypes.data_as(A.c_i64p), npair, None, None, 0))
@@ -635,8 +661,11 @@ class NativeShardPipeline:
             chk(lib.rpt_shard_roots(self.h, keys.ctypes.data_as(A.c_i64p),
                                     vals.ctypes.data_as(A.c_i64p), nk, base, n_prev, n_own,
                                     roots.data_ptr(), C_.byref(nr), st), "rpt_shard_roots")
-        all_roots = comm.all_gather_var(roots[:int(nr.value)]) if W > 1 else \
-            [roots[:int(nr.value)]]
+        if W > 1:
+            all_roots, mx = comm.all_gather_capped(roots[:int(nr.value)], self._cap_roots)
+            self._cap_roots = max(self._cap_roots, mx + mx // 4 + 64)
+        else:
+            all_roots = [roots[:int(nr.value)]]
         reps = torch.cat([a.to(self.dev) for a in all_roots]).contiguous()
         n_clusters = int(reps.numel())
         # 8. labels + K9 of the own frames (one readback)
@@ -665,8 +694,12 @@ class NativeShardPipeline:
             [S, frame0], built_local.astype(np.float64), [-1.0] * (F - len(built_local)),
             first_noise, seg["frame"], seg["label"], seg["count"], seg["first"], seg["cx"],
             seg["cy"], seg["mi"]]).astype(np.float64)
-        parts = comm.all_gather_var(torch.from_numpy(packed)) if W > 1 else \
-            [torch.from_numpy(packed)]
+        if W > 1:
+            parts, mx = comm.all_gather_capped(torch.from_numpy(packed), self._cap_parts)
+            self._cap_parts = max(self._cap_parts, mx + mx // 4 + 64)
+            parts = [q.cpu() for q in parts]
+        else:
+            parts = [torch.from_numpy(packed)]
         mark("stdbscan")
         self._n_own = n_own if n_tot else 0
         labels = None
@@ -691,6 +724,31 @@ class NativeShardPipeline:
             for (a, ta), (b, tb) in zip(marks[:-1], marks[1:]):
                 res.stage_ms[b] = (tb - ta) * 1e3
         return res
+
+    def _gather_pairs(self, comm: Comm, pb: torch.Tensor, room: int) -> np.ndarray:
+        """Every rank's equivalence pairs from pb = [count | 2*count ids] (device), in one
+        collective while every count fits the capacity."""
+        if comm.world == 1:
+            k = int(pb[0].item())
+            return pb[1:1 + 2 * k].cpu().numpy()
+        cap = self._cap_pairs
+        buf = torch.zeros(1 + cap, dtype=torch.int64, device=comm.cdev)
+        w = min(1 + room, 1 + cap)
+        buf[:w] = pb[:w].to(comm.cdev)
+        out = torch.empty(comm.world * (1 + cap), dtype=torch.int64, device=comm.cdev)
+        dist.all_gather_into_tensor(out, buf, group=comm.group)
+        out = out.reshape(comm.world, 1 + cap).cpu().numpy()
+        cnts = out[:, 0]
+        m = int(cnts.max()) if len(cnts) else 0
+        self._cap_pairs = max(cap, 2 * m + 64)
+        if 2 * m <= cap:
+            return np.concatenate([row[1:1 + 2 * int(c)] for row, c in zip(out, cnts)])
+        k = int(cnts[comm.rank])
+        full = comm.all_gather_fixed(pb[1:1 + 2 * m].contiguous() if 2 * m <= room else
+                                     torch.cat([pb[1:1 + 2 * k],
+                                                torch.zeros(2 * m - 2 * k, dtype=torch.int64,
+                                                            device=pb.device)])).numpy()
+        return np.concatenate([row[:2 * int(c)] for row, c in zip(full, cnts)])
 
     def labels_local(self) -> torch.Tensor:
         """Labels (device int32, a copy) of this rank's kept points of the last run."""

@@ -3,6 +3,7 @@ stages from the test-only oracle-backed CpuOps.  The sharded result (labels, per
 in reference order, tracked objects) must equal the single-process oracle run of the stack."""
 from __future__ import annotations
 
+import json
 import os
 import socket
 import sys
@@ -114,3 +115,45 @@ def test_merge_equivalences_chains():
     keys, reps = merge_equivalences(pairs)
     m = dict(zip(keys.tolist(), reps.tolist()))
     assert m[10] == m[7] == m[99] == 4 and m[30] == m[25] == 20
+
+
+def _capped_worker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+
+    from rpt.dist import Comm
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = Comm(torch.device("cpu"))
+    res = {}
+    for dt in (torch.int64, torch.float64):
+        t = torch.arange(10 * rank + 3, dtype=dt) + 1000 * rank  # ragged: 3, 13, 23 elements
+        for cap in (64, 5, 0):  # fits / falls back / empty block
+            got, mx = comm.all_gather_capped(t, cap)
+            res[f"{dt}|{cap}"] = [[g.tolist() for g in got], mx]
+    empty, mx0 = comm.all_gather_capped(torch.zeros(0, dtype=torch.int64), 8)
+    res["empty"] = [[g.tolist() for g in empty], mx0]
+    with open(os.path.join(out_dir, f"capped{rank}.json"), "w") as f:
+        json.dump(res, f)
+    dist.destroy_process_group()
+
+
+def test_all_gather_capped_gloo():
+    """Comm.all_gather_capped: one gather when every length fits, the two-round fallback when
+    one does not (decided alike on every rank), ragged and empty pieces."""
+    import torch.multiprocessing as mp
+
+    world = 3
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_capped_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        outs = []
+        for r in range(world):
+            with open(os.path.join(d, f"capped{r}.json")) as f:
+                outs.append(json.load(f))
+    expect = [[float(v) + 1000 * r for v in range(10 * r + 3)] for r in range(world)]
+    for res in outs:
+        for key, (got, mx) in ((k, v) for k, v in res.items() if k != "empty"):
+            assert mx == 23, key
+            assert [[float(v) for v in g] for g in got] == expect, key
+        assert res["empty"] == [[[], [], []], 0]

@@ -25,16 +25,23 @@ def _free_port():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,frames,impl,lanes", [(2, 14, "native", 1), (3, 6, "native", 1),
-                                                     (2, 14, "python", 1), (2, 8, "native", 2)])
+                                                     (2, 14, "python", 1), (2, 8, "native", 2),
+                                                     (3, 6, "native-tinycaps", 1)])
 def test_sharded_gpu_matches_single_gpu(world, frames, impl, lanes):
     """lanes = 2: two stacks in flight (rpt.dist.ShardLanes: a process group, stream and thread
-    per lane); each lane's last run is checked."""
+    per lane); each lane's last run is checked.  native-tinycaps: the one-collective gathers
+    (pairs, representatives, segments) with one-element capacities, i.e. their two-round
+    fallbacks."""
+    extra = []
+    if impl == "native-tinycaps":
+        impl, extra = "native", ["--tiny-caps"]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={world}", "--master-addr=127.0.0.1",
            f"--master-port={_free_port()}", str(ROOT / "tools" / "dist_check.py"),
-           "--backend", "gloo", "--frames", str(frames), "--impl", impl, "--lanes", str(lanes)]
+           "--backend", "gloo", "--frames", str(frames), "--impl", impl, "--lanes", str(lanes),
+           *extra]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-4000:]

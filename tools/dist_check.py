@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--impl", default="native", choices=("native", "python"),
                     help="native: NativeShardPipeline (librpt shard driver); python: "
                          "ShardedStackPipeline over HipOps")
+    ap.add_argument("--tiny-caps", action="store_true",
+                    help="native: one-element capacities for the one-collective gathers (every "
+                         "gather takes its two-round fallback)")
     args = ap.parse_args()
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
@@ -74,6 +77,8 @@ def main():
         pipe = NativeShardPipeline(Comm(dev), cfg.gains, cfg.rows, cfg.bins, PathParams())
         pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
                           F * 3)
+        if args.tiny_caps:
+            pipe._cap_pairs = pipe._cap_roots = pipe._cap_parts = 1
         res = pipe.run(echo, rank * F)
         runs.append((res, pipe.labels_local()))
     else:
