@@ -305,7 +305,9 @@ int32_t rpt_stack_frame_offsets(const rpt_stack* h, int32_t which, int64_t* out)
 int32_t rpt_stack_segments(const rpt_stack* h, int32_t* frame, int32_t* label, int64_t* count,
                            int64_t* first, float* cx, float* cy, float* mean_i,
                            int64_t* frame_first_noise);
-/* device copies (each nullable, [n_clustered]) of the clustered points and their labels */
+/* device copies (each nullable, [n_clustered]) of the clustered points and their labels; gain
+ * only after a run given a gain table (RPT_EINVAL otherwise: without one the per-point gains
+ * are not written -- 8 B per point less K1 and land traffic) */
 int32_t rpt_stack_points(const rpt_stack* h, float* x, float* y, float* intensity,
                          int32_t* gain, int32_t* point_frame, int32_t* labels, void* stream);
 /* ---- frame-sharded multi-GPU driver ----------------------------------------

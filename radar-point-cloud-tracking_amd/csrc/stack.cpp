@@ -276,6 +276,7 @@ struct rpt_stack {
     if (ev_rb) (void)hipEventDestroy(ev_rb);
   }
 
+  bool had_gain = false;  // the last run wrote per-point gains (gain table given)
   int32_t run(const rpt_stack_params& p, const void* echo, const float* scale,
               const float* cos_t, const float* sin_t, const int32_t* gain, rpt_stack_result* out,
               hipStream_t st);
@@ -293,6 +294,7 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
   const int64_t n_files = (int64_t)F * G;
   n_frames = F;
   land_applied = false;
+  had_gain = gain != nullptr;
   const bool timing = p.timing != 0;
   if (timing && !ev_ok) {
     for (auto& e : ev) RPT_HIP(hipEventCreate(&e));
@@ -638,6 +640,10 @@ int32_t rpt_stack_points(const rpt_stack* h, float* x, float* y, float* intensit
     if (dst && src && n) RPT_HIP(hipMemcpyAsync(dst, src, n * es, hipMemcpyDeviceToDevice, st));
     return RPT_OK;
   };
+  if (gain && !h->had_gain) {
+    set_error("rpt_stack_points: the last rpt_stack_run had no gain table, so no per-point gains");
+    return RPT_EINVAL;
+  }
   const bool l = h->land_applied;
   RPT_TRY(cp(x, l ? h->x2.p : h->x.p, 4));
   RPT_TRY(cp(y, l ? h->y2.p : h->y.p, 4));
@@ -857,6 +863,7 @@ int32_t rpt_shard_polar(rpt_shard* h, const rpt_stack_params* p, const void* ech
   const hipStream_t st = as_stream(stream);
   rpt_stack& S = h->st;
   h->p = *p;
+  S.had_gain = gain != nullptr;  // per-point gains only with a gain table
   const int32_t F = p->n_frames, G = p->files_per_frame;
   h->F = F;
   const int64_t n_files = (int64_t)F * G;
@@ -1027,8 +1034,9 @@ int32_t rpt_shard_land_apply(rpt_shard* h, const double* grid, int64_t cells,
     if (N > 0) {  // the fused compaction (kept points in order, new frame offsets)
       RPT_TRY(S.t.ensure(cap, st));
       RPT_TRY(S.bnd.ensure(2 * sizeof(Bounds), st));
-      RPT_TRY(land_compact_dev(S.x.p, S.y.p, S.v.p, S.g.p, S.pf.p, N, S.land_cell.p,
-                               S.land_mask.p, F, S.x2.p, S.y2.p, S.v2.p, S.g2.p, S.pf2.p, S.t.p,
+      RPT_TRY(land_compact_dev(S.x.p, S.y.p, S.v.p, S.had_gain ? S.g.p : nullptr, S.pf.p, N,
+                               S.land_cell.p, S.land_mask.p, F, S.x2.p, S.y2.p, S.v2.p,
+                               S.had_gain ? S.g2.p : nullptr, S.pf2.p, S.t.p,
                                S.new_off.p, reinterpret_cast<Bounds*>(S.bnd.p), st));
     } else
       RPT_HIP(hipMemsetAsync(S.new_off.p, 0, sizeof(int64_t) * (F + 1), st));

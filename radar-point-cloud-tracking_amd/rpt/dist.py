@@ -539,7 +539,7 @@ class NativeShardPipeline:
         scale_d, cos_d, sin_d = self.geo
         # 1. K1 + bounds (one readback), then every rank's counts / bounds
         chk(lib.rpt_shard_polar(self.h, C_.byref(sp), echo.data_ptr(), scale_d.data_ptr(),
-                                cos_d.data_ptr(), sin_d.data_ptr(), self.gain_d.data_ptr(),
+                                cos_d.data_ptr(), sin_d.data_ptr(), None,  # no per-point gains
                                 C_.byref(info), st), "rpt_shard_polar")
         n_points = int(info.n_points)
         allinfo = comm.all_gather_fixed(torch.tensor(

@@ -174,9 +174,11 @@ class FrameStackPipeline:
                               1 if self.timing else 0)
         r = _abi.StackResult()
         scale_d, cos_d, sin_d = self.geo
+        # per-point gains only when the points are handed back (nothing downstream reads them)
         _abi.check(lib.rpt_stack_run(h, _abi.C.byref(sp), echo.data_ptr(),
                                      scale_d.data_ptr(), cos_d.data_ptr(), sin_d.data_ptr(),
-                                     self.gain_d.data_ptr(), _abi.C.byref(r), stream),
+                                     self.gain_d.data_ptr() if keep_points else None,
+                                     _abi.C.byref(r), stream),
                    "rpt_stack_run")
         fo = np.empty(F + 1, np.int64)
         _abi.check(lib.rpt_stack_frame_offsets(h, 0, fo.ctypes.data_as(_abi.c_i64p)))

@@ -565,3 +565,33 @@ def test_full_size_partition_is_order_invariant(gpu):
             d2 = (xh[w].astype(np.float64) - xh[i]) ** 2 + (yh[w].astype(np.float64) - yh[i]) ** 2
             assert int((d2 <= 64.0).sum()) < 15
     assert res.n_clusters > 10 and res.n_segments > 100
+
+
+def test_stack_points_gain_needs_gain_table(gpu):
+    """Without keep_points the pipeline runs rpt_stack_run with no gain table (no per-point gains
+    are written); rpt_stack_points must then refuse a gain output instead of copying stale
+    values, and still hand back the other arrays."""
+    from rpt import _abi
+    from rpt._device import stream_handle
+    from rpt.pipeline import FrameStackPipeline, PathParams
+    from rpt.synth import DeviceSynth, SynthConfig
+
+    cfg = SynthConfig(n_frames=12, rows=512)
+    ds = DeviceSynth(cfg, gpu)
+    echo = ds.echo()
+    pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), gpu)
+    pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
+                      cfg.n_frames * 3)
+    a = pipe.run(echo, keep_points=True)
+    res = pipe.run(echo)  # no gain table
+    n = res.n_clustered_input
+    assert n == a.n_clustered_input
+    lib = _abi.load()
+    g = torch.empty(n, dtype=torch.int32, device=gpu)
+    x = torch.empty(n, dtype=torch.float32, device=gpu)
+    st = stream_handle(gpu)
+    assert lib.rpt_stack_points(pipe._h, None, None, None, g.data_ptr(), None, None, st) == \
+        _abi.RPT_EINVAL
+    assert lib.rpt_stack_points(pipe._h, x.data_ptr(), None, None, None, None, None, st) == 0
+    torch.cuda.synchronize(gpu)
+    assert torch.equal(x, a.points["x"])
