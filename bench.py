@@ -382,18 +382,19 @@ def main():
                 "bytes_model": "17 B/point x points entering ST-DBSCAN (SURVEY.md 8d)",
                 "avg_ms": round(k5, 4), "points": n_in}
     stage = {k: round(v / args.steps, 3) for k, v in stage_acc.items()}
-    # the largest stage, K1 (count + scan + write): echo read once + 20 B per emitted point
-    # (x, y, intensity, gain, frame slot) + 12 B of row geometry per row, over its event time
+    # the largest stage, K1 (count + scan + write): echo read once + 16 B per emitted point
+    # (x, y, intensity, frame slot; no per-point gain without keep_points) + 12 B of row geometry
+    # per row, over its event time
     roof_k1 = None
     if stage.get("polar") and not dist:
-        k1_bytes = int(echo.numel() * echo.element_size()) + 20 * int(pts) + \
+        k1_bytes = int(echo.numel() * echo.element_size()) + 16 * int(pts) + \
             12 * int(echo.shape[0]) * int(echo.shape[1]) * int(echo.shape[2])
         k1_ach = k1_bytes / (stage["polar"] * 1e-3) / 1e9
         roof_k1 = {"kernel": "K1 stage = k_group_count_u8 + scans + k_group_starts + "
                              "k_expand_write (+ unstaged groups)",
                    "bound": "hbm", "achieved": round(k1_ach, 2), "peak": HBM_PEAK_GBS,
                    "unit": "GB/s", "frac": round(k1_ach / HBM_PEAK_GBS, 4),
-                   "avg_ms": stage["polar"], "bytes_model": "1 B per echo sample + 20 B per "
+                   "avg_ms": stage["polar"], "bytes_model": "1 B per echo sample + 16 B per "
                    "point written + 12 B per row (SURVEY 8d's K1 terms for u8 echo)",
                    "bytes": k1_bytes}
 
