@@ -396,7 +396,11 @@ def main():
                    "unit": "GB/s", "frac": round(k1_ach / HBM_PEAK_GBS, 4),
                    "avg_ms": stage["polar"], "bytes_model": "1 B per echo sample + 16 B per "
                    "point written + 12 B per row (SURVEY 8d's K1 terms for u8 echo)",
-                   "bytes": k1_bytes}
+                   "bytes": k1_bytes, "traffic": None}
+        t1 = ROOT / "profiles" / "r2" / f"k1_traffic_{wkey}.json"
+        if t1.exists():  # PMC-measured HBM bytes of the K1 kernels, same workload (pmc_r2.sh)
+            roof_k1["traffic"] = int(json.loads(t1.read_text())["bytes_per_launch"])
+            roof_k1["traffic_unit"] = f"bytes per run (PMC, {t1.relative_to(ROOT)})"
 
     # K5 again at the size SURVEY 8(d) sets its 0.40 target for: the configs[4] per-GPU share
     # (125 dense frames, ~61 M points), after the timed region; hipEvents as above

@@ -55,3 +55,14 @@ res = {"kernels": {k: (None if r is None else {"fetch_kib": r[2], "write_kib": r
        "workload": workload}
 (out_dir / out_name).write_text(json.dumps(res, indent=1))
 print(json.dumps(res))
+# K1 (the largest stage): count + group starts + expand write + the unstaged groups' write
+K1 = ("k_group_count_u8", "k_group_starts", "k_expand_write", "k_group_write_u8")
+k1 = [r for r in rows if any(k in r[0] for k in K1)]
+if k1:
+    res1 = {"kernels": {r[0][:80]: {"fetch_kib": r[2], "write_kib": r[3], "bytes": r[4]}
+                        for r in k1},
+            "bytes_per_launch": sum(r[4] for r in k1),
+            "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch, summed over the K1 kernels",
+            "workload": workload}
+    (out_dir / out_name.replace("k5_", "k1_")).write_text(json.dumps(res1, indent=1))
+    print(json.dumps(res1))
