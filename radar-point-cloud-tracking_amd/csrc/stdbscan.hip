@@ -1924,7 +1924,9 @@ __global__ __launch_bounds__(kBlock) void k_cell_roots(int32_t* parent,
   }
 }
 
-// cell_root (nullable): k_cell_roots' output, read for core points of mutual cells (skey, mutual)
+// cell_root (nullable): k_cell_roots' output, read for core points of mutual cells (skey, mutual).
+// cell_key (nullable, pre-filled with INT_MAX): per cell the smallest component key among its
+// core points, by a segmented wave minimum over the sorted points (k_cell_min_key fused in).
 __global__ __launch_bounds__(kBlock) void k_ccmin(int32_t* parent,
                                                  const uint8_t* __restrict__ core, int64_t n,
                                                  const int32_t* __restrict__ sorig,
@@ -1935,28 +1937,46 @@ __global__ __launch_bounds__(kBlock) void k_ccmin(int32_t* parent,
                                                  const int32_t* __restrict__ skey = nullptr,
                                                  const uint8_t* __restrict__ mutual = nullptr,
                                                  const int32_t* __restrict__ cell_root = nullptr,
-                                                 int64_t cells = 0) {
+                                                 int64_t cells = 0,
+                                                 int32_t* __restrict__ cell_key = nullptr) {
+  const int lane = threadIdx.x & 63;
   for (int64_t tile = (int64_t)blockIdx.x * kBlock * kItems; tile < n;
        tile += (int64_t)gridDim.x * kBlock * kItems) {
-    block_append(
-        tile, n,
-        [&](int64_t s) -> bool {
-          if (!core[s]) {
-            ccmin[s] = -1;
-            return true;
-          }
+    uint32_t bits = 0;
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const int64_t s = tile + (int64_t)k * kBlock + threadIdx.x;
+      const bool in = s < n;
+      const int32_t key = (in && skey) ? skey[s] : -1;
+      int m = -1;
+      if (in) {
+        if (!core[s]) {
+          ccmin[s] = -1;
+          bits |= 1u << k;
+        } else {
           int x;
-          const int32_t key = cell_root ? skey[s] : -1;
           if (cell_root && (int64_t)key < cells && key >= 0 && mutual[key])
             x = cell_root[key];
           else
             x = uf_find(parent, (int)s);
-          const int m = sorig[x];
+          m = sorig[x];
           ccmin[s] = m;
           if (x == (int)s) atomicOr(min_bits + (m >> 5), 1u << (m & 31));
-          return false;
-        },
-        nc_list, nc_count);
+        }
+      }
+      if (cell_key) {  // kernel-uniform: every lane of the wave takes part
+        int v = (m >= 0 && (int64_t)key < cells) ? m : INT_MAX;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {  // sorted keys: equal at distance off = run
+          const int ov = __shfl_up(v, off, 64);
+          const int ok = __shfl_up(key, off, 64);
+          if (lane >= off && ok == key) v = min(v, ov);
+        }
+        const int next = __shfl_down(key, 1, 64);
+        if ((lane == 63 || next != key) && key >= 0 && v != INT_MAX) atomicMin(cell_key + key, v);
+      }
+    }
+    block_append_bits(tile, bits, nc_list, nc_count);
   }
 }
 
@@ -2491,7 +2511,8 @@ struct DbscanState {
   int32_t* min_pref = nullptr;   // exclusive popcount prefix of min_bits' words (+ total)
   int64_t min_words() const { return n / 32 + 1; }
   int32_t* n_clusters_ptr() const { return min_pref + min_words(); }
-  int32_t cluster_ids(hipStream_t st);
+  int32_t cluster_ids(hipStream_t st, int32_t* cell_key);
+  int32_t* cell_root = nullptr;  // per cell: root of a mutual cell's core points (k_cell_roots)
   int uf_flags = -1;                         // see XcdRange; -1 = read RPT_UF_FLAGS once
   int k5_legacy = -1;                        // 1: round-1 K5 (fill + point queue); RPT_K5_MODE
   int k5_fill = 0;
@@ -2646,6 +2667,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   bud.add<int32_t>(n);      // slab (global finalize; denoise: orig -> sorted)
   bud.add<uint8_t>(C1);     // fok (denoise)
   bud.add<int32_t>(C1);     // cell_min
+  bud.add<int32_t>(C1);     // cell_root
   bud.add<uint64_t>(C1);    // cell_min_pair (union star initialisation)
   bud.add<uint32_t>(n / 32 + 1);  // min_bits
   bud.add<int32_t>(n / 32 + 2);   // min_pref
@@ -2682,6 +2704,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   slab = arena.carve_n<int32_t>(n);
   fok = arena.carve_n<uint8_t>(C1);
   cell_min = arena.carve_n<int32_t>(C1);
+  cell_root = arena.carve_n<int32_t>(C1);
   cell_min_pair = arena.carve_n<uint64_t>(C1);
   min_bits = arena.carve_n<uint32_t>(n / 32 + 1);
   min_pref = arena.carve_n<int32_t>(n / 32 + 2);
@@ -2915,17 +2938,18 @@ int32_t DbscanState::union_pass(hipStream_t st) {
 }
 
 // component minima (k_ccmin; also queues the non-core points) -> MinRank prefix and cluster count
-int32_t DbscanState::cluster_ids(hipStream_t st) {
+// cell_key (nullable, pre-filled with INT_MAX): also the per-cell smallest component key
+int32_t DbscanState::cluster_ids(hipStream_t st, int32_t* cell_key) {
   const int64_t W = min_words();
   RPT_HIP(hipMemsetAsync(min_bits, 0, sizeof(uint32_t) * W, st));
-  // per-cell roots of the mutual cells into cell_min (re-filled before k_cell_min_key)
+  // per-cell roots of the mutual cells (read by k_ccmin for their core points)
   const bool cr = cell_roots_enabled();
   if (cr)
     hipLaunchKernelGGL(k_cell_roots, dim3(grid_for(n, kBlock, 2048)), dim3(kBlock), 0, st, parent,
-                       occ, n_occ_dev, C, mutual, rep, cell_min);
+                       occ, n_occ_dev, C, mutual, rep, cell_root);
   hipLaunchKernelGGL(k_ccmin, dim3(tile_grid(n)), dim3(kBlock), 0, st, parent, core, n, sorig,
                      ccmin, min_bits, nc_list, nc_list + n, skey, mutual,
-                     cr ? (const int32_t*)cell_min : nullptr, C);
+                     cr ? (const int32_t*)cell_root : nullptr, C, cell_key);
   hipLaunchKernelGGL(k_word_popc, dim3(grid_for(W, kBlock, 2048)), dim3(kBlock), 0, st, min_bits,
                      W, min_pref);
   RPT_CHECK_LAUNCH();
@@ -2947,12 +2971,11 @@ int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hi
   }
   int32_t* nc_count = nc_list + n;
   RPT_HIP(hipMemsetAsync(nc_count, 0, sizeof(int32_t), st));
-  RPT_TRY(cluster_ids(st));
-  const MinRank mr{min_bits, min_pref};
-  hipLaunchKernelGGL(k_label_core, dim3(gb), dim3(kBlock), 0, st, ccmin, n, sorig, mr, labels);
   const int gc = grid_for(C, kBlock, 8192);
   hipLaunchKernelGGL(k_fill_i32, dim3(gc), dim3(kBlock), 0, st, cell_min, C, INT_MAX);
-  hipLaunchKernelGGL(k_cell_min_key, dim3(gb), dim3(kBlock), 0, st, skey, ccmin, n, C, cell_min);
+  RPT_TRY(cluster_ids(st, cell_min));  // also the per-cell smallest keys (k_cell_min_key fused)
+  const MinRank mr{min_bits, min_pref};
+  hipLaunchKernelGGL(k_label_core, dim3(gb), dim3(kBlock), 0, st, ccmin, n, sorig, mr, labels);
   if (dim == 2)
     hipLaunchKernelGGL((k_label<2, false>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
                        rec<2>(), occ_bits, slab_t, ccmin, cell_min, mutual, sorig, mr, nc_list,
@@ -3058,7 +3081,7 @@ int32_t DbscanState::labels_fifo(int32_t* labels, rpt_stdbscan_stats* stats, hip
   int32_t* nc_count = nc_list + n;
   int32_t* spos = slab;
   RPT_HIP(hipMemsetAsync(nc_count, 0, sizeof(int32_t), st));
-  RPT_TRY(cluster_ids(st));
+  RPT_TRY(cluster_ids(st, nullptr));
   hipLaunchKernelGGL(k_inverse_perm, dim3(gb), dim3(kBlock), 0, st, sorig, n, spos);
   RPT_CHECK_LAUNCH();
   const MinRank mr{min_bits, min_pref};
