@@ -339,6 +339,15 @@ __global__ __launch_bounds__(kBlock) void k_occ_list(const int32_t* __restrict__
 constexpr int kBucketBlock = 1024;
 constexpr int kBucketCells = 16384;  // per-slab cells held in LDS (64 KiB)
 constexpr int kBucketU = 4;          // points per thread per round (loads in flight together)
+constexpr int64_t kChunkPts = 16384;  // points per slab-bucket block when a slab is split
+// RPT_SLAB_CHUNKS=k: k blocks per slab (1 = the single-block k_slab_bucket; A/B)
+static int slab_chunks_override() {
+  static const int v = [] {
+    const char* e = std::getenv("RPT_SLAB_CHUNKS");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
 
 // slab_lo[s] = first point of slab s (points ordered by slab), slab_lo[nt] = n
 __global__ void k_slab_lo(const float* __restrict__ t, int64_t n, Geom g,
@@ -492,6 +501,162 @@ __global__ __launch_bounds__(kBucketBlock) void k_slab_bucket(
   if (s == g.nt - 1 && threadIdx.x == 0) {  // the isolated cell (empty here) and the end
     cell_start[g.cells] = hi;
     cell_start[g.cells + 1] = hi;
+  }
+}
+
+// Several blocks per slab (dense slabs: one block per slab leaves most CUs idle and serialises
+// hundreds of thousands of points per block).  Chunk ch of slab s is its points
+// [lo + ch*len/CH, lo + (ch+1)*len/CH).  hist: [nt][CH][P] per-chunk cell counts, turned by
+// k_slab_chunk_scan into per-chunk write cursors; the scan also writes cell_start, the slab's
+// occupied cells + bits and its occupied count exactly like k_slab_bucket.
+__device__ __forceinline__ void slab_chunk(const int32_t* __restrict__ slab_lo, int s, int ch,
+                                           int CH, int& lo, int& hi) {
+  const int a = slab_lo[s], b = slab_lo[s + 1];
+  const int64_t len = (int64_t)(b - a);
+  lo = a + (int)(len * ch / CH);
+  hi = a + (int)(len * (ch + 1) / CH);
+}
+
+__global__ __launch_bounds__(kBucketBlock) void k_slab_chunk_hist(
+    const float* __restrict__ x, const float* __restrict__ y, int64_t stride, Geom g,
+    const int32_t* __restrict__ slab_lo, int CH, int32_t* __restrict__ hist_g) {
+  extern __shared__ int32_t hist[];
+  const int s = blockIdx.x / CH, ch = blockIdx.x - s * CH;
+  const int P = g.nx * g.ny;
+  int lo, hi;
+  slab_chunk(slab_lo, s, ch, CH, lo, hi);
+  for (int c = threadIdx.x; c < P; c += kBucketBlock) hist[c] = 0;
+  __syncthreads();
+  for (int i0 = lo; i0 < hi; i0 += kBucketBlock * kBucketU) {
+    float px[kBucketU], py[kBucketU];
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u) {
+      const int i = i0 + u * kBucketBlock + threadIdx.x;
+      px[u] = (i < hi) ? x[(int64_t)i * stride] : 0.f;
+      py[u] = (i < hi) ? y[(int64_t)i * stride] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u) {
+      const int i = i0 + u * kBucketBlock + threadIdx.x;
+      if (i < hi)
+        atomicAdd(&hist[cell_of((double)py[u], g.oy, g.inv_cs, g.ny) * g.nx +
+                        cell_of((double)px[u], g.ox, g.inv_cs, g.nx)], 1);
+    }
+  }
+  __syncthreads();
+  int32_t* out = hist_g + (int64_t)blockIdx.x * P;
+  for (int c = threadIdx.x; c < P; c += kBucketBlock) out[c] = hist[c];
+}
+
+__global__ __launch_bounds__(kBucketBlock) void k_slab_chunk_scan(
+    Geom g, const int32_t* __restrict__ slab_lo, int CH, int32_t* __restrict__ hist_g,
+    int32_t* __restrict__ cell_start, int32_t* __restrict__ occ_tmp,
+    int32_t* __restrict__ slab_occ, uint32_t* __restrict__ occ_bits) {
+  __shared__ int32_t wsum[kBucketBlock / 64], wocc[kBucketBlock / 64];
+  const int s = blockIdx.x;
+  const int P = g.nx * g.ny;
+  const int lo = slab_lo[s], hi = slab_lo[s + 1];
+  int32_t* hs = hist_g + (int64_t)s * CH * P;
+  const int per = (P + kBucketBlock - 1) / kBucketBlock;
+  const int c0 = threadIdx.x * per, c1 = min(c0 + per, P);
+  int run = 0, orun = 0;
+  for (int c = c0; c < c1; ++c) {
+    int h = 0;
+    for (int ch = 0; ch < CH; ++ch) h += hs[(int64_t)ch * P + c];
+    run += h;
+    orun += (h > 0) ? 1 : 0;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x / 64;
+  int incl = run, oincl = orun;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(incl, off, 64);
+    const int oo = __shfl_up(oincl, off, 64);
+    if (lane >= off) {
+      incl += o;
+      oincl += oo;
+    }
+  }
+  if (lane == 63) {
+    wsum[w] = incl;
+    wocc[w] = oincl;
+  }
+  __syncthreads();
+  int before = 0, obefore = 0, otot = 0;
+  for (int v = 0; v < kBucketBlock / 64; ++v) {
+    if (v < w) {
+      before += wsum[v];
+      obefore += wocc[v];
+    }
+    otot += wocc[v];
+  }
+  int acc = before + incl - run;
+  int oacc = lo + obefore + oincl - orun;
+  uint32_t word = 0xffffffffu, mask = 0u;
+  for (int c = c0; c < c1; ++c) {
+    cell_start[(int64_t)s * P + c] = lo + acc;
+    int h = 0;
+    for (int ch = 0; ch < CH; ++ch) {  // per-chunk cursors (slab-local), chunk order
+      const int k = hs[(int64_t)ch * P + c];
+      hs[(int64_t)ch * P + c] = acc + h;
+      h += k;
+    }
+    acc += h;
+    if (h > 0) {
+      const int64_t key = (int64_t)s * P + c;
+      occ_tmp[oacc++] = (int32_t)key;
+      const uint32_t wd = (uint32_t)(key >> 5);
+      if (wd != word) {
+        if (mask) atomicOr(occ_bits + word, mask);
+        word = wd;
+        mask = 0u;
+      }
+      mask |= 1u << (key & 31);
+    }
+  }
+  if (mask) atomicOr(occ_bits + word, mask);
+  if (threadIdx.x == 0) slab_occ[s] = otot;
+  if (s == g.nt - 1 && threadIdx.x == 0) {  // the isolated cell (empty here) and the end
+    cell_start[g.cells] = hi;
+    cell_start[g.cells + 1] = hi;
+  }
+}
+
+__global__ __launch_bounds__(kBucketBlock) void k_slab_chunk_scatter(
+    const float* __restrict__ x, const float* __restrict__ y, int64_t stride,
+    const float* __restrict__ t, Geom g, const int32_t* __restrict__ slab_lo, int CH,
+    const int32_t* __restrict__ hist_g, float4* __restrict__ pts, int32_t* __restrict__ sorig,
+    int32_t* __restrict__ skey) {
+  extern __shared__ int32_t cur[];
+  const int s = blockIdx.x / CH, ch = blockIdx.x - s * CH;
+  const int P = g.nx * g.ny;
+  int lo, hi;
+  slab_chunk(slab_lo, s, ch, CH, lo, hi);
+  const int base = slab_lo[s];
+  const int32_t* hc = hist_g + (int64_t)blockIdx.x * P;
+  for (int c = threadIdx.x; c < P; c += kBucketBlock) cur[c] = hc[c];
+  __syncthreads();
+  for (int i0 = lo; i0 < hi; i0 += kBucketBlock * kBucketU) {
+    float px[kBucketU], py[kBucketU], pt[kBucketU];
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u) {
+      const int i = i0 + u * kBucketBlock + threadIdx.x;
+      px[u] = (i < hi) ? x[(int64_t)i * stride] : 0.f;
+      py[u] = (i < hi) ? y[(int64_t)i * stride] : 0.f;
+      pt[u] = (i < hi) ? t[i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u) {
+      const int i = i0 + u * kBucketBlock + threadIdx.x;
+      if (i < hi) {
+        const int c = cell_of((double)py[u], g.oy, g.inv_cs, g.ny) * g.nx +
+                      cell_of((double)px[u], g.ox, g.inv_cs, g.nx);
+        const int dst = base + atomicAdd(&cur[c], 1);
+        pts[dst] = make_float4(px[u], py[u], pt[u], pt[u]);
+        sorig[dst] = i;
+        skey[dst] = s * P + c;
+      }
+    }
   }
 }
 
@@ -2734,11 +2899,37 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
     // the slabs write their occupied cells (ascending) into hpos at their point offsets, the
     // occupancy bits and their counts; one scan over the slabs and a gather give the list
     const size_t hist_bytes = sizeof(int32_t) * (size_t)nx * ny;
-    RPT_HIP(hipFuncSetAttribute((const void*)k_slab_bucket,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)hist_bytes));
-    hipLaunchKernelGGL(k_slab_bucket, dim3((unsigned)nt), dim3(kBucketBlock), hist_bytes, st, x,
-                       y, stride, t, g, slab_lo, pts, sorig, skey, cell_start, hpos, slab_occ,
-                       occ_bits);
+    // blocks per slab (measured, same box): dense slabs (> 128 k points) split into ~kChunkPts
+    // point chunks (configs[4] share: grid 2.93 -> 2.04 ms); short stacks split until ~512 blocks
+    // fill the GPU (125 frames: 0.193 -> 0.177 ms); 1000 standard slabs stay one block each
+    // (three chunks measured 1.10 -> 1.25 ms).  The chunk histograms live in the radix key
+    // buffers (4 n words, dead on this path).
+    const int64_t avg = n / std::max<int64_t>(nt, 1);
+    int64_t ch = avg > 8 * kChunkPts ? (avg + kChunkPts - 1) / kChunkPts : 1;
+    ch = std::max<int64_t>(ch, (512 + nt - 1) / std::max<int64_t>(nt, 1));
+    int CH = (int)std::min<int64_t>(ch, 64);
+    while (CH > 1 && (int64_t)nt * CH * nx * ny > 4 * n) --CH;
+    if (slab_chunks_override() > 0) CH = slab_chunks_override();
+    if (CH > 1 && (int64_t)nt * CH * nx * ny <= 4 * n) {
+      int32_t* hist_g = reinterpret_cast<int32_t*>(keys);
+      RPT_HIP(hipFuncSetAttribute((const void*)k_slab_chunk_hist,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)hist_bytes));
+      RPT_HIP(hipFuncSetAttribute((const void*)k_slab_chunk_scatter,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)hist_bytes));
+      hipLaunchKernelGGL(k_slab_chunk_hist, dim3((unsigned)(nt * CH)), dim3(kBucketBlock),
+                         hist_bytes, st, x, y, stride, g, slab_lo, CH, hist_g);
+      hipLaunchKernelGGL(k_slab_chunk_scan, dim3((unsigned)nt), dim3(kBucketBlock), 0, st, g,
+                         slab_lo, CH, hist_g, cell_start, hpos, slab_occ, occ_bits);
+      hipLaunchKernelGGL(k_slab_chunk_scatter, dim3((unsigned)(nt * CH)), dim3(kBucketBlock),
+                         hist_bytes, st, x, y, stride, t, g, slab_lo, CH, hist_g, pts, sorig,
+                         skey);
+    } else {
+      RPT_HIP(hipFuncSetAttribute((const void*)k_slab_bucket,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)hist_bytes));
+      hipLaunchKernelGGL(k_slab_bucket, dim3((unsigned)nt), dim3(kBucketBlock), hist_bytes, st,
+                         x, y, stride, t, g, slab_lo, pts, sorig, skey, cell_start, hpos,
+                         slab_occ, occ_bits);
+    }
     RPT_CHECK_LAUNCH();
     RPT_TRY(exclusive_scan_total_i32(slab_occ, occ_base, nt, st));
     hipLaunchKernelGGL(k_occ_gather, dim3((unsigned)nt), dim3(kBlock), 0, st, hpos, slab_lo,
