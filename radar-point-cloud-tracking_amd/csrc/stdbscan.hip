@@ -337,7 +337,7 @@ __global__ __launch_bounds__(kBlock) void k_occ_list(const int32_t* __restrict__
 // histogram scan directly.  Order inside a cell is arrival order: nothing downstream depends on
 // it (roots are minimum ORIGINAL indices, counts and minima are order-free).
 constexpr int kBucketBlock = 1024;
-constexpr int kBucketCells = 16384;  // per-slab cells held in LDS (64 KiB)
+constexpr int kBucketCells = 16384;  // max per-slab cells for the LDS histogram (<= 64 KiB)
 constexpr int kBucketU = 4;          // points per thread per round (loads in flight together)
 constexpr int64_t kChunkPts = 16384;  // points per slab-bucket block when a slab is split
 // RPT_SLAB_CHUNKS=k: k blocks per slab (1 = the single-block k_slab_bucket; A/B)

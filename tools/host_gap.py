@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Host time per step around rpt_stack_run (one stack in flight): wall per step, time inside the
-native call, and the Python before / after it.  Usage: python tools/host_gap.py FRAMES [async]"""
+native call, and the Python before / after it.  Usage: python tools/host_gap.py FRAMES
+[async | nohost] (nohost: async with the order + tracker stage replaced by a no-op)."""
 import sys
 import time
 from pathlib import Path
@@ -14,7 +15,10 @@ from rpt.pipeline import FrameStackPipeline, PathParams  # noqa: E402
 from rpt.synth import DeviceSynth, SynthConfig  # noqa: E402
 
 F = int(sys.argv[1]) if len(sys.argv) > 1 else 125
-async_host = len(sys.argv) > 2 and sys.argv[2] == "async"
+async_host = len(sys.argv) > 2 and sys.argv[2] in ("async", "nohost")
+if len(sys.argv) > 2 and sys.argv[2] == "nohost":  # host stage replaced by a no-op (GIL probe)
+    import rpt.pipeline as _pl
+    _pl.order_and_track = lambda *a, **k: (None, None, None)
 dev = torch.device("cuda", 0)
 cfg = SynthConfig(n_frames=F, rows=4096)
 ds = DeviceSynth(cfg, dev)
