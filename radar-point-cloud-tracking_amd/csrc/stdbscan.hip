@@ -2361,14 +2361,22 @@ __global__ __launch_bounds__(kBlock) void k_ccmin_global(int32_t* parent,
                                                         int64_t nr, int32_t* __restrict__ ccmin,
                                                         int32_t* __restrict__ gl,
                                                         int32_t* __restrict__ nc_list,
-                                                        int32_t* __restrict__ nc_count) {
+                                                        int32_t* __restrict__ nc_count,
+                                                        const int32_t* __restrict__ skey = nullptr,
+                                                        const uint8_t* __restrict__ mutual = nullptr,
+                                                        const int32_t* __restrict__ cell_root = nullptr,
+                                                        int64_t cells = 0) {
   for (int64_t tile = (int64_t)blockIdx.x * kBlock * kItems; tile < n;
        tile += (int64_t)gridDim.x * kBlock * kItems) {
     block_append(
         tile, n,
         [&](int64_t s) -> bool {
           if (!core[s]) return true;
-          const int x = uf_find(parent, (int)s);
+          // core points of a mutual cell: their cell's root (k_cell_roots), as in k_ccmin
+          const int32_t key = cell_root ? skey[s] : -1;
+          const int x = (cell_root && key >= 0 && (int64_t)key < cells && mutual[key])
+                            ? cell_root[key]
+                            : uf_find(parent, (int)s);
           const int m = sorig[x];
           ccmin[s] = m;
           if (x == (int)s) gl[m] = rep_id(reps, nr, rep[m]);
@@ -3218,8 +3226,13 @@ int32_t DbscanState::labels_global(const int64_t* rep_orig, const int64_t* reps,
   const int gb = grid_for(n, kBlock, 2048);
   int32_t* nc_count = nc_list + n;
   RPT_HIP(hipMemsetAsync(nc_count, 0, sizeof(int32_t), st));
+  const bool cr = cell_roots_enabled();
+  if (cr)
+    hipLaunchKernelGGL(k_cell_roots, dim3(grid_for(n, kBlock, 2048)), dim3(kBlock), 0, st, parent,
+                       occ, n_occ_dev, C, mutual, rep, cell_root);
   hipLaunchKernelGGL(k_ccmin_global, dim3(tile_grid(n)), dim3(kBlock), 0, st, parent, core, n,
-                     sorig, rep_orig, reps, nr, ccmin, cid, nc_list, nc_count);
+                     sorig, rep_orig, reps, nr, ccmin, cid, nc_list, nc_count, skey, mutual,
+                     cr ? (const int32_t*)cell_root : nullptr, C);
   hipLaunchKernelGGL(k_label_global_core, dim3(gb), dim3(kBlock), 0, st, core, ccmin, cid, sorig,
                      n, slab, labels);
   const int gc = grid_for(C, kBlock, 8192);
