@@ -310,6 +310,10 @@ int32_t rpt_stack_segments(const rpt_stack* h, int32_t* frame, int32_t* label, i
  * are not written -- 8 B per point less K1 and land traffic) */
 int32_t rpt_stack_points(const rpt_stack* h, float* x, float* y, float* intensity,
                          int32_t* gain, int32_t* point_frame, int32_t* labels, void* stream);
+/* core flags (dev u8 [n_clustered], 1 = core) of the last run's clustered points, in the order
+ * of rpt_stack_points: K5's result, for full-size invariant checks.  Call on the stream of that
+ * run, before another ST-DBSCAN runs on it (the flags live in that stream's ST-DBSCAN state). */
+int32_t rpt_stack_core_flags(const rpt_stack* h, uint8_t* core, void* stream);
 /* ---- frame-sharded multi-GPU driver ----------------------------------------
  * One rank's phases of ONE global stack whose contiguous frame ranges are spread over ranks; the
  * caller runs the collectives between phases (rpt/dist.py: torch.distributed over RCCL / gloo) on
@@ -450,13 +454,24 @@ int32_t rpt_tracker_object_history(const rpt_tracker* t, int32_t idx, float* px,
  * file's end are zero.  status_out[i]: 0 ok, 1 unreadable or more fields than names (read_csv
  * raises: the reference returns an empty sweep), 2 no data row (df.empty: empty sweep), 3 a value
  * that is not an integer in 0..255 with echo_dtype u8 (parse again as f32), 4 a non-numeric value
- * (the reference's to_numpy(float32) raises ValueError). */
+ * (the reference's to_numpy(float32) raises ValueError).
+ * detail_out (nullable) [n_files][5]: {kind (0 none, 1 I/O error, 2 tokenizing error, 3
+ * non-numeric value, 5 genfromtxt rows of < 5 fields), errno | expected fields | field index |
+ * field count, physical line (1-based), fields seen, gain flags (bit 0 the first row's Gain is
+ * NaN, bit 1 rows disagree -- NaN-aware like Series.unique())}: the parts of the exception
+ * texts read_csv / to_numpy raise ("Error tokenizing data. C error: Expected E fields in line L,
+ * saw S") and of int(df["Gain"].iloc[0]) / unique().
+ * mode 0: read_csv as above.  mode 1: np.genfromtxt(delimiter=',', skip_header=1,
+ * filling_values=0.0) first, read_csv when genfromtxt raises (rows of different field counts) --
+ * the denoise loader (PointCloudWorkF/stdbscan_denoising_pipeline.py:97-119): '#' starts a
+ * comment, empty or unreadable fields are 0.0, one data row is an empty sweep (status 2);
+ * status 6: a field count other than 5 + bins (not supported). */
 int32_t rpt_csv_count_rows(const char* const* paths, int32_t n_files, int64_t* rows_out,
                            int32_t n_threads);
 int32_t rpt_csv_parse_sweeps(const char* const* paths, int32_t n_files, int32_t rows_cap,
                              int32_t bins, int32_t echo_dtype, void* echo /*host*/,
                              float* scale, float* angle, float* gain_col, int32_t* status_out,
-                             int32_t n_threads);
+                             int64_t* detail_out, int32_t mode, int32_t n_threads);
 
 /* ---- synthetic input (bench / parity tests) -----------------------------------------
  * Deterministic u8 echo [n_frames][n_gains][rows][bins] from integer hashes; see

@@ -60,6 +60,11 @@ def _lib():
         lib.oracle_stdbscan_denoise.restype = C.c_int32
         lib.oracle_stdbscan_denoise.argtypes = lib.oracle_stdbscan.argtypes[:7] + [
             C.c_int32, C.c_void_p]
+        lib.oracle_sample_check.restype = C.c_int32
+        lib.oracle_sample_check.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int64,
+                                            C.c_double, C.c_double, C.c_void_p, C.c_int64,
+                                            C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                            C.c_void_p]
         lib.oracle_neighbour_counts.restype = C.c_int32
         lib.oracle_neighbour_counts.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int64,
                                                 C.c_double, C.c_double, C.c_void_p]
@@ -120,6 +125,27 @@ def stdbscan_denoise(coords, times, eps_space: float, eps_time: float, min_sampl
     if r < 0:
         raise MemoryError("oracle_stdbscan_denoise failed")
     return labels
+
+
+def sample_check(coords, times, eps_space: float, eps_time: float, idx, core, labels):
+    """For the sample points idx: exact neighbour counts (self included) and the smallest /
+    largest label among their core neighbours under the CLAIMED core flags and labels of every
+    point (-1 when none) -- the checker for full-size runs the oracle cannot label whole."""
+    c, t = _prep(coords, times)
+    idx = np.ascontiguousarray(idx, dtype=np.int64)
+    core = np.ascontiguousarray(core, dtype=np.uint8)
+    labels = np.ascontiguousarray(labels, dtype=np.int32)
+    assert core.shape[0] == labels.shape[0] == c.shape[0]
+    cnt = np.empty(len(idx), np.int64)
+    lo = np.empty(len(idx), np.int32)
+    hi = np.empty(len(idx), np.int32)
+    r = _lib().oracle_sample_check(c.ctypes.data, c.shape[1], t.ctypes.data, c.shape[0],
+                                   float(eps_space), float(eps_time), idx.ctypes.data, len(idx),
+                                   core.ctypes.data, labels.ctypes.data, cnt.ctypes.data,
+                                   lo.ctypes.data, hi.ctypes.data)
+    if r < 0:
+        raise ValueError("oracle_sample_check needs integral finite times (grid mode)")
+    return cnt, lo, hi
 
 
 def neighbour_counts(coords, times, eps_space: float, eps_time: float) -> np.ndarray:

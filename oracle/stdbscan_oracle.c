@@ -143,7 +143,26 @@ static void build_grid(ctx_t* x) {
     pairs[2 * m + 1] = i;
     ++m;
   }
-  qsort(pairs, (size_t)m, 2 * sizeof(int64_t), cmp_pair);
+  /* (key, index) order: a stable counting sort when the key range is small (same order as
+   * the comparison sort, linear time on stacks of tens of millions of points) */
+  const double nkeys = cells * (double)(x->smax + 1);
+  if (nkeys <= 4.0 * (double)m + 16777216.0) {
+    const int64_t K = (int64_t)nkeys;
+    int64_t* cnt = (int64_t*)calloc((size_t)K + 1, sizeof(int64_t));
+    int64_t* tmp = (int64_t*)malloc(sizeof(int64_t) * 2 * (size_t)(m > 0 ? m : 1));
+    for (int64_t k = 0; k < m; ++k) ++cnt[pairs[2 * k] + 1];
+    for (int64_t k = 0; k < K; ++k) cnt[k + 1] += cnt[k];
+    for (int64_t k = 0; k < m; ++k) {
+      const int64_t d = cnt[pairs[2 * k]]++;
+      tmp[2 * d] = pairs[2 * k];
+      tmp[2 * d + 1] = pairs[2 * k + 1];
+    }
+    free(cnt);
+    free(pairs);
+    pairs = tmp;
+  } else {
+    qsort(pairs, (size_t)m, 2 * sizeof(int64_t), cmp_pair);
+  }
   x->gc = (float*)malloc(sizeof(float) * (size_t)(m > 0 ? m : 1) * (size_t)x->dim);
   x->gt = (float*)malloc(sizeof(float) * (size_t)(m > 0 ? m : 1));
   for (int64_t k = 0; k < m; ++k) {
@@ -361,6 +380,63 @@ int32_t oracle_neighbour_counts(const float* coords, int32_t dim, const float* t
   for (int64_t i = 0; i < n; ++i) counts[i] = neighbours(&x, i, nb);
   free(x.order); free(x.tsorted); free(nb); free(x.gkey); free(x.gidx); free(x.gc);
   free(x.gt);
+  return 0;
+}
+
+/* For sample points idx[0..m): the exact neighbour count (self included) and, given a claimed
+ * labelling (core flags + labels of ALL points, e.g. a device run's), the smallest and largest
+ * label among the core neighbours (-1 / -1 when none).  A full-size invariant check: core flags
+ * of the sample must equal count >= min_samples, a core sample's core neighbours all share its
+ * label, a non-core sample takes the smallest adjacent label.  OpenMP. */
+static int pair_ok(const ctx_t* x, int64_t i, int64_t p);
+
+int32_t oracle_sample_check(const float* coords, int32_t dim, const float* times, int64_t n,
+                            double eps_space, double eps_time, const int64_t* idx, int64_t m,
+                            const uint8_t* core, const int32_t* labels, int64_t* count_out,
+                            int32_t* lo_out, int32_t* hi_out) {
+  ctx_t x;
+  memset(&x, 0, sizeof(x));
+  x.c = coords;
+  x.dim = dim;
+  x.t = times;
+  x.eps2 = (eps_space >= 0.0) ? eps_space * eps_space : -1.0;
+  x.epst = (float)eps_time;
+  x.n = n;
+  build_grid(&x);
+  if (!x.grid) {
+    free(x.gkey); free(x.gidx); free(x.gc); free(x.gt);
+    return -1;
+  }
+  const int64_t mr = max_ranges(&x);
+#pragma omp parallel
+  {
+    int64_t* r = (int64_t*)malloc(sizeof(int64_t) * 2 * (size_t)mr);
+#pragma omp for schedule(dynamic, 16)
+    for (int64_t k = 0; k < m; ++k) {
+      const int64_t i = idx[k];
+      int64_t cnt = 0;
+      int32_t lo = -1, hi = -1;
+      if (isfinite(x.t[i])) {
+        const int64_t nr = grid_ranges(&x, i, r);
+        for (int64_t q = 0; q < nr; ++q)
+          for (int64_t p = r[2 * q]; p < r[2 * q + 1]; ++p) {
+            if (!pair_ok(&x, i, p)) continue;
+            ++cnt;
+            const int64_t j = x.gidx[p];
+            if (core[j]) {
+              const int32_t l = labels[j];
+              if (lo < 0 || l < lo) lo = l;
+              if (hi < 0 || l > hi) hi = l;
+            }
+          }
+      }
+      count_out[k] = cnt;
+      lo_out[k] = lo;
+      hi_out[k] = hi;
+    }
+    free(r);
+  }
+  free(x.gkey); free(x.gidx); free(x.gc); free(x.gt);
   return 0;
 }
 

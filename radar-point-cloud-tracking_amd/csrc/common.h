@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -34,6 +35,18 @@ void clear_error();
 #define RPT_CHECK_LAUNCH() RPT_HIP(hipGetLastError())
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// A/B switches (RPT_* environment variables selecting a replaced kernel form for same-box
+// measurements) exist only in the A/B build (-DRPT_AB, tools/ab_*.sh): the shipped librpt.so
+// ignores the environment and always runs the default forms the parity suite covers.
+inline const char* ab_env(const char* name) {
+#ifdef RPT_AB
+  return std::getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 // Waits for the work queued on st so far by polling an event (readback latency; prims.hip).
 int32_t wait_stream(hipStream_t st);  // also reports device faults (check_device_faults)

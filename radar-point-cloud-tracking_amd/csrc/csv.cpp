@@ -23,6 +23,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cctype>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -33,9 +34,13 @@
 namespace rpt {
 namespace {
 
-bool read_file(const char* path, std::string& buf) {
+bool read_file(const char* path, std::string& buf, int* err = nullptr) {
+  errno = 0;
   FILE* f = std::fopen(path, "rb");
-  if (!f) return false;
+  if (!f) {
+    if (err) *err = errno;
+    return false;
+  }
   buf.clear();
   if (std::fseek(f, 0, SEEK_END) == 0) {
     const long sz = std::ftell(f);
@@ -46,6 +51,7 @@ bool read_file(const char* path, std::string& buf) {
   size_t k;
   while ((k = std::fread(tmp, 1, sizeof tmp, f)) > 0) buf.append(tmp, k);
   const bool ok = !std::ferror(f);
+  if (!ok && err) *err = errno ? errno : EIO;
   std::fclose(f);
   return ok;
 }
@@ -56,21 +62,29 @@ inline bool is_blank_line(const char* a, const char* b) {
   return true;
 }
 
-// Data lines after the first physical line: [begin, end) ranges without the newline.
-void data_lines(const std::string& s, std::vector<std::pair<const char*, const char*>>& out) {
+// Data lines after the first physical line: [begin, end) ranges without the newline, and (when
+// asked) their 1-based physical line numbers.
+void data_lines(const std::string& s, std::vector<std::pair<const char*, const char*>>& out,
+                std::vector<int64_t>* lineno = nullptr) {
   out.clear();
+  if (lineno) lineno->clear();
   const char* p = s.data();
   const char* e = p + s.size();
   const char* nl = static_cast<const char*>(std::memchr(p, '\n', (size_t)(e - p)));
   if (!nl) return;  // header only (or nothing)
   p = nl + 1;
+  int64_t ln = 2;
   while (p < e) {
     const char* q = static_cast<const char*>(std::memchr(p, '\n', (size_t)(e - p)));
     const char* le = q ? q : e;
     const char* lt = le;
     if (lt > p && lt[-1] == '\r') --lt;
-    if (lt > p && !is_blank_line(p, lt)) out.push_back({p, lt});
+    if (lt > p && !is_blank_line(p, lt)) {
+      out.push_back({p, lt});
+      if (lineno) lineno->push_back(ln);
+    }
     p = q ? q + 1 : e;
+    ++ln;
   }
 }
 
@@ -122,11 +136,144 @@ inline FieldKind parse_field(const char* a, const char* b, double* v) {
 
 constexpr int kMeta = 5;  // Status, Scale, Range, Gain, Angle
 
+// Python float(str) on one field [a, b): surrounding whitespace, optional sign, decimal digits
+// with single underscores between digits, optional fraction / exponent, or nan / inf /
+// infinity in any case.  false = float() raises (genfromtxt then uses the filling value).
+inline bool py_float(const char* a, const char* b, double* v) {
+  auto ws = [](char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\n' || c == '\v' || c == '\f'; };
+  while (a < b && ws(*a)) ++a;
+  while (b > a && ws(b[-1])) --b;
+  if (a == b || b - a > 120) return false;
+  char tmp[128];
+  int n = 0;
+  const char* p = a;
+  if (*p == '+' || *p == '-') tmp[n++] = *p++;
+  auto word = [&](const char* w) {
+    const size_t L = std::strlen(w);
+    if ((size_t)(b - p) != L) return false;
+    for (size_t k = 0; k < L; ++k)
+      if (std::tolower((unsigned char)p[k]) != w[k]) return false;
+    return true;
+  };
+  if (word("nan") || word("inf") || word("infinity")) {
+    *v = std::tolower((unsigned char)*p) == 'n' ? NAN : INFINITY;
+    if (n && tmp[0] == '-') *v = -*v;
+    return true;
+  }
+  // digits (with underscores between digits) [. digits] [e [sign] digits]
+  auto digits = [&](bool& any) {
+    any = false;
+    bool prev_digit = false;
+    while (p < b) {
+      if (*p >= '0' && *p <= '9') {
+        tmp[n++] = *p++;
+        any = prev_digit = true;
+      } else if (*p == '_' && prev_digit && p + 1 < b && p[1] >= '0' && p[1] <= '9') {
+        ++p;
+        prev_digit = false;
+      } else {
+        break;
+      }
+    }
+  };
+  bool int_part = false, frac_part = false;
+  digits(int_part);
+  if (p < b && *p == '.') {
+    tmp[n++] = *p++;
+    digits(frac_part);
+  }
+  if (!int_part && !frac_part) return false;
+  if (p < b && (*p == 'e' || *p == 'E')) {
+    tmp[n++] = *p++;
+    if (p < b && (*p == '+' || *p == '-')) tmp[n++] = *p++;
+    bool ex = false;
+    digits(ex);
+    if (!ex) return false;
+  }
+  if (p != b) return false;
+  tmp[n] = 0;
+  *v = std::strtod(tmp, nullptr);
+  return true;
+}
+
+// np.genfromtxt(path, delimiter=',', skip_header=1, dtype=float32, filling_values=0.0), the first
+// loader of PointCloudWorkF/stdbscan_denoising_pipeline.py:97-119: the first physical line is
+// skipped, text from '#' on is a comment, blank lines are skipped, a field float() cannot read
+// (empty, non-numeric) is 0.0, every row must have the first row's field count (else genfromtxt
+// raises and the reference falls back to pandas: return -1).  One row gives a 1-D array and no
+// column gives none: both the reference's "data.ndim != 2" empty sweep (return 2).  Field counts
+// other than 5 + bins: return 6 (fewer than 5 make data[:, 4] raise in the reference, det[0] = 5).
+int32_t parse_genfromtxt(const std::string& buf, int32_t rows_cap, int32_t bins, int32_t dt,
+                         void* echo_f, float* scale_f, float* angle_f, int64_t* det,
+                         std::vector<std::pair<const char*, const char*>>& lines) {
+  lines.clear();
+  const char* p = buf.data();
+  const char* e = p + buf.size();
+  const char* nl = static_cast<const char*>(std::memchr(p, '\n', (size_t)(e - p)));
+  p = nl ? nl + 1 : e;
+  int64_t ncols = -1;
+  while (p < e) {
+    const char* q = static_cast<const char*>(std::memchr(p, '\n', (size_t)(e - p)));
+    const char* le = q ? q : e;
+    const char* hc = static_cast<const char*>(std::memchr(p, '#', (size_t)(le - p)));
+    const char* lt = hc ? hc : le;
+    if (!is_blank_line(p, lt)) {
+      int64_t nf = 1;
+      for (const char* c = p; (c = static_cast<const char*>(std::memchr(c, ',', (size_t)(lt - c)))); ++c)
+        ++nf;
+      if (ncols < 0) ncols = nf;
+      if (nf != ncols) return -1;  // genfromtxt: "Line #k (got m columns instead of n)"
+      lines.push_back({p, lt});
+    }
+    p = q ? q + 1 : e;
+  }
+  const int64_t R = (int64_t)lines.size();
+  if (R <= 1 || ncols <= 1) return 2;
+  if (ncols < kMeta) {
+    det[0] = 5;
+    det[1] = ncols;
+    return 1;
+  }
+  if (ncols != kMeta + bins) return 6;
+  if (R > rows_cap) return 6;
+  for (int64_t r = 0; r < R; ++r) {
+    const char* a = lines[(size_t)r].first;
+    const char* le = lines[(size_t)r].second;
+    uint8_t* e8 = static_cast<uint8_t*>(echo_f) + (size_t)r * bins;
+    float* e32 = static_cast<float*>(echo_f) + (size_t)r * bins;
+    for (int64_t f = 0; f < ncols; ++f) {
+      const char* c = static_cast<const char*>(std::memchr(a, ',', (size_t)(le - a)));
+      const char* fe = c ? c : le;
+      double v = 0.0;
+      if (!py_float(a, fe, &v)) v = 0.0;  // filling_values
+      if (f >= kMeta) {
+        if (dt == RPT_ECHO_U8) {
+          if (!(v >= 0.0 && v <= 255.0 && v == std::floor(v))) return 3;
+          e8[f - kMeta] = (uint8_t)v;
+        } else {
+          e32[f - kMeta] = (float)v;
+        }
+      } else if (f == 1) {
+        scale_f[r] = (float)v;
+      } else if (f == 4) {
+        angle_f[r] = (float)v;
+      }
+      a = c ? c + 1 : le;
+    }
+  }
+  return 0;
+}
+
 // status: 0 ok, 1 unreadable / tokenizing error (empty sweep), 2 no data row (df.empty),
-// 3 a value not representable in u8 (the caller re-parses as float32), 4 non-numeric value
+// 3 a value not representable in u8 (the caller re-parses as float32), 4 non-numeric value.
+// det[5]: {kind (0 none, 1 I/O error, 2 tokenizing error, 3 non-numeric value, 5 genfromtxt
+// rows of fewer than 5 fields), errno | expected fields | field index | field count,
+// physical line, fields seen, gain flags (bit 0 first-row Gain NaN, bit 1 rows disagree)}
+constexpr int kDetail = 5;
 int32_t parse_one(const char* path, int32_t rows_cap, int32_t bins, int32_t dt, void* echo_f,
                   float* scale_f, float* angle_f, float* gain_f, std::string& buf,
-                  std::vector<std::pair<const char*, const char*>>& lines) {
+                  std::vector<std::pair<const char*, const char*>>& lines,
+                  std::vector<int64_t>& lineno, int64_t* det, int32_t mode) {
   const size_t row_bytes = (size_t)bins * (dt == RPT_ECHO_U8 ? 1 : 4);
   auto zero_tail = [&](int64_t from) {
     if (from >= rows_cap) return;
@@ -135,11 +282,28 @@ int32_t parse_one(const char* path, int32_t rows_cap, int32_t bins, int32_t dt, 
     for (int64_t r = from; r < rows_cap; ++r) scale_f[r] = angle_f[r] = 0.0f;
   };
   *gain_f = 0.0f;
-  if (!read_file(path, buf)) {
+  for (int k = 0; k < kDetail; ++k) det[k] = 0;
+  int err = 0;
+  if (!read_file(path, buf, &err)) {
+    det[0] = 1;
+    det[1] = err;
     zero_tail(0);
     return 1;
   }
-  data_lines(buf, lines);
+  if (mode == 1) {  // genfromtxt first; pandas when it raises (inconsistent field counts)
+    const int32_t gs = parse_genfromtxt(buf, rows_cap, bins, dt, echo_f, scale_f, angle_f, det,
+                                        lines);
+    if (gs >= 0) {
+      if (gs == 0) {
+        zero_tail((int64_t)lines.size());
+      } else {
+        zero_tail(0);
+        if (gs == 2) lines.clear();
+      }
+      return gs;
+    }
+  }
+  data_lines(buf, lines, &lineno);
   if (lines.empty()) {
     zero_tail(0);
     return 2;
@@ -169,9 +333,18 @@ int32_t parse_one(const char* path, int32_t rows_cap, int32_t bins, int32_t dt, 
     for (;;) {
       const char* c = static_cast<const char*>(std::memchr(p, ',', (size_t)(e - p)));
       const char* fe = c ? c : e;
-      if (f >= n_fields + skip) {
+      if (f >= n_fields + skip) {  // "Expected 1029 fields in line L, saw S": read_csv raises
+        int64_t saw = f + 1;
+        for (const char* q = fe; q < e && (q = static_cast<const char*>(
+                                               std::memchr(q, ',', (size_t)(e - q))));
+             ++q)
+          ++saw;
+        det[0] = 2;
+        det[1] = n_fields + skip;
+        det[2] = lineno[(size_t)r];
+        det[3] = saw;
         zero_tail(0);
-        return 1;  // "Expected 1029 fields ... saw more": read_csv raises
+        return 1;
       }
       if (f < skip) {  // index columns
         ++f;
@@ -181,7 +354,33 @@ int32_t parse_one(const char* path, int32_t rows_cap, int32_t bins, int32_t dt, 
       }
       double v = 0.0;
       const FieldKind k = parse_field(p, fe, &v);
-      if (k == kBad) {
+      // read_csv mode: the tracker never converts Status / Range (object columns are harmless
+      // there) and reads Gain only through int(iloc[0]) / unique(): a text Gain counts as NaN
+      const int fcol = f - skip;
+      if (k == kBad && !(mode == 0 && (fcol == 0 || fcol == 2 || fcol == 3))) {
+        // to_numpy(float32) of the object column(s): numpy converts column block by column
+        // block, so the value it names is the first bad one of the LEFTMOST bad column
+        int64_t bl = lineno[(size_t)r], bc = f;
+        for (int64_t r2 = r + 1; r2 < (int64_t)lines.size() && bc > 0; ++r2) {
+          const char* a2 = lines[(size_t)r2].first;
+          const char* e2 = lines[(size_t)r2].second;
+          for (int64_t f2 = 0; f2 < bc; ++f2) {
+            const char* c2 = static_cast<const char*>(std::memchr(a2, ',', (size_t)(e2 - a2)));
+            double v2;
+            const int fc2 = (int)(f2 - skip);
+            if (f2 >= skip && !(mode == 0 && (fc2 == 0 || fc2 == 2 || fc2 == 3)) &&
+                parse_field(a2, c2 ? c2 : e2, &v2) == kBad) {
+              bl = lineno[(size_t)r2];
+              bc = f2;
+              break;
+            }
+            if (!c2) break;
+            a2 = c2 + 1;
+          }
+        }
+        det[0] = 3;
+        det[1] = bc;  // physical field index (implicit index columns included)
+        det[2] = bl;
         zero_tail(0);
         return 4;
       }
@@ -203,10 +402,13 @@ int32_t parse_one(const char* path, int32_t rows_cap, int32_t bins, int32_t dt, 
         an = (k == kNum) ? (float)v : NAN;
       } else if (fc == 3) {  // Gain: the first value, NaN when rows disagree (unique() > 1)
         const float gv = (k == kNum) ? (float)v : NAN;
-        if (r == 0)
+        if (r == 0) {
           *gain_f = gv;
-        else if (!(gv == *gain_f))
+          if (gv != gv) det[4] |= 1;
+        } else if (!(gv == *gain_f) && !(gv != gv && (det[4] & 1))) {
           *gain_f = NAN;
+          det[4] |= 2;
+        }
       }
       ++f;
       if (!c) break;
@@ -271,10 +473,10 @@ int32_t rpt_csv_count_rows(const char* const* paths, int32_t n_files, int64_t* r
 int32_t rpt_csv_parse_sweeps(const char* const* paths, int32_t n_files, int32_t rows_cap,
                              int32_t bins, int32_t echo_dtype, void* echo, float* scale,
                              float* angle, float* gain_col, int32_t* status_out,
-                             int32_t n_threads) {
+                             int64_t* detail_out, int32_t mode, int32_t n_threads) {
   clear_error();
   if (n_files < 0 || rows_cap < 0 || bins <= 0 ||
-      (echo_dtype != RPT_ECHO_U8 && echo_dtype != RPT_ECHO_F32) ||
+      (echo_dtype != RPT_ECHO_U8 && echo_dtype != RPT_ECHO_F32) || mode < 0 || mode > 1 ||
       (n_files > 0 && (!paths || !echo || !scale || !angle || !gain_col || !status_out))) {
     set_error("rpt_csv_parse_sweeps: bad arguments");
     return RPT_EINVAL;
@@ -284,13 +486,16 @@ int32_t rpt_csv_parse_sweeps(const char* const* paths, int32_t n_files, int32_t 
   auto work = [&]() {
     std::string buf;
     std::vector<std::pair<const char*, const char*>> lines;
+    std::vector<int64_t> lineno;
+    int64_t det_local[kDetail];
     for (;;) {
       const int32_t i = next.fetch_add(1);
       if (i >= n_files) return;
       status_out[i] = parse_one(
           paths[i], rows_cap, bins, echo_dtype,
           static_cast<char*>(echo) + (size_t)i * (size_t)rows_cap * (size_t)bins * es,
-          scale + (size_t)i * rows_cap, angle + (size_t)i * rows_cap, gain_col + i, buf, lines);
+          scale + (size_t)i * rows_cap, angle + (size_t)i * rows_cap, gain_col + i, buf, lines,
+          lineno, detail_out ? detail_out + (size_t)i * kDetail : det_local, mode);
     }
   };
   const int T = resolve_threads(n_threads, n_files);

@@ -609,7 +609,7 @@ int32_t bounds_xy(const float* x, const float* y, int64_t n, float* out4, hipStr
 // RPT_LAND_U8=0: the int32 + float64 atomics kernel also for u8 points (A/B)
 static bool land_u8_enabled() {
   static const bool on = [] {
-    const char* e = std::getenv("RPT_LAND_U8");
+    const char* e = ab_env("RPT_LAND_U8");
     return !(e && std::atoi(e) == 0);
   }();
   return on;

@@ -765,7 +765,7 @@ inline uint32_t u8_k(int T) {
 constexpr int kExpandBlocks = 2048;
 inline bool expand_write_enabled() {
   static const bool on = [] {
-    const char* e = std::getenv("RPT_K1_EXPAND");
+    const char* e = ab_env("RPT_K1_EXPAND");
     return !(e && std::atoi(e) == 0);
   }();
   return on;

@@ -64,6 +64,7 @@ int32_t stdbscan_bounds_dev(const float* x, const float* y, const float* t, int6
 int32_t frame_times_dev(const int32_t* pf, int64_t n_max, const int64_t* n_dev, float* t,
                         hipStream_t st);
 int32_t stdbscan_fill_stats(void* state, int32_t n_clusters, rpt_stdbscan_stats* stats);
+int32_t stdbscan_core_flags(void* state, int64_t n, uint8_t* out, hipStream_t st);
 int32_t cluster_summaries_dev(const int32_t* labels, const float* x, const float* y,
                               const float* inten, const int32_t* pf, int64_t n, int32_t n_frames,
                               int bits, int64_t s_hint, int32_t* o_frame, int32_t* o_label,
@@ -277,6 +278,8 @@ struct rpt_stack {
   }
 
   bool had_gain = false;  // the last run wrote per-point gains (gain table given)
+  void* db_state = nullptr;      // the last run's ST-DBSCAN state (per device and stream) ...
+  hipStream_t db_stream = nullptr;  // ... and its stream (rpt_stack_core_flags)
   int32_t run(const rpt_stack_params& p, const void* echo, const float* scale,
               const float* cos_t, const float* sin_t, const int32_t* gain, rpt_stack_result* out,
               hipStream_t st);
@@ -295,6 +298,7 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
   n_frames = F;
   land_applied = false;
   had_gain = gain != nullptr;
+  db_state = nullptr;
   const bool timing = p.timing != 0;
   if (timing && !ev_ok) {
     for (auto& e : ev) RPT_HIP(hipEventCreate(&e));
@@ -314,7 +318,7 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
   const bool grouped = p.echo_dtype == RPT_ECHO_U8 && p.bins == 1024 &&
                        (uintptr_t)echo % 16 == 0;
   if (k1_staged < 0) {
-    const char* e = std::getenv("RPT_K1_STAGE");
+    const char* e = ab_env("RPT_K1_STAGE");
     k1_staged = (e && std::atoi(e) == 0) ? 0 : 1;
   }
   uint32_t* mk = nullptr;
@@ -484,6 +488,8 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
   RPT_TRY(stdbscan_deferred(cx, cy, nullptr, 1, t.p, n_in_, p.eps_space, p.eps_time,
                             p.min_samples, labels.p, &sts, st, 2, &ncl_dev, &dstate,
                             land_applied ? dbscan_bounds.data() : nullptr));
+  db_state = dstate;
+  db_stream = st;
   if (timing) RPT_HIP(hipEventRecord(ev[3], st));
 
   // ---- K9 summaries (per-(frame, label) segments)
@@ -652,6 +658,20 @@ int32_t rpt_stack_points(const rpt_stack* h, float* x, float* y, float* intensit
   RPT_TRY(cp(point_frame, l ? h->pf2.p : h->pf.p, 4));
   RPT_TRY(cp(labels, h->labels.p, 4));
   return RPT_OK;
+}
+
+int32_t rpt_stack_core_flags(const rpt_stack* h, uint8_t* core, void* stream) {
+  clear_error();
+  if (!h || !core) return RPT_EINVAL;
+  if (!h->db_state || h->n_in <= 0) {
+    set_error("rpt_stack_core_flags: the last rpt_stack_run clustered no points");
+    return RPT_EINVAL;
+  }
+  if (as_stream(stream) != h->db_stream) {
+    set_error("rpt_stack_core_flags: call on the stream of the last rpt_stack_run");
+    return RPT_EINVAL;
+  }
+  return stdbscan_core_flags(h->db_state, h->n_in, core, as_stream(stream));
 }
 
 }  // extern "C"
@@ -875,7 +895,7 @@ int32_t rpt_shard_polar(rpt_shard* h, const rpt_stack_params* p, const void* ech
   const bool grouped = p->echo_dtype == RPT_ECHO_U8 && p->bins == 1024 &&
                        (uintptr_t)echo % 16 == 0;
   if (S.k1_staged < 0) {
-    const char* e = std::getenv("RPT_K1_STAGE");
+    const char* e = ab_env("RPT_K1_STAGE");
     S.k1_staged = (e && std::atoi(e) == 0) ? 0 : 1;
   }
   uint32_t* mk = nullptr;  // staged kept samples, as in rpt_stack_run

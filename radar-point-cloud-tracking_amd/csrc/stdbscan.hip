@@ -343,7 +343,7 @@ constexpr int64_t kChunkPts = 16384;  // points per slab-bucket block when a sla
 // RPT_SLAB_CHUNKS=k: k blocks per slab (1 = the single-block k_slab_bucket; A/B)
 static int slab_chunks_override() {
   static const int v = [] {
-    const char* e = std::getenv("RPT_SLAB_CHUNKS");
+    const char* e = ab_env("RPT_SLAB_CHUNKS");
     return e ? std::atoi(e) : 0;
   }();
   return v;
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(kBucketBlock) void k_slab_bucket(
     const uint64_t hm = __ballot(v && (ln == 0 || up != c));
     const uint64_t lm = __ballot(v && (ln == 63 || dn != c));
     const uint64_t below = (ln == 63) ? ~0ull : ((2ull << ln) - 1ull);
-    head = 63 - __builtin_clzll(hm & below | 1ull);  // hm has a bit at or below ln when v
+    head = 63 - __builtin_clzll((hm & below) | 1ull);  // hm has a bit at or below ln when v
     const int last = ln + __builtin_ctzll((lm >> ln) | (1ull << (63 - ln)));
     rank = ln - head;
     len = last - head + 1;
@@ -1179,10 +1179,9 @@ __device__ __forceinline__ int classify_cells(const float4& A1, const float4& B1
   return (dmax <= g.eps2 && tm <= g.epst) ? 1 : 2;
 }
 
-// Tuning flags of the union kernels (rpt_set_tuning / RPT_UF_FLAGS): bit 0 = finds inside the
+// Tuning flags of the union kernels (RPT_UF_FLAGS in the A/B build): bit 0 = finds inside the
 // union kernels do not path-halve (agent-scope stores drop the line from the XCD's L2; k_compress
-// compresses afterwards); bit 2 = timing experiment only: skip the box-certain unites (labels
-// are then WRONG); bit 1 = XCD-aware item ranges (blockIdx % 8 = XCD under round-robin
+// compresses afterwards); bit 1 = XCD-aware item ranges (blockIdx % 8 = XCD under round-robin
 // placement: each XCD unions a contiguous range of cells, so its L2 keeps their parents).
 // XcdRange is also the item split of the K5 / K7 queue kernels.
 struct XcdRange {
@@ -1206,7 +1205,7 @@ constexpr uint32_t kPmaskFull = 0x80000000u;
 // RPT_CELL_ROOTS=0: k_ccmin walks every core point's parent chain (A/B)
 static bool cell_roots_enabled() {
   static const bool on = [] {
-    const char* e = std::getenv("RPT_CELL_ROOTS");
+    const char* e = ab_env("RPT_CELL_ROOTS");
     return !(e && std::atoi(e) == 0);
   }();
   return on;
@@ -1334,7 +1333,7 @@ __global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
                                                           const float2* __restrict__ slab_t,
                                                           int32_t* __restrict__ cflag,
                                                           int32_t* __restrict__ zero_counter,
-                                                          uint8_t* __restrict__ core, int exp) {
+                                                          uint8_t* __restrict__ core) {
   // legacy pipeline: the level-4 queue counter, zeroed here instead of by a memset launch
   // (k_core_fill, the next kernel on the stream, is its first user)
   if (zero_counter && blockIdx.x == 0 && threadIdx.x == 0) *zero_counter = 0;
@@ -1397,8 +1396,6 @@ __global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
       const bool reach = sv && sr.x <= sr.y && gap <= g.epst;  // this lane's slab is in reach
       if (need <= 0 || (mu && e - b >= need)) {
         flag = 1;
-      } else if (exp) {  // timing experiment only (RPT_K5_EXP): flags are WRONG
-        flag = 2;
       } else {
         int lo = 0, hi = 0;
         const float4 A1 = rec_boxA<2>(ra), A2 = rec_boxB(ra);
@@ -1918,7 +1915,6 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
                                         (uint32_t)(m1 >> 32) & ~kPmaskFull)
                            : make_uint4(0u, 0u, 0u, kPmaskFull);
         }
-        if (uf_flags & 4) continue;  // timing experiment only
         // neighbours' roots in parallel, then ONE unite per distinct root (dense regions give
         // a dozen box-certain neighbours that mostly share a root already)
         const int rA = uf_find(parent, ra, halve);
@@ -2689,7 +2685,6 @@ struct DbscanState {
   int uf_flags = -1;                         // see XcdRange; -1 = read RPT_UF_FLAGS once
   int k5_legacy = -1;                        // 1: round-1 K5 (fill + point queue); RPT_K5_MODE
   int k5_fill = 0;
-  int k5_exp = 0;                            // timing experiments only (RPT_K5_EXP)
   int bucket_mode = -1;                      // RPT_K4_BUCKET (default 1): slab-bucket K4
   template <int D>
   const CellRec<D>* rec() const {
@@ -2758,7 +2753,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   g.eps2 = eps_space * eps_space;
   g.epst = epst;
   static const bool screen_on = [] {
-    const char* e = std::getenv("RPT_F32_SCREEN");
+    const char* e = ab_env("RPT_F32_SCREEN");
     return !(e && e[0] == '0');
   }();
   const bool screen = screen_on && g.eps2 >= 1e-20 && g.eps2 <= 1e30;
@@ -2778,7 +2773,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   // so more of them are decided whole: 0.7 eps in 2-D (1000-frame stack 12.86 -> 12.41 ms, the
   // dense share's K5 0.66 -> 0.84 of roofline, same box); RPT_CELL_SIDE overrides (0.5 - 0.7)
   static const double side_f = [] {
-    const char* e = std::getenv("RPT_CELL_SIDE");
+    const char* e = ab_env("RPT_CELL_SIDE");
     const double v = e ? std::atof(e) : 0.0;
     return (v >= 0.5 && v <= 0.7) ? v : 0.7;
   }();
@@ -2894,7 +2889,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
     return RPT_ENOMEM;
   }
   if (bucket_mode < 0) {
-    const char* e = std::getenv("RPT_K4_BUCKET");
+    const char* e = ab_env("RPT_K4_BUCKET");
     bucket_mode = (e && std::atoi(e) == 0) ? 0 : 1;
   }
   // time-ordered finite 2-D points with a slab's cells fitting LDS: per-slab counting sort
@@ -3002,9 +2997,7 @@ int32_t DbscanState::core_pass(hipStream_t st) {
     // default 0: the folded variants measured no faster on the 100- and 1000-frame stacks
     // (profiles/r2/ab_k5_k1.md): the per-point flag writes moved into the cell kernel cost what
     // the fill pass cost, and the cell-wise slow pass balances worse than the point queue
-    const char* x = std::getenv("RPT_K5_EXP");
-    k5_exp = x ? std::atoi(x) : 0;
-    const char* e = std::getenv("RPT_K5_MODE");
+    const char* e = ab_env("RPT_K5_MODE");
     k5_legacy = e ? std::atoi(e) : 0;
     k5_legacy = (k5_legacy == 0) ? 1 : 0;
     k5_fill = (e && std::atoi(e) == 2) ? 1 : 0;
@@ -3021,7 +3014,7 @@ int32_t DbscanState::core_pass(hipStream_t st) {
     if (oct) {
       hipLaunchKernelGGL(k_core_cells_oct, dim3((grid_for(8 * n, kBlock, 8192) + 7) & ~7), dim3(kBlock), 0,
                          st, g, (int)rs, occ, n_occ, rec<2>(), mutual, occ_bits, slab_t, cflag,
-                         (int32_t*)nullptr, k5_fill ? (uint8_t*)nullptr : core, k5_exp);
+                         (int32_t*)nullptr, k5_fill ? (uint8_t*)nullptr : core);
       if (k5_fill)
         hipLaunchKernelGGL(k_core_fill<false>, dim3(tile_grid(n)), dim3(kBlock), 0, st, skey, n,
                            cflag, core, slow, n_slow);
@@ -3052,7 +3045,7 @@ int32_t DbscanState::core_pass(hipStream_t st) {
   if (oct) {
     hipLaunchKernelGGL(k_core_cells_oct, dim3((grid_for(8 * n, kBlock, 8192) + 7) & ~7), dim3(kBlock), 0,
                        st, g, (int)rs, occ, n_occ, rec<2>(), mutual, occ_bits, slab_t, cflag,
-                       n_slow, (uint8_t*)nullptr, k5_exp);
+                       n_slow, (uint8_t*)nullptr);
   } else {
     RPT_HIP(hipMemsetAsync(n_slow, 0, sizeof(int32_t), st));
     RPT_HIP(hipMemsetAsync(n_cq, 0, sizeof(int32_t), st));
@@ -3081,8 +3074,8 @@ int32_t DbscanState::core_pass(hipStream_t st) {
 int32_t DbscanState::union_pass(hipStream_t st) {
   if (degenerate) return RPT_OK;
   if (uf_flags < 0) {
-    const char* e = std::getenv("RPT_UF_FLAGS");
-    uf_flags = e ? std::atoi(e) : kDefaultUfFlags;
+    const char* e = ab_env("RPT_UF_FLAGS");
+    uf_flags = e ? (std::atoi(e) & 3) : kDefaultUfFlags;
   }
   const int gb = grid_for(n, kBlock, 2048);
   const int gc = grid_for(C, kBlock, 8192);
@@ -3098,7 +3091,7 @@ int32_t DbscanState::union_pass(hipStream_t st) {
   hipLaunchKernelGGL(k_parent_init_pair, dim3(gb), dim3(kBlock), 0, st, parent, n, core, skey,
                      mutual, cmin, C, rep);
   if (union_list < 0) {
-    const char* e = std::getenv("RPT_UNION_LIST");
+    const char* e = ab_env("RPT_UNION_LIST");
     union_list = (e && std::atoi(e) == 0) ? 0 : 1;
   }
   if (dim == 2) {
@@ -3125,7 +3118,7 @@ int32_t DbscanState::union_pass(hipStream_t st) {
   // every later reader walks to the root with path halving (k_ccmin, k_comp_out, ...), so a
   // separate compression pass only moves that work; RPT_UF_COMPRESS=1 keeps it (A/B)
   if (uf_compress < 0) {
-    const char* e = std::getenv("RPT_UF_COMPRESS");
+    const char* e = ab_env("RPT_UF_COMPRESS");
     uf_compress = (e && std::atoi(e) == 1) ? 1 : 0;
   }
   if (uf_compress)
@@ -3467,6 +3460,19 @@ int32_t stdbscan_deferred(const float* x, const float* y, const float* z, int64_
   *n_clusters_dev = S->defer ? S->n_clusters_ptr() : nullptr;
   *state = S;
   return s_;
+}
+
+// core flags (original order) of the state's last run: the stack driver's K5 result, for tests
+int32_t stdbscan_core_flags(void* state, int64_t n, uint8_t* out, hipStream_t st) {
+  DbscanState* S = static_cast<DbscanState*>(state);
+  if (!S || S->degenerate || S->n != n || !S->core || !S->sorig) {
+    set_error("rpt_stack_core_flags: no core flags for this run");
+    return RPT_EINVAL;
+  }
+  hipLaunchKernelGGL(k_core_to_orig, dim3(grid_for(n, kBlock, 2048)), dim3(kBlock), 0, st,
+                     S->core, S->sorig, n, out);
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
 }
 
 int32_t stdbscan_fill_stats(void* state, int32_t n_clusters, rpt_stdbscan_stats* stats) {

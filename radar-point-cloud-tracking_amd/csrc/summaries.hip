@@ -739,7 +739,7 @@ static int32_t summaries_impl(const int32_t* labels, const float* x, const float
   // per-frame counting sort unless forced off (RPT_K9_RADIX=1, or a redo after a frame held more
   // than kFsMaxKeys labels) or frames are huge (one 8-wave block per frame)
   static const bool env_radix = [] {
-    const char* e = std::getenv("RPT_K9_RADIX");
+    const char* e = ab_env("RPT_K9_RADIX");
     return e && e[0] == '1';
   }();
   const bool frame_sort = !force_radix && !env_radix && n_frames > 0 && n > 0 &&

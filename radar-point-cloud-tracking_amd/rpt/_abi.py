@@ -198,6 +198,7 @@ _SIGS = [
     ("rpt_stack_segments", C.c_int32, [vp, c_i32p, c_i32p, c_i64p, c_i64p, c_f32p, c_f32p, c_f32p,
                                        c_i64p]),
     ("rpt_stack_points", C.c_int32, [vp, vp, vp, vp, vp, vp, vp, vp]),
+    ("rpt_stack_core_flags", C.c_int32, [vp, vp, vp]),
     ("rpt_shard_create", vp, []),
     ("rpt_shard_destroy", None, [vp]),
     ("rpt_shard_polar", C.c_int32, [vp, C.POINTER(StackParams), vp, vp, vp, vp, vp,
@@ -235,7 +236,7 @@ _SIGS = [
     ("rpt_csv_count_rows", C.c_int32, [C.POINTER(C.c_char_p), C.c_int32, c_i64p, C.c_int32]),
     ("rpt_csv_parse_sweeps", C.c_int32,
      [C.POINTER(C.c_char_p), C.c_int32, C.c_int32, C.c_int32, C.c_int32, vp, c_f32p, c_f32p,
-      c_f32p, c_i32p, C.c_int32]),
+      c_f32p, c_i32p, c_i64p, C.c_int32, C.c_int32]),
     ("rpt_synth_echo", C.c_int32,
      [C.POINTER(SynthParams), C.c_int64, C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp]),
 ]

@@ -7,6 +7,11 @@ version, flags, offload arch) differs from the one recorded in ``build/STAMP``.
 ``-ffp-contract=off`` is global: the parity
 contract (bit-identical labels and centroids) forbids FMA contraction of the reference's
 separately rounded float operations.
+
+``build(ab=True)`` (``python -m rpt._build --ab``) compiles the same sources with ``-DRPT_AB``
+into ``rpt/librpt_ab.so`` (objects under ``build_ab/``): the only build whose kernels read the
+``RPT_*`` A/B switches from the environment (csrc/common.h ``ab_env``).  ``tools/ab_*.sh`` load it
+through ``RPT_LIB``; the shipped ``librpt.so`` ignores the environment.
 """
 from __future__ import annotations
 
@@ -21,6 +26,8 @@ CSRC = PKG_DIR.parent / "csrc"
 INCLUDE = PKG_DIR.parent.parent / "include"
 BUILD = PKG_DIR.parent / "build"
 LIB = PKG_DIR / "librpt.so"
+BUILD_AB = PKG_DIR.parent / "build_ab"
+LIB_AB = PKG_DIR / "librpt_ab.so"
 
 ARCH = os.environ.get("RPT_OFFLOAD_ARCH", "gfx950")
 COMMON_FLAGS = [
@@ -54,8 +61,8 @@ def _headers_mtime() -> float:
     return max((h.stat().st_mtime for h in hs), default=0.0)
 
 
-def _compile(src: Path, obj: Path) -> str:
-    cmd = [_hipcc(), *COMMON_FLAGS, "-c", str(src), "-o", str(obj)]
+def _compile(src: Path, obj: Path, extra=()) -> str:
+    cmd = [_hipcc(), *COMMON_FLAGS, *extra, "-c", str(src), "-o", str(obj)]
     if src.suffix == ".cpp":
         cmd.insert(1, "-x")
         cmd.insert(2, "hip")
@@ -65,41 +72,46 @@ def _compile(src: Path, obj: Path) -> str:
     return r.stderr
 
 
-def _stamp() -> str:
+def _stamp(extra=()) -> str:
     r = subprocess.run([_hipcc(), "--version"], capture_output=True, text=True)
-    return "\n".join([r.stdout.strip(), " ".join(COMMON_FLAGS), ARCH]) + "\n"
+    return "\n".join([r.stdout.strip(), " ".join([*COMMON_FLAGS, *extra]), ARCH]) + "\n"
 
 
-def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -> Path:
-    BUILD.mkdir(parents=True, exist_ok=True)
-    stamp_file = BUILD / "STAMP"
-    stamp = _stamp()
+def build(verbose: bool = False, force: bool = False, jobs: int | None = None,
+          ab: bool = False) -> Path:
+    extra = ("-DRPT_AB",) if ab else ()
+    build_dir, lib = (BUILD_AB, LIB_AB) if ab else (BUILD, LIB)
+    build_dir.mkdir(parents=True, exist_ok=True)
+    stamp_file = build_dir / "STAMP"
+    stamp = _stamp(extra)
     if not stamp_file.exists() or stamp_file.read_text() != stamp:
         force = True  # other flags, arch or compiler: objects built before are stale
     hdr_t = _headers_mtime()
     todo = []
     objs = []
     for src in _sources():
-        obj = BUILD / (src.name + ".o")
+        obj = build_dir / (src.name + ".o")
         objs.append(obj)
         if force or not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, hdr_t):
             todo.append((src, obj))
     jobs = jobs or min(8, max(1, os.cpu_count() or 1))
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        for (src, _), warn in zip(todo, ex.map(lambda a: _compile(*a), todo)):
+        for (src, _), warn in zip(todo, ex.map(lambda a: _compile(*a, extra), todo)):
             if verbose and warn.strip():
                 print(f"[rpt build] {src.name}:\n{warn}")
-    if todo or not LIB.exists():
-        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB),
+    if todo or not lib.exists():
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib),
                *[str(o) for o in objs]]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
-            raise RuntimeError(f"link of librpt.so failed:\n{r.stderr}")
+            raise RuntimeError(f"link of {lib.name} failed:\n{r.stderr}")
     stamp_file.write_text(stamp)
     if verbose:
-        print(f"[rpt build] {LIB} ({len(todo)} objects rebuilt)")
-    return LIB
+        print(f"[rpt build] {lib} ({len(todo)} objects rebuilt)")
+    return lib
 
 
 if __name__ == "__main__":
-    build(verbose=True)
+    import sys
+
+    build(verbose=True, ab="--ab" in sys.argv[1:])

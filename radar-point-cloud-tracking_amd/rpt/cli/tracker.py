@@ -65,12 +65,18 @@ def run_pipeline(data_dir: Path, output_dir: Path, max_frames: int = 0,
     import torch
 
     dev = torch.device("cuda", 0) if device is None else torch.device(device)
-    errors: List[Path] = []
-    stack = load_frame_stack(frame_files, dev, threads=csv_threads, on_error=errors.append)
-    for p in errors:
-        print(f"Error loading {p}: could not parse the file as the radar CSV format")
+    errors: List[tuple] = []
+    stack = load_frame_stack(frame_files, dev, threads=csv_threads,
+                             on_error=lambda p, e: errors.append((p, e)))
+    # build_frame's per-file "Error loading" lines (:194) interleave with the progress lines
+    frame_of = {Path(p): i for i, ff in enumerate(frame_files) for p in ff.values()}
+    by_frame = {}
+    for p, e in errors:
+        by_frame.setdefault(frame_of[Path(p)], []).append((p, e))
     F = len(frame_files)
     for i in range(F):
+        for p, e in by_frame.get(i, []):
+            print(f"Error loading {p}: {e}")
         if (i + 1) % 50 == 0:
             print(f"  Processed {i + 1}/{F} frames...")
     params = PathParams(eps_space=float(eps_space), eps_time=float(eps_time),

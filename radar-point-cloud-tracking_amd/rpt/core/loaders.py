@@ -48,7 +48,8 @@ class PointCloud:
 def load_radar_csv(path: Path, config: Optional[RadarConfig] = None) -> RadarSweep:
     """loaders.py:46-101: pd.read_csv(names=Status..Echo_n, skiprows=1) semantics through the
     native parser; an empty CSV raises ValueError, a malformed one raises like read_csv."""
-    from .ingest import STATUS_EMPTY, STATUS_NON_NUMERIC, STATUS_OK, read_sweeps
+    from .ingest import (GAIN_DISAGREE, GAIN_FIRST_NAN, STATUS_EMPTY, STATUS_NON_NUMERIC,
+                         STATUS_OK, read_sweeps)
 
     if config is None:
         config = RadarConfig()
@@ -61,15 +62,20 @@ def load_radar_csv(path: Path, config: Optional[RadarConfig] = None) -> RadarSwe
         raise ValueError(f"CSV is empty: {path}")
     if st == STATUS_NON_NUMERIC:
         raise ValueError(f"could not convert string to float in {path}")
-    if st != STATUS_OK:
-        raise ValueError(f"Error tokenizing data in {path}")
+    if st != STATUS_OK:  # read_csv's own exception text (ParserError is a ValueError)
+        raise ValueError(b.errors[0] or f"Error tokenizing data in {path}")
     n = int(b.rows[0])
     angles_rad = np.deg2rad(b.angle[0, :n] * config.angle_scale)
     echo = b.echo[0, :n].astype(np.float32)
     scale = b.scale[0, :n].copy()
     ranges = (scale[:, None] / echo.shape[1]) * np.arange(echo.shape[1], dtype=np.float32)
-    g = float(b.gain[0])
-    gain = int(g) if np.isfinite(g) else None
+    # gains = df["Gain"].unique(); one value -> int(it) (int(nan) raises), several -> None (:88-92)
+    flags = int(b.gain_flags[0])
+    gain = None
+    if not flags & GAIN_DISAGREE:
+        if flags & GAIN_FIRST_NAN:
+            raise ValueError("cannot convert float NaN to integer")
+        gain = int(float(b.gain[0]))
     return RadarSweep(angles_rad=angles_rad, ranges=ranges, intensities=echo, scale=scale,
                       gain=gain, source_path=path)
 

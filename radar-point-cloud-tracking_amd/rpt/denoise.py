@@ -108,13 +108,34 @@ class DenoiseFrames:
     z: torch.Tensor          # intensity
     t: torch.Tensor          # device float32 [n]: frame index (empty frames keep theirs)
     frame_counts: np.ndarray  # int64 [n_frames]
+    failed: List[tuple] = None  # [(frame index, exception text)] of frames whose load raised
 
 
-def load_frames(frames: List[Dict[int, Path]], device=None, threads: int = 0) -> DenoiseFrames:
+class FrameLoadError(Exception):
+    """A frame's load raised in the reference (sequential mode re-raises it as its own type)."""
+
+
+def _raise_like_reference(detail_kind: int, msg: str):
+    if detail_kind == 1:
+        import errno as _errno
+        code = int(msg.split("]")[0].split()[-1]) if msg.startswith("[Errno") else _errno.EIO
+        raise OSError(code, msg)
+    if detail_kind == 5:
+        raise IndexError(msg)
+    raise ValueError(msg)
+
+
+def load_frames(frames: List[Dict[int, Path]], device=None, threads: int = 0,
+                parallel: bool = False) -> DenoiseFrames:
     """load_frame / load_radar_csv (:97-152, :219-231) for every frame on the device: sweeps
-    parsed natively, K1 (threshold > 10, every 4th kept sample of each file) in one batch with
-    the frame's files in its dict order, times = frame index."""
-    from .core.ingest import STATUS_NON_NUMERIC, read_sweeps
+    parsed natively with the reference loader's semantics (np.genfromtxt first, pd.read_csv when
+    it raises: rpt.core.ingest MODE_GENFROMTXT), K1 (threshold > 10, every 4th kept sample of
+    each file) in one batch with the frame's files in its dict order, times = frame index.
+    A file whose load raises fails its whole frame (load_frame stops at it): with parallel=True
+    (load_frames_parallel, :234-257) the frame is empty and listed in `failed`; otherwise the
+    exception propagates as in the sequential loop (:910-915)."""
+    from .core.ingest import (MODE_GENFROMTXT, STATUS_NON_NUMERIC, STATUS_UNSUPPORTED,
+                              read_sweeps)
     from .core.transforms import trig_tables
 
     dev = require_gpu(device)
@@ -127,22 +148,40 @@ def load_frames(frames: List[Dict[int, Path]], device=None, threads: int = 0) ->
     n_files = len(paths)
     empty = torch.zeros(0, dtype=torch.float32, device=dev)
     if n_files == 0:
-        return DenoiseFrames(empty, empty, empty, empty, np.zeros(len(frames), np.int64))
-    batch = read_sweeps(paths, bins=NUM_ECHO_COLUMNS, threads=threads)
-    bad = [p for p, s in zip(paths, batch.status) if s == STATUS_NON_NUMERIC]
-    if bad:
-        raise ValueError(f"could not convert string to float in {bad[0]}")
+        return DenoiseFrames(empty, empty, empty, empty, np.zeros(len(frames), np.int64), [])
+    batch = read_sweeps(paths, bins=NUM_ECHO_COLUMNS, threads=threads, mode=MODE_GENFROMTXT)
+    unsup = [p for p, s in zip(paths, batch.status) if s == STATUS_UNSUPPORTED]
+    if unsup:
+        raise NotImplementedError(f"{unsup[0]}: rows of other than {5 + NUM_ECHO_COLUMNS} "
+                                  "fields are not supported by the denoise loader")
+    failed, dead = [], set()
+    for j, p in enumerate(paths):
+        f = fidx[j]
+        if f in dead:
+            continue   # load_frame stopped at this frame's first failing file
+        msg = batch.errors[j]
+        if msg is None and batch.status[j] == STATUS_NON_NUMERIC:
+            msg = f"could not convert string to float in {p}"
+        if msg is None:
+            continue
+        if not parallel:
+            _raise_like_reference(int(batch.detail_kind[j]), msg)
+        dead.add(f)
+        failed.append((f, msg))
+    keep_file = np.array([fidx[j] not in dead for j in range(n_files)], bool)
     R = max(int(batch.echo.shape[1]), 1)
     scale = np.zeros((n_files, R), np.float32)
     cos_t = np.zeros((n_files, R), np.float32)
     sin_t = np.zeros((n_files, R), np.float32)
     for j in range(n_files):
         n = int(batch.rows[j])
-        if batch.status[j] != 0 or n <= 0:
+        if batch.status[j] != 0 or n <= 0 or not keep_file[j]:
             continue
         scale[j, :n] = batch.scale[j, :n]
         cos_t[j, :n], sin_t[j, :n] = trig_tables(batch.angle[j, :n], ANGLE_SCALE)
     echo = np.ascontiguousarray(batch.echo)
+    if dead:   # a failed frame is empty (load_frames_parallel's empty arrays)
+        echo[~keep_file] = 0
     if echo.shape[1] == 0:
         echo = np.zeros((n_files, 1, NUM_ECHO_COLUMNS), echo.dtype)
     dt = _abi.ECHO_U8 if echo.dtype == np.uint8 else _abi.ECHO_F32
@@ -173,7 +212,7 @@ def load_frames(frames: List[Dict[int, Path]], device=None, threads: int = 0) ->
         fo_h = fo.cpu().numpy()
     counts = np.zeros(len(frames), np.int64)
     np.add.at(counts, np.asarray(fidx, np.int64), np.diff(fo_h))
-    return DenoiseFrames(x[:n], y[:n], z[:n], t[:n], counts)
+    return DenoiseFrames(x[:n], y[:n], z[:n], t[:n], counts, failed)
 
 
 def st_dbscan(coords, times, eps_space: float, eps_time: float, min_samples: int,
@@ -296,15 +335,22 @@ def run_pipeline(data_dir: Path, output_dir: Path, eps_space: float = DEFAULT_EP
         frames = frames[:max_frames]
         print(f"  Processing first {len(frames)} frames")
     print("\n[3/5] Converting radar data to Cartesian point clouds...")
-    if parallel and len(frames) > 4:
+    par = parallel and len(frames) > 4
+    if par:
         print(f"  Using parallel loading with {MAX_WORKERS} workers...")
-        progress = [f"  Loaded {k}/{len(frames)} frames..." for k in range(20, len(frames) + 1, 20)]
+    fr = load_frames(frames, device, parallel=par)
+    if par:
+        # load_frames_parallel (:234-257): a failed frame's warning, then every 20th completion
+        # (printed here in frame order; the reference's as_completed order varies run to run)
+        failed = dict(fr.failed)
+        for k in range(1, len(frames) + 1):
+            if k - 1 in failed:
+                print(f"  Warning: Failed to load frame {k - 1}: {failed[k - 1]}")
+            if k % 20 == 0:
+                print(f"  Loaded {k}/{len(frames)} frames...")
     else:
-        progress = [f"  Processed {k}/{len(frames)} frames..."
-                    for k in range(10, len(frames) + 1, 10)]
-    fr = load_frames(frames, device)
-    for line in progress:
-        print(line)
+        for k in range(10, len(frames) + 1, 10):
+            print(f"  Processed {k}/{len(frames)} frames...")
     total = int(fr.frame_counts.sum())
     print(f"  Total points: {total:,}")
     if total == 0:

@@ -22,7 +22,7 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 import torch
 
-from .core.ingest import STATUS_NON_NUMERIC, STATUS_UNREADABLE, read_sweeps
+from .core.ingest import GAIN_FIRST_NAN, STATUS_NON_NUMERIC, STATUS_OK, read_sweeps
 from .core.transforms import trig_tables
 
 
@@ -39,8 +39,10 @@ class FrameStackInput:
 
 def load_frame_stack(frame_files: Sequence[Dict[int, Path]], device, bins: int = 1024,
                      threads: int = 0, on_error=None) -> FrameStackInput:
-    """on_error(path): called for each file the reference's read_csv would reject (it prints
-    "Error loading ..." and uses an empty sweep)."""
+    """on_error(path, message): called, in frame order, for each file the reference's read_csv
+    would reject, with the text of read_csv's exception (the reference prints
+    f"Error loading {path}: {e}" and uses an empty sweep, :191-195).  A data file whose first
+    Gain value is missing raises ValueError like the reference's int(df["Gain"].iloc[0]) (:200)."""
     gains = sorted({g for ff in frame_files for g in ff})
     F, G = len(frame_files), len(gains)
     slots, paths = [], []
@@ -50,10 +52,14 @@ def load_frame_stack(frame_files: Sequence[Dict[int, Path]], device, bins: int =
                 slots.append(f * G + k)
                 paths.append(Path(ff[g]))
     batch = read_sweeps(paths, bins=bins, threads=threads)
-    bad = [p for p, s in zip(paths, batch.status) if s == STATUS_NON_NUMERIC]
-    if bad:
-        # the reference's to_numpy(np.float32) raises on a non-numeric column (uncaught, :207)
-        raise ValueError(f"could not convert string to float in {bad[0]}")
+    for j, p in enumerate(paths):  # the first file (in the reference's load order) that raises
+        st = int(batch.status[j])
+        if st == STATUS_OK and batch.rows[j] > 0 and batch.gain_flags[j] & GAIN_FIRST_NAN:
+            # int(df["Gain"].iloc[0]) of a NaN (uncaught, :200)
+            raise ValueError(f"cannot convert float NaN to integer ({p})")
+        if st == STATUS_NON_NUMERIC:
+            # the reference's to_numpy(np.float32) raises on a non-numeric column (uncaught, :207)
+            raise ValueError(f"could not convert string to float in {p}")
     R = max(int(batch.echo.shape[1]), 1)
     dt = torch.uint8 if batch.echo.dtype == np.uint8 else torch.float32
     echo = torch.zeros((F * G, R, bins), dtype=dt, device=device)
@@ -65,8 +71,8 @@ def load_frame_stack(frame_files: Sequence[Dict[int, Path]], device, bins: int =
         echo.index_copy_(0, idx, torch.from_numpy(batch.echo).to(device))
     for j, (s, p) in enumerate(zip(slots, paths)):
         st = int(batch.status[j])
-        if st == STATUS_UNREADABLE and on_error is not None:
-            on_error(p)
+        if batch.errors[j] is not None and on_error is not None:
+            on_error(p, batch.errors[j])
         n = int(batch.rows[j])
         if st != 0 or n <= 0:
             continue
@@ -89,8 +95,7 @@ def frame_points(frame_files: Dict[int, Path], threshold: float, stride: int, de
     from ._device import stream_handle
 
     stack = load_frame_stack([frame_files], device, bins=bins, threads=threads,
-                             on_error=lambda p: print(f"Error loading {p}: could not parse the "
-                                                      "file as the radar CSV format"))
+                             on_error=lambda p, e: print(f"Error loading {p}: {e}"))
     lib = _abi.load()
     G, R = len(stack.gains), stack.rows
     dt = _abi.ECHO_U8 if stack.echo.dtype == torch.uint8 else _abi.ECHO_F32

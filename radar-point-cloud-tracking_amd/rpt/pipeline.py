@@ -233,6 +233,12 @@ class FrameStackPipeline:
                                             pts["v"].data_ptr(), pts["gain"].data_ptr(),
                                             pts["frame"].data_ptr(), labels.data_ptr(), stream),
                        "rpt_stack_points")
+            if n:  # K5's core flags of the same points (full-size invariant checks)
+                pts["core"] = torch.empty(n, dtype=torch.uint8, device=self.dev)
+                if stream != stream_handle(self.dev):
+                    torch.cuda.current_stream(self.dev).synchronize()
+                _abi.check(lib.rpt_stack_core_flags(h, pts["core"].data_ptr(), stream),
+                           "rpt_stack_core_flags")
             if stream != stream_handle(self.dev):  # the caller reads them on torch's stream
                 torch.cuda.ExternalStream(stream, device=self.dev).synchronize()
             res.labels, res.points = labels, pts

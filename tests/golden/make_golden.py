@@ -27,6 +27,9 @@ are reproducible.  Outputs (all in tests/golden/):
   g10_denoise_pipeline.npz
                     stdbscan_denoising_pipeline.run_pipeline (:862-1046, no_viz) on a synthetic
                     CSV stack: stdout, both binary PLYs, denoising_stats.csv, clusters.csv
+  g11_corrupt.npz   the tracker's run_pipeline and the denoise run_pipeline (parallel loading)
+                    on a CSV stack with malformed files (corrupt_csv_stack): a tokenizing error,
+                    a one-row file, a comment line, empty fields, an empty Scale field
   meta.json         library versions / CPU of the generating run
 
     python tests/golden/make_golden.py [g7 g8 ...]   # only the named fixtures
@@ -558,6 +561,66 @@ def g10_denoise_pipeline(den, tmp: Path):
     np.savez_compressed(OUT / "g10_denoise_pipeline.npz", **rec)
 
 
+def corrupt_csv_stack(root: Path, denoise: bool = False):
+    """synth_csv_stack with malformed files (regenerated by the tests, never stored):
+    frame 3 gain 50: a last row with two fields too many (read_csv's tokenizing error; the
+    tracker prints "Error loading ...", the denoise loader fails the whole frame); frame 5 gain
+    40: one data row (genfromtxt's 1-D array: an empty sweep for the denoise loader); frame 6
+    gain 75: a comment line after row 10; frame 8 gain 40: empty echo fields in row 4; with
+    denoise=True also an empty Scale field in frame 6 gain 75's row 7 (genfromtxt fills 0.0;
+    pandas' NaN would reach the tracker's BallTree, which raises)."""
+    synth_csv_stack(root)
+    files = {g: sorted((root / f"gain_{g}").glob("*.csv")) for g in (40, 50, 75)}
+
+    def edit(path, fn):
+        lines = path.read_text().splitlines()
+        path.write_text("\n".join(fn(lines)) + "\n")
+
+    edit(files[50][3], lambda L: L + [L[-1] + ",7,7"])
+    edit(files[40][5], lambda L: L[:2])
+
+    def f6(L):
+        if denoise:
+            row = L[1 + 7].split(",")
+            row[1] = ""
+            L[1 + 7] = ",".join(row)
+        return L[:11] + ["# note: gain check"] + L[11:]
+    edit(files[75][6], f6)
+
+    def f8(L):
+        row = L[1 + 4].split(",")
+        for c in (5, 6, 300, 301, 302):
+            row[c] = ""
+        L[1 + 4] = ",".join(row)
+        return L
+    edit(files[40][8], f8)
+    return root
+
+
+def g11_corrupt(trk, den, tmp: Path):
+    rec = {}
+    data = corrupt_csv_stack(tmp / "stack")
+    buf = io.StringIO()
+    with redirect_stdout(buf):
+        trk.run_pipeline(data, tmp / "out", visualize=False)
+    rec["tracker_stdout"] = np.array(buf.getvalue())
+    for name in ("tracked_objects.csv", "trajectories.csv", "clusters.csv"):
+        rec["tracker_" + name.replace(".csv", "")] = np.array((tmp / "out" / name).read_text())
+    data = corrupt_csv_stack(tmp / "dstack", denoise=True)
+    out = tmp / "dout"
+    buf = io.StringIO()
+    with redirect_stdout(buf):
+        den.run_pipeline(data, out, eps_space=8.0, eps_time=2.0, min_samples=15, min_frames=2,
+                         max_frames=0, no_viz=True, parallel=True)
+    rec["denoise_stdout"] = np.array(buf.getvalue())
+    for name in ("denoised_point_cloud.ply", "raw_point_cloud.ply"):
+        rec["denoise_" + name.replace(".", "_")] = np.frombuffer((out / name).read_bytes(),
+                                                                 np.uint8)
+    for name in ("denoising_stats.csv", "clusters.csv"):
+        rec["denoise_" + name.replace(".", "_")] = np.array((out / name).read_text())
+    np.savez_compressed(OUT / "g11_corrupt.npz", **rec)
+
+
 def main():
     if not REF.exists():
         raise SystemExit("make_golden.py must run where /root/reference exists (build container)")
@@ -587,12 +650,14 @@ def main():
             g7_ply(ref3, tmp / "g7")
         if want("g8"):
             g8_fuse_max(tmp / "g8")
-        if want("g9") or want("g10"):
+        if want("g9") or want("g10") or want("g11"):
             den = _load("ref_denoise", REF / "PointCloudWorkF" / "stdbscan_denoising_pipeline.py")
             if want("g9"):
                 g9_denoise(den)
             if want("g10"):
                 g10_denoise_pipeline(den, tmp / "g10")
+            if want("g11"):
+                g11_corrupt(trk, den, tmp / "g11")
     import scipy
     import sklearn
     mp = OUT / "meta.json"

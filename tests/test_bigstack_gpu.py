@@ -1,0 +1,169 @@
+"""Parity at the bench's own headline workload (BASELINE configs[3]): ONE 1000-frame 3-gain
+fused stack, ~50 M points, land filter + ST-DBSCAN + per-frame clusters + tracker — bit-exact
+against the oracle (4_temporal_object_tracker.py run_pipeline :941-991).
+
+The oracle's outputs for the two seeded stacks the bench alternates (std0 = SynthConfig(
+n_frames=1000), std1 = seed 1 / target seed 124) are committed as per-frame / per-object digests
+by tests/golden/make_bigstack.py (the oracle needs minutes on this size; the digests are
+compared here in seconds, tests/_digest.py).
+
+* the bench's submit path: FrameStackPipeline(lanes=3, async_host=True) with std0 / std1
+  alternating, so every lane's second stack differs from its first (K1 capacity, K9 label-bit
+  and segment-count speculation from the previous run miss inside the checked runs);
+* the frame-sharded path at its real per-rank share: 8 ranks x 125 frames (gloo, sharing the
+  one GPU), rank 0 digests the gathered result.
+"""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from _digest import compare, device_digest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = Path(__file__).resolve().parents[1]
+GOLD = Path(__file__).resolve().parent / "golden"
+
+
+def _gold(name):
+    return json.loads((GOLD / f"bigstack_{name}.json").read_text())
+
+
+def _cfg(name):
+    from rpt.synth import SynthConfig
+
+    return SynthConfig(**_gold(name)["synth"])
+
+
+@pytest.mark.timeout(600)
+def test_bench_stacks_lanes3_match_oracle(gpu):
+    from rpt.pipeline import FrameStackPipeline, PathParams
+    from rpt.synth import DeviceSynth
+
+    names = ["std0", "std1"]
+    cfgs = [_cfg(n) for n in names]
+    dss = [DeviceSynth(c, gpu) for c in cfgs]
+    echoes = [d.echo() for d in dss]
+    torch.cuda.synchronize(gpu)
+    c0 = cfgs[0]
+    assert all(np.array_equal(d.geo.cos_t, dss[0].geo.cos_t) for d in dss)
+    pipe = FrameStackPipeline(c0.gains, c0.rows, c0.bins, PathParams(), gpu, async_host=True,
+                              lanes=3)
+    pipe.set_geometry(np.full(c0.rows, c0.scale, np.float32), dss[0].geo.cos_t,
+                      dss[0].geo.sin_t, c0.n_frames * len(c0.gains))
+    order = [0, 1, 0, 1, 0]   # lanes 0,1,2,0,1: lanes 0 and 1 switch workloads on their 2nd run
+    futs = [pipe.submit(echoes[k], keep_points=True) for k in order]
+    for i, (k, f) in enumerate(zip(order, futs)):
+        res = f.result().finish()
+        got = device_digest(res)
+        compare(got, _gold(names[k]), f"run {i} ({names[k]}, lane {i % 3})")
+        del res
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("world,lanes", [(8, 1), (4, 2)])
+def test_sharded_share_matches_oracle(world, lanes):
+    """world x (1000/world) frames: the per-rank shares of the 1000-frame stack (8 ranks = the
+    configs[3] strong-scaling share); lanes 2 alternates std0 / std1 through rpt.dist.ShardLanes."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env["OMP_NUM_THREADS"] = "2"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", str(ROOT / "tools" / "dist_check.py"),
+           "--backend", "gloo", "--frames", str(1000 // world), "--lanes", str(lanes),
+           "--digest", "std0,std1" if lanes > 1 else "std0"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=840)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "ok=True" in out, out[-4000:]
+
+
+@pytest.mark.timeout(600)
+def test_dense_config4_share_invariants(gpu):
+    """configs[4]'s per-GPU share at 8 GPUs: 125 dense frames (~490k points per frame, ~61 M
+    points, one component chaining the stack) — too large for a whole-stack oracle run, so
+    full-size invariants of the reference semantics instead:
+      * K5: the core flags of 20,000 random points equal the oracle's exact neighbour count
+        >= min_samples (oracle.sample_check);
+      * a core sample's core neighbours all carry its label; a non-core sample carries the
+        smallest label among its core neighbours, -1 without one (4_temporal_object_tracker.py
+        :493-504, the BFS's result);
+      * over ALL points: every core point is labelled, cluster ids ascend with each cluster's
+        minimum core index (the BFS opens clusters in index order), ids are dense;
+      * K9: segment counts equal the (frame, label) histogram; the centroids and mean
+        intensities of the largest and of 40 random segments equal np.mean as :527-531 take it.
+    """
+    import oracle
+    from rpt.pipeline import FrameStackPipeline, PathParams
+    from rpt.synth import DeviceSynth, dense_config
+
+    cfg = dense_config(n_frames=125)
+    ds = DeviceSynth(cfg, gpu)
+    pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), gpu)
+    pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
+                      cfg.n_frames * len(cfg.gains))
+    res = pipe.run(ds.echo(), keep_points=True)
+    n = res.n_clustered_input
+    assert n > 55_000_000
+    x = res.points["x"].cpu().numpy()
+    y = res.points["y"].cpu().numpy()
+    v = res.points["v"].cpu().numpy()
+    pf = res.points["frame"].cpu().numpy()
+    core = res.points["core"].cpu().numpy()
+    lab = res.labels.cpu().numpy()
+    xy = np.column_stack([x, y])
+    t = pf.astype(np.float32)
+
+    rng = np.random.default_rng(7)
+    idx = np.unique(np.concatenate([rng.choice(n, 20_000, replace=False), [0, n - 1]]))
+    cnt, lo, hi = oracle.sample_check(xy, t, 8.0, 2.0, idx, core, lab)
+    np.testing.assert_array_equal(core[idx], (cnt >= 15).astype(np.uint8))
+    c = core[idx] == 1
+    np.testing.assert_array_equal(lo[c], lab[idx][c])
+    np.testing.assert_array_equal(hi[c], lab[idx][c])
+    np.testing.assert_array_equal(lab[idx][~c], lo[~c])
+
+    cl = lab[core == 1]
+    assert (cl >= 0).all() and ((lab >= 0) | (core == 0)).all()
+    ids, first = np.unique(cl, return_index=True)
+    np.testing.assert_array_equal(ids, np.arange(res.n_clusters))
+    assert (np.diff(first) > 0).all(), "cluster ids must ascend with their minimum core index"
+    assert lab.max() == res.n_clusters - 1
+
+    seg = res.seg
+    m = lab >= 0
+    key = pf[m].astype(np.int64) << 32 | lab[m].astype(np.int64)
+    uk, uc = np.unique(key, return_counts=True)
+    sk = seg["frame"].astype(np.int64) << 32 | seg["label"].astype(np.int64)
+    o = np.argsort(sk)
+    np.testing.assert_array_equal(sk[o], uk)
+    np.testing.assert_array_equal(seg["count"][o], uc)
+    assert seg["count"].sum() == m.sum() and len(uk) == res.n_segments
+    pick = np.unique(np.concatenate([[int(np.argmax(seg["count"]))],
+                                     rng.choice(res.n_segments, 40, replace=False)]))
+    fstart = np.searchsorted(pf, np.arange(pf.max() + 2))
+    for s in pick:
+        f, lb = int(seg["frame"][s]), int(seg["label"][s])
+        a, b = fstart[f], fstart[f + 1]
+        sel = lab[a:b] == lb
+        cxy = np.mean(xy[a:b][sel], axis=0)
+        assert (seg["cx"][s], seg["cy"][s]) == (cxy[0], cxy[1]), (f, lb)
+        assert seg["mi"][s] == np.float32(np.mean(v[a:b][sel])), (f, lb)

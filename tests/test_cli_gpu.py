@@ -47,6 +47,40 @@ def test_tracker_cli_matches_reference_run_pipeline(tmp_path, golden):
         assert (out / f"{name}.csv").read_text() == str(g[name]), name
 
 
+def _ref_root(text: str, marker: str) -> str:
+    """The reference's temp data root, from its first line naming a file under it."""
+    for l in text.splitlines():
+        if marker in l and "/gain_" in l:
+            return l[l.index("/"):l.index("/gain_")]
+    return "\0"
+
+
+def test_tracker_cli_malformed_files_match_reference(tmp_path, golden):
+    """g11: a file with a too-long row (read_csv's tokenizing error: "Error loading {path}: {e}"
+    with pandas' text, printed while frames build, :193-194), a one-row file, a comment line and
+    empty echo fields (pandas reads the comment as a short row and NaN, fillna(0))."""
+    sys.path.insert(0, str(GOLDEN))
+    from make_golden import corrupt_csv_stack
+
+    from rpt.cli.tracker import run_pipeline
+
+    g = golden("g11_corrupt.npz")
+    data = corrupt_csv_stack(tmp_path / "stack")
+    out = tmp_path / "out"
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        run_pipeline(data, out, visualize=False)
+    ref_out = str(g["tracker_stdout"])
+    ref_dir = [l for l in ref_out.splitlines() if l.startswith("Results saved to: ")][0]
+    ref_dir = ref_dir[len("Results saved to: "):]
+    ref_out = ref_out.replace(_ref_root(ref_out, "Error loading"), "<DATA>")
+    got = buf.getvalue().replace(str(data), "<DATA>")
+    assert "Error loading <DATA>/gain_50/" in got
+    assert _norm(got, str(out)) == _norm(ref_out, ref_dir)
+    for name in ("tracked_objects", "trajectories", "clusters"):
+        assert (out / f"{name}.csv").read_text() == str(g["tracker_" + name]), name
+
+
 def test_tracker_cli_flags_and_max_frames(tmp_path):
     """argparse surface (:1057-1088): --max-frames truncates the grouped frames (:933-935),
     --no-land-filter skips the filter, --intensity-threshold is accepted and ignored."""

@@ -173,3 +173,155 @@ def test_discover_and_group_frames(tmp_path):
     assert parse_timestamp("20250813_142602_181.csv")[1] % 1000 == 181
     with pytest.raises(ValueError):
         parse_timestamp("x.csv")
+
+
+# ------------------------------------------------------------ exception texts (stdout parity)
+def _pandas_error_text(path, bins=B):
+    """str(e) of what the reference's read (:191-198, + to_numpy :203-207) raises, else None."""
+    cols = ["Status", "Scale", "Range", "Gain", "Angle"] + [f"Echo_{i}" for i in range(bins)]
+    try:
+        df = pd.read_csv(path, header=None, names=cols, skiprows=1, engine="c")
+    except Exception as e:  # the reference prints f"Error loading {path}: {e}"
+        return str(e)
+    try:
+        df.to_numpy(dtype=np.float32)
+    except ValueError as e:
+        return str(e)
+    return None
+
+
+ERROR_CASES = {
+    "later_row_too_many_fields": CASES["later_row_too_many_fields"],
+    "too_many_after_blank_lines": HDR + _row([1] * B) + "\n\n\n" + _row([2] * (B + 3)) + "\n",
+    "index_then_too_many": HDR + _row([1] * (B + 1)) + "\n" + _row([2] * (B + 2)) + "\n",
+    "crlf_too_many": CASES["later_row_too_many_fields"].replace("\n", "\r\n"),
+    "text_value": CASES["text_value"],
+    "text_in_two_columns": HDR + _row([1] * B) + "\n" + _row(["zz"] + [1] * (B - 1)) + "\n" +
+    _row([1, "yy"] + [1] * (B - 2)) + "\n" + _row(["xx"] * B) + "\n",
+    "text_with_space": HDR + _row([1, " ab c"] + [1] * (B - 2)) + "\n",
+}
+
+
+@pytest.mark.parametrize("name", sorted(ERROR_CASES))
+def test_error_text_matches_pandas(tmp_path, name):
+    """The "Error loading {path}: {e}" text (:194) and the non-numeric ValueError text: the
+    tokenizer's expected fields, physical line and fields seen; the leftmost bad column's first
+    bad value as numpy's column-block conversion names it."""
+    p = tmp_path / f"{name}.csv"
+    p.write_text(ERROR_CASES[name])
+    exp = _pandas_error_text(p)
+    assert exp is not None
+    b = read_sweeps([p], bins=B)
+    assert b.errors[0] == exp
+
+
+def test_missing_file_error_text(tmp_path):
+    p = tmp_path / "nope.csv"
+    with pytest.raises(FileNotFoundError) as ei:
+        pd.read_csv(p, header=None, names=COLS, skiprows=1, engine="c")
+    assert read_sweeps([p], bins=B).errors[0] == str(ei.value)
+
+
+def test_gain_first_row_and_unique(tmp_path):
+    """int(df["Gain"].iloc[0]) (:200) and radar_pipeline's unique() rule (loaders.py:88-92):
+    all-NaN raises like int(nan), rows that disagree give None, one value gives it."""
+    from rpt.core.ingest import GAIN_DISAGREE, GAIN_FIRST_NAN
+    from rpt.core.loaders import load_radar_csv
+
+    files = {"same": [40, 40, 40], "mixed": [40, 50, 40], "first_nan": ["", 40, 40],
+             "all_nan": ["", "nan", ""], "later_nan": [40, "", 40]}
+    for name, gains in files.items():
+        p = tmp_path / f"{name}.csv"
+        p.write_text(HDR + "".join(_row([20] * B, gain=g) + "\n" for g in gains))
+        b = read_sweeps([p], bins=B)
+        df = pd.read_csv(p, header=None, names=COLS, skiprows=1, engine="c")
+        u = df["Gain"].unique()
+        assert bool(b.gain_flags[0] & GAIN_FIRST_NAN) == bool(np.isnan(df["Gain"].iloc[0]))
+        assert bool(b.gain_flags[0] & GAIN_DISAGREE) == (len(u) > 1), name
+        if len(u) == 1 and np.isnan(u[0]):
+            with pytest.raises(ValueError):
+                load_radar_csv(p, _cfg16())
+        else:
+            assert load_radar_csv(p, _cfg16()).gain == (int(u[0]) if len(u) == 1 else None)
+
+
+def _cfg16():
+    from rpt.config import RadarConfig
+
+    return RadarConfig(num_echo_columns=B)
+
+
+# ----------------------------------------------------- the denoise loader (genfromtxt first)
+def _genfromtxt_ref(path, bins=B):
+    """PointCloudWorkF/stdbscan_denoising_pipeline.py:104-120: genfromtxt, pandas fallback,
+    the ndim/size check.  Returns ("raise", text) | ("empty", None) | ("ok", (echo, scale,
+    angle))."""
+    import warnings
+
+    cols = ["Status", "Scale", "Range", "Gain", "Angle"] + [f"Echo_{i}" for i in range(bins)]
+    try:
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            data = np.genfromtxt(path, delimiter=",", skip_header=1, dtype=np.float32,
+                                 filling_values=0.0)
+    except Exception:
+        try:
+            df = pd.read_csv(path, header=None, names=cols, skiprows=1, engine="c")
+            if df.empty:
+                return "empty", None
+            data = df.to_numpy(dtype=np.float32)
+        except Exception as e:
+            return "raise", str(e)
+    if data.size == 0 or data.ndim != 2:
+        return "empty", None
+    try:
+        return "ok", (data[:, 5:], data[:, 1], data[:, 4])
+    except IndexError as e:
+        return "raise", str(e)
+
+
+GF_CASES = {
+    "plain": CASES["plain"],
+    "single_row": HDR + _row(list(range(20, 20 + B))) + "\n",
+    "header_only": HDR,
+    "empty_file": "",
+    "hash_comment": HDR + _row([30] * B) + "\n" + _row([12, "13#"] + [99] * (B - 2)) + "\n" +
+    _row([31] * B) + "\n# a comment line\n",
+    "empty_fields_fill_zero": HDR + _row([""] * 3 + [44] * (B - 3), scale="", angle="") + "\n" +
+    _row([45] * B) + "\n",
+    "nan_inf_text": HDR + _row(["nan", "inf", "NA", "abc", "1_0", " 12 "] + [50] * (B - 6)) +
+    "\n" + _row([51] * B, scale="nan") + "\n",
+    "ragged_rows_pandas_fallback": HDR + _row([60] * B) + "\n" + _row([61] * (B - 4)) + "\n",
+    "ragged_one_row_fallback_keeps_it": HDR + _row([62] * B) + "\n" + "1,2\n",
+    "ragged_and_too_many": HDR + _row([1] * B) + "\n" + _row([2] * (B - 1)) + "\n" +
+    _row([3] * (B + 2)) + "\n",
+    "ragged_text": HDR + _row([1] * B) + "\n" + _row(["q"] * (B - 1)) + "\n",
+    "crlf": CASES["crlf"],
+    "four_columns": HDR + "1,2,3,4\n1,2,3,4\n",
+}
+
+
+@pytest.mark.parametrize("name", sorted(GF_CASES))
+def test_genfromtxt_mode_matches_denoise_loader(tmp_path, name):
+    from rpt.core.ingest import MODE_GENFROMTXT
+
+    p = tmp_path / f"{name}.csv"
+    p.write_text(GF_CASES[name])
+    kind, ref = _genfromtxt_ref(p)
+    b = read_sweeps([p], bins=B, mode=MODE_GENFROMTXT)
+    st = int(b.status[0])
+    if kind == "ok":
+        e, sc, an = ref
+        R = e.shape[0]
+        assert st == STATUS_OK
+        got = b.echo[0, :R].astype(np.float32)
+        # the echo only matters through `> 10` and its value where kept; NaN (pandas fallback
+        # without fillna) and 0 keep nothing alike
+        np.testing.assert_array_equal(np.nan_to_num(got, nan=0.0), np.nan_to_num(e, nan=0.0))
+        np.testing.assert_array_equal(b.scale[0, :R], sc)
+        np.testing.assert_array_equal(b.angle[0, :R], an)
+        assert not b.echo[0, R:].any()
+    elif kind == "empty":
+        assert st == STATUS_EMPTY
+    else:
+        assert b.errors[0] == ref

@@ -118,3 +118,32 @@ def test_denoise_pipeline_matches_reference_outputs(tmp_path, golden):
         assert (out / name).read_bytes() == bytes(g[name.replace(".", "_")]), name
     for name in ("denoising_stats.csv", "clusters.csv"):
         assert (out / name).read_text() == str(g[name.replace(".", "_")]), name
+
+
+def test_denoise_pipeline_malformed_files_parallel(tmp_path, golden):
+    """g11 through the denoise drop-in with parallel loading (> 4 frames, :905-907): the
+    genfromtxt-first loader (:104-119) -- a comment line skipped, empty fields and an empty
+    Scale read as 0.0, a one-row file an empty sweep -- and a file whose load raises (a
+    too-long row: genfromtxt raises, then read_csv's tokenizing error) failing its whole frame
+    with load_frames_parallel's warning (:248-251); stdout, PLYs and CSVs byte-identical."""
+    sys.path.insert(0, str(GOLDEN))
+    from make_golden import corrupt_csv_stack
+
+    from rpt.denoise import run_pipeline
+
+    g = golden("g11_corrupt.npz")
+    data = corrupt_csv_stack(tmp_path / "dstack", denoise=True)
+    out = tmp_path / "dout"
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        run_pipeline(data, out, eps_space=8.0, eps_time=2.0, min_samples=15, min_frames=2,
+                     max_frames=0, no_viz=True, parallel=True)
+    ref_out = str(g["denoise_stdout"])
+    ref_dir = [l for l in ref_out.splitlines() if l.startswith("Results saved to: ")][0]
+    ref_dir = ref_dir[len("Results saved to: "):]
+    assert "Warning: Failed to load frame 3" in buf.getvalue()
+    assert buf.getvalue().replace(str(out), "<OUT>") == ref_out.replace(ref_dir, "<OUT>")
+    for name in ("denoised_point_cloud.ply", "raw_point_cloud.ply"):
+        assert (out / name).read_bytes() == bytes(g["denoise_" + name.replace(".", "_")]), name
+    for name in ("denoising_stats.csv", "clusters.csv"):
+        assert (out / name).read_text() == str(g["denoise_" + name.replace(".", "_")]), name

@@ -222,3 +222,19 @@ def test_everything_on_land_raises_like_sklearn(gpu):
     else:  # some land-sector cells fell short of the persistence rule: compare as usual
         res = _pipe(cfg, ds, gpu).run(echo, keep_points=True)
         check_stack_vs_oracle(res, cfg.n_frames, frames, *expect)
+
+
+@pytest.mark.timeout(900)
+def test_dense_stack_12_frames_land(gpu):
+    """configs[4]'s density over 12 frames, so the land filter runs (> 10 frames, :954) with
+    ~490k points per frame; the union-find oracle.  At this density every 5 m cell is persistent
+    but dominated by clutter echoes (11-39), so no cell reaches LAND_MIN_INTENSITY (:405-408):
+    the grid is built over all 5.9 M points and nothing is removed -- as in the oracle."""
+    from rpt.synth import DeviceSynth, dense_config
+
+    cfg = dense_config(n_frames=12)
+    ds = DeviceSynth(cfg, gpu)
+    res, frames = _run_and_check(gpu, cfg, ds.echo(), ds, dbscan=oracle.stdbscan_uf,
+                                 expect_land=False)
+    assert op.land_filter(frames)[3].sum() == res.n_land_cells == 0
+    assert res.n_points > 12 * 350_000

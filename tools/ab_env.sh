@@ -3,6 +3,9 @@
 VAR=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
+# RPT_* switches are read only by the A/B build (python -m rpt._build --ab, built on the CPU host)
+export RPT_LIB="$PWD/radar-point-cloud-tracking_amd/rpt/librpt_ab.so"
+[ -f "$RPT_LIB" ] || { echo "build librpt_ab.so first: (cd radar-point-cloud-tracking_amd && python -m rpt._build --ab)"; exit 1; }
 mkdir -p gpurun_out
 for v in "$@"; do
   env "$VAR=$v" timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 --warmup 3 \

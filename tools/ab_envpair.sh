@@ -4,6 +4,9 @@
 # Optional TESTS=... runs first (stop on failure).
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
+# RPT_* switches are read only by the A/B build (python -m rpt._build --ab, built on the CPU host)
+export RPT_LIB="$PWD/radar-point-cloud-tracking_amd/rpt/librpt_ab.so"
+[ -f "$RPT_LIB" ] || { echo "build librpt_ab.so first: (cd radar-point-cloud-tracking_amd && python -m rpt._build --ab)"; exit 1; }
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 if [ -n "$TESTS" ]; then

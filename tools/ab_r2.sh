@@ -4,6 +4,9 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
+# RPT_* switches are read only by the A/B build (python -m rpt._build --ab, built on the CPU host)
+export RPT_LIB="$PWD/radar-point-cloud-tracking_amd/rpt/librpt_ab.so"
+[ -f "$RPT_LIB" ] || { echo "build librpt_ab.so first: (cd radar-point-cloud-tracking_amd && python -m rpt._build --ab)"; exit 1; }
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_stdbscan_gpu.py tests/test_fullsize_gpu.py \
   tests/test_path_gpu.py -x -q --timeout 600 --timeout-method thread > gpurun_out/t_ab.log 2>&1

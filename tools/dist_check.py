@@ -6,6 +6,10 @@ the whole stack and asserts identical labels, per-frame cluster rows and tracked
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29511 tools/dist_check.py --backend gloo --frames 14
 (--backend gloo lets several ranks share one GPU; nccl = RCCL needs one GPU per rank.)
+
+--digest std0[,std1]: the ranks run shares of the committed 1000-frame oracle workloads
+(tests/golden/bigstack_<name>.json, tests/golden/make_bigstack.py) instead, alternating the named
+workloads over the runs, and rank 0 compares every run's gathered result with the oracle digest.
 """
 from __future__ import annotations
 
@@ -35,6 +39,9 @@ def main():
     ap.add_argument("--impl", default="native", choices=("native", "python"),
                     help="native: NativeShardPipeline (librpt shard driver); python: "
                          "ShardedStackPipeline over HipOps")
+    ap.add_argument("--digest", default=None,
+                    help="comma-separated bigstack workloads (tests/golden/bigstack_<name>.json): "
+                         "compare with the oracle digests instead of the single-GPU pipeline")
     ap.add_argument("--tiny-caps", action="store_true",
                     help="native: one-element capacities for the one-collective gathers (every "
                          "gather takes its two-round fallback)")
@@ -57,6 +64,8 @@ def main():
     from rpt.synth import DeviceSynth, SynthConfig
 
     F = args.frames
+    if args.digest:
+        sys.exit(run_digest(args, rank, world, dev))
     cfg = SynthConfig(n_frames=F, rows=args.rows, frame0=rank * F)
     ds = DeviceSynth(cfg, dev)
     echo = ds.echo()
@@ -96,6 +105,69 @@ def main():
     flag = Comm(dev).all_reduce(flag, dist.ReduceOp.MIN)
     dist.destroy_process_group()
     sys.exit(0 if int(flag.item()) == 1 else 1)
+
+
+def run_digest(args, rank, world, dev):
+    """Shares of the committed oracle workloads; every run checked against its digest."""
+    import json
+
+    sys.path.insert(0, str(ROOT / "tests"))
+    from _digest import compare, shard_digest
+    from rpt.dist import Comm, ShardLanes
+    from rpt.pipeline import PathParams
+    from rpt.synth import DeviceSynth, SynthConfig
+
+    F = args.frames
+    names = args.digest.split(",")
+    gold = {n: json.loads((ROOT / "tests" / "golden" / f"bigstack_{n}.json").read_text())
+            for n in names}
+    dss = {n: DeviceSynth(SynthConfig(**{**gold[n]["synth"], "n_frames": F, "frame0": rank * F}),
+                          dev) for n in names}
+    echoes = {n: dss[n].echo() for n in names}
+    torch.cuda.synchronize(dev)
+    c0 = dss[names[0]].cfg
+    lanes = ShardLanes(dev, args.lanes, c0.gains, c0.rows, c0.bins, PathParams(),
+                       async_host=True)
+    lanes.set_geometry(np.full(c0.rows, c0.scale, np.float32), dss[names[0]].geo.cos_t,
+                       dss[names[0]].geo.sin_t, F * len(c0.gains))
+    # run k goes to lane k % lanes; each lane alternates the workloads over its runs, so every
+    # lane's last (checked) run differs from its previous one
+    L = args.lanes
+    seq = [names[(k % L + k // L) % len(names)] for k in range(2 * L)]
+    futs = [lanes.submit(echoes[n], rank * F) for n in seq]
+    outs = [f.result().finish() for f in futs]   # every lane idle before the checks' gathers
+    torch.cuda.synchronize(dev)
+    comm = Comm(dev)
+    ok = True
+    for i in range(L):
+        k = len(seq) - L + i
+        n, res, pipe = seq[k], outs[k], lanes.pipes[i]
+        mine = pipe.labels_local().cpu().to(torch.int64)
+        fo = np.empty(F + 1, np.int64)
+        pipe._abi.check(pipe.lib.rpt_shard_frame_offsets(
+            pipe.h, 1, fo.ctypes.data_as(pipe._abi.c_i64p)), "rpt_shard_frame_offsets")
+        labels = comm.all_gather_var(mine)
+        counts = comm.all_gather_fixed(torch.from_numpy(np.diff(fo)))
+        if rank == 0:
+            lab = torch.cat([l.cpu() for l in labels]).numpy().astype(np.int32)
+            got = shard_digest(res, lab, counts.reshape(-1).numpy())
+            try:
+                compare(got, gold[n], f"run {k} ({n}, lane {i})")
+                good = True
+            except AssertionError as e:
+                print(f"[dist_check] MISMATCH {e}", flush=True)
+                good = False
+            ok &= good
+            print(f"[dist_check] digest run {k} {n} (lane {i}, after {seq[k - L] if k >= L else '-'}):"
+                  f" world={world} frames/rank={F} points={res.n_points_global} "
+                  f"clusters={res.n_clusters} objects={len(res.tracker.objects())} match={good}",
+                  flush=True)
+    lanes.close()
+    flag = comm.all_reduce(torch.tensor([1 if ok else 0], dtype=torch.int32), dist.ReduceOp.MIN)
+    if rank == 0:
+        print(f"[dist_check] digest ok={bool(int(flag.item()) == 1)}", flush=True)
+    dist.destroy_process_group()
+    return 0 if int(flag.item()) == 1 else 1
 
 
 def check(res, labels, rank, world, args, dev):
