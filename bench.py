@@ -12,6 +12,10 @@ fused stack (12.6 GB of u8 echo, ~50 M points), land filter + ST-DBSCAN + tracki
 scaling: at N GPUs every rank owns 1000/N contiguous frames of that same stack (rpt/dist.py), so
 the driver's N=1,2,4,8 values measure the "6x at 8 GPUs on a 1000-frame stack" target directly.
 At N=1 the whole stack runs on one MI355X (it fits: 288 GB HBM).
+Two differently seeded stacks of that shape (seed 0 / targets 123 and seed 1 / targets 124 --
+tests/golden/bigstack_std{0,1}.json hold the oracle's digests of both) alternate over the steps,
+so no step replays the previous step's input on its lane (the K1 capacity and K9 label-bit /
+segment-count guesses from the previous run are exercised inside the timed region).
   --frames F     weak scaling instead: F frames per GPU (F=100 is configs[2], round 1's line)
   --dense        configs[4]'s density (~500k points per frame, rpt.synth.dense_config)
   --h2d-steps K  also time K steps that first copy the echo from pinned host memory (reported
@@ -21,9 +25,14 @@ step k+1's device work runs while step k's host stage and readbacks finish, and 
 latency-bound kernels share the CUs; 3 measured +4-5 % over 2 in interleaved same-box runs, 4
 no better); `one_stack_in_flight` repeats the steps strictly one after
 another, and K5's roofline is taken from that leg (K5 alone on the GPU).
-After the timed region (N=1, timing on), K5 is also timed on the configs[4] per-GPU share (125
-dense frames), where SURVEY.md §8(d) sets the 0.40 roofline target: `roofline_configs4_share`
-(`--no-dense-k5` skips it).
+After the timed region (N=1, timing on), K5 is also timed on the per-GPU shares at 8 GPUs, where
+SURVEY.md §8(d) sets the 0.40 roofline target: `roofline_c4_share` (125 standard frames, the
+configs[3] stack's share) and `roofline_configs4_share` (125 dense frames, configs[4]'s), one
+stack in flight (`--no-dense-k5` skips both).
+`cpu_baseline`: oracle/refpath.py -- the reference's own algorithmic structure (whole-stack
+sklearn BallTree, per-neighbour time filter, seed-set expansion; calibrated against the
+reference in the build container, profiles/r3/refpath_calibration.json) -- on the first frame
+of the same stack, one thread, on this node's host.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--total-frames T | --frames F] [--dense]
 """
@@ -52,26 +61,39 @@ def _log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(echo_host: np.ndarray, cfg, geo, max_seconds: float = 30.0):
-    """Oracle (the pinned CPU restatement, 1 thread) on the first frames of the same workload."""
+def cpu_baseline(echo_host: np.ndarray, cfg, geo, structure: bool = True):
+    """The per-frame path on the host, 1 thread, on the first frames of the same workload:
+    polar scatter + fusion (numpy), st_dbscan and the tracker.  structure=True: st_dbscan with
+    the reference's algorithmic structure (oracle/refpath.py); False: the oracle's grid-indexed C
+    BFS.  Returns (points, frames, seconds, labels-equal-to-the-oracle, index name)."""
     import oracle
     from oracle import path as op
+    from oracle.refpath import stdbscan_structure
+    from oracle.tracker import Tracker
 
     F, G, R, B = echo_host.shape
     t0 = time.perf_counter()
-    per_frame = []
-    for f in range(F):
-        per_frame.append({gain: op.polar_scatter(echo_host[f, k], np.full(R, cfg.scale, np.float32),
-                                                 geo.cos_t, geo.sin_t)
-                          for k, gain in enumerate(cfg.gains)})
-        if time.perf_counter() - t0 > max_seconds:
-            break
+    per_frame = [{gain: op.polar_scatter(echo_host[f, k], np.full(R, cfg.scale, np.float32),
+                                         geo.cos_t, geo.sin_t)
+                  for k, gain in enumerate(cfg.gains)} for f in range(F)]
     frames = op.build_frames(per_frame)
     npts = sum(len(p) for _, p, _ in frames)
-    op.run_path(frames)
+    if len(frames) > 10:
+        frames = op.land_filter(frames)[0]
+    xy, t = op.stack_coords(frames)
+    index = "oracle grid BFS (C)"
+    if structure:
+        labels, index = stdbscan_structure(xy, t, 8.0, 2.0, 15)
+    else:
+        labels = oracle.stdbscan(xy, t, 8.0, 2.0, 15)
+    clusters = op.frame_clusters(frames, labels)
+    trk = Tracker()
+    for fid, _, _ in frames:
+        trk.update([(c[2], fid) for c in clusters.get(fid, [])], fid)
     dt = time.perf_counter() - t0
-    del oracle
-    return npts, len(frames), dt
+    same = bool(np.array_equal(labels, oracle.stdbscan(xy, t, 8.0, 2.0, 15))) if structure \
+        else True
+    return npts, len(frames), dt, same, index
 
 
 def _cpu_model() -> str:
@@ -99,6 +121,43 @@ def _reference_measured():
                     "frames and do not extrapolate to 100-1000 frames"}
 
 
+def _traffic(name):
+    """PMC-measured HBM bytes per launch committed for a workload (tools/pmc.sh: separate
+    FETCH_SIZE / WRITE_SIZE passes, gfx950 read correction), newest round first."""
+    for rd in ("r3", "r2"):
+        f = ROOT / "profiles" / rd / name
+        if f.exists():
+            d = json.loads(f.read_text())
+            return int(d["bytes_per_launch"]), str(f.relative_to(ROOT))
+    return None, None
+
+
+def _k5_share(dev, cfg, label, wkey):
+    """K5 (hipEvents around the core-flag pass) on one per-GPU share, one stack in flight: one
+    warm-up run, then three timed runs."""
+    from rpt.pipeline import FrameStackPipeline, PathParams
+    from rpt.synth import DeviceSynth
+
+    ds = DeviceSynth(cfg, dev)
+    echo = ds.echo()
+    pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), dev, timing=True)
+    pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
+                      cfg.n_frames * len(cfg.gains))
+    res = [pipe.run(echo).finish() for _ in range(4)][1:]
+    k5 = float(np.mean([r.stage_ms["dbscan_core"] for r in res]))
+    n = res[-1].n_clustered_input
+    ach = K5_BYTES_PER_POINT * n / (k5 * 1e-3) / 1e9
+    tr, src = _traffic(f"k5_traffic_{wkey}.json")
+    out = {"workload": label, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(ach / HBM_PEAK_GBS, 4), "avg_ms": round(k5, 4), "points": n,
+           "runs": len(res), "traffic": tr,
+           "traffic_unit": f"bytes per launch (PMC, {src})" if src else None,
+           "stage_ms": {k: round(float(np.mean([r.stage_ms[k] for r in res])), 3)
+                        for k in res[0].stage_ms}}
+    del pipe, echo, ds
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -109,14 +168,18 @@ def main():
     ap.add_argument("--frames", type=int, default=None,
                     help="frames per GPU instead (weak scaling)")
     ap.add_argument("--dense", action="store_true", help="configs[4] density (~500k pts/frame)")
+    ap.add_argument("--single-seed", action="store_true",
+                    help="replay ONE stack every step (round-2 behaviour) instead of alternating "
+                         "two differently seeded stacks")
     ap.add_argument("--h2d-steps", type=int, default=2,
                     help="extra steps timed with the echo's H2D copy from pinned host memory "
                          "(0 = skip)")
-    ap.add_argument("--cpu-frames", type=int, default=8)
+    ap.add_argument("--cpu-frames", type=int, default=1,
+                    help="frames of the stack the CPU baseline runs (reference structure)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-stage hipEvent timing")
     ap.add_argument("--no-dense-k5", action="store_true",
-                    help="skip the K5 roofline leg at the configs[4] per-GPU share")
+                    help="skip the K5 roofline legs at the 8-GPU per-GPU shares")
     ap.add_argument("--sharded", action="store_true",
                     help="run the frame-sharded (multi-GPU) pipeline even with one rank")
     ap.add_argument("--python-shard", action="store_true",
@@ -125,9 +188,7 @@ def main():
     ap.add_argument("--lanes", type=int, default=None,
                     help="stacks in flight at once (default 3 on one GPU: native handles on "
                          "separate streams; 1 with N>1 ranks, where a lane is also a process "
-                         "group -- rpt.dist.ShardLanes -- and several RCCL communicators "
-                         "sharing a rank's hardware queues can order their kernels differently "
-                         "on different GPUs); 1 = strictly one after another")
+                         "group -- rpt.dist.ShardLanes); 1 = strictly one after another")
     ap.add_argument("--no-one-stack", action="store_true",
                     help="skip the one-stack-in-flight leg (and so K5's roofline)")
     ap.add_argument("--sync-host", action="store_true",
@@ -152,6 +213,8 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
+    from dataclasses import replace as dc_replace
+
     from rpt import _abi
     from rpt.pipeline import FrameStackPipeline, PathParams
     from rpt.synth import DeviceSynth, SynthConfig
@@ -168,8 +231,11 @@ def main():
         cfg = dense_config(n_frames=F, frame0=rank * F)
     else:
         cfg = SynthConfig(n_frames=F, frame0=rank * F)
-    ds = DeviceSynth(cfg, dev)
-    echo = ds.echo()
+    # the stacks the steps alternate over (same geometry, other data and target seeds)
+    cfgs = [cfg] if args.single_seed else [cfg, dc_replace(cfg, seed=1, target_seed=124)]
+    dss = [DeviceSynth(c, dev) for c in cfgs]
+    echoes = [d.echo() for d in dss]
+    ds, E = dss[0], len(echoes)
     torch.cuda.synchronize(dev)
     timing = not args.no_timing
     if dist:
@@ -191,7 +257,7 @@ def main():
                 tuple(torch.from_numpy(np.tile(a, F * G)).to(dev) for a in
                       (np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t)),
                 torch.tensor(list(cfg.gains) * F, dtype=torch.int32, device=dev))
-            run = lambda: pipe.run(echo, _abi.ECHO_U8, rank * F)  # noqa: E731
+            run = lambda e: pipe.run(e, _abi.ECHO_U8, rank * F)  # noqa: E731
         elif args.lanes > 1:
             # several stacks in flight (rpt.dist.ShardLanes: per lane a process group, stream and
             # thread); K5 and the stage times come from the one-stack-in-flight leg below
@@ -202,45 +268,45 @@ def main():
             lanes_.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t,
                                 ds.geo.sin_t, cfg.n_frames * len(cfg.gains))
             ops = lanes_.pipes[0]
-            run = lambda: lanes_.submit(echo, rank * F)  # noqa: E731
+            run = lambda e: lanes_.submit(e, rank * F)  # noqa: E731
         else:
             ops = pipe = NativeShardPipeline(Comm(dev), cfg.gains, cfg.rows, cfg.bins,
                                              PathParams(), timing=timing,
                                              async_host=not args.sync_host, host_workers=4)
             pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t,
                               ds.geo.sin_t, cfg.n_frames * len(cfg.gains))
-            run = lambda: pipe.run(echo, rank * F)  # noqa: E731
+            run = lambda e: pipe.run(e, rank * F)  # noqa: E731
     else:
         pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), dev, timing=timing,
                                   async_host=not args.sync_host, lanes=args.lanes)
         pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
                           cfg.n_frames * len(cfg.gains))
-        run = lambda: pipe.submit(echo)  # noqa: E731
+        run = lambda e: pipe.submit(e)  # noqa: E731
 
     def resolve(r):
         return r.result() if hasattr(r, "result") else r
 
-    for _ in range(args.warmup):
-        resolve(run()).finish()
+    def points_of(r):  # K1 points of the whole (global) stack of a run
+        return float(r.n_points_global if dist else r.n_points)
+
+    for k in range(args.warmup):
+        resolve(run(echoes[k % E])).finish()
     torch.cuda.synchronize(dev)
     if dist:
         tdist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     stage_acc = {}
-    k5_ms = []
-    res = None
+    k5 = []      # (K5 ms, points entering ST-DBSCAN) per timed run
     results = []
     sharded_lanes = dist and not args.python_shard and args.lanes > 1
-    for _ in range(args.steps):
-        res = run()
-        results.append(res)
+    for k in range(args.steps):
+        results.append(run(echoes[k % E]))
         if timing and dist and not sharded_lanes:
-            k5_ms.append(ops.last_core_ms())
+            k5.append((ops.last_core_ms(), ops.core_points))
     results = [resolve(r) for r in results]
     if timing and not dist:
-        k5_ms = [r.stage_ms["dbscan_core"] for r in results]
-    res = results[-1]
+        k5 = [(r.stage_ms["dbscan_core"], r.n_clustered_input) for r in results]
     for r in results:  # host stages (order + tracker) of the last runs, in order
         r.finish()
     torch.cuda.synchronize(dev)
@@ -249,41 +315,40 @@ def main():
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     for r in results:
-        for k, v in r.stage_ms.items():
-            stage_acc[k] = stage_acc.get(k, 0.0) + v
+        for key, v in r.stage_ms.items():
+            stage_acc[key] = stage_acc.get(key, 0.0) + v
+    pts_total = sum(points_of(r) for r in results)
+    res = results[-1]
     if dist:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         dt = float(t[0])
-        pts = float(res.n_points_global)        # K1 points of the whole global stack
-        n_core_in = ops.core_points             # [halo | own | halo] points of this rank
         summary = {"points_clustered_rank0": res.n_clustered_local, "clusters": res.n_clusters,
                    "segments": res.n_segments, "objects": len(res.tracker)
                    if res.tracker is not None else None}
     else:
-        pts = float(res.n_points)
-        n_core_in = res.n_clustered_input
         summary = {"points_clustered_rank0": res.n_clustered_input, "clusters": res.n_clusters,
                    "segments": res.n_segments, "objects": len(res.tracker)}
-    value = pts * args.steps / dt / 1e6
+    summary["points_per_stack"] = sorted({int(points_of(r)) for r in results})
+    value = pts_total / dt / 1e6
     ms_step = dt / args.steps * 1e3
 
     # one stack in flight (lanes = 1): the same steps strictly one after another.  K5's roofline
-    # is taken here, where its kernels have the GPU to themselves (with two stacks in flight the
-    # other stack's kernels share the CUs and stretch every event-timed stage)
+    # is taken here, where its kernels have the GPU to themselves (with several stacks in flight
+    # the other stacks' kernels share the CUs and stretch every event-timed stage)
     seq = None
     if sharded_lanes:  # every rank: lane 0's pipeline, one stack at a time
-        for _ in range(max(args.warmup, 1)):
-            ops.run(echo, rank * F).finish()
+        for k in range(max(args.warmup, 1)):
+            ops.run(echoes[k % E], rank * F).finish()
         torch.cuda.synchronize(dev)
         tdist.barrier()
         ts0 = time.perf_counter()
         sres = []
-        k5_ms = []
-        for _ in range(args.steps):
-            sres.append(ops.run(echo, rank * F))
+        k5 = []
+        for k in range(args.steps):
+            sres.append(ops.run(echoes[k % E], rank * F))
             if timing:
-                k5_ms.append(ops.last_core_ms())
+                k5.append((ops.last_core_ms(), ops.core_points))
         for r in sres:
             r.finish()
         torch.cuda.synchronize(dev)
@@ -291,44 +356,45 @@ def main():
         t = torch.tensor([time.perf_counter() - ts0], dtype=torch.float64, device=dev)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         dts = float(t[0])
-        seq = {"value": round(pts * args.steps / dts / 1e6, 3), "unit": "Mpoints/s",
-               "ms_per_step": round(dts / args.steps * 1e3, 3), "steps": args.steps,
-               "note": "same workload, one stack in flight per rank"}
+        seq = {"value": round(sum(points_of(r) for r in sres) / dts / 1e6, 3),
+               "unit": "Mpoints/s", "ms_per_step": round(dts / args.steps * 1e3, 3),
+               "steps": args.steps, "note": "same workload, one stack in flight per rank"}
         if timing:
             stage_acc = {}
             for r in sres:
-                for k, v in r.stage_ms.items():
-                    stage_acc[k] = stage_acc.get(k, 0.0) + v
+                for key, v in r.stage_ms.items():
+                    stage_acc[key] = stage_acc.get(key, 0.0) + v
     if not dist and args.lanes > 1 and not args.no_one_stack:
         spipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), dev, timing=timing,
                                    async_host=not args.sync_host, lanes=1)
         spipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t,
                            ds.geo.sin_t, cfg.n_frames * len(cfg.gains))
-        for _ in range(max(args.warmup, 1)):
-            resolve(spipe.submit(echo)).finish()
+        for k in range(max(args.warmup, 1)):
+            resolve(spipe.submit(echoes[k % E])).finish()
         torch.cuda.synchronize(dev)
         ts0 = time.perf_counter()
-        sres = [resolve(spipe.submit(echo)) for _ in range(args.steps)]
+        sres = [resolve(spipe.submit(echoes[k % E])) for k in range(args.steps)]
         for r in sres:
             r.finish()
         torch.cuda.synchronize(dev)
         dts = time.perf_counter() - ts0
-        seq = {"value": round(pts * args.steps / dts / 1e6, 3), "unit": "Mpoints/s",
-               "ms_per_step": round(dts / args.steps * 1e3, 3), "steps": args.steps,
-               "note": "same workload, one stack in flight (lanes=1)"}
+        seq = {"value": round(sum(points_of(r) for r in sres) / dts / 1e6, 3),
+               "unit": "Mpoints/s", "ms_per_step": round(dts / args.steps * 1e3, 3),
+               "steps": args.steps, "note": "same workload, one stack in flight (lanes=1)"}
         if timing:
-            k5_ms = [r.stage_ms["dbscan_core"] for r in sres]
-            # per-stage times from this leg too: with two stacks in flight every event-timed
-            # stage also contains the other stack's interleaved kernels
+            k5 = [(r.stage_ms["dbscan_core"], r.n_clustered_input) for r in sres]
+            # per-stage times from this leg too: with several stacks in flight every event-timed
+            # stage also contains the other stacks' interleaved kernels
             stage_acc = {}
             for r in sres:
-                for k, v in r.stage_ms.items():
-                    stage_acc[k] = stage_acc.get(k, 0.0) + v
+                for key, v in r.stage_ms.items():
+                    stage_acc[key] = stage_acc.get(key, 0.0) + v
         del spipe
 
-    # optional leg: the same steps with the echo's H2D copy from pinned host memory inside
+    # optional leg: steps with the echo's H2D copy from pinned host memory inside (stack 0)
     h2d = None
     if args.h2d_steps > 0:
+        echo = echoes[0]
         host = torch.empty(echo.shape, dtype=echo.dtype, pin_memory=True)
         host.copy_(echo)
         torch.cuda.synchronize(dev)
@@ -338,9 +404,10 @@ def main():
         hres = []
         for _ in range(args.h2d_steps):
             echo.copy_(host, non_blocking=True)
-            hres.append(run())
+            hres.append(run(echo))
+        hres = [resolve(r) for r in hres]
         for r in hres:
-            resolve(r).finish()
+            r.finish()
         torch.cuda.synchronize(dev)
         if dist:
             tdist.barrier()
@@ -349,46 +416,40 @@ def main():
             t = torch.tensor([dth], dtype=torch.float64, device=dev)
             tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
             dth = float(t[0])
-        h2d = {"value": round(pts * args.h2d_steps / dth / 1e6, 3), "unit": "Mpoints/s",
-               "ms_per_step": round(dth / args.h2d_steps * 1e3, 3), "steps": args.h2d_steps,
+        h2d = {"value": round(sum(points_of(r) for r in hres) / dth / 1e6, 3),
+               "unit": "Mpoints/s", "ms_per_step": round(dth / args.h2d_steps * 1e3, 3),
+               "steps": args.h2d_steps,
                "echo_bytes_per_rank": int(echo.numel() * echo.element_size()),
-               "note": "each step first copies the u8 echo from pinned host memory (PCIe), "
-                       "then runs the same path; not the headline value"}
+               "note": "each step first copies the u8 echo of stack 0 from pinned host memory "
+                       "(PCIe), then runs the same path; not the headline value"}
         del host
 
     wkey = f"{'dense' if args.dense else 'std'}_{F}f"
-    traffic, tsrc = None, None
-    for tfile in (ROOT / "profiles" / "r2" / f"k5_traffic_{wkey}.json",
-                  ROOT / "profiles" / "r1" / "k5_traffic.json"):
-        if tfile.exists() and not dist and (tfile.parent.name == "r2" or wkey == "std_100f"):
-            # PMC-measured HBM bytes per K5 launch of this same workload (tools/pmc.sh: separate
-            # FETCH_SIZE / WRITE_SIZE passes, gfx950 read correction); committed under profiles/
-            traffic = json.loads(tfile.read_text()).get("bytes_per_launch")
-            tsrc = str(tfile.relative_to(ROOT))
-            break
+    traffic, tsrc = (None, None) if dist else _traffic(f"k5_traffic_{wkey}.json")
     roof = None
-    k5_ms = [v for v in k5_ms if v is not None]
-    if k5_ms:
-        k5 = float(np.mean(k5_ms))
-        n_in = n_core_in
-        achieved = K5_BYTES_PER_POINT * n_in / (k5 * 1e-3) / 1e9
+    k5 = [(a, b) for a, b in k5 if a is not None]
+    if k5:
+        k5_ms = float(np.mean([a for a, _ in k5]))
+        n_in = float(np.mean([b for _, b in k5]))
+        achieved = K5_BYTES_PER_POINT * n_in / (k5_ms * 1e-3) / 1e9
         roof = {"kernel": "K5 = k_core_cells_oct + k_core_fill + k_core_slow (core flags)",
                 "measured_in": "one-stack-in-flight leg" if seq is not None else "timed steps",
                 "bound": "hbm",
                 "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None if traffic is None else int(traffic),
+                "traffic": traffic,
                 "traffic_unit": f"bytes per launch (PMC, {tsrc})" if tsrc else None,
                 "bytes_model": "17 B/point x points entering ST-DBSCAN (SURVEY.md 8d)",
-                "avg_ms": round(k5, 4), "points": n_in}
+                "avg_ms": round(k5_ms, 4), "points": int(n_in), "runs": len(k5)}
     stage = {k: round(v / args.steps, 3) for k, v in stage_acc.items()}
     # the largest stage, K1 (count + scan + write): echo read once + 16 B per emitted point
     # (x, y, intensity, frame slot; no per-point gain without keep_points) + 12 B of row geometry
     # per row, over its event time
     roof_k1 = None
     if stage.get("polar") and not dist:
-        k1_bytes = int(echo.numel() * echo.element_size()) + 16 * int(pts) + \
-            12 * int(echo.shape[0]) * int(echo.shape[1]) * int(echo.shape[2])
+        e0 = echoes[0]
+        k1_bytes = int(e0.numel() * e0.element_size()) + 16 * int(pts_total / args.steps) + \
+            12 * int(e0.shape[0]) * int(e0.shape[1]) * int(e0.shape[2])
         k1_ach = k1_bytes / (stage["polar"] * 1e-3) / 1e9
         roof_k1 = {"kernel": "K1 stage = k_group_count_u8 + scans + k_group_starts + "
                              "k_expand_write (+ unstaged groups)",
@@ -397,45 +458,47 @@ def main():
                    "avg_ms": stage["polar"], "bytes_model": "1 B per echo sample + 16 B per "
                    "point written + 12 B per row (SURVEY 8d's K1 terms for u8 echo)",
                    "bytes": k1_bytes, "traffic": None}
-        t1 = ROOT / "profiles" / "r2" / f"k1_traffic_{wkey}.json"
-        if t1.exists():  # PMC-measured HBM bytes of the K1 kernels, same workload (pmc_r2.sh)
-            roof_k1["traffic"] = int(json.loads(t1.read_text())["bytes_per_launch"])
-            roof_k1["traffic_unit"] = f"bytes per run (PMC, {t1.relative_to(ROOT)})"
+        t1, src1 = _traffic(f"k1_traffic_{wkey}.json")
+        if t1 is not None:  # PMC-measured HBM bytes of the K1 kernels, same workload
+            roof_k1["traffic"] = t1
+            roof_k1["traffic_unit"] = f"bytes per run (PMC, {src1})"
 
-    # K5 again at the size SURVEY 8(d) sets its 0.40 target for: the configs[4] per-GPU share
-    # (125 dense frames, ~61 M points), after the timed region; hipEvents as above
-    roof_c4 = None
+    # K5 again at the per-GPU shares where SURVEY 8(d) sets its 0.40 target (8 GPUs): the
+    # configs[3] stack's 125 standard frames and configs[4]'s 125 dense frames
+    roof_c4 = roof_c4d = None
     if rank == 0 and not dist and not args.dense and timing and not args.no_dense_k5:
         from rpt.synth import dense_config
-        dcfg = dense_config(n_frames=125)
-        dds = DeviceSynth(dcfg, dev)
-        decho = dds.echo()
-        dpipe = FrameStackPipeline(dcfg.gains, dcfg.rows, dcfg.bins, PathParams(), dev,
-                                   timing=True)
-        dpipe.set_geometry(np.full(dcfg.rows, dcfg.scale, np.float32), dds.geo.cos_t,
-                           dds.geo.sin_t, dcfg.n_frames * len(dcfg.gains))
-        dres = [dpipe.run(decho).finish() for _ in range(4)][1:]  # one warm-up run
-        dk5 = float(np.mean([r.stage_ms["dbscan_core"] for r in dres]))
-        dn = dres[-1].n_clustered_input
-        dach = K5_BYTES_PER_POINT * dn / (dk5 * 1e-3) / 1e9
-        roof_c4 = {"workload": "configs[4] per-GPU share: 125 dense frames (~500k pts/frame)",
-                   "achieved": round(dach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                   "frac": round(dach / HBM_PEAK_GBS, 4), "avg_ms": round(dk5, 4),
-                   "points": dn, "runs": len(dres)}
-        del dpipe, decho, dds
+
+        roof_c4 = _k5_share(dev, SynthConfig(n_frames=125),
+                            "configs[3] per-GPU share at 8 GPUs: 125 standard frames",
+                            "std_125f")
+        roof_c4d = _k5_share(dev, dense_config(n_frames=125),
+                             "configs[4] per-GPU share at 8 GPUs: 125 dense frames "
+                             "(~490k pts/frame)", "dense_125f")
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and not dist:
         cf = min(args.cpu_frames, F)
-        eh = echo[:cf].cpu().numpy()
-        npts, nfr, cdt = cpu_baseline(eh, cfg, ds.geo)
-        cpu = {"value": round(npts / cdt / 1e6, 5), "unit": "Mpoints/s", "cores": 1,
+        eh = echoes[0][:cf].cpu().numpy()
+        npts, nfr, cdt, same, index = cpu_baseline(eh, cfg, ds.geo, structure=True)
+        gp, gf, gdt, _, _ = cpu_baseline(echoes[0][:8].cpu().numpy(), cfg, ds.geo,
+                                         structure=False)
+        cpu = {"value": round(npts / cdt / 1e6, 6), "unit": "Mpoints/s", "cores": 1,
                "kind": "port",
-               "what": "oracle grid-BFS port: oracle/ C grid-indexed BFS restatement of st_dbscan "
-                       "+ numpy polar/land + Python tracker, 1 thread -- NOT the reference's "
-                       "BallTree path (that one is reference_measured)",
-               "cpu_model": _cpu_model(),
-               "sample": f"first {nfr} frames of the same stack ({npts} points), {cdt:.1f} s",
+               "what": "the reference's algorithmic structure restated (oracle/refpath.py: "
+                       "whole-stack sklearn BallTree query, per-neighbour float32 time filter "
+                       "in Python, seed-set expansion; calibrated to 0.93-1.03x the reference's "
+                       "own time in the build container, profiles/r3/refpath_calibration.json) "
+                       "+ numpy polar scatter + oracle tracker, 1 thread on this node",
+               "index": index, "labels_equal_oracle": same,
+               "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
+               "sample": f"first {nfr} frame(s) of the same stack ({npts} points), {cdt:.1f} s; "
+                         f"the reference's cost per point grows with the frames in its one "
+                         f"BallTree, so the rate does not extrapolate to 1000 frames",
+               "grid_bfs_port": {"value": round(gp / gdt / 1e6, 5), "unit": "Mpoints/s",
+                                 "sample": f"first {gf} frames ({gp} points), {gdt:.1f} s",
+                                 "what": "oracle/ grid-indexed C BFS (not the reference's "
+                                         "structure), 1 thread"},
                "reference_measured": _reference_measured()}
     if rank == 0:
         what = "dense (configs[4] density, ~500k pts/frame)" if args.dense else \
@@ -455,9 +518,11 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
             "scaling": scaling, "vs_baseline": None,
             "dtype": "u8 echo / f32 geometry / f64 distance",
-            "data": "synthetic (device-generated, seeded)",
+            "data": "synthetic (device-generated, seeded): "
+                    + ("one stack replayed" if E == 1 else
+                       "two stacks (seed 0 / 1) alternating over the steps"),
             "config": {"workload": wl, "total_frames": total, "frames_per_gpu": F,
-                       "points_per_step": int(pts), **summary,
+                       "points_per_step": int(round(pts_total / args.steps)), **summary,
                        "parallelism": (f"frame-sharded x{world}"
                                        f"{' (python stages)' if args.python_shard else ''}")
                        if dist else "single GPU",
@@ -466,7 +531,8 @@ def main():
                        "overlapped: step k's order+tracker runs on a host thread during step "
                        "k+1's device work; the timed region ends after the last one"},
             "one_stack_in_flight": seq,
-            "roofline": roof, "roofline_configs4_share": roof_c4, "roofline_k1": roof_k1,
+            "roofline": roof, "roofline_c4_share": roof_c4, "roofline_configs4_share": roof_c4d,
+            "roofline_k1": roof_k1,
             "cpu_baseline": cpu,
             "h2d_inclusive": h2d, "stage_ms": stage,
             "stage_ms_from": "one_stack_in_flight" if seq is not None else "timed steps",

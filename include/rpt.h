@@ -178,7 +178,7 @@ int32_t rpt_stdbscan(const float* x, const float* y, const float* z, int64_t str
  * their minimum core index; a non-core point takes the smallest cluster m adjacent to it through a
  * core point with (its index > m, or it is a neighbour of core point m) -- the FIFO expansion's
  * result, :340-367.  n == 0 is not an error (no labels written).  RPT_ENOTSUP when
- * eps_time > 30 with min_frames >= 2.  Synchronises. */
+ * eps_time > 30 with min_frames > 256 (the distinct-frame list of a wave).  Synchronises. */
 /* pandas DataFrame.groupby(labels).mean() of float32 x / y / intensity columns (pandas 2.x
  * group_mean: float32 Kahan-compensated sum in row order, / (float)count), for labels in
  * [0, n_labels) (noise -1 and labels >= n_labels ignored): count (dev int64) and the three means

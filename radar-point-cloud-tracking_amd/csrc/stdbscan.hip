@@ -2527,6 +2527,102 @@ __global__ __launch_bounds__(kBlock) void k_frames_points(const float4* __restri
   }
 }
 
+// numpy float32 -> int32 astype on x86-64: truncation; NaN / out of range -> INT32_MIN
+__device__ __forceinline__ int32_t np_i32(float v) {
+  if (!(v == v) || v >= 2147483648.f || v < -2147483648.f) return INT32_MIN;
+  return (int32_t)v;
+}
+
+// The same frame count for any eps_t (k_frames_points' 64-bit offset set needs |dt| <= 30): the
+// distinct int32(t) frames seen so far are a list spread over the wave, kFramesPerLane per lane
+// (lane k holds entries k, k + 64, ...), appended one new frame at a time, so at most
+// min_frames <= 64 * kFramesPerLane entries ever exist (the host checks the bound).
+constexpr int kFramesPerLane = 4;
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_frames_points_list(
+    const float4* __restrict__ pts, const int32_t* __restrict__ skey, Geom g,
+    const CellRec<D>* __restrict__ crec, const uint32_t* __restrict__ occ_bits,
+    const float2* __restrict__ slab_t, int integral, int min_frames,
+    const int32_t* __restrict__ list, const int32_t* __restrict__ count,
+    uint8_t* __restrict__ core) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+  const int64_t nq = *count;
+  for (int64_t q = w0; q < nq; q += nw) {
+    const int s = list[q];
+    const float4 p = pts[s];
+    int cx, cy, cz;
+    decode_key<D>(skey[s], g, cx, cy, cz);
+    const Window w = make_window<D, false>(cx, cy, cz, p.w, p.w, g, slab_t);
+    int32_t fr[kFramesPerLane];
+#pragma unroll
+    for (int k = 0; k < kFramesPerLane; ++k) fr[k] = 0;
+    int nseen = 0;
+    // v (this lane's candidate frame, valid when has): add it unless already listed
+    auto add = [&](bool has, int32_t v) {
+      bool fresh = has;
+      // membership: compare against every listed entry (broadcast one register row at a time;
+      // nseen is wave-uniform, so every lane runs every shuffle)
+#pragma unroll
+      for (int r = 0; r < kFramesPerLane; ++r) {
+        if (r * 64 >= nseen) break;
+        const int lim = min(nseen - r * 64, 64);
+        for (int k = 0; k < lim; ++k) {
+          const int32_t e = __shfl(fr[r], k);
+          if (e == v) fresh = false;
+        }
+      }
+      // append the distinct fresh values, lowest lane first
+      uint64_t m = __ballot(fresh);
+      while (m && nseen < min_frames) {
+        const int l = __ffsll((unsigned long long)m) - 1;
+        const int32_t nv = __shfl(v, l);
+        const int r = nseen / 64, k = nseen % 64;
+#pragma unroll
+        for (int rr = 0; rr < kFramesPerLane; ++rr)
+          if (rr == r && lane == k) fr[rr] = nv;
+        ++nseen;
+        if (fresh && v == nv) fresh = false;
+        m = __ballot(fresh);
+      }
+    };
+    for (int base = 0; base < w.total && nseen < min_frames; base += 64) {
+      const int qq = base + lane;
+      const int64_t c = (qq < w.total) ? window_cell<D>(w, qq, g, slab_t, p.w, p.w) : -1;
+      int b = 0, e = 0, cls = 0;
+      if (c >= 0 && ((occ_bits[c >> 5] >> (c & 31)) & 1u)) {
+        const CellRec<D> cr = crec[c];
+        b = cr.b;
+        e = cr.e;
+        cls = classify<D>(p, rec_boxA<D>(cr), rec_boxB(cr), g);
+      }
+      uint64_t pm = __ballot(cls != 0);
+      while (pm && nseen < min_frames) {
+        const int l = __ffsll((unsigned long long)pm) - 1;
+        pm &= pm - 1;
+        const int bb = __shfl(b, l), cl = __shfl(cls, l);
+        // a whole-cell hit in frame-id data is one frame: its first point says which
+        const int ee = (cl == 1 && integral) ? bb + 1 : __shfl(e, l);
+        for (int j0 = bb; j0 < ee && nseen < min_frames; j0 += 64) {
+          const int j = j0 + lane;
+          bool has = false;
+          int32_t v = 0;
+          if (j < ee) {
+            const float4 pj = pts[j];
+            if (cl == 1 || adjacent<D>(p, pj, g)) {
+              has = true;
+              v = np_i32(pj.w);
+            }
+          }
+          add(has, v);
+        }
+      }
+    }
+    if (lane == 0) core[s] = (nseen >= min_frames) ? 1 : 0;
+  }
+}
+
 // spos[orig] = sorted position
 __global__ void k_inverse_perm(const int32_t* __restrict__ sorig, int64_t n,
                                int32_t* __restrict__ spos) {
@@ -3260,14 +3356,25 @@ int32_t DbscanState::frames_pass(int32_t min_frames, hipStream_t st) {
                      cells ? (const uint8_t*)fok : (const uint8_t*)nullptr, (int)min_frames,
                      refine ? 1 : 0, core, list, count);
   if (refine) {
-    if (dim == 2)
+    // offsets of int32(t) within +-31 of the point's own frame fit the 64-bit set (|dt| <=
+    // eps_t <= 30); larger windows list the distinct frames instead
+    const bool small = (double)g.epst <= 30.0;
+    if (dim == 2 && small)
       hipLaunchKernelGGL(k_frames_points<2>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
                          rec<2>(), occ_bits, slab_t, integral_t ? 1 : 0, (int)min_frames, list,
                          count, core);
-    else
+    else if (small)
       hipLaunchKernelGGL(k_frames_points<3>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
                          rec<3>(), occ_bits, slab_t, integral_t ? 1 : 0, (int)min_frames, list,
                          count, core);
+    else if (dim == 2)
+      hipLaunchKernelGGL(k_frames_points_list<2>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts,
+                         skey, g, rec<2>(), occ_bits, slab_t, integral_t ? 1 : 0,
+                         (int)min_frames, list, count, core);
+    else
+      hipLaunchKernelGGL(k_frames_points_list<3>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts,
+                         skey, g, rec<3>(), occ_bits, slab_t, integral_t ? 1 : 0,
+                         (int)min_frames, list, count, core);
   }
   RPT_CHECK_LAUNCH();
   return RPT_OK;
@@ -3364,8 +3471,10 @@ int32_t stdbscan_denoise(const float* x, const float* y, const float* t, int64_t
     set_error("rpt_stdbscan_denoise: null labels");
     return RPT_EINVAL;
   }
-  if (min_frames >= 2 && !((float)eps_time <= 30.0f) && (float)eps_time == (float)eps_time) {
-    set_error("rpt_stdbscan_denoise: eps_time > 30 with min_frames >= 2 is not supported");
+  if (min_frames > 64 * kFramesPerLane && !((float)eps_time <= 30.0f) &&
+      (float)eps_time == (float)eps_time) {
+    set_error("rpt_stdbscan_denoise: min_frames > %d with eps_time > 30 is not supported",
+              64 * kFramesPerLane);
     return RPT_ENOTSUP;
   }
   int dev = 0;

@@ -70,8 +70,40 @@ def test_denoise_float_times_and_edges(gpu):
     assert (st_dbscan(xy, t, -1.0, 2.0, 3, 2, device=gpu) == -1).all()
     np.testing.assert_array_equal(st_dbscan(xy, t, -1.0, 2.0, 0, 0, device=gpu),
                                   np.arange(3000, dtype=np.int32))
+    # the distinct-frame list holds 256 frames: more min_frames with eps_time > 30 is refused
     with pytest.raises(NotImplementedError):
-        st_dbscan(xy, t, 5.0, 40.0, 5, 2, device=gpu)
+        st_dbscan(xy, t, 5.0, 40.0, 5, 257, device=gpu)
+
+
+@pytest.mark.parametrize("eps_time,min_frames,float_t", [(40.0, 2, False), (45.5, 5, False),
+                                                          (120.0, 30, False), (31.0, 3, True),
+                                                          (64.0, 70, False)])
+def test_denoise_wide_time_window(gpu, eps_time, min_frames, float_t):
+    """eps_time > 30 (the distinct int32(t) frames as a wave-wide list instead of a 64-bit offset
+    set, k_frames_points_list): buoys seen in a random subset of 200 frames, clutter, a NaN
+    time; against the oracle's FIFO restatement (:264-369)."""
+    from rpt.denoise import st_dbscan
+
+    rng = np.random.default_rng(int(eps_time * 10) + min_frames)
+    pts, ts = [], []
+    for c in rng.random((25, 2)) * 300:
+        fr = np.sort(rng.choice(200, rng.integers(20, 120), replace=False))
+        k = rng.integers(1, 4, len(fr))
+        pts.append(np.repeat(c[None], k.sum(), 0) + rng.normal(0, 1.5, (k.sum(), 2)))
+        ts.append(np.repeat(fr, k))
+    pts.append(rng.random((3000, 2)) * 300)
+    ts.append(rng.integers(0, 200, 3000))
+    xy = np.vstack(pts).astype(np.float32)
+    t = np.concatenate(ts).astype(np.float32)
+    if float_t:
+        t = (t + rng.random(len(t)).astype(np.float32) * 0.9).astype(np.float32)
+    t[::997] = np.nan
+    perm = rng.permutation(len(t))
+    xy, t = xy[perm], t[perm]
+    lab = st_dbscan(xy, t, 5.0, eps_time, 12, min_frames, device=gpu)
+    ref = oracle.stdbscan_denoise(xy, t, 5.0, eps_time, 12, min_frames)
+    assert (ref >= 0).sum() > 500
+    np.testing.assert_array_equal(lab, ref)
 
 
 def test_label_means_match_pandas_group_mean(gpu):

@@ -19,6 +19,21 @@ def test_stdbscan_oracle_matches_reference_labels(golden):
         np.testing.assert_array_equal(lab, g[f"c{k}_labels"], err_msg=f"uf case {k}")
 
 
+def test_reference_structure_baseline_matches_reference_labels(golden):
+    """oracle/refpath.py (bench.py's cpu_baseline: whole-stack BallTree + per-neighbour time
+    filter + seed-set expansion, the reference's structure) gives the reference's labels."""
+    from oracle.refpath import stdbscan_structure
+
+    g = golden("g2_stdbscan.npz")
+    for k in range(int(g["n_cases"])):
+        c, t = g[f"c{k}_coords"], g[f"c{k}_times"]
+        if len(c) == 0:
+            continue
+        eps, et, ms = g[f"c{k}_params"]
+        lab, _ = stdbscan_structure(c, t, eps, et, int(ms))
+        np.testing.assert_array_equal(lab, g[f"c{k}_labels"], err_msg=f"case {k}")
+
+
 def test_stdbscan_uf_matches_bfs_on_dense_stacks():
     """The set-formulation checker (used at full stack sizes) against the BFS oracle on dense
     multi-frame clouds: chained clusters, border points between clusters, frame-id gaps, NaN

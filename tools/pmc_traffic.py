@@ -7,6 +7,7 @@ Writes profiles/<tag>/<name> (default k5_traffic.json) and a per-kernel summary 
 import csv
 import glob
 import json
+import os
 import sys
 from collections import defaultdict
 from pathlib import Path
@@ -15,7 +16,8 @@ ROOT = Path(__file__).resolve().parents[1]
 tag = sys.argv[1] if len(sys.argv) > 1 else "r1"
 out_name = sys.argv[2] if len(sys.argv) > 2 else "k5_traffic.json"
 workload = sys.argv[3] if len(sys.argv) > 3 else "bench.py default (100-frame stack)"
-K5 = ("k_core_cells_oct", "k_core_cell_fast", "k_core_cell_window", "k_core_fill", "k_core_slow")
+K5 = ("k_core_cells_oct", "k_core_cell_fast", "k_core_cell_window", "k_core_fill", "k_core_slow",
+      "k_core_tiles")
 
 
 def load(counter):
@@ -31,7 +33,10 @@ def load(counter):
 
 
 fetch, write = load("FETCH_SIZE"), load("WRITE_SIZE")
-out_dir = ROOT / "profiles" / tag
+# RPT_PROFILE_OUT: write there instead (on the GPU box: a gpurun_out/ subdirectory, the only
+# place whose files come back; tools/collect_r3.sh copies them into profiles/<tag>/)
+out_dir = Path(os.environ["RPT_PROFILE_OUT"]) if os.environ.get("RPT_PROFILE_OUT") else \
+    ROOT / "profiles" / tag
 out_dir.mkdir(parents=True, exist_ok=True)
 rows = []
 for name in sorted(set(fetch) | set(write)):
@@ -39,7 +44,9 @@ for name in sorted(set(fetch) | set(write)):
     fa = sum(f) / len(f) if f else 0.0
     wa = sum(w) / len(w) if w else 0.0
     rows.append((name, len(f), fa, wa, (2 * fa + wa) * 1024))
-with open(out_dir / "pmc_traffic_by_kernel.csv", "w", newline="") as fh:
+by_kernel = "pmc_traffic_by_kernel.csv" if out_name == "k5_traffic.json" else \
+    out_name.replace("k5_traffic_", "pmc_traffic_by_kernel_").replace(".json", ".csv")
+with open(out_dir / by_kernel, "w", newline="") as fh:
     wr = csv.writer(fh)
     wr.writerow(["kernel", "launches", "FETCH_SIZE_KiB_avg", "WRITE_SIZE_KiB_avg",
                  "hbm_bytes_per_launch_corrected"])
