@@ -1324,6 +1324,7 @@ __device__ __forceinline__ void write_cell_flags(uint8_t* __restrict__ core, int
 // keep many short dependency chains in flight.  cflag as k_core_cell_fast / _window (level 3
 // turns it into point flags).
 constexpr int kCwMaxR = 3;
+constexpr int kCwBatch = 5;  // candidate records per lane in flight together (k_core_cells_oct)
 __global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
                                                           const int32_t* __restrict__ occ,
                                                           const int32_t* __restrict__ n_occ,
@@ -1399,38 +1400,52 @@ __global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
       } else {
         int lo = 0, hi = 0;
         const float4 A1 = rec_boxA<2>(ra), A2 = rec_boxB(ra);
-        // rows nearest first (the cell's own row, then +-1, then +-2); the eight lanes stop as
-        // soon as the adjacent-to-every-point count reaches min_samples (most cells: after the
-        // own row), saving the outer rows' record round trips
+        // the lane's occupied candidates as one 25-bit mask, rows nearest first (bits 0-4 the
+        // cell's own row, 5-14 rows -1 / +1, 15-24 rows -2 / +2), taken kCwBatch at a time with
+        // all their record loads in flight together: a sparse cell's few candidates cost ONE
+        // round trip instead of one per row; the eight lanes stop as soon as the adjacent-to-
+        // every-point count reaches min_samples (dense cells: after the own row's batch)
+        uint32_t m25 = 0;
+        if (reach) {
+#pragma unroll
+          for (int k = 0; k < 5; ++k) {
+            const int dy = (k == 0) ? 2 : ((k & 1) ? 2 - (k + 1) / 2 : 2 + k / 2);
+            m25 |= m5[dy] << (5 * k);
+          }
+        }
         bool decided = false;
+        while (true) {
+          int rem = m25 ? 1 : 0;
 #pragma unroll
-        for (int k = 0; k < 5; ++k) {
-          const int dy = (k == 0) ? 2 : ((k & 1) ? 2 - (k + 1) / 2 : 2 + k / 2);
-          const uint32_t m = reach ? m5[dy] : 0u;
-          if (m) {
-            const int row = (sl * g.ny + (cy + dy - 2)) * g.nx + (cx - 2);
-            // the row's (up to 5) candidate records in flight together, then classified
-            CellRec<2> cr[5];
+          for (int off = 4; off > 0; off >>= 1) rem += __shfl_xor(rem, off, 8);
+          if (rem == 0) break;  // (uniform over the cell's eight lanes)
+          CellRec<2> cr[kCwBatch];
+          bool has[kCwBatch];
 #pragma unroll
-            for (int dx = 0; dx < 5; ++dx)
-              if ((m >> dx) & 1u) cr[dx] = crec[row + dx];
-#pragma unroll
-            for (int dx = 0; dx < 5; ++dx) {
-              if (!((m >> dx) & 1u)) continue;
-              const int cls =
-                  classify_cells<2, true>(A1, rec_boxA<2>(cr[dx]), A2, rec_boxB(cr[dx]), g);
-              lo += (cls == 1) ? cr[dx].e - cr[dx].b : 0;
-              hi += (cls != 0) ? cr[dx].e - cr[dx].b : 0;
+          for (int i = 0; i < kCwBatch; ++i) {
+            has[i] = m25 != 0;
+            if (has[i]) {
+              const int p = __builtin_ctz(m25);
+              m25 &= m25 - 1;
+              const int k = p / 5, dx = p - 5 * k;
+              const int dy = (k == 0) ? 2 : ((k & 1) ? 2 - (k + 1) / 2 : 2 + k / 2);
+              cr[i] = crec[(sl * g.ny + (cy + dy - 2)) * g.nx + (cx + dx - 2)];
             }
           }
-          if (k == 0 || k == 2) {
-            int ls = lo;
 #pragma unroll
-            for (int off = 4; off > 0; off >>= 1) ls += __shfl_xor(ls, off, 8);
-            if (ls >= need) {
-              decided = true;
-              break;
-            }
+          for (int i = 0; i < kCwBatch; ++i) {
+            if (!has[i]) continue;
+            const int cls =
+                classify_cells<2, true>(A1, rec_boxA<2>(cr[i]), A2, rec_boxB(cr[i]), g);
+            lo += (cls == 1) ? cr[i].e - cr[i].b : 0;
+            hi += (cls != 0) ? cr[i].e - cr[i].b : 0;
+          }
+          int ls = lo;
+#pragma unroll
+          for (int off = 4; off > 0; off >>= 1) ls += __shfl_xor(ls, off, 8);
+          if (ls >= need) {
+            decided = true;
+            break;
           }
         }
         if (decided) {
@@ -1703,6 +1718,296 @@ __global__ __launch_bounds__(kBlock) void k_core_slow_cells(const float4* __rest
         }
         if (lane == 0) core[s] = (cnt >= need) ? 1 : 0;
       }
+    }
+  }
+}
+
+// ---- K5 by LDS tiles (2-D, slab window <= 7): the occupied-cell records a slab-row band needs
+// are staged in LDS ONCE per workgroup instead of fetched from HBM/L2 by every cell that has them
+// as a candidate (~30 record loads per sparse cell).  A tile = slab s x rows [y0, y0 + BY); its
+// workgroup stages the records of rows [y0 - 2, y0 + BY + 2) of slabs s - R .. s + R (ranges of
+// the ascending occupied list, found through rowq: the first occupied index of every (slab, row))
+// and a dense u16 map (slab offset, row, x) -> staged index, then
+//   cell pass: eight lanes per own cell as k_core_cells_oct (lane j = slab offset; own row first,
+//     early exit once the adjacent-to-every-point count reaches min_samples), records from LDS;
+//     decided cells write their points' flags;
+//   slow pass: one wave per undecided own cell, its candidate cells (LDS) classified against the
+//     CELL once, then its points one by one: a box test per candidate, the undecided candidates'
+//     points (global, 64 at a time) until min_samples.
+// A tile whose records exceed kTileCap reads them from global memory instead (the same code).
+constexpr int kTileBlock = 512;
+constexpr int kTileCap = 1536;   // staged CellRec<2> per tile (48 KiB)
+constexpr int kTileMap = 8192;   // u16 map entries (16 KiB): W * (BY + 4) * nx <= this
+constexpr int kTileUnd = 1024;   // undecided own cells per tile: BY * nx <= this
+
+// rowcnt[r] = occupied cells of row r = (slab, y) (bits [r nx, (r + 1) nx) of occ_bits)
+__global__ __launch_bounds__(kBlock) void k_row_occ(const uint32_t* __restrict__ occ_bits,
+                                                   int64_t nrows, int nx,
+                                                   int32_t* __restrict__ rowcnt) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nrows;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b0 = r * nx, b1 = b0 + nx;
+    int c = 0;
+    for (int64_t w = b0 >> 5; w <= (b1 - 1) >> 5; ++w) {
+      uint32_t m = occ_bits[w];
+      const int64_t lo = w << 5;
+      if (lo < b0) m &= ~0u << (b0 - lo);
+      if (lo + 32 > b1) m &= ~0u >> (lo + 32 - b1);
+      c += __popc(m);
+    }
+    rowcnt[r] = c;
+  }
+}
+
+__global__ __launch_bounds__(kTileBlock) void k_core_tiles(
+    Geom g, int R, int BY, int nbands, int64_t ntiles, const int32_t* __restrict__ occ,
+    const int32_t* __restrict__ n_occ, const int32_t* __restrict__ rowq,
+    const CellRec<2>* __restrict__ crec, const uint8_t* __restrict__ mutual,
+    const uint32_t* __restrict__ occ_bits, const float2* __restrict__ slab_t,
+    const float4* __restrict__ pts, uint8_t* __restrict__ core) {
+  __shared__ CellRec<2> srec[kTileCap];
+  __shared__ uint16_t smap[kTileMap];
+  __shared__ int s_und[kTileUnd];
+  __shared__ int s_q0[8], s_base[8], s_reach[8];
+  __shared__ int s_total, s_nund;
+  const int need = g.min_samples;
+  const int W = 2 * R + 1, MR = BY + 4;
+  // XCD-contiguous tile ranges (grid a multiple of 8: blockIdx % 8 is the XCD): neighbouring
+  // tiles stage overlapping records, which then stay in one XCD's L2
+  const int64_t tile = (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  if (tile > ntiles) return;
+  if (tile == ntiles) {  // the isolated cell (non-finite times: no neighbour, not even itself)
+    const int64_t no = *n_occ;
+    if (no > 0 && (int64_t)occ[no - 1] >= g.cells) {
+      const CellRec<2> ri = crec[occ[no - 1]];
+      write_cell_flags(core, ri.b, ri.e, threadIdx.x, blockDim.x, need <= 0 ? 1 : 0);
+    }
+    return;
+  }
+  const int s = (int)(tile / nbands), band = (int)(tile % nbands);
+  const int y0 = band * BY, y1 = min(y0 + BY, g.ny);
+  const int ya = max(y0 - 2, 0), yb = min(y1 + 2, g.ny);
+  const int qo0 = rowq[(int64_t)s * g.ny + y0], qo1 = rowq[(int64_t)s * g.ny + y1];
+  if (qo1 <= qo0) return;  // no own cell (uniform over the block)
+  if (threadIdx.x < 8) {
+    const int so = threadIdx.x, sl = s - R + so;
+    int q0 = 0, cnt = 0, rc = 0;
+    if (so < W && sl >= 0 && sl < g.nt) {
+      const float2 own = slab_t[s], sr = slab_t[sl];
+      const float gap = (own.x > sr.y) ? (own.x - sr.y) : ((sr.x > own.y) ? (sr.x - own.y) : 0.f);
+      rc = (sr.x <= sr.y && gap <= g.epst) ? 1 : 0;
+      if (rc) {
+        q0 = rowq[(int64_t)sl * g.ny + ya];
+        cnt = rowq[(int64_t)sl * g.ny + yb] - q0;
+      }
+    }
+    // exclusive scan of the eight counts inside the first eight lanes
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 8; off <<= 1) {
+      const int o = __shfl_up(incl, off, 8);
+      if (so >= off) incl += o;
+    }
+    s_q0[so] = q0;
+    s_base[so] = incl - cnt;
+    s_reach[so] = rc;
+    if (so == 7) s_total = incl;
+  }
+  if (threadIdx.x == 0) s_nund = 0;
+  __syncthreads();
+  const bool lds = s_total <= kTileCap;
+  if (lds) {
+    const int mapn = W * MR * g.nx;
+    for (int i = threadIdx.x; i < mapn; i += blockDim.x) smap[i] = 0xFFFF;
+    __syncthreads();
+    for (int so = 0; so < W; ++so) {
+      const int q0 = s_q0[so], base = s_base[so];
+      const int cnt = (so + 1 < 8 ? s_base[so + 1] : s_total) - base;
+      for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
+        const int32_t key = occ[q0 + i];
+        srec[base + i] = crec[key];
+        const int x = key % g.nx, y = (key / g.nx) % g.ny;
+        smap[(so * MR + (y - y0 + 2)) * g.nx + x] = (uint16_t)(base + i);
+      }
+    }
+    __syncthreads();
+  }
+  // the five candidate cells (x = cx - 2 .. cx + 2) of row y of slab offset so: present flags
+  // and records, from LDS or (overflowing tile) from occ_bits + crec
+  auto row5 = [&](int so, int y, int cx, CellRec<2>* cr) -> uint32_t {
+    uint32_t m = 0;
+    if (lds) {
+      const int mrow = (so * MR + (y - y0 + 2)) * g.nx;
+      uint16_t id[5];
+#pragma unroll
+      for (int dx = 0; dx < 5; ++dx) {
+        const int x = cx + dx - 2;
+        id[dx] = (x >= 0 && x < g.nx) ? smap[mrow + x] : (uint16_t)0xFFFF;
+      }
+#pragma unroll
+      for (int dx = 0; dx < 5; ++dx)
+        if (id[dx] != 0xFFFF) {
+          cr[dx] = srec[id[dx]];
+          m |= 1u << dx;
+        }
+      return m;
+    }
+    const int k0 = ((s - R + so) * g.ny + y) * g.nx + (cx - 2);
+    const int kk = k0 < 0 ? 0 : k0;
+    const uint32_t lo_w = occ_bits[kk >> 5], hi_w = occ_bits[(kk >> 5) + 1];
+    m = (k0 < 0) ? ((lo_w << (-k0)) & 31u)
+                 : (__builtin_amdgcn_alignbit(hi_w, lo_w, (uint32_t)(kk & 31)) & 31u);
+    const int lo_x = cx - 2 < 0 ? 2 - cx : 0;
+    const int hi_x = cx + 2 - (g.nx - 1);
+    m &= ~((1u << lo_x) - 1u);
+    if (hi_x > 0) m &= (31u >> hi_x);
+#pragma unroll
+    for (int dx = 0; dx < 5; ++dx)
+      if ((m >> dx) & 1u) cr[dx] = crec[k0 + dx];
+    return m;
+  };
+  auto own_rec = [&](int q, int32_t ca) -> CellRec<2> {
+    return lds ? srec[s_base[R] + (q - s_q0[R])] : crec[ca];
+  };
+
+  // ---- cell pass: eight lanes per own cell
+  const int j = threadIdx.x & 7;
+  const int cpr = blockDim.x / 8;
+  for (int qc = qo0; qc < qo1; qc += cpr) {
+    const int q = qc + (int)threadIdx.x / 8;
+    const bool act = q < qo1;
+    int flag = 0, b = 0, e = 0;
+    if (act) {
+      const int32_t ca = occ[q];
+      const int cx = ca % g.nx, cy = (ca / g.nx) % g.ny;
+      const CellRec<2> ra = own_rec(q, ca);
+      b = ra.b;
+      e = ra.e;
+      if (need <= 0 || (mutual[ca] && e - b >= need)) {
+        flag = 1;
+      } else {
+        const bool sv = j < W && s_reach[j];
+        const float4 A1 = rec_boxA<2>(ra), A2 = rec_boxB(ra);
+        int lo = 0, hi = 0;
+        bool decided = false;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+          const int dy = (k == 0) ? 2 : ((k & 1) ? 2 - (k + 1) / 2 : 2 + k / 2);
+          const int y = cy + dy - 2;
+          if (sv && y >= 0 && y < g.ny) {
+            CellRec<2> cr[5];
+            const uint32_t m = row5(j, y, cx, cr);
+#pragma unroll
+            for (int dx = 0; dx < 5; ++dx) {
+              if (!((m >> dx) & 1u)) continue;
+              const int cls =
+                  classify_cells<2, true>(A1, rec_boxA<2>(cr[dx]), A2, rec_boxB(cr[dx]), g);
+              lo += (cls == 1) ? cr[dx].e - cr[dx].b : 0;
+              hi += (cls != 0) ? cr[dx].e - cr[dx].b : 0;
+            }
+          }
+          if (k == 0 || k == 2) {
+            int ls = lo;
+#pragma unroll
+            for (int off = 4; off > 0; off >>= 1) ls += __shfl_xor(ls, off, 8);
+            if (ls >= need) {
+              decided = true;
+              break;
+            }
+          }
+        }
+        if (decided) {
+          flag = 1;
+        } else {
+#pragma unroll
+          for (int off = 4; off > 0; off >>= 1) {
+            lo += __shfl_xor(lo, off, 8);
+            hi += __shfl_xor(hi, off, 8);
+          }
+          flag = (lo >= need) ? 1 : ((hi < need) ? 0 : 2);
+        }
+      }
+      if (flag == 2 && j == 0) s_und[atomicAdd(&s_nund, 1)] = q;  // < BY * nx <= kTileUnd
+    }
+    if (act && flag != 2) write_cell_flags(core, b, e, j, 8, (uint8_t)flag);
+  }
+  __syncthreads();
+
+  // ---- slow pass: one wave per undecided own cell
+  const int lane = threadIdx.x & 63;
+  const int nund = s_nund;
+  constexpr int kSR = 3;  // candidate positions per lane: W * 25 <= 175 <= 3 * 64
+  for (int u = (int)threadIdx.x / 64; u < nund; u += (int)blockDim.x / 64) {
+    const int q = s_und[u];
+    const int32_t ca = occ[q];
+    const CellRec<2> ra = own_rec(q, ca);
+    const float4 A1 = rec_boxA<2>(ra), A2 = rec_boxB(ra);
+    const int cx = ca % g.nx, cy = (ca / g.nx) % g.ny;
+    float4 cA[kSR], cB[kSR];
+    int cb[kSR], ce[kSR], ccls[kSR];
+#pragma unroll
+    for (int r = 0; r < kSR; ++r) {
+      cb[r] = ce[r] = ccls[r] = 0;
+      cA[r] = cB[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int pos = r * 64 + lane;
+      const int so = pos / 25, rem = pos - so * 25;
+      const int y = cy + rem / 5 - 2, x = cx + rem % 5 - 2;
+      if (pos < W * 25 && s_reach[so] && y >= 0 && y < g.ny && x >= 0 && x < g.nx) {
+        bool have = false;
+        CellRec<2> cr;
+        if (lds) {
+          const uint16_t id = smap[(so * MR + (y - y0 + 2)) * g.nx + x];
+          if (id != 0xFFFF) {
+            cr = srec[id];
+            have = true;
+          }
+        } else {
+          const int64_t k = ((int64_t)(s - R + so) * g.ny + y) * g.nx + x;
+          if ((occ_bits[k >> 5] >> (k & 31)) & 1u) {
+            cr = crec[k];
+            have = true;
+          }
+        }
+        if (have) {
+          const int cls = classify_cells<2, true>(A1, rec_boxA<2>(cr), A2, rec_boxB(cr), g);
+          if (cls) {
+            cb[r] = cr.b;
+            ce[r] = cr.e;
+            ccls[r] = cls;
+            cA[r] = rec_boxA<2>(cr);
+            cB[r] = rec_boxB(cr);
+          }
+        }
+      }
+    }
+    int full = 0;
+#pragma unroll
+    for (int r = 0; r < kSR; ++r) full += (ccls[r] == 1) ? ce[r] - cb[r] : 0;
+    const int lo_c = wave_sum(full);  // adjacent to every point of the cell
+    for (int sp = ra.b; sp < ra.e; ++sp) {
+      const float4 p = pts[sp];
+      int cls[kSR];
+      int add = 0;
+#pragma unroll
+      for (int r = 0; r < kSR; ++r) {
+        cls[r] = (ccls[r] == 2) ? classify<2>(p, cA[r], cB[r], g) : 0;
+        add += (cls[r] == 1) ? ce[r] - cb[r] : 0;
+      }
+      int cnt = lo_c + wave_sum(add);
+#pragma unroll
+      for (int r = 0; r < kSR; ++r) {
+        uint64_t pm = __ballot(cls[r] == 2);
+        while (pm && cnt < need) {
+          const int l = __ffsll((unsigned long long)pm) - 1;
+          pm &= pm - 1;
+          const int bb = __shfl(cb[r], l), ee = __shfl(ce[r], l);
+          for (int j0 = bb; j0 < ee && cnt < need; j0 += 64) {
+            const int jj = j0 + lane;
+            cnt += __popcll(__ballot((jj < ee) && adjacent<2>(p, pts[jj], g)));
+          }
+        }
+      }
+      if (lane == 0) core[sp] = (cnt >= need) ? 1 : 0;
     }
   }
 }
@@ -2313,6 +2618,227 @@ __global__ __launch_bounds__(kBlock, 7) void k_label(const float4* __restrict__ 
   }
 }
 
+// K7/K8 by LDS tiles (2-D, slab window <= 7; k_core_tiles' tiles and rowq): the border labels of
+// the non-core points of a tile's own cells, with every candidate cell's record, smallest
+// component key (cell_key) and mutual flag staged in LDS once per tile.  One wave per own cell
+// holding non-core points: its candidates (lanes) classified against the CELL once, then per
+// non-core point the k_label rule -- wholly adjacent cells give their key, the partial ones are
+// resolved in increasing key order while the key can still win (a mutual cell by any adjacent
+// core point, another cell by the smallest key among its adjacent core points).  Overflowing
+// tiles read the same data from global memory.  GLOBAL as in k_label.
+constexpr int kTileCapL = 1280;  // staged cells per tile (32 B record + key + mutual each)
+template <bool GLOBAL>
+__global__ __launch_bounds__(kTileBlock) void k_label_tiles(
+    Geom g, int R, int BY, int nbands, int64_t ntiles, const int32_t* __restrict__ occ,
+    const int32_t* __restrict__ n_occ, const int32_t* __restrict__ rowq,
+    const CellRec<2>* __restrict__ crec,
+    const uint8_t* __restrict__ mutual, const uint32_t* __restrict__ occ_bits,
+    const float2* __restrict__ slab_t, const float4* __restrict__ pts,
+    const int32_t* __restrict__ key_of, const int32_t* __restrict__ cell_key,
+    const int32_t* __restrict__ sorig, MinRank cid, int32_t need, int32_t* __restrict__ labels) {
+  __shared__ CellRec<2> srec[kTileCapL];
+  __shared__ int sck[kTileCapL];
+  __shared__ uint8_t smu[kTileCapL];
+  __shared__ uint16_t smap[kTileMap];
+  __shared__ int s_q0[8], s_base[8], s_reach[8];
+  __shared__ int s_total;
+  const int W = 2 * R + 1, MR = BY + 4;
+  const int64_t tile = (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  if (tile > ntiles) return;
+  if (tile == ntiles) {  // the isolated cell (non-finite times): its non-core points are noise
+    const int64_t no = *n_occ;
+    if (no > 0 && (int64_t)occ[no - 1] >= g.cells) {
+      const CellRec<2> ri = crec[occ[no - 1]];
+      for (int sp = ri.b + (int)threadIdx.x; sp < ri.e; sp += blockDim.x)
+        if (key_of[sp] < 0) labels[sorig[sp]] = -1;
+    }
+    return;
+  }
+  const int s = (int)(tile / nbands), band = (int)(tile % nbands);
+  const int y0 = band * BY, y1 = min(y0 + BY, g.ny);
+  const int ya = max(y0 - 2, 0), yb = min(y1 + 2, g.ny);
+  const int qo0 = rowq[(int64_t)s * g.ny + y0], qo1 = rowq[(int64_t)s * g.ny + y1];
+  if (qo1 <= qo0) return;
+  if (threadIdx.x < 8) {
+    const int so = threadIdx.x, sl = s - R + so;
+    int q0 = 0, cnt = 0, rc = 0;
+    if (so < W && sl >= 0 && sl < g.nt) {
+      const float2 own = slab_t[s], sr = slab_t[sl];
+      const float gap = (own.x > sr.y) ? (own.x - sr.y) : ((sr.x > own.y) ? (sr.x - own.y) : 0.f);
+      rc = (sr.x <= sr.y && gap <= g.epst) ? 1 : 0;
+      if (rc) {
+        q0 = rowq[(int64_t)sl * g.ny + ya];
+        cnt = rowq[(int64_t)sl * g.ny + yb] - q0;
+      }
+    }
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 8; off <<= 1) {
+      const int o = __shfl_up(incl, off, 8);
+      if (so >= off) incl += o;
+    }
+    s_q0[so] = q0;
+    s_base[so] = incl - cnt;
+    s_reach[so] = rc;
+    if (so == 7) s_total = incl;
+  }
+  __syncthreads();
+  const bool lds = s_total <= kTileCapL;
+  if (lds) {
+    const int mapn = W * MR * g.nx;
+    for (int i = threadIdx.x; i < mapn; i += blockDim.x) smap[i] = 0xFFFF;
+    __syncthreads();
+    for (int so = 0; so < W; ++so) {
+      const int q0 = s_q0[so], base = s_base[so];
+      const int cnt = (so + 1 < 8 ? s_base[so + 1] : s_total) - base;
+      for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
+        const int32_t key = occ[q0 + i];
+        srec[base + i] = crec[key];
+        sck[base + i] = cell_key[key];
+        smu[base + i] = mutual[key];
+        const int x = key % g.nx, y = (key / g.nx) % g.ny;
+        smap[(so * MR + (y - y0 + 2)) * g.nx + x] = (uint16_t)(base + i);
+      }
+    }
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & 63;
+  constexpr int kSR = 3;
+  for (int q = qo0 + (int)threadIdx.x / 64; q < qo1; q += (int)blockDim.x / 64) {
+    const int32_t ca = occ[q];
+    const CellRec<2> ra = lds ? srec[s_base[R] + (q - s_q0[R])] : crec[ca];
+    if ((lds ? smu[s_base[R] + (q - s_q0[R])] : mutual[ca]) && ra.e - ra.b >= need)
+      continue;  // all core
+    // the cell's non-core points, 64 flags at a time (key_of < 0: not core)
+    const float4 A1 = rec_boxA<2>(ra), A2 = rec_boxB(ra);
+    const int cx = ca % g.nx, cy = (ca / g.nx) % g.ny;
+    bool have_cands = false;
+    float4 cA[kSR], cB[kSR];
+    int cb[kSR], ce[kSR], ck[kSR], mu[kSR];
+    for (int sp0 = ra.b; sp0 < ra.e; sp0 += 64) {
+      const int spl = sp0 + lane;
+      uint64_t ncm = __ballot(spl < ra.e && key_of[spl] < 0);
+      if (!ncm) continue;
+      if (!have_cands) {  // candidates of the cell with core points that may reach its box
+        have_cands = true;
+#pragma unroll
+        for (int r = 0; r < kSR; ++r) {
+          cb[r] = ce[r] = 0;
+          ck[r] = INT_MAX;
+          mu[r] = 0;
+          cA[r] = cB[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+          const int pos = r * 64 + lane;
+          const int so = pos / 25, rem = pos - so * 25;
+          const int y = cy + rem / 5 - 2, x = cx + rem % 5 - 2;
+          if (pos < W * 25 && s_reach[so] && y >= 0 && y < g.ny && x >= 0 && x < g.nx) {
+            int id = -1;
+            int kk = INT_MAX;
+            CellRec<2> cr;
+            uint8_t m = 0;
+            if (lds) {
+              const uint16_t u = smap[(so * MR + (y - y0 + 2)) * g.nx + x];
+              if (u != 0xFFFF) {
+                id = u;
+                kk = sck[u];
+              }
+              if (kk != INT_MAX) {
+                cr = srec[id];
+                m = smu[id];
+              }
+            } else {
+              const int64_t k = ((int64_t)(s - R + so) * g.ny + y) * g.nx + x;
+              if ((occ_bits[k >> 5] >> (k & 31)) & 1u) kk = cell_key[k];
+              if (kk != INT_MAX) {
+                cr = crec[k];
+                m = mutual[k];
+              }
+            }
+            if (kk != INT_MAX &&
+                classify_cells<2, true>(A1, rec_boxA<2>(cr), A2, rec_boxB(cr), g) != 0) {
+              cb[r] = cr.b;
+              ce[r] = cr.e;
+              ck[r] = kk;
+              mu[r] = m;
+              cA[r] = rec_boxA<2>(cr);
+              cB[r] = rec_boxB(cr);
+            }
+          }
+        }
+      }
+      while (ncm) {
+        const int l0 = __ffsll((unsigned long long)ncm) - 1;
+        ncm &= ncm - 1;
+        const int sp = sp0 + l0;
+        const float4 p = pts[sp];
+        int cls[kSR];
+        int v = INT_MAX;
+#pragma unroll
+        for (int r = 0; r < kSR; ++r) {
+          cls[r] = (ck[r] != INT_MAX) ? classify<2>(p, cA[r], cB[r], g) : 0;
+          if (cls[r] == 1) v = min(v, ck[r]);
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off));
+        int best = v;
+        uint32_t pend = 0;
+#pragma unroll
+        for (int r = 0; r < kSR; ++r) pend |= (cls[r] == 2) ? (1u << r) : 0u;
+        while (true) {
+          int mine = INT_MAX, mk = -1;
+#pragma unroll
+          for (int r = 0; r < kSR; ++r)
+            if (((pend >> r) & 1u) && ck[r] < best && ck[r] < mine) {
+              mine = ck[r];
+              mk = r;
+            }
+          int mm = mine;
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1) mm = min(mm, __shfl_xor(mm, off));
+          if (mm == INT_MAX) break;
+          const uint64_t at = __ballot(mine == mm);
+          const int l = __ffsll((unsigned long long)at) - 1;
+          const int kl = __shfl(mk, l);
+          int bsel = 0, esel = 0, msel = 0;
+#pragma unroll
+          for (int r = 0; r < kSR; ++r)
+            if (r == kl) {
+              bsel = cb[r];
+              esel = ce[r];
+              msel = mu[r];
+            }
+          if (lane == l) pend &= ~(1u << kl);
+          const int bl = __shfl(bsel, l), el = __shfl(esel, l);
+          if (__shfl(msel, l)) {  // one component: a single adjacent core point decides
+            bool hit = false;
+            for (int j0 = bl; j0 < el && !hit; j0 += 64) {
+              const int j = j0 + lane;
+              hit = __ballot((j < el) && key_of[j] >= 0 && adjacent<2>(p, pts[j], g)) != 0;
+            }
+            if (hit) best = mm;
+          } else {
+            int lb = INT_MAX;
+            for (int j0 = bl; j0 < el; j0 += 64) {
+              const int j = j0 + lane;
+              if (j < el) {
+                const int m = key_of[j];
+                if (m >= 0 && m < best && m < lb && adjacent<2>(p, pts[j], g)) lb = m;
+              }
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) lb = min(lb, __shfl_xor(lb, off));
+            best = min(best, lb);
+          }
+        }
+        if (lane == 0) {
+          int32_t out = -1;
+          if (best != INT_MAX) out = GLOBAL ? best : cid[best];
+          labels[sorig[sp]] = out;
+        }
+      }
+    }
+  }
+}
+
 // Degenerate parameters (negative/NaN eps): nobody has a neighbour, not even itself.
 __global__ __launch_bounds__(kBlock) void k_isolated_labels(int32_t* labels, int64_t n,
                                                            int singletons) {
@@ -2781,6 +3307,23 @@ struct DbscanState {
   int uf_flags = -1;                         // see XcdRange; -1 = read RPT_UF_FLAGS once
   int k5_legacy = -1;                        // 1: round-1 K5 (fill + point queue); RPT_K5_MODE
   int k5_fill = 0;
+  int k5_tiles = -1;                         // 1: K5 by LDS tiles (k_core_tiles); RPT_K5_TILES
+  int k7_tiles = -1;                         // 1: K7 by LDS tiles (k_label_tiles); RPT_K7_TILES
+  int32_t* rowq = nullptr;    // first occupied-list index of every (slab, row) + total (tiles)
+  int32_t* rowcnt = nullptr;  // occupied cells per (slab, row)
+  bool rowq_ok = false;       // rowq built for this grid (the core pass's tile path)
+  int tile_by = 0, tile_nbands = 0, tile_R = 0;
+  // the label pass on the core pass's tiles (rowq built, RPT_K7_TILES not 0)
+  bool use_label_tiles() {
+    if (k7_tiles < 0) {  // RPT_K7_TILES=1 (measured slower than k_label, see k_core_tiles)
+      const char* e = ab_env("RPT_K7_TILES");
+      k7_tiles = (e && std::atoi(e) == 1) ? 1 : 0;
+    }
+    return k7_tiles && rowq_ok && dim == 2 && g.nz == 1;
+  }
+  unsigned tile_grid_blocks() const {  // the tiles + the isolated cell's, a multiple of 8
+    return (unsigned)((((int64_t)g.nt * tile_nbands + 1) + 7) & ~(int64_t)7);
+  }
   int bucket_mode = -1;                      // RPT_K4_BUCKET (default 1): slab-bucket K4
   template <int D>
   const CellRec<D>* rec() const {
@@ -2942,6 +3485,8 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   bud.add<int32_t>(nt + 1);        // slab_lo (slab-bucket path)
   bud.add<int32_t>(nt + 1);        // slab_occ (slab-bucket path)
   bud.add<int32_t>(nt + 1);        // occ_base (slab-bucket path)
+  bud.add<int32_t>((size_t)(ny * nz * nt) + 1);  // rowq (LDS-tile passes)
+  bud.add<int32_t>((size_t)(ny * nz * nt) + 1);  // row counts
   RPT_TRY(arena.reserve(bud.bytes, st));
   (void)arena.carve_n<Bounds>(1);
   uint32_t* keys = arena.carve_n<uint32_t>(n);
@@ -2980,7 +3525,10 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   int32_t* slab_lo = arena.carve_n<int32_t>(nt + 1);
   int32_t* slab_occ = arena.carve_n<int32_t>(nt + 1);
   int32_t* occ_base = arena.carve_n<int32_t>(nt + 1);
-  if (!slab_lo) {
+  rowq = arena.carve_n<int32_t>((size_t)(ny * nz * nt) + 1);
+  rowcnt = arena.carve_n<int32_t>((size_t)(ny * nz * nt) + 1);
+  rowq_ok = false;
+  if (!slab_lo || !rowcnt) {
     set_error("internal: scratch carve overflow");
     return RPT_ENOMEM;
   }
@@ -3104,6 +3652,35 @@ int32_t DbscanState::core_pass(hipStream_t st) {
   const double rs = integral_t ? std::ceil(std::floor((double)g.epst) / g.ct)
                                : std::ceil((double)g.epst / g.ct) + 1.0;
   const bool oct = dim == 2 && rs <= (double)kCwMaxR && g.nz == 1;
+  if (k5_tiles < 0) {  // RPT_K5_TILES=1: the LDS-tile pass (k_core_tiles; measured slower)
+    const char* e = ab_env("RPT_K5_TILES");
+    k5_tiles = (e && std::atoi(e) == 1) ? 1 : 0;
+  }
+  if (oct && k5_tiles) {
+    // LDS tiles: band height BY with the map (W slabs x BY + 4 rows x nx) and the undecided list
+    // (BY x nx own cells) within their LDS arrays; rowq (kept for the label pass's tiles)
+    const int R = (int)rs, W = 2 * R + 1;
+    const int by = std::min({8, kTileMap / (W * g.nx) - 4, kTileUnd / g.nx});
+    const int64_t nrows = (int64_t)g.nt * g.ny;
+    if (by >= 1) {
+      hipLaunchKernelGGL(k_row_occ, dim3(grid_for(nrows, kBlock, 4096)), dim3(kBlock), 0, st,
+                         occ_bits, nrows, g.nx, rowcnt);
+      RPT_CHECK_LAUNCH();
+      RPT_TRY(exclusive_scan_total_i32(rowcnt, rowq, nrows, st));
+      rowq_ok = true;
+      const int nbands = (g.ny + by - 1) / by;
+      tile_by = by;
+      tile_nbands = nbands;
+      tile_R = R;
+      const int64_t ntiles = (int64_t)g.nt * nbands;
+      const unsigned grid = (unsigned)(((ntiles + 1) + 7) & ~(int64_t)7);
+      hipLaunchKernelGGL(k_core_tiles, dim3(grid), dim3(kTileBlock), 0, st, g, R, by, nbands,
+                         ntiles, occ, n_occ, rowq, rec<2>(), mutual, occ_bits, slab_t, pts, core);
+      RPT_CHECK_LAUNCH();
+      tm.mark();
+      return RPT_OK;
+    }
+  }
   if (!k5_legacy) {
     // cells decide (and write their points' flags) in one pass; the undecided cells' points are
     // settled by k_core_slow_cells, which walks the occupied cells itself (no queue, no fill)
@@ -3264,7 +3841,12 @@ int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hi
   RPT_TRY(cluster_ids(st, cell_min));  // also the per-cell smallest keys (k_cell_min_key fused)
   const MinRank mr{min_bits, min_pref};
   hipLaunchKernelGGL(k_label_core, dim3(gb), dim3(kBlock), 0, st, ccmin, n, sorig, mr, labels);
-  if (dim == 2)
+  if (use_label_tiles())
+    hipLaunchKernelGGL((k_label_tiles<false>), dim3(tile_grid_blocks()), dim3(kTileBlock), 0, st,
+                       g, tile_R, tile_by, tile_nbands, (int64_t)g.nt * tile_nbands, occ,
+                       n_occ_dev, rowq, rec<2>(), mutual, occ_bits, slab_t, pts, ccmin, cell_min,
+                       sorig, mr, min_samples, labels);
+  else if (dim == 2)
     hipLaunchKernelGGL((k_label<2, false>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
                        rec<2>(), occ_bits, slab_t, ccmin, cell_min, mutual, sorig, mr, nc_list,
                        nc_count, labels);
@@ -3327,7 +3909,12 @@ int32_t DbscanState::labels_global(const int64_t* rep_orig, const int64_t* reps,
   const int gc = grid_for(C, kBlock, 8192);
   hipLaunchKernelGGL(k_fill_i32, dim3(gc), dim3(kBlock), 0, st, cell_min, C, INT_MAX);
   hipLaunchKernelGGL(k_cell_min_key, dim3(gb), dim3(kBlock), 0, st, skey, slab, n, C, cell_min);
-  if (dim == 2)
+  if (use_label_tiles())
+    hipLaunchKernelGGL((k_label_tiles<true>), dim3(tile_grid_blocks()), dim3(kTileBlock), 0, st,
+                       g, tile_R, tile_by, tile_nbands, (int64_t)g.nt * tile_nbands, occ,
+                       n_occ_dev, rowq, rec<2>(), mutual, occ_bits, slab_t, pts, slab, cell_min,
+                       sorig, MinRank{nullptr, nullptr}, min_samples, labels);
+  else if (dim == 2)
     hipLaunchKernelGGL((k_label<2, true>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
                        rec<2>(), occ_bits, slab_t, slab, cell_min, mutual, sorig,
                        MinRank{nullptr, nullptr}, nc_list, nc_count, labels);
