@@ -23,6 +23,8 @@ so the ranks cooperate; the result is identical to a single-device run:
 """
 from __future__ import annotations
 
+import contextlib
+import threading
 import time
 from concurrent.futures import Future, ThreadPoolExecutor
 from dataclasses import dataclass, field
@@ -451,6 +453,116 @@ def _unpack_parts(parts, F: int):
     return seg, np.concatenate(built), np.concatenate(fos), np.concatenate(orders)
 
 
+class CommSequencer:
+    """Orders the collectives of several stacks in flight on ONE communicator.
+
+    Each step (a stack run) passes through `phases` collective slots in order.  Steps are
+    registered at submission and grouped: a group closes when it holds `lanes` steps or when the
+    submitter waits for a result (close_group()).  Slot (step s, phase p) of a closed group of n
+    steps starting at step s0 runs at position base + p * n + (s - s0) of one global sequence:
+    inside a group the steps take their phase-p collectives in step order, phase by phase.  The
+    submitter's sequence of submissions and waits is the same on every rank, so every rank
+    issues the same collectives in the same order on the same process group -- no second
+    communicator whose kernels could be ordered differently on different GPUs (RCCL spinning
+    kernels sharing a process's hardware queues) -- while a lane's device phases between its
+    collectives overlap the other lanes' waits.  A step that fails poisons the sequencer so the
+    other lanes raise instead of waiting for slots that never come."""
+
+    def __init__(self, lanes: int, phases: int):
+        self.L, self.P = int(lanes), int(phases)
+        self.cv = threading.Condition()
+        self.turn = 0
+        self.failed: Optional[BaseException] = None
+        self.groups: List[List[int]] = []   # [start step, size, closed, base]
+        self.group_of: Dict[int, int] = {}
+
+    def register(self, step: int):
+        """Called by the submitter, in step order, before the step runs."""
+        with self.cv:
+            g = self.groups[-1] if self.groups else None
+            if g is None or g[2]:
+                base = g[3] + self.P * g[1] if g is not None else 0
+                g = [step, 0, False, base]
+                self.groups.append(g)
+            g[1] += 1
+            self.group_of[step] = len(self.groups) - 1
+            if g[1] == self.L:
+                g[2] = True
+                self.cv.notify_all()
+
+    def close_group(self):
+        """No more steps join the open group (the submitter is about to wait on a result)."""
+        with self.cv:
+            if self.groups and not self.groups[-1][2]:
+                self.groups[-1][2] = True
+                self.cv.notify_all()
+
+    def _index(self, step: int, phase: int) -> int:  # under self.cv
+        g = self.groups[self.group_of[step]]
+        while phase > 0 and not g[2] and self.failed is None:
+            self.cv.wait()
+        return g[3] + phase * g[1] + (step - g[0])
+
+    def _acquire(self, step: int, phase: int):
+        with self.cv:
+            idx = self._index(step, phase)
+            while self.turn != idx and self.failed is None:
+                self.cv.wait()
+            if self.failed is not None:
+                raise RuntimeError("collective sequence aborted by another stack") \
+                    from self.failed
+            return idx
+
+    def _release(self, idx: int):
+        with self.cv:
+            self.turn = idx + 1
+            self.cv.notify_all()
+
+    def abort(self, exc: BaseException):
+        with self.cv:
+            if self.failed is None:
+                self.failed = exc
+            self.cv.notify_all()
+
+    def step(self, step: int) -> "_StepSlots":
+        return _StepSlots(self, step)
+
+
+class _StepSlots:
+    """One step's walk through its slots: slot(k) first passes the skipped slots < k (their
+    turns still come in order), close() passes the remaining ones."""
+
+    def __init__(self, seq: CommSequencer, step: int):
+        self.seq, self.step, self.next = seq, step, 0
+
+    def _pass(self, upto: int):
+        while self.next < upto:
+            self.seq._release(self.seq._acquire(self.step, self.next))
+            self.next += 1
+
+    @contextlib.contextmanager
+    def slot(self, k: int):
+        self._pass(k)
+        i = self.seq._acquire(self.step, k)
+        try:
+            yield
+        finally:
+            self.seq._release(i)
+            self.next = k + 1
+
+    def close(self):
+        self._pass(self.seq.P)
+
+
+class _NoSlots:
+    @contextlib.contextmanager
+    def slot(self, k: int):
+        yield
+
+    def close(self):
+        pass
+
+
 class NativeShardPipeline:
     """The frame-sharded path with every per-rank stage in librpt's shard driver (rpt_shard_*,
     csrc/stack.cpp): one native call per phase, each at most one packed readback; the
@@ -505,11 +617,18 @@ class NativeShardPipeline:
             self.lib.rpt_shard_destroy(h)
             self.h = None
 
-    def run(self, echo: torch.Tensor, frame0: int) -> ShardResult:
-        with torch.cuda.device(self.dev):
-            return self._run(echo, frame0)
+    N_SLOTS = 9  # collective phases of one step (CommSequencer slots)
 
-    def _run(self, echo: torch.Tensor, frame0: int) -> ShardResult:
+    def run(self, echo: torch.Tensor, frame0: int, slots=None) -> ShardResult:
+        """slots: a CommSequencer step (several stacks in flight on one communicator) or None."""
+        slots = slots if slots is not None else _NoSlots()
+        with torch.cuda.device(self.dev):
+            try:
+                return self._run(echo, frame0, slots)
+            finally:
+                slots.close()
+
+    def _run(self, echo: torch.Tensor, frame0: int, slots) -> ShardResult:
         from ._device import stream_handle
         from .stages import LAND_MIN_INTENSITY, LAND_PERSISTENCE_THRESHOLD
 
@@ -542,9 +661,10 @@ class NativeShardPipeline:
                                 cos_d.data_ptr(), sin_d.data_ptr(), None,  # no per-point gains
                                 C_.byref(info), st), "rpt_shard_polar")
         n_points = int(info.n_points)
-        allinfo = comm.all_gather_fixed(torch.tensor(
-            [n_points, info.n_built, *[float(b) for b in info.bounds]],
-            dtype=torch.float64)).numpy()
+        with slots.slot(0):
+            allinfo = comm.all_gather_fixed(torch.tensor(
+                [n_points, info.n_built, *[float(b) for b in info.bounds]],
+                dtype=torch.float64)).numpy()
         n_global = int(allinfo[:, 0].sum())
         n_built = int(allinfo[:, 1].sum())
         mark("polar")
@@ -560,7 +680,8 @@ class NativeShardPipeline:
             grid = ws.get("grid", 2 * cells, torch.float64)
             chk(lib.rpt_shard_land_grid(self.h, gbp, grid.data_ptr(), cells, st),
                 "rpt_shard_land_grid")
-            grid = comm.all_reduce(grid, _SUM)
+            with slots.slot(1):
+                grid = comm.all_reduce(grid, _SUM)
         # 3. mask + compaction; own x / y / t land between room for the two halos
         h = int(np.floor(p.eps_time)) if np.isfinite(p.eps_time) and p.eps_time >= 0 else 0
         if W > 1 and h > F:
@@ -577,8 +698,9 @@ class NativeShardPipeline:
                                      Y[off:].data_ptr(), T[off:].data_ptr(), C_.byref(info), st),
             "rpt_shard_land_apply")
         n_own, n_head, n_tail = int(info.n_kept), int(info.n_head), int(info.n_tail)
-        kinfo = comm.all_gather_fixed(torch.tensor([n_own, n_head, n_tail],
-                                                   dtype=torch.int64)).numpy()
+        with slots.slot(2):
+            kinfo = comm.all_gather_fixed(torch.tensor([n_own, n_head, n_tail],
+                                                       dtype=torch.int64)).numpy()
         kept = kinfo[:, 0]
         P = int(kept[:r].sum())
         n_in_global = int(kept.sum())
@@ -593,8 +715,9 @@ class NativeShardPipeline:
         if halo:
             def pack(a, b):
                 return torch.cat([X[off + a:off + b], Y[off + a:off + b], T[off + a:off + b]])
-            hp, hn = comm.exchange_known(pack(0, n_head), pack(n_own - n_tail, n_own),
-                                         3 * n_prev, 3 * n_next)
+            with slots.slot(3):
+                hp, hn = comm.exchange_known(pack(0, n_head), pack(n_own - n_tail, n_own),
+                                             3 * n_prev, 3 * n_next)
             if n_prev:
                 X[off - n_prev:off] = hp[:n_prev]
                 Y[off - n_prev:off] = hp[n_prev:2 * n_prev]
@@ -619,8 +742,9 @@ class NativeShardPipeline:
         self.core_points = n_tot
         if halo:
             c_own = core[n_prev:n_prev + n_own]
-            cp, cn = comm.exchange_known(c_own[:n_head].contiguous(),
-                                         c_own[n_own - n_tail:].contiguous(), n_prev, n_next)
+            with slots.slot(4):
+                cp, cn = comm.exchange_known(c_own[:n_head].contiguous(),
+                                             c_own[n_own - n_tail:].contiguous(), n_prev, n_next)
             if n_prev:
                 core[:n_prev] = cp
             if n_next:
@@ -633,8 +757,10 @@ class NativeShardPipeline:
         pairs = np.zeros(0, np.int64)
         if halo:
             g_own = comp[n_prev:n_prev + n_own]
-            op_, on_ = comm.exchange_known(g_own[:n_head].contiguous(),
-                                           g_own[n_own - n_tail:].contiguous(), n_prev, n_next)
+            with slots.slot(5):
+                op_, on_ = comm.exchange_known(g_own[:n_head].contiguous(),
+                                               g_own[n_own - n_tail:].contiguous(), n_prev,
+                                               n_next)
             pcap = n_prev + n_next
             pb = ws.get("pairs", 1 + 2 * max(pcap, 1), torch.int64)
             if n_tot:
@@ -645,7 +771,8 @@ class NativeShardPipeline:
                 pb[0] = 0
             # [pair count | pairs]: one gather of the first 1 + cap words carries every rank's
             # count and (when they fit) its pairs; a larger count sends the rest in a second round
-            pairs = self._gather_pairs(comm, pb, 2 * max(pcap, 1))
+            with slots.slot(6):
+                pairs = self._gather_pairs(comm, pb, 2 * max(pcap, 1))
         npair = len(pairs) // 2
         pairs = np.ascontiguousarray(pairs, np.int64)
         nk = int(lib.rpt_merge_equivalences(pairs.ctypes.data_as(A.c_i64p), npair, None, None, 0))
@@ -662,7 +789,8 @@ class NativeShardPipeline:
                                     vals.ctypes.data_as(A.c_i64p), nk, base, n_prev, n_own,
                                     roots.data_ptr(), C_.byref(nr), st), "rpt_shard_roots")
         if W > 1:
-            all_roots, mx = comm.all_gather_capped(roots[:int(nr.value)], self._cap_roots)
+            with slots.slot(7):
+                all_roots, mx = comm.all_gather_capped(roots[:int(nr.value)], self._cap_roots)
             self._cap_roots = max(self._cap_roots, mx + mx // 4 + 64)
         else:
             all_roots = [roots[:int(nr.value)]]
@@ -695,7 +823,8 @@ class NativeShardPipeline:
             first_noise, seg["frame"], seg["label"], seg["count"], seg["first"], seg["cx"],
             seg["cy"], seg["mi"]]).astype(np.float64)
         if W > 1:
-            parts, mx = comm.all_gather_capped(torch.from_numpy(packed), self._cap_parts)
+            with slots.slot(8):
+                parts, mx = comm.all_gather_capped(torch.from_numpy(packed), self._cap_parts)
             self._cap_parts = max(self._cap_parts, mx + mx // 4 + 64)
             parts = [q.cpu() for q in parts]
         else:
@@ -762,12 +891,14 @@ class NativeShardPipeline:
 
 
 class ShardLanes:
-    """Several stacks in flight on the frame-sharded path: lane i owns a NativeShardPipeline
-    with its own process group (its own RCCL communicator, so one lane's collectives never
-    interleave with another's), its own HIP stream and one worker thread.  submit() hands the
-    stacks to the lanes in turn; every rank submits the same sequence, so each lane's collectives
-    pair up across ranks.  Step k+1's device work then runs while step k waits on collectives,
-    readbacks or its host stage -- the sharded form of FrameStackPipeline(lanes=...)."""
+    """Several stacks in flight on the frame-sharded path, through ONE communicator: lane i owns
+    a NativeShardPipeline, a HIP stream and one worker thread; all lanes share the default
+    process group, and a CommSequencer gives every rank the same global order of the lanes'
+    collectives (step by step within a group of `lanes` consecutive steps, phase by phase), so
+    no second RCCL communicator exists whose kernels could interleave differently on different
+    GPUs.  submit() hands the stacks to the lanes in turn; every rank submits the same sequence.
+    Step k+1's device phases then run while step k waits on collectives, readbacks or its host
+    stage -- the sharded form of FrameStackPipeline(lanes=...)."""
 
     def __init__(self, dev: torch.device, lanes: int, gains: Sequence[int], rows: int,
                  bins: int, params: PathParams = None, timing: bool = False,
@@ -775,35 +906,52 @@ class ShardLanes:
         if lanes < 1:
             raise ValueError("lanes must be >= 1")
         self.dev = dev
-        world = dist.get_world_size()
-        groups = [None] + [dist.new_group(list(range(world))) for _ in range(lanes - 1)]
-        self.pipes = [NativeShardPipeline(Comm(dev, g), gains, rows, bins, params, timing=timing,
+        comm = Comm(dev)
+        self.pipes = [NativeShardPipeline(comm, gains, rows, bins, params, timing=timing,
                                           async_host=async_host, host_workers=host_workers)
-                      for g in groups]
+                      for _ in range(lanes)]
+        self.seq = CommSequencer(lanes, NativeShardPipeline.N_SLOTS)
         self.streams = [torch.cuda.Stream(dev) for _ in range(lanes)] if lanes > 1 else [None]
         self.pools = [ThreadPoolExecutor(max_workers=1) for _ in range(lanes)]
-        self._next = 0
+        self._step = 0
 
     def set_geometry(self, scale, cos_t, sin_t, n_files: int):
         for p in self.pipes:
             p.set_geometry(scale, cos_t, sin_t, n_files)
 
     def submit(self, echo: torch.Tensor, frame0: int) -> Future:
-        """Runs the next lane on (echo, frame0); Future of its ShardResult (call finish())."""
-        li = self._next
-        self._next = (li + 1) % len(self.pipes)
+        """Runs the next step on lane step % lanes; Future of its ShardResult (call finish())."""
+        step = self._step
+        self._step += 1
+        li = step % len(self.pipes)
         pipe, s = self.pipes[li], self.streams[li]
+        self.seq.register(step)
+        slots = self.seq.step(step)
 
         def work():
-            with torch.cuda.device(self.dev):
-                if s is None:
-                    return pipe.run(echo, frame0)
-                s.wait_stream(torch.cuda.default_stream(self.dev))  # the echo is ready
-                with torch.cuda.stream(s):
-                    return pipe.run(echo, frame0)
+            try:
+                with torch.cuda.device(self.dev):
+                    if s is None:
+                        return pipe.run(echo, frame0, slots)
+                    s.wait_stream(torch.cuda.default_stream(self.dev))  # the echo is ready
+                    with torch.cuda.stream(s):
+                        return pipe.run(echo, frame0, slots)
+            except BaseException as e:
+                self.seq.abort(e)
+                raise
 
-        return self.pools[li].submit(work)
+        fut = self.pools[li].submit(work)
+        seq = self.seq
+        wait = fut.result
+
+        def result(timeout=None):  # waiting on a step closes the open group (same on all ranks)
+            seq.close_group()
+            return wait(timeout)
+
+        fut.result = result
+        return fut
 
     def close(self):
+        self.seq.close_group()
         for p in self.pools:
             p.shutdown(wait=True)

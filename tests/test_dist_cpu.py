@@ -4,6 +4,7 @@ in reference order, tracked objects) must equal the single-process oracle run of
 from __future__ import annotations
 
 import json
+import time
 import os
 import socket
 import sys
@@ -157,3 +158,78 @@ def test_all_gather_capped_gloo():
             assert mx == 23, key
             assert [[float(v) for v in g] for g in got] == expect, key
         assert res["empty"] == [[[], [], []], 0]
+
+
+def test_comm_sequencer_orders_lanes_deterministically():
+    """rpt.dist.CommSequencer: several lane threads, random delays between their slots and
+    skipped slots -- the slots are entered in ONE order, (step // L, phase, step % L), whatever
+    the timing, so every rank issues its collectives in the same order on one communicator."""
+    import random
+    import threading
+    from concurrent.futures import ThreadPoolExecutor
+
+    from rpt.dist import CommSequencer
+
+    for trial in range(5):
+        L, P, steps = 3, 6, 13
+        seq = CommSequencer(L, P)
+        log, lock = [], threading.Lock()
+        rng = random.Random(trial)
+        skip = {(s, p) for s in range(steps) for p in range(P) if rng.random() < 0.3}
+        delays = {(s, p): rng.random() * 0.002 for s in range(steps) for p in range(P)}
+
+        def run(step):
+            slots = seq.step(step)
+            try:
+                for p in range(P):
+                    time.sleep(delays[(step, p)])
+                    if (step, p) in skip:
+                        continue
+                    with slots.slot(p):
+                        with lock:
+                            log.append((step, p))
+            finally:
+                slots.close()
+
+        pools = [ThreadPoolExecutor(max_workers=1) for _ in range(L)]
+        # steps 0-4 submitted together, then a wait (closes the group {3, 4}), then the rest
+        futs = []
+        for s in range(steps):
+            seq.register(s)
+            futs.append(pools[s % L].submit(run, s))
+            if s == 4:
+                seq.close_group()
+                futs[-1].result(timeout=30)
+        seq.close_group()
+        for f in futs:
+            f.result(timeout=30)
+        groups = [(0, 3), (3, 2), (5, 3), (8, 3), (11, 2)]  # (first step, size)
+        gi = {s: k for k, (a, n) in enumerate(groups) for s in range(a, a + n)}
+        exp = sorted(((s, p) for s in range(steps) for p in range(P) if (s, p) not in skip),
+                     key=lambda sp: (gi[sp[0]], sp[1], sp[0]))
+        assert log == exp
+
+
+def test_comm_sequencer_abort_releases_waiters():
+    import threading
+
+    from rpt.dist import CommSequencer
+
+    seq = CommSequencer(2, 2)
+    seq.register(0)
+    seq.register(1)
+    err = []
+
+    def waiter():
+        try:
+            with seq.step(1).slot(0):
+                pass
+        except RuntimeError as e:
+            err.append(e)
+
+    t = threading.Thread(target=waiter)
+    t.start()
+    time.sleep(0.05)
+    seq.abort(ValueError("step 0 failed"))
+    t.join(5)
+    assert not t.is_alive() and err
