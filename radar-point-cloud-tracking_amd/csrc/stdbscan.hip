@@ -2050,7 +2050,11 @@ __global__ __launch_bounds__(kBlock) void k_init_occ_cells(const int32_t* __rest
                                                           const int32_t* __restrict__ n_occ,
                                                           int64_t cells,
                                                           int32_t* __restrict__ rep,
-                                                          unsigned long long* __restrict__ cmin) {
+                                                          unsigned long long* __restrict__ cmin,
+                                                          int32_t* __restrict__ zero_counter =
+                                                              nullptr) {
+  // the union passes' cell-list counter, zeroed here (its first user is two launches later)
+  if (zero_counter && blockIdx.x == 0 && threadIdx.x == 0) *zero_counter = 0;
   const int64_t m = *n_occ;
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m;
        q += (int64_t)gridDim.x * blockDim.x) {
@@ -2119,11 +2123,16 @@ __device__ __forceinline__ void uf_unite(int32_t* parent, const int32_t* __restr
 
 // K6a: mutual-cell x mutual-cell unions, one wave per occupied cell A, lanes over the candidate
 // cells B > A of its window (each unordered pair once).
-// PARTIAL = false: only pairs the boxes prove fully adjacent (cheap, no search).
+// PARTIAL = false: only pairs the boxes prove fully adjacent (cheap, no search).  A wave takes 64
+//                  occupied cells at a time: their headers (cell, rep, mutual) in one coalesced
+//                  round, then the mutual cells with core points one after another (half the
+//                  occupied cells of a radar stack are noise cells, each a wave's dependent load
+//                  chain otherwise).  With pmask: each cell's undecided candidates are recorded,
+//                  and the cells that have any are listed in plist (one atomic per 64 cells).
 // PARTIAL = true : undecided pairs whose roots still differ after the first pass (a kernel
 //                  boundary later, so most such pairs are already connected), searched for one
 //                  adjacent core pair: B's core points that can reach A's box, each tested
-//                  against A's points 64 at a time.
+//                  against A's points 64 at a time.  With plist: only the listed cells.
 template <int D, bool PARTIAL>
 __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict__ pts, Geom g,
                                                        const int32_t* __restrict__ cell_start,
@@ -2138,142 +2147,277 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
                                                        const int32_t* __restrict__ sorig,
                                                        int32_t* __restrict__ parent,
                                                        int uf_flags,
-                                                       uint4* __restrict__ pmask = nullptr) {
+                                                       uint4* __restrict__ pmask = nullptr,
+                                                       int32_t* __restrict__ plist = nullptr,
+                                                       int32_t* __restrict__ pcount = nullptr) {
   const int lane = threadIdx.x & 63;
   const bool halve = !(uf_flags & 1);
-  const XcdRange xr = xcd_items(*n_occ, (uf_flags & 2) != 0);
-  for (int64_t q = xr.first; q < xr.end; q += xr.step) {
-    const int ca = occ[q];
-    if ((int64_t)ca >= g.cells) continue;  // the isolated (non-finite time) cell
-    const int ra = rep[ca];
-    const uint8_t ma = mutual[ca];
-    const CellRec<D> ra_rec = crec[ca];
-    if (ra < 0 || !ma) continue;
-    const int ba = ra_rec.b, ea = ra_rec.e;  // core points anywhere in [b, e): scans start at b
-    const float4 A1 = rec_boxA<D>(ra_rec), A2 = rec_boxB(ra_rec);
-    int cx, cy, cz;
-    decode_key<D>(ca, g, cx, cy, cz);
-    // only cells B > A: slabs from A's own on (slabs are the slowest key dimension); the boxes'
-    // time ranges are checked by classify_cells, so the slab window is not shrunk first
-    const int sa = (int)((int64_t)ca / ((int64_t)g.nx * g.ny * g.nz));
-    const Window w = make_window<D, false>(cx, cy, cz, A2.z, A2.w, g, slab_t, sa);
-    // PARTIAL with the first pass's mask of this cell's undecided candidates (window positions
-    // < 127): only those are visited, no enumeration or classification of the window again
-    uint4 pm = make_uint4(0u, 0u, 0u, kPmaskFull);
-    if (PARTIAL && pmask) pm = pmask[q];
-    const bool listed = PARTIAL && !(pm.w & kPmaskFull);
-    for (int base = 0; base < w.total; base += 64 * kR) {
-      int64_t cb[kR];
-      uint32_t wb[kR];
-      int rb[kR], cls[kR], ebv[kR], bbv[kR];
-      if (listed) {
+  const int64_t no = *n_occ;
+  const bool from_list = PARTIAL && plist;
+  const int64_t items = from_list ? (int64_t)*pcount : (no + 63) / 64;
+  const XcdRange xr = xcd_items(items, (uf_flags & 2) != 0);
+  for (int64_t it = xr.first; it < xr.end; it += xr.step) {
+    int ql = -1, cal = INT_MAX, ral = -1;
+    uint8_t mal = 0;
+    if (from_list) {
+      if (lane == 0) ql = plist[it];
+    } else if (it * 64 + lane < no) {
+      ql = (int)(it * 64 + lane);
+    }
+    if (ql >= 0) cal = occ[ql];
+    if ((int64_t)cal < g.cells) {  // (not the isolated, non-finite time cell)
+      ral = rep[cal];
+      mal = mutual[cal];
+    }
+    uint64_t todo = __ballot(ral >= 0 && mal);
+    uint64_t lmask = 0;  // !PARTIAL: cells of this chunk with undecided candidates (plist)
+    while (todo) {
+      const int lq = __ffsll((unsigned long long)todo) - 1;
+      todo &= todo - 1;
+      const int64_t q = __shfl(ql, lq);
+      const int ca = __shfl(cal, lq);
+      const int ra = __shfl(ral, lq);
+      const CellRec<D> ra_rec = crec[ca];
+      const int ba = ra_rec.b, ea = ra_rec.e;  // core points anywhere in [b, e): scans start at b
+      const float4 A1 = rec_boxA<D>(ra_rec), A2 = rec_boxB(ra_rec);
+      int cx, cy, cz;
+      decode_key<D>(ca, g, cx, cy, cz);
+      // only cells B > A: slabs from A's own on (slabs are the slowest key dimension); the boxes'
+      // time ranges are checked by classify_cells, so the slab window is not shrunk first
+      const int sa = (int)((int64_t)ca / ((int64_t)g.nx * g.ny * g.nz));
+      const Window w = make_window<D, false>(cx, cy, cz, A2.z, A2.w, g, slab_t, sa);
+      // PARTIAL with the first pass's mask of this cell's undecided candidates (window positions
+      // < 127): only those are visited, no enumeration or classification of the window again
+      uint4 pm = make_uint4(0u, 0u, 0u, kPmaskFull);
+      if (PARTIAL && pmask) pm = pmask[q];
+      const bool listed = PARTIAL && !(pm.w & kPmaskFull);
+      for (int base = 0; base < w.total; base += 64 * kR) {
+        int64_t cb[kR];
+        uint32_t wb[kR];
+        int rb[kR], cls[kR], ebv[kR], bbv[kR];
+        if (listed) {
+#pragma unroll
+          for (int k = 0; k < kR; ++k) {
+            rb[k] = -1;
+            cls[k] = 0;
+            ebv[k] = 0;
+            bbv[k] = 0;
+            const uint32_t word = k == 0 ? (lane < 32 ? pm.x : pm.y) : (lane < 32 ? pm.z : pm.w);
+            if (k < 2 && ((word >> (lane & 31)) & 1u)) {
+              const int64_t c = window_cell<D>(w, k * 64 + lane, g, slab_t, A2.z, A2.w);
+              const CellRec<D> cr = crec[c];
+              rb[k] = rep[c];
+              ebv[k] = cr.e;
+              bbv[k] = cr.b;
+              cls[k] = 2;
+            }
+          }
+        } else {
+#pragma unroll
+        for (int k = 0; k < kR; ++k) {
+          const int qq = base + k * 64 + lane;
+          cb[k] = (qq < w.total) ? window_cell<D>(w, qq, g, slab_t, A2.z, A2.w) : -1;
+          if (cb[k] <= (int64_t)ca) cb[k] = -1;
+        }
+#pragma unroll
+        for (int k = 0; k < kR; ++k) wb[k] = (cb[k] >= 0) ? occ_bits[cb[k] >> 5] : 0u;
 #pragma unroll
         for (int k = 0; k < kR; ++k) {
           rb[k] = -1;
           cls[k] = 0;
           ebv[k] = 0;
           bbv[k] = 0;
-          const uint32_t word = k == 0 ? (lane < 32 ? pm.x : pm.y) : (lane < 32 ? pm.z : pm.w);
-          if (k < 2 && ((word >> (lane & 31)) & 1u)) {
-            const int64_t c = window_cell<D>(w, k * 64 + lane, g, slab_t, A2.z, A2.w);
-            const CellRec<D> cr = crec[c];
-            rb[k] = rep[c];
+          if (cb[k] >= 0 && ((wb[k] >> (cb[k] & 31)) & 1u)) {
+            const CellRec<D> cr = crec[cb[k]];
+            const int r = rep[cb[k]];
+            const uint8_t m = mutual[cb[k]];
             ebv[k] = cr.e;
             bbv[k] = cr.b;
-            cls[k] = 2;
+            if (r >= 0 && m) {
+              rb[k] = r;
+              cls[k] = classify_cells<D>(A1, rec_boxA<D>(cr), A2, rec_boxB(cr), g);
+            }
           }
         }
-      } else {
-#pragma unroll
-      for (int k = 0; k < kR; ++k) {
-        const int qq = base + k * 64 + lane;
-        cb[k] = (qq < w.total) ? window_cell<D>(w, qq, g, slab_t, A2.z, A2.w) : -1;
-        if (cb[k] <= (int64_t)ca) cb[k] = -1;
-      }
-#pragma unroll
-      for (int k = 0; k < kR; ++k) wb[k] = (cb[k] >= 0) ? occ_bits[cb[k] >> 5] : 0u;
-#pragma unroll
-      for (int k = 0; k < kR; ++k) {
-        rb[k] = -1;
-        cls[k] = 0;
-        ebv[k] = 0;
-        bbv[k] = 0;
-        if (cb[k] >= 0 && ((wb[k] >> (cb[k] & 31)) & 1u)) {
-          const CellRec<D> cr = crec[cb[k]];
-          const int r = rep[cb[k]];
-          const uint8_t m = mutual[cb[k]];
-          ebv[k] = cr.e;
-          bbv[k] = cr.b;
-          if (r >= 0 && m) {
-            rb[k] = r;
-            cls[k] = classify_cells<D>(A1, rec_boxA<D>(cr), A2, rec_boxB(cr), g);
+        }
+        if (!PARTIAL) {
+          if (pmask && base == 0) {  // the undecided candidates for the second pass
+            const uint64_t m0 = __ballot(cls[0] == 2), m1 = __ballot(cls[1] == 2);
+            if (lane == 0)
+              pmask[q] = (w.total < 128)
+                             ? make_uint4((uint32_t)m0, (uint32_t)(m0 >> 32), (uint32_t)m1,
+                                          (uint32_t)(m1 >> 32) & ~kPmaskFull)
+                             : make_uint4(0u, 0u, 0u, kPmaskFull);
+            if (w.total >= 128 || (m0 | m1)) lmask |= 1ull << lq;
           }
+          // neighbours' roots in parallel, then ONE unite per distinct root (dense regions give
+          // a dozen box-certain neighbours that mostly share a root already)
+          const int rA = uf_find(parent, ra, halve);
+#pragma unroll
+          for (int k = 0; k < kR; ++k) {
+            const int rt = (cls[k] == 1) ? uf_find(parent, rb[k], halve) : -1;
+            bool pend = rt >= 0 && rt != rA;
+            bool mine = false;
+            uint64_t pm = __ballot(pend);
+            while (pm) {
+              const int l = __ffsll((unsigned long long)pm) - 1;
+              const int v = __shfl(rt, l);
+              mine = mine || (lane == l);
+              pend = pend && (rt != v);
+              pm = __ballot(pend);
+            }
+            if (mine) uf_unite(parent, sorig, rA, rt, halve);
+          }
+          continue;
         }
-      }
-      }
-      if (!PARTIAL) {
-        if (pmask && base == 0) {  // the undecided candidates for the second pass
-          const uint64_t m0 = __ballot(cls[0] == 2), m1 = __ballot(cls[1] == 2);
-          if (lane == 0)
-            pmask[q] = (w.total < 128)
-                           ? make_uint4((uint32_t)m0, (uint32_t)(m0 >> 32), (uint32_t)m1,
-                                        (uint32_t)(m1 >> 32) & ~kPmaskFull)
-                           : make_uint4(0u, 0u, 0u, kPmaskFull);
-        }
-        // neighbours' roots in parallel, then ONE unite per distinct root (dense regions give
-        // a dozen box-certain neighbours that mostly share a root already)
-        const int rA = uf_find(parent, ra, halve);
 #pragma unroll
         for (int k = 0; k < kR; ++k) {
-          const int rt = (cls[k] == 1) ? uf_find(parent, rb[k], halve) : -1;
-          bool pend = rt >= 0 && rt != rA;
-          bool mine = false;
-          uint64_t pm = __ballot(pend);
+          const bool cand =
+              (cls[k] == 2) && uf_find(parent, ra, halve) != uf_find(parent, rb[k], halve);
+          uint64_t pm = __ballot(cand);
           while (pm) {
             const int l = __ffsll((unsigned long long)pm) - 1;
-            const int v = __shfl(rt, l);
-            mine = mine || (lane == l);
-            pend = pend && (rt != v);
-            pm = __ballot(pend);
-          }
-          if (mine) uf_unite(parent, sorig, rA, rt, halve);
-        }
-        continue;
-      }
-#pragma unroll
-      for (int k = 0; k < kR; ++k) {
-        const bool cand =
-            (cls[k] == 2) && uf_find(parent, ra, halve) != uf_find(parent, rb[k], halve);
-        uint64_t pm = __ballot(cand);
-        while (pm) {
-          const int l = __ffsll((unsigned long long)pm) - 1;
-          pm &= pm - 1;
-          const int rbl = __shfl(rb[k], l);
-          const int ebl = __shfl(ebv[k], l);
-          const int bbl = __shfl(bbv[k], l);
-          bool hit = false;
-          for (int jb0 = bbl; jb0 < ebl && !hit; jb0 += 64) {
-            const int jb = jb0 + lane;
-            float4 pb = make_float4(0.f, 0.f, 0.f, 0.f);
-            bool cb_ok = false;
-            if (jb < ebl && core[jb]) {
-              pb = pts[jb];
-              cb_ok = classify<D>(pb, A1, A2, g) != 0;
-            }
-            uint64_t bm = __ballot(cb_ok);
-            while (bm && !hit) {
-              const int lb = __ffsll((unsigned long long)bm) - 1;
-              bm &= bm - 1;
-              const float4 pq = shfl_f4(pb, lb);
-              for (int ja0 = ba; ja0 < ea && !hit; ja0 += 64) {
-                const int ja = ja0 + lane;
-                const bool adj = (ja < ea) && core[ja] && adjacent<D>(pq, pts[ja], g);
-                hit = __ballot(adj) != 0;
+            pm &= pm - 1;
+            const int rbl = __shfl(rb[k], l);
+            const int ebl = __shfl(ebv[k], l);
+            const int bbl = __shfl(bbv[k], l);
+            bool hit = false;
+            for (int jb0 = bbl; jb0 < ebl && !hit; jb0 += 64) {
+              const int jb = jb0 + lane;
+              float4 pb = make_float4(0.f, 0.f, 0.f, 0.f);
+              bool cb_ok = false;
+              if (jb < ebl && core[jb]) {
+                pb = pts[jb];
+                cb_ok = classify<D>(pb, A1, A2, g) != 0;
+              }
+              uint64_t bm = __ballot(cb_ok);
+              while (bm && !hit) {
+                const int lb = __ffsll((unsigned long long)bm) - 1;
+                bm &= bm - 1;
+                const float4 pq = shfl_f4(pb, lb);
+                for (int ja0 = ba; ja0 < ea && !hit; ja0 += 64) {
+                  const int ja = ja0 + lane;
+                  const bool adj = (ja < ea) && core[ja] && adjacent<D>(pq, pts[ja], g);
+                  hit = __ballot(adj) != 0;
+                }
               }
             }
+            if (hit && lane == 0) uf_unite(parent, sorig, ra, rbl, halve);
           }
-          if (hit && lane == 0) uf_unite(parent, sorig, ra, rbl, halve);
         }
+      }
+    }
+    if (!PARTIAL && plist && lmask) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(pcount, __popcll(lmask));
+      base = __shfl(base, 0);
+      if ((lmask >> lane) & 1ull) plist[base + __popcll(lmask & ((1ull << lane) - 1ull))] = ql;
+    }
+  }
+}
+
+// K6b over the first pass's cell list (2-D): one wave per listed cell, lane l over window
+// positions l and l + 64 of its pmask (a window of >= 128 positions is walked 64 positions at a
+// time instead, classifying again), then k_union_cells<D, true>'s search for each undecided
+// pair whose roots still differ.  Without the kR-wide enumeration the kernel holds far fewer
+// registers than k_union_cells<2, true> (twice the waves per SIMD: the pass is a chain of
+// dependent loads per cell).
+__global__ __launch_bounds__(kBlock) void k_union_listed(const float4* __restrict__ pts, Geom g,
+                                                        const int32_t* __restrict__ occ,
+                                                        const CellRec<2>* __restrict__ crec,
+                                                        const uint32_t* __restrict__ occ_bits,
+                                                        const float2* __restrict__ slab_t,
+                                                        const uint8_t* __restrict__ core,
+                                                        const int32_t* __restrict__ rep,
+                                                        const uint8_t* __restrict__ mutual,
+                                                        const int32_t* __restrict__ sorig,
+                                                        int32_t* __restrict__ parent, int uf_flags,
+                                                        const uint4* __restrict__ pmask,
+                                                        const int32_t* __restrict__ plist,
+                                                        const int32_t* __restrict__ pcount) {
+  const int lane = threadIdx.x & 63;
+  const bool halve = !(uf_flags & 1);
+  const XcdRange xr = xcd_items(*pcount, false);
+  for (int64_t i = xr.first; i < xr.end; i += xr.step) {
+    const int q = plist[i];
+    const int ca = occ[q];
+    const int ra = rep[ca];
+    const uint4 pm = pmask[q];
+    const CellRec<2> ra_rec = crec[ca];
+    const int ba = ra_rec.b, ea = ra_rec.e;
+    const float4 A1 = rec_boxA<2>(ra_rec), A2 = rec_boxB(ra_rec);
+    int cx, cy, cz;
+    decode_key<2>(ca, g, cx, cy, cz);
+    const int sa = (int)((int64_t)ca / ((int64_t)g.nx * g.ny));
+    const Window w = make_window<2, false>(cx, cy, cz, A2.z, A2.w, g, slab_t, sa);
+    // the undecided candidate of this lane (rb >= 0) -> one adjacent core pair unites A and B
+    auto settle = [&](int rb, int bb, int eb) {
+      const bool cand = rb >= 0 && uf_find(parent, ra, halve) != uf_find(parent, rb, halve);
+      uint64_t cm = __ballot(cand);
+      while (cm) {
+        const int l = __ffsll((unsigned long long)cm) - 1;
+        cm &= cm - 1;
+        const int rbl = __shfl(rb, l);
+        const int ebl = __shfl(eb, l);
+        const int bbl = __shfl(bb, l);
+        bool hit = false;
+        for (int jb0 = bbl; jb0 < ebl && !hit; jb0 += 64) {
+          const int jb = jb0 + lane;
+          float4 pb = make_float4(0.f, 0.f, 0.f, 0.f);
+          bool cb_ok = false;
+          if (jb < ebl && core[jb]) {
+            pb = pts[jb];
+            cb_ok = classify<2>(pb, A1, A2, g) != 0;
+          }
+          uint64_t bm = __ballot(cb_ok);
+          while (bm && !hit) {
+            const int lb = __ffsll((unsigned long long)bm) - 1;
+            bm &= bm - 1;
+            const float4 pq = shfl_f4(pb, lb);
+            for (int ja0 = ba; ja0 < ea && !hit; ja0 += 64) {
+              const int ja = ja0 + lane;
+              const bool adj = (ja < ea) && core[ja] && adjacent<2>(pq, pts[ja], g);
+              hit = __ballot(adj) != 0;
+            }
+          }
+        }
+        if (hit && lane == 0) uf_unite(parent, sorig, ra, rbl, halve);
+      }
+    };
+    if (!(pm.w & kPmaskFull)) {
+      int rb[2], ebv[2], bbv[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        rb[k] = -1;
+        ebv[k] = bbv[k] = 0;
+        const uint32_t word = k == 0 ? (lane < 32 ? pm.x : pm.y) : (lane < 32 ? pm.z : pm.w);
+        if ((word >> (lane & 31)) & 1u) {
+          const int64_t c = window_cell<2>(w, k * 64 + lane, g, slab_t, A2.z, A2.w);
+          const CellRec<2> cr = crec[c];
+          rb[k] = rep[c];
+          ebv[k] = cr.e;
+          bbv[k] = cr.b;
+        }
+      }
+      settle(rb[0], bbv[0], ebv[0]);
+      settle(rb[1], bbv[1], ebv[1]);
+    } else {
+      for (int base = 0; base < w.total; base += 64) {
+        const int qq = base + lane;
+        int64_t c = (qq < w.total) ? window_cell<2>(w, qq, g, slab_t, A2.z, A2.w) : -1;
+        if (c <= (int64_t)ca || !((occ_bits[c >> 5] >> (c & 31)) & 1u)) c = -1;
+        int rb = -1, bb = 0, eb = 0;
+        if (c >= 0) {
+          const CellRec<2> cr = crec[c];
+          const int r = rep[c];
+          if (r >= 0 && mutual[c] &&
+              classify_cells<2>(A1, rec_boxA<2>(cr), A2, rec_boxB(cr), g) == 2) {
+            rb = r;
+            bb = cr.b;
+            eb = cr.e;
+          }
+        }
+        settle(rb, bb, eb);
       }
     }
   }
@@ -2502,8 +2646,10 @@ __global__ __launch_bounds__(kBlock) void k_cell_min_key(const int32_t* __restri
 // GLOBAL = false: key = ccmin (component-min original index, local run), label = cid[key];
 // GLOBAL = true : key = slab (the core point's final label: labels are ranks of the sorted global
 //                 representatives, so the smallest label is the smallest representative).
-template <int D, bool GLOBAL>
+template <int D, bool GLOBAL, int W = 64>
 // 7 waves/SIMD (72 VGPRs, one spill): 80 VGPRs left it at 6 and latency-bound (-2 %)
+// W = 32: two points per wave, one per half (the same candidate loads per point, twice the
+// points in flight: the pass is a chain of dependent loads per point, not bandwidth)
 __global__ __launch_bounds__(kBlock, 7) void k_label(const float4* __restrict__ pts,
                                                  const int32_t* __restrict__ skey, Geom g,
                                                  const CellRec<D>* __restrict__ crec,
@@ -2517,10 +2663,28 @@ __global__ __launch_bounds__(kBlock, 7) void k_label(const float4* __restrict__ 
                                                  const int32_t* __restrict__ nc_list,
                                                  const int32_t* __restrict__ nc_count,
                                                  int32_t* __restrict__ labels) {
+  static_assert(W == 32 || W == 64, "a point per wave or per half-wave");
+  constexpr int P = 64 / W;  // points per wave
   const int lane = threadIdx.x & 63;
+  const int hl = lane & (W - 1);      // lane within the point's group
+  const int h0 = lane - hl;           // the group's first lane
+  const int shift = (W == 64) ? 0 : h0;
+  // the group's bits of a wave ballot
+  auto gbal = [&](bool v) -> uint64_t {
+    const uint64_t b = __ballot(v);
+    return (W == 64) ? b : ((b >> shift) & 0xffffffffull);
+  };
+  auto gmin = [&](int v) -> int {
+#pragma unroll
+    for (int off = W / 2; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off));
+    return v;
+  };
+  const int64_t nc = *nc_count;
   // XCD-aware ranges of the (cell-ordered) queue: neighbouring points' windows share an L2
-  const XcdRange xr = xcd_items(*nc_count, true);
-  for (int64_t q = xr.first; q < xr.end; q += xr.step) {
+  const XcdRange xr = xcd_items((nc + P - 1) / P, true);
+  for (int64_t qp = xr.first; qp < xr.end; qp += xr.step) {
+    const int64_t q = qp * P + (lane / W);
+    if (q >= nc) continue;  // (group-uniform)
     const int s = nc_list[q];
     const int32_t key = skey[s];
     int best = INT_MAX;
@@ -2532,12 +2696,12 @@ __global__ __launch_bounds__(kBlock, 7) void k_label(const float4* __restrict__ 
       // super-rounds of kR candidates per lane, loads of one kind issued together: the cells'
       // smallest keys (empty cells hold INT_MAX, so no occupancy lookup), then the records of
       // the cells with core points -- two dependent rounds per super-round
-      for (int base = 0; base < w.total; base += 64 * kR) {
+      for (int base = 0; base < w.total; base += W * kR) {
         int64_t c[kR];
         int ck[kR], cb[kR], ce[kR], cls[kR], mu[kR];
 #pragma unroll
         for (int k = 0; k < kR; ++k) {
-          const int qq = base + k * 64 + lane;
+          const int qq = base + k * W + hl;
           c[k] = (qq < w.total) ? window_cell<D>(w, qq, g, slab_t, p.w, p.w) : -1;
         }
 #pragma unroll
@@ -2555,9 +2719,7 @@ __global__ __launch_bounds__(kBlock, 7) void k_label(const float4* __restrict__ 
             if (cls[k] == 1) v = min(v, ck[k]);
           }
         }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off));
-        best = min(best, v);
+        best = min(best, gmin(v));
         // the partially reachable cells, smallest key first, while a key can still win
         uint32_t pend = 0;
 #pragma unroll
@@ -2570,12 +2732,10 @@ __global__ __launch_bounds__(kBlock, 7) void k_label(const float4* __restrict__ 
               mine = ck[k];
               mk = k;
             }
-          int mm = mine;
-#pragma unroll
-          for (int off = 32; off > 0; off >>= 1) mm = min(mm, __shfl_xor(mm, off));
+          const int mm = gmin(mine);
           if (mm == INT_MAX) break;
-          const uint64_t at = __ballot(mine == mm);
-          const int l = __ffsll((unsigned long long)at) - 1;
+          const uint64_t at = gbal(mine == mm);
+          const int l = h0 + __ffsll((unsigned long long)at) - 1;
           const int kl = __shfl(mk, l);
           int bsel = 0, esel = 0, msel = 0;
 #pragma unroll
@@ -2589,28 +2749,26 @@ __global__ __launch_bounds__(kBlock, 7) void k_label(const float4* __restrict__ 
           const int bl = __shfl(bsel, l), el = __shfl(esel, l);
           if (__shfl(msel, l)) {  // one component: a single adjacent core point decides
             bool hit = false;
-            for (int j0 = bl; j0 < el && !hit; j0 += 64) {
-              const int j = j0 + lane;
-              hit = __ballot((j < el) && key_of[j] >= 0 && adjacent<D>(p, pts[j], g)) != 0;
+            for (int j0 = bl; j0 < el && !hit; j0 += W) {
+              const int j = j0 + hl;
+              hit = gbal((j < el) && key_of[j] >= 0 && adjacent<D>(p, pts[j], g)) != 0;
             }
             if (hit) best = mm;
           } else {
             int lb = INT_MAX;
-            for (int j0 = bl; j0 < el; j0 += 64) {
-              const int j = j0 + lane;
+            for (int j0 = bl; j0 < el; j0 += W) {
+              const int j = j0 + hl;
               if (j < el) {
                 const int m = key_of[j];
                 if (m >= 0 && m < best && m < lb && adjacent<D>(p, pts[j], g)) lb = m;
               }
             }
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) lb = min(lb, __shfl_xor(lb, off));
-            best = min(best, lb);
+            best = min(best, gmin(lb));
           }
         }
       }
     }
-    if (lane == 0) {
+    if (hl == 0) {
       int32_t out = -1;
       if (best != INT_MAX) out = GLOBAL ? best : cid[best];
       labels[sorig[s]] = out;
@@ -3324,6 +3482,23 @@ struct DbscanState {
   unsigned tile_grid_blocks() const {  // the tiles + the isolated cell's, a multiple of 8
     return (unsigned)((((int64_t)g.nt * tile_nbands + 1) + 7) & ~(int64_t)7);
   }
+  // slabs each side a cell's points can reach: eps_t / slab width, +1 for the slab's extent;
+  // integral times with integral slab widths: a slab holds whole time values, so ceil(floor(eps_t)
+  // / width) slabs each side hold every time within eps_t
+  double slab_reach() const {
+    return integral_t ? std::ceil(std::floor((double)g.epst) / g.ct)
+                      : std::ceil((double)g.epst / g.ct) + 1.0;
+  }
+  // the eight-lanes-per-cell K5 / K6 kernels (2-D, at most kCwMaxR slabs each side)
+  bool oct_ok() const { return dim == 2 && g.nz == 1 && slab_reach() <= (double)kCwMaxR; }
+  int k7_w = -1;  // lanes per non-core point in k_label (32: two points per wave); RPT_K7_W
+  int label_w() {
+    if (k7_w < 0) {
+      const char* e = ab_env("RPT_K7_W");
+      k7_w = (e && std::atoi(e) == 64) ? 64 : 32;
+    }
+    return k7_w;
+  }
   int bucket_mode = -1;                      // RPT_K4_BUCKET (default 1): slab-bucket K4
   template <int D>
   const CellRec<D>* rec() const {
@@ -3646,12 +3821,8 @@ int32_t DbscanState::core_pass(hipStream_t st) {
     k5_legacy = (k5_legacy == 0) ? 1 : 0;
     k5_fill = (e && std::atoi(e) == 2) ? 1 : 0;
   }
-  // slabs each side a cell's points can reach: eps_t / slab width, +1 for the slab's extent;
-  // integral times with integral slab widths: a slab holds whole time values, so ceil(floor(eps_t)
-  // / width) slabs each side hold every time within eps_t
-  const double rs = integral_t ? std::ceil(std::floor((double)g.epst) / g.ct)
-                               : std::ceil((double)g.epst / g.ct) + 1.0;
-  const bool oct = dim == 2 && rs <= (double)kCwMaxR && g.nz == 1;
+  const double rs = slab_reach();
+  const bool oct = oct_ok();
   if (k5_tiles < 0) {  // RPT_K5_TILES=1: the LDS-tile pass (k_core_tiles; measured slower)
     const char* e = ab_env("RPT_K5_TILES");
     k5_tiles = (e && std::atoi(e) == 1) ? 1 : 0;
@@ -3758,23 +3929,34 @@ int32_t DbscanState::union_pass(hipStream_t st) {
   (void)gc;
   // per-cell (min original index, sorted index) of the core points, one u64 per cell
   auto* cmin = reinterpret_cast<unsigned long long*>(cell_min_pair);
-  hipLaunchKernelGGL(k_init_occ_cells, dim3(gb), dim3(kBlock), 0, st, occ, n_occ, C, rep, cmin);
-  hipLaunchKernelGGL(k_cell_min_pair, dim3(gb), dim3(kBlock), 0, st, skey, core, sorig, n, C,
-                     cmin);
-  hipLaunchKernelGGL(k_parent_init_pair, dim3(gb), dim3(kBlock), 0, st, parent, n, core, skey,
-                     mutual, cmin, C, rep);
   if (union_list < 0) {
     const char* e = ab_env("RPT_UNION_LIST");
     union_list = (e && std::atoi(e) == 0) ? 0 : 1;
   }
+  // 2-D: the first union pass lists its cells with undecided candidates in nc_list (free until
+  // the label pass), their count at nc_list[n] (zeroed by k_init_occ_cells)
+  const bool listing = union_list && dim == 2;
+  int32_t* plist = listing ? nc_list : nullptr;
+  int32_t* pcount = listing ? nc_list + n : nullptr;
+  hipLaunchKernelGGL(k_init_occ_cells, dim3(gb), dim3(kBlock), 0, st, occ, n_occ, C, rep, cmin,
+                     pcount);
+  hipLaunchKernelGGL(k_cell_min_pair, dim3(gb), dim3(kBlock), 0, st, skey, core, sorig, n, C,
+                     cmin);
+  hipLaunchKernelGGL(k_parent_init_pair, dim3(gb), dim3(kBlock), 0, st, parent, n, core, skey,
+                     mutual, cmin, C, rep);
   if (dim == 2) {
-    uint4* pm = union_list ? pmask : nullptr;
+    uint4* pm = listing ? pmask : nullptr;
     hipLaunchKernelGGL((k_union_cells<2, false>), dim3(gw), dim3(kBlock), 0, st, pts, g,
                        cell_start, occ, n_occ, rec<2>(), occ_bits, slab_t, core, rep, mutual, sorig,
-                       parent, uf_flags, pm);
-    hipLaunchKernelGGL((k_union_cells<2, true>), dim3(gw), dim3(kBlock), 0, st, pts, g,
-                       cell_start, occ, n_occ, rec<2>(), occ_bits, slab_t, core, rep, mutual, sorig,
-                       parent, uf_flags, pm);
+                       parent, uf_flags, pm, plist, pcount);
+    if (listing)
+      hipLaunchKernelGGL(k_union_listed, dim3(gw), dim3(kBlock), 0, st, pts, g, occ, rec<2>(),
+                         occ_bits, slab_t, core, rep, mutual, sorig, parent, uf_flags, pm, plist,
+                         pcount);
+    else
+      hipLaunchKernelGGL((k_union_cells<2, true>), dim3(gw), dim3(kBlock), 0, st, pts, g,
+                         cell_start, occ, n_occ, rec<2>(), occ_bits, slab_t, core, rep, mutual,
+                         sorig, parent, uf_flags, pm, plist, pcount);
     hipLaunchKernelGGL(k_union<2>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
                        boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
   } else {
@@ -3847,11 +4029,13 @@ int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hi
                        n_occ_dev, rowq, rec<2>(), mutual, occ_bits, slab_t, pts, ccmin, cell_min,
                        sorig, mr, min_samples, labels);
   else if (dim == 2)
-    hipLaunchKernelGGL((k_label<2, false>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
+    hipLaunchKernelGGL(label_w() == 32 ? (k_label<2, false, 32>) : (k_label<2, false, 64>),
+                       dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
                        rec<2>(), occ_bits, slab_t, ccmin, cell_min, mutual, sorig, mr, nc_list,
                        nc_count, labels);
   else
-    hipLaunchKernelGGL((k_label<3, false>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
+    hipLaunchKernelGGL((k_label<3, false, 64>),
+                       dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
                        rec<3>(), occ_bits, slab_t, ccmin, cell_min, mutual, sorig, mr, nc_list,
                        nc_count, labels);
   RPT_CHECK_LAUNCH();
@@ -3915,11 +4099,13 @@ int32_t DbscanState::labels_global(const int64_t* rep_orig, const int64_t* reps,
                        n_occ_dev, rowq, rec<2>(), mutual, occ_bits, slab_t, pts, slab, cell_min,
                        sorig, MinRank{nullptr, nullptr}, min_samples, labels);
   else if (dim == 2)
-    hipLaunchKernelGGL((k_label<2, true>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
+    hipLaunchKernelGGL(label_w() == 32 ? (k_label<2, true, 32>) : (k_label<2, true, 64>),
+                       dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
                        rec<2>(), occ_bits, slab_t, slab, cell_min, mutual, sorig,
                        MinRank{nullptr, nullptr}, nc_list, nc_count, labels);
   else
-    hipLaunchKernelGGL((k_label<3, true>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
+    hipLaunchKernelGGL((k_label<3, true, 64>),
+                       dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
                        rec<3>(), occ_bits, slab_t, slab, cell_min, mutual, sorig,
                        MinRank{nullptr, nullptr}, nc_list, nc_count, labels);
   RPT_CHECK_LAUNCH();

@@ -51,6 +51,8 @@ for seed in range(4):
     CASES.append(("floattime", seed))
 for seed in range(4):
     CASES.append(("lattice", seed))
+for seed in range(4):
+    CASES.append(("widetime2d", seed))
 
 
 def _make(kind, seed):
@@ -84,6 +86,12 @@ def _make(kind, seed):
         t = rng.integers(0, 4, len(c)).astype(np.float32)
         return c, t, float(rng.choice([1.0, 2.0, 3.0])), float(rng.choice([0.0, 1.0])), \
             int(rng.choice([2, 3, 5, 7]))
+    if kind == "widetime2d":  # forward slab windows of >= 128 cells (the union passes' walk)
+        F = int(rng.integers(12, 30))
+        c, t = _blobs(rng, F, int(rng.integers(3, 10)), int(rng.integers(10, 60)), 60,
+                      spread=2.5)
+        return c, t, float(rng.choice([5.0, 8.0])), float(rng.choice([4.0, 6.0, 9.0])), \
+            int(rng.choice([10, 30, 60]))
     raise ValueError(kind)
 
 
