@@ -2528,15 +2528,18 @@ __global__ __launch_bounds__(kBlock) void k_cell_roots(int32_t* parent,
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m;
        q += (int64_t)gridDim.x * blockDim.x) {
     const int32_t c = occ[q];
-    if ((int64_t)c >= cells || !mutual[c]) continue;
-    const int r = rep[c];
-    if (r >= 0) cell_root[c] = uf_find(parent, r);
+    if ((int64_t)c >= cells) continue;
+    const int r = mutual[c] ? rep[c] : -1;
+    cell_root[c] = (r >= 0) ? uf_find(parent, r) : -1;  // -1: walk each point's own chain
   }
 }
 
-// cell_root (nullable): k_cell_roots' output, read for core points of mutual cells (skey, mutual).
+// cell_root (nullable): k_cell_roots' output (-1: not a mutual cell with core points), read for
+// core points through skey.
 // cell_key (nullable, pre-filled with INT_MAX): per cell the smallest component key among its
 // core points, by a segmented wave minimum over the sorted points (k_cell_min_key fused in).
+// The kItems points of a thread go through the dependent loads level by level (keys + flags,
+// cell roots, component minima), each level's loads in flight together; the atomics come last.
 __global__ __launch_bounds__(kBlock) void k_ccmin(int32_t* parent,
                                                  const uint8_t* __restrict__ core, int64_t n,
                                                  const int32_t* __restrict__ sorig,
@@ -2550,43 +2553,57 @@ __global__ __launch_bounds__(kBlock) void k_ccmin(int32_t* parent,
                                                  int64_t cells = 0,
                                                  int32_t* __restrict__ cell_key = nullptr) {
   const int lane = threadIdx.x & 63;
+  (void)mutual;
   for (int64_t tile = (int64_t)blockIdx.x * kBlock * kItems; tile < n;
        tile += (int64_t)gridDim.x * kBlock * kItems) {
-    uint32_t bits = 0;
+    int32_t key[kItems], x[kItems];
+    uint32_t cbits = 0, inb = 0;
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
       const int64_t s = tile + (int64_t)k * kBlock + threadIdx.x;
-      const bool in = s < n;
-      const int32_t key = (in && skey) ? skey[s] : -1;
-      int m = -1;
-      if (in) {
-        if (!core[s]) {
-          ccmin[s] = -1;
-          bits |= 1u << k;
-        } else {
-          int x;
-          if (cell_root && (int64_t)key < cells && key >= 0 && mutual[key])
-            x = cell_root[key];
-          else
-            x = uf_find(parent, (int)s);
-          m = sorig[x];
-          ccmin[s] = m;
-          if (x == (int)s) atomicOr(min_bits + (m >> 5), 1u << (m & 31));
-        }
+      key[k] = -1;
+      if (s < n) {
+        inb |= 1u << k;
+        if (skey) key[k] = skey[s];
+        if (core[s]) cbits |= 1u << k;
       }
-      if (cell_key) {  // kernel-uniform: every lane of the wave takes part
-        int v = (m >= 0 && (int64_t)key < cells) ? m : INT_MAX;
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      x[k] = -1;
+      if (((cbits >> k) & 1u) && cell_root && key[k] >= 0 && (int64_t)key[k] < cells)
+        x[k] = cell_root[key[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const int s = (int)(tile + (int64_t)k * kBlock + threadIdx.x);
+      if (((cbits >> k) & 1u) && x[k] < 0) x[k] = uf_find(parent, s);
+    }
+    int m[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) m[k] = ((cbits >> k) & 1u) ? sorig[x[k]] : -1;
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const int64_t s = tile + (int64_t)k * kBlock + threadIdx.x;
+      if ((inb >> k) & 1u) ccmin[s] = m[k];
+      if (((cbits >> k) & 1u) && x[k] == (int)s) atomicOr(min_bits + (m[k] >> 5), 1u << (m[k] & 31));
+    }
+    if (cell_key) {  // kernel-uniform: every lane of the wave takes part
+#pragma unroll
+      for (int k = 0; k < kItems; ++k) {
+        int v = (m[k] >= 0 && (int64_t)key[k] < cells) ? m[k] : INT_MAX;
+        const int kk = key[k];
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {  // sorted keys: equal at distance off = run
           const int ov = __shfl_up(v, off, 64);
-          const int ok = __shfl_up(key, off, 64);
-          if (lane >= off && ok == key) v = min(v, ov);
+          const int ok = __shfl_up(kk, off, 64);
+          if (lane >= off && ok == kk) v = min(v, ov);
         }
-        const int next = __shfl_down(key, 1, 64);
-        if ((lane == 63 || next != key) && key >= 0 && v != INT_MAX) atomicMin(cell_key + key, v);
+        const int next = __shfl_down(kk, 1, 64);
+        if ((lane == 63 || next != kk) && kk >= 0 && v != INT_MAX) atomicMin(cell_key + kk, v);
       }
     }
-    block_append_bits(tile, bits, nc_list, nc_count);
+    block_append_bits(tile, inb & ~cbits, nc_list, nc_count);
   }
 }
 
