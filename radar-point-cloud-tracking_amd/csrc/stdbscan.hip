@@ -756,7 +756,9 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ 
                                                     float4* __restrict__ boxA,
                                                     float4* __restrict__ boxB,
                                                     uint8_t* __restrict__ mutual,
-                                                    CellRec<D>* __restrict__ crec) {
+                                                    CellRec<D>* __restrict__ crec,
+                                                    unsigned long long* __restrict__ cmin =
+                                                        nullptr) {
   const int j = threadIdx.x & 7;
   const int64_t no = *n_occ;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t - j < no * 8;
@@ -827,6 +829,7 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ 
       }
       const float dt = t1 - t0;
       mutual[c] = (d2 <= g.eps2 && dt <= g.epst) ? 1 : 0;
+      if (cmin) cmin[c] = ~0ull;  // the core pass's per-cell minima (k_core_fill, k_core_slow)
     }
   }
 }
@@ -1469,12 +1472,20 @@ __global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
 // Level 3, one thread per point: the cell's decision; points of undecided cells are queued for
 // level 4 (block-aggregated append; QUEUE = false: the undecided cells are left to
 // k_core_slow_cells).
+// cmin (nullable, ~0 for the occupied cells): the union's per-cell (min original, sorted) pair
+// of the core points (k_cell_min_pair folded in): all-core cells here, by a segmented wave
+// minimum over the sorted points; the undecided cells' core points in k_core_slow.
 template <bool QUEUE>
 __global__ __launch_bounds__(kBlock) void k_core_fill(const int32_t* __restrict__ skey, int64_t n,
                                                      const int32_t* __restrict__ cflag,
                                                      uint8_t* __restrict__ core,
                                                      int32_t* __restrict__ slow,
-                                                     int32_t* __restrict__ n_slow) {
+                                                     int32_t* __restrict__ n_slow,
+                                                     const int32_t* __restrict__ sorig = nullptr,
+                                                     unsigned long long* __restrict__ cmin =
+                                                         nullptr,
+                                                     int64_t cells = 0) {
+  const int lane = threadIdx.x & 63;
   for (int64_t tile = (int64_t)blockIdx.x * kBlock * kItems; tile < n;
        tile += (int64_t)gridDim.x * kBlock * kItems) {
     // all keys, then all cell flags, in flight together (two rounds of memory latency per tile,
@@ -1495,6 +1506,32 @@ __global__ __launch_bounds__(kBlock) void k_core_fill(const int32_t* __restrict_
       if (s < n) core[s] = (f[k] == 1) ? 1 : 0;
       bits |= (f[k] == 2) ? (1u << k) : 0u;
     }
+    if (cmin) {  // kernel-uniform
+      uint32_t so[kItems];
+#pragma unroll
+      for (int k = 0; k < kItems; ++k) {
+        const int64_t s = tile + (int64_t)k * kBlock + threadIdx.x;
+        so[k] = (f[k] == 1 && s < n) ? (uint32_t)sorig[s] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < kItems; ++k) {
+        const int64_t s = tile + (int64_t)k * kBlock + threadIdx.x;
+        const int kk = key[k];
+        uint64_t v = (f[k] == 1 && kk >= 0 && (int64_t)kk < cells)
+                         ? (((uint64_t)so[k] << 32) | (uint32_t)s)
+                         : ~0ull;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {  // sorted keys: equal at distance off = same run
+          const uint32_t olo = (uint32_t)__shfl_up((int)(uint32_t)v, off, 64);
+          const uint32_t ohi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), off, 64);
+          const int ok = __shfl_up(kk, off, 64);
+          if (lane >= off && ok == kk) v = min(v, ((uint64_t)ohi << 32) | olo);
+        }
+        const int next = __shfl_down(kk, 1, 64);
+        if ((lane == 63 || next != kk) && kk >= 0 && v != ~0ull)
+          atomicMin(cmin + kk, (unsigned long long)v);
+      }
+    }
     if (QUEUE) block_append_bits(tile, bits, slow, n_slow);
   }
 }
@@ -1511,7 +1548,10 @@ __global__ __launch_bounds__(kBlock, 8) void k_core_slow(const float4* __restric
                                                      const float2* __restrict__ slab_t,
                                                      const int32_t* __restrict__ slow,
                                                      const int32_t* __restrict__ n_slow,
-                                                     uint8_t* __restrict__ core) {
+                                                     uint8_t* __restrict__ core,
+                                                     const int32_t* __restrict__ sorig = nullptr,
+                                                     unsigned long long* __restrict__ cmin =
+                                                         nullptr) {
   const int lane = threadIdx.x & 63;
   const int need = g.min_samples;
   // XCD-aware ranges of the (cell-ordered) queue: neighbouring points' windows share an L2
@@ -1566,7 +1606,11 @@ __global__ __launch_bounds__(kBlock, 8) void k_core_slow(const float4* __restric
         }
       }
     }
-    if (lane == 0) core[s] = (cnt >= need) ? 1 : 0;
+    if (lane == 0) {
+      core[s] = (cnt >= need) ? 1 : 0;
+      if (cmin && cnt >= need && (int64_t)key < g.cells)
+        atomicMin(cmin + key, ((unsigned long long)(uint32_t)sorig[s] << 32) | (uint32_t)s);
+    }
   }
 }
 
@@ -2061,7 +2105,7 @@ __global__ __launch_bounds__(kBlock) void k_init_occ_cells(const int32_t* __rest
     const int32_t c = occ[q];
     if ((int64_t)c < cells) {
       rep[c] = -1;
-      cmin[c] = ~0ull;
+      if (cmin) cmin[c] = ~0ull;
     }
   }
 }
@@ -3467,6 +3511,7 @@ struct DbscanState {
   int32_t *occ = nullptr, *hpos = nullptr;  // occupied cells (ascending), head-flag scan
   const int32_t* n_occ_dev = nullptr;        // the occupied-cell count (hpos[n] or the slab scan's)
   uint64_t* cell_min_pair = nullptr;         // per cell (min core original index, its sorted index)
+  bool cmin_ready = false;  // cell_min_pair filled by the core pass for the current core flags
   void* crec = nullptr;                      // CellRec<dim>[C + 1]
   uint32_t* occ_bits = nullptr;              // 1 bit per cell
   uint4* pmask = nullptr;  // union passes' undecided-candidate masks per occupied cell (aliases
@@ -3796,7 +3841,8 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
     n_occ_dev = hpos + n;
   }
   hipLaunchKernelGGL(k_cell_box<D>, dim3(grid_for(8 * n, kBlock, 8192)), dim3(kBlock), 0, st,
-                     pts, cell_start, occ, n_occ_dev, g, boxA, boxB, mutual, cr);
+                     pts, cell_start, occ, n_occ_dev, g, boxA, boxB, mutual, cr,
+                     reinterpret_cast<unsigned long long*>(cell_min_pair));
   RPT_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_slab_range<D>, dim3((unsigned)nt), dim3(kBlock), 0, st, cr, occ, hpos,
                      cell_start, (int64_t)(C / nt), (int)nt, slab_t, bucket ? occ_base : nullptr);
@@ -3819,6 +3865,7 @@ int32_t DbscanState::build(const float* x, const float* y, const float* z, int64
 }
 
 int32_t DbscanState::core_pass(hipStream_t st) {
+  cmin_ready = false;
   if (degenerate) return RPT_OK;
   // cflag lives in rep (int32 per cell, rebuilt by union_pass); the cell queue in ccmin and the
   // point queue in nc_list (both rebuilt later), counters in cid[n] / nc_list[n]
@@ -3903,6 +3950,8 @@ int32_t DbscanState::core_pass(hipStream_t st) {
     tm.mark();
     return RPT_OK;
   }
+  // oct: the union's per-cell minima (cell_min_pair) come out of the fill and slow passes
+  auto* cm = oct ? reinterpret_cast<unsigned long long*>(cell_min_pair) : nullptr;
   if (oct) {
     hipLaunchKernelGGL(k_core_cells_oct, dim3((grid_for(8 * n, kBlock, 8192) + 7) & ~7), dim3(kBlock), 0,
                        st, g, (int)rs, occ, n_occ, rec<2>(), mutual, occ_bits, slab_t, cflag,
@@ -3920,14 +3969,15 @@ int32_t DbscanState::core_pass(hipStream_t st) {
                          rec<3>(), occ_bits, slab_t, cq, n_cq, cflag);
   }
   hipLaunchKernelGGL(k_core_fill<true>, dim3(tile_grid(n)), dim3(kBlock), 0, st, skey, n, cflag,
-                     core, slow, n_slow);
+                     core, slow, n_slow, sorig, cm, C);
   if (dim == 2)
     hipLaunchKernelGGL(k_core_slow<2>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<2>(), occ_bits, slab_t, slow, n_slow, core);
+                       rec<2>(), occ_bits, slab_t, slow, n_slow, core, sorig, cm);
   else
     hipLaunchKernelGGL(k_core_slow<3>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
                        rec<3>(), occ_bits, slab_t, slow, n_slow, core);
   RPT_CHECK_LAUNCH();
+  cmin_ready = cm != nullptr;
   tm.mark();
   return RPT_OK;
 }
@@ -3955,10 +4005,12 @@ int32_t DbscanState::union_pass(hipStream_t st) {
   const bool listing = union_list && dim == 2;
   int32_t* plist = listing ? nc_list : nullptr;
   int32_t* pcount = listing ? nc_list + n : nullptr;
-  hipLaunchKernelGGL(k_init_occ_cells, dim3(gb), dim3(kBlock), 0, st, occ, n_occ, C, rep, cmin,
-                     pcount);
-  hipLaunchKernelGGL(k_cell_min_pair, dim3(gb), dim3(kBlock), 0, st, skey, core, sorig, n, C,
-                     cmin);
+  // the per-cell minima: from the core pass (cmin_ready) or from the final core flags here
+  hipLaunchKernelGGL(k_init_occ_cells, dim3(gb), dim3(kBlock), 0, st, occ, n_occ, C, rep,
+                     cmin_ready ? nullptr : cmin, pcount);
+  if (!cmin_ready)
+    hipLaunchKernelGGL(k_cell_min_pair, dim3(gb), dim3(kBlock), 0, st, skey, core, sorig, n, C,
+                       cmin);
   hipLaunchKernelGGL(k_parent_init_pair, dim3(gb), dim3(kBlock), 0, st, parent, n, core, skey,
                      mutual, cmin, C, rep);
   if (dim == 2) {
@@ -4131,6 +4183,7 @@ int32_t DbscanState::labels_global(const int64_t* rep_orig, const int64_t* reps,
 
 int32_t DbscanState::frames_pass(int32_t min_frames, hipStream_t st) {
   if (degenerate || min_frames < 1) return RPT_OK;  // <= 0: every core point qualifies
+  cmin_ready = false;  // core points may be demoted below
   const bool refine = min_frames >= 2;
   int32_t* list = nc_list;  // free until labels_fifo rebuilds it
   int32_t* count = nc_list + n;
@@ -4409,6 +4462,7 @@ int32_t dbscan_core(DbscanState* S, uint8_t* core_out, hipStream_t st) {
   return RPT_OK;
 }
 int32_t dbscan_set_core(DbscanState* S, const uint8_t* core_in, hipStream_t st) {
+  S->cmin_ready = false;
   hipLaunchKernelGGL(k_core_from_orig, dim3(grid_for(S->n, kBlock, 2048)), dim3(kBlock), 0, st,
                      core_in, S->sorig, S->n, S->core);
   RPT_CHECK_LAUNCH();

@@ -26,10 +26,12 @@ def _free_port():
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,frames,impl,lanes", [(2, 14, "native", 1), (3, 6, "native", 1),
                                                      (2, 14, "python", 1), (2, 8, "native", 2),
+                                                     (3, 6, "native", 3),
                                                      (3, 6, "native-tinycaps", 1)])
 def test_sharded_gpu_matches_single_gpu(world, frames, impl, lanes):
-    """lanes = 2: two stacks in flight (rpt.dist.ShardLanes: a process group, stream and thread
-    per lane); each lane's last run is checked.  native-tinycaps: the one-collective gathers
+    """lanes = 2 / 3: stacks in flight (rpt.dist.ShardLanes: a stream and thread per lane, every
+    lane's collectives through the ONE process group in the CommSequencer's global order; the
+    bench's N > 1 default is 2); each lane's last run is checked.  native-tinycaps: the one-collective gathers
     (pairs, representatives, segments) with one-element capacities, i.e. their two-round
     fallbacks."""
     extra = []

@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Structure of a bench stack as the ST-DBSCAN kernels see it (core / border / noise counts, grid
+cells, candidate windows of the non-core points) -- for kernel design, not a test.
+    python tools/stack_stats.py [frames] [dense]"""
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+for p in (str(ROOT / "radar-point-cloud-tracking_amd"), str(ROOT)):
+    sys.path.insert(0, p)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from rpt.pipeline import FrameStackPipeline, PathParams  # noqa: E402
+from rpt.synth import DeviceSynth, SynthConfig, dense_config  # noqa: E402
+
+F = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
+cfg = dense_config(n_frames=F) if len(sys.argv) > 2 else SynthConfig(n_frames=F)
+dev = torch.device("cuda", 0)
+ds = DeviceSynth(cfg, dev)
+pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), dev)
+pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
+                  cfg.n_frames * len(cfg.gains))
+res = pipe.run(ds.echo(), keep_points=True)
+x = res.points["x"].cpu().numpy()
+y = res.points["y"].cpu().numpy()
+pf = res.points["frame"].cpu().numpy().astype(np.int64)
+core = res.points["core"].cpu().numpy().astype(bool)
+lab = res.labels.cpu().numpy()
+n = len(x)
+print(f"n {n} core {core.sum()} noncore {(~core).sum()} border {((~core) & (lab >= 0)).sum()} "
+      f"noise {(lab < 0).sum()} clusters {res.n_clusters}")
+side = 0.7 * 8.0 * (1 + 2**-20)
+cx = np.floor((x - x.min()) / side).astype(np.int64)
+cy = np.floor((y - y.min()) / side).astype(np.int64)
+nx, ny = int(cx.max()) + 1, int(cy.max()) + 1
+s = pf - pf.min()
+key = (s * ny + cy) * nx + cx
+u, inv, cnt = np.unique(key, return_inverse=True, return_counts=True)
+ccore = np.bincount(inv, weights=core, minlength=len(u))
+cnc = np.bincount(inv, weights=~core, minlength=len(u))
+print(f"grid {nx}x{ny}x{int(s.max()) + 1} occupied {len(u)} cells with core {(ccore > 0).sum()} "
+      f"all-core {(ccore == cnt).sum()} with non-core {(cnc > 0).sum()}")
+print("non-core per cell holding non-core:", np.bincount(cnc[cnc > 0].astype(int))[:12].tolist())
+print("non-core points in cells with core points:", int(cnc[ccore > 0].sum()))
+cs = np.sort(u[ccore > 0])
+nc = np.nonzero(~core)[0]
+rng = np.random.default_rng(0)
+smp = rng.choice(nc, min(200000, len(nc)), replace=False)
+tot = np.zeros(len(smp), np.int64)
+for ds_ in range(-2, 3):
+    for dy in range(-2, 3):
+        for dx in range(-2, 3):
+            ok = (cy[smp] + dy >= 0) & (cy[smp] + dy < ny) & (cx[smp] + dx >= 0) & (cx[smp] + dx < nx)
+            k = key[smp] + (ds_ * ny + dy) * nx + dx
+            i = np.minimum(np.searchsorted(cs, k), len(cs) - 1)
+            tot += ok & (cs[i] == k)
+print(f"non-core: core cells in the 5x5x5 window mean {tot.mean():.2f}, zero {np.mean(tot == 0):.3f}, "
+      f"p90 {np.percentile(tot, 90)}")
