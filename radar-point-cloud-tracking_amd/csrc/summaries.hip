@@ -12,9 +12,11 @@
 // slots; up to kFsMaxKeys labels per frame) or, beyond that, a stable radix sort of (label+1,
 // index) keeps each label's points in index order, so every (frame, label) run is contiguous and
 // ordered; segments come frame-major (hash order inside a frame) from the counting sort,
-// label-major from the radix sort (consumers bucket them by frame, tracker.cpp order_clusters).  Two waves per run (x, y): the
-// order-preserving float32 chain is fed from LDS, so a run of k points costs ~k dependent adds
-// (~4.4 cycles each), not k memory latencies.
+// label-major from the radix sort (consumers bucket them by frame, tracker.cpp order_clusters).
+// Runs of up to kLaneChainMax points: one lane per run (k_runs_lane: 64 runs' order-preserving
+// float32 chains per add instruction); a longer run takes one wave for its x and y chains (lanes 0
+// and 1, fed from LDS, so it costs ~k dependent adds of ~4.4 cycles, not k memory latencies) and
+// one for its intensity.
 // Radix path: noise (key 0) sorts first in index order, so each frame's first noise point is the
 // head of its frame within the noise run (no atomics).
 #include <climits>
@@ -133,27 +135,36 @@ __global__ void k_gather_runs(const uint32_t* __restrict__ sv, int64_t n,
   }
 }
 
-// Order-preserving float32 sum of g[b..e) (np.add.reduce from the first element), computed by
-// one wave: lanes stage 1,024-element chunks in the wave's LDS slice (the next chunk's loads in
-// flight meanwhile) and the wave-uniform chain consumes broadcast 16-byte LDS reads issued a batch
-// ahead.  The dependent v_add_f32 (~4.4 cycles on gfx950, tools/microbench/chain.hip) is the
-// floor; a packed x/y add is no faster (8.5 cycles), so x and y run on separate waves.
-__device__ __forceinline__ float seq_sum(const float* __restrict__ g, int b, int e, int lane,
-                                         float* __restrict__ sb) {
-  constexpr int kPre = 16, kChunk = 64 * kPre, V = 8;
-  float pre[kPre];
+// Order-preserving float32 sums of gx[b..e) and gy[b..e) (np.add.reduce from the first element),
+// computed by ONE wave: lanes stage 1,024-element chunks of both in the wave's LDS slice (the next
+// chunks' loads in flight meanwhile) and the chains run in lane 0 (x) and lane 1 (y) of the same
+// instructions, each lane consuming 16-byte LDS reads of its own half issued a batch ahead: one
+// dependent v_add_f32 (~4.4 cycles on gfx950, tools/microbench/chain.hip) per element advances
+// both chains, so a run costs one SIMD's issue slots once, not twice (a packed x/y add would be
+// no faster: 8.5 cycles).  Lane 0 returns the x sum, lane 1 the y sum (other lanes repeat them).
+constexpr int kSeqChunk = 1024;
+__device__ __forceinline__ float seq_sum(const float* __restrict__ gx,
+                                         const float* __restrict__ gy, int b, int e, int lane,
+                                         float* __restrict__ sbuf) {
+  constexpr int kPre = kSeqChunk / 64, kChunk = kSeqChunk, V = 8;
+  float pre[kPre], prey[kPre];
   auto load_chunk = [&](int c0) {
 #pragma unroll
     for (int t = 0; t < kPre; ++t) {
       const int idx = c0 + t * 64 + lane;
-      pre[t] = (idx < e) ? g[idx] : 0.f;
+      pre[t] = (idx < e) ? gx[idx] : 0.f;
+      prey[t] = (idx < e) ? gy[idx] : 0.f;
     }
   };
+  float* __restrict__ sb = sbuf + (lane & 1) * kChunk;  // this lane's chain: x or y
   float acc = 0.f;
   load_chunk(b);
   for (int c0 = b; c0 < e; c0 += kChunk) {
 #pragma unroll
-    for (int t = 0; t < kPre; ++t) sb[t * 64 + lane] = pre[t];
+    for (int t = 0; t < kPre; ++t) {
+      sbuf[t * 64 + lane] = pre[t];
+      sbuf[kChunk + t * 64 + lane] = prey[t];
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -290,54 +301,215 @@ __device__ __forceinline__ float mean_intensity(const float* __restrict__ gi, in
   return tot / fk;
 }
 
-// Three waves per (frame, label) run: wave 0 sums x (np.mean axis 0, sequential float32 in index
-// order), wave 1 sums y — two pure dependent-add chains on different SIMDs — and wave 2 takes
-// the mean intensity (lane-parallel), so no other work sits in the chains' instruction streams.
-// META: the frame sort already wrote frame/label/count/first and o_count gives each run's length
-// (runs are not adjacent: noise slots sit between frames); otherwise runs tile [0, n) and the
-// metadata comes from the sorted keys.
+// Runs of at most kLaneChainMax points are summarised one LANE per run (k_runs_lane below);
+// longer runs take a wave for both chains (seq_sum: a wave-wide chain issues one or two useful
+// adds per wave instruction, and thousands of short runs made K9 VALU-issue and latency bound).
+constexpr int kLaneChainMax = 3072;
+
+// META: run [b, e) of segment su (o_count holds the lengths: runs are not adjacent, noise slots
+// sit between frames); otherwise runs tile [0, n).
 template <bool META>
-// 5 waves/SIMD (96 VGPRs, 3 spills; 104 gave 4): K9 0.88 -> 0.83 ms at 1000 frames
-__global__ __launch_bounds__(kBlock, 5) void k_summarize(
+__device__ __forceinline__ void run_bounds(const int64_t* __restrict__ seg_start,
+                                           const int64_t* __restrict__ o_count, int64_t n_seg,
+                                           int64_t n, int64_t su, int& b, int& e) {
+  b = (int)seg_start[su];
+  e = META ? (int)(b + o_count[su]) : (int)((su + 1 < n_seg) ? seg_start[su + 1] : n);
+}
+
+// One lane per run: lane l of wave w summarises run 64 w + l -- the x and y chains
+// (sequentially from the first point, np.mean axis 0) and the intensity sum (exact integer sum,
+// see mean_intensity; numpy's pairwise sum by the lane otherwise) in one pass over 16-B loads,
+// kLq float4s of each column per block, all in flight together: 64 runs' chains advance per add
+// instruction, and the loads in flight per lane bound it (a radar stack's runs are a few points
+// each, plus one long run per frame).  Runs longer than kLaneChainMax are listed for k_summarize
+// (long_list / *n_long, zeroed beforehand) instead.  Every lane takes part in the wave-level
+// steps; lanes without a run of their own walk an empty range.
+constexpr int kLq = 8;  // float4 loads per column per block (32 points)
+template <bool META>
+__global__ __launch_bounds__(kBlock, 2) void k_runs_lane(
     const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
     const int64_t* __restrict__ seg_start, const int32_t* __restrict__ n_seg_dev, int64_t n,
     const float* __restrict__ gx, const float* __restrict__ gy, const float* __restrict__ gi,
     const int32_t* __restrict__ pf, int32_t* __restrict__ o_frame, int32_t* __restrict__ o_label,
     int64_t* __restrict__ o_count, int64_t* __restrict__ o_first, float* __restrict__ o_cx,
-    float* __restrict__ o_cy, float* __restrict__ o_mi) {
-  __shared__ float s_buf[kBlock / 64][1024];
-  const int64_t n_seg = *n_seg_dev;  // the segment count stays on the device (no readback)
+    float* __restrict__ o_cy, float* __restrict__ o_mi, int32_t* __restrict__ long_list,
+    int32_t* __restrict__ n_long) {
+  const int64_t n_seg = *n_seg_dev;
   const int lane = threadIdx.x & 63;
   const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
   const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
-  for (int64_t w = w0; w < 3 * n_seg; w += nw) {
-    const int su = __builtin_amdgcn_readfirstlane((int)(w / 3));
-    const int comp = __builtin_amdgcn_readfirstlane((int)(w - (int64_t)su * 3));
-    const int b = __builtin_amdgcn_readfirstlane((int)seg_start[su]);
-    const int e = __builtin_amdgcn_readfirstlane(
-        META ? (int)(b + o_count[su]) : (int)((su + 1 < n_seg) ? seg_start[su + 1] : n));
-    const int k = e - b;
-    const float fk = (float)k;
-    if (comp == 2) {
-      const float mi = mean_intensity(gi, b, e, lane);
-      if (lane == 0) o_mi[su] = mi;
-      continue;
+  const int64_t groups = (n_seg + 63) / 64;
+  for (int64_t w = w0; w < groups; w += nw) {  // (wave-uniform)
+    const int64_t su = w * 64 + lane;
+    const bool valid = su < n_seg;
+    int b = 0, e = 0;
+    if (valid) run_bounds<META>(seg_start, o_count, n_seg, n, su, b, e);
+    const bool lng = valid && e - b > kLaneChainMax;
+    const uint64_t lm = __ballot(lng);
+    if (lm) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(n_long, __popcll(lm));
+      base = __shfl(base, 0);
+      if (lng) long_list[base + __popcll(lm & ((1ull << lane) - 1ull))] = (int32_t)su;
     }
-    const float sum = seq_sum(comp ? gy : gx, b, e, lane, s_buf[threadIdx.x / 64]);
-    if (lane == 0) {
-      if (comp) {
-        o_cy[su] = sum / fk;
-      } else if (META) {
-        o_cx[su] = sum / fk;
-      } else {
+    const bool mine = valid && !lng;
+    if (!mine) b = e = 0;
+    float ax = 0.f, ay = 0.f;
+    uint64_t isum = 0;
+    bool small_int = true;
+    auto ivisit = [&](float v, bool on) {
+      const bool ok = v >= 0.f && v == floorf(v) && v < 16777216.f;
+      small_int = small_int && (ok || !on);
+      isum += on ? (uint64_t)(uint32_t)v : 0ull;
+    };
+    int i = b;
+    if (i < e) {
+      ax = gx[i];
+      ay = gy[i];
+      ivisit(gi[i], true);
+      ++i;
+    }
+    for (; i < e && (i & 3); ++i) {
+      ax = ax + gx[i];
+      ay = ay + gy[i];
+      ivisit(gi[i], true);
+    }
+    // whole float4s [i, i + 4 nq) in blocks of kLq per column; the block loop runs to the wave's
+    // largest block count with branch-free loads (a lane past its own blocks re-reads a valid
+    // block, the longest lane's if it has none) and selects instead of branches around the adds
+    const int nq = (e - i) >> 2;
+    const int nblk = nq / kLq;
+    int nbmax = nblk;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) nbmax = max(nbmax, __shfl_xor(nbmax, off));
+    if (nbmax > 0) {
+      const int lmax = __ffsll((unsigned long long)__ballot(nblk == nbmax)) - 1;
+      const int i0 = nblk > 0 ? i : __shfl(i, lmax);
+      const int last = nblk > 0 ? nblk - 1 : 0;
+      const float4* __restrict__ px = reinterpret_cast<const float4*>(gx + i0);
+      const float4* __restrict__ py = reinterpret_cast<const float4*>(gy + i0);
+      const float4* __restrict__ pi = reinterpret_cast<const float4*>(gi + i0);
+      for (int k = 0; k < nbmax; ++k) {
+        const int kk = min(k, last);
+        float4 qx[kLq], qy[kLq], qi[kLq];
+#pragma unroll
+        for (int u = 0; u < kLq; ++u) {
+          qx[u] = px[kk * kLq + u];
+          qy[u] = py[kk * kLq + u];
+          qi[u] = pi[kk * kLq + u];
+        }
+        const bool on = k < nblk;
+#pragma unroll
+        for (int u = 0; u < kLq; ++u) {
+          float tx = ax + qx[u].x, ty = ay + qy[u].x;
+          tx = tx + qx[u].y;
+          ty = ty + qy[u].y;
+          tx = tx + qx[u].z;
+          ty = ty + qy[u].z;
+          tx = tx + qx[u].w;
+          ty = ty + qy[u].w;
+          ax = on ? tx : ax;
+          ay = on ? ty : ay;
+          ivisit(qi[u].x, on);
+          ivisit(qi[u].y, on);
+          ivisit(qi[u].z, on);
+          ivisit(qi[u].w, on);
+        }
+      }
+    }
+    for (int q = nblk * kLq; q < nq; ++q) {
+      const float4 vx = reinterpret_cast<const float4*>(gx + i)[q];
+      const float4 vy = reinterpret_cast<const float4*>(gy + i)[q];
+      const float4 vi = reinterpret_cast<const float4*>(gi + i)[q];
+      ax = ax + vx.x;
+      ax = ax + vx.y;
+      ax = ax + vx.z;
+      ax = ax + vx.w;
+      ay = ay + vy.x;
+      ay = ay + vy.y;
+      ay = ay + vy.z;
+      ay = ay + vy.w;
+      ivisit(vi.x, true);
+      ivisit(vi.y, true);
+      ivisit(vi.z, true);
+      ivisit(vi.w, true);
+    }
+    for (i += 4 * nq; i < e; ++i) {
+      ax = ax + gx[i];
+      ay = ay + gy[i];
+      ivisit(gi[i], true);
+    }
+    if (mine) {
+      const int k = e - b;
+      const float fk = (float)k;
+      o_cx[su] = ax / fk;
+      o_cy[su] = ay / fk;
+      float mi;
+      if (small_int && isum < 16777216u) {
+        mi = (float)isum / fk;
+      } else {  // numpy's pairwise sum (k <= kLaneChainMax < 8192: one buffer chunk)
+        float tot = 0.f;
+        tot = tot + pairwise_f32(gi, b, k);
+        mi = tot / fk;
+      }
+      o_mi[su] = mi;
+      if (!META) {
         const uint32_t i0 = sv[b];
         o_frame[su] = pf[i0];
         o_label[su] = (int32_t)sk[b] - 1;
         o_count[su] = k;
         o_first[su] = i0;
-        o_cx[su] = sum / fk;
       }
     }
+  }
+}
+
+// The runs longer than kLaneChainMax (k_runs_lane's list): two waves each, one for the mean
+// intensity (lane-parallel) and one for the x and y chains (np.mean axis 0, sequential float32 in
+// index order; seq_sum) -- pure dependent-add chains, so no other work sits in their instruction
+// stream.  META: the frame sort already wrote frame/label/count/first; otherwise the metadata
+// comes from the sorted keys (written by the intensity wave).
+template <bool META>
+// 4 waves/SIMD (128 VGPRs: the x and y prefetch registers; 5 spilled 23)
+__global__ __launch_bounds__(kBlock, 4) void k_summarize(
+    const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
+    const int64_t* __restrict__ seg_start, const int32_t* __restrict__ n_seg_dev, int64_t n,
+    const float* __restrict__ gx, const float* __restrict__ gy, const float* __restrict__ gi,
+    const int32_t* __restrict__ pf, int32_t* __restrict__ o_frame, int32_t* __restrict__ o_label,
+    int64_t* __restrict__ o_count, int64_t* __restrict__ o_first, float* __restrict__ o_cx,
+    float* __restrict__ o_cy, float* __restrict__ o_mi, const int32_t* __restrict__ long_list,
+    const int32_t* __restrict__ n_long_dev) {
+  __shared__ float s_buf[kBlock / 64][2 * kSeqChunk];
+  const int64_t n_seg = *n_seg_dev;  // the segment count stays on the device (no readback)
+  const int64_t n_long = *n_long_dev;
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+  for (int64_t w = w0; w < 2 * n_long; w += nw) {
+    const int su = __builtin_amdgcn_readfirstlane(long_list[w >> 1]);
+    const int comp = __builtin_amdgcn_readfirstlane((int)(w & 1));
+    int b, e;
+    run_bounds<META>(seg_start, o_count, n_seg, n, su, b, e);
+    b = __builtin_amdgcn_readfirstlane(b);
+    e = __builtin_amdgcn_readfirstlane(e);
+    const int k = e - b;
+    const float fk = (float)k;
+    if (comp == 1) {
+      const float mi = mean_intensity(gi, b, e, lane);
+      if (lane == 0) {
+        o_mi[su] = mi;
+        if (!META) {
+          const uint32_t i0 = sv[b];
+          o_frame[su] = pf[i0];
+          o_label[su] = (int32_t)sk[b] - 1;
+          o_count[su] = k;
+          o_first[su] = i0;
+        }
+      }
+      continue;
+    }
+    const float sum = seq_sum(gx, gy, b, e, lane, s_buf[threadIdx.x / 64]);
+    if (lane < 2) (lane ? o_cy : o_cx)[su] = sum / fk;
   }
 }
 
@@ -718,6 +890,11 @@ __global__ void k_fill_i64(int64_t* p, int64_t n, int64_t v) {
 
 }  // namespace
 
+// k_summarize's grid: two waves per long run, the count known only on the device (loops)
+static int long_grid(int64_t s_hint) {
+  return grid_for(2 * std::min<int64_t>(s_hint, 8192), kBlock / 64, 4096);
+}
+
 // bits: radix bits of the label keys (label + 1 < 2^bits); s_hint: expected segment count (sizes
 // the summarize grid, which loops over the device count); *n_seg_dev: the count, on the device.
 static int32_t summaries_impl(const int32_t* labels, const float* x, const float* y,
@@ -751,7 +928,7 @@ static int32_t summaries_impl(const int32_t* labels, const float* x, const float
     for (int k = 0; k < 4; ++k) b.add<int32_t>(n + 1);
     b.add<int64_t>(n + 1);
     for (int k = 0; k < 3; ++k) b.add<int32_t>((int64_t)n_frames + 1);
-    b.add<int32_t>(1);
+    b.add<int32_t>(2);
     RPT_TRY(sc.reserve(b.bytes, st));
     float* gx = sc.carve_n<float>(n + 1);
     float* gy = sc.carve_n<float>(n + 1);
@@ -764,8 +941,8 @@ static int32_t summaries_impl(const int32_t* labels, const float* x, const float
     int32_t* fstart = sc.carve_n<int32_t>((int64_t)n_frames + 1);
     int32_t* nseg_f = sc.carve_n<int32_t>((int64_t)n_frames + 1);
     int32_t* base = sc.carve_n<int32_t>((int64_t)n_frames + 1);
-    int32_t* ovf = sc.carve_n<int32_t>(1);
-    RPT_HIP(hipMemsetAsync(ovf, 0, sizeof(int32_t), st));
+    int32_t* ovf = sc.carve_n<int32_t>(2);  // [overflow flag, long-run count]
+    RPT_HIP(hipMemsetAsync(ovf, 0, 2 * sizeof(int32_t), st));
     hipLaunchKernelGGL(k_frame_sort, dim3(n_frames), dim3(kFsWaves * 64), 0, st, labels, pf, n,
                        x, y, inten, gx, gy, gi, fstart, tstart, tlen, tlabel, tfirst, nseg_f,
                        frame_first_noise, ovf);
@@ -775,9 +952,15 @@ static int32_t summaries_impl(const int32_t* labels, const float* x, const float
                        n_frames, fstart, nseg_f, base, tstart, tlen, tlabel, tfirst, o_frame,
                        o_label, o_count, o_first, seg_start);
     hipLaunchKernelGGL(k_seg_total_fix, dim3(1), dim3(64), 0, st, ovf, base + n_frames);
-    hipLaunchKernelGGL(k_summarize<true>, dim3(grid_for(3 * sh, kBlock / 64, 16384)),
+    // short runs one lane each; the long ones listed (in tlen, dead after the compaction) for
+    // k_summarize's waves
+    hipLaunchKernelGGL(k_runs_lane<true>, dim3(grid_for((sh + 63) / 64, kBlock / 64, 4096)),
                        dim3(kBlock), 0, st, nullptr, nullptr, seg_start, base + n_frames, n, gx,
-                       gy, gi, pf, o_frame, o_label, o_count, o_first, o_cx, o_cy, o_mi);
+                       gy, gi, pf, o_frame, o_label, o_count, o_first, o_cx, o_cy, o_mi, tlen,
+                       ovf + 1);
+    hipLaunchKernelGGL(k_summarize<true>, dim3(long_grid(sh)), dim3(kBlock), 0, st, nullptr,
+                       nullptr, seg_start, base + n_frames, n, gx, gy, gi, pf, o_frame, o_label,
+                       o_count, o_first, o_cx, o_cy, o_mi, tlen, ovf + 1);
     RPT_CHECK_LAUNCH();
     *n_seg_dev = base + n_frames;
     return RPT_OK;
@@ -789,6 +972,7 @@ static int32_t summaries_impl(const int32_t* labels, const float* x, const float
   b.add<int32_t>(n + 1);
   b.add<int64_t>(n + 1);
   for (int k = 0; k < 3; ++k) b.add<float>(n + 1);
+  b.add<int32_t>(1);
   RPT_TRY(sc.reserve(b.bytes, st));
   uint32_t* keys = sc.carve_n<uint32_t>(n + 1);
   uint32_t* vals = sc.carve_n<uint32_t>(n + 1);
@@ -801,6 +985,7 @@ static int32_t summaries_impl(const int32_t* labels, const float* x, const float
   float* gx = sc.carve_n<float>(n + 1);
   float* gy = sc.carve_n<float>(n + 1);
   float* gi = sc.carve_n<float>(n + 1);
+  int32_t* n_long = sc.carve_n<int32_t>(1);
   if (n == 0) {
     RPT_HIP(hipMemsetAsync(pos, 0, sizeof(int32_t), st));
     *n_seg_dev = pos;
@@ -817,9 +1002,14 @@ static int32_t summaries_impl(const int32_t* labels, const float* x, const float
   RPT_TRY(exclusive_scan_total_i32(head, pos, n, st));
   hipLaunchKernelGGL(k_seg_starts, dim3(g), dim3(kBlock), 0, st, head, pos, n, seg_start);
   hipLaunchKernelGGL(k_gather_runs, dim3(g), dim3(kBlock), 0, st, sv, n, x, y, inten, gx, gy, gi);
-  hipLaunchKernelGGL(k_summarize<false>, dim3(grid_for(3 * sh, kBlock / 64, 16384)), dim3(kBlock), 0, st,
-                     sk, sv, seg_start, pos + n, n, gx, gy, gi, pf, o_frame, o_label, o_count,
-                     o_first, o_cx, o_cy, o_mi);
+  // short runs one lane each; the long ones listed (in head, dead after k_seg_starts)
+  RPT_HIP(hipMemsetAsync(n_long, 0, sizeof(int32_t), st));
+  hipLaunchKernelGGL(k_runs_lane<false>, dim3(grid_for((sh + 63) / 64, kBlock / 64, 4096)),
+                     dim3(kBlock), 0, st, sk, sv, seg_start, pos + n, n, gx, gy, gi, pf, o_frame,
+                     o_label, o_count, o_first, o_cx, o_cy, o_mi, head, n_long);
+  hipLaunchKernelGGL(k_summarize<false>, dim3(long_grid(sh)), dim3(kBlock), 0, st, sk, sv,
+                     seg_start, pos + n, n, gx, gy, gi, pf, o_frame, o_label, o_count, o_first,
+                     o_cx, o_cy, o_mi, head, n_long);
   RPT_CHECK_LAUNCH();
   *n_seg_dev = pos + n;
   return RPT_OK;
@@ -907,6 +1097,7 @@ int32_t label_means(const int32_t* labels, const float* x, const float* y, const
   b.add<int32_t>(n + 1);
   b.add<int64_t>(n + 1);
   for (int k = 0; k < 3; ++k) b.add<float>(n + 1);
+  b.add<int32_t>(1);
   RPT_TRY(sc.reserve(b.bytes, st));
   uint32_t* keys = sc.carve_n<uint32_t>(n + 1);
   uint32_t* vals = sc.carve_n<uint32_t>(n + 1);

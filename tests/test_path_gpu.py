@@ -326,10 +326,15 @@ def test_mean_intensity_pairwise_chunks(gpu):
 
 
 def _radix_summaries_in_child(frames, lab, ncl):
-    """_summaries_device in a child process with RPT_K9_RADIX=1 (read once per process)."""
+    """_summaries_device in a child process on the A/B build (librpt_ab.so, built by
+    __graft_entry__.build(): the only build that reads RPT_* switches) with RPT_K9_RADIX=1."""
     import os
     import subprocess
     import tempfile
+
+    from rpt import _build
+
+    assert _build.LIB_AB.exists(), "librpt_ab.so missing: run __graft_entry__.build()"
 
     with tempfile.TemporaryDirectory() as d:
         np.savez(os.path.join(d, "in.npz"), lab=lab, ncl=ncl,
@@ -344,7 +349,7 @@ def _radix_summaries_in_child(frames, lab, ncl):
             " int(g['ncl']))\n"
             f"np.savez({os.path.join(d, 'out.npz')!r}, fo=fo, order=order,"
             " **{'s_' + k: v for k, v in seg.items()})\n")
-        env = dict(os.environ, RPT_K9_RADIX="1")
+        env = dict(os.environ, RPT_K9_RADIX="1", RPT_LIB=str(_build.LIB_AB))
         subprocess.run([sys.executable, "-c", code], check=True, env=env, timeout=240,
                        cwd=os.path.dirname(os.path.abspath(__file__)))
         o = np.load(os.path.join(d, "out.npz"))
@@ -356,7 +361,8 @@ def _radix_summaries_in_child(frames, lab, ncl):
 def test_summaries_frame_sort_matches_radix_path(gpu, crowded):
     """K9's per-frame counting sort and its radix path (RPT_K9_RADIX=1, in a child process) give
     the same segments — frame-major vs label-major — on frames of ragged sizes, empty frames,
-    noise-only frames and runs interleaved point by point; `crowded` adds a frame with more
+    noise-only frames, runs interleaved point by point, a run longer than a lane summarises and
+    non-integer intensities (both checked against numpy); `crowded` adds a frame with more
     labels than the frame sort takes (the sync entry point then redoes K9 on the radix path)."""
     rng = np.random.default_rng(21)
     sizes = [0, 1, 63, 64, 65, 3000, 0, 517, 20000, 5, 0] + ([6000] if crowded else [])
@@ -368,6 +374,10 @@ def test_summaries_frame_sort_matches_radix_path(gpu, crowded):
         lab = rng.integers(-1, 3000 if k == 11 else 40 + k, m).astype(np.int32)
         if k == 9:
             lab[:] = -1
+        if k == 8:  # one run far longer than a lane takes (summarised by whole waves)
+            lab[rng.random(m) < 0.6] = 7
+        if k in (3, 8):  # non-integer intensities: numpy's pairwise sum (lane / wave forms)
+            p[:, 2] = rng.random(m).astype(np.float32) * 255
         frames.append((k, p, None))
         labs.append(lab)
     lab = np.concatenate(labs)
@@ -389,6 +399,7 @@ def test_summaries_frame_sort_matches_radix_path(gpu, crowded):
         assert a[0]["first"][s] == np.nonzero(m)[0][0]
         c = np.mean(pts[m][:, :2], axis=0)
         assert a[0]["cx"][s] == c[0] and a[0]["cy"][s] == c[1]
+        assert float(a[0]["mi"][s]) == float(np.mean(pts[m][:, 2]))
     assert len(a[0]["label"]) == len({(f, l) for f, l in zip(pf, lab) if l >= 0})
 
 
