@@ -228,6 +228,10 @@ struct Geom {
   // (> e2hi) is <= (>) eps2 in the float64 bound too (margins 1e-5 >> the float32 rounding);
   // e2lo = -1 / e2hi = inf disable it (eps2 outside [1e-20, 1e30])
   float e2lo, e2hi;
+  // integral times (slabs hold whole time values): every neighbour of a point or cell in slab s
+  // lies in slabs [s - rt, s + rt] (DbscanState::slab_reach), so the scan windows take exactly
+  // those; -1: non-integral times, windows from the time range with one slab of slack each side
+  int rt;
 };
 
 // cell index floor((v - o) / side) as a multiply by the host's float64 reciprocal (a float64
@@ -1069,8 +1073,14 @@ __device__ __forceinline__ Window make_window(int cx, int cy, int cz, float tlo,
   constexpr int PER = (D == 3) ? 125 : 25;
   Window w;
   const double et = (double)g.epst;
-  int s0 = (int)fmax(floor(((double)tlo - et - g.ot) * g.inv_ct) - 1.0, (double)s_min);
-  int s1 = (int)fmin(floor(((double)thi + et - g.ot) * g.inv_ct) + 1.0, (double)(g.nt - 1));
+  int s0, s1;
+  if (g.rt >= 0) {  // integral times: the slabs of tlo / thi (exact) +- rt
+    s0 = max(slab_of(tlo, g) - g.rt, s_min);
+    s1 = min(slab_of(thi, g) + g.rt, g.nt - 1);
+  } else {
+    s0 = (int)fmax(floor(((double)tlo - et - g.ot) * g.inv_ct) - 1.0, (double)s_min);
+    s1 = (int)fmin(floor(((double)thi + et - g.ot) * g.inv_ct) + 1.0, (double)(g.nt - 1));
+  }
   // shrink to the slabs in reach: one lane per slab (independent loads), ballot (callers are
   // whole waves with uniform arguments)
   const int lane = threadIdx.x & 63;
@@ -3687,6 +3697,10 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   g.nz = (int)nz;
   g.nt = (int)nt;
   g.cells = nx * ny * nz * nt;
+  {
+    const double r = slab_reach();  // (infinite for an infinite eps_time: generic windows)
+    g.rt = (integral_t && r < 1e9) ? (int)std::min(r, (double)nt) : -1;
+  }
   C = g.cells;
   const int64_t C1 = C + 1;  // + the isolated cell (non-finite t)
   Budget bud;
