@@ -109,6 +109,46 @@ def test_sharded_protocol_matches_single_process(world, n_frames):
                                       np.vstack([np.vstack(o.positions) for o in objs]))
 
 
+def _short_share_worker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+
+    from _cpu_ops import CpuOps
+    from rpt.dist import Comm, ShardedStackPipeline
+    from rpt.pipeline import PathParams
+    from rpt.synth import make_geometry, numpy_echo
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = _cfg(world)
+    geo = make_geometry(cfg)
+    echo = numpy_echo(cfg, geo, frames=range(rank, rank + 1))
+    pipe = ShardedStackPipeline(CpuOps(cfg.scale, geo.cos_t, geo.sin_t),
+                                Comm(torch.device("cpu")), cfg.gains, cfg.rows, cfg.bins,
+                                PathParams(eps_space=8.0, eps_time=2.0, min_samples=15))
+    pipe.set_geometry(None, torch.tensor(list(cfg.gains), dtype=torch.int32))
+    try:
+        pipe.run(torch.from_numpy(echo), 1, rank)
+        msg = "no error"
+    except ValueError as e:
+        msg = str(e)
+    (Path(out_dir) / f"rank{rank}.txt").write_text(msg)
+    dist.destroy_process_group()
+
+
+def test_sharded_share_shorter_than_halo_raises():
+    """A rank must own at least floor(eps_time) frames (the halo comes from the neighbouring ranks
+    only): one frame per rank with eps_time = 2 raises ValueError on every rank."""
+    import torch.multiprocessing as mp
+
+    with tempfile.TemporaryDirectory() as td:
+        mp.start_processes(_short_share_worker, args=(2, _free_port(), td), nprocs=2, join=True,
+                           start_method="spawn")
+        for r in range(2):
+            assert (Path(td) / f"rank{r}.txt").read_text() == \
+                "each rank needs at least floor(eps_time)=2 frames"
+
+
 def test_merge_equivalences_chains():
     from rpt.dist import merge_equivalences
 
