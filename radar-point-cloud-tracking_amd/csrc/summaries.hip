@@ -304,7 +304,9 @@ __device__ __forceinline__ float mean_intensity(const float* __restrict__ gi, in
 // Runs of at most kLaneChainMax points are summarised one LANE per run (k_runs_lane below);
 // longer runs take a wave for both chains (seq_sum: a wave-wide chain issues one or two useful
 // adds per wave instruction, and thousands of short runs made K9 VALU-issue and latency bound).
-constexpr int kLaneChainMax = 3072;
+// A lane streams ~32 points per memory round trip, a wave's chain ~1,000 per 4 us: the lane form
+// wins only for short runs (3,072 made the 125-frame stack's K9 slower: 143 us of lane chains).
+constexpr int kLaneChainMax = 128;
 
 // META: run [b, e) of segment su (o_count holds the lengths: runs are not adjacent, noise slots
 // sit between frames); otherwise runs tile [0, n).
