@@ -1597,10 +1597,18 @@ __global__ __launch_bounds__(kBlock, 8) void k_core_slow(const float4* __restric
           cls[r] = classify<D>(p, rec_boxA<D>(cr), rec_boxB(cr), g);
         }
       }
-      int add = 0;
+      // whole-cell accepts (lower bound) and every cell that may hold a neighbour (upper bound,
+      // with the super-rounds still to come): a point whose upper bound stays below min_samples
+      // is decided without a pair test
+      int add = 0, may = 0;
 #pragma unroll
-      for (int r = 0; r < kR; ++r) add += (cls[r] == 1) ? e[r] - b[r] : 0;
+      for (int r = 0; r < kR; ++r) {
+        add += (cls[r] == 1) ? e[r] - b[r] : 0;
+        may += (cls[r] == 2) ? e[r] - b[r] : 0;
+      }
       cnt += wave_sum(add);
+      const bool last = base + 64 * kR >= w.total;
+      if (last && cnt + wave_sum(may) < need) break;
 #pragma unroll
       for (int r = 0; r < kR; ++r) {
         uint64_t pm = __ballot(cls[r] == 2);

@@ -505,6 +505,39 @@ def test_speculative_k1_write_regrows(gpu):
         np.testing.assert_array_equal(a.seg[k], b.seg[k])
 
 
+@pytest.mark.parametrize("rows,thr,stride,p", [(1000, 10.0, 1, 0.02), (1000, 127.5, 3, 0.1),
+                                               (4093, 200.0, 4, 0.08), (16, -3.0, 1, 1.0),
+                                               (1000, 10.0, 1, 0.25)])
+def test_k1_stack_driver_matches_public_k1(gpu, rows, thr, stride, p):
+    """The stack driver's K1 (staged count, speculative capacity-bounded write, regrow) against
+    the public rpt_polar_count/write on the same sparse random sweeps: thresholds on both sides of
+    127, strides 1 / 3 / 4, row counts that are not multiples of the 4-row group or 64, densities
+    from sparse to dense (the last case keeps more than 256 samples in most groups: the unstaged
+    write), every pipeline run twice (buffers regrown on the first run, reused on the second)."""
+    from rpt.pipeline import FrameStackPipeline, PathParams
+    from rpt.core.transforms import trig_tables
+
+    rng = np.random.default_rng(rows + int(thr) + stride)
+    F, gains = 2, (40, 50, 75)
+    vals = rng.integers(0, 256, (F * 3, rows, 1024))
+    echo = np.where(rng.random((F * 3, rows, 1024)) < p, vals, 0).astype(np.uint8)
+    scale = np.full(rows, 231.5, np.float32)
+    angle = np.floor(np.arange(rows) * 8196 / rows).astype(np.float32)
+    ref = _k1(gpu, echo, [scale] * (F * 3), [angle] * (F * 3), gains=gains, threshold=thr,
+              stride=stride)
+    ct, st_ = trig_tables(angle)
+    pipe = FrameStackPipeline(gains, rows, 1024, PathParams(threshold=thr, stride=stride,
+                                                           land_filter=False), gpu)
+    pipe.set_geometry(scale, ct, st_, F * 3)
+    ed = torch.from_numpy(echo.reshape(F, 3, rows, 1024)).to(gpu)
+    for _ in range(2):
+        res = pipe.run(ed, keep_points=True)
+        assert res.n_points == len(ref[0])
+        got = [res.points[k].cpu().numpy() for k in ("x", "y", "v", "gain", "frame")]
+        for a, b, name in zip(got, ref[:5], ("x", "y", "v", "gain", "frame")):
+            np.testing.assert_array_equal(a, b, err_msg=name)
+
+
 def test_concurrent_lanes_match_single_lane(gpu):
     """Two lanes (two native handles on two streams, submitted from two threads, the library's
     scratch and scan state per stream) give the same results as one lane, run after run: four
