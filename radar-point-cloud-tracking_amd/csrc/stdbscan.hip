@@ -2378,6 +2378,126 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
   }
 }
 
+// K6a (2-D, box-certain pass) with TWO cells per wave: each half-wave takes one mutual cell with
+// core points of the 64-cell chunk, lanes over its candidate cells B > A (window positions
+// k * 32 + lane, k < kR: the exact-slab windows of integral times hold 75 positions), so two
+// cells' dependent load chains (record -> occupancy -> candidate records -> roots) are in flight
+// per wave instead of one.  Same unions, undecided-candidate masks (position p -> bit p of the
+// 128-bit pmask, as k_union_listed reads them) and plist as k_union_cells<2, false>.
+__global__ __launch_bounds__(kBlock) void k_union_cells_pair(
+    const float4* __restrict__ pts, Geom g, const int32_t* __restrict__ occ,
+    const int32_t* __restrict__ n_occ, const CellRec<2>* __restrict__ crec,
+    const uint32_t* __restrict__ occ_bits, const float2* __restrict__ slab_t,
+    const int32_t* __restrict__ rep, const uint8_t* __restrict__ mutual,
+    const int32_t* __restrict__ sorig, int32_t* __restrict__ parent, int uf_flags,
+    uint4* __restrict__ pmask, int32_t* __restrict__ plist, int32_t* __restrict__ pcount) {
+  constexpr int W = 32;
+  const int lane = threadIdx.x & 63;
+  const int hl = lane & (W - 1), h0 = lane - hl;
+  auto hbal = [&](bool v) -> uint32_t { return (uint32_t)(__ballot(v) >> h0); };
+  const bool halve = !(uf_flags & 1);
+  const int64_t no = *n_occ;
+  const int64_t items = (no + 63) / 64;
+  const XcdRange xr = xcd_items(items, (uf_flags & 2) != 0);
+  for (int64_t it = xr.first; it < xr.end; it += xr.step) {
+    int ql = -1, cal = INT_MAX, ral = -1;
+    uint8_t mal = 0;
+    if (it * 64 + lane < no) ql = (int)(it * 64 + lane);
+    if (ql >= 0) cal = occ[ql];
+    if ((int64_t)cal < g.cells) {  // (not the isolated, non-finite time cell)
+      ral = rep[cal];
+      mal = mutual[cal];
+    }
+    uint64_t todo = __ballot(ral >= 0 && mal);
+    uint64_t lmask = 0;  // cells of this chunk with undecided candidates (plist)
+    while (todo) {  // (wave-uniform) two cells at a time, one per half
+      const int l0 = __ffsll((unsigned long long)todo) - 1;
+      todo &= todo - 1;
+      const int l1 = todo ? __ffsll((unsigned long long)todo) - 1 : -1;
+      if (l1 >= 0) todo &= todo - 1;
+      const int lq = h0 ? l1 : l0;  // this half's cell (-1: the upper half idles)
+      const int lsrc = lq < 0 ? 0 : lq;
+      const int64_t q = __shfl(ql, lsrc);
+      const int ca = __shfl(cal, lsrc);
+      const int ra = __shfl(ral, lsrc);
+      bool any_und = false;
+      if (lq >= 0) {  // (half-uniform)
+        const CellRec<2> ra_rec = crec[ca];
+        const float4 A1 = rec_boxA<2>(ra_rec), A2 = rec_boxB(ra_rec);
+        int cx, cy, cz;
+        decode_key<2>(ca, g, cx, cy, cz);
+        const int sa = (int)((int64_t)ca / ((int64_t)g.nx * g.ny));
+        const Window w = make_window<2, false>(cx, cy, cz, A2.z, A2.w, g, slab_t, sa);
+        for (int base = 0; base < w.total; base += W * kR) {
+          int64_t cb[kR];
+          uint32_t wb[kR];
+          int rb[kR], cls[kR];
+#pragma unroll
+          for (int k = 0; k < kR; ++k) {
+            const int qq = base + k * W + hl;
+            cb[k] = (qq < w.total) ? window_cell<2>(w, qq, g, slab_t, A2.z, A2.w) : -1;
+            if (cb[k] <= (int64_t)ca) cb[k] = -1;
+          }
+#pragma unroll
+          for (int k = 0; k < kR; ++k) wb[k] = (cb[k] >= 0) ? occ_bits[cb[k] >> 5] : 0u;
+#pragma unroll
+          for (int k = 0; k < kR; ++k) {
+            rb[k] = -1;
+            cls[k] = 0;
+            if (cb[k] >= 0 && ((wb[k] >> (cb[k] & 31)) & 1u)) {
+              const CellRec<2> cr = crec[cb[k]];
+              const int r = rep[cb[k]];
+              const uint8_t m = mutual[cb[k]];
+              if (r >= 0 && m) {
+                rb[k] = r;
+                cls[k] = classify_cells<2>(A1, rec_boxA<2>(cr), A2, rec_boxB(cr), g);
+              }
+            }
+          }
+          if (pmask && base == 0) {  // the undecided candidates for the second pass
+            uint32_t wd[kR];
+#pragma unroll
+            for (int k = 0; k < kR; ++k) wd[k] = hbal(cls[k] == 2);
+            static_assert(kR == 4, "the 128-bit pmask holds 4 x 32 window positions");
+            if (hl == 0)
+              pmask[q] = (w.total < 128)
+                             ? make_uint4(wd[0], wd[1], wd[2], wd[3] & ~kPmaskFull)
+                             : make_uint4(0u, 0u, 0u, kPmaskFull);
+            any_und = w.total >= 128 || (wd[0] | wd[1] | wd[2] | wd[3]) != 0u;
+          }
+          // neighbours' roots in parallel, then ONE unite per distinct root
+          const int rA = uf_find(parent, ra, halve);
+#pragma unroll
+          for (int k = 0; k < kR; ++k) {
+            const int rt = (cls[k] == 1) ? uf_find(parent, rb[k], halve) : -1;
+            bool pend = rt >= 0 && rt != rA;
+            bool mine = false;
+            uint32_t pm = hbal(pend);
+            while (pm) {  // (half-uniform)
+              const int l = h0 + __ffs(pm) - 1;
+              const int v = __shfl(rt, l);
+              mine = mine || (lane == l);
+              pend = pend && (rt != v);
+              pm = hbal(pend);
+            }
+            if (mine) uf_unite(parent, sorig, rA, rt, halve);
+          }
+        }
+      }
+      // cells with undecided candidates -> plist (lane 0 / 32 hold each half's flag)
+      const bool u0 = __shfl((int)any_und, 0) != 0, u1 = __shfl((int)any_und, 32) != 0;
+      if (u0) lmask |= 1ull << l0;
+      if (u1 && l1 >= 0) lmask |= 1ull << l1;
+    }
+    if (plist && lmask) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(pcount, __popcll(lmask));
+      base = __shfl(base, 0);
+      if ((lmask >> lane) & 1ull) plist[base + __popcll(lmask & ((1ull << lane) - 1ull))] = ql;
+    }
+  }
+}
+
 // K6b over the first pass's cell list (2-D): one wave per listed cell, lane l over window
 // positions l and l + 64 of its pmask (a window of >= 128 positions is walked 64 positions at a
 // time instead, classifying again), then k_union_cells<D, true>'s search for each undecided
@@ -3535,6 +3655,7 @@ struct DbscanState {
   uint4* pmask = nullptr;  // union passes' undecided-candidate masks per occupied cell (aliases
                            // the grid build's radix key buffers, dead after the build)
   int union_list = -1;     // RPT_UNION_LIST=0: the second union pass enumerates every window
+  int union_pair = -1;     // RPT_UNION_PAIR=0: one cell per wave in the box-certain union pass
   int uf_compress = -1;    // RPT_UF_COMPRESS=1: a compression pass closes the union stage
   uint32_t* min_bits = nullptr;  // component minima, 1 bit per original index (MinRank)
   int32_t* min_pref = nullptr;   // exclusive popcount prefix of min_bits' words (+ total)
@@ -4022,6 +4143,10 @@ int32_t DbscanState::union_pass(hipStream_t st) {
     const char* e = ab_env("RPT_UNION_LIST");
     union_list = (e && std::atoi(e) == 0) ? 0 : 1;
   }
+  if (union_pair < 0) {
+    const char* e = ab_env("RPT_UNION_PAIR");
+    union_pair = (e && std::atoi(e) == 0) ? 0 : 1;
+  }
   // 2-D: the first union pass lists its cells with undecided candidates in nc_list (free until
   // the label pass), their count at nc_list[n] (zeroed by k_init_occ_cells)
   const bool listing = union_list && dim == 2;
@@ -4037,9 +4162,14 @@ int32_t DbscanState::union_pass(hipStream_t st) {
                      mutual, cmin, C, rep);
   if (dim == 2) {
     uint4* pm = listing ? pmask : nullptr;
-    hipLaunchKernelGGL((k_union_cells<2, false>), dim3(gw), dim3(kBlock), 0, st, pts, g,
-                       cell_start, occ, n_occ, rec<2>(), occ_bits, slab_t, core, rep, mutual, sorig,
-                       parent, uf_flags, pm, plist, pcount);
+    if (union_pair)  // two cells per wave (RPT_UNION_PAIR=0 in the A/B build: one)
+      hipLaunchKernelGGL(k_union_cells_pair, dim3(gw), dim3(kBlock), 0, st, pts, g, occ, n_occ,
+                         rec<2>(), occ_bits, slab_t, rep, mutual, sorig, parent, uf_flags, pm,
+                         plist, pcount);
+    else
+      hipLaunchKernelGGL((k_union_cells<2, false>), dim3(gw), dim3(kBlock), 0, st, pts, g,
+                         cell_start, occ, n_occ, rec<2>(), occ_bits, slab_t, core, rep, mutual,
+                         sorig, parent, uf_flags, pm, plist, pcount);
     if (listing)
       hipLaunchKernelGGL(k_union_listed, dim3(gw), dim3(kBlock), 0, st, pts, g, occ, rec<2>(),
                          occ_bits, slab_t, core, rep, mutual, sorig, parent, uf_flags, pm, plist,
