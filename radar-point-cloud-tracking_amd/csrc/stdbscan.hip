@@ -2384,7 +2384,8 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
 // cells' dependent load chains (record -> occupancy -> candidate records -> roots) are in flight
 // per wave instead of one.  Same unions, undecided-candidate masks (position p -> bit p of the
 // 128-bit pmask, as k_union_listed reads them) and plist as k_union_cells<2, false>.
-__global__ __launch_bounds__(kBlock) void k_union_cells_pair(
+// 6 waves/SIMD (77 VGPRs, no spill; the unconstrained build took 81 and 5)
+__global__ __launch_bounds__(kBlock, 6) void k_union_cells_pair(
     const float4* __restrict__ pts, Geom g, const int32_t* __restrict__ occ,
     const int32_t* __restrict__ n_occ, const CellRec<2>* __restrict__ crec,
     const uint32_t* __restrict__ occ_bits, const float2* __restrict__ slab_t,
