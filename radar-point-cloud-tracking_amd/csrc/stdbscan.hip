@@ -2552,16 +2552,24 @@ __global__ __launch_bounds__(kBlock) void k_union_listed(const float4* __restric
             pb = pts[jb];
             cb_ok = classify<2>(pb, A1, A2, g) != 0;
           }
-          uint64_t bm = __ballot(cb_ok);
-          while (bm && !hit) {
-            const int lb = __ffsll((unsigned long long)bm) - 1;
-            bm &= bm - 1;
-            const float4 pq = shfl_f4(pb, lb);
-            for (int ja0 = ba; ja0 < ea && !hit; ja0 += 64) {
-              const int ja = ja0 + lane;
-              const bool adj = (ja < ea) && core[ja] && adjacent<2>(pq, pts[ja], g);
-              hit = __ballot(adj) != 0;
+          // this chunk's B core points that can reach A's box (bm) against A's core points 64
+          // at a time: each lane loads ONE A point per chunk and tests it against every such B
+          // point (shuffles, no loads), so an A chunk costs one round trip for all of them (B
+          // point by B point, a pair with no adjacent points walked |B| x |A|/64 round trips)
+          const uint64_t bm = __ballot(cb_ok);
+          for (int ja0 = ba; bm && ja0 < ea && !hit; ja0 += 64) {
+            const int ja = ja0 + lane;
+            const bool va = (ja < ea) && core[ja];
+            const float4 pa = va ? pts[ja] : make_float4(0.f, 0.f, 0.f, 0.f);
+            bool adj = false;
+            uint64_t rest = bm;
+            while (rest) {  // (wave-uniform)
+              const int lb = __ffsll((unsigned long long)rest) - 1;
+              rest &= rest - 1;
+              const float4 pq = shfl_f4(pb, lb);
+              adj = adj || (va && adjacent<2>(pq, pa, g));
             }
+            hit = __ballot(adj) != 0;
           }
         }
         if (hit && lane == 0) uf_unite(parent, sorig, ra, rbl, halve);
