@@ -2855,10 +2855,10 @@ __global__ __launch_bounds__(kBlock) void k_cell_min_key(const int32_t* __restri
 // GLOBAL = true : key = slab (the core point's final label: labels are ranks of the sorted global
 //                 representatives, so the smallest label is the smallest representative).
 template <int D, bool GLOBAL, int W = 64>
-// 7 waves/SIMD (72 VGPRs, one spill): 80 VGPRs left it at 6 and latency-bound (-2 %)
+// 6 waves/SIMD (80 VGPRs, no spill; with two candidate points per lane per round 7 spilled 8)
 // W = 32: two points per wave, one per half (the same candidate loads per point, twice the
 // points in flight: the pass is a chain of dependent loads per point, not bandwidth)
-__global__ __launch_bounds__(kBlock, 7) void k_label(const float4* __restrict__ pts,
+__global__ __launch_bounds__(kBlock, 6) void k_label(const float4* __restrict__ pts,
                                                  const int32_t* __restrict__ skey, Geom g,
                                                  const CellRec<D>* __restrict__ crec,
                                                  const uint32_t* __restrict__ occ_bits,
@@ -2955,21 +2955,28 @@ __global__ __launch_bounds__(kBlock, 7) void k_label(const float4* __restrict__ 
             }
           if (lane == l) pend &= ~(1u << kl);
           const int bl = __shfl(bsel, l), el = __shfl(esel, l);
+          // two points per lane per round (their loads issued together): a dense cell costs
+          // half the dependent round trips
           if (__shfl(msel, l)) {  // one component: a single adjacent core point decides
             bool hit = false;
-            for (int j0 = bl; j0 < el && !hit; j0 += W) {
-              const int j = j0 + hl;
-              hit = gbal((j < el) && key_of[j] >= 0 && adjacent<D>(p, pts[j], g)) != 0;
+            for (int j0 = bl; j0 < el && !hit; j0 += 2 * W) {
+              const int j = j0 + hl, j2 = j + W;
+              const bool v1 = j < el, v2 = j2 < el;
+              const int k1 = v1 ? key_of[j] : -1, k2 = v2 ? key_of[j2] : -1;
+              const float4 p1 = v1 ? pts[j] : p, p2 = v2 ? pts[j2] : p;
+              hit = gbal((k1 >= 0 && adjacent<D>(p, p1, g)) ||
+                         (k2 >= 0 && adjacent<D>(p, p2, g))) != 0;
             }
             if (hit) best = mm;
           } else {
             int lb = INT_MAX;
-            for (int j0 = bl; j0 < el; j0 += W) {
-              const int j = j0 + hl;
-              if (j < el) {
-                const int m = key_of[j];
-                if (m >= 0 && m < best && m < lb && adjacent<D>(p, pts[j], g)) lb = m;
-              }
+            for (int j0 = bl; j0 < el; j0 += 2 * W) {
+              const int j = j0 + hl, j2 = j + W;
+              const bool v1 = j < el, v2 = j2 < el;
+              const int m1 = v1 ? key_of[j] : -1, m2 = v2 ? key_of[j2] : -1;
+              const float4 p1 = v1 ? pts[j] : p, p2 = v2 ? pts[j2] : p;
+              if (m1 >= 0 && m1 < best && m1 < lb && adjacent<D>(p, p1, g)) lb = m1;
+              if (m2 >= 0 && m2 < best && m2 < lb && adjacent<D>(p, p2, g)) lb = m2;
             }
             best = min(best, gmin(lb));
           }
