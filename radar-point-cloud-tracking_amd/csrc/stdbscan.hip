@@ -2391,19 +2391,23 @@ __global__ __launch_bounds__(kBlock, 6) void k_union_cells_pair(
     const uint32_t* __restrict__ occ_bits, const float2* __restrict__ slab_t,
     const int32_t* __restrict__ rep, const uint8_t* __restrict__ mutual,
     const int32_t* __restrict__ sorig, int32_t* __restrict__ parent, int uf_flags,
-    uint4* __restrict__ pmask, int32_t* __restrict__ plist, int32_t* __restrict__ pcount) {
+    uint4* __restrict__ pmask, int32_t* __restrict__ plist, int32_t* __restrict__ pcount,
+    int cpw) {
   constexpr int W = 32;
   const int lane = threadIdx.x & 63;
   const int hl = lane & (W - 1), h0 = lane - hl;
   auto hbal = [&](bool v) -> uint32_t { return (uint32_t)(__ballot(v) >> h0); };
   const bool halve = !(uf_flags & 1);
   const int64_t no = *n_occ;
-  const int64_t items = (no + 63) / 64;
+  // cpw (<= 64) occupied cells per wave iteration: 64 on large stacks (one header load per lane),
+  // fewer on small ones, whose waves would otherwise each walk dozens of cells in turn while most
+  // of the GPU idles
+  const int64_t items = (no + cpw - 1) / cpw;
   const XcdRange xr = xcd_items(items, (uf_flags & 2) != 0);
   for (int64_t it = xr.first; it < xr.end; it += xr.step) {
     int ql = -1, cal = INT_MAX, ral = -1;
     uint8_t mal = 0;
-    if (it * 64 + lane < no) ql = (int)(it * 64 + lane);
+    if (lane < cpw && it * cpw + lane < no) ql = (int)(it * cpw + lane);
     if (ql >= 0) cal = occ[ql];
     if ((int64_t)cal < g.cells) {  // (not the isolated, non-finite time cell)
       ral = rep[cal];
@@ -4181,7 +4185,7 @@ int32_t DbscanState::union_pass(hipStream_t st) {
     if (union_pair)  // two cells per wave (RPT_UNION_PAIR=0 in the A/B build: one)
       hipLaunchKernelGGL(k_union_cells_pair, dim3(gw), dim3(kBlock), 0, st, pts, g, occ, n_occ,
                          rec<2>(), occ_bits, slab_t, rep, mutual, sorig, parent, uf_flags, pm,
-                         plist, pcount);
+                         plist, pcount, n > (int64_t(1) << 24) ? 64 : 16);
     else
       hipLaunchKernelGGL((k_union_cells<2, false>), dim3(gw), dim3(kBlock), 0, st, pts, g,
                          cell_start, occ, n_occ, rec<2>(), occ_bits, slab_t, core, rep, mutual,
