@@ -272,6 +272,7 @@ __device__ __forceinline__ int nth_bit16(uint32_t m, uint32_t n) {
 // them.  The count pass writes one kept count per GROUP; the write pass walks the group's rows in
 // order and carries the in-file rank across them, so no per-row reduction or prefix is needed.
 constexpr int kGroupRows = 4;  // k_group_write_u8 selects the rows' geometry among 4
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 struct GroupMap {
   uint32_t gpf;   // groups per file = ceil(rows / kGroupRows)
@@ -360,9 +361,13 @@ __global__ __launch_bounds__(kBlock) void k_group_count_u8(const uint8_t* __rest
     group_rows(gm, grp, &f, &row0, &nr);
     uint4 v[kGroupRows];
 #pragma unroll
-    for (int k = 0; k < kGroupRows; ++k)
-      v[k] = (k < nr) ? *reinterpret_cast<const uint4*>(echo + (row0 + k) * 1024 + lane * 16)
-                      : make_uint4(0u, 0u, 0u, 0u);
+    for (int k = 0; k < kGroupRows; ++k) {
+      // streamed once: non-temporal loads keep the echo out of L2's reuse set
+      const u32x4 q = (k < nr) ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
+                                     echo + (row0 + k) * 1024 + lane * 16))
+                               : u32x4{0u, 0u, 0u, 0u};
+      v[k] = make_uint4(q.x, q.y, q.z, q.w);
+    }
     if constexpr (STAGE) {
       uint32_t m[kGroupRows];
       int c[kGroupRows], incl[kGroupRows];

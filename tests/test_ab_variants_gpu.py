@@ -84,3 +84,27 @@ def test_ab_kernel_forms_match_shipped_library(gpu, combo):
         for k in ref:
             np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{k} with {COMBOS[combo]}")
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("combo", range(len(COMBOS)))
+def test_ab_kernel_forms_sharded_match_single(gpu, combo):
+    """The frame-sharded path (2 gloo ranks on cuda:0, librpt's rpt_shard_* driver; the sharded
+    labelling step reads the cell roots the switches change) on librpt_ab.so with each switch set:
+    rank 0 checks it against the single-GPU stack of the same build and switches, which the test
+    above ties to the shipped library (tools/dist_check.py, as tests/test_dist_gpu.py)."""
+    from pathlib import Path
+
+    from rpt import _build
+    from test_dist_gpu import _free_port
+
+    root = Path(__file__).resolve().parents[1]
+    env = dict(os.environ, RPT_LIB=str(_build.LIB_AB), **COMBOS[combo])
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           str(root / "tools" / "dist_check.py"), "--backend", "gloo", "--frames", "14",
+           "--impl", "native", "--lanes", "1"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=600)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "ok=True" in out, out[-4000:]
