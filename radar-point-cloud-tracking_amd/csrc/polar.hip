@@ -538,9 +538,9 @@ __global__ __launch_bounds__(kBlock) void k_group_write_u8(
 constexpr int kGsBits = 40;
 constexpr uint64_t kGsMask = (1ull << kGsBits) - 1ull;
 constexpr uint64_t kUnstaged = 1ull << 63;
-constexpr int kTileOut = 1024;  // outputs per block tile, 4 per thread
+constexpr int kTileOut = 1024;  // outputs per block tile, 4 per thread (8: 86 VGPRs, slower)
 constexpr int kOutPerThread = kTileOut / kBlock;
-static_assert(kOutPerThread == 4, "k_expand_write stores a thread's outputs as one 16-B vector");
+static_assert(kOutPerThread % 4 == 0, "k_expand_write stores a thread's outputs as 16-B vectors");
 constexpr int kWin = 1024;  // groups in the LDS window
 
 __global__ __launch_bounds__(kBlock) void k_group_starts(const int64_t* __restrict__ gprefix,
@@ -636,13 +636,29 @@ __global__ __launch_bounds__(kBlock) void k_expand_write(
     if (threadIdx.x == 0) s_glo = g;
   }
   __syncthreads();
+  // the window of the next tile is loaded into registers while this tile's entries, geometry and
+  // stores are in flight (its first group is known once phase A has searched this window)
+  constexpr int kWinPer = kWin / kBlock;
+  uint64_t wv[kWinPer];
+  auto load_win = [&](uint32_t glo_) {
+    const uint32_t wn_ = min((uint32_t)kWin, n_groups - glo_);
+#pragma unroll
+    for (int q = 0; q < kWinPer; ++q) {
+      const uint32_t j = threadIdx.x + q * kBlock;
+      wv[q] = j < wn_ ? gword[glo_ + j] : ~0ull;
+    }
+  };
+  auto store_win = [&]() {
+#pragma unroll
+    for (int q = 0; q < kWinPer; ++q) s_win[threadIdx.x + q * kBlock] = wv[q];
+  };
+  uint32_t glo = s_glo;
+  load_win(glo);
+  store_win();
+  __syncthreads();
   const float inv_bins = 1.0f / 1024.0f;  // exact: step = scale / 1024 == scale * 2^-10
   for (int64_t t = t0; t < t1; ++t) {
-    const uint32_t glo = s_glo;
     const uint32_t wn = min((uint32_t)kWin, n_groups - glo);
-    for (uint32_t j = threadIdx.x; j < (uint32_t)kWin; j += kBlock)
-      s_win[j] = j < wn ? gword[glo + j] : ~0ull;
-    __syncthreads();
     const bool truncated = glo + wn < n_groups;
     const uint64_t O0 = (uint64_t)t * kTileOut;
     // phase A: this thread's kOutPerThread consecutive outputs: the first one's group by the LDS
@@ -672,7 +688,8 @@ __global__ __launch_bounds__(kBlock) void k_expand_write(
         }
         ok[k] = in && !(w & kUnstaged);
         grp[k] = g;
-        idx[k] = (uint32_t)((O - (w & kGsMask)) * stride + ((w & ~kUnstaged) >> kGsBits));
+        // mod 2^32 like the 64-bit form (only staged groups use it: idx < kStageSlots)
+        idx[k] = ((uint32_t)O - (uint32_t)w) * stride + (uint32_t)((w & ~kUnstaged) >> kGsBits);
       }
     } else {
 #pragma unroll
@@ -689,22 +706,44 @@ __global__ __launch_bounds__(kBlock) void k_expand_write(
       s_glo = (j == wn - 1u && truncated) ? thread_find_group(gword, glo + j, n_groups, On)
                                           : glo + j;
     }
+    __syncthreads();  // every search of this window done; s_glo of the next tile visible
+    if (t + 1 < t1) {
+      glo = s_glo;
+      load_win(glo);
+    }
     // phase B: the staged entries, then the rows' geometry, then the stores
     uint32_t ent[kOutPerThread];
-#pragma unroll
-    for (int k = 0; k < kOutPerThread; ++k)
-      ent[k] = ok[k] ? entries[(int64_t)grp[k] * kStageSlots + idx[k]] : 0u;
-    float sc[kOutPerThread], cc[kOutPerThread], ss[kOutPerThread];
-    uint32_t fl[kOutPerThread];
+    // every load unconditional (a slot that writes nothing reads entry 0 / its group's first
+    // row) and masked by selects: conditional loads would each end in a full vmcnt wait
 #pragma unroll
     for (int k = 0; k < kOutPerThread; ++k) {
-      const uint32_t f = grp[k] / gm.gpf;
+      const uint32_t e = entries[ok[k] ? (int64_t)grp[k] * kStageSlots + idx[k] : 0];
+      ent[k] = ok[k] ? e : 0u;
+    }
+    float sc[kOutPerThread], cc[kOutPerThread], ss[kOutPerThread];
+    uint32_t fl[kOutPerThread], pfl[kOutPerThread];
+    // one division per thread: its outputs' groups are grp[0] or a few after it (steps over
+    // file / frame boundaries instead of dividing again)
+    const uint32_t f0 = grp[0] / gm.gpf, r0 = grp[0] - f0 * gm.gpf;
+    const uint32_t fpf = (uint32_t)files_per_frame, p0 = f0 / fpf, q0 = f0 - p0 * fpf;
+#pragma unroll
+    for (int k = 0; k < kOutPerThread; ++k) {
+      uint32_t f = f0, r = r0 + (grp[k] - grp[0]);
+      while (r >= gm.gpf) {
+        r -= gm.gpf;
+        ++f;
+      }
+      uint32_t pf = p0, q = q0 + (f - f0);
+      while (q >= fpf) {
+        q -= fpf;
+        ++pf;
+      }
       fl[k] = f;
-      const int64_t row = (int64_t)f * gm.rows +
-                          (int64_t)(grp[k] - f * gm.gpf) * kGroupRows + (ent[k] >> 18);
-      sc[k] = ok[k] ? scale[row] : 0.f;
-      cc[k] = ok[k] ? cos_t[row] : 0.f;
-      ss[k] = ok[k] ? sin_t[row] : 0.f;
+      pfl[k] = pf;
+      const int64_t row = (int64_t)f * gm.rows + (int64_t)r * kGroupRows + (ent[k] >> 18);
+      sc[k] = scale[row];
+      cc[k] = cos_t[row];
+      ss[k] = sin_t[row];
     }
     float ox[kOutPerThread], oy[kOutPerThread], ov[kOutPerThread];
     int32_t og[kOutPerThread], op[kOutPerThread];
@@ -716,15 +755,21 @@ __global__ __launch_bounds__(kBlock) void k_expand_write(
       oy[k] = rr * ss[k];
       ov[k] = (float)(ent[k] & 0xffu);
       og[k] = gain ? gain[fl[k]] : 0;
-      op[k] = (int32_t)(fl[k] / (uint32_t)files_per_frame);
+      op[k] = (int32_t)pfl[k];
       all_ok = all_ok && ok[k];
     }
     if (VEC && all_ok) {  // 16-B stores (the common case)
-      *reinterpret_cast<float4*>(x + Ob) = make_float4(ox[0], ox[1], ox[2], ox[3]);
-      *reinterpret_cast<float4*>(y + Ob) = make_float4(oy[0], oy[1], oy[2], oy[3]);
-      *reinterpret_cast<float4*>(val + Ob) = make_float4(ov[0], ov[1], ov[2], ov[3]);
-      if (gain_out) *reinterpret_cast<int4*>(gain_out + Ob) = make_int4(og[0], og[1], og[2], og[3]);
-      if (pf_out) *reinterpret_cast<int4*>(pf_out + Ob) = make_int4(op[0], op[1], op[2], op[3]);
+#pragma unroll
+      for (int h = 0; h < kOutPerThread; h += 4) {
+        const uint64_t o = Ob + h;
+        *reinterpret_cast<float4*>(x + o) = make_float4(ox[h], ox[h + 1], ox[h + 2], ox[h + 3]);
+        *reinterpret_cast<float4*>(y + o) = make_float4(oy[h], oy[h + 1], oy[h + 2], oy[h + 3]);
+        *reinterpret_cast<float4*>(val + o) = make_float4(ov[h], ov[h + 1], ov[h + 2], ov[h + 3]);
+        if (gain_out)
+          *reinterpret_cast<int4*>(gain_out + o) = make_int4(og[h], og[h + 1], og[h + 2], og[h + 3]);
+        if (pf_out)
+          *reinterpret_cast<int4*>(pf_out + o) = make_int4(op[h], op[h + 1], op[h + 2], op[h + 3]);
+      }
     } else {
 #pragma unroll
       for (int k = 0; k < kOutPerThread; ++k) {
@@ -737,7 +782,8 @@ __global__ __launch_bounds__(kBlock) void k_expand_write(
         if (pf_out) pf_out[oo] = op[k];
       }
     }
-    __syncthreads();  // s_win and s_glo of the next tile
+    if (t + 1 < t1) store_win();
+    __syncthreads();  // the next tile's window
   }
 }
 
