@@ -1527,19 +1527,33 @@ __global__ __launch_bounds__(kBlock) void k_core_fill(const int32_t* __restrict_
       for (int k = 0; k < kItems; ++k) {
         const int64_t s = tile + (int64_t)k * kBlock + threadIdx.x;
         const int kk = key[k];
-        uint64_t v = (f[k] == 1 && kk >= 0 && (int64_t)kk < cells)
-                         ? (((uint64_t)so[k] << 32) | (uint32_t)s)
-                         : ~0ull;
+        // sorted keys: a run of equal keys is one cell; dist = lanes since this lane's run head
+        const int prevk = __shfl_up(kk, 1, 64), next = __shfl_down(kk, 1, 64);
+        const uint64_t hm = __ballot(lane == 0 || prevk != kk);
+        const uint64_t upto = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
+        const int dist = lane - (63 - __builtin_clzll(hm & upto));
+        const bool in = f[k] == 1 && kk >= 0 && (int64_t)kk < cells;
+        const bool tail = (lane == 63 || next != kk) && kk >= 0;
+        if (n < (int64_t(1) << 26)) {  // kernel-uniform: (original << 6 | lane) fits 32 bits
+          uint32_t v = in ? ((so[k] << 6) | (uint32_t)lane) : ~0u;
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {  // sorted keys: equal at distance off = same run
-          const uint32_t olo = (uint32_t)__shfl_up((int)(uint32_t)v, off, 64);
-          const uint32_t ohi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), off, 64);
-          const int ok = __shfl_up(kk, off, 64);
-          if (lane >= off && ok == kk) v = min(v, ((uint64_t)ohi << 32) | olo);
+          for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t o = (uint32_t)__shfl_up((int)v, off, 64);
+            if (off <= dist) v = min(v, o);
+          }
+          if (tail && v != ~0u)
+            atomicMin(cmin + kk, ((unsigned long long)(v >> 6) << 32) |
+                                     (uint32_t)(s - lane + (int)(v & 63u)));
+        } else {
+          uint64_t v = in ? (((uint64_t)so[k] << 32) | (uint32_t)s) : ~0ull;
+#pragma unroll
+          for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t olo = (uint32_t)__shfl_up((int)(uint32_t)v, off, 64);
+            const uint32_t ohi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), off, 64);
+            if (off <= dist) v = min(v, ((uint64_t)ohi << 32) | olo);
+          }
+          if (tail && v != ~0ull) atomicMin(cmin + kk, (unsigned long long)v);
         }
-        const int next = __shfl_down(kk, 1, 64);
-        if ((lane == 63 || next != kk) && kk >= 0 && v != ~0ull)
-          atomicMin(cmin + kk, (unsigned long long)v);
       }
     }
     if (QUEUE) block_append_bits(tile, bits, slow, n_slow);
