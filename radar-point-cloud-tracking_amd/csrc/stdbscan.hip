@@ -2802,13 +2802,16 @@ __global__ __launch_bounds__(kBlock) void k_ccmin(int32_t* parent,
       for (int k = 0; k < kItems; ++k) {
         int v = (m[k] >= 0 && (int64_t)key[k] < cells) ? m[k] : INT_MAX;
         const int kk = key[k];
+        // sorted keys: a run of equal keys is one cell; dist = lanes since this lane's run head
+        const int prevk = __shfl_up(kk, 1, 64), next = __shfl_down(kk, 1, 64);
+        const uint64_t hm = __ballot(lane == 0 || prevk != kk);
+        const uint64_t upto = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
+        const int dist = lane - (63 - __builtin_clzll(hm & upto));
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {  // sorted keys: equal at distance off = run
+        for (int off = 1; off < 64; off <<= 1) {
           const int ov = __shfl_up(v, off, 64);
-          const int ok = __shfl_up(kk, off, 64);
-          if (lane >= off && ok == kk) v = min(v, ov);
+          if (off <= dist) v = min(v, ov);
         }
-        const int next = __shfl_down(kk, 1, 64);
         if ((lane == 63 || next != kk) && kk >= 0 && v != INT_MAX) atomicMin(cell_key + kk, v);
       }
     }
