@@ -2144,20 +2144,42 @@ __global__ __launch_bounds__(kBlock) void k_init_occ_cells(const int32_t* __rest
 
 // Star initialisation from k_cell_min_pair: core points of a mutual cell under the cell's
 // representative, other points roots; the representative records itself in rep.
+// kPU points per thread per tile, every load branch-free (clamped indices, results masked by
+// selects) so each tile costs two rounds of memory latency: keys + flags, then the cells' minima.
+constexpr int kPU = 8;
 __global__ __launch_bounds__(kBlock) void k_parent_init_pair(
     int32_t* __restrict__ parent, int64_t n, const uint8_t* __restrict__ core,
     const int32_t* __restrict__ skey, const uint8_t* __restrict__ mutual,
     const unsigned long long* __restrict__ cmin, int64_t cells, int32_t* __restrict__ rep) {
-  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
-       s += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t k = skey[s];
-    int32_t p = (int32_t)s;
-    if (core[s] && (int64_t)k < cells) {
-      const int32_t r = (int32_t)(uint32_t)cmin[k];
-      if (r == (int32_t)s) rep[k] = r;
-      if (mutual[k]) p = r;
+  for (int64_t tile = (int64_t)blockIdx.x * kBlock * kPU; tile < n;
+       tile += (int64_t)gridDim.x * kBlock * kPU) {
+    int32_t k[kPU];
+    uint32_t c[kPU];
+#pragma unroll
+    for (int u = 0; u < kPU; ++u) {
+      const int64_t s = min(tile + (int64_t)u * kBlock + threadIdx.x, n - 1);
+      k[u] = skey[s];
+      c[u] = core[s];
     }
-    parent[s] = p;
+    bool q[kPU];
+    unsigned long long m[kPU];
+    uint32_t mu[kPU];
+#pragma unroll
+    for (int u = 0; u < kPU; ++u) {
+      q[u] = c[u] != 0u && k[u] >= 0 && (int64_t)k[u] < cells;
+      const int32_t kk = q[u] ? k[u] : 0;  // cells >= 1 whenever n >= 1
+      m[u] = cmin[kk];
+      mu[u] = mutual[kk];
+    }
+#pragma unroll
+    for (int u = 0; u < kPU; ++u) {
+      const int64_t s = tile + (int64_t)u * kBlock + threadIdx.x;
+      if (s < n) {
+        const int32_t r = (int32_t)(uint32_t)m[u];
+        if (q[u] && r == (int32_t)s) rep[k[u]] = r;
+        parent[s] = (q[u] && mu[u]) ? r : (int32_t)s;
+      }
+    }
   }
 }
 
@@ -4195,8 +4217,8 @@ int32_t DbscanState::union_pass(hipStream_t st) {
   if (!cmin_ready)
     hipLaunchKernelGGL(k_cell_min_pair, dim3(gb), dim3(kBlock), 0, st, skey, core, sorig, n, C,
                        cmin);
-  hipLaunchKernelGGL(k_parent_init_pair, dim3(gb), dim3(kBlock), 0, st, parent, n, core, skey,
-                     mutual, cmin, C, rep);
+  hipLaunchKernelGGL(k_parent_init_pair, dim3(grid_for(n, kBlock * kPU, 2048)), dim3(kBlock), 0,
+                     st, parent, n, core, skey, mutual, cmin, C, rep);
   if (dim == 2) {
     uint4* pm = listing ? pmask : nullptr;
     if (union_pair)  // two cells per wave (RPT_UNION_PAIR=0 in the A/B build: one)
