@@ -382,9 +382,12 @@ __global__ __launch_bounds__(kCompBlock) void k_land_tile_counts(const int32_t* 
     const int64_t i = i0 + (int64_t)k * kCompBlock;
     cl[k] = (i < n) ? cell[i] : -1;
   }
+  uint32_t lnd[kCompItems];  // branch-free: the flags' loads in flight together (>= 1 cell)
+#pragma unroll
+  for (int k = 0; k < kCompItems; ++k) lnd[k] = land[cl[k] >= 0 ? cl[k] : 0];
   int c = 0;
 #pragma unroll
-  for (int k = 0; k < kCompItems; ++k) c += (cl[k] >= 0 && !land[cl[k]]) ? 1 : 0;
+  for (int k = 0; k < kCompItems; ++k) c += (cl[k] >= 0 && !lnd[k]) ? 1 : 0;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
   __shared__ int ws[kCompBlock / 64];
@@ -415,9 +418,14 @@ __global__ __launch_bounds__(kCompBlock) void k_land_compact(
     const int64_t i = i0 + (int64_t)k * kCompBlock;
     cl[k] = (i < n) ? cell[i] : -1;
   }
+  // every load below is branch-free (clamped index, result masked) so a thread's loads of a batch
+  // are in flight together: conditional loads each ended in a full vmcnt wait
+  uint32_t lnd[kCompItems];
+#pragma unroll
+  for (int k = 0; k < kCompItems; ++k) lnd[k] = land[cl[k] >= 0 ? cl[k] : 0];  // >= 1 cell
   uint32_t km = 0;
 #pragma unroll
-  for (int k = 0; k < kCompItems; ++k) km |= (cl[k] >= 0 && !land[cl[k]]) ? (1u << k) : 0u;
+  for (int k = 0; k < kCompItems; ++k) km |= (cl[k] >= 0 && !lnd[k]) ? (1u << k) : 0u;
   __shared__ int cw[kCompItems * NW];  // per (item k, wave) counts, then their exclusive scan
 #pragma unroll
   for (int k = 0; k < kCompItems; ++k) {
@@ -440,22 +448,38 @@ __global__ __launch_bounds__(kCompBlock) void k_land_compact(
   const int64_t tb = tile_base[blockIdx.x];
   uint32_t mnx = 0xffffffffu, mxx = 0u, mny = 0xffffffffu, mxy = 0u;
   int mnf = INT_MAX, mxf = INT_MIN, flags = 0;
-#pragma unroll 4
-  for (int k = 0; k < kCompItems; ++k) {
+  constexpr int kB = 4;  // items per batch of loads
+#pragma unroll
+  for (int k0 = 0; k0 < kCompItems; k0 += kB) {
+    int fb[kB], fp[kB], gb[kB];
+    float xb[kB], yb[kB], vb[kB];
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      const int64_t i = min(i0 + (int64_t)(k0 + u) * kCompBlock, n - 1);
+      fb[u] = pf[i];
+      fp[u] = pf[i > 0 ? i - 1 : 0];
+      xb[u] = x[i];
+      yb[u] = y[i];
+      vb[u] = v[i];
+      gb[u] = go ? g[i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+    const int k = k0 + u;
     const int64_t i = i0 + (int64_t)k * kCompBlock;
     const bool kp = (km >> k) & 1u;
     const uint64_t bk = __ballot(kp);
     if (i < n) {
-      const int f = pf[i];
+      const int f = fb[u];
       // input order; the kept points descend only if the input does
-      if (i > 0 && f < pf[i - 1]) flags |= 2;
+      if (i > 0 && f < fp[u]) flags |= 2;
       if (kp) {
         const int64_t o = tb + cw[k * NW + w] + __popcll(bk & lt);
-        const float px = x[i], py = y[i];
+        const float px = xb[u], py = yb[u];
         xo[o] = px;
         yo[o] = py;
-        vo[o] = v[i];
-        if (go) go[o] = g[i];
+        vo[o] = vb[u];
+        if (go) go[o] = gb[u];
         pfo[o] = f;
         to[o] = (float)f;
         if (!isfinite(px) || !isfinite(py)) flags |= 1;
@@ -467,6 +491,7 @@ __global__ __launch_bounds__(kCompBlock) void k_land_compact(
         mnf = min(mnf, f);
         mxf = max(mxf, f);
       }
+    }
     }
   }
 #pragma unroll

@@ -2857,10 +2857,31 @@ __global__ __launch_bounds__(kBlock) void k_label_core(const int32_t* __restrict
                                                       const int32_t* __restrict__ sorig,
                                                       MinRank cid,
                                                       int32_t* __restrict__ labels) {
-  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
-       s += (int64_t)gridDim.x * blockDim.x) {
-    const int own = ccmin[s];
-    if (own >= 0) labels[sorig[s]] = cid[own];
+  // kPU points per thread per tile, loads branch-free (clamped, masked): two memory rounds per
+  // tile (ccmin + sorig, then the rank words) instead of two per point
+  for (int64_t tile = (int64_t)blockIdx.x * kBlock * kPU; tile < n;
+       tile += (int64_t)gridDim.x * kBlock * kPU) {
+    int32_t own[kPU], so[kPU];
+#pragma unroll
+    for (int u = 0; u < kPU; ++u) {
+      const int64_t s = min(tile + (int64_t)u * kBlock + threadIdx.x, n - 1);
+      own[u] = ccmin[s];
+      so[u] = sorig[s];
+    }
+    uint32_t w[kPU];
+    int32_t pr[kPU];
+#pragma unroll
+    for (int u = 0; u < kPU; ++u) {
+      const int32_t m = own[u] >= 0 ? own[u] : 0;
+      w[u] = cid.bits[m >> 5];
+      pr[u] = cid.pref[m >> 5];
+    }
+#pragma unroll
+    for (int u = 0; u < kPU; ++u) {
+      const int64_t s = tile + (int64_t)u * kBlock + threadIdx.x;
+      if (s < n && own[u] >= 0)
+        labels[so[u]] = pr[u] + __popc(w[u] & ((1u << (own[u] & 31)) - 1u));
+    }
   }
 }
 
@@ -4302,7 +4323,8 @@ int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hi
   hipLaunchKernelGGL(k_fill_i32, dim3(gc), dim3(kBlock), 0, st, cell_min, C, INT_MAX);
   RPT_TRY(cluster_ids(st, cell_min));  // also the per-cell smallest keys (k_cell_min_key fused)
   const MinRank mr{min_bits, min_pref};
-  hipLaunchKernelGGL(k_label_core, dim3(gb), dim3(kBlock), 0, st, ccmin, n, sorig, mr, labels);
+  hipLaunchKernelGGL(k_label_core, dim3(grid_for(n, kBlock * kPU, 2048)), dim3(kBlock), 0, st,
+                     ccmin, n, sorig, mr, labels);
   if (use_label_tiles())
     hipLaunchKernelGGL((k_label_tiles<false>), dim3(tile_grid_blocks()), dim3(kTileBlock), 0, st,
                        g, tile_R, tile_by, tile_nbands, (int64_t)g.nt * tile_nbands, occ,
@@ -4443,7 +4465,8 @@ int32_t DbscanState::labels_fifo(int32_t* labels, rpt_stdbscan_stats* stats, hip
   hipLaunchKernelGGL(k_inverse_perm, dim3(gb), dim3(kBlock), 0, st, sorig, n, spos);
   RPT_CHECK_LAUNCH();
   const MinRank mr{min_bits, min_pref};
-  hipLaunchKernelGGL(k_label_core, dim3(gb), dim3(kBlock), 0, st, ccmin, n, sorig, mr, labels);
+  hipLaunchKernelGGL(k_label_core, dim3(grid_for(n, kBlock * kPU, 2048)), dim3(kBlock), 0, st,
+                     ccmin, n, sorig, mr, labels);
   if (dim == 2)
     hipLaunchKernelGGL((k_label_fifo<2>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
                        rec<2>(), occ_bits, slab_t, ccmin, rep, sorig, spos, mr, nc_list,
