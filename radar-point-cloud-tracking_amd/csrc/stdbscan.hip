@@ -1500,15 +1500,20 @@ __global__ __launch_bounds__(kBlock) void k_core_fill(const int32_t* __restrict_
        tile += (int64_t)gridDim.x * kBlock * kItems) {
     // all keys, then all cell flags, in flight together (two rounds of memory latency per tile,
     // not two per item)
+    // branch-free (clamped indices, results masked): each level's loads in flight together
     int32_t key[kItems];
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
       const int64_t s = tile + (int64_t)k * kBlock + threadIdx.x;
-      key[k] = (s < n) ? skey[s] : -1;
+      const int32_t kv = skey[min(s, n - 1)];
+      key[k] = (s < n) ? kv : -1;
     }
     int f[kItems];
 #pragma unroll
-    for (int k = 0; k < kItems; ++k) f[k] = (key[k] >= 0) ? cflag[key[k]] : 0;
+    for (int k = 0; k < kItems; ++k) {
+      const int32_t fv = cflag[key[k] >= 0 ? key[k] : 0];
+      f[k] = (key[k] >= 0) ? fv : 0;
+    }
     uint32_t bits = 0;
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
@@ -2790,20 +2795,27 @@ __global__ __launch_bounds__(kBlock) void k_ccmin(int32_t* parent,
     int32_t key[kItems], x[kItems];
     uint32_t cbits = 0, inb = 0;
 #pragma unroll
+    // levels 1, 2 and 4 load branch-free (clamped indices, results masked), so each level's
+    // loads are in flight together; only the parent-chain walk (points outside mutual cells)
+    // stays conditional
     for (int k = 0; k < kItems; ++k) {
       const int64_t s = tile + (int64_t)k * kBlock + threadIdx.x;
-      key[k] = -1;
-      if (s < n) {
-        inb |= 1u << k;
-        if (skey) key[k] = skey[s];
-        if (core[s]) cbits |= 1u << k;
-      }
+      const int64_t sc = min(s, n - 1);
+      const int32_t kv = skey ? skey[sc] : -1;  // kernel-uniform pointer test
+      const uint8_t cv = core[sc];
+      const bool in = s < n;
+      key[k] = in ? kv : -1;
+      inb |= in ? (1u << k) : 0u;
+      cbits |= (in && cv) ? (1u << k) : 0u;
     }
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
       x[k] = -1;
-      if (((cbits >> k) & 1u) && cell_root && key[k] >= 0 && (int64_t)key[k] < cells)
-        x[k] = cell_root[key[k]];
+      if (cell_root) {  // kernel-uniform
+        const bool q = ((cbits >> k) & 1u) && key[k] >= 0 && (int64_t)key[k] < cells;
+        const int32_t r = cell_root[q ? key[k] : 0];  // cells >= 1
+        x[k] = q ? r : -1;
+      }
     }
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
@@ -2812,7 +2824,11 @@ __global__ __launch_bounds__(kBlock) void k_ccmin(int32_t* parent,
     }
     int m[kItems];
 #pragma unroll
-    for (int k = 0; k < kItems; ++k) m[k] = ((cbits >> k) & 1u) ? sorig[x[k]] : -1;
+    for (int k = 0; k < kItems; ++k) {
+      const bool c = (cbits >> k) & 1u;
+      const int32_t v = sorig[c ? x[k] : 0];
+      m[k] = c ? v : -1;
+    }
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
       const int64_t s = tile + (int64_t)k * kBlock + threadIdx.x;
