@@ -400,12 +400,14 @@ __global__ __launch_bounds__(kBucketBlock) void k_slab_bucket(
            cell_of((double)px, g.ox, g.inv_cs, g.nx);
   };
   for (int i0 = lo; i0 < hi; i0 += kBucketBlock * kBucketU) {
+    // loads from clamped indices (the slab is not empty here): a conditional load would be a
+    // branch ending in a full vmcnt wait, one round trip per point instead of per round
     float px[kBucketU], py[kBucketU];
 #pragma unroll
     for (int u = 0; u < kBucketU; ++u) {
-      const int i = i0 + u * kBucketBlock + threadIdx.x;
-      px[u] = (i < hi) ? x[(int64_t)i * stride] : 0.f;
-      py[u] = (i < hi) ? y[(int64_t)i * stride] : 0.f;
+      const int i = min(i0 + u * kBucketBlock + (int)threadIdx.x, hi - 1);
+      px[u] = x[(int64_t)i * stride];
+      py[u] = y[(int64_t)i * stride];
     }
 #pragma unroll
     for (int u = 0; u < kBucketU; ++u) {
@@ -480,10 +482,10 @@ __global__ __launch_bounds__(kBucketBlock) void k_slab_bucket(
     float px[kBucketU], py[kBucketU], pt[kBucketU];
 #pragma unroll
     for (int u = 0; u < kBucketU; ++u) {
-      const int i = i0 + u * kBucketBlock + threadIdx.x;
-      px[u] = (i < hi) ? x[(int64_t)i * stride] : 0.f;
-      py[u] = (i < hi) ? y[(int64_t)i * stride] : 0.f;
-      pt[u] = (i < hi) ? t[i] : 0.f;
+      const int i = min(i0 + u * kBucketBlock + (int)threadIdx.x, hi - 1);  // branch-free
+      px[u] = x[(int64_t)i * stride];
+      py[u] = y[(int64_t)i * stride];
+      pt[u] = t[i];
     }
 #pragma unroll
     for (int u = 0; u < kBucketU; ++u) {
@@ -535,9 +537,9 @@ __global__ __launch_bounds__(kBucketBlock) void k_slab_chunk_hist(
     float px[kBucketU], py[kBucketU];
 #pragma unroll
     for (int u = 0; u < kBucketU; ++u) {
-      const int i = i0 + u * kBucketBlock + threadIdx.x;
-      px[u] = (i < hi) ? x[(int64_t)i * stride] : 0.f;
-      py[u] = (i < hi) ? y[(int64_t)i * stride] : 0.f;
+      const int i = min(i0 + u * kBucketBlock + (int)threadIdx.x, hi - 1);  // branch-free
+      px[u] = x[(int64_t)i * stride];
+      py[u] = y[(int64_t)i * stride];
     }
 #pragma unroll
     for (int u = 0; u < kBucketU; ++u) {
@@ -644,10 +646,10 @@ __global__ __launch_bounds__(kBucketBlock) void k_slab_chunk_scatter(
     float px[kBucketU], py[kBucketU], pt[kBucketU];
 #pragma unroll
     for (int u = 0; u < kBucketU; ++u) {
-      const int i = i0 + u * kBucketBlock + threadIdx.x;
-      px[u] = (i < hi) ? x[(int64_t)i * stride] : 0.f;
-      py[u] = (i < hi) ? y[(int64_t)i * stride] : 0.f;
-      pt[u] = (i < hi) ? t[i] : 0.f;
+      const int i = min(i0 + u * kBucketBlock + (int)threadIdx.x, hi - 1);  // branch-free
+      px[u] = x[(int64_t)i * stride];
+      py[u] = y[(int64_t)i * stride];
+      pt[u] = t[i];
     }
 #pragma unroll
     for (int u = 0; u < kBucketU; ++u) {
