@@ -32,13 +32,26 @@ __global__ __launch_bounds__(kBlock) void k_bounds_xy(const float* __restrict__ 
                                                      const float* __restrict__ y, int64_t n,
                                                      uint32_t* __restrict__ out) {
   uint32_t mnx = 0xffffffffu, mxx = 0u, mny = 0xffffffffu, mxy = 0u;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t a = f2ord(x[i]), b = f2ord(y[i]);
-    mnx = min(mnx, a);
-    mxx = max(mxx, a);
-    mny = min(mny, b);
-    mxy = max(mxy, b);
+  // kBU points per thread per round, loaded together from clamped indices (a repeated valid
+  // point leaves minima and maxima unchanged)
+  constexpr int kBU = 4;
+  for (int64_t b0 = (int64_t)blockIdx.x * blockDim.x * kBU; b0 < n;
+       b0 += (int64_t)gridDim.x * blockDim.x * kBU) {
+    float xs[kBU], ys[kBU];
+#pragma unroll
+    for (int u = 0; u < kBU; ++u) {
+      const int64_t i = min(b0 + (int64_t)u * blockDim.x + threadIdx.x, n - 1);
+      xs[u] = x[i];
+      ys[u] = y[i];
+    }
+#pragma unroll
+    for (int u = 0; u < kBU; ++u) {
+      const uint32_t a = f2ord(xs[u]), b = f2ord(ys[u]);
+      mnx = min(mnx, a);
+      mxx = max(mxx, a);
+      mny = min(mny, b);
+      mxy = max(mxy, b);
+    }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -231,10 +244,10 @@ __global__ __launch_bounds__(kGridBlock) void k_land_grid_lds_u8(
     float px[kU], py[kU], pv[kU];
 #pragma unroll
     for (int k = 0; k < kU; ++k) {
-      const int64_t i = b0 + (int64_t)k * kGridBlock + threadIdx.x;
-      px[k] = i < n ? x[i] : 0.f;
-      py[k] = i < n ? y[i] : 0.f;
-      pv[k] = i < n ? val[i] : 0.f;
+      const int64_t i = min(b0 + (int64_t)k * kGridBlock + threadIdx.x, n - 1);  // branch-free
+      px[k] = x[i];
+      py[k] = y[i];
+      pv[k] = val[i];
     }
 #pragma unroll
     for (int k = 0; k < kU; ++k) {
