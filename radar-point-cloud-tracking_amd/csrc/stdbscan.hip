@@ -3343,23 +3343,55 @@ __global__ __launch_bounds__(kBlock) void k_ccmin_global(int32_t* parent,
                                                         const uint8_t* __restrict__ mutual = nullptr,
                                                         const int32_t* __restrict__ cell_root = nullptr,
                                                         int64_t cells = 0) {
+  // level by level as in k_ccmin (keys + flags, cell roots, originals: branch-free loads, each
+  // level's loads in flight together); only the parent-chain walk stays conditional
   for (int64_t tile = (int64_t)blockIdx.x * kBlock * kItems; tile < n;
        tile += (int64_t)gridDim.x * kBlock * kItems) {
-    block_append(
-        tile, n,
-        [&](int64_t s) -> bool {
-          if (!core[s]) return true;
-          // core points of a mutual cell: their cell's root (k_cell_roots), as in k_ccmin
-          const int32_t key = cell_root ? skey[s] : -1;
-          const int x = (cell_root && key >= 0 && (int64_t)key < cells && mutual[key])
-                            ? cell_root[key]
-                            : uf_find(parent, (int)s);
-          const int m = sorig[x];
-          ccmin[s] = m;
-          if (x == (int)s) gl[m] = rep_id(reps, nr, rep[m]);
-          return false;
-        },
-        nc_list, nc_count);
+    int32_t key[kItems], x[kItems];
+    uint32_t cbits = 0, nbits = 0;
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const int64_t s = tile + (int64_t)k * kBlock + threadIdx.x;
+      const int64_t sc = min(s, n - 1);
+      const int32_t kv = cell_root ? skey[sc] : -1;  // kernel-uniform pointer test
+      const uint8_t cv = core[sc];
+      const bool in = s < n;
+      key[k] = in ? kv : -1;
+      cbits |= (in && cv) ? (1u << k) : 0u;
+      nbits |= (in && !cv) ? (1u << k) : 0u;  // non-core: queued for k_label
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      x[k] = -1;
+      if (cell_root) {  // core points of a mutual cell: their cell's root (k_cell_roots)
+        const bool q = ((cbits >> k) & 1u) && key[k] >= 0 && (int64_t)key[k] < cells;
+        const int32_t kk = q ? key[k] : 0;  // cells >= 1
+        const uint8_t mu = mutual[kk];
+        const int32_t cr = cell_root[kk];
+        x[k] = (q && mu) ? cr : -1;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const int s = (int)(tile + (int64_t)k * kBlock + threadIdx.x);
+      if (((cbits >> k) & 1u) && x[k] < 0) x[k] = uf_find(parent, s);
+    }
+    int m[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const bool c = (cbits >> k) & 1u;
+      const int32_t v = sorig[c ? x[k] : 0];
+      m[k] = c ? v : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const int64_t s = tile + (int64_t)k * kBlock + threadIdx.x;
+      if ((cbits >> k) & 1u) {
+        ccmin[s] = m[k];
+        if (x[k] == (int)s) gl[m[k]] = rep_id(reps, nr, rep[m[k]]);
+      }
+    }
+    block_append_bits(tile, nbits, nc_list, nc_count);
   }
 }
 // slab[s] = final label of core point s (-1 for non-core); core labels written out
