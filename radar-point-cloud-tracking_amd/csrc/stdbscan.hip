@@ -1386,17 +1386,23 @@ __global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
       const float2 own = slab_t[cs];
       float2 sr = make_float2(1.f, 0.f);
       uint32_t m5[5] = {0u, 0u, 0u, 0u, 0u};
-      if (sv) {
-        sr = slab_t[sl];
+      {
+        // branch-free: a lane out of the window reads its own slab's words and masks them off,
+        // so the eleven loads of every lane are in flight together (a conditional load is a
+        // branch ending in a full vmcnt wait)
+        const int slc = sv ? sl : cs;
+        const float2 srv = slab_t[slc];
+        sr = sv ? srv : sr;
         const int lo_x = cx - 2 < 0 ? 2 - cx : 0;
         const int hi_x = cx + 2 - (g.nx - 1);
 #pragma unroll
         for (int dy = 0; dy < 5; ++dy) {
           const int y = cy + dy - 2;
-          if (y < 0 || y >= g.ny) continue;
+          const bool yv = sv && y >= 0 && y < g.ny;
+          const int yc = min(max(y, 0), g.ny - 1);
           // bit dx <-> key k0 + dx (x = cx - 2 + dx); columns outside [0, nx) are cleared
           // (int32 keys: cells < 2^30)
-          const int k0 = (sl * g.ny + y) * g.nx + (cx - 2);
+          const int k0 = (slc * g.ny + yc) * g.nx + (cx - 2);
           const int kk = k0 < 0 ? 0 : k0;
           const int w = kk >> 5;
           const uint32_t lo_w = occ_bits[w], hi_w = occ_bits[w + 1];
@@ -1404,7 +1410,7 @@ __global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
                                 : (__builtin_amdgcn_alignbit(hi_w, lo_w, (uint32_t)(kk & 31)) & 31u);
           m &= ~((1u << lo_x) - 1u);
           if (hi_x > 0) m &= (31u >> hi_x);
-          m5[dy] = m;
+          m5[dy] = yv ? m : 0u;
         }
       }
       const float gap =
@@ -1438,14 +1444,14 @@ __global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
           bool has[kCwBatch];
 #pragma unroll
           for (int i = 0; i < kCwBatch; ++i) {
+            // branch-free record loads (a lane without a candidate re-reads its own cell's)
             has[i] = m25 != 0;
-            if (has[i]) {
-              const int p = __builtin_ctz(m25);
-              m25 &= m25 - 1;
-              const int k = p / 5, dx = p - 5 * k;
-              const int dy = (k == 0) ? 2 : ((k & 1) ? 2 - (k + 1) / 2 : 2 + k / 2);
-              cr[i] = crec[(sl * g.ny + (cy + dy - 2)) * g.nx + (cx + dx - 2)];
-            }
+            const int p = __builtin_ctz(m25 | (1u << 31));
+            m25 &= m25 - 1;
+            const int k = p / 5, dx = p - 5 * k;
+            const int dy = (k == 0) ? 2 : ((k & 1) ? 2 - (k + 1) / 2 : 2 + k / 2);
+            const int key = (sl * g.ny + (cy + dy - 2)) * g.nx + (cx + dx - 2);
+            cr[i] = crec[has[i] ? key : ca];
           }
 #pragma unroll
           for (int i = 0; i < kCwBatch; ++i) {
