@@ -190,8 +190,16 @@ def main():
                          "instead of the native shard driver")
     ap.add_argument("--lanes", type=int, default=None,
                     help="stacks in flight at once (default 3 on one GPU: native handles on "
-                         "separate streams; 1 with N>1 ranks, where a lane is also a process "
-                         "group -- rpt.dist.ShardLanes); 1 = strictly one after another")
+                         "separate streams; with N>1 ranks (or --sharded) see --help's "
+                         "docstring: a lane is a NativeShardPipeline with its own stream and "
+                         "thread, all lanes on ONE process group in rpt.dist.CommSequencer's "
+                         "order); 1 = strictly one after another")
+    ap.add_argument("--sequenced", action="store_true",
+                    help="sharded runs at one rank: keep the CommSequencer's slot order although "
+                         "every collective is the identity (what the ordering costs)")
+    ap.add_argument("--host-workers", type=int, default=8,
+                    help="threads for rank 0's host stage (cluster order + tracker) of "
+                         "consecutive steps")
     ap.add_argument("--no-one-stack", action="store_true",
                     help="skip the one-stack-in-flight leg (and so K5's roofline)")
     ap.add_argument("--sync-host", action="store_true",
@@ -267,7 +275,9 @@ def main():
             from rpt.dist import ShardLanes
 
             lanes_ = ShardLanes(dev, args.lanes, cfg.gains, cfg.rows, cfg.bins, PathParams(),
-                                timing=timing, async_host=not args.sync_host, host_workers=4)
+                                timing=timing, async_host=not args.sync_host,
+                                host_workers=args.host_workers,
+                                sequenced=True if args.sequenced else None)
             lanes_.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t,
                                 ds.geo.sin_t, cfg.n_frames * len(cfg.gains))
             ops = lanes_.pipes[0]
@@ -275,7 +285,8 @@ def main():
         else:
             ops = pipe = NativeShardPipeline(Comm(dev), cfg.gains, cfg.rows, cfg.bins,
                                              PathParams(), timing=timing,
-                                             async_host=not args.sync_host, host_workers=4)
+                                             async_host=not args.sync_host,
+                                             host_workers=args.host_workers)
             pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t,
                               ds.geo.sin_t, cfg.n_frames * len(cfg.gains))
             run = lambda e: pipe.run(e, rank * F)  # noqa: E731
@@ -335,6 +346,23 @@ def main():
     summary["points_per_stack"] = sorted({int(points_of(r)) for r in results})
     value = pts_total / dt / 1e6
     ms_step = dt / args.steps * 1e3
+    # steady state: the steps after the pipeline has filled (the first `lanes` steps) up to the
+    # last step's device completion (the last host stage -- the drain -- excluded); max over ranks
+    steady = None
+    L_ = 1 if args.python_shard else args.lanes
+    if args.steps > L_ + 1:
+        td = [r.t_done for r in results]
+        span = td[-1] - td[L_ - 1]
+        if dist:
+            t = torch.tensor([span], dtype=torch.float64, device=dev)
+            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+            span = float(t[0])
+        pts_ss = sum(points_of(r) for r in results[L_:])
+        steady = {"value": round(pts_ss / span / 1e6, 3), "unit": "Mpoints/s",
+                  "ms_per_step": round(span / (args.steps - L_) * 1e3, 3),
+                  "steps": args.steps - L_,
+                  "note": f"steps {L_}..{args.steps - 1}: from step {L_ - 1}'s device completion "
+                          f"to the last step's (pipeline fill and the last host stage excluded)"}
 
     # one stack in flight (lanes = 1): the same steps strictly one after another.  K5's roofline
     # is taken here, where its kernels have the GPU to themselves (with several stacks in flight
@@ -533,6 +561,7 @@ def main():
                        "host_stage": "inline" if args.sync_host else
                        "overlapped: step k's order+tracker runs on a host thread during step "
                        "k+1's device work; the timed region ends after the last one"},
+            "steady_state": steady,
             "one_stack_in_flight": seq,
             "roofline": roof, "roofline_c4_share": roof_c4, "roofline_configs4_share": roof_c4d,
             "roofline_k1": roof_k1,

@@ -315,21 +315,29 @@ int32_t rpt_stack_points(const rpt_stack* h, float* x, float* y, float* intensit
  * run, before another ST-DBSCAN runs on it (the flags live in that stream's ST-DBSCAN state). */
 int32_t rpt_stack_core_flags(const rpt_stack* h, uint8_t* core, void* stream);
 /* ---- frame-sharded multi-GPU driver ----------------------------------------
- * One rank's phases of ONE global stack whose contiguous frame ranges are spread over ranks; the
- * caller runs the collectives between phases (rpt/dist.py: torch.distributed over RCCL / gloo) on
- * buffers it owns.  Results equal rpt_stack_run over the whole stack.  Sequence per step:
- *   polar -> [all_gather info] -> land_grid -> [all_reduce grid] -> land_apply ->
- *   [all_gather kept/head/tail; halo x,y,t P2P] -> core -> [halo core P2P] -> components ->
- *   [halo component P2P] -> pairs -> [all_gather pairs; rpt_merge_equivalences] -> roots ->
- *   [all_gather roots] -> finish -> segments (rank 0 runs the host order + tracker) */
+ * One rank's phases of ONE global stack whose contiguous frame ranges are spread over ranks
+ * (replaces the whole-stack st_dbscan(frames) of 4_temporal_object_tracker.py:466-506 when the
+ * stack is split over GPUs); the caller runs the collectives between phases (rpt/dist.py:
+ * torch.distributed over RCCL / gloo) on buffers it owns.  Results equal rpt_stack_run over the
+ * whole stack.  Per step (host waits marked *):
+ *   polar* -> [all_gather info*] -> land_grid -> [all_reduce grid] -> halo ->
+ *   [P2P x/y/t, capacities = the neighbours' n_head_k1 / n_tail_k1] -> window* ->
+ *   [P2P core flags] -> link -> [P2P component ids] -> pairs -> [all_gather pairs] ->
+ *   finish -> [all_gather packed results*] -> rpt_shard_host_stage on rank 0.
+ * Point ids are (rank << 40) | own index; labels are numbered per rank and mapped to the global
+ * numbering with the representative tables of the packed results. */
 typedef struct rpt_shard rpt_shard;
 typedef struct rpt_shard_info {
-  int64_t n_points;       /* K1 points of this rank's frames */
-  int32_t n_built;        /* of them, frames with at least one point */
-  int32_t pad0;
-  float bounds[4];        /* min x, max x, min y, max y of the K1 points (+inf/-inf: none) */
-  int64_t n_kept;         /* points after the land filter */
-  int64_t n_head, n_tail; /* kept points of the first / last halo_frames frames */
+  int64_t n_points;        /* K1 points of this rank's frames */
+  int32_t n_built;         /* of them, frames with at least one point */
+  int32_t halo_frames;     /* hf = min(floor(eps_time), n_frames), 0 if eps_time is not >= 0 */
+  float bounds[4];         /* min x, max x, min y, max y of the K1 points (+inf/-inf: none) */
+  int64_t n_head_k1;       /* K1 points of the first hf frames (the prev rank's halo capacity) */
+  int64_t n_tail_k1;       /* K1 points of the last hf frames (the next rank's halo capacity) */
+  /* set by rpt_shard_window: */
+  int64_t n_kept;          /* own points after the land filter */
+  int64_t n_head, n_tail;  /* own kept points of the first / last hf frames */
+  int64_t n_prev, n_next;  /* halo points received from rank - 1 / rank + 1 */
   int64_t n_land_cells;
 } rpt_shard_info;
 rpt_shard* rpt_shard_create(void);
@@ -344,46 +352,70 @@ int64_t rpt_shard_land_cells(const float* global_bounds, double resolution);
 int32_t rpt_shard_land_grid(rpt_shard* h, const float* global_bounds, double* grid, int64_t cells,
                             void* stream);
 /* land mask from the all-reduced grid (NULL: no land filter) with the GLOBAL built-frame count,
- * compaction, and the kept points as float32 x/y/t (dev, capacity n_points) with t = frame0 + frame
- * slot; n_kept / n_head / n_tail / n_land_cells in info; synchronises */
-int32_t rpt_shard_land_apply(rpt_shard* h, const double* grid, int64_t cells,
-                             int32_t n_built_global, int32_t halo_frames, int64_t frame0,
-                             float* x_out, float* y_out, float* t_out, rpt_shard_info* info,
-                             void* stream);
-/* core flags (dev u8 [n]) of [prev halo | own | next halo] (dev float32 x/y/t [n], n > 0) */
-int32_t rpt_shard_core(rpt_shard* h, const float* x, const float* y, const float* t, int64_t n,
-                       uint8_t* core, void* stream);
+ * compaction, and the own first / last hf frames packed for the neighbours: send_prev / send_next
+ * (dev int32 [4 + 3 * n_head_k1] / [4 + 3 * n_tail_k1], nullable) = {count, own kept total lo,
+ * hi, 0} then x, y, t (float32 bits; t = frame0 + frame slot) at offsets 4, 4 + cap, 4 + 2 cap.
+ * No sync. */
+int32_t rpt_shard_halo(rpt_shard* h, const double* grid, int64_t cells, int32_t n_built_global,
+                       int32_t rank, int64_t frame0, int32_t* send_prev, int32_t* send_next,
+                       void* stream);
+/* the window [prev halo | own | next halo] from the received halo buffers (capacities as sent;
+ * NULL / 0 at the ends of the rank chain), its grid build and K5 core flags; flags_prev /
+ * flags_next (dev u8, capacity n_head_k1 / n_tail_k1) receive the own edge points' flags for the
+ * neighbours; the window counts in info.  Synchronises once (counts + grid bounds). */
+int32_t rpt_shard_window(rpt_shard* h, const int32_t* recv_prev, int64_t cap_prev,
+                         const int32_t* recv_next, int64_t cap_next, uint8_t* flags_prev,
+                         uint8_t* flags_next, rpt_shard_info* info, void* stream);
 /* duration of the last core-flag pass (params.timing != 0; synchronises), -1 if not timed */
 double rpt_shard_core_ms(rpt_shard* h);
-/* components with the halo flags replaced by their owners': comp (dev int64 [n]) = base +
- * component-minimum local index, -1 for non-core (base = global index of point 0) */
-int32_t rpt_shard_components(rpt_shard* h, const uint8_t* core, int64_t base, int64_t* comp,
-                             void* stream);
-/* equivalence pairs between the halo points' components (comp[0, n_prev), comp[n - n_next, n))
- * and their owners' (owner_prev / owner_next, dev int64): pairs (dev int64 [1 + 2*cap]) = count,
- * then (min, max) pairs; no sync */
-int32_t rpt_shard_pairs(rpt_shard* h, const int64_t* comp, int64_t n_prev,
-                        const int64_t* owner_prev, int64_t n_next, const int64_t* owner_next,
+/* halo flags from their owners (dev u8 [n_prev] / [n_next]), components; comp_prev / comp_next
+ * (dev int64 [n_head] / [n_tail], nullable) receive the own edge points' component ids (-1: not
+ * core).  No sync. */
+int32_t rpt_shard_link(rpt_shard* h, const uint8_t* flags_prev, const uint8_t* flags_next,
+                       int64_t* comp_prev, int64_t* comp_next, void* stream);
+/* distinct equivalence pairs between the halo points' components and their owners' ids
+ * (owner_prev / owner_next, dev int64 [n_prev] / [n_next]): pairs (dev int64 [1 + 2 cap]) =
+ * the full pair count (may exceed cap), then (min, max) pairs.  No sync. */
+int32_t rpt_shard_pairs(rpt_shard* h, const int64_t* owner_prev, const int64_t* owner_next,
                         int64_t* pairs, int64_t cap, void* stream);
 /* host: union of equivalence pairs [n_pairs][2] -> sorted distinct ids (keys_out) and each
  * id's class minimum (reps_out), up to cap; returns the number of ids */
 int64_t rpt_merge_equivalences(const int64_t* pairs, int64_t n_pairs, int64_t* keys_out,
                                int64_t* reps_out, int64_t cap);
-/* representatives (keys/vals host, sorted) and the global roots among own points
- * [n_prev, n_prev + n_own) into roots (dev int64, capacity n_own); *n_roots (sync) */
-int32_t rpt_shard_roots(rpt_shard* h, const int64_t* keys, const int64_t* vals, int64_t n_keys,
-                        int64_t base, int64_t n_prev, int64_t n_own, int64_t* roots,
-                        int64_t* n_roots, void* stream);
-/* labels from every rank's roots (dev int64, ascending) + K9 summaries of the own points;
- * *n_segments (sync); the segments then via rpt_shard_segments (local frame slots) */
-int32_t rpt_shard_finish(rpt_shard* h, const int64_t* reps_sorted, int64_t n_reps,
-                         int64_t* n_segments, void* stream);
-int32_t rpt_shard_segments(const rpt_shard* h, int32_t* frame, int32_t* label, int64_t* count,
-                           int64_t* first, float* cx, float* cy, float* mean_i,
-                           int64_t* frame_first_noise);
-/* labels (dev int32 [n_kept]) of the own kept points of the last rpt_shard_finish; no sync */
-int32_t rpt_shard_labels(const rpt_shard* h, int32_t* out, void* stream);
+/* equivalence merge of every rank's pairs (gathered_pairs: dev int64 [world][row_words], the
+ * all_gather of rpt_shard_pairs' buffers; or NULL with the host merge keys_host / vals_host
+ * [n_keys]), representatives, labels, K9 of the own points, and everything rank 0 needs packed
+ * into out (dev int64 [out_cap]): [magic, S, n_reps, flags, words, F, frame0, kept] [built F]
+ * [first noise F] [count S] [first S] [frame << 32 | local label S] [cx | cy << 32 S] [mi S]
+ * [reps n_reps]; flags 1: some rank's pairs exceeded their capacity, 2: too many ids for the
+ * device merge (merge on the host), 4: out_cap too small (words = the size needed); S = -1: a
+ * frame held more labels than K9's frame sort takes (force_radix).  own_pairs: this rank's
+ * rpt_shard_pairs buffer.  No sync. */
+int32_t rpt_shard_finish(rpt_shard* h, const int64_t* gathered_pairs, int32_t world,
+                         int64_t row_words, const int64_t* own_pairs, const int64_t* keys_host,
+                         const int64_t* vals_host, int64_t n_keys, int32_t force_radix,
+                         int64_t* out, int64_t out_cap, void* stream);
+/* labels (dev int32 [n_kept]) of the own kept points of the last finish, through
+ * local_to_global (dev int32 [n_reps], from rpt_shard_host_stage); no sync */
+int32_t rpt_shard_labels(const rpt_shard* h, const int32_t* local_to_global, int64_t n_reps,
+                         int32_t* out, void* stream);
 int32_t rpt_shard_frame_offsets(const rpt_shard* h, int32_t which, int64_t* out);
+/* host, over the all-gathered packed results (host int64 [world][row_words]): sizes[4] = total
+ * segments, built frames, frames, clusters (distinct representatives) */
+int32_t rpt_shard_gathered_sizes(const int64_t* gathered, int32_t world, int64_t row_words,
+                                 int64_t* sizes);
+struct rpt_tracker;
+/* host: rank 0's stage -- the global label numbering (rank of each representative), every
+ * segment (frame = global frame id), the built frame ids, per frame slot the reference cluster
+ * order (frame_off [frames + 1], order [segments]: indices into the segments), and the tracker
+ * (nullable) updated over the built frames; each output nullable (seg_frame NULL: only
+ * local_to_global [n_reps of which_rank], the label map of one rank).  No device work. */
+int32_t rpt_shard_host_stage(const int64_t* gathered, int32_t world, int64_t row_words,
+                             struct rpt_tracker* trk, int32_t* seg_frame, int32_t* seg_label,
+                             int64_t* seg_count, int64_t* seg_first, float* seg_cx,
+                             float* seg_cy, float* seg_mi, int64_t* built_ids,
+                             int64_t* frame_off, int64_t* order, int32_t* local_to_global,
+                             int32_t which_rank);
 
 /* ---- host: per-frame cluster order of the reference -----------------------------------
  * From the segments of rpt_cluster_summaries (copied to host) and frame_first_noise: for each

@@ -234,7 +234,10 @@ int32_t parse_genfromtxt(const std::string& buf, int32_t rows_cap, int32_t bins,
     det[1] = ncols;
     return 1;
   }
-  if (ncols != kMeta + bins) return 6;
+  if (ncols != kMeta + bins) {  // another bin count: the caller re-parses with ncols - 5 bins
+    det[1] = ncols;
+    return 6;
+  }
   if (R > rows_cap) return 6;
   for (int64_t r = 0; r < R; ++r) {
     const char* a = lines[(size_t)r].first;

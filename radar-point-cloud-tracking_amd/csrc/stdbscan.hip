@@ -3348,7 +3348,9 @@ __global__ __launch_bounds__(kBlock) void k_ccmin_global(int32_t* parent,
                                                         const int32_t* __restrict__ skey = nullptr,
                                                         const uint8_t* __restrict__ mutual = nullptr,
                                                         const int32_t* __restrict__ cell_root = nullptr,
-                                                        int64_t cells = 0) {
+                                                        int64_t cells = 0,
+                                                        const int64_t* __restrict__ nr_dev = nullptr) {
+  if (nr_dev) nr = *nr_dev;  // the representative count stays on the device (shard driver)
   // level by level as in k_ccmin (keys + flags, cell roots, originals: branch-free loads, each
   // level's loads in flight together); only the parent-chain walk stays conditional
   for (int64_t tile = (int64_t)blockIdx.x * kBlock * kItems; tile < n;
@@ -3863,7 +3865,7 @@ struct DbscanState {
   bool defer = false;
   int32_t fill_stats(int32_t n_clusters, rpt_stdbscan_stats* stats);
   int32_t labels_global(const int64_t* rep_orig, const int64_t* reps, int64_t nr,
-                        int32_t* labels, hipStream_t st);
+                        int32_t* labels, hipStream_t st, const int64_t* nr_dev = nullptr);
   // denoise variant: the min_frames core condition, then the FIFO border labels
   int32_t frames_pass(int32_t min_frames, hipStream_t st);
   int32_t labels_fifo(int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st);
@@ -4431,7 +4433,7 @@ int32_t DbscanState::fill_stats(int32_t ncl, rpt_stdbscan_stats* stats) {
 }
 
 int32_t DbscanState::labels_global(const int64_t* rep_orig, const int64_t* reps, int64_t nr,
-                                   int32_t* labels, hipStream_t st) {
+                                   int32_t* labels, hipStream_t st, const int64_t* nr_dev) {
   if (degenerate) {
     set_error("rpt_dbscan_labels_global: degenerate parameters are handled by rpt_stdbscan");
     return RPT_ENOTSUP;
@@ -4445,7 +4447,7 @@ int32_t DbscanState::labels_global(const int64_t* rep_orig, const int64_t* reps,
                        occ, n_occ_dev, C, mutual, rep, cell_root);
   hipLaunchKernelGGL(k_ccmin_global, dim3(tile_grid(n)), dim3(kBlock), 0, st, parent, core, n,
                      sorig, rep_orig, reps, nr, ccmin, cid, nc_list, nc_count, skey, mutual,
-                     cr ? (const int32_t*)cell_root : nullptr, C);
+                     cr ? (const int32_t*)cell_root : nullptr, C, nr_dev);
   hipLaunchKernelGGL(k_label_global_core, dim3(gb), dim3(kBlock), 0, st, core, ccmin, cid, sorig,
                      n, slab, labels);
   const int gc = grid_for(C, kBlock, 8192);
@@ -4478,6 +4480,9 @@ int32_t DbscanState::frames_pass(int32_t min_frames, hipStream_t st) {
   int32_t* count = nc_list + n;
   const int32_t* n_occ = n_occ_dev;
   const bool cells = refine && integral_t && dim == 2 && g.nz == 1;
+  // a whole-cell hit is one frame only when a slab is one frame: the cell cap can widen the slabs
+  // (ct = 2, 4, ... for long runs of frames over a small region), then every point is read
+  const int one_frame_cells = (integral_t && g.ct == 1.0) ? 1 : 0;
   if (cells) {
     const int R = (int)std::min<double>(std::floor((double)g.epst / g.ct), 64.0);
     hipLaunchKernelGGL(k_frames_cells, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, st, g, R,
@@ -4493,19 +4498,19 @@ int32_t DbscanState::frames_pass(int32_t min_frames, hipStream_t st) {
     const bool small = (double)g.epst <= 30.0;
     if (dim == 2 && small)
       hipLaunchKernelGGL(k_frames_points<2>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                         rec<2>(), occ_bits, slab_t, integral_t ? 1 : 0, (int)min_frames, list,
+                         rec<2>(), occ_bits, slab_t, one_frame_cells, (int)min_frames, list,
                          count, core);
     else if (small)
       hipLaunchKernelGGL(k_frames_points<3>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                         rec<3>(), occ_bits, slab_t, integral_t ? 1 : 0, (int)min_frames, list,
+                         rec<3>(), occ_bits, slab_t, one_frame_cells, (int)min_frames, list,
                          count, core);
     else if (dim == 2)
       hipLaunchKernelGGL(k_frames_points_list<2>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts,
-                         skey, g, rec<2>(), occ_bits, slab_t, integral_t ? 1 : 0,
+                         skey, g, rec<2>(), occ_bits, slab_t, one_frame_cells,
                          (int)min_frames, list, count, core);
     else
       hipLaunchKernelGGL(k_frames_points_list<3>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts,
-                         skey, g, rec<3>(), occ_bits, slab_t, integral_t ? 1 : 0,
+                         skey, g, rec<3>(), occ_bits, slab_t, one_frame_cells,
                          (int)min_frames, list, count, core);
   }
   RPT_CHECK_LAUNCH();
@@ -4768,6 +4773,33 @@ int32_t dbscan_components(DbscanState* S, int32_t* comp_out, hipStream_t st) {
 int32_t dbscan_labels_global(DbscanState* S, const int64_t* rep, const int64_t* reps, int64_t nr,
                              int32_t* labels, hipStream_t st) {
   return S->labels_global(rep, reps, nr, labels, st);
+}
+// the frame-sharded driver's forms: grid bounds read back by the caller with its own results
+// (host_bounds: a Bounds), the representative count on the device
+int32_t dbscan_build_given(DbscanState* S, const float* x, const float* y, const float* t,
+                           int64_t n, double eps_space, double eps_time, int32_t ms,
+                           const void* host_bounds, hipStream_t st) {
+  RPT_TRY(check_args(x, y, nullptr, 1, t, n, 2));
+  S->given_bounds = host_bounds;
+  const int32_t s_ = S->build(x, y, nullptr, 1, t, n, eps_space, eps_time, ms, false, st);
+  S->given_bounds = nullptr;
+  RPT_TRY(s_);
+  if (S->degenerate) {
+    set_error("rpt_shard: negative or NaN eps");
+    return RPT_ENOTSUP;
+  }
+  return RPT_OK;
+}
+int32_t dbscan_labels_global_dev(DbscanState* S, const int64_t* rep, const int64_t* reps,
+                                 const int64_t* nr_dev, int32_t* labels, hipStream_t st) {
+  return S->labels_global(rep, reps, 0, labels, st, nr_dev);
+}
+// device u8 core flags in the state's sorted order -> original order (out) without a pass
+int32_t dbscan_core_orig(DbscanState* S, uint8_t* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_core_to_orig, dim3(grid_for(S->n, kBlock, 2048)), dim3(kBlock), 0, st,
+                     S->core, S->sorig, S->n, out);
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
 }
 
 }  // namespace rpt

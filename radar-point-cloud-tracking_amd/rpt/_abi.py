@@ -125,11 +125,15 @@ class ShardInfo(C.Structure):
     _fields_ = [
         ("n_points", C.c_int64),
         ("n_built", C.c_int32),
-        ("pad0", C.c_int32),
+        ("halo_frames", C.c_int32),
         ("bounds", C.c_float * 4),
+        ("n_head_k1", C.c_int64),
+        ("n_tail_k1", C.c_int64),
         ("n_kept", C.c_int64),
         ("n_head", C.c_int64),
         ("n_tail", C.c_int64),
+        ("n_prev", C.c_int64),
+        ("n_next", C.c_int64),
         ("n_land_cells", C.c_int64),
     ]
 
@@ -205,20 +209,22 @@ _SIGS = [
                                     C.POINTER(ShardInfo), vp]),
     ("rpt_shard_land_cells", C.c_int64, [c_f32p, C.c_double]),
     ("rpt_shard_land_grid", C.c_int32, [vp, c_f32p, vp, C.c_int64, vp]),
-    ("rpt_shard_land_apply", C.c_int32, [vp, vp, C.c_int64, C.c_int32, C.c_int32, C.c_int64, vp,
-                                         vp, vp, C.POINTER(ShardInfo), vp]),
-    ("rpt_shard_core", C.c_int32, [vp, vp, vp, vp, C.c_int64, vp, vp]),
+    ("rpt_shard_halo", C.c_int32, [vp, vp, C.c_int64, C.c_int32, C.c_int32, C.c_int64, vp, vp,
+                                   vp]),
+    ("rpt_shard_window", C.c_int32, [vp, vp, C.c_int64, vp, C.c_int64, vp, vp,
+                                     C.POINTER(ShardInfo), vp]),
     ("rpt_shard_core_ms", C.c_double, [vp]),
-    ("rpt_shard_components", C.c_int32, [vp, vp, C.c_int64, vp, vp]),
-    ("rpt_shard_pairs", C.c_int32, [vp, vp, C.c_int64, vp, C.c_int64, vp, vp, C.c_int64, vp]),
+    ("rpt_shard_link", C.c_int32, [vp, vp, vp, vp, vp, vp]),
+    ("rpt_shard_pairs", C.c_int32, [vp, vp, vp, vp, C.c_int64, vp]),
     ("rpt_merge_equivalences", C.c_int64, [c_i64p, C.c_int64, c_i64p, c_i64p, C.c_int64]),
-    ("rpt_shard_roots", C.c_int32, [vp, c_i64p, c_i64p, C.c_int64, C.c_int64, C.c_int64,
-                                    C.c_int64, vp, c_i64p, vp]),
-    ("rpt_shard_finish", C.c_int32, [vp, vp, C.c_int64, c_i64p, vp]),
-    ("rpt_shard_segments", C.c_int32, [vp, c_i32p, c_i32p, c_i64p, c_i64p, c_f32p, c_f32p,
-                                       c_f32p, c_i64p]),
-    ("rpt_shard_labels", C.c_int32, [vp, vp, vp]),
+    ("rpt_shard_finish", C.c_int32, [vp, vp, C.c_int32, C.c_int64, vp, c_i64p, c_i64p,
+                                     C.c_int64, C.c_int32, vp, C.c_int64, vp]),
+    ("rpt_shard_labels", C.c_int32, [vp, vp, C.c_int64, vp, vp]),
     ("rpt_shard_frame_offsets", C.c_int32, [vp, C.c_int32, c_i64p]),
+    ("rpt_shard_gathered_sizes", C.c_int32, [c_i64p, C.c_int32, C.c_int64, c_i64p]),
+    ("rpt_shard_host_stage", C.c_int32, [c_i64p, C.c_int32, C.c_int64, vp, c_i32p, c_i32p,
+                                         c_i64p, c_i64p, c_f32p, c_f32p, c_f32p, c_i64p, c_i64p,
+                                         c_i64p, c_i32p, C.c_int32]),
     ("rpt_order_clusters", C.c_int32, [C.c_int32, C.c_int64, c_i32p, c_i32p, c_i64p, c_i64p,
                                         c_i64p, c_i64p]),
     ("rpt_set_order", C.c_int32, [c_i32p, C.c_int32, c_i32p]),

@@ -40,6 +40,8 @@ class SweepBatch:
     gain_flags: np.ndarray       # int64 [n_files]: GAIN_FIRST_NAN | GAIN_DISAGREE bits
     detail_kind: np.ndarray      # int64 [n_files]: 0 none, 1 I/O, 2 tokenizer, 3 non-numeric,
                                  # 5 genfromtxt rows of < 5 fields (rpt_csv_parse_sweeps)
+    n_fields: Optional[np.ndarray] = None  # int64 [n_files]: fields per row of the files
+                                           # with STATUS_UNSUPPORTED (0 for the others)
 
 
 def read_csv_error(path, detail) -> Optional[str]:
@@ -117,4 +119,5 @@ def read_sweeps(paths: Sequence[Union[str, Path]], bins: int = 1024, threads: in
     return SweepBatch(echo=echo, scale=scale, angle=angle, gain=gain[:n], rows=rows,
                       status=status[:n].copy(),
                       errors=[read_csv_error(p, detail[i]) for i, p in enumerate(paths)],
-                      gain_flags=detail[:n, 4].copy(), detail_kind=detail[:n, 0].copy())
+                      gain_flags=detail[:n, 4].copy(), detail_kind=detail[:n, 0].copy(),
+                      n_fields=np.where(status[:n] == STATUS_UNSUPPORTED, detail[:n, 1], 0))

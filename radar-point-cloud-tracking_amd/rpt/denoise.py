@@ -130,16 +130,17 @@ def load_frames(frames: List[Dict[int, Path]], device=None, threads: int = 0,
     """load_frame / load_radar_csv (:97-152, :219-231) for every frame on the device: sweeps
     parsed natively with the reference loader's semantics (np.genfromtxt first, pd.read_csv when
     it raises: rpt.core.ingest MODE_GENFROMTXT), K1 (threshold > 10, every 4th kept sample of
-    each file) in one batch with the frame's files in its dict order, times = frame index.
+    each file) with the frame's files in its dict order, times = frame index.  A file whose
+    genfromtxt rows hold 5 + W fields with W != 1024 has W bins (num_bins = data[:, 5:].shape[1],
+    range resolution Scale / W, :128-134): such files are parsed and scattered as batches of
+    their own width and their points put back in file order.
     A file whose load raises fails its whole frame (load_frame stops at it): with parallel=True
     (load_frames_parallel, :234-257) the frame is empty and listed in `failed`; otherwise the
     exception propagates as in the sequential loop (:910-915)."""
     from .core.ingest import (MODE_GENFROMTXT, STATUS_NON_NUMERIC, STATUS_UNSUPPORTED,
                               read_sweeps)
-    from .core.transforms import trig_tables
 
     dev = require_gpu(device)
-    lib = _abi.load()
     paths, fidx = [], []
     for f, fr in enumerate(frames):
         for p in fr.values():
@@ -150,69 +151,123 @@ def load_frames(frames: List[Dict[int, Path]], device=None, threads: int = 0,
     if n_files == 0:
         return DenoiseFrames(empty, empty, empty, empty, np.zeros(len(frames), np.int64), [])
     batch = read_sweeps(paths, bins=NUM_ECHO_COLUMNS, threads=threads, mode=MODE_GENFROMTXT)
-    unsup = [p for p, s in zip(paths, batch.status) if s == STATUS_UNSUPPORTED]
-    if unsup:
-        raise NotImplementedError(f"{unsup[0]}: rows of other than {5 + NUM_ECHO_COLUMNS} "
-                                  "fields are not supported by the denoise loader")
+    # files of another bin count, re-parsed per width (their status and errors replace the first
+    # parse's; genfromtxt itself raises nothing for them)
+    groups = {NUM_ECHO_COLUMNS: ([j for j in range(n_files)
+                                  if batch.status[j] != STATUS_UNSUPPORTED], batch, None)}
+    status = list(batch.status)
+    errors = list(batch.errors)
+    kinds = list(batch.detail_kind)
+    widths = sorted({int(w) - 5 for w, s_ in zip(batch.n_fields, batch.status)
+                     if s_ == STATUS_UNSUPPORTED})
+    for W in widths:
+        js = [j for j in range(n_files) if batch.status[j] == STATUS_UNSUPPORTED and
+              int(batch.n_fields[j]) - 5 == W]
+        if W <= 0:   # Status..Angle only: no echo column, no point (:139-156 on an empty mask)
+            for j in js:
+                status[j] = -1
+            continue
+        sub = read_sweeps([paths[j] for j in js], bins=W, threads=threads, mode=MODE_GENFROMTXT)
+        for k, j in enumerate(js):
+            status[j], errors[j], kinds[j] = sub.status[k], sub.errors[k], sub.detail_kind[k]
+        groups[W] = (js, sub, list(range(len(js))))
     failed, dead = [], set()
     for j, p in enumerate(paths):
         f = fidx[j]
         if f in dead:
             continue   # load_frame stopped at this frame's first failing file
-        msg = batch.errors[j]
-        if msg is None and batch.status[j] == STATUS_NON_NUMERIC:
+        msg = errors[j]
+        if msg is None and status[j] == STATUS_NON_NUMERIC:
             msg = f"could not convert string to float in {p}"
         if msg is None:
             continue
         if not parallel:
-            _raise_like_reference(int(batch.detail_kind[j]), msg)
+            _raise_like_reference(int(kinds[j]), msg)
         dead.add(f)
         failed.append((f, msg))
-    keep_file = np.array([fidx[j] not in dead for j in range(n_files)], bool)
+    counts = np.zeros(len(frames), np.int64)
+    js0, b0, _ = groups[NUM_ECHO_COLUMNS]
+    with torch.cuda.device(dev):
+        if len(groups) == 1 and len(js0) == n_files:   # every file 1024 bins: one K1 batch
+            x, y, z, pf, fo_h = _k1_files(b0, js0, [fidx[j] not in dead for j in js0],
+                                          NUM_ECHO_COLUMNS, dev)
+            n = int(fo_h[-1])
+            t = torch.empty_like(x)
+            if n:
+                ids = torch.tensor(fidx, dtype=torch.int64, device=dev)
+                _abi.check(_abi.load().rpt_frame_times(pf.data_ptr(), n, ids.data_ptr(),
+                                                       t.data_ptr(), stream_handle(dev)),
+                           "rpt_frame_times")
+            np.add.at(counts, np.asarray(fidx, np.int64), np.diff(fo_h))
+            return DenoiseFrames(x[:n], y[:n], z[:n], t[:n], counts, failed)
+        # K1 per width group, then every file's points in the global file order
+        per_file: List[Optional[Tuple[torch.Tensor, ...]]] = [None] * n_files
+        for W, (js, b, idx) in groups.items():
+            if not js:
+                continue
+            x, y, z, _, fo_h = _k1_files(b, js if idx is None else idx,
+                                         [fidx[j] not in dead for j in js], W, dev)
+            for k, j in enumerate(js):
+                per_file[j] = (x[fo_h[k]:fo_h[k + 1]], y[fo_h[k]:fo_h[k + 1]],
+                               z[fo_h[k]:fo_h[k + 1]])
+        pieces = [(j, pc) for j, pc in enumerate(per_file) if pc is not None and pc[0].numel()]
+        for j, pc in pieces:
+            counts[fidx[j]] += pc[0].numel()
+        if not pieces:
+            return DenoiseFrames(empty, empty, empty, empty, counts, failed)
+        x, y, z = (torch.cat([pc[k] for _, pc in pieces]) for k in range(3))
+        t = torch.cat([torch.full((pc[0].numel(),), float(fidx[j]), dtype=torch.float32,
+                                  device=dev) for j, pc in pieces])
+    return DenoiseFrames(x, y, z, t, counts, failed)
+
+
+def _k1_files(batch, idx: List[int], keep: List[bool], bins: int, dev):
+    """K1 (threshold, stride 4 per file) over the files `idx` of a parsed batch of `bins` bins
+    (files not kept scatter nothing) -> device x, y, intensity, file slot per point, and the
+    host file offsets [len(idx) + 1]."""
+    from .core.transforms import trig_tables
+
+    lib = _abi.load()
+    n_files = len(idx)
     R = max(int(batch.echo.shape[1]), 1)
     scale = np.zeros((n_files, R), np.float32)
     cos_t = np.zeros((n_files, R), np.float32)
     sin_t = np.zeros((n_files, R), np.float32)
-    for j in range(n_files):
+    for k, j in enumerate(idx):
         n = int(batch.rows[j])
-        if batch.status[j] != 0 or n <= 0 or not keep_file[j]:
+        if batch.status[j] != 0 or n <= 0 or not keep[k]:
             continue
-        scale[j, :n] = batch.scale[j, :n]
-        cos_t[j, :n], sin_t[j, :n] = trig_tables(batch.angle[j, :n], ANGLE_SCALE)
-    echo = np.ascontiguousarray(batch.echo)
-    if dead:   # a failed frame is empty (load_frames_parallel's empty arrays)
-        echo[~keep_file] = 0
-    if echo.shape[1] == 0:
-        echo = np.zeros((n_files, 1, NUM_ECHO_COLUMNS), echo.dtype)
+        scale[k, :n] = batch.scale[j, :n]
+        cos_t[k, :n], sin_t[k, :n] = trig_tables(batch.angle[j, :n], ANGLE_SCALE)
+    if not batch.echo.shape[1]:
+        echo = np.zeros((n_files, 1, bins), batch.echo.dtype)
+    elif list(idx) == list(range(batch.echo.shape[0])):
+        echo = np.ascontiguousarray(batch.echo)
+    else:
+        echo = np.ascontiguousarray(batch.echo[idx])
+    drop = ~np.asarray(keep, bool)
+    if drop.any():   # a failed frame is empty (load_frames_parallel's empty arrays)
+        echo[drop] = 0
     dt = _abi.ECHO_U8 if echo.dtype == np.uint8 else _abi.ECHO_F32
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
-    with torch.cuda.device(dev):
-        st = stream_handle(dev)
-        ed, sc, ct, sn = T(echo), T(scale), T(cos_t), T(sin_t)
-        rp = torch.empty(n_files * R + 1, dtype=torch.int64, device=dev)
-        fo = torch.empty(n_files + 1, dtype=torch.int64, device=dev)
-        tot = _abi.C.c_int64(0)
-        thr = float(np.float32(INTENSITY_THRESHOLD))
-        _abi.check(lib.rpt_polar_count(ed.data_ptr(), dt, n_files, R, NUM_ECHO_COLUMNS, thr,
-                                       POINT_STRIDE, rp.data_ptr(), fo.data_ptr(),
-                                       _abi.C.byref(tot), st), "rpt_polar_count")
-        n = int(tot.value)
-        x = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
-        y, z, t = torch.empty_like(x), torch.empty_like(x), torch.empty_like(x)
-        pf = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
-        _abi.check(lib.rpt_polar_write(ed.data_ptr(), dt, n_files, R, NUM_ECHO_COLUMNS,
-                                       sc.data_ptr(), ct.data_ptr(), sn.data_ptr(), None, thr,
-                                       POINT_STRIDE, rp.data_ptr(), fo.data_ptr(), 1,
-                                       x.data_ptr(), y.data_ptr(), z.data_ptr(), None,
-                                       pf.data_ptr(), st), "rpt_polar_write")
-        ids = torch.tensor(fidx, dtype=torch.int64, device=dev)
-        if n:
-            _abi.check(lib.rpt_frame_times(pf.data_ptr(), n, ids.data_ptr(), t.data_ptr(), st),
-                       "rpt_frame_times")
-        fo_h = fo.cpu().numpy()
-    counts = np.zeros(len(frames), np.int64)
-    np.add.at(counts, np.asarray(fidx, np.int64), np.diff(fo_h))
-    return DenoiseFrames(x[:n], y[:n], z[:n], t[:n], counts, failed)
+    st = stream_handle(dev)
+    ed, sc, ct, sn = T(echo), T(scale), T(cos_t), T(sin_t)
+    rp = torch.empty(n_files * R + 1, dtype=torch.int64, device=dev)
+    fo = torch.empty(n_files + 1, dtype=torch.int64, device=dev)
+    tot = _abi.C.c_int64(0)
+    thr = float(np.float32(INTENSITY_THRESHOLD))
+    _abi.check(lib.rpt_polar_count(ed.data_ptr(), dt, n_files, R, bins, thr, POINT_STRIDE,
+                                   rp.data_ptr(), fo.data_ptr(), _abi.C.byref(tot), st),
+               "rpt_polar_count")
+    n = int(tot.value)
+    x = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+    y, z = torch.empty_like(x), torch.empty_like(x)
+    pf = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    _abi.check(lib.rpt_polar_write(ed.data_ptr(), dt, n_files, R, bins, sc.data_ptr(),
+                                   ct.data_ptr(), sn.data_ptr(), None, thr, POINT_STRIDE,
+                                   rp.data_ptr(), fo.data_ptr(), 1, x.data_ptr(), y.data_ptr(),
+                                   z.data_ptr(), None, pf.data_ptr(), st), "rpt_polar_write")
+    return x, y, z, pf, fo.cpu().numpy()
 
 
 def st_dbscan(coords, times, eps_space: float, eps_time: float, min_samples: int,

@@ -72,6 +72,16 @@ class Comm:
         dist.all_gather_into_tensor(out, c, group=self.group)
         return out.cpu().reshape(self.world, -1)
 
+    def all_gather_dev(self, t: torch.Tensor) -> torch.Tensor:
+        """all_gather of a 1-D tensor of the same length on every rank -> [world * len] on the
+        input's device (RCCL: stays in stream order, no host wait)."""
+        if self.world == 1:
+            return t.reshape(-1)
+        c = self._c(t).reshape(-1)
+        out = torch.empty(self.world * c.numel(), dtype=c.dtype, device=self.cdev)
+        dist.all_gather_into_tensor(out, c, group=self.group)
+        return out.to(t.device)
+
     def all_gather_var(self, t: torch.Tensor) -> List[torch.Tensor]:
         """all_gather of 1-D tensors of different lengths (returned on the input's device)."""
         if self.world == 1:
@@ -233,6 +243,7 @@ class ShardResult:
     seg: Optional[Dict[str, np.ndarray]] = None  # rank 0: all segments, global frame slots
     built_global: Optional[np.ndarray] = None
     stage_ms: Dict[str, float] = field(default_factory=dict)
+    t_done: float = 0.0                         # perf_counter when the device part ended
     _pending: Optional[Future] = None
 
     def finish(self) -> "ShardResult":
@@ -456,66 +467,80 @@ def _unpack_parts(parts, F: int):
 class CommSequencer:
     """Orders the collectives of several stacks in flight on ONE communicator.
 
-    Each step (a stack run) passes through `phases` collective slots in order.  Steps are
-    registered at submission and grouped: a group closes when it holds `lanes` steps or when the
-    submitter waits for a result (close_group()).  Slot (step s, phase p) of a closed group of n
-    steps starting at step s0 runs at position base + p * n + (s - s0) of one global sequence:
-    inside a group the steps take their phase-p collectives in step order, phase by phase.  The
-    submitter's sequence of submissions and waits is the same on every rank, so every rank
-    issues the same collectives in the same order on the same process group -- no second
-    communicator whose kernels could be ordered differently on different GPUs (RCCL spinning
-    kernels sharing a process's hardware queues) -- while a lane's device phases between its
-    collectives overlap the other lanes' waits.  A step that fails poisons the sequencer so the
-    other lanes raise instead of waiting for slots that never come."""
+    Each step (a stack run) passes through `phases` collective slots in order.  The slots of
+    all steps follow one fixed software-pipeline order: step s starts its phase 0 at slot time
+    s * d (d = ceil(phases / lanes): the lanes' stagger) and takes phase p at time s * d + p;
+    slots are entered by time, ties by step.  In steady state the lanes are thus a fraction of a
+    step apart -- while one lane waits on a collective or a readback another runs device work --
+    instead of moving phase by phase together.  The order depends only on the sequence of
+    submissions, which is the same on every rank, so every rank issues the same collectives in
+    the same order on the same process group (no second communicator whose kernels could be
+    ordered differently on different GPUs).  A slot may have to wait for a step that is not
+    submitted yet; when the submitter stops submitting to wait for results (close_group()) the
+    steps submitted so far form a closed epoch and later submissions start a new one after it.
+    A step that fails poisons the sequencer so the other lanes raise instead of waiting."""
 
     def __init__(self, lanes: int, phases: int):
         self.L, self.P = int(lanes), int(phases)
+        self.d = max(1, -(-self.P // self.L))
         self.cv = threading.Condition()
-        self.turn = 0
         self.failed: Optional[BaseException] = None
-        self.groups: List[List[int]] = []   # [start step, size, closed, base]
-        self.group_of: Dict[int, int] = {}
+        self.epochs: List[List[int]] = []   # [first step, base time, closed (0/1)]
+        self.epoch_of: Dict[int, int] = {}
+        self.next_phase: Dict[int, int] = {}  # step -> its next phase (steps not done)
+        self.n_reg = 0
+        self.t_end = 0                         # one past the last slot time of any step
 
     def register(self, step: int):
         """Called by the submitter, in step order, before the step runs."""
         with self.cv:
-            g = self.groups[-1] if self.groups else None
-            if g is None or g[2]:
-                base = g[3] + self.P * g[1] if g is not None else 0
-                g = [step, 0, False, base]
-                self.groups.append(g)
-            g[1] += 1
-            self.group_of[step] = len(self.groups) - 1
-            if g[1] == self.L:
-                g[2] = True
-                self.cv.notify_all()
+            e = self.epochs[-1] if self.epochs else None
+            if e is None or e[2]:
+                e = [step, self.t_end, 0]
+                self.epochs.append(e)
+            self.epoch_of[step] = len(self.epochs) - 1
+            self.next_phase[step] = 0
+            self.n_reg = step + 1
+            self.t_end = max(self.t_end, self._time(step, self.P - 1) + 1)
+            self.cv.notify_all()
 
     def close_group(self):
-        """No more steps join the open group (the submitter is about to wait on a result)."""
+        """No more steps join the open epoch (the submitter is about to wait on a result)."""
         with self.cv:
-            if self.groups and not self.groups[-1][2]:
-                self.groups[-1][2] = True
+            if self.epochs and not self.epochs[-1][2]:
+                self.epochs[-1][2] = 1
                 self.cv.notify_all()
 
-    def _index(self, step: int, phase: int) -> int:  # under self.cv
-        g = self.groups[self.group_of[step]]
-        while phase > 0 and not g[2] and self.failed is None:
-            self.cv.wait()
-        return g[3] + phase * g[1] + (step - g[0])
+    def _time(self, step: int, phase: int) -> int:
+        e = self.epochs[self.epoch_of[step]]
+        return e[1] + (step - e[0]) * self.d + phase
+
+    def _blocked(self, step: int, phase: int) -> bool:  # under self.cv
+        key = (self._time(step, phase), step)
+        for s, q in self.next_phase.items():
+            if s != step and (self._time(s, q), s) < key:
+                return True
+        e = self.epochs[-1]
+        if not e[2]:  # the open epoch's next (unsubmitted) step could come first
+            t = e[1] + (self.n_reg - e[0]) * self.d
+            if (t, self.n_reg) < key:
+                return True
+        return False
 
     def _acquire(self, step: int, phase: int):
         with self.cv:
-            idx = self._index(step, phase)
-            while self.turn != idx and self.failed is None:
+            while self.failed is None and self._blocked(step, phase):
                 self.cv.wait()
             if self.failed is not None:
                 raise RuntimeError("collective sequence aborted by another stack") \
                     from self.failed
-            return idx
 
-    def _release(self, idx: int):
+    def _release(self, step: int, phase: int):
         with self.cv:
-            self.turn = idx + 1
+            if phase + 1 >= self.P:
+                self.next_phase.pop(step, None)
+            else:
+                self.next_phase[step] = phase + 1
             self.cv.notify_all()
 
     def abort(self, exc: BaseException):
@@ -527,6 +552,11 @@ class CommSequencer:
     def step(self, step: int) -> "_StepSlots":
         return _StepSlots(self, step)
 
+    def order(self, steps: int) -> List[Tuple[int, int]]:
+        """The (step, phase) slot order of `steps` steps submitted without a wait."""
+        return sorted(((s, q) for s in range(steps) for q in range(self.P)),
+                      key=lambda a: (a[0] * self.d + a[1], a[0]))
+
 
 class _StepSlots:
     """One step's walk through its slots: slot(k) first passes the skipped slots < k (their
@@ -537,17 +567,18 @@ class _StepSlots:
 
     def _pass(self, upto: int):
         while self.next < upto:
-            self.seq._release(self.seq._acquire(self.step, self.next))
+            self.seq._acquire(self.step, self.next)
+            self.seq._release(self.step, self.next)
             self.next += 1
 
     @contextlib.contextmanager
     def slot(self, k: int):
         self._pass(k)
-        i = self.seq._acquire(self.step, k)
+        self.seq._acquire(self.step, k)
         try:
             yield
         finally:
-            self.seq._release(i)
+            self.seq._release(self.step, k)
             self.next = k + 1
 
     def close(self):
@@ -565,10 +596,23 @@ class _NoSlots:
 
 class NativeShardPipeline:
     """The frame-sharded path with every per-rank stage in librpt's shard driver (rpt_shard_*,
-    csrc/stack.cpp): one native call per phase, each at most one packed readback; the
-    collectives between phases (torch.distributed: RCCL over xGMI, or gloo) move tensors this
-    class owns.  Same protocol and results as ShardedStackPipeline (module doc), which stays as
-    the CPU-testable restatement (tests/test_dist_cpu.py)."""
+    csrc/shard.cpp) and the collectives between them here (torch.distributed: RCCL over xGMI, or
+    gloo).  Per step (csrc/shard.cpp's header has the phases):
+
+      polar* [all_gather info*] land_grid [all_reduce grid] halo [P2P x/y/t] window*
+      [P2P core flags] link [P2P component ids] pairs [all_gather pairs] finish
+      [all_gather packed results*]
+
+    -- three host waits (*), the other collectives stay in stream order.  Sizes the host does
+    not know when it issues a collective are capacities: the halo buffers take the neighbour's
+    K1 count of its edge frames (from the info gather), the pair and result buffers capacities
+    grown from earlier steps; a step whose pairs or results did not fit (every rank sees every
+    header) is finished again with larger ones, in the same order on every rank.  Rank 0's host
+    stage (the global label numbering, the reference cluster order and the tracker) is ONE
+    native call that releases the GIL.  Same results as ShardedStackPipeline (module doc), which
+    stays as the CPU-testable restatement (tests/test_dist_cpu.py)."""
+
+    N_SLOTS = 8  # collective phases of one step (CommSequencer slots): 7 + the rare redo
 
     def __init__(self, comm: Comm, gains: Sequence[int], rows: int, bins: int,
                  params: PathParams = None, timing: bool = False, async_host: bool = False,
@@ -588,11 +632,11 @@ class NativeShardPipeline:
         self.ws = _Ws(self.dev)
         self._host = ThreadPoolExecutor(max_workers=host_workers) if async_host else None
         self.core_points = 0
-        self._n_own = 0
         self._core_ms = False
-        # capacities of the one-collective gathers (grown from what earlier steps needed; a step
-        # that exceeds one falls back to the two-round gather, consistently on every rank)
-        self._cap_pairs, self._cap_roots, self._cap_parts = 4096, 4096, 65536
+        # capacities (grown from what earlier steps needed; a step that exceeds one is finished
+        # again with a larger one, consistently on every rank)
+        self._cap_pairs, self._cap_out = 1024, 1 << 15
+        self._last = None  # (gathered results on the device, rows, words per row) of the last run
 
     def set_geometry(self, scale, cos_t, sin_t, n_files: int):
         def rep(a):
@@ -616,8 +660,6 @@ class NativeShardPipeline:
         if h:
             self.lib.rpt_shard_destroy(h)
             self.h = None
-
-    N_SLOTS = 9  # collective phases of one step (CommSequencer slots)
 
     def run(self, echo: torch.Tensor, frame0: int, slots=None) -> ShardResult:
         """slots: a CommSequencer step (several stacks in flight on one communicator) or None."""
@@ -647,6 +689,14 @@ class NativeShardPipeline:
         def chk(status, what):
             A.check(status, what)
 
+        def ptr(t):
+            return t.data_ptr() if t is not None and t.numel() else None
+
+        if W > 1 and not (np.isfinite(p.eps_time) and p.eps_time >= 0):
+            raise ValueError("the frame-sharded path needs a finite eps_time >= 0")
+        if W > 1 and int(np.floor(p.eps_time)) > F:
+            raise ValueError(f"each rank needs at least floor(eps_time)="
+                             f"{int(np.floor(p.eps_time))} frames")
         dt = {torch.uint8: A.ECHO_U8, torch.float32: A.ECHO_F32}[echo.dtype]
         echo = echo.contiguous()
         sp = A.StackParams(F, G, self.rows, self.bins, dt, float(np.float32(p.threshold)),
@@ -656,15 +706,15 @@ class NativeShardPipeline:
                            1 if self.timing else 0)
         info = A.ShardInfo()
         scale_d, cos_d, sin_d = self.geo
-        # 1. K1 + bounds (one readback), then every rank's counts / bounds
+        # 1. K1 + bounds + edge-frame counts (one readback), then every rank's
         chk(lib.rpt_shard_polar(self.h, C_.byref(sp), echo.data_ptr(), scale_d.data_ptr(),
                                 cos_d.data_ptr(), sin_d.data_ptr(), None,  # no per-point gains
                                 C_.byref(info), st), "rpt_shard_polar")
         n_points = int(info.n_points)
         with slots.slot(0):
             allinfo = comm.all_gather_fixed(torch.tensor(
-                [n_points, info.n_built, *[float(b) for b in info.bounds]],
-                dtype=torch.float64)).numpy()
+                [n_points, info.n_built, *[float(b) for b in info.bounds], info.n_head_k1,
+                 info.n_tail_k1], dtype=torch.float64)).numpy()
         n_global = int(allinfo[:, 0].sum())
         n_built = int(allinfo[:, 1].sum())
         mark("polar")
@@ -682,167 +732,74 @@ class NativeShardPipeline:
                 "rpt_shard_land_grid")
             with slots.slot(1):
                 grid = comm.all_reduce(grid, _SUM)
-        # 3. mask + compaction; own x / y / t land between room for the two halos
-        h = int(np.floor(p.eps_time)) if np.isfinite(p.eps_time) and p.eps_time >= 0 else 0
-        if W > 1 and h > F:
-            raise ValueError(f"each rank needs at least floor(eps_time)={h} frames")
-        halo = W > 1 and h > 0
-        cap_prev = int(allinfo[r - 1, 0]) if halo and r > 0 else 0
-        cap_next = int(allinfo[r + 1, 0]) if halo and r < W - 1 else 0
-        cap = cap_prev + n_points + cap_next
-        xyt = ws.get("xyt", 3 * max(cap, 1), torch.float32)
-        X, Y, T = xyt[:cap], xyt[cap:2 * cap], xyt[2 * cap:3 * cap]
-        off = cap_prev
-        chk(lib.rpt_shard_land_apply(self.h, grid.data_ptr() if grid is not None else None,
-                                     cells, n_built, h, int(frame0), X[off:].data_ptr(),
-                                     Y[off:].data_ptr(), T[off:].data_ptr(), C_.byref(info), st),
-            "rpt_shard_land_apply")
-        n_own, n_head, n_tail = int(info.n_kept), int(info.n_head), int(info.n_tail)
-        with slots.slot(2):
-            kinfo = comm.all_gather_fixed(torch.tensor([n_own, n_head, n_tail],
-                                                       dtype=torch.int64)).numpy()
-        kept = kinfo[:, 0]
-        P = int(kept[:r].sum())
-        n_in_global = int(kept.sum())
+        # 3. mask + compaction; the own edge frames for the neighbours (capacities: K1 counts)
+        hf = int(info.halo_frames)
+        halo = W > 1 and hf > 0
+        has_p, has_n = halo and r > 0, halo and r < W - 1
+        cap_sp = int(info.n_head_k1) if has_p else 0     # my first hf frames, to rank r - 1
+        cap_sn = int(info.n_tail_k1) if has_n else 0     # my last hf frames, to rank r + 1
+        cap_rp = int(allinfo[r - 1, 7]) if has_p else 0  # rank r - 1's last hf frames
+        cap_rn = int(allinfo[r + 1, 6]) if has_n else 0  # rank r + 1's first hf frames
+        hsp = ws.get("hsp", 4 + 3 * cap_sp, torch.int32) if has_p else None
+        hsn = ws.get("hsn", 4 + 3 * cap_sn, torch.int32) if has_n else None
+        chk(lib.rpt_shard_halo(self.h, ptr(grid), cells, n_built, r, int(frame0), ptr(hsp),
+                               ptr(hsn), st), "rpt_shard_halo")
+        rp = rn = None
+        if halo:
+            empty = torch.empty(0, dtype=torch.int32, device=self.dev)
+            with slots.slot(2):
+                rp, rn = comm.exchange_known(hsp if has_p else empty, hsn if has_n else empty,
+                                             4 + 3 * cap_rp if has_p else 0,
+                                             4 + 3 * cap_rn if has_n else 0)
         mark("land")
-        if n_in_global == 0:
-            if n_built > 0:  # BallTree on 0 samples (sklearn ValueError)
-                raise ValueError("Found array with 0 sample(s) (shape=(0, 2)) while a minimum "
-                                 "of 1 is required.")
-        n_prev = int(kinfo[r - 1, 2]) if halo and r > 0 else 0
-        n_next = int(kinfo[r + 1, 1]) if halo and r < W - 1 else 0
-        # 4. halo: x / y / t of the first / last h frames to the neighbours (sizes known)
-        if halo:
-            def pack(a, b):
-                return torch.cat([X[off + a:off + b], Y[off + a:off + b], T[off + a:off + b]])
-            with slots.slot(3):
-                hp, hn = comm.exchange_known(pack(0, n_head), pack(n_own - n_tail, n_own),
-                                             3 * n_prev, 3 * n_next)
-            if n_prev:
-                X[off - n_prev:off] = hp[:n_prev]
-                Y[off - n_prev:off] = hp[n_prev:2 * n_prev]
-                T[off - n_prev:off] = hp[2 * n_prev:]
-            if n_next:
-                e = off + n_own
-                X[e:e + n_next] = hn[:n_next]
-                Y[e:e + n_next] = hn[n_next:2 * n_next]
-                T[e:e + n_next] = hn[2 * n_next:]
-        lo = off - n_prev
+        # 4. window, its grid build and core flags (one readback); own edge flags for the
+        #    neighbours
+        fsp = ws.get("fsp", max(cap_sp, 1), torch.uint8)
+        fsn = ws.get("fsn", max(cap_sn, 1), torch.uint8)
+        chk(lib.rpt_shard_window(self.h, ptr(rp), cap_rp, ptr(rn), cap_rn,
+                                 fsp.data_ptr() if has_p else None,
+                                 fsn.data_ptr() if has_n else None, C_.byref(info), st),
+            "rpt_shard_window")
+        n_own, n_head, n_tail = int(info.n_kept), int(info.n_head), int(info.n_tail)
+        n_prev, n_next = int(info.n_prev), int(info.n_next)
         n_tot = n_prev + n_own + n_next
-        base = P - n_prev
-        mark("halo")
-        # 5. core flags; the halo points' flags from their owners
-        core = ws.get("core", max(n_tot, 1), torch.uint8)
-        self._core_ms = False
-        if n_tot:
-            chk(lib.rpt_shard_core(self.h, X[lo:].data_ptr(), Y[lo:].data_ptr(),
-                                   T[lo:].data_ptr(), n_tot, core.data_ptr(), st),
-                "rpt_shard_core")
-            self._core_ms = self.timing   # read (synchronising) by last_core_ms()
+        self._core_ms = self.timing and n_tot > 0
         self.core_points = n_tot
+        mark("halo")
+        # 5. halo core flags from their owners, components, own edge component ids
+        flp = fln = None
         if halo:
-            c_own = core[n_prev:n_prev + n_own]
+            with slots.slot(3):
+                flp, fln = comm.exchange_known(fsp[:n_head] if has_p else fsp[:0],
+                                               fsn[:n_tail] if has_n else fsn[:0],
+                                               n_prev, n_next)
+        csp = ws.get("csp", max(n_head, 1), torch.int64)
+        csn = ws.get("csn", max(n_tail, 1), torch.int64)
+        chk(lib.rpt_shard_link(self.h, ptr(flp), ptr(fln), csp.data_ptr() if has_p else None,
+                               csn.data_ptr() if has_n else None, st), "rpt_shard_link")
+        owp = own_ = None
+        if halo:
             with slots.slot(4):
-                cp, cn = comm.exchange_known(c_own[:n_head].contiguous(),
-                                             c_own[n_own - n_tail:].contiguous(), n_prev, n_next)
-            if n_prev:
-                core[:n_prev] = cp
-            if n_next:
-                core[n_prev + n_own:n_tot] = cn
-        # 6. components; equivalences across ranks from the halo points' owners
-        comp = ws.get("comp", max(n_tot, 1), torch.int64)
-        if n_tot:
-            chk(lib.rpt_shard_components(self.h, core.data_ptr(), base, comp.data_ptr(), st),
-                "rpt_shard_components")
-        pairs = np.zeros(0, np.int64)
-        if halo:
-            g_own = comp[n_prev:n_prev + n_own]
-            with slots.slot(5):
-                op_, on_ = comm.exchange_known(g_own[:n_head].contiguous(),
-                                               g_own[n_own - n_tail:].contiguous(), n_prev,
-                                               n_next)
-            pcap = n_prev + n_next
-            pb = ws.get("pairs", 1 + 2 * max(pcap, 1), torch.int64)
-            if n_tot:
-                chk(lib.rpt_shard_pairs(self.h, comp.data_ptr(), n_prev, op_.data_ptr(), n_next,
-                                        on_.data_ptr(), pb.data_ptr(), pcap, st),
-                    "rpt_shard_pairs")
-            else:
-                pb[0] = 0
-            # [pair count | pairs]: one gather of the first 1 + cap words carries every rank's
-            # count and (when they fit) its pairs; a larger count sends the rest in a second round
-            with slots.slot(6):
-                pairs = self._gather_pairs(comm, pb, 2 * max(pcap, 1))
-        npair = len(pairs) // 2
-        pairs = np.ascontiguousarray(pairs, np.int64)
-        nk = int(lib.rpt_merge_equivalences(pairs.ctypes.data_as(A.c_i64p), npair, None, None, 0))
-        keys = np.empty(max(nk, 1), np.int64)
-        vals = np.empty(max(nk, 1), np.int64)
-        lib.rpt_merge_equivalences(pairs.ctypes.data_as(A.c_i64p), npair,
-                                   keys.ctypes.data_as(A.c_i64p), vals.ctypes.data_as(A.c_i64p),
-                                   nk)
-        # 7. representatives this rank owns, every rank's (ascending in rank order)
-        roots = ws.get("roots", max(n_own, 1), torch.int64)
-        nr = C_.c_int64(0)
-        if n_tot:
-            chk(lib.rpt_shard_roots(self.h, keys.ctypes.data_as(A.c_i64p),
-                                    vals.ctypes.data_as(A.c_i64p), nk, base, n_prev, n_own,
-                                    roots.data_ptr(), C_.byref(nr), st), "rpt_shard_roots")
-        if W > 1:
-            with slots.slot(7):
-                all_roots, mx = comm.all_gather_capped(roots[:int(nr.value)], self._cap_roots)
-            self._cap_roots = max(self._cap_roots, mx + mx // 4 + 64)
-        else:
-            all_roots = [roots[:int(nr.value)]]
-        reps = torch.cat([a.to(self.dev) for a in all_roots]).contiguous()
-        n_clusters = int(reps.numel())
-        # 8. labels + K9 of the own frames (one readback)
-        nseg = C_.c_int64(0)
-        if n_tot:
-            chk(lib.rpt_shard_finish(self.h, reps.data_ptr(), n_clusters, C_.byref(nseg), st),
-                "rpt_shard_finish")
-        S = int(nseg.value)
-        seg = {"frame": np.empty(S, np.int32), "label": np.empty(S, np.int32),
-               "count": np.empty(S, np.int64), "first": np.empty(S, np.int64),
-               "cx": np.empty(S, np.float32), "cy": np.empty(S, np.float32),
-               "mi": np.empty(S, np.float32)}
-        first_noise = np.full(F, -1, np.int64)
-        if n_tot:
-            ptr = lambda a, t: a.ctypes.data_as(t)  # noqa: E731
-            chk(lib.rpt_shard_segments(
-                self.h, ptr(seg["frame"], A.c_i32p), ptr(seg["label"], A.c_i32p),
-                ptr(seg["count"], A.c_i64p), ptr(seg["first"], A.c_i64p),
-                ptr(seg["cx"], A.c_f32p), ptr(seg["cy"], A.c_f32p), ptr(seg["mi"], A.c_f32p),
-                ptr(first_noise, A.c_i64p)), "rpt_shard_segments")
-        fo = np.empty(F + 1, np.int64)
-        chk(lib.rpt_shard_frame_offsets(self.h, 0, fo.ctypes.data_as(A.c_i64p)),
-            "rpt_shard_frame_offsets")
-        built_local = np.nonzero(np.diff(fo) > 0)[0]
-        packed = np.concatenate([
-            [S, frame0], built_local.astype(np.float64), [-1.0] * (F - len(built_local)),
-            first_noise, seg["frame"], seg["label"], seg["count"], seg["first"], seg["cx"],
-            seg["cy"], seg["mi"]]).astype(np.float64)
-        if W > 1:
-            with slots.slot(8):
-                parts, mx = comm.all_gather_capped(torch.from_numpy(packed), self._cap_parts)
-            self._cap_parts = max(self._cap_parts, mx + mx // 4 + 64)
-            parts = [q.cpu() for q in parts]
-        else:
-            parts = [torch.from_numpy(packed)]
+                owp, own_ = comm.exchange_known(csp[:n_head] if has_p else csp[:0],
+                                                csn[:n_tail] if has_n else csn[:0],
+                                                n_prev, n_next)
+        # 6.-7. pairs, gathered; merge, labels, K9 and the packed results, gathered
+        g_host, gathered, cap_out = self._finish(slots, owp, own_, W, r)
         mark("stdbscan")
-        self._n_own = n_own if n_tot else 0
-        labels = None
+        if int(g_host[:, 7].sum()) == 0 and n_built > 0:   # BallTree on 0 samples
+            raise ValueError("Found array with 0 sample(s) (shape=(0, 2)) while a minimum of 1 "
+                             "is required.")
+        self._last = (gathered, W, cap_out)
         res = ShardResult(n_points_local=n_points, n_points_global=n_global,
-                          n_clustered_local=n_own, n_clusters=n_clusters, labels_local=labels)
+                          n_clustered_local=n_own, n_clusters=-1, labels_local=None)
         if r == 0:
-            res.n_segments = int(sum(float(t[0]) for t in parts))
-
-            def host_stage():
-                t0 = time.perf_counter()
-                all_seg, built, fo_g, order_g = _unpack_parts(parts, F)
-                trk = track_ordered(built - frame0, fo_g, order_g, all_seg, p, built)
-                return all_seg, built, fo_g, order_g, trk, (time.perf_counter() - t0) * 1e3
-
+            sizes = np.zeros(4, np.int64)
+            gh = np.ascontiguousarray(g_host)
+            chk(lib.rpt_shard_gathered_sizes(gh.ctypes.data_as(A.c_i64p), W, cap_out,
+                                             sizes.ctypes.data_as(A.c_i64p)),
+                "rpt_shard_gathered_sizes")
+            res.n_segments, res.n_clusters = int(sizes[0]), int(sizes[3])
+            host_stage = self._host_stage(gh, W, cap_out, sizes, p)
             if self._host is not None:
                 res._pending = self._host.submit(host_stage)
             else:
@@ -852,42 +809,172 @@ class NativeShardPipeline:
         if self.timing:
             for (a, ta), (b, tb) in zip(marks[:-1], marks[1:]):
                 res.stage_ms[b] = (tb - ta) * 1e3
+        res.t_done = time.perf_counter()
         return res
 
-    def _gather_pairs(self, comm: Comm, pb: torch.Tensor, room: int) -> np.ndarray:
-        """Every rank's equivalence pairs from pb = [count | 2*count ids] (device), in one
-        collective while every count fits the capacity."""
-        if comm.world == 1:
-            k = int(pb[0].item())
-            return pb[1:1 + 2 * k].cpu().numpy()
-        cap = self._cap_pairs
-        buf = torch.zeros(1 + cap, dtype=torch.int64, device=comm.cdev)
-        w = min(1 + room, 1 + cap)
-        buf[:w] = pb[:w].to(comm.cdev)
-        out = torch.empty(comm.world * (1 + cap), dtype=torch.int64, device=comm.cdev)
-        dist.all_gather_into_tensor(out, buf, group=comm.group)
-        out = out.reshape(comm.world, 1 + cap).cpu().numpy()
-        cnts = out[:, 0]
-        m = int(cnts.max()) if len(cnts) else 0
-        self._cap_pairs = max(cap, 2 * m + 64)
-        if 2 * m <= cap:
-            return np.concatenate([row[1:1 + 2 * int(c)] for row, c in zip(out, cnts)])
-        k = int(cnts[comm.rank])
-        full = comm.all_gather_fixed(pb[1:1 + 2 * m].contiguous() if 2 * m <= room else
-                                     torch.cat([pb[1:1 + 2 * k],
-                                                torch.zeros(2 * m - 2 * k, dtype=torch.int64,
-                                                            device=pb.device)])).numpy()
-        return np.concatenate([row[:2 * int(c)] for row, c in zip(full, cnts)])
+    def _finish(self, slots, owp, own_, W: int, r: int):
+        """pairs -> [all_gather] -> finish -> [all_gather] -> readback; finished again (slot 7,
+        every rank alike) while some rank's pairs or results did not fit their capacity, the
+        merge needs the host, or K9 must take the radix path."""
+        A, lib, comm, ws = self._abi, self.lib, self.comm, self.ws
+        from ._device import stream_handle
+        st = stream_handle(self.dev)
+
+        def ptr(t):
+            return t.data_ptr() if t is not None and t.numel() else None
+
+        def pairs_step():
+            cap = self._cap_pairs
+            pb = ws.get("pairs", 1 + 2 * cap, torch.int64)
+            A.check(lib.rpt_shard_pairs(self.h, ptr(owp), ptr(own_), pb.data_ptr(), cap, st),
+                    "rpt_shard_pairs")
+            return pb, cap
+
+        def gather(t):
+            return comm.all_gather_dev(t) if W > 1 else t
+
+        def finish_step(pb, gp, row, keys=None, vals=None, radix=False):
+            cap_out = self._cap_out
+            out = ws.get("out", cap_out, torch.int64)
+            if keys is None:
+                A.check(lib.rpt_shard_finish(self.h, gp.data_ptr(), W, row, pb.data_ptr(), None,
+                                             None, 0, 1 if radix else 0, out.data_ptr(), cap_out,
+                                             st), "rpt_shard_finish")
+            else:
+                A.check(lib.rpt_shard_finish(self.h, None, W, row, pb.data_ptr(),
+                                             keys.ctypes.data_as(A.c_i64p),
+                                             vals.ctypes.data_as(A.c_i64p), len(keys),
+                                             1 if radix else 0, out.data_ptr(), cap_out, st),
+                        "rpt_shard_finish")
+            return out, cap_out
+
+        def readback(g, cap_out):
+            g2 = g.reshape(W, cap_out)
+            if r == 0:
+                return g2.cpu().numpy()
+            h = np.zeros((W, cap_out), np.int64)   # the other ranks need the headers only
+            h[:, :8] = g2[:, :8].cpu().numpy()
+            return h
+
+        pb, cap = pairs_step()
+        with slots.slot(5):
+            gp = gather(pb)
+        out, cap_out = finish_step(pb, gp, 1 + 2 * cap)
+        with slots.slot(6):
+            g = gather(out)
+        g_host = readback(g, cap_out)
+        hdr = g_host[:, :8]
+        bad = int(np.bitwise_or.reduce(hdr[:, 3])) or bool((hdr[:, 1] < 0).any())
+        if not bad:
+            return g_host, g, cap_out
+        with slots.slot(7):   # rare: the same decisions on every rank (every header is seen)
+            keys = vals = None
+            for _ in range(4):
+                hdr = g_host[:, :8]
+                flags = int(np.bitwise_or.reduce(hdr[:, 3]))
+                radix = bool(hdr[r, 1] < 0)
+                if not flags and not (hdr[:, 1] < 0).any():
+                    break
+                if flags & 1:   # some rank's pairs exceeded the capacity
+                    counts = gp.reshape(W, 1 + 2 * cap)[:, 0].cpu().numpy()
+                    self._cap_pairs = int(counts.max()) + int(counts.max()) // 4 + 64
+                    pb, cap = pairs_step()
+                    gp = gather(pb)
+                    keys = vals = None
+                if flags & 2 or keys is not None:   # too many ids for the device merge
+                    rows = gp.reshape(W, 1 + 2 * cap).cpu().numpy()
+                    pairs = np.concatenate([row[1:1 + 2 * int(min(row[0], cap))]
+                                            for row in rows]).astype(np.int64)
+                    nk = int(lib.rpt_merge_equivalences(pairs.ctypes.data_as(A.c_i64p),
+                                                        len(pairs) // 2, None, None, 0))
+                    keys = np.empty(max(nk, 1), np.int64)
+                    vals = np.empty(max(nk, 1), np.int64)
+                    lib.rpt_merge_equivalences(pairs.ctypes.data_as(A.c_i64p), len(pairs) // 2,
+                                               keys.ctypes.data_as(A.c_i64p),
+                                               vals.ctypes.data_as(A.c_i64p), nk)
+                    keys, vals = keys[:nk], vals[:nk]
+                if flags & 4:   # some rank's results exceeded the capacity
+                    need = int(hdr[:, 4].max())
+                    self._cap_out = need + need // 4 + 1024
+                out, cap_out = finish_step(pb, gp, 1 + 2 * cap, keys, vals, radix)
+                g = gather(out)
+                g_host = readback(g, cap_out)
+            else:
+                raise RuntimeError("rpt_shard: the packed results did not settle")
+        return g_host, g, cap_out
+
+    def _host_stage(self, gh: np.ndarray, W: int, cap_out: int, sizes: np.ndarray, p):
+        """Rank 0: one native call (GIL released) -- global labels, every segment, the built
+        frames, the reference cluster order and the tracker."""
+        from .native_tracker import NativeTracker
+        A, lib = self._abi, self.lib
+
+        def host_stage():
+            t0 = time.perf_counter()
+            S, B, Ft = int(sizes[0]), int(sizes[1]), int(sizes[2])
+            seg = {"frame": np.empty(S, np.int32), "label": np.empty(S, np.int32),
+                   "count": np.empty(S, np.int64), "first": np.empty(S, np.int64),
+                   "cx": np.empty(S, np.float32), "cy": np.empty(S, np.float32),
+                   "mi": np.empty(S, np.float32)}
+            built = np.empty(max(B, 1), np.int64)
+            fo = np.empty(Ft + 1, np.int64)
+            order = np.empty(max(S, 1), np.int64)
+            trk = NativeTracker(p.max_association_distance, p.max_missed_frames,
+                                p.motion_history_frames, p.stationary_velocity_threshold)
+            P = lambda a, t: a.ctypes.data_as(t)  # noqa: E731
+            A.check(lib.rpt_shard_host_stage(
+                P(gh, A.c_i64p), W, cap_out, trk._h, P(seg["frame"], A.c_i32p),
+                P(seg["label"], A.c_i32p), P(seg["count"], A.c_i64p), P(seg["first"], A.c_i64p),
+                P(seg["cx"], A.c_f32p), P(seg["cy"], A.c_f32p), P(seg["mi"], A.c_f32p),
+                P(built, A.c_i64p), P(fo, A.c_i64p), P(order, A.c_i64p), None, -1),
+                "rpt_shard_host_stage")
+            return seg, built[:B], fo, order[:S], trk, (time.perf_counter() - t0) * 1e3
+
+        return host_stage
 
     def labels_local(self) -> torch.Tensor:
-        """Labels (device int32, a copy) of this rank's kept points of the last run."""
+        """Global labels (device int32, a copy) of this rank's kept points of the last run (reads
+        every rank's representative table back: for checks, not the hot path)."""
         from ._device import stream_handle
-        out = torch.empty(self._n_own, dtype=torch.int32, device=self.dev)
-        if self._n_own:
-            self._abi.check(self.lib.rpt_shard_labels(self.h, out.data_ptr(),
-                                                      stream_handle(self.dev)),
-                            "rpt_shard_labels")
+        A = self._abi
+        gathered, W, cap = self._last
+        gh = np.ascontiguousarray(gathered.reshape(W, cap).cpu().numpy())
+        r = self.comm.rank
+        nr = int(gh[r, 2])
+        m = np.empty(max(nr, 1), np.int32)
+        A.check(self.lib.rpt_shard_host_stage(gh.ctypes.data_as(A.c_i64p), W, cap, None, None,
+                                              None, None, None, None, None, None, None, None,
+                                              None, m.ctypes.data_as(A.c_i32p), r),
+                "rpt_shard_host_stage")
+        md = torch.from_numpy(m).to(self.dev)
+        n = int(gh[r, 7])
+        out = torch.empty(n, dtype=torch.int32, device=self.dev)
+        if n:
+            A.check(self.lib.rpt_shard_labels(self.h, md.data_ptr(), nr, out.data_ptr(),
+                                              stream_handle(self.dev)), "rpt_shard_labels")
         return out
+
+
+class ShardStepFuture(Future):
+    """Future of one ShardLanes step: every way of waiting on it through its own methods closes
+    the sequencer's open group first, so a partial group (fewer than `lanes` steps) is never
+    left waiting for steps that will not be submitted."""
+
+    def __init__(self, seq: "CommSequencer"):
+        super().__init__()
+        self._seq = seq
+
+    def result(self, timeout=None):
+        self._seq.close_group()
+        return super().result(timeout)
+
+    def exception(self, timeout=None):
+        self._seq.close_group()
+        return super().exception(timeout)
+
+    def add_done_callback(self, fn):
+        self._seq.close_group()
+        super().add_done_callback(fn)
 
 
 class ShardLanes:
@@ -902,11 +989,17 @@ class ShardLanes:
 
     def __init__(self, dev: torch.device, lanes: int, gains: Sequence[int], rows: int,
                  bins: int, params: PathParams = None, timing: bool = False,
-                 async_host: bool = False, host_workers: int = 2):
+                 async_host: bool = False, host_workers: int = 2,
+                 sequenced: Optional[bool] = None):
+        """sequenced: order the lanes' collective slots (default: with more than one rank; at
+        one rank every collective is the identity -- True keeps the ordering anyway, to measure
+        what it costs)."""
         if lanes < 1:
             raise ValueError("lanes must be >= 1")
         self.dev = dev
         comm = Comm(dev)
+        self.world = comm.world
+        self.sequenced = comm.world > 1 if sequenced is None else bool(sequenced)
         self.pipes = [NativeShardPipeline(comm, gains, rows, bins, params, timing=timing,
                                           async_host=async_host, host_workers=host_workers)
                       for _ in range(lanes)]
@@ -919,37 +1012,45 @@ class ShardLanes:
         for p in self.pipes:
             p.set_geometry(scale, cos_t, sin_t, n_files)
 
-    def submit(self, echo: torch.Tensor, frame0: int) -> Future:
-        """Runs the next step on lane step % lanes; Future of its ShardResult (call finish())."""
+    def submit(self, echo: torch.Tensor, frame0: int) -> "ShardStepFuture":
+        """Runs the next step on lane step % lanes; a future of its ShardResult (call finish()).
+        Waiting on it through result() / exception() / add_done_callback() first closes the
+        open group (the same on every rank); a caller waiting by other means
+        (concurrent.futures.wait, as_completed) calls flush() first."""
         step = self._step
         self._step += 1
         li = step % len(self.pipes)
         pipe, s = self.pipes[li], self.streams[li]
         self.seq.register(step)
-        slots = self.seq.step(step)
+        # one rank: every collective is the identity, nothing to order
+        slots = self.seq.step(step) if self.sequenced else _NoSlots()
+        fut = ShardStepFuture(self.seq)
 
         def work():
+            if not fut.set_running_or_notify_cancel():
+                return
             try:
                 with torch.cuda.device(self.dev):
                     if s is None:
-                        return pipe.run(echo, frame0, slots)
-                    s.wait_stream(torch.cuda.default_stream(self.dev))  # the echo is ready
-                    with torch.cuda.stream(s):
-                        return pipe.run(echo, frame0, slots)
+                        r = pipe.run(echo, frame0, slots)
+                    else:
+                        s.wait_stream(torch.cuda.default_stream(self.dev))  # the echo is ready
+                        with torch.cuda.stream(s):
+                            r = pipe.run(echo, frame0, slots)
             except BaseException as e:
                 self.seq.abort(e)
-                raise
+                fut.set_exception(e)
+                return
+            fut.set_result(r)
 
-        fut = self.pools[li].submit(work)
-        seq = self.seq
-        wait = fut.result
-
-        def result(timeout=None):  # waiting on a step closes the open group (same on all ranks)
-            seq.close_group()
-            return wait(timeout)
-
-        fut.result = result
+        self.pools[li].submit(work)
         return fut
+
+    def flush(self):
+        """Close the open group: its steps take their collective turns without waiting for more
+        submissions (call before waiting on steps by any means other than the futures' own
+        result() / exception() / add_done_callback(); every rank at the same point)."""
+        self.seq.close_group()
 
     def close(self):
         self.seq.close_group()

@@ -60,6 +60,7 @@ class StackResult:
     labels: Optional[torch.Tensor] = None
     points: Optional[Dict[str, torch.Tensor]] = None
     stage_ms: Dict[str, float] = field(default_factory=dict)
+    t_done: float = 0.0              # perf_counter when the device work and readbacks ended
     _pending: Optional[Future] = None
 
     def finish(self) -> "StackResult":
@@ -135,33 +136,39 @@ class FrameStackPipeline:
             raise TypeError("echo must be uint8 or float32")
         return dt
 
-    def run(self, echo: torch.Tensor, keep_points: bool = False) -> StackResult:
+    def run(self, echo: torch.Tensor, keep_points: bool = False,
+            keep_core: bool = False) -> StackResult:
         """K1 -> land filter -> ST-DBSCAN -> K9 in one native call (rpt_stack_run), then the
-        host stage (cluster order + tracker) inline or on the worker pool (async_host)."""
-        return self._run_lane(self._h, stream_handle(self.dev), echo, keep_points)
+        host stage (cluster order + tracker) inline or on the worker pool (async_host).
+        keep_points: hand back the clustered points and their labels (res.points, res.labels);
+        keep_core: also K5's core flag of every such point (res.points["core"], the full-size
+        invariant tests; one more kernel and sync)."""
+        return self._run_lane(self._h, stream_handle(self.dev), echo, keep_points, keep_core)
 
-    def submit(self, echo: torch.Tensor, keep_points: bool = False) -> Future:
+    def submit(self, echo: torch.Tensor, keep_points: bool = False,
+               keep_core: bool = False) -> Future:
         """Queues a run on the next lane and returns a Future of its StackResult (lanes == 1:
         runs inline).  The echo must stay unchanged until the future is done."""
         if self._lane_pool is None:
             f = Future()
-            f.set_result(self.run(echo, keep_points))
+            f.set_result(self.run(echo, keep_points, keep_core))
             return f
         lane = self._next_lane
         self._next_lane = (lane + 1) % len(self._hs)
         s = self._streams[lane]
         s.wait_stream(torch.cuda.current_stream(self.dev))  # the echo's producer
         return self._lane_pool[lane].submit(self._run_lane, self._hs[lane], s.cuda_stream, echo,
-                                            keep_points)
+                                            keep_points, keep_core)
 
-    def _run_lane(self, h, stream: int, echo: torch.Tensor, keep_points: bool) -> StackResult:
+    def _run_lane(self, h, stream: int, echo: torch.Tensor, keep_points: bool,
+                  keep_core: bool = False) -> StackResult:
         # librpt allocates and records events on the calling thread's current HIP device; lane
         # threads (and callers whose current device differs) must run on the pipeline's
         with torch.cuda.device(self.dev):
-            return self._run_lane_dev(h, stream, echo, keep_points)
+            return self._run_lane_dev(h, stream, echo, keep_points, keep_core)
 
-    def _run_lane_dev(self, h, stream: int, echo: torch.Tensor, keep_points: bool
-                      ) -> StackResult:
+    def _run_lane_dev(self, h, stream: int, echo: torch.Tensor, keep_points: bool,
+                      keep_core: bool) -> StackResult:
         p, lib = self.p, self.lib
         G = len(self.gains)
         F = echo.shape[0]
@@ -207,7 +214,8 @@ class FrameStackPipeline:
                           frame_ids=built, n_land_cells=int(r.n_land_cells),
                           n_clusters=int(r.n_clusters), n_segments=S, seg=seg,
                           frame_order_offsets=None, frame_order=None, tracker=None,
-                          stage_ms=stage_ms, first_noise=first_noise)
+                          stage_ms=stage_ms, first_noise=first_noise,
+                          t_done=time.perf_counter())
 
         def host_stage():
             t0 = time.perf_counter()
@@ -233,7 +241,7 @@ class FrameStackPipeline:
                                             pts["v"].data_ptr(), pts["gain"].data_ptr(),
                                             pts["frame"].data_ptr(), labels.data_ptr(), stream),
                        "rpt_stack_points")
-            if n:  # K5's core flags of the same points (full-size invariant checks)
+            if n and keep_core:  # K5's core flags of the same points (invariant checks)
                 pts["core"] = torch.empty(n, dtype=torch.uint8, device=self.dev)
                 if stream != stream_handle(self.dev):
                     torch.cuda.current_stream(self.dev).synchronize()

@@ -96,13 +96,13 @@ def test_sharded_share_matches_oracle(world, lanes):
     assert "ok=True" in out, out[-4000:]
 
 
-@pytest.mark.timeout(600)
-def test_dense_config4_share_invariants(gpu):
-    """configs[4]'s per-GPU share at 8 GPUs: 125 dense frames (~490k points per frame, ~61 M
-    points, one component chaining the stack) — too large for a whole-stack oracle run, so
-    full-size invariants of the reference semantics instead:
-      * K5: the core flags of 20,000 random points equal the oracle's exact neighbour count
-        >= min_samples (oracle.sample_check);
+def _dense_invariants(gpu, n_frames, min_points):
+    """Full-size invariants of the reference semantics on a dense stack the
+    whole-stack oracle cannot label:
+      * K5: the core flags of >= 200,000 sample points equal the oracle's exact neighbour count
+        >= min_samples (oracle.sample_check) -- 180,000 random points plus EVERY point of 50
+        random 16 m x 16 m patches of random frames, so whole cells (K5 decides most cells as a
+        unit) are checked point by point, not one sample per cell;
       * a core sample's core neighbours all carry its label; a non-core sample carries the
         smallest label among its core neighbours, -1 without one (4_temporal_object_tracker.py
         :493-504, the BFS's result);
@@ -115,25 +115,35 @@ def test_dense_config4_share_invariants(gpu):
     from rpt.pipeline import FrameStackPipeline, PathParams
     from rpt.synth import DeviceSynth, dense_config
 
-    cfg = dense_config(n_frames=125)
+    cfg = dense_config(n_frames=n_frames)
     ds = DeviceSynth(cfg, gpu)
     pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), gpu)
     pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
                       cfg.n_frames * len(cfg.gains))
-    res = pipe.run(ds.echo(), keep_points=True)
+    res = pipe.run(ds.echo(), keep_points=True, keep_core=True)
     n = res.n_clustered_input
-    assert n > 55_000_000
+    assert n > min_points
     x = res.points["x"].cpu().numpy()
     y = res.points["y"].cpu().numpy()
     v = res.points["v"].cpu().numpy()
     pf = res.points["frame"].cpu().numpy()
     core = res.points["core"].cpu().numpy()
     lab = res.labels.cpu().numpy()
+    del res.points, res.labels
     xy = np.column_stack([x, y])
     t = pf.astype(np.float32)
+    fstart = np.searchsorted(pf, np.arange(pf.max() + 2))
 
     rng = np.random.default_rng(7)
-    idx = np.unique(np.concatenate([rng.choice(n, 20_000, replace=False), [0, n - 1]]))
+    patches = []
+    for f in rng.choice(int(pf.max()) + 1, 50):
+        a, b = fstart[f], fstart[f + 1]
+        c = xy[a + rng.integers(0, b - a)]
+        inside = (np.abs(x[a:b] - c[0]) <= 8.0) & (np.abs(y[a:b] - c[1]) <= 8.0)
+        patches.append(a + np.nonzero(inside)[0])
+    patch = np.concatenate(patches)
+    idx = np.unique(np.concatenate([rng.choice(n, 180_000, replace=False), patch, [0, n - 1]]))
+    assert len(idx) >= 200_000 and len(patch) > 15_000
     cnt, lo, hi = oracle.sample_check(xy, t, 8.0, 2.0, idx, core, lab)
     np.testing.assert_array_equal(core[idx], (cnt >= 15).astype(np.uint8))
     c = core[idx] == 1
@@ -159,7 +169,6 @@ def test_dense_config4_share_invariants(gpu):
     assert seg["count"].sum() == m.sum() and len(uk) == res.n_segments
     pick = np.unique(np.concatenate([[int(np.argmax(seg["count"]))],
                                      rng.choice(res.n_segments, 40, replace=False)]))
-    fstart = np.searchsorted(pf, np.arange(pf.max() + 2))
     for s in pick:
         f, lb = int(seg["frame"][s]), int(seg["label"][s])
         a, b = fstart[f], fstart[f + 1]
@@ -167,3 +176,18 @@ def test_dense_config4_share_invariants(gpu):
         cxy = np.mean(xy[a:b][sel], axis=0)
         assert (seg["cx"][s], seg["cy"][s]) == (cxy[0], cxy[1]), (f, lb)
         assert seg["mi"][s] == np.float32(np.mean(v[a:b][sel])), (f, lb)
+
+
+@pytest.mark.timeout(600)
+def test_dense_config4_share_invariants(gpu):
+    """configs[4]'s per-GPU share at 8 GPUs: 125 dense frames (~490k points per frame, ~61 M
+    points, one component chaining the stack); _dense_invariants."""
+    _dense_invariants(gpu, 125, 55_000_000)
+
+
+@pytest.mark.timeout(900)
+def test_dense_above_2_26_points_invariants(gpu):
+    """140 dense frames: ~68.7 M points enter ST-DBSCAN, past 2^26 = 67.1 M, where K5's fill
+    pass keeps its per-cell (original, sorted) minima in 64 bits (csrc/stdbscan.hip
+    k_core_fill); the configs[4] share at fewer than 8 GPUs is above it.  _dense_invariants."""
+    _dense_invariants(gpu, 140, 1 << 26)

@@ -106,6 +106,33 @@ def test_denoise_wide_time_window(gpu, eps_time, min_frames, float_t):
     np.testing.assert_array_equal(lab, ref)
 
 
+@pytest.mark.parametrize("eps_time,min_frames", [(40.0, 6), (2.0, 4)])
+def test_denoise_wide_slabs(gpu, eps_time, min_frames):
+    """Long runs of frames over a small region: the grid's cell cap (max(2^22, 4n) cells) widens
+    the slabs to two frames each (ct = 2), so a cell wholly inside eps can hold points of two
+    frames and must not be counted as one (k_frames_points / k_frames_points_list)."""
+    from rpt.denoise import st_dbscan
+
+    rng = np.random.default_rng(7)
+    n_frames = 200_000
+    pts, ts = [], []
+    for c in rng.random((400, 2)) * 30:
+        f0 = int(rng.integers(0, n_frames - 12))
+        fr = np.repeat(np.arange(f0, f0 + 10), 2)   # two returns per frame, 10 frames
+        pts.append(c + rng.normal(0, 0.5, (len(fr), 2)))
+        ts.append(fr)
+    pts.append(rng.random((20_000, 2)) * 30)
+    ts.append(rng.integers(0, n_frames, 20_000))
+    xy = np.vstack(pts).astype(np.float32)
+    t = np.concatenate(ts).astype(np.float32)
+    perm = rng.permutation(len(t))
+    xy, t = xy[perm], t[perm]
+    lab = st_dbscan(xy, t, 8.0, eps_time, 4, min_frames, device=gpu)
+    ref = oracle.stdbscan_denoise(xy, t, 8.0, eps_time, 4, min_frames)
+    assert (ref >= 0).sum() > 2000
+    np.testing.assert_array_equal(lab, ref)
+
+
 def test_label_means_match_pandas_group_mean(gpu):
     """rpt_label_means = pandas groupby mean of float32 columns (Kahan-compensated float32)."""
     import pandas as pd
@@ -179,3 +206,45 @@ def test_denoise_pipeline_malformed_files_parallel(tmp_path, golden):
         assert (out / name).read_bytes() == bytes(g["denoise_" + name.replace(".", "_")]), name
     for name in ("denoising_stats.csv", "clusters.csv"):
         assert (out / name).read_text() == str(g["denoise_" + name.replace(".", "_")]), name
+
+
+def test_denoise_loader_other_bin_counts(gpu, tmp_path):
+    """The genfromtxt loader takes num_bins from the file (data[:, 5:], :128-134): a sweep of 512
+    echo columns has range resolution Scale / 512; a file of only Status..Angle has no echo
+    column and no point.  Points of every file in frame / file order against the reference's
+    arithmetic on np.genfromtxt's array (oracle.path.polar_scatter)."""
+    sys.path.insert(0, str(GOLDEN))
+    from make_golden import echo_block, write_csv
+
+    from oracle.path import polar_scatter, trig_tables
+    from rpt.denoise import load_frames
+
+    rng = np.random.default_rng(11)
+    rows = 40
+    frames, expect = [], []
+    for f in range(3):
+        fr = {}
+        for k, (g, bins) in enumerate(((40, 1024), (50, 512 if f == 1 else 1024),
+                                       (75, 0 if f == 2 else 1024))):
+            p = tmp_path / f"f{f}_g{g}.csv"
+            scale = rng.uniform(500, 2000, rows).astype(np.float32)
+            angle = np.sort(rng.choice(8196, rows, replace=False))
+            if bins:
+                write_csv(p, 1, scale, 0, g, angle, echo_block(rng, rows, bins))
+            else:   # Status..Angle only
+                p.write_text("Status,Scale,Range,Gain,Angle\n" + "".join(
+                    f"1,{scale[r]:g},0,{g},{angle[r]}\n" for r in range(rows)))
+            fr[k] = p
+            if bins:
+                data = np.genfromtxt(p, delimiter=",", skip_header=1, dtype=np.float32,
+                                     filling_values=0.0)
+                c, s = trig_tables(data[:, 4])
+                xs, ys, vs = polar_scatter(data[:, 5:], data[:, 1], c, s)
+                expect.append((xs, ys, vs, np.full(len(xs), f, np.float32)))
+        frames.append(fr)
+    got = load_frames(frames, device=gpu)
+    for k, name in enumerate(("x", "y", "z", "t")):
+        np.testing.assert_array_equal(getattr(got, name).cpu().numpy(),
+                                      np.concatenate([e[k] for e in expect]), err_msg=name)
+    assert got.frame_counts.tolist() == [sum(len(e[0]) for e in expect if e[3][:1].tolist() == [f])
+                                         for f in range(3)]

@@ -202,8 +202,9 @@ def test_all_gather_capped_gloo():
 
 def test_comm_sequencer_orders_lanes_deterministically():
     """rpt.dist.CommSequencer: several lane threads, random delays between their slots and
-    skipped slots -- the slots are entered in ONE order, (step // L, phase, step % L), whatever
-    the timing, so every rank issues its collectives in the same order on one communicator."""
+    skipped slots -- the slots are entered in ONE order (the software-pipeline order: step s
+    takes phase p at time s * d + p, ties by step), whatever the timing, so every rank issues its
+    collectives in the same order on one communicator."""
     import random
     import threading
     from concurrent.futures import ThreadPoolExecutor
@@ -243,11 +244,50 @@ def test_comm_sequencer_orders_lanes_deterministically():
         seq.close_group()
         for f in futs:
             f.result(timeout=30)
-        groups = [(0, 3), (3, 2), (5, 3), (8, 3), (11, 2)]  # (first step, size)
-        gi = {s: k for k, (a, n) in enumerate(groups) for s in range(a, a + n)}
+        # two epochs (the wait after step 4 closes the first): step s of an epoch starting at
+        # step a with base time b takes phase p at time b + (s - a) * d + p, d = ceil(P / L)
+        d = -(-P // L)
+        base = {s: (0, 0) if s < 5 else (5, 4 * d + P) for s in range(steps)}
         exp = sorted(((s, p) for s in range(steps) for p in range(P) if (s, p) not in skip),
-                     key=lambda sp: (gi[sp[0]], sp[1], sp[0]))
+                     key=lambda sp: (base[sp[0]][1] + (sp[0] - base[sp[0]][0]) * d + sp[1],
+                                     sp[0]))
         assert log == exp
+
+
+def test_shard_step_future_closes_partial_group():
+    """A group of fewer than `lanes` steps: waiting through the step future's result(),
+    exception() or add_done_callback() closes it (the steps' later phases can take their turn);
+    ShardLanes.flush() is the same close for callers waiting by other means."""
+    import threading
+
+    from rpt.dist import CommSequencer, ShardStepFuture
+
+    for how in ("result", "exception", "callback"):
+        seq = CommSequencer(3, 2)
+        seq.register(0)
+        fut = ShardStepFuture(seq)
+
+        def work():
+            slots = seq.step(0)
+            with slots.slot(0):
+                pass
+            with slots.slot(1):   # phase > 0 waits until the group is closed
+                pass
+            slots.close()
+            fut.set_result(7)
+
+        t = threading.Thread(target=work)
+        t.start()
+        if how == "result":
+            assert fut.result(timeout=5) == 7
+        elif how == "exception":
+            assert fut.exception(timeout=5) is None
+        else:
+            done = threading.Event()
+            fut.add_done_callback(lambda f: done.set())
+            assert done.wait(5)
+        t.join(5)
+        assert not t.is_alive()
 
 
 def test_comm_sequencer_abort_releases_waiters():

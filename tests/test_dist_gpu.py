@@ -23,20 +23,7 @@ def _free_port():
     return p
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("world,frames,impl,lanes", [(2, 14, "native", 1), (3, 6, "native", 1),
-                                                     (2, 14, "python", 1), (2, 8, "native", 2),
-                                                     (3, 6, "native", 3),
-                                                     (3, 6, "native-tinycaps", 1)])
-def test_sharded_gpu_matches_single_gpu(world, frames, impl, lanes):
-    """lanes = 2 / 3: stacks in flight (rpt.dist.ShardLanes: a stream and thread per lane, every
-    lane's collectives through the ONE process group in the CommSequencer's global order; the
-    bench's N > 1 default is 2); each lane's last run is checked.  native-tinycaps: the one-collective gathers
-    (pairs, representatives, segments) with one-element capacities, i.e. their two-round
-    fallbacks."""
-    extra = []
-    if impl == "native-tinycaps":
-        impl, extra = "native", ["--tiny-caps"]
+def _run(world, frames, impl, lanes, extra, timeout=600):
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
@@ -44,7 +31,37 @@ def test_sharded_gpu_matches_single_gpu(world, frames, impl, lanes):
            f"--master-port={_free_port()}", str(ROOT / "tools" / "dist_check.py"),
            "--backend", "gloo", "--frames", str(frames), "--impl", impl, "--lanes", str(lanes),
            *extra]
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-4000:]
     assert "ok=True" in out, out[-4000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,frames,impl,lanes", [(2, 14, "native", 1), (3, 6, "native", 1),
+                                                     (2, 14, "python", 1), (2, 8, "native", 2),
+                                                     (3, 6, "native", 3),
+                                                     (3, 6, "native-tinycaps", 1),
+                                                     (4, 4, "native-tinycaps", 2)])
+def test_sharded_gpu_matches_single_gpu(world, frames, impl, lanes):
+    """lanes = 2 / 3: stacks in flight (rpt.dist.ShardLanes: a stream and thread per lane, every
+    lane's collectives through the ONE process group in the CommSequencer's software-pipeline
+    order); each lane's last run is checked.  native-tinycaps: one-pair / 16-word capacities for
+    the pair and packed-result gathers, so every step is finished again with grown capacities
+    (the redo slot)."""
+    extra = []
+    if impl == "native-tinycaps":
+        impl, extra = "native", ["--tiny-caps"]
+    _run(world, frames, impl, lanes, extra)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("world,frames,lanes", [(8, 2, 1), (4, 4, 2)])
+def test_sharded_dense_giant_component_matches_oracle(world, frames, lanes):
+    """configs[4]'s density split over ranks of 2 and 4 frames: one giant component crosses
+    every rank boundary (its halo ids pair up along the whole chain), ~490k points per frame;
+    rank 0 compares labels, the per-frame cluster rows in reference order and the tracked objects
+    with the oracle's run_path (union-find ST-DBSCAN) over the whole stack
+    (4_temporal_object_tracker.py:466-506, 508-536, 984-991)."""
+    _run(world, frames, "native", lanes, ["--dense", "--oracle"], timeout=840)

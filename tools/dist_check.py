@@ -42,9 +42,15 @@ def main():
     ap.add_argument("--digest", default=None,
                     help="comma-separated bigstack workloads (tests/golden/bigstack_<name>.json): "
                          "compare with the oracle digests instead of the single-GPU pipeline")
+    ap.add_argument("--dense", action="store_true",
+                    help="configs[4] density (rpt.synth.dense_config): one giant component "
+                         "crossing every rank boundary")
+    ap.add_argument("--oracle", action="store_true",
+                    help="rank 0 checks against the oracle's run_path (union-find ST-DBSCAN) "
+                         "over the whole stack instead of the single-GPU pipeline")
     ap.add_argument("--tiny-caps", action="store_true",
-                    help="native: one-element capacities for the one-collective gathers (every "
-                         "gather takes its two-round fallback)")
+                    help="native: one-pair / 16-word capacities for the pair and result gathers "
+                         "(every step is finished again with grown ones)")
     args = ap.parse_args()
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
@@ -66,7 +72,7 @@ def main():
     F = args.frames
     if args.digest:
         sys.exit(run_digest(args, rank, world, dev))
-    cfg = SynthConfig(n_frames=F, rows=args.rows, frame0=rank * F)
+    cfg = _config(args, F, rank * F)
     ds = DeviceSynth(cfg, dev)
     echo = ds.echo()
     runs = []  # (result, this rank's labels) per checked run
@@ -87,7 +93,7 @@ def main():
         pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
                           F * 3)
         if args.tiny_caps:
-            pipe._cap_pairs = pipe._cap_roots = pipe._cap_parts = 1
+            pipe._cap_pairs, pipe._cap_out = 1, 16
         res = pipe.run(echo, rank * F)
         runs.append((res, pipe.labels_local()))
     else:
@@ -170,6 +176,55 @@ def run_digest(args, rank, world, dev):
     return 0 if int(flag.item()) == 1 else 1
 
 
+def _config(args, n_frames, frame0=0):
+    from rpt.synth import SynthConfig, dense_config
+
+    if args.dense:
+        return dense_config(n_frames=n_frames, rows=args.rows, frame0=frame0)
+    return SynthConfig(n_frames=n_frames, rows=args.rows, frame0=frame0)
+
+
+_ORACLE = {}
+
+
+def check_oracle(res, labels, world, args, dev):
+    """Rank 0: the sharded run against the oracle's run_path over the whole stack (land filter,
+    union-find ST-DBSCAN, per-frame clusters, tracker): labels, per-frame cluster rows in the
+    reference order, tracked objects."""
+    import oracle
+    from oracle import path as op
+    from rpt.synth import DeviceSynth
+
+    sys.path.insert(0, str(ROOT / "tests"))
+    from _stack_check import oracle_stack
+
+    key = (args.frames * world, args.dense)
+    if key not in _ORACLE:   # once per stack (every lane's last run is checked)
+        full = _config(args, args.frames * world)
+        dsf = DeviceSynth(full, dev)
+        frames = oracle_stack(dsf.echo().cpu().numpy(), full, dsf.geo)
+        _ORACLE[key] = op.run_path(frames, dbscan=oracle.stdbscan_uf)
+    o_frames, o_labels, o_clusters, o_trk = _ORACLE[key]
+    got = torch.cat([l.cpu() for l in labels]).numpy()
+    ok = bool(np.array_equal(got, o_labels.astype(np.int64)))
+    fo, order, seg = res.frame_order_offsets, res.frame_order, res.seg
+    rows = [(f, int(seg["label"][s]), int(seg["count"][s]), seg["cx"][s], seg["cy"][s],
+             float(seg["mi"][s])) for f in range(len(fo) - 1) for s in order[fo[f]:fo[f + 1]]]
+    exp = [(fid, c[0], c[1], c[2][0], c[2][1], c[3]) for fid, _, _ in o_frames
+           for c in o_clusters.get(fid, [])]
+    rows_ok = rows == exp
+    a, b = list(o_trk.objects.values()), res.tracker.objects()
+    trk_ok = [x.object_id for x in a] == [x.object_id for x in b] and all(
+        np.array_equal(np.vstack(x.positions), np.vstack(y.positions)) and
+        x.frames_seen == y.frames_seen for x, y in zip(a, b))
+    ok &= rows_ok and trk_ok
+    print(f"[dist_check] oracle world={world} dense={args.dense} points={res.n_points_global} "
+          f"clusters={res.n_clusters} (oracle {int(o_labels.max()) + 1}) segments="
+          f"{res.n_segments} objects={len(b)} labels_equal={np.array_equal(got, o_labels)} "
+          f"rows_equal={rows_ok} tracks_equal={trk_ok} lanes={args.lanes} ok={ok}", flush=True)
+    return ok
+
+
 def check(res, labels, rank, world, args, dev):
     """Rank 0: the sharded run against the single-GPU pipeline over the whole stack."""
     from rpt.pipeline import FrameStackPipeline, PathParams
@@ -177,8 +232,10 @@ def check(res, labels, rank, world, args, dev):
 
     F = args.frames
     ok = True
+    if rank == 0 and args.oracle:
+        return check_oracle(res, labels, world, args, dev)
     if rank == 0:
-        full = SynthConfig(n_frames=F * world, rows=args.rows)
+        full = _config(args, F * world)
         dsf = DeviceSynth(full, dev)
         single = FrameStackPipeline(full.gains, full.rows, full.bins, PathParams(), dev)
         single.set_geometry(np.full(full.rows, full.scale, np.float32), dsf.geo.cos_t,

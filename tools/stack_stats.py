@@ -21,7 +21,7 @@ ds = DeviceSynth(cfg, dev)
 pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), dev)
 pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
                   cfg.n_frames * len(cfg.gains))
-res = pipe.run(ds.echo(), keep_points=True)
+res = pipe.run(ds.echo(), keep_points=True, keep_core=True)
 x = res.points["x"].cpu().numpy()
 y = res.points["y"].cpu().numpy()
 pf = res.points["frame"].cpu().numpy().astype(np.int64)

@@ -87,16 +87,65 @@ def _cluster_track(trk, frames):
             "clusters": sum(len(v) for v in cbf.values()), "objects": len(tr.objects)}
 
 
+def calibrate_refpath(trk, out_path: str, runs: int):
+    """bench.py's cpu_baseline runs oracle/refpath.py (the reference's algorithmic structure)
+    on the GPU box, where the reference cannot go: time it against the reference's own st_dbscan
+    (:443-506) here, interleaved, on the same input (frame 0 of the bench stack, 3 gains fused),
+    one thread, and write the ratio (profiles/<round>/refpath_calibration.json)."""
+    import oracle
+    from oracle.refpath import stdbscan_structure
+    from rpt.synth import SynthConfig, make_geometry, numpy_echo
+
+    cfg = SynthConfig(n_frames=1000)
+    geo = make_geometry(cfg)
+    frames = _frames(trk, numpy_echo(cfg, geo, frames=range(0, 1)), cfg, geo)
+    xy = np.vstack([f.points[:, :2] for f in frames]).astype(np.float32)
+    t = np.concatenate([np.full(f.num_points, f.frame_id, np.float32) for f in frames])
+    rec = []
+    same = True
+    for k in range(runs):
+        t0 = time.perf_counter()
+        trk.st_dbscan(frames, trk.EPS_SPACE, trk.EPS_TIME, trk.MIN_SAMPLES)
+        t1 = time.perf_counter()
+        lab, index = stdbscan_structure(xy, t, 8.0, 2.0, 15)
+        t2 = time.perf_counter()
+        rec.append({"reference": round(t1 - t0, 2), "refpath": round(t2 - t1, 2)})
+        same &= bool(np.array_equal(lab, oracle.stdbscan(xy, t, 8.0, 2.0, 15)))
+        print("calibration run", k, rec[-1], flush=True)
+    out = {"what": "oracle/refpath.py (the reference's algorithmic structure: whole-stack sklearn "
+                   "BallTree + per-neighbour float32 time filter + seed-set expansion) timed "
+                   "against the reference's own st_dbscan (PointCloudWork/"
+                   "4_temporal_object_tracker.py:443-536), interleaved, same input, one thread, "
+                   "build container",
+           "input": f"frame 0 of the bench stack (SynthConfig(n_frames=1000), 3 gains fused): "
+                    f"{len(xy):,} points, eps 8 / eps_t 2 / min 15",
+           "cpu_model": _cpu_model(), "index": index, "runs_s": rec,
+           "ratio_refpath_over_reference": [round(r["refpath"] / r["reference"], 3)
+                                            for r in rec],
+           "labels_identical_to_oracle": same,
+           "script": "tools/time_reference.py --calibrate-refpath (reference imported from "
+                     "/root/reference; it never travels to the GPU box)"}
+    Path(out_path).parent.mkdir(parents=True, exist_ok=True)
+    Path(out_path).write_text(json.dumps(out, indent=1) + "\n")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--budget-s", type=float, default=600.0)
     ap.add_argument("--max-prefix", type=int, default=6)
     ap.add_argument("--out", default=str(ROOT / "profiles" / "r2" / "reference_cpu.json"))
+    ap.add_argument("--calibrate-refpath", default=None, metavar="OUT_JSON",
+                    help="only time oracle/refpath.py against the reference's st_dbscan and "
+                         "write OUT_JSON")
+    ap.add_argument("--runs", type=int, default=2)
     args = ap.parse_args()
     if not REF.exists():
         raise SystemExit("time_reference.py must run where /root/reference exists (build container)")
     os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
     trk = _load("ref_tracker4", REF / "PointCloudWork" / "4_temporal_object_tracker.py")
+    if args.calibrate_refpath:
+        calibrate_refpath(trk, args.calibrate_refpath, args.runs)
+        return
     ref3 = _load("ref_stdbscan3", REF / "PointCloudWork" / "3_stdbscan_point_clouds.py")
     from make_golden import write_csv
     from rpt.synth import SynthConfig, make_geometry, numpy_echo
