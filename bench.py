@@ -34,7 +34,8 @@ configs[3] stack's share) and `roofline_configs4_share` (125 dense frames, confi
 stack in flight (`--no-dense-k5` skips both).
 `cpu_baseline`: oracle/refpath.py -- the reference's own algorithmic structure (whole-stack
 sklearn BallTree, per-neighbour time filter, seed-set expansion; calibrated against the
-reference in the build container, profiles/r3/refpath_calibration.json) -- on the first frame
+reference in the build container by tools/time_reference.py --calibrate-refpath,
+profiles/r4/refpath_calibration.json) -- on the first frame
 of the same stack, one thread, on this node's host.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--total-frames T | --frames F] [--dense]
@@ -518,8 +519,9 @@ def main():
                "kind": "port",
                "what": "the reference's algorithmic structure restated (oracle/refpath.py: "
                        "whole-stack sklearn BallTree query, per-neighbour float32 time filter "
-                       "in Python, seed-set expansion; calibrated to 0.93-1.03x the reference's "
-                       "own time in the build container, profiles/r3/refpath_calibration.json) "
+                       "in Python, seed-set expansion; calibrated to 1.05-1.12x the reference's "
+                       "own time in the build container by tools/time_reference.py "
+                       "--calibrate-refpath, profiles/r4/refpath_calibration.json) "
                        "+ numpy polar scatter + oracle tracker, 1 thread on this node",
                "index": index, "labels_equal_oracle": same,
                "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),

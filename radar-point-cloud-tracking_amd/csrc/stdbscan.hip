@@ -353,6 +353,29 @@ static int slab_chunks_override() {
   return v;
 }
 
+// RPT_CHUNK_SCAN=1: the one-block-per-slab k_slab_chunk_scan (A/B)
+static bool chunk_scan_legacy() {
+  static const bool v = [] {
+    const char* e = ab_env("RPT_CHUNK_SCAN");
+    return e && std::atoi(e) == 1;
+  }();
+  return v;
+}
+
+// occ_base[s] = the first occupied-list position of slab s (the flags' exclusive scan at the
+// slab's first cell), occ_base[nt] = the occupied count
+__global__ void k_slab_occ_base(const int32_t* __restrict__ pos, int P, int64_t nt,
+                                int32_t* __restrict__ occ_base) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s <= nt;
+       s += (int64_t)gridDim.x * blockDim.x)
+    occ_base[s] = pos[s * P];
+}
+
+// cell_start[cells] = n (the scan's total) -> the isolated cell (empty) ends there too
+__global__ void k_cell_start_end(int32_t* __restrict__ cell_start, int64_t cells) {
+  if (threadIdx.x == 0) cell_start[cells + 1] = cell_start[cells];
+}
+
 // slab_lo[s] = first point of slab s (points ordered by slab), slab_lo[nt] = n
 __global__ void k_slab_lo(const float* __restrict__ t, int64_t n, Geom g,
                           int32_t* __restrict__ slab_lo) {
@@ -626,6 +649,64 @@ __global__ __launch_bounds__(kBucketBlock) void k_slab_chunk_scan(
     cell_start[g.cells] = hi;
     cell_start[g.cells + 1] = hi;
   }
+}
+
+// The same outputs as k_slab_chunk_scan from fully parallel, coalesced passes over every
+// (slab, cell) -- one block per slab walking its cells in per-thread runs left most CUs idle
+// and read the [chunk][cell] histograms with a lane stride (2.2 GB per dense 125-frame share):
+//   k_chunk_totals   cell_start[key] = the cell's count over the slab's chunks
+//   (in-place exclusive scan of cell_start: the points are slab-major, so the global prefix IS
+//    every cell's first point)
+//   k_chunk_cursors  per-chunk slab-local write cursors, occupancy words (one ballot per 64
+//                    keys), occupied flags
+//   (exclusive scan of the flags) -> k_occ_write: the ascending occupied list and its count.
+__global__ void k_chunk_totals(const int32_t* __restrict__ hist_g, int64_t cells, int P, int CH,
+                               int32_t* __restrict__ cell_start) {
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < cells;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = k / P;
+    const int32_t* h = hist_g + s * (int64_t)CH * P + (k - s * P);
+    int t = 0;
+    for (int ch = 0; ch < CH; ++ch) t += h[(int64_t)ch * P];
+    cell_start[k] = t;
+  }
+}
+
+__global__ void k_chunk_cursors(int32_t* __restrict__ hist_g, int64_t cells, int P, int CH,
+                                const int32_t* __restrict__ cell_start,
+                                const int32_t* __restrict__ slab_lo,
+                                uint32_t* __restrict__ occ_bits, int32_t* __restrict__ occf) {
+  // whole waves over 64 consecutive keys (the grid stride is a multiple of 64): the wave's
+  // ballot of occupied cells is two whole occupancy words
+  const int lane = threadIdx.x & 63;
+  for (int64_t k0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~(int64_t)63; k0 < cells;
+       k0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = k0 + lane;
+    bool o = false;
+    if (k < cells) {
+      const int64_t s = k / P;
+      int32_t* h = hist_g + s * (int64_t)CH * P + (k - s * P);
+      int acc = cell_start[k] - slab_lo[s];
+      const int first = acc;
+      for (int ch = 0; ch < CH; ++ch) {
+        const int v = h[(int64_t)ch * P];
+        h[(int64_t)ch * P] = acc;
+        acc += v;
+      }
+      o = acc > first;
+      occf[k] = o ? 1 : 0;
+    }
+    const uint64_t m = __ballot(o);
+    if (lane == 0) occ_bits[k0 >> 5] = (uint32_t)m;
+    if (lane == 32) occ_bits[(k0 >> 5) + 1] = (uint32_t)(m >> 32);
+  }
+}
+
+__global__ void k_occ_write(const int32_t* __restrict__ occf, const int32_t* __restrict__ pos,
+                            int64_t cells, int32_t* __restrict__ occ) {
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < cells;
+       k += (int64_t)gridDim.x * blockDim.x)
+    if (occf[k]) occ[pos[k]] = (int32_t)k;
 }
 
 __global__ __launch_bounds__(kBucketBlock) void k_slab_chunk_scatter(
@@ -4083,8 +4164,28 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)hist_bytes));
       hipLaunchKernelGGL(k_slab_chunk_hist, dim3((unsigned)(nt * CH)), dim3(kBucketBlock),
                          hist_bytes, st, x, y, stride, g, slab_lo, CH, hist_g);
-      hipLaunchKernelGGL(k_slab_chunk_scan, dim3((unsigned)nt), dim3(kBucketBlock), 0, st, g,
-                         slab_lo, CH, hist_g, cell_start, hpos, slab_occ, occ_bits);
+      if (chunk_scan_legacy()) {
+        hipLaunchKernelGGL(k_slab_chunk_scan, dim3((unsigned)nt), dim3(kBucketBlock), 0, st, g,
+                           slab_lo, CH, hist_g, cell_start, hpos, slab_occ, occ_bits);
+      } else {
+        // cell_start, cursors, occupancy from coalesced passes; the flags and their positions in
+        // cell_min / cell_root (C1 words each, first written after the grid build)
+        const int64_t cells = (int64_t)nt * nx * ny;
+        const int P = (int)(nx * ny);
+        const int gc = grid_for(cells, kBlock, 8192);
+        hipLaunchKernelGGL(k_chunk_totals, dim3(gc), dim3(kBlock), 0, st, hist_g, cells, P, CH,
+                           cell_start);
+        RPT_TRY(exclusive_scan_total_i32(cell_start, cell_start, cells, st));
+        hipLaunchKernelGGL(k_chunk_cursors, dim3(gc), dim3(kBlock), 0, st, hist_g, cells, P, CH,
+                           cell_start, slab_lo, occ_bits, cell_min);
+        RPT_TRY(exclusive_scan_total_i32(cell_min, cell_root, cells, st));
+        hipLaunchKernelGGL(k_occ_write, dim3(gc), dim3(kBlock), 0, st, cell_min, cell_root,
+                           cells, occ);
+        hipLaunchKernelGGL(k_cell_start_end, dim3(1), dim3(64), 0, st, cell_start, cells);
+        hipLaunchKernelGGL(k_slab_occ_base, dim3(grid_for(nt + 1, kBlock, 1024)), dim3(kBlock), 0,
+                           st, cell_root, P, nt, occ_base);
+        RPT_CHECK_LAUNCH();
+      }
       hipLaunchKernelGGL(k_slab_chunk_scatter, dim3((unsigned)(nt * CH)), dim3(kBucketBlock),
                          hist_bytes, st, x, y, stride, t, g, slab_lo, CH, hist_g, pts, sorig,
                          skey);
@@ -4096,11 +4197,15 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
                          slab_occ, occ_bits);
     }
     RPT_CHECK_LAUNCH();
-    RPT_TRY(exclusive_scan_total_i32(slab_occ, occ_base, nt, st));
-    hipLaunchKernelGGL(k_occ_gather, dim3((unsigned)nt), dim3(kBlock), 0, st, hpos, slab_lo,
-                       occ_base, occ);
-    RPT_CHECK_LAUNCH();
-    n_occ_dev = occ_base + nt;
+    if (CH > 1 && (int64_t)nt * CH * nx * ny <= 4 * n && !chunk_scan_legacy()) {
+      n_occ_dev = occ_base + nt;  // the occupied list is written already
+    } else {
+      RPT_TRY(exclusive_scan_total_i32(slab_occ, occ_base, nt, st));
+      hipLaunchKernelGGL(k_occ_gather, dim3((unsigned)nt), dim3(kBlock), 0, st, hpos, slab_lo,
+                         occ_base, occ);
+      RPT_CHECK_LAUNCH();
+      n_occ_dev = occ_base + nt;
+    }
   } else {
     hipLaunchKernelGGL(k_keys<D>, dim3(gb), dim3(kBlock), 0, st, x, y, z, stride, t, n, g, keys,
                        vals);
