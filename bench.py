@@ -25,9 +25,11 @@ step k+1's device work runs while step k's host stage and readbacks finish, and 
 latency-bound kernels share the CUs; 3 measured +4-5 % over 2 in interleaved same-box runs, 4
 no better); `one_stack_in_flight` repeats the steps strictly one after
 another, and K5's roofline is taken from that leg (K5 alone on the GPU).
-At N>1 (the frame-sharded path) two stacks are in flight per rank by default: their collectives
-go through ONE communicator in a fixed global order (rpt.dist.CommSequencer); at one rank on a
-125-frame share, 2 lanes measured 2.33 ms per step against 2.62 (1 lane) and 2.53 (3 lanes).
+At N>1 (the frame-sharded path) three stacks are in flight per rank by default: their
+collectives go through ONE communicator in a fixed software-pipeline order
+(rpt.dist.CommSequencer); at one rank on the 125-frame share (the 8-GPU per-rank share) the shard
+driver v2 measured 1.48 ms per step with 3 lanes (1.62 ms with the sequencer's order kept,
+--sequenced) against 2.12 ms with 1 (profiles/r4/bench_sharded1rank_125f_*.json).
 After the timed region (N=1, timing on), K5 is also timed on the per-GPU shares at 8 GPUs, where
 SURVEY.md §8(d) sets the 0.40 roofline target: `roofline_c4_share` (125 standard frames, the
 configs[3] stack's share) and `roofline_configs4_share` (125 dense frames, configs[4]'s), one
@@ -211,7 +213,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if args.lanes is None:
-        args.lanes = 3 if world == 1 and not args.sharded else 2
+        args.lanes = 3
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # --sharded: the frame-sharded multi-GPU path even at one rank (measures its per-rank cost)
     dist = world > 1 or args.sharded

@@ -2963,9 +2963,17 @@ __global__ __launch_bounds__(kBlock) void k_label_core(const int32_t* __restrict
                                                       MinRank cid,
                                                       int32_t* __restrict__ labels) {
   // kPU points per thread per tile, loads branch-free (clamped, masked): two memory rounds per
-  // tile (ccmin + sorig, then the rank words) instead of two per point
-  for (int64_t tile = (int64_t)blockIdx.x * kBlock * kPU; tile < n;
-       tile += (int64_t)gridDim.x * kBlock * kPU) {
+  // tile (ccmin + sorig, then the rank words) instead of two per point.  XCD-contiguous tiles
+  // (grid a multiple of 8): the blocks of one XCD take one eighth of the sorted points, i.e. a
+  // run of whole frames, so the labels they scatter (original order, within those frames) fill
+  // their lines in that XCD's L2 instead of eight L2s writing partial lines of the same frames
+  const int64_t T = (n + (int64_t)kBlock * kPU - 1) / ((int64_t)kBlock * kPU);
+  const bool xm = (gridDim.x & 7) == 0;
+  const int64_t xg = blockIdx.x & 7, nbx = gridDim.x >> 3;
+  const int64_t t_lo = xm ? T * xg / 8 : blockIdx.x, t_hi = xm ? T * (xg + 1) / 8 : T;
+  const int64_t t_step = xm ? nbx : gridDim.x;
+  for (int64_t ti = t_lo + (xm ? (int64_t)(blockIdx.x >> 3) : 0); ti < t_hi; ti += t_step) {
+    const int64_t tile = ti * kBlock * kPU;
     int32_t own[kPU], so[kPU];
 #pragma unroll
     for (int u = 0; u < kPU; ++u) {
@@ -4156,15 +4164,20 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
     int CH = (int)std::min<int64_t>(ch, 64);
     while (CH > 1 && (int64_t)nt * CH * nx * ny > 4 * n) --CH;
     if (slab_chunks_override() > 0) CH = slab_chunks_override();
+    const bool coalesced_scan = CH >= 8 && (int64_t)nt * CH * nx * ny <= 4 * n &&
+                                !chunk_scan_legacy();
     if (CH > 1 && (int64_t)nt * CH * nx * ny <= 4 * n) {
       int32_t* hist_g = reinterpret_cast<int32_t*>(keys);
+      // the coalesced passes pay for their extra launches only with many chunks per slab (dense
+      // slabs: configs[4] share 357 -> 115 us); a few chunks per slab (short standard stacks,
+      // split to fill the GPU) keep the one-block-per-slab scan (125 frames: 38 vs 53 us)
       RPT_HIP(hipFuncSetAttribute((const void*)k_slab_chunk_hist,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)hist_bytes));
       RPT_HIP(hipFuncSetAttribute((const void*)k_slab_chunk_scatter,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)hist_bytes));
       hipLaunchKernelGGL(k_slab_chunk_hist, dim3((unsigned)(nt * CH)), dim3(kBucketBlock),
                          hist_bytes, st, x, y, stride, g, slab_lo, CH, hist_g);
-      if (chunk_scan_legacy()) {
+      if (!coalesced_scan) {
         hipLaunchKernelGGL(k_slab_chunk_scan, dim3((unsigned)nt), dim3(kBucketBlock), 0, st, g,
                            slab_lo, CH, hist_g, cell_start, hpos, slab_occ, occ_bits);
       } else {
@@ -4197,7 +4210,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
                          slab_occ, occ_bits);
     }
     RPT_CHECK_LAUNCH();
-    if (CH > 1 && (int64_t)nt * CH * nx * ny <= 4 * n && !chunk_scan_legacy()) {
+    if (coalesced_scan) {
       n_occ_dev = occ_base + nt;  // the occupied list is written already
     } else {
       RPT_TRY(exclusive_scan_total_i32(slab_occ, occ_base, nt, st));
@@ -4486,7 +4499,7 @@ int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hi
   hipLaunchKernelGGL(k_fill_i32, dim3(gc), dim3(kBlock), 0, st, cell_min, C, INT_MAX);
   RPT_TRY(cluster_ids(st, cell_min));  // also the per-cell smallest keys (k_cell_min_key fused)
   const MinRank mr{min_bits, min_pref};
-  hipLaunchKernelGGL(k_label_core, dim3(grid_for(n, kBlock * kPU, 2048)), dim3(kBlock), 0, st,
+  hipLaunchKernelGGL(k_label_core, dim3((grid_for(n, kBlock * kPU, 2048) + 7) & ~7), dim3(kBlock), 0, st,
                      ccmin, n, sorig, mr, labels);
   if (use_label_tiles())
     hipLaunchKernelGGL((k_label_tiles<false>), dim3(tile_grid_blocks()), dim3(kTileBlock), 0, st,
@@ -4631,7 +4644,7 @@ int32_t DbscanState::labels_fifo(int32_t* labels, rpt_stdbscan_stats* stats, hip
   hipLaunchKernelGGL(k_inverse_perm, dim3(gb), dim3(kBlock), 0, st, sorig, n, spos);
   RPT_CHECK_LAUNCH();
   const MinRank mr{min_bits, min_pref};
-  hipLaunchKernelGGL(k_label_core, dim3(grid_for(n, kBlock * kPU, 2048)), dim3(kBlock), 0, st,
+  hipLaunchKernelGGL(k_label_core, dim3((grid_for(n, kBlock * kPU, 2048) + 7) & ~7), dim3(kBlock), 0, st,
                      ccmin, n, sorig, mr, labels);
   if (dim == 2)
     hipLaunchKernelGGL((k_label_fifo<2>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
