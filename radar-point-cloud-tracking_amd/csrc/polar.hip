@@ -343,13 +343,29 @@ __device__ __forceinline__ uint32_t kept_entry(const GroupLds& L,
 // read of the echo for the whole K1).  A group that keeps more (dense sweeps) is read from the
 // echo again by the write pass.
 constexpr int kStageSlots = 256;
+// Slot position of in-group kept rank i in a staged group of `total` entries.  With stride 4 (the
+// reference's POINT_STRIDE) the ranks of each residue mod 4 are contiguous and the four residues
+// packed back to back in [0, total): the write pass reads every 4th rank from one residue, i.e.
+// consecutive entries, instead of one entry in four from every line of the slot, while the count
+// pass still fills one contiguous region per group (a fixed 64-entry stride per residue left four
+// partly written lines per sparse group: +9 % on the count pass).
+__device__ __forceinline__ uint32_t phase_base(uint32_t ph, uint32_t total) {
+  uint32_t b = 0u;
+#pragma unroll
+  for (uint32_t j = 0u; j < 3u; ++j) b += (j < ph) ? ((total + 3u - j) >> 2) : 0u;
+  return b;
+}
+__device__ __forceinline__ uint32_t stage_pos(uint32_t i, uint32_t total, bool ph4) {
+  return ph4 ? phase_base(i & 3u, total) + (i >> 2) : i;
+}
 
 template <bool HI, bool STAGE>
 __global__ __launch_bounds__(kBlock) void k_group_count_u8(const uint8_t* __restrict__ echo,
                                                           uint32_t n_groups, GroupMap gm,
                                                           uint32_t K,
                                                           int32_t* __restrict__ group_count,
-                                                          uint32_t* __restrict__ entries) {
+                                                          uint32_t* __restrict__ entries,
+                                                          int ph4) {
   const int lane = threadIdx.x & 63;
   const uint32_t wave0 = blockIdx.x * kWavesPerBlock + threadIdx.x / 64;
   const uint32_t n_waves = gridDim.x * kWavesPerBlock;
@@ -390,7 +406,8 @@ __global__ __launch_bounds__(kBlock) void k_group_count_u8(const uint8_t* __rest
         __shared__ GroupLds s_lds[kWavesPerBlock];
         GroupLds& L = s_lds[threadIdx.x / 64];
         group_to_lds(L, lane, m, incl, v);
-        for (uint32_t i = (uint32_t)lane; i < total; i += 64u) e[i] = kept_entry(L, rb, i);
+        for (uint32_t i = (uint32_t)lane; i < total; i += 64u)
+          e[stage_pos(i, total, ph4 != 0)] = kept_entry(L, rb, i);
         wave_lds_sync();  // the slice is rewritten by the next group
       }
       if (lane == 0) group_count[grp] = (int32_t)total;
@@ -509,7 +526,7 @@ __global__ __launch_bounds__(kBlock) void k_group_write_u8(
       const int64_t oo = out0 + o;
       if (oo >= cap) break;
       const uint32_t i = o * us - rank;  // in-group kept rank
-      const uint32_t ent = staged ? e[i] : kept_entry(L, rb, i);
+      const uint32_t ent = staged ? e[stage_pos(i, total, us == 4u)] : kept_entry(L, rb, i);
       const int rk = (int)(ent >> 18);
       const float sc = rk == 0 ? r_sc[0] : (rk == 1 ? r_sc[1] : (rk == 2 ? r_sc[2] : r_sc[3]));
       const float cc = rk == 0 ? r_c[0] : (rk == 1 ? r_c[1] : (rk == 2 ? r_c[2] : r_c[3]));
@@ -565,7 +582,11 @@ __global__ __launch_bounds__(kBlock) void k_group_starts(const int64_t* __restri
       const uint64_t first = (rank + stride - 1u) / stride;
       const uint64_t last = (rank + total + stride - 1u) / stride;
       const uint64_t gs = (uint64_t)file_offsets[f] + first;
-      const uint64_t phase = first * stride - rank;
+      // slot position of the first emitted output's entry: its in-group rank, or with stride 4
+      // (residues packed, stage_pos) the base of its residue
+      const uint64_t ph = first * stride - rank;
+      const uint64_t phase = stride == 4u ? (uint64_t)phase_base((uint32_t)ph, (uint32_t)total)
+                                          : ph;
       un = last > first && total > (uint64_t)kStageSlots;
       gword[g] = gs | (phase << kGsBits) | (un ? kUnstaged : 0ull);
       if (un) slot = atomicAdd(&s_n, 1u);
@@ -688,8 +709,10 @@ __global__ __launch_bounds__(kBlock) void k_expand_write(
         }
         ok[k] = in && !(w & kUnstaged);
         grp[k] = g;
-        // mod 2^32 like the 64-bit form (only staged groups use it: idx < kStageSlots)
-        idx[k] = ((uint32_t)O - (uint32_t)w) * stride + (uint32_t)((w & ~kUnstaged) >> kGsBits);
+        // the entry's slot position, mod 2^32 like the 64-bit form (only staged groups use it:
+        // idx < kStageSlots): consecutive outputs are consecutive entries with stride 4
+        const uint32_t d = (uint32_t)O - (uint32_t)w;
+        idx[k] = (stride == 4u ? d : d * stride) + (uint32_t)((w & ~kUnstaged) >> kGsBits);
       }
     } else {
 #pragma unroll
@@ -848,7 +871,7 @@ int32_t count_impl(const T* echo, int64_t n_files, int rows, int bins, float thr
     const auto* e8 = reinterpret_cast<const uint8_t*>(echo);
 #define RPT_K1C(HI, S)                                                                    \
   hipLaunchKernelGGL((k_group_count_u8<HI, S>), dim3(grid), dim3(kBlock), 0, st, e8,        \
-                     (uint32_t)n_units, gm, u8_k(T8), rc, entries)
+                     (uint32_t)n_units, gm, u8_k(T8), rc, entries, stride == 4 ? 1 : 0)
     if (entries) {
       if (T8 <= 127)
         RPT_K1C(false, true);

@@ -158,10 +158,6 @@ __device__ __forceinline__ float seq_sum(const float* __restrict__ gx,
   };
   float* __restrict__ sb = sbuf + (lane & 1) * kChunk;  // this lane's chain: x or y
   float acc = 0.f;
-  // the chain is one dependent add per element: the SIMD's VALU issue goes to this wave first
-  // (other waves on the SIMD -- the run's intensity wave, other kernels' waves -- would otherwise
-  // take issue slots from the critical path; MI355X_MICROARCH.md: priority, then age)
-  __builtin_amdgcn_s_setprio(3);
   load_chunk(b);
   for (int c0 = b; c0 < e; c0 += kChunk) {
 #pragma unroll
@@ -265,7 +261,6 @@ __device__ __forceinline__ float seq_sum(const float* __restrict__ gx,
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  __builtin_amdgcn_s_setprio(0);
   return acc;
 }
 

@@ -13,6 +13,7 @@ if [ -z "$NOTESTS" ]; then
 fi
 for W in ${WL:-dense std}; do
   A=(--lanes 1 --total-frames 125); [ $W = dense ] && A+=(--dense)
+  [ $W = std1000 ] && A=(--lanes 1 --total-frames 1000)
   bash tools/kprof.sh ${W}_new "${A[@]}" || exit 1
   RPT_LIB="$PWD/abl/librpt_base.so" bash tools/kprof.sh ${W}_base "${A[@]}" || exit 1
   for t in new base; do
