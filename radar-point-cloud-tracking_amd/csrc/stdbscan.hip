@@ -845,7 +845,10 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ 
                                                     uint8_t* __restrict__ mutual,
                                                     CellRec<D>* __restrict__ crec,
                                                     unsigned long long* __restrict__ cmin =
-                                                        nullptr) {
+                                                        nullptr,
+                                                    const int32_t* __restrict__ sorig = nullptr) {
+  // sorig (kernel-uniform): cmin[c] = the (min original, sorted) pair over ALL the cell's points
+  // (the fused K5 keeps it for all-core cells), read alongside the points; otherwise none (~0)
   const int j = threadIdx.x & 7;
   const int64_t no = *n_occ;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t - j < no * 8;
@@ -860,15 +863,19 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ 
     }
     float x0 = FLT_MAX, x1 = -FLT_MAX, y0 = FLT_MAX, y1 = -FLT_MAX;
     float z0 = FLT_MAX, z1 = -FLT_MAX, t0 = FLT_MAX, t1 = -FLT_MAX;
+    uint64_t mn = ~0ull;
     // 8 loads in flight per lane: a dense cell (hundreds of points) is otherwise a chain of
     // dependent load round trips on its 8 lanes
     constexpr int kU = 8;
     for (int s0 = b + j; s0 < e; s0 += 8 * kU) {
       float4 pp[kU];
+      uint32_t so[kU];
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const int s2 = s0 + 8 * u;
-        pp[u] = (s2 < e) ? pts[s2] : pts[s0];  // duplicates of a cell point leave the box as is
+        const int sc = (s2 < e) ? s2 : s0;  // duplicates of a cell point leave the box as is
+        pp[u] = pts[sc];
+        if (sorig) so[u] = (uint32_t)sorig[sc];
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
@@ -877,6 +884,20 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ 
         y0 = fminf(y0, p.y); y1 = fmaxf(y1, p.y);
         z0 = fminf(z0, p.z); z1 = fmaxf(z1, p.z);
         t0 = fminf(t0, p.w); t1 = fmaxf(t1, p.w);
+        if (sorig) {
+          const int s2 = s0 + 8 * u;
+          const uint64_t v = ((uint64_t)so[u] << 32) | (uint32_t)((s2 < e) ? s2 : s0);
+          mn = v < mn ? v : mn;
+        }
+      }
+    }
+    if (sorig) {
+#pragma unroll
+      for (int off = 4; off > 0; off >>= 1) {
+        const uint32_t olo = (uint32_t)__shfl_xor((int)(uint32_t)mn, off, 8);
+        const uint32_t ohi = (uint32_t)__shfl_xor((int)(uint32_t)(mn >> 32), off, 8);
+        const uint64_t o = ((uint64_t)ohi << 32) | olo;
+        mn = o < mn ? o : mn;
       }
     }
 #pragma unroll
@@ -916,7 +937,7 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ 
       }
       const float dt = t1 - t0;
       mutual[c] = (d2 <= g.eps2 && dt <= g.epst) ? 1 : 0;
-      if (cmin) cmin[c] = ~0ull;  // the core pass's per-cell minima (k_core_fill, k_core_slow)
+      if (cmin) cmin[c] = sorig ? mn : ~0ull;  // the core pass's per-cell minima
     }
   }
 }
@@ -1411,6 +1432,74 @@ __device__ __forceinline__ void write_cell_flags(uint8_t* __restrict__ core, int
   for (int s = we + j; s < e; s += lanes) core[s] = v;
 }
 
+// The FUSED epilogue of k_core_cells_oct (whole wave, wave-uniform control): lanes 8k hold cell k
+// of the wave (act, key, point range [b, e), flag 0 / 1 / 2).  The cells' (min original, sorted)
+// pairs over ALL their points come from k_cell_box (allmin): an all-core cell keeps it, every other
+// cell is reset to none here (the undecided cells' core points are folded in by k_core_slow).
+// The queued points go to the block's LDS queue (an LDS atomic per wave; one global atomic per
+// BLOCK when the block flushes it at its end -- a global same-address atomic per wave serialised
+// ~100 k of them at 1000 frames: +0.8 ms); a wave whose points no longer fit reserves globally.
+constexpr int kCwQueue = 2048;
+struct CwQueue {
+  int32_t item[kCwQueue];
+  int n;      // reserved (may pass kCwQueue)
+  int fail;   // first reservation that did not fit
+  int base;
+};
+__device__ __forceinline__ void cells_fill_epilogue(const Geom& g, bool act, int32_t ca, int b,
+                                                    int e, int flag, uint8_t* __restrict__ core,
+                                                    unsigned long long* __restrict__ cmin,
+                                                    int32_t* __restrict__ slow,
+                                                    int32_t* __restrict__ n_slow, CwQueue& lq) {
+  const int lane = threadIdx.x & 63;
+  if (act && (lane & 7) == 0 && flag != 1 && (int64_t)ca < g.cells) cmin[ca] = ~0ull;
+  // active cells are a prefix of the eight (occupied-list positions below the range end)
+  const int na = __popcll(__ballot(act && (lane & 7) == 0));
+  if (na == 0) return;
+  int gb[8], gf[8];
+  int E = 0, nu = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    gb[k] = __builtin_amdgcn_readlane(b, 8 * k);
+    const int ek = __builtin_amdgcn_readlane(e, 8 * k);
+    gf[k] = __builtin_amdgcn_readlane(flag, 8 * k);
+    if (k < na) {
+      E = ek;
+      nu += (gf[k] == 2) ? ek - gb[k] : 0;
+    }
+  }
+  const int B = gb[0];
+  int ub = 0;
+  int32_t* qdst = lq.item;
+  if (nu > 0) {  // the undecided cells' points: one queue reservation per wave
+    if (lane == 0) {
+      ub = atomicAdd(&lq.n, nu);
+      if (ub + nu > kCwQueue) {
+        atomicMin(&lq.fail, ub);
+        ub = -1 - atomicAdd(n_slow, nu);
+      }
+    }
+    ub = __shfl(ub, 0);
+    if (ub < 0) {
+      qdst = slow;
+      ub = -1 - ub;
+    }
+  }
+  const uint64_t below = (1ull << lane) - 1ull;
+  for (int s0 = B; s0 < E; s0 += 64) {
+    const int s = s0 + lane;
+    const bool in = s < E;
+    int fl = gf[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) fl = (k < na && s >= gb[k]) ? gf[k] : fl;
+    const bool u = in && fl == 2;
+    const uint64_t um = nu > 0 ? __ballot(u) : 0ull;
+    if (u) qdst[ub + __popcll(um & below)] = s;
+    ub += __popcll(um);
+    if (in) core[s] = (fl == 1) ? 1 : 0;
+  }
+}
+
 // 2-D grids whose slab window is at most 7 slabs (R <= 3): K5 levels 1-3 in one kernel, EIGHT
 // lanes per occupied cell.  A mutual cell with >= min_samples points is all core (the bulk);
 // otherwise lane j < 2R+1 owns slab cs - R + j of the cell's window.  The window comes from the
@@ -1419,9 +1508,18 @@ __device__ __forceinline__ void write_cell_flags(uint8_t* __restrict__ core, int
 // with the cell's record, then the records of its (few) occupied candidates; eight cells per wave
 // keep many short dependency chains in flight.  cflag as k_core_cell_fast / _window (level 3
 // turns it into point flags).
+//
+// FUSED (the default pipeline): the level-3 fill folded in.  A wave's eight cells are consecutive
+// occupied cells, so their points are ONE contiguous range of the sorted order (the cells between
+// consecutive occupied keys are empty); after the decisions the whole wave walks that range 64
+// points at a time: the point flags (byte stores, 64 consecutive bytes per instruction) and the
+// undecided cells' points appended to the level-4 queue (one atomic per wave).  The all-core
+// cells' (min original, sorted) pairs are k_cell_box's (allmin).  No per-point loads at all.
 constexpr int kCwMaxR = 3;
 constexpr int kCwBatch = 5;  // candidate records per lane in flight together (k_core_cells_oct)
-__global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
+template <bool FUSED = false>
+// 5 waves/SIMD (<= 96 VGPRs; the fused epilogue and its LDS queue would take 99: 4 waves)
+__global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
                                                           const int32_t* __restrict__ occ,
                                                           const int32_t* __restrict__ n_occ,
                                                           const CellRec<2>* __restrict__ crec,
@@ -1430,10 +1528,22 @@ __global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
                                                           const float2* __restrict__ slab_t,
                                                           int32_t* __restrict__ cflag,
                                                           int32_t* __restrict__ zero_counter,
-                                                          uint8_t* __restrict__ core) {
+                                                          uint8_t* __restrict__ core,
+                                                          unsigned long long* __restrict__ cmin =
+                                                              nullptr,
+                                                          int32_t* __restrict__ slow = nullptr,
+                                                          int32_t* __restrict__ n_slow = nullptr) {
   // legacy pipeline: the level-4 queue counter, zeroed here instead of by a memset launch
   // (k_core_fill, the next kernel on the stream, is its first user)
-  if (zero_counter && blockIdx.x == 0 && threadIdx.x == 0) *zero_counter = 0;
+  if (!FUSED && zero_counter && blockIdx.x == 0 && threadIdx.x == 0) *zero_counter = 0;
+  __shared__ CwQueue lq;
+  if (FUSED) {
+    if (threadIdx.x == 0) {
+      lq.n = 0;
+      lq.fail = kCwQueue;
+    }
+    __syncthreads();
+  }
   const int64_t no = *n_occ;
   const int need = g.min_samples;
   const int j = threadIdx.x & 7;
@@ -1562,9 +1672,20 @@ __global__ __launch_bounds__(kBlock) void k_core_cells_oct(Geom g, int R,
         }
       }
     }
-    if (act && j == 0) cflag[ca] = flag;
-    // decided cells write their points' flags here (the undecided ones are k_core_slow_cells')
-    if (core && act && flag != 2) write_cell_flags(core, b, e, j, 8, (uint8_t)flag);
+    if constexpr (!FUSED) {
+      if (act && j == 0) cflag[ca] = flag;
+      // decided cells write their points' flags here (the undecided ones are k_core_slow_cells')
+      if (core && act && flag != 2) write_cell_flags(core, b, e, j, 8, (uint8_t)flag);
+    } else {
+      cells_fill_epilogue(g, act, ca, b, e, flag, core, cmin, slow, n_slow, lq);
+    }
+  }
+  if constexpr (FUSED) {  // flush the block's queue (the cell loop is block-uniform)
+    __syncthreads();
+    const int m = min(lq.n, lq.fail);
+    if (threadIdx.x == 0) lq.base = m > 0 ? atomicAdd(n_slow, m) : 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < m; i += blockDim.x) slow[lq.base + i] = lq.item[i];
   }
 }
 
@@ -3893,6 +4014,34 @@ struct DbscanState {
   int uf_flags = -1;                         // see XcdRange; -1 = read RPT_UF_FLAGS once
   int k5_legacy = -1;                        // 1: round-1 K5 (fill + point queue); RPT_K5_MODE
   int k5_fill = 0;
+  int k5_fused = -1;                         // 0: separate level-3 fill pass; RPT_K5_FUSED
+  void k5_env() {
+    if (k5_legacy < 0) {  // RPT_K5_MODE: 0 round-1 queue pipeline, 1 cells write point flags,
+                          // 2 cells + point-flag fill (no queue); both 1/2 end in k_core_slow_cells
+      // default 0: the folded variants measured no faster on the 100- and 1000-frame stacks
+      // (profiles/r2/ab_k5_k1.md): the per-point flag writes moved into the cell kernel by 8 lanes
+      // per cell cost what the fill pass cost, and the cell-wise slow pass balances worse than the
+      // point queue
+      const char* e = ab_env("RPT_K5_MODE");
+      k5_legacy = e ? std::atoi(e) : 0;
+      k5_legacy = (k5_legacy == 0) ? 1 : 0;
+      k5_fill = (e && std::atoi(e) == 2) ? 1 : 0;
+    }
+    if (k5_tiles < 0) {  // RPT_K5_TILES=1: the LDS-tile pass (k_core_tiles; measured slower)
+      const char* e = ab_env("RPT_K5_TILES");
+      k5_tiles = (e && std::atoi(e) == 1) ? 1 : 0;
+    }
+    if (k5_fused < 0) {  // RPT_K5_FUSED=0: the separate level-3 fill pass (A/B)
+      const char* e = ab_env("RPT_K5_FUSED");
+      k5_fused = (e && std::atoi(e) == 0) ? 0 : 1;
+    }
+  }
+  // the default K5 pipeline: the cell pass writes the point flags and the queue itself, with the
+  // all-core cells' minima from k_cell_box (decided at build time, before k_cell_box runs)
+  bool k5_fused_path() {
+    k5_env();
+    return oct_ok() && k5_legacy && k5_fused && !k5_tiles;
+  }
   int k5_tiles = -1;                         // 1: K5 by LDS tiles (k_core_tiles); RPT_K5_TILES
   int k7_tiles = -1;                         // 1: K7 by LDS tiles (k_label_tiles); RPT_K7_TILES
   int32_t* rowq = nullptr;    // first occupied-list index of every (slab, row) + total (tiles)
@@ -4241,7 +4390,8 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   }
   hipLaunchKernelGGL(k_cell_box<D>, dim3(grid_for(8 * n, kBlock, 8192)), dim3(kBlock), 0, st,
                      pts, cell_start, occ, n_occ_dev, g, boxA, boxB, mutual, cr,
-                     reinterpret_cast<unsigned long long*>(cell_min_pair));
+                     reinterpret_cast<unsigned long long*>(cell_min_pair),
+                     k5_fused_path() ? (const int32_t*)sorig : nullptr);
   RPT_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_slab_range<D>, dim3((unsigned)nt), dim3(kBlock), 0, st, cr, occ, hpos,
                      cell_start, (int64_t)(C / nt), (int)nt, slab_t, bucket ? occ_base : nullptr);
@@ -4274,22 +4424,9 @@ int32_t DbscanState::core_pass(hipStream_t st) {
   int32_t* slow = nc_list;
   int32_t* n_slow = nc_list + n;
   const int32_t* n_occ = n_occ_dev;
-  if (k5_legacy < 0) {  // RPT_K5_MODE: 0 round-1 queue pipeline, 1 cells write point flags,
-                        // 2 cells + point-flag fill (no queue); both 1/2 end in k_core_slow_cells
-    // default 0: the folded variants measured no faster on the 100- and 1000-frame stacks
-    // (profiles/r2/ab_k5_k1.md): the per-point flag writes moved into the cell kernel cost what
-    // the fill pass cost, and the cell-wise slow pass balances worse than the point queue
-    const char* e = ab_env("RPT_K5_MODE");
-    k5_legacy = e ? std::atoi(e) : 0;
-    k5_legacy = (k5_legacy == 0) ? 1 : 0;
-    k5_fill = (e && std::atoi(e) == 2) ? 1 : 0;
-  }
+  k5_env();
   const double rs = slab_reach();
   const bool oct = oct_ok();
-  if (k5_tiles < 0) {  // RPT_K5_TILES=1: the LDS-tile pass (k_core_tiles; measured slower)
-    const char* e = ab_env("RPT_K5_TILES");
-    k5_tiles = (e && std::atoi(e) == 1) ? 1 : 0;
-  }
   if (oct && k5_tiles) {
     // LDS tiles: band height BY with the map (W slabs x BY + 4 rows x nx) and the undecided list
     // (BY x nx own cells) within their LDS arrays; rowq (kept for the label pass's tiles)
@@ -4319,7 +4456,7 @@ int32_t DbscanState::core_pass(hipStream_t st) {
     // cells decide (and write their points' flags) in one pass; the undecided cells' points are
     // settled by k_core_slow_cells, which walks the occupied cells itself (no queue, no fill)
     if (oct) {
-      hipLaunchKernelGGL(k_core_cells_oct, dim3((grid_for(8 * n, kBlock, 8192) + 7) & ~7), dim3(kBlock), 0,
+      hipLaunchKernelGGL(k_core_cells_oct<false>, dim3((grid_for(8 * n, kBlock, 8192) + 7) & ~7), dim3(kBlock), 0,
                          st, g, (int)rs, occ, n_occ, rec<2>(), mutual, occ_bits, slab_t, cflag,
                          (int32_t*)nullptr, k5_fill ? (uint8_t*)nullptr : core);
       if (k5_fill)
@@ -4351,8 +4488,20 @@ int32_t DbscanState::core_pass(hipStream_t st) {
   }
   // oct: the union's per-cell minima (cell_min_pair) come out of the fill and slow passes
   auto* cm = oct ? reinterpret_cast<unsigned long long*>(cell_min_pair) : nullptr;
+  if (k5_fused_path()) {
+    RPT_HIP(hipMemsetAsync(n_slow, 0, sizeof(int32_t), st));
+    hipLaunchKernelGGL(k_core_cells_oct<true>, dim3((grid_for(8 * n, kBlock, 8192) + 7) & ~7),
+                       dim3(kBlock), 0, st, g, (int)rs, occ, n_occ, rec<2>(), mutual, occ_bits,
+                       slab_t, (int32_t*)nullptr, (int32_t*)nullptr, core, cm, slow, n_slow);
+    hipLaunchKernelGGL(k_core_slow<2>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
+                       rec<2>(), occ_bits, slab_t, slow, n_slow, core, sorig, cm);
+    RPT_CHECK_LAUNCH();
+    cmin_ready = true;
+    tm.mark();
+    return RPT_OK;
+  }
   if (oct) {
-    hipLaunchKernelGGL(k_core_cells_oct, dim3((grid_for(8 * n, kBlock, 8192) + 7) & ~7), dim3(kBlock), 0,
+    hipLaunchKernelGGL(k_core_cells_oct<false>, dim3((grid_for(8 * n, kBlock, 8192) + 7) & ~7), dim3(kBlock), 0,
                        st, g, (int)rs, occ, n_occ, rec<2>(), mutual, occ_bits, slab_t, cflag,
                        n_slow, (uint8_t*)nullptr);
   } else {
