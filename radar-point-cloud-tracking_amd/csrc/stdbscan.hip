@@ -394,15 +394,23 @@ __global__ __launch_bounds__(kBucketBlock) void k_slab_bucket(
     const float* __restrict__ t, Geom g, const int32_t* __restrict__ slab_lo,
     float4* __restrict__ pts, int32_t* __restrict__ sorig, int32_t* __restrict__ skey,
     int32_t* __restrict__ cell_start, int32_t* __restrict__ occ_tmp,
-    int32_t* __restrict__ slab_occ, uint32_t* __restrict__ occ_bits) {
+    int32_t* __restrict__ slab_occ, uint32_t* __restrict__ occ_bits,
+    unsigned long long* __restrict__ cmin_all = nullptr) {
   // the slab's nx * ny cell counts, sized at launch (a 463-m sweep at cells of 5.6 m: 27 KiB, so
   // several slabs share a CU instead of one 64-KiB histogram each)
+  // cmin_all (nullable; the fused K5): every occupied cell's (min original, sorted) pair over all
+  // its points -- the smallest index per cell by an LDS atomicMin per run in the count pass (a
+  // run's head lane holds its smallest index), written by that point at its scatter
   extern __shared__ int32_t hist[];
   __shared__ int32_t wsum[kBucketBlock / 64], wocc[kBucketBlock / 64];
   const int s = blockIdx.x;
   const int P = g.nx * g.ny;
+  int32_t* mn = hist + P;  // (cmin_all only: the launch sizes 2P words)
   const int lo = slab_lo[s], hi = slab_lo[s + 1];
-  for (int c = threadIdx.x; c < P; c += kBucketBlock) hist[c] = 0;
+  for (int c = threadIdx.x; c < P; c += kBucketBlock) {
+    hist[c] = 0;
+    if (cmin_all) mn[c] = INT_MAX;
+  }
   __syncthreads();
   // consecutive points (along a ray) often share a cell: a run of equal cells in a wave takes
   // ONE LDS atomic (by its head lane) instead of one per point
@@ -439,7 +447,10 @@ __global__ __launch_bounds__(kBucketBlock) void k_slab_bucket(
       const int c = v ? cell_xy(px[u], py[u]) : -1;
       int rank, len, head;
       runs(c, v, rank, len, head);
-      if (v && rank == 0) atomicAdd(&hist[c], len);
+      if (v && rank == 0) {
+        atomicAdd(&hist[c], len);
+        if (cmin_all) atomicMin(&mn[c], i);
+      }
     }
   }
   __syncthreads();
@@ -524,6 +535,8 @@ __global__ __launch_bounds__(kBucketBlock) void k_slab_bucket(
         pts[dst] = make_float4(px[u], py[u], pt[u], pt[u]);
         sorig[dst] = i;
         skey[dst] = s * P + c;
+        if (cmin_all && mn[c] == i)
+          cmin_all[(int64_t)s * P + c] = ((unsigned long long)(uint32_t)i << 32) | (uint32_t)dst;
       }
     }
   }
@@ -1442,6 +1455,7 @@ __device__ __forceinline__ void write_cell_flags(uint8_t* __restrict__ core, int
 constexpr int kCwQueue = 2048;
 struct CwQueue {
   int32_t item[kCwQueue];
+  int32_t key[kCwQueue];  // the queued point's cell key (k_core_slow skips its skey read)
   int n;      // reserved (may pass kCwQueue)
   int fail;   // first reservation that did not fit
   int base;
@@ -1450,17 +1464,19 @@ __device__ __forceinline__ void cells_fill_epilogue(const Geom& g, bool act, int
                                                     int e, int flag, uint8_t* __restrict__ core,
                                                     unsigned long long* __restrict__ cmin,
                                                     int32_t* __restrict__ slow,
+                                                    int32_t* __restrict__ slowk,
                                                     int32_t* __restrict__ n_slow, CwQueue& lq) {
   const int lane = threadIdx.x & 63;
   if (act && (lane & 7) == 0 && flag != 1 && (int64_t)ca < g.cells) cmin[ca] = ~0ull;
   // active cells are a prefix of the eight (occupied-list positions below the range end)
   const int na = __popcll(__ballot(act && (lane & 7) == 0));
   if (na == 0) return;
-  int gb[8], gf[8];
+  int gb[8], gf[8], gc[8];
   int E = 0, nu = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     gb[k] = __builtin_amdgcn_readlane(b, 8 * k);
+    gc[k] = __builtin_amdgcn_readlane(ca, 8 * k);
     const int ek = __builtin_amdgcn_readlane(e, 8 * k);
     gf[k] = __builtin_amdgcn_readlane(flag, 8 * k);
     if (k < na) {
@@ -1471,6 +1487,7 @@ __device__ __forceinline__ void cells_fill_epilogue(const Geom& g, bool act, int
   const int B = gb[0];
   int ub = 0;
   int32_t* qdst = lq.item;
+  int32_t* kdst = lq.key;
   if (nu > 0) {  // the undecided cells' points: one queue reservation per wave
     if (lane == 0) {
       ub = atomicAdd(&lq.n, nu);
@@ -1482,6 +1499,7 @@ __device__ __forceinline__ void cells_fill_epilogue(const Geom& g, bool act, int
     ub = __shfl(ub, 0);
     if (ub < 0) {
       qdst = slow;
+      kdst = slowk;
       ub = -1 - ub;
     }
   }
@@ -1489,12 +1507,20 @@ __device__ __forceinline__ void cells_fill_epilogue(const Geom& g, bool act, int
   for (int s0 = B; s0 < E; s0 += 64) {
     const int s = s0 + lane;
     const bool in = s < E;
-    int fl = gf[0];
+    int fl = gf[0], c = gc[0];
 #pragma unroll
-    for (int k = 1; k < 8; ++k) fl = (k < na && s >= gb[k]) ? gf[k] : fl;
+    for (int k = 1; k < 8; ++k) {
+      const bool sel = k < na && s >= gb[k];
+      fl = sel ? gf[k] : fl;
+      c = sel ? gc[k] : c;
+    }
     const bool u = in && fl == 2;
     const uint64_t um = nu > 0 ? __ballot(u) : 0ull;
-    if (u) qdst[ub + __popcll(um & below)] = s;
+    if (u) {
+      const int o = ub + __popcll(um & below);
+      qdst[o] = s;
+      kdst[o] = c;
+    }
     ub += __popcll(um);
     if (in) core[s] = (fl == 1) ? 1 : 0;
   }
@@ -1532,6 +1558,7 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
                                                           unsigned long long* __restrict__ cmin =
                                                               nullptr,
                                                           int32_t* __restrict__ slow = nullptr,
+                                                          int32_t* __restrict__ slowk = nullptr,
                                                           int32_t* __restrict__ n_slow = nullptr) {
   // legacy pipeline: the level-4 queue counter, zeroed here instead of by a memset launch
   // (k_core_fill, the next kernel on the stream, is its first user)
@@ -1677,7 +1704,7 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
       // decided cells write their points' flags here (the undecided ones are k_core_slow_cells')
       if (core && act && flag != 2) write_cell_flags(core, b, e, j, 8, (uint8_t)flag);
     } else {
-      cells_fill_epilogue(g, act, ca, b, e, flag, core, cmin, slow, n_slow, lq);
+      cells_fill_epilogue(g, act, ca, b, e, flag, core, cmin, slow, slowk, n_slow, lq);
     }
   }
   if constexpr (FUSED) {  // flush the block's queue (the cell loop is block-uniform)
@@ -1685,7 +1712,10 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
     const int m = min(lq.n, lq.fail);
     if (threadIdx.x == 0) lq.base = m > 0 ? atomicAdd(n_slow, m) : 0;
     __syncthreads();
-    for (int i = threadIdx.x; i < m; i += blockDim.x) slow[lq.base + i] = lq.item[i];
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {
+      slow[lq.base + i] = lq.item[i];
+      slowk[lq.base + i] = lq.key[i];
+    }
   }
 }
 
@@ -1790,18 +1820,32 @@ __global__ __launch_bounds__(kBlock, 8) void k_core_slow(const float4* __restric
                                                      uint8_t* __restrict__ core,
                                                      const int32_t* __restrict__ sorig = nullptr,
                                                      unsigned long long* __restrict__ cmin =
-                                                         nullptr) {
+                                                         nullptr,
+                                                     const int32_t* __restrict__ slowk = nullptr) {
   const int lane = threadIdx.x & 63;
   const int need = g.min_samples;
   // XCD-aware ranges of the (cell-ordered) queue: neighbouring points' windows share an L2
   const XcdRange xr = xcd_items(*n_slow, true);
   for (int64_t q = xr.first; q < xr.end; q += xr.step) {
     const int s = slow[q];
-    const int32_t key = skey[s];
+    // slowk (the fused cell pass): the key comes with the queue entry, and with integral times
+    // the window is the key's slab +- rt, so the occupancy loads do not wait for the point
+    const int32_t key = slowk ? slowk[q] : skey[s];
     const float4 p = pts[s];
     int cx, cy, cz;
     decode_key<D>(key, g, cx, cy, cz);
-    const Window w = make_window<D, false>(cx, cy, cz, p.w, p.w, g, slab_t);
+    Window w;
+    if (slowk && g.rt >= 0) {  // slab_of(p.w) is the key's slab (same cell_of)
+      const int cs = (int)((int64_t)key / ((int64_t)g.nx * g.ny * g.nz));
+      w.s0 = max(cs - g.rt, 0);
+      w.nS = max(min(cs + g.rt, g.nt - 1) - w.s0 + 1, 0);
+      w.x0 = cx - 2;
+      w.y0 = cy - 2;
+      w.z0 = (D == 3) ? cz - 2 : 0;
+      w.total = w.nS * ((D == 3) ? 125 : 25);
+    } else {
+      w = make_window<D, false>(cx, cy, cz, p.w, p.w, g, slab_t);
+    }
     int cnt = 0;
     // super-rounds of kR candidates per lane: every lane's bitmap words, then records, are
     // loaded together (one dependent level each for up to 64*kR candidates)
@@ -4015,6 +4059,7 @@ struct DbscanState {
   int k5_legacy = -1;                        // 1: round-1 K5 (fill + point queue); RPT_K5_MODE
   int k5_fill = 0;
   int k5_fused = -1;                         // 0: separate level-3 fill pass; RPT_K5_FUSED
+  bool bucket_allmin = false;  // this build's cell minima came from k_slab_bucket
   void k5_env() {
     if (k5_legacy < 0) {  // RPT_K5_MODE: 0 round-1 queue pipeline, 1 cells write point flags,
                           // 2 cells + point-flag fill (no queue); both 1/2 end in k_core_slow_cells
@@ -4293,6 +4338,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
     bucket_mode = (e && std::atoi(e) == 0) ? 0 : 1;
   }
   // time-ordered finite 2-D points with a slab's cells fitting LDS: per-slab counting sort
+  bucket_allmin = false;
   const bool bucket = bucket_mode && D == 2 && hb.n_finite_t == n && !hb.t_descends &&
                       (int64_t)nx * ny <= kBucketCells && nt < (int64_t(1) << 31);
   if (bucket) {
@@ -4352,11 +4398,16 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
                          hist_bytes, st, x, y, stride, t, g, slab_lo, CH, hist_g, pts, sorig,
                          skey);
     } else {
+      // the fused K5's all-core cell minima from the counting sort when both LDS arrays fit 64 KiB
+      bucket_allmin = k5_fused_path() && 2 * hist_bytes <= 65536;
+      const size_t lds = bucket_allmin ? 2 * hist_bytes : hist_bytes;
       RPT_HIP(hipFuncSetAttribute((const void*)k_slab_bucket,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)hist_bytes));
-      hipLaunchKernelGGL(k_slab_bucket, dim3((unsigned)nt), dim3(kBucketBlock), hist_bytes, st,
-                         x, y, stride, t, g, slab_lo, pts, sorig, skey, cell_start, hpos,
-                         slab_occ, occ_bits);
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(k_slab_bucket, dim3((unsigned)nt), dim3(kBucketBlock), lds, st, x, y,
+                         stride, t, g, slab_lo, pts, sorig, skey, cell_start, hpos, slab_occ,
+                         occ_bits,
+                         bucket_allmin ? reinterpret_cast<unsigned long long*>(cell_min_pair)
+                                       : nullptr);
     }
     RPT_CHECK_LAUNCH();
     if (coalesced_scan) {
@@ -4390,8 +4441,9 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   }
   hipLaunchKernelGGL(k_cell_box<D>, dim3(grid_for(8 * n, kBlock, 8192)), dim3(kBlock), 0, st,
                      pts, cell_start, occ, n_occ_dev, g, boxA, boxB, mutual, cr,
-                     reinterpret_cast<unsigned long long*>(cell_min_pair),
-                     k5_fused_path() ? (const int32_t*)sorig : nullptr);
+                     bucket_allmin ? nullptr
+                                   : reinterpret_cast<unsigned long long*>(cell_min_pair),
+                     (k5_fused_path() && !bucket_allmin) ? (const int32_t*)sorig : nullptr);
   RPT_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_slab_range<D>, dim3((unsigned)nt), dim3(kBlock), 0, st, cr, occ, hpos,
                      cell_start, (int64_t)(C / nt), (int)nt, slab_t, bucket ? occ_base : nullptr);
@@ -4492,9 +4544,9 @@ int32_t DbscanState::core_pass(hipStream_t st) {
     RPT_HIP(hipMemsetAsync(n_slow, 0, sizeof(int32_t), st));
     hipLaunchKernelGGL(k_core_cells_oct<true>, dim3((grid_for(8 * n, kBlock, 8192) + 7) & ~7),
                        dim3(kBlock), 0, st, g, (int)rs, occ, n_occ, rec<2>(), mutual, occ_bits,
-                       slab_t, (int32_t*)nullptr, (int32_t*)nullptr, core, cm, slow, n_slow);
+                       slab_t, (int32_t*)nullptr, (int32_t*)nullptr, core, cm, slow, cq, n_slow);
     hipLaunchKernelGGL(k_core_slow<2>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<2>(), occ_bits, slab_t, slow, n_slow, core, sorig, cm);
+                       rec<2>(), occ_bits, slab_t, slow, n_slow, core, sorig, cm, cq);
     RPT_CHECK_LAUNCH();
     cmin_ready = true;
     tm.mark();
