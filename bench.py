@@ -130,7 +130,7 @@ def _reference_measured():
 def _traffic(name):
     """PMC-measured HBM bytes per launch committed for a workload (tools/pmc.sh: separate
     FETCH_SIZE / WRITE_SIZE passes, gfx950 read correction), newest round first."""
-    for rd in ("r3", "r2"):
+    for rd in ("r4", "r3", "r2"):
         f = ROOT / "profiles" / rd / name
         if f.exists():
             d = json.loads(f.read_text())

@@ -358,6 +358,16 @@ __device__ __forceinline__ uint32_t phase_base(uint32_t ph, uint32_t total) {
 __device__ __forceinline__ uint32_t stage_pos(uint32_t i, uint32_t total, bool ph4) {
   return ph4 ? phase_base(i & 3u, total) + (i >> 2) : i;
 }
+// the same with the group's residue bases computed once (wave-uniform: scalar registers)
+struct StageBases {
+  uint32_t b1, b2, b3;
+  __device__ explicit StageBases(uint32_t total)
+      : b1((total + 3u) >> 2), b2(b1 + ((total + 2u) >> 2)), b3(b2 + ((total + 1u) >> 2)) {}
+  __device__ uint32_t pos(uint32_t i) const {
+    const uint32_t r = i & 3u;
+    return (r == 0u ? 0u : (r == 1u ? b1 : (r == 2u ? b2 : b3))) + (i >> 2);
+  }
+};
 
 template <bool HI, bool STAGE>
 __global__ __launch_bounds__(kBlock) void k_group_count_u8(const uint8_t* __restrict__ echo,
@@ -367,14 +377,25 @@ __global__ __launch_bounds__(kBlock) void k_group_count_u8(const uint8_t* __rest
                                                           uint32_t* __restrict__ entries,
                                                           int ph4) {
   const int lane = threadIdx.x & 63;
-  const uint32_t wave0 = blockIdx.x * kWavesPerBlock + threadIdx.x / 64;
+  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock +
+                                                        threadIdx.x / 64);
   const uint32_t n_waves = gridDim.x * kWavesPerBlock;
+  // the group's (file, group-in-file) stepped incrementally: one division per wave, not one per
+  // group (a 32-bit division by a runtime value is a few dozen scalar instructions)
+  const uint32_t dq = n_waves / gm.gpf, dr = n_waves - dq * gm.gpf;
+  uint32_t gf = wave0 / gm.gpf, gr = wave0 - gf * gm.gpf;
   for (uint32_t g0 = wave0; g0 < n_groups; g0 += n_waves) {
-    const uint32_t grp = __builtin_amdgcn_readfirstlane(g0);
-    uint32_t f;
-    int64_t row0;
-    int nr;
-    group_rows(gm, grp, &f, &row0, &nr);
+    const uint32_t grp = g0;
+    const uint32_t f = gf;
+    const int r0 = (int)gr * kGroupRows;
+    const int64_t row0 = (int64_t)f * gm.rows + r0;
+    const int nr = min(kGroupRows, gm.rows - r0);
+    gf += dq;
+    gr += dr;
+    if (gr >= gm.gpf) {
+      gr -= gm.gpf;
+      ++gf;
+    }
     uint4 v[kGroupRows];
 #pragma unroll
     for (int k = 0; k < kGroupRows; ++k) {
@@ -386,28 +407,35 @@ __global__ __launch_bounds__(kBlock) void k_group_count_u8(const uint8_t* __rest
     }
     if constexpr (STAGE) {
       uint32_t m[kGroupRows];
-      int c[kGroupRows], incl[kGroupRows];
+      int incl[kGroupRows];
 #pragma unroll
-      for (int k = 0; k < kGroupRows; ++k) {
+      for (int k = 0; k < kGroupRows; ++k)
         m[k] = (k < nr) ? mask16(keep_bits<HI>(v[k].x, K), keep_bits<HI>(v[k].y, K),
                                  keep_bits<HI>(v[k].z, K), keep_bits<HI>(v[k].w, K))
                         : 0u;  // a zero sample is kept when T = -1: rows past nr keep nothing
-        c[k] = __popc(m[k]);
-        incl[k] = wave_incl_scan_dpp(c[k]);
-      }
+      // two rows per scan: a row's inclusive lane count is <= 1024, so the low and high halves
+      // of one 32-bit DPP scan never carry into each other (the pass is half VALU-bound: PMC)
+      static_assert(kGroupRows == 4, "rows are scanned in pairs");
       uint32_t rb[kGroupRows + 1];
       rb[0] = 0;
 #pragma unroll
-      for (int k = 0; k < kGroupRows; ++k)
-        rb[k + 1] = rb[k] + (uint32_t)__builtin_amdgcn_readlane(incl[k], 63);
+      for (int k = 0; k < kGroupRows; k += 2) {
+        const int pair = wave_incl_scan_dpp(__popc(m[k]) | (__popc(m[k + 1]) << 16));
+        incl[k] = pair & 0xffff;
+        incl[k + 1] = (int)((uint32_t)pair >> 16);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane(pair, 63);
+        rb[k + 1] = rb[k] + (tot & 0xffffu);
+        rb[k + 2] = rb[k + 1] + (tot >> 16);
+      }
       const uint32_t total = rb[kGroupRows];
       if (total != 0u && total <= (uint32_t)kStageSlots) {  // wave-uniform
         uint32_t* e = entries + (int64_t)grp * kStageSlots;
         __shared__ GroupLds s_lds[kWavesPerBlock];
         GroupLds& L = s_lds[threadIdx.x / 64];
         group_to_lds(L, lane, m, incl, v);
+        const StageBases sb(total);
         for (uint32_t i = (uint32_t)lane; i < total; i += 64u)
-          e[stage_pos(i, total, ph4 != 0)] = kept_entry(L, rb, i);
+          e[ph4 ? sb.pos(i) : i] = kept_entry(L, rb, i);
         wave_lds_sync();  // the slice is rewritten by the next group
       }
       if (lane == 0) group_count[grp] = (int32_t)total;

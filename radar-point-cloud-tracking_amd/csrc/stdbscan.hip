@@ -999,18 +999,33 @@ __global__ __launch_bounds__(kBlock) void k_slab_range(const CellRec<D>* __restr
 
 // ---------------------------------------------------------------- neighbour predicates
 
-// Exact pair test (see file header).
+// Exact pair test (see file header): the float64 squared distance against eps^2.  A float32
+// screen decides first (Geom::e2lo / e2hi, the classify_cells screen): the float32 distance is
+// within a few 2^-24 of the float64 one (relative), far inside the 1e-5 margins, so only pairs
+// within 1e-5 of eps reach the float64 test -- the float64 ops (half rate, plus conversions) were
+// most of the VALU of the pair-testing kernels.
 template <int D>
 __device__ __forceinline__ bool adjacent(const float4& a, const float4& b, const Geom& g) {
   const float dt = fabsf(a.w - b.w);
-  const double dx = (double)a.x - (double)b.x;
-  const double dy = (double)a.y - (double)b.y;
-  double d2 = dx * dx + dy * dy;
+  const float fx = a.x - b.x, fy = a.y - b.y;
+  float f2 = fx * fx + fy * fy;
   if (D == 3) {
-    const double dz = (double)a.z - (double)b.z;
-    d2 = d2 + dz * dz;
+    const float fz = a.z - b.z;
+    f2 = f2 + fz * fz;
   }
-  return (d2 <= g.eps2) && (dt <= g.epst);
+  bool near = !(f2 <= g.e2lo) && !(f2 > g.e2hi);  // (NaN: near, the float64 test decides)
+  bool in = f2 <= g.e2lo;
+  if (near) {
+    const double dx = (double)a.x - (double)b.x;
+    const double dy = (double)a.y - (double)b.y;
+    double d2 = dx * dx + dy * dy;
+    if (D == 3) {
+      const double dz = (double)a.z - (double)b.z;
+      d2 = d2 + dz * dz;
+    }
+    in = d2 <= g.eps2;
+  }
+  return in && (dt <= g.epst);
 }
 
 // |p - [lo, hi]| lower bound and the farthest-end distance, float64, each rounded like the pair
@@ -1031,6 +1046,23 @@ __device__ __forceinline__ int classify(const float4& p, const float4& A, const 
   const float tmin = (p.w < tlo) ? (tlo - p.w) : ((p.w > thi) ? (p.w - thi) : 0.f);
   if (!(tmin <= g.epst)) return 0;
   const float tmax = fmaxf(fabsf(p.w - tlo), fabsf(p.w - thi));
+  {
+    // float32 screen of the spatial bounds (as adjacent / classify_cells): float64 only when a
+    // bound lies within 1e-5 of eps^2
+    auto fgap = [](float v, float lo, float hi) { return fmaxf(fmaxf(lo - v, v - hi), 0.f); };
+    auto fspan = [](float v, float lo, float hi) { return fmaxf(fabsf(v - lo), fabsf(v - hi)); };
+    const float gx = fgap(p.x, A.x, A.y), gy = fgap(p.y, A.z, A.w);
+    const float sx = fspan(p.x, A.x, A.y), sy = fspan(p.y, A.z, A.w);
+    float fmn = gx * gx + gy * gy, fmx = sx * sx + sy * sy;
+    if (D == 3) {
+      const float gz = fgap(p.z, B.x, B.y), sz = fspan(p.z, B.x, B.y);
+      fmn = fmn + gz * gz;
+      fmx = fmx + sz * sz;
+    }
+    if (fmn > g.e2hi) return 0;
+    if (fmx <= g.e2lo) return (tmax <= g.epst) ? 1 : 2;
+    if (fmn <= g.e2lo && fmx > g.e2hi) return 2;
+  }
   double mnx, mxx, mny, mxy;
   span_dist(p.x, A.x, A.y, mnx, mxx);
   span_dist(p.y, A.z, A.w, mny, mxy);

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Build abl/librpt_base.so from a commit (default HEAD) in a temporary worktree: the same-box A/B
+# baseline of tools/r4_suite_ab.sh.   bash tools/ab_base.sh [rev]
+set -e
+cd "$(dirname "$0")/.."
+REV=${1:-HEAD}
+WT=$(mktemp -d /tmp/rpt_base.XXXXXX)
+git worktree add -f "$WT" "$REV" -q
+(cd "$WT" && python -c "import sys; sys.path.insert(0, 'radar-point-cloud-tracking_amd'); from rpt import _build; _build.build()" > /dev/null)
+mkdir -p abl
+cp "$WT/radar-point-cloud-tracking_amd/rpt/librpt.so" abl/librpt_base.so
+git worktree remove --force "$WT"
+echo "abl/librpt_base.so <- $(git rev-parse --short "$REV")"
