@@ -25,11 +25,13 @@ step k+1's device work runs while step k's host stage and readbacks finish, and 
 latency-bound kernels share the CUs; 3 measured +4-5 % over 2 in interleaved same-box runs, 4
 no better); `one_stack_in_flight` repeats the steps strictly one after
 another, and K5's roofline is taken from that leg (K5 alone on the GPU).
-At N>1 (the frame-sharded path) three stacks are in flight per rank by default: their
-collectives go through ONE communicator in a fixed software-pipeline order
-(rpt.dist.CommSequencer); at one rank on the 125-frame share (the 8-GPU per-rank share) the shard
-driver v2 measured 1.48 ms per step with 3 lanes (1.62 ms with the sequencer's order kept,
---sequenced) against 2.12 ms with 1 (profiles/r4/bench_sharded1rank_125f_*.json).
+At N>1 (the frame-sharded path) one stack is in flight per rank by default; `--lanes 3` keeps
+three, their collectives through ONE communicator in a fixed software-pipeline order
+(rpt.dist.CommSequencer, validated with gloo at 8 ranks, not yet on RCCL across GPUs, hence not
+the default).  With one rank (`--sharded`, the 125-frame per-rank share of 8 GPUs) the default
+stays 3: the shard driver v2 measured 1.48 ms per step with 3 lanes (1.62 ms with the
+sequencer's order kept, --sequenced) against 2.12 ms with 1
+(profiles/r4/bench_sharded1rank_125f_*.json).
 After the timed region (N=1, timing on), K5 is also timed on the per-GPU shares at 8 GPUs, where
 SURVEY.md §8(d) sets the 0.40 roofline target: `roofline_c4_share` (125 standard frames, the
 configs[3] stack's share) and `roofline_configs4_share` (125 dense frames, configs[4]'s), one
@@ -192,11 +194,11 @@ def main():
                     help="sharded runs: ShardedStackPipeline (HipOps stages composed in Python) "
                          "instead of the native shard driver")
     ap.add_argument("--lanes", type=int, default=None,
-                    help="stacks in flight at once (default 3 on one GPU: native handles on "
-                         "separate streams; with N>1 ranks (or --sharded) see --help's "
-                         "docstring: a lane is a NativeShardPipeline with its own stream and "
-                         "thread, all lanes on ONE process group in rpt.dist.CommSequencer's "
-                         "order); 1 = strictly one after another")
+                    help="stacks in flight at once (default 3 at one rank: native handles on "
+                         "separate streams; default 1 at N>1 ranks, where a lane is a "
+                         "NativeShardPipeline with its own stream and thread, all lanes on ONE "
+                         "process group in rpt.dist.CommSequencer's order); 1 = strictly one "
+                         "after another")
     ap.add_argument("--sequenced", action="store_true",
                     help="sharded runs at one rank: keep the CommSequencer's slot order although "
                          "every collective is the identity (what the ordering costs)")
@@ -213,7 +215,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if args.lanes is None:
-        args.lanes = 3
+        # several lanes share one RCCL communicator only through CommSequencer's order, which has
+        # run on gloo (8 ranks) and at one rank, never on RCCL across GPUs: one lane per rank
+        # until it has (--lanes 3 opts in)
+        args.lanes = 3 if world == 1 else 1
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # --sharded: the frame-sharded multi-GPU path even at one rank (measures its per-rank cost)
     dist = world > 1 or args.sharded
