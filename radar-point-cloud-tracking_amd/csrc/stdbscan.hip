@@ -214,6 +214,24 @@ __global__ __launch_bounds__(kBlock) void k_bounds_final(const Bounds* __restric
 }
 
 // ---------------------------------------------------------------- grid geometry
+// n / d for 0 <= n < 2^31 by one 32 x 32 -> 64-bit multiply and a shift (Granlund-Montgomery):
+// m = ceil(2^(31+k) / d) with 2^(k-1) < d <= 2^k, so m < 2^32 and the rounding error n * (m / 2^(31+k)
+// - 1 / d) < 2^-k <= 1 / d never reaches the next integer.  The cell-key decodes of the latency-
+// bound window kernels divided by runtime grid sizes (a few dozen VALU instructions each).
+struct FastDiv {
+  uint32_t m;
+  int s;
+  void init(uint32_t d) {
+    int k = 0;
+    while ((uint64_t(1) << k) < d) ++k;
+    s = 31 + k;
+    m = (uint32_t)(((uint64_t(1) << s) + d - 1) / d);
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    return (uint32_t)(((uint64_t)n * m) >> s);
+  }
+};
+
 struct Geom {
   double ox, oy, oz, ot;  // origins (minima)
   double cs;              // spatial cell side
@@ -232,6 +250,27 @@ struct Geom {
   // lies in slabs [s - rt, s + rt] (DbscanState::slab_reach), so the scan windows take exactly
   // those; -1: non-integral times, windows from the time range with one slab of slack each side
   int rt;
+  // 1: every time is an integer and a slab is ONE time value (ct == 1), so any two points whose
+  // slabs lie within rt <= floor(eps_t) of each other pass the time test: the window kernels, whose
+  // candidates all come from such windows, skip the time bounds of their box classifications
+  int tfree;
+  FastDiv fnx, fny, fnz, fslab;  // by nx, ny, nz and nx * ny * nz (a key's slab)
+  // cell key (< 2^31) -> x, y, z, slab
+  __device__ __forceinline__ void split(uint32_t k, int& x, int& y, int& z, int& s) const {
+    const uint32_t r = fnx.div(k);
+    x = (int)(k - r * (uint32_t)nx);
+    const uint32_t r2 = fny.div(r);
+    y = (int)(r - r2 * (uint32_t)ny);
+    if (nz == 1) {
+      z = 0;
+      s = (int)r2;
+    } else {
+      const uint32_t r3 = fnz.div(r2);
+      z = (int)(r2 - r3 * (uint32_t)nz);
+      s = (int)r3;
+    }
+  }
+  __device__ __forceinline__ int slab_of_key(int64_t k) const { return (int)fslab.div((uint32_t)k); }
 };
 
 // cell index floor((v - o) / side) as a multiply by the host's float64 reciprocal (a float64
@@ -1087,12 +1126,8 @@ __device__ __forceinline__ void for_each_cell(const float4& p, int32_t key, cons
                                               const float4* __restrict__ boxA,
                                               const float4* __restrict__ boxB,
                                               const float2* __restrict__ slab_t, F&& f) {
-  const int cx = key % g.nx;
-  int r = key / g.nx;
-  const int cy = r % g.ny;
-  r /= g.ny;
-  const int cz = (D == 3) ? (r % g.nz) : 0;
-  const int cs = (D == 3) ? (r / g.nz) : r;
+  int cx, cy, cz, cs;
+  g.split((uint32_t)key, cx, cy, cz, cs);
   // conservative slab window (+-1 slack), culled by each slab's actual time range
   const double tp = (double)p.w, et = (double)g.epst;
   int s0 = (int)fmax(floor((tp - et - g.ot) * g.inv_ct) - 1.0, 0.0);
@@ -1265,12 +1300,9 @@ __device__ __forceinline__ Window make_window(int cx, int cy, int cz, float tlo,
 template <int D>
 __device__ __forceinline__ void decode_key(int64_t key, const Geom& g, int& cx, int& cy, int& cz) {
   // keys of real cells are < 2^30 (cmax): 32-bit divisions, not the 64-bit ones' call sequence
-  const int k = (int)key;
-  cx = k % g.nx;
-  int r = k / g.nx;
-  cy = r % g.ny;
-  r /= g.ny;
-  cz = (D == 3) ? (r % g.nz) : 0;
+  int cs;
+  g.split((uint32_t)key, cx, cy, cz, cs);
+  if (D != 3) cz = 0;
 }
 
 // q-th cell of the window; -1 when outside the grid or its slab holds nothing within reach
@@ -1307,15 +1339,20 @@ template <int D, bool SCREEN = false>
 __device__ __forceinline__ int classify_cells(const float4& A1, const float4& B1,
                                               const float4& A2, const float4& B2,
                                               const Geom& g) {
+  // interval gap: max(b0 - a1, a0 - b1, 0) (one v_max3; equal to the branchy form, since a
+  // float32 difference has the sign of the exact one)
   auto gap = [](float a0, float a1, float b0, float b1) -> float {
-    return (b0 > a1) ? (b0 - a1) : ((a0 > b1) ? (a0 - b1) : 0.f);
+    return fmaxf(fmaxf(b0 - a1, a0 - b1), 0.f);
   };
   auto gapd = [](float a0, float a1, float b0, float b1) -> double {
     return (b0 > a1) ? ((double)b0 - (double)a1) : ((a0 > b1) ? ((double)a0 - (double)b1) : 0.0);
   };
-  const float tg = gap(A2.z, A2.w, B2.z, B2.w);
-  if (!(tg <= g.epst)) return 0;
-  const float tm = fmaxf(fabsf(B2.w - A2.z), fabsf(A2.w - B2.z));
+  float tm = 0.f;  // (tfree: every pair of the window is within eps_t)
+  if (!g.tfree) {  // kernel-uniform
+    const float tg = gap(A2.z, A2.w, B2.z, B2.w);
+    if (!(tg <= g.epst)) return 0;
+    tm = fmaxf(fabsf(B2.w - A2.z), fabsf(A2.w - B2.z));
+  }
   if (D == 2 && SCREEN) {
     const float fx = gap(A1.x, A1.y, B1.x, B1.y), fy = gap(A1.z, A1.w, B1.z, B1.w);
     const float fmn = fx * fx + fy * fy;
@@ -1477,6 +1514,12 @@ __device__ __forceinline__ void write_cell_flags(uint8_t* __restrict__ core, int
   for (int s = we + j; s < e; s += lanes) core[s] = v;
 }
 
+// Row of mask position k (0..4, own row first: dy = 0, -1, +1, -2, +2) as dy + 2, branch-free
+// (3-bit fields of one constant): 2, 1, 3, 0, 4.
+__device__ __forceinline__ int cw_row(int k) {
+  return (int)__builtin_amdgcn_ubfe(16586u, (uint32_t)(3 * k), 3u);
+}
+
 // The FUSED epilogue of k_core_cells_oct (whole wave, wave-uniform control): lanes 8k hold cell k
 // of the wave (act, key, point range [b, e), flag 0 / 1 / 2).  The cells' (min original, sorted)
 // pairs over ALL their points come from k_cell_box (allmin): an all-core cell keeps it, every other
@@ -1623,10 +1666,8 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
       b = ri.b;
       e = ri.e;
     } else if (act) {
-      const int cx = ca % g.nx;
-      const int rr = ca / g.nx;
-      const int cy = rr % g.ny;
-      const int cs = rr / g.ny;
+      int cx, cy, cz, cs;
+      g.split((uint32_t)ca, cx, cy, cz, cs);
       const int sl = cs + j - R;
       const bool sv = j <= 2 * R && sl >= 0 && sl < g.nt;
       const CellRec<2> ra = crec[ca];
@@ -1685,6 +1726,9 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
           }
         }
         bool decided = false;
+        // key of window row dy = -2, column dx = -2 in this lane's slab (candidate key = rowbase
+        // + (dy + 2) * nx + (dx + 2))
+        const int rowbase = (sl * g.ny + (cy - 2)) * g.nx + (cx - 2);
         while (true) {
           int rem = m25 ? 1 : 0;
 #pragma unroll
@@ -1699,8 +1743,9 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
             const int p = __builtin_ctz(m25 | (1u << 31));
             m25 &= m25 - 1;
             const int k = p / 5, dx = p - 5 * k;
-            const int dy = (k == 0) ? 2 : ((k & 1) ? 2 - (k + 1) / 2 : 2 + k / 2);
-            const int key = (sl * g.ny + (cy + dy - 2)) * g.nx + (cx + dx - 2);
+            // (24-bit multiply: full rate, where a 32-bit v_mul_lo is quarter rate)
+            const int key = rowbase + (int)__umul24((uint32_t)cw_row(k),
+                                                    (uint32_t)g.nx) + dx;
             cr[i] = crec[has[i] ? key : ca];
           }
 #pragma unroll
@@ -1868,7 +1913,7 @@ __global__ __launch_bounds__(kBlock, 8) void k_core_slow(const float4* __restric
     decode_key<D>(key, g, cx, cy, cz);
     Window w;
     if (slowk && g.rt >= 0) {  // slab_of(p.w) is the key's slab (same cell_of)
-      const int cs = (int)((int64_t)key / ((int64_t)g.nx * g.ny * g.nz));
+      const int cs = g.slab_of_key(key);
       w.s0 = max(cs - g.rt, 0);
       w.nS = max(min(cs + g.rt, g.nt - 1) - w.s0 + 1, 0);
       w.x0 = cx - 2;
@@ -2193,7 +2238,8 @@ __global__ __launch_bounds__(kTileBlock) void k_core_tiles(
       for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
         const int32_t key = occ[q0 + i];
         srec[base + i] = crec[key];
-        const int x = key % g.nx, y = (key / g.nx) % g.ny;
+        int x, y, z_, s_;
+        g.split((uint32_t)key, x, y, z_, s_);
         smap[(so * MR + (y - y0 + 2)) * g.nx + x] = (uint16_t)(base + i);
       }
     }
@@ -2246,7 +2292,8 @@ __global__ __launch_bounds__(kTileBlock) void k_core_tiles(
     int flag = 0, b = 0, e = 0;
     if (act) {
       const int32_t ca = occ[q];
-      const int cx = ca % g.nx, cy = (ca / g.nx) % g.ny;
+      int cx, cy, cz_, cs_;
+      g.split((uint32_t)ca, cx, cy, cz_, cs_);
       const CellRec<2> ra = own_rec(q, ca);
       b = ra.b;
       e = ra.e;
@@ -2309,7 +2356,8 @@ __global__ __launch_bounds__(kTileBlock) void k_core_tiles(
     const int32_t ca = occ[q];
     const CellRec<2> ra = own_rec(q, ca);
     const float4 A1 = rec_boxA<2>(ra), A2 = rec_boxB(ra);
-    const int cx = ca % g.nx, cy = (ca / g.nx) % g.ny;
+    int cx, cy, cz_, cs_;
+    g.split((uint32_t)ca, cx, cy, cz_, cs_);
     float4 cA[kSR], cB[kSR];
     int cb[kSR], ce[kSR], ccls[kSR];
 #pragma unroll
@@ -2573,7 +2621,7 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
       decode_key<D>(ca, g, cx, cy, cz);
       // only cells B > A: slabs from A's own on (slabs are the slowest key dimension); the boxes'
       // time ranges are checked by classify_cells, so the slab window is not shrunk first
-      const int sa = (int)((int64_t)ca / ((int64_t)g.nx * g.ny * g.nz));
+      const int sa = g.slab_of_key(ca);
       const Window w = make_window<D, false>(cx, cy, cz, A2.z, A2.w, g, slab_t, sa);
       // PARTIAL with the first pass's mask of this cell's undecided candidates (window positions
       // < 127): only those are visited, no enumeration or classification of the window again
@@ -2758,7 +2806,7 @@ __global__ __launch_bounds__(kBlock, 6) void k_union_cells_pair(
         const float4 A1 = rec_boxA<2>(ra_rec), A2 = rec_boxB(ra_rec);
         int cx, cy, cz;
         decode_key<2>(ca, g, cx, cy, cz);
-        const int sa = (int)((int64_t)ca / ((int64_t)g.nx * g.ny));
+        const int sa = g.slab_of_key(ca);
         const Window w = make_window<2, false>(cx, cy, cz, A2.z, A2.w, g, slab_t, sa);
         for (int base = 0; base < w.total; base += W * kR) {
           int64_t cb[kR];
@@ -2862,7 +2910,7 @@ __global__ __launch_bounds__(kBlock) void k_union_listed(const float4* __restric
     const float4 A1 = rec_boxA<2>(ra_rec), A2 = rec_boxB(ra_rec);
     int cx, cy, cz;
     decode_key<2>(ca, g, cx, cy, cz);
-    const int sa = (int)((int64_t)ca / ((int64_t)g.nx * g.ny));
+    const int sa = g.slab_of_key(ca);
     const Window w = make_window<2, false>(cx, cy, cz, A2.z, A2.w, g, slab_t, sa);
     // the undecided candidate of this lane (rb >= 0) -> one adjacent core pair unites A and B
     auto settle = [&](int rb, int bb, int eb) {
@@ -3443,7 +3491,8 @@ __global__ __launch_bounds__(kTileBlock) void k_label_tiles(
         srec[base + i] = crec[key];
         sck[base + i] = cell_key[key];
         smu[base + i] = mutual[key];
-        const int x = key % g.nx, y = (key / g.nx) % g.ny;
+        int x, y, z_, s_;
+        g.split((uint32_t)key, x, y, z_, s_);
         smap[(so * MR + (y - y0 + 2)) * g.nx + x] = (uint16_t)(base + i);
       }
     }
@@ -3458,7 +3507,8 @@ __global__ __launch_bounds__(kTileBlock) void k_label_tiles(
       continue;  // all core
     // the cell's non-core points, 64 flags at a time (key_of < 0: not core)
     const float4 A1 = rec_boxA<2>(ra), A2 = rec_boxB(ra);
-    const int cx = ca % g.nx, cy = (ca / g.nx) % g.ny;
+    int cx, cy, cz_, cs_;
+    g.split((uint32_t)ca, cx, cy, cz_, cs_);
     bool have_cands = false;
     float4 cA[kSR], cB[kSR];
     int cb[kSR], ce[kSR], ck[kSR], mu[kSR];
@@ -3729,10 +3779,8 @@ __global__ __launch_bounds__(kBlock) void k_frames_cells(Geom g, int R,
        q += (int64_t)gridDim.x * blockDim.x) {
     const int32_t ca = occ[q];
     if ((int64_t)ca >= g.cells) continue;  // non-finite time: settled per point
-    const int cx = ca % g.nx;
-    const int rr = ca / g.nx;
-    const int cy = rr % g.ny;
-    const int cs = rr / g.ny;
+    int cx, cy, cz_, cs;
+    g.split((uint32_t)ca, cx, cy, cz_, cs);
     const CellRec<2> ra = crec[ca];
     const float4 A1 = rec_boxA<2>(ra), B1 = rec_boxB(ra);
     int frames = 1;  // the cell's own
@@ -3742,7 +3790,8 @@ __global__ __launch_bounds__(kBlock) void k_frames_cells(Geom g, int R,
       const int64_t c = ((int64_t)sl * g.ny + cy) * g.nx + cx;
       if (!((occ_bits[c >> 5] >> (c & 31)) & 1u)) continue;
       const CellRec<2> rc = crec[c];
-      frames += (classify_cells<2>(A1, B1, rec_boxA<2>(rc), rec_boxB(rc), g) == 1) ? 1 : 0;
+      // (box A of both cells, then box B of both: classify_cells' argument order)
+      frames += (classify_cells<2>(A1, rec_boxA<2>(rc), B1, rec_boxB(rc), g) == 1) ? 1 : 0;
     }
     fok[ca] = frames >= min_frames ? 1 : 0;
   }
@@ -4279,9 +4328,14 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   g.nz = (int)nz;
   g.nt = (int)nt;
   g.cells = nx * ny * nz * nt;
+  g.fnx.init((uint32_t)nx);
+  g.fny.init((uint32_t)ny);
+  g.fnz.init((uint32_t)nz);
+  g.fslab.init((uint32_t)(nx * ny * nz));
   {
     const double r = slab_reach();  // (infinite for an infinite eps_time: generic windows)
     g.rt = (integral_t && r < 1e9) ? (int)std::min(r, (double)nt) : -1;
+    g.tfree = (g.rt >= 0 && ct == 1.0 && (double)g.rt <= std::floor((double)epst)) ? 1 : 0;
   }
   C = g.cells;
   const int64_t C1 = C + 1;  // + the isolated cell (non-finite t)
