@@ -177,29 +177,38 @@ __device__ __forceinline__ float seq_sum(const float* __restrict__ gx,
     }
     const float4* sb4 = reinterpret_cast<const float4*>(sb);
     if (i == 0 && m == kChunk) {
-      // a whole chunk (the bulk of a long run): fully unrolled, three rotating batches of 16
-      // elements, each batch's LDS reads issued two batches ahead of its adds (at most 12 reads
-      // in flight, counted waits only)
-      constexpr int kB = 4, kNb = kChunk / (4 * kB);
-      float4 r[3][kB];
+      // a whole chunk (the bulk of a long run): two 32-element register windows in ping-pong,
+      // each filled by ONE burst of 8 LDS reads issued a window ahead of its adds (bursts, not
+      // four reads between every 16 adds: 1.70 -> 1.56 ms on the dense share's 490 k-point
+      // chains, tools/microbench/chain_lds.hip, where 64-element windows measure the same; the
+      // dependent add alone, register operands, costs 5.0 cycles there and this feed 7.6)
+      constexpr int kW = 8, kNw = kChunk / (4 * kW);
+      float4 wa[kW], wb[kW];
 #pragma unroll
-      for (int u = 0; u < kB; ++u) {
-        r[0][u] = sb4[u];
-        r[1][u] = sb4[kB + u];
-      }
+      for (int u = 0; u < kW; ++u) wa[u] = sb4[u];
 #pragma unroll
-      for (int bt = 0; bt < kNb; ++bt) {
-        if (bt + 2 < kNb) {
+      for (int w = 0; w < kNw; w += 2) {
 #pragma unroll
-          for (int u = 0; u < kB; ++u) r[(bt + 2) % 3][u] = sb4[(bt + 2) * kB + u];
+        for (int u = 0; u < kW; ++u) wb[u] = sb4[(w + 1) * kW + u];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < kW; ++u) {
+          acc = acc + wa[u].x;
+          acc = acc + wa[u].y;
+          acc = acc + wa[u].z;
+          acc = acc + wa[u].w;
+        }
+        if (w + 2 < kNw) {
+#pragma unroll
+          for (int u = 0; u < kW; ++u) wa[u] = sb4[(w + 2) * kW + u];
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int u = 0; u < kB; ++u) {
-          acc = acc + r[bt % 3][u].x;
-          acc = acc + r[bt % 3][u].y;
-          acc = acc + r[bt % 3][u].z;
-          acc = acc + r[bt % 3][u].w;
+        for (int u = 0; u < kW; ++u) {
+          acc = acc + wb[u].x;
+          acc = acc + wb[u].y;
+          acc = acc + wb[u].z;
+          acc = acc + wb[u].w;
         }
       }
       i = kChunk;
@@ -472,8 +481,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_runs_lane(
 // stream.  META: the frame sort already wrote frame/label/count/first; otherwise the metadata
 // comes from the sorted keys (written by the intensity wave).
 template <bool META>
-// 4 waves/SIMD (128 VGPRs: the x and y prefetch registers; 5 spilled 23)
-__global__ __launch_bounds__(kBlock, 4) void k_summarize(
+// 2 waves/SIMD (up to 256 VGPRs: the x and y prefetch registers and the chain's two register
+// windows; 4 waves spilled 17; a long run's waves are few, occupancy does not bound them)
+__global__ __launch_bounds__(kBlock, 2) void k_summarize(
     const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
     const int64_t* __restrict__ seg_start, const int32_t* __restrict__ n_seg_dev, int64_t n,
     const float* __restrict__ gx, const float* __restrict__ gy, const float* __restrict__ gi,

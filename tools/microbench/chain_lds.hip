@@ -14,7 +14,7 @@
 namespace {
 constexpr int kRuns = 125, kLen = 490000;
 
-__global__ void k_prod(const float* gx, const float* gy, float* out) {
+__global__ __launch_bounds__(64) void k_prod(const float* gx, const float* gy, float* out) {
   __shared__ float sb[2 * rpt::kSeqChunk];
   const int r = blockIdx.x, lane = threadIdx.x;
   const float s = rpt::seq_sum(gx, gy, r * kLen, (r + 1) * kLen, lane, sb);
@@ -151,6 +151,213 @@ __global__ __launch_bounds__(64) void k_walk(const float* gx, const float* gy, f
   if (lane == 15) out[2 * r] = acc;
   if (lane == 31) out[2 * r + 1] = acc;
 }
+// register operands for the chain (as k_regs) with ds_read_b128 issued alongside into registers
+// the chain never reads: does the LDS instruction stream itself slow the dependent adds?
+__global__ __launch_bounds__(64) void k_regs_lds(const float* gx, float* out) {
+  __shared__ float4 sb[256];
+  const int lane = threadIdx.x;
+  sb[lane] = make_float4(gx[lane], gx[lane + 64], gx[lane + 128], gx[lane + 192]);
+  sb[lane + 64] = sb[lane];
+  __syncthreads();
+  float v[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = gx[k * 64 + lane];
+  float acc = 0.f;
+  float4 sink = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = 0; i < kLen / 16; ++i) {
+    float4 d[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) d[u] = sb[((i * 4 + u) & 127) + (lane & 1) * 0];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc = acc + v[k];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      sink.x = fmaxf(sink.x, d[u].x);
+    }
+  }
+  if (lane < 2) out[2 * blockIdx.x + lane] = acc + (sink.x > 1e30f ? 1.f : 0.f);
+}
+// the chain reads operands that came from LDS 64 elements earlier (a 256-element register
+// window per lane, refilled 64 elements at a time by ds_read_b128, two lanes active)
+__global__ __launch_bounds__(64) void k_lds_window(const float* gx, const float* gy, float* out) {
+  __shared__ float sbuf[2][1024];
+  const int lane = threadIdx.x, r = blockIdx.x;
+  const int b = r * kLen;
+  const int full = (kLen / 1024) * 1024;
+  float acc = 0.f;
+  for (int c0 = 0; c0 < full; c0 += 1024) {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      sbuf[0][t * 64 + lane] = gx[b + c0 + t * 64 + lane];
+      sbuf[1][t * 64 + lane] = gy[b + c0 + t * 64 + lane];
+    }
+    __syncthreads();
+    const float4* s4 = reinterpret_cast<const float4*>(sbuf[lane & 1]);
+    float4 wa[16], wb[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) wa[u] = s4[u];
+#pragma unroll
+    for (int blk = 0; blk < 16; blk += 2) {
+      if (blk + 1 < 16) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) wb[u] = s4[(blk + 1) * 16 + u];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        acc = (c0 == 0 && blk == 0 && u == 0) ? wa[0].x : acc + wa[u].x;
+        acc = acc + wa[u].y;
+        acc = acc + wa[u].z;
+        acc = acc + wa[u].w;
+      }
+      if (blk + 2 < 16) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) wa[u] = s4[(blk + 2) * 16 + u];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        acc = acc + wb[u].x;
+        acc = acc + wb[u].y;
+        acc = acc + wb[u].z;
+        acc = acc + wb[u].w;
+      }
+    }
+    __syncthreads();
+  }
+  if (lane < 2) out[2 * r + lane] = acc;
+}
+// ldswin + the next chunk's global loads in registers during the chain (as seq_sum), two lanes
+// x / y, exact first element: the candidate production form
+template <int kW>
+__global__ __launch_bounds__(64) void k_lds_window2(const float* gx, const float* gy, float* out) {
+  constexpr int kNw = 256 / kW;
+  __shared__ float sbuf[2][1024];
+  const int lane = threadIdx.x, r = blockIdx.x;
+  const int b = r * kLen, e = (r + 1) * kLen;
+  float pre[16], prey[16];
+  auto load_chunk = [&](int c0) {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int idx = c0 + t * 64 + lane;
+      pre[t] = (idx < e) ? gx[idx] : 0.f;
+      prey[t] = (idx < e) ? gy[idx] : 0.f;
+    }
+  };
+  load_chunk(b);
+  float acc = 0.f;
+  const float4* s4 = reinterpret_cast<const float4*>(sbuf[lane & 1]);
+  for (int c0 = b; c0 < e; c0 += 1024) {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      sbuf[0][t * 64 + lane] = pre[t];
+      sbuf[1][t * 64 + lane] = prey[t];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (c0 + 1024 < e) load_chunk(c0 + 1024);
+    const int m = (e - c0 < 1024) ? (e - c0) : 1024;
+    if (m == 1024) {
+      float4 wa[kW], wb[kW];
+#pragma unroll
+      for (int u = 0; u < kW; ++u) wa[u] = s4[u];
+#pragma unroll
+      for (int blk = 0; blk < kNw; blk += 2) {
+#pragma unroll
+        for (int u = 0; u < kW; ++u) wb[u] = s4[(blk + 1) * kW + u];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < kW; ++u) {
+          acc = (c0 == b && blk == 0 && u == 0) ? wa[0].x : acc + wa[u].x;
+          acc = acc + wa[u].y;
+          acc = acc + wa[u].z;
+          acc = acc + wa[u].w;
+        }
+        if (blk + 2 < kNw) {
+#pragma unroll
+          for (int u = 0; u < kW; ++u) wa[u] = s4[(blk + 2) * kW + u];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < kW; ++u) {
+          acc = acc + wb[u].x;
+          acc = acc + wb[u].y;
+          acc = acc + wb[u].z;
+          acc = acc + wb[u].w;
+        }
+      }
+    } else {
+      const float* s1 = sbuf[lane & 1];
+      for (int i = 0; i < m; ++i) acc = (c0 == b && i == 0) ? s1[0] : acc + s1[i];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (lane < 2) out[2 * r + lane] = acc;
+}
+// DPP row_share: the x run's 1024-element chunk in 64 registers of row 0 (lane i of register k
+// = element 16 k + i), the y run's in row 1; ONE v_add_f32 per element whose data operand is
+// read from lane N of the row by the DPP row_share:N modifier (gfx90a+), the accumulator a plain
+// operand (no DPP on the dependent value, so no DPP wait states).  No LDS; the next chunk's 64
+// registers are loaded (coalesced, 64 B per row) while this chunk is summed.
+template <int N>
+__device__ __forceinline__ float row_share(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                               0x150 + N, 0xF, 0xF, false));
+}
+template <int N>
+__device__ __forceinline__ void share_step(float& acc, float v) {
+  acc = acc + row_share<N>(v);
+}
+__device__ __forceinline__ void share16(float& acc, float v) {
+  share_step<0>(acc, v); share_step<1>(acc, v); share_step<2>(acc, v); share_step<3>(acc, v);
+  share_step<4>(acc, v); share_step<5>(acc, v); share_step<6>(acc, v); share_step<7>(acc, v);
+  share_step<8>(acc, v); share_step<9>(acc, v); share_step<10>(acc, v); share_step<11>(acc, v);
+  share_step<12>(acc, v); share_step<13>(acc, v); share_step<14>(acc, v); share_step<15>(acc, v);
+}
+__global__ __launch_bounds__(64) void k_share(const float* gx, const float* gy, float* out) {
+  const int lane = threadIdx.x, r = blockIdx.x;
+  const int i = lane & 15;
+  const float* src = ((lane >> 4) & 1) ? gy : gx;
+  const int b = r * kLen, e = b + kWalkFull;
+  float va[64], vb[64];
+  auto load = [&](float (&v)[64], int c0) {
+#pragma unroll
+    for (int k = 0; k < 64; ++k) v[k] = src[min(c0 + 16 * k + i, e - 1)];
+  };
+  auto sum = [&](const float (&v)[64], float acc, bool first) {
+    if (first) {
+      acc = row_share<0>(v[0]);
+      share_step<1>(acc, v[0]); share_step<2>(acc, v[0]); share_step<3>(acc, v[0]);
+      share_step<4>(acc, v[0]); share_step<5>(acc, v[0]); share_step<6>(acc, v[0]);
+      share_step<7>(acc, v[0]); share_step<8>(acc, v[0]); share_step<9>(acc, v[0]);
+      share_step<10>(acc, v[0]); share_step<11>(acc, v[0]); share_step<12>(acc, v[0]);
+      share_step<13>(acc, v[0]); share_step<14>(acc, v[0]); share_step<15>(acc, v[0]);
+    } else {
+      share16(acc, v[0]);
+    }
+#pragma unroll
+    for (int k = 1; k < 64; ++k) share16(acc, v[k]);
+    return acc;
+  };
+  load(va, b);
+  float acc = 0.f;
+  bool first = true;
+  for (int c0 = b; c0 < e; c0 += 2048) {
+    load(vb, c0 + 1024);
+    acc = sum(va, acc, first);
+    first = false;
+    if (c0 + 1024 >= e) break;
+    load(va, c0 + 2048);
+    acc = sum(vb, acc, false);
+  }
+  if (lane == 0) out[2 * r] = acc;
+  if (lane == 16) out[2 * r + 1] = acc;
+}
 }  // namespace
 
 int main() {
@@ -239,7 +446,52 @@ int main() {
     printf("%-10s %8.1f us  %.3f ns/elem  %.2f cycles/elem at 2.4 GHz  mismatches %d (x0 %g vs %g)\n",
            "walk", ms * 1e3, ms * 1e6 / kWalkFull, ms * 1e6 / kWalkFull * 2.4, bad, h[0], wref[0]);
   }
+  {
+    auto timeit = [&](const char* name, auto launch) {
+      launch();
+      (void)hipDeviceSynchronize();
+      (void)hipEventRecord(e0);
+      launch();
+      (void)hipEventRecord(e1);
+      (void)hipEventSynchronize(e1);
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      printf("%-10s %8.1f us  %.2f cycles/elem at 2.4 GHz\n", name, ms * 1e3,
+             ms * 1e6 / kLen * 2.4);
+    };
+    timeit("regs+lds", [&] { hipLaunchKernelGGL(k_regs_lds, kRuns, 64, 0, 0, gx, o2); });
+    timeit("ldswin", [&] { hipLaunchKernelGGL(k_lds_window, kRuns, 64, 0, 0, gx, gy, o2); });
+  }
+  {
+    std::vector<float> wref(2 * kRuns);
+    for (int r = 0; r < kRuns; ++r) {
+      float ax = hx[(size_t)r * kLen], ay = hy[(size_t)r * kLen];
+      for (int i = 1; i < kWalkFull; ++i) {
+        ax = ax + hx[(size_t)r * kLen + i];
+        ay = ay + hy[(size_t)r * kLen + i];
+      }
+      wref[2 * r] = ax;
+      wref[2 * r + 1] = ay;
+    }
+    hipLaunchKernelGGL(k_share, kRuns, 64, 0, 0, gx, gy, o2);
+    (void)hipDeviceSynchronize();
+    (void)hipEventRecord(e0);
+    hipLaunchKernelGGL(k_share, kRuns, 64, 0, 0, gx, gy, o2);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    std::vector<float> h(2 * kRuns);
+    (void)hipMemcpy(h.data(), o2, kRuns * 8, hipMemcpyDeviceToHost);
+    int bad = 0;
+    for (int q = 0; q < 2 * kRuns; ++q) bad += (h[q] != wref[q]);
+    printf("%-10s %8.1f us  %.2f cycles/elem at 2.4 GHz  mismatches %d\n", "share",
+           ms * 1e3, ms * 1e6 / kWalkFull * 2.4, bad);
+  }
   run("prod", [&] { hipLaunchKernelGGL(k_prod, kRuns, 64, 0, 0, gx, gy, o1); }, o1);
+  run("ldswin2-16", [&] { hipLaunchKernelGGL(k_lds_window2<16>, kRuns, 64, 0, 0, gx, gy, o2); }, o2);
+  run("ldswin2-8", [&] { hipLaunchKernelGGL(k_lds_window2<8>, kRuns, 64, 0, 0, gx, gy, o2); }, o2);
+  run("ldswin2-32", [&] { hipLaunchKernelGGL(k_lds_window2<32>, kRuns, 64, 0, 0, gx, gy, o2); }, o2);
   run("exec2-d1", [&] { hipLaunchKernelGGL(k_exec2<1>, kRuns, 64, 0, 0, gx, gy, o2); }, o2);
   run("exec2-d2", [&] { hipLaunchKernelGGL(k_exec2<2>, kRuns, 64, 0, 0, gx, gy, o2); }, o2);
   run("exec2-d4", [&] { hipLaunchKernelGGL(k_exec2<4>, kRuns, 64, 0, 0, gx, gy, o2); }, o2);
