@@ -645,16 +645,17 @@ __device__ int fs_insert(FsLds& L, int v) {
   return -1;
 }
 
-__device__ __forceinline__ int fs_find(const FsLds& L, int v) {
+__device__ __forceinline__ int fs_find_keys(const int* keys, int v) {
   uint32_t s = fs_hash(v);
   for (int probe = 0; probe < kFsSlots; ++probe) {
-    const int k = L.keys[s];
+    const int k = keys[s];
     if (k == v) return (int)s;
     if (k == -1) return -1;
     s = (s + 1) & (kFsSlots - 1);
   }
   return -1;
 }
+__device__ __forceinline__ int fs_find(const FsLds& L, int v) { return fs_find_keys(L.keys, v); }
 
 // Lanes with equal keys in this 64-point step: the lowest such lane (leader), the lane's rank
 // among them and their number.  One ballot per distinct key, scalar loop.
@@ -865,6 +866,328 @@ __global__ __launch_bounds__(kFsWaves * 64) void k_frame_sort(
   }
 }
 
+// ---- the per-frame counting sort with C blocks per frame (frames of hundreds of thousands of
+// points: one block per frame left most CUs idle for the whole sort -- the dense share's 125
+// frames on 256 CUs).  Chunk c of frame f is its points [lo + len*c/C, lo + len*(c+1)/C), each
+// chunk's waves own contiguous parts of it exactly as k_frame_sort's waves own the frame's:
+//   k_fsc_count   per chunk: k_frame_sort's pass 1; its labels (slot order) with their per-wave
+//                 counts -> the chunk's entry list, and its first noise point
+//   k_fsc_merge   per frame: the chunks' labels in one LDS hash, the run offsets and segment
+//                 lists exactly as k_frame_sort, then per chunk IN ORDER each entry's base =
+//                 its run's start + the counts of the earlier chunks (stable across chunks)
+//   k_fsc_scatter per chunk: per-wave cursors from the bases and the per-wave counts, then
+//                 k_frame_sort's pass 2.
+constexpr int kFsCap = kFsMaxKeys;  // entries per chunk list (more labels: overflow -> radix)
+
+__device__ __forceinline__ void fsc_chunk(const int32_t* __restrict__ pf, int64_t n, int C,
+                                          int b, int& f, int& lo, int& clo, int& chi) {
+  f = b / C;
+  const int c = b - f * C;
+  lo = __builtin_amdgcn_readfirstlane((int)lower_bound_i32(pf, n, f));
+  const int hi = __builtin_amdgcn_readfirstlane((int)lower_bound_i32(pf, n, f + 1));
+  const int64_t len = hi - lo;
+  clo = lo + (int)(len * c / C);
+  chi = lo + (int)(len * (c + 1) / C);
+}
+
+__global__ __launch_bounds__(kFsWaves * 64) void k_fsc_count(
+    const int32_t* __restrict__ labels, const int32_t* __restrict__ pf, int64_t n, int C,
+    int32_t* __restrict__ ent_key, uint32_t* __restrict__ ent_cnt, int32_t* __restrict__ nent,
+    int32_t* __restrict__ fnoise_c, int32_t* __restrict__ overflow) {
+  __shared__ FsLds L;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int f, lo, clo, chi;
+  fsc_chunk(pf, n, C, blockIdx.x, f, lo, clo, chi);
+  for (int s = tid; s < kFsSlots; s += kFsWaves * 64) {
+    L.keys[s] = -1;
+#pragma unroll
+    for (int q = 0; q < kFsWaves; ++q) L.cnt[q][s] = 0u;
+  }
+  if (tid == 0) {
+    L.nkeys = 0;
+    L.overflow = 0;
+  }
+  __syncthreads();
+  const int nch = (chi - clo + 63) / 64, cpw = (nch + kFsWaves - 1) / kFsWaves;
+  const int cb0 = w * cpw, cb1 = min(nch, cb0 + cpw);
+  int wfn = INT_MAX;
+  constexpr int U1 = 8;
+  for (int cb = cb0; cb < cb1; cb += U1) {
+    int lab[U1];
+#pragma unroll
+    for (int u = 0; u < U1; ++u) {
+      const int i = clo + (cb + u) * 64 + lane;
+      lab[u] = (cb + u < cb1 && i < chi) ? labels[i] : -2;
+    }
+#pragma unroll
+    for (int u = 0; u < U1; ++u) {
+      const int v = lab[u] + 1;
+      if (wfn == INT_MAX) {
+        const uint64_t m0 = __ballot(v == 0);
+        if (m0) wfn = clo + (cb + u) * 64 + __builtin_ctzll(m0);
+      }
+      const bool valid = v >= 1;
+      int leader, rank, cm;
+      wave_group(v, valid, lane, leader, rank, cm);
+      if (valid && lane == leader) {
+        const int s = fs_insert(L, v);
+        if (s >= 0) L.cnt[w][s] += (uint32_t)cm;
+      }
+    }
+  }
+  if (lane == 0) L.fnoise[w] = wfn;
+  __syncthreads();
+  if (L.overflow) {
+    if (tid == 0) {
+      nent[blockIdx.x] = 0;
+      atomicExch(overflow, 1);
+    }
+    return;
+  }
+  if (tid == 0) {
+    int m = INT_MAX;
+#pragma unroll
+    for (int q = 0; q < kFsWaves; ++q) m = min(m, L.fnoise[q]);
+    fnoise_c[blockIdx.x] = m;
+  }
+  // the occupied slots in slot order -> entries 0 .. K-1
+  uint32_t pcount = 0u;
+#pragma unroll
+  for (int j = 0; j < kFsSpt; ++j) pcount += (L.keys[kFsSpt * tid + j] != -1) ? 1u : 0u;
+  const uint32_t ip = wave_incl_scan(pcount, lane);
+  if (lane == 63) L.wsum[1][w] = ip;
+  __syncthreads();
+  uint32_t pp = 0, tp = 0;
+#pragma unroll
+  for (int q = 0; q < kFsWaves; ++q) {
+    if (q < w) pp += L.wsum[1][q];
+    tp += L.wsum[1][q];
+  }
+  uint32_t k = pp + ip - pcount;
+  const int64_t e0 = (int64_t)blockIdx.x * kFsCap;
+#pragma unroll
+  for (int j = 0; j < kFsSpt; ++j) {
+    const int sj = kFsSpt * tid + j;
+    if (L.keys[sj] != -1) {
+      ent_key[e0 + k] = L.keys[sj];
+#pragma unroll
+      for (int q = 0; q < kFsWaves; ++q) ent_cnt[(e0 + k) * kFsWaves + q] = L.cnt[q][sj];
+      ++k;
+    }
+  }
+  if (tid == 0) nent[blockIdx.x] = (int32_t)tp;
+}
+
+struct FscLds {
+  int keys[kFsSlots];
+  uint32_t tot[kFsSlots];
+  int off[kFsSlots];
+  uint32_t run[kFsSlots];
+  uint32_t wsum[2][kFsWaves];
+  int nkeys, overflow;
+};
+
+__device__ int fsc_insert(FscLds& L, int v) {
+  uint32_t s = fs_hash(v);
+  for (int probe = 0; probe < kFsSlots; ++probe) {
+    const int k = __atomic_load_n(&L.keys[s], __ATOMIC_RELAXED);
+    if (k == v) return (int)s;
+    if (k == -1) {
+      const int old = atomicCAS(&L.keys[s], -1, v);
+      if (old == -1) {
+        if (atomicAdd(&L.nkeys, 1) >= kFsMaxKeys) L.overflow = 1;
+        return (int)s;
+      }
+      if (old == v) return (int)s;
+    }
+    s = (s + 1) & (kFsSlots - 1);
+  }
+  L.overflow = 1;
+  return -1;
+}
+
+__global__ __launch_bounds__(kFsWaves * 64) void k_fsc_merge(
+    const int32_t* __restrict__ pf, int64_t n, int C, const int32_t* __restrict__ ent_key,
+    const uint32_t* __restrict__ ent_cnt, const int32_t* __restrict__ nent,
+    const int32_t* __restrict__ fnoise_c, int32_t* __restrict__ ent_base,
+    int32_t* __restrict__ ent_run, int32_t* __restrict__ fstart,
+    int32_t* __restrict__ tmp_start, int32_t* __restrict__ tmp_len,
+    int32_t* __restrict__ tmp_label, int32_t* __restrict__ nseg_f,
+    int64_t* __restrict__ first_noise, int32_t* __restrict__ overflow) {
+  __shared__ FscLds L;
+  const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lo = __builtin_amdgcn_readfirstlane((int)lower_bound_i32(pf, n, f));
+  for (int s = tid; s < kFsSlots; s += kFsWaves * 64) {
+    L.keys[s] = -1;
+    L.tot[s] = 0u;
+  }
+  if (tid == 0) {
+    L.nkeys = 0;
+    L.overflow = 0;
+    fstart[f] = lo;
+  }
+  __syncthreads();
+  if (*overflow) {  // a chunk overflowed: K9 is redone on the radix path
+    if (tid == 0) nseg_f[f] = 0;
+    return;
+  }
+  auto entry_total = [&](int64_t e) {
+    uint32_t t = 0u;
+#pragma unroll
+    for (int q = 0; q < kFsWaves; ++q) t += ent_cnt[e * kFsWaves + q];
+    return t;
+  };
+  for (int c = 0; c < C; ++c) {
+    const int b = f * C + c, m = nent[b];
+    for (int k = tid; k < m; k += kFsWaves * 64) {
+      const int64_t e = (int64_t)b * kFsCap + k;
+      const int s = fsc_insert(L, ent_key[e]);
+      if (s >= 0) atomicAdd(&L.tot[s], entry_total(e));
+    }
+  }
+  __syncthreads();
+  if (L.overflow) {
+    if (tid == 0) {
+      nseg_f[f] = 0;
+      atomicExch(overflow, 1);
+    }
+    return;
+  }
+  if (tid == 0 && first_noise) {
+    int m = INT_MAX;
+    for (int c = 0; c < C; ++c) m = min(m, fnoise_c[f * C + c]);
+    if (m != INT_MAX) first_noise[f] = m;
+  }
+  // run offsets and the frame's segment list, in slot order (as k_frame_sort)
+  uint32_t tt[kFsSpt];
+  uint32_t a = 0u, pcount = 0u;
+#pragma unroll
+  for (int j = 0; j < kFsSpt; ++j) {
+    const uint32_t t = L.tot[kFsSpt * tid + j];
+    tt[j] = t;
+    a += t;
+    pcount += (t != 0u);
+  }
+  const uint32_t ia = wave_incl_scan(a, lane), ip = wave_incl_scan(pcount, lane);
+  if (lane == 63) {
+    L.wsum[0][w] = ia;
+    L.wsum[1][w] = ip;
+  }
+  __syncthreads();
+  uint32_t pa = 0, pp = 0, tp = 0;
+#pragma unroll
+  for (int q = 0; q < kFsWaves; ++q) {
+    if (q < w) {
+      pa += L.wsum[0][q];
+      pp += L.wsum[1][q];
+    }
+    tp += L.wsum[1][q];
+  }
+  {
+    uint32_t o = pa + ia - a, q = pp + ip - pcount;
+#pragma unroll
+    for (int j = 0; j < kFsSpt; ++j) {
+      const int sj = kFsSpt * tid + j;
+      if (tt[j] != 0u) {
+        L.off[sj] = (int)o;
+        L.run[sj] = o;
+        tmp_start[lo + q] = lo + (int)o;
+        tmp_len[lo + q] = (int)tt[j];
+        tmp_label[lo + q] = L.keys[sj] - 1;
+      }
+      o += tt[j];
+      q += (tt[j] != 0u);
+    }
+  }
+  if (tid == 0) nseg_f[f] = (int)tp;
+  __syncthreads();
+  // each chunk's entry base: its run's start plus the earlier chunks' counts of the label (a
+  // chunk's entries hold distinct labels, so its threads never share a slot)
+  for (int c = 0; c < C; ++c) {
+    const int b = f * C + c, m = nent[b];
+    for (int k = tid; k < m; k += kFsWaves * 64) {
+      const int64_t e = (int64_t)b * kFsCap + k;
+      const int s = fs_find_keys(L.keys, ent_key[e]);
+      ent_base[e] = (int)L.run[s];
+      ent_run[e] = L.off[s];
+      L.run[s] += entry_total(e);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kFsWaves * 64) void k_fsc_scatter(
+    const int32_t* __restrict__ labels, const int32_t* __restrict__ pf, int64_t n, int C,
+    const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ inten,
+    float* __restrict__ gx, float* __restrict__ gy, float* __restrict__ gi,
+    int32_t* __restrict__ tmp_first, const int32_t* __restrict__ ent_key,
+    const uint32_t* __restrict__ ent_cnt, const int32_t* __restrict__ nent,
+    const int32_t* __restrict__ ent_base, const int32_t* __restrict__ ent_run,
+    const int32_t* __restrict__ overflow) {
+  __shared__ FsLds L;
+  if (*overflow) return;  // (block-uniform)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int f, lo, clo, chi;
+  fsc_chunk(pf, n, C, blockIdx.x, f, lo, clo, chi);
+  for (int s = tid; s < kFsSlots; s += kFsWaves * 64) L.keys[s] = -1;
+  if (tid == 0) {
+    L.nkeys = 0;
+    L.overflow = 0;
+  }
+  __syncthreads();
+  const int m = nent[blockIdx.x];
+  for (int k = tid; k < m; k += kFsWaves * 64) {
+    const int64_t e = (int64_t)blockIdx.x * kFsCap + k;
+    const int s = fs_insert(L, ent_key[e]);
+    uint32_t run = (uint32_t)ent_base[e];
+#pragma unroll
+    for (int q = 0; q < kFsWaves; ++q) {
+      L.cnt[q][s] = run;
+      run += ent_cnt[e * kFsWaves + q];
+    }
+    L.off[s] = ent_run[e];
+  }
+  __syncthreads();
+  const int nch = (chi - clo + 63) / 64, cpw = (nch + kFsWaves - 1) / kFsWaves;
+  const int cb0 = w * cpw, cb1 = min(nch, cb0 + cpw);
+  constexpr int U2 = 4;
+  for (int cb = cb0; cb < cb1; cb += U2) {
+    int lab[U2];
+    float px[U2], py[U2], pv[U2];
+#pragma unroll
+    for (int u = 0; u < U2; ++u) {
+      const int i = clo + (cb + u) * 64 + lane;
+      const bool in = cb + u < cb1 && i < chi;
+      lab[u] = in ? labels[i] : -2;
+      px[u] = in ? x[i] : 0.f;
+      py[u] = in ? y[i] : 0.f;
+      pv[u] = in ? inten[i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U2; ++u) {
+      const int i = clo + (cb + u) * 64 + lane;
+      const int v = lab[u] + 1;
+      const bool valid = v >= 1;
+      int leader, rank, cm;
+      wave_group(v, valid, lane, leader, rank, cm);
+      int base = 0;
+      if (valid && lane == leader) {
+        const int s = fs_find(L, v);
+        base = (int)L.cnt[w][s];
+        L.cnt[w][s] = (uint32_t)(base + cm);
+        if (base == L.off[s]) tmp_first[lo + base] = i;
+      }
+      base = __shfl(base, leader < 0 ? lane : leader);
+      if (valid) {
+        const int p = lo + base + rank;
+        gx[p] = px[u];
+        gy[p] = py[u];
+        gi[p] = pv[u];
+      }
+    }
+  }
+}
+
 __global__ void k_seg_total_fix(const int32_t* __restrict__ overflow, int32_t* __restrict__ total) {
   if (threadIdx.x == 0 && *overflow) *total = -1;
 }
@@ -935,12 +1258,25 @@ static int32_t summaries_impl(const int32_t* labels, const float* x, const float
                           n / n_frames <= (int64_t(1) << 20);
   if (radix_used) *radix_used = !frame_sort;
   if (frame_sort) {
+    // blocks per frame: one up to 64 k points per frame on average, else ~64 k points each (at
+    // most 16): the dense share's 490 k-point frames take 8
+    const int64_t ppf = n / std::max<int32_t>(n_frames, 1);
+    const int C = (int)std::min<int64_t>(16, std::max<int64_t>(1, (ppf + 65535) / 65536));
+    const int64_t NC = (int64_t)n_frames * C;
     Budget b;
     for (int k = 0; k < 3; ++k) b.add<float>(n + 1);
     for (int k = 0; k < 4; ++k) b.add<int32_t>(n + 1);
     b.add<int64_t>(n + 1);
     for (int k = 0; k < 3; ++k) b.add<int32_t>((int64_t)n_frames + 1);
     b.add<int32_t>(2);
+    if (C > 1) {
+      b.add<int32_t>(NC * kFsCap);
+      b.add<uint32_t>(NC * kFsCap * kFsWaves);
+      b.add<int32_t>(NC * kFsCap);
+      b.add<int32_t>(NC * kFsCap);
+      b.add<int32_t>(NC);
+      b.add<int32_t>(NC);
+    }
     RPT_TRY(sc.reserve(b.bytes, st));
     float* gx = sc.carve_n<float>(n + 1);
     float* gy = sc.carve_n<float>(n + 1);
@@ -954,10 +1290,32 @@ static int32_t summaries_impl(const int32_t* labels, const float* x, const float
     int32_t* nseg_f = sc.carve_n<int32_t>((int64_t)n_frames + 1);
     int32_t* base = sc.carve_n<int32_t>((int64_t)n_frames + 1);
     int32_t* ovf = sc.carve_n<int32_t>(2);  // [overflow flag, long-run count]
+    int32_t *ent_key = nullptr, *nent = nullptr, *fnoise_c = nullptr, *ent_base = nullptr,
+            *ent_run = nullptr;
+    uint32_t* ent_cnt = nullptr;
+    if (C > 1) {
+      ent_key = sc.carve_n<int32_t>(NC * kFsCap);
+      ent_cnt = sc.carve_n<uint32_t>(NC * kFsCap * kFsWaves);
+      ent_base = sc.carve_n<int32_t>(NC * kFsCap);
+      ent_run = sc.carve_n<int32_t>(NC * kFsCap);
+      nent = sc.carve_n<int32_t>(NC);
+      fnoise_c = sc.carve_n<int32_t>(NC);
+    }
     RPT_HIP(hipMemsetAsync(ovf, 0, 2 * sizeof(int32_t), st));
-    hipLaunchKernelGGL(k_frame_sort, dim3(n_frames), dim3(kFsWaves * 64), 0, st, labels, pf, n,
-                       x, y, inten, gx, gy, gi, fstart, tstart, tlen, tlabel, tfirst, nseg_f,
-                       frame_first_noise, ovf);
+    if (C == 1) {
+      hipLaunchKernelGGL(k_frame_sort, dim3(n_frames), dim3(kFsWaves * 64), 0, st, labels, pf, n,
+                         x, y, inten, gx, gy, gi, fstart, tstart, tlen, tlabel, tfirst, nseg_f,
+                         frame_first_noise, ovf);
+    } else {
+      hipLaunchKernelGGL(k_fsc_count, dim3((unsigned)NC), dim3(kFsWaves * 64), 0, st, labels, pf,
+                         n, C, ent_key, ent_cnt, nent, fnoise_c, ovf);
+      hipLaunchKernelGGL(k_fsc_merge, dim3(n_frames), dim3(kFsWaves * 64), 0, st, pf, n, C,
+                         ent_key, ent_cnt, nent, fnoise_c, ent_base, ent_run, fstart, tstart,
+                         tlen, tlabel, nseg_f, frame_first_noise, ovf);
+      hipLaunchKernelGGL(k_fsc_scatter, dim3((unsigned)NC), dim3(kFsWaves * 64), 0, st, labels,
+                         pf, n, C, x, y, inten, gx, gy, gi, tfirst, ent_key, ent_cnt, nent,
+                         ent_base, ent_run, ovf);
+    }
     RPT_CHECK_LAUNCH();
     RPT_TRY(exclusive_scan_total_i32(nseg_f, base, n_frames, st));
     hipLaunchKernelGGL(k_seg_compact, dim3(grid_for(n_frames, 4, 1024)), dim3(256), 0, st,

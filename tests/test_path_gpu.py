@@ -358,6 +358,53 @@ def _radix_summaries_in_child(frames, lab, ncl):
 
 
 @pytest.mark.parametrize("crowded", [False, True])
+def test_summaries_chunked_frame_sort_matches_radix_path(gpu, crowded):
+    """Frames of hundreds of thousands of points (the dense share's shape) take the frame sort
+    with several blocks per frame (k_fsc_count / k_fsc_merge / k_fsc_scatter: a run spans
+    chunks, each chunk's part placed after the earlier chunks'): the same segments, first
+    points, counts and float32 centroids as the radix path and numpy, runs interleaved point by
+    point across chunk boundaries, an empty frame, a giant run per frame; `crowded` puts more
+    labels in one frame than the frame sort takes (redone on the radix path)."""
+    rng = np.random.default_rng(33)
+    sizes = [300000, 0, 250000, 180000, 70000, 3]
+    frames, labs = [], []
+    for k, m in enumerate(sizes):
+        p = np.column_stack([rng.normal(0, 50, m), rng.normal(0, 50, m),
+                             rng.integers(0, 255, m)]).astype(np.float32)
+        lab = rng.integers(-1, 12 + 3 * k, m).astype(np.int32)
+        lab[rng.random(m) < 0.7] = 5 + k  # one giant run per frame
+        if crowded and k == 3:
+            lab = rng.integers(-1, 4000, m).astype(np.int32)
+        frames.append((k, p, None))
+        labs.append(lab)
+    lab = np.concatenate(labs)
+    ncl = int(lab.max()) + 1
+    a = _summaries_device(gpu, frames, lab, ncl)
+    b = _radix_summaries_in_child(frames, lab, ncl)
+    ka = np.lexsort((a[0]["label"], a[0]["frame"]))
+    kb = np.lexsort((b[0]["label"], b[0]["frame"]))
+    assert np.all(np.diff(a[0]["frame"]) >= 0) != crowded  # frame-major unless redone
+    for key in a[0]:
+        np.testing.assert_array_equal(a[0][key][ka], b[0][key][kb], err_msg=key)
+    np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(a[0]["label"][a[2]], b[0]["label"][b[2]])
+    pf = np.concatenate([np.full(m, k, np.int32) for k, m in enumerate(sizes)])
+    pts = np.vstack([p for _, p, _ in frames])
+    order = np.lexsort((np.arange(len(lab)), lab, pf))  # (frame, label) runs in index order
+    key = pf.astype(np.int64)[order] * (ncl + 2) + lab[order] + 1
+    heads = np.flatnonzero(np.r_[True, key[1:] != key[:-1]])
+    ends = np.r_[heads[1:], len(key)]
+    runs = {(int(pf[order[h]]), int(lab[order[h]])): order[h:e] for h, e in zip(heads, ends)
+            if lab[order[h]] >= 0}
+    assert len(runs) == len(a[0]["label"])
+    for s in range(len(a[0]["label"])):
+        idx = runs[(int(a[0]["frame"][s]), int(a[0]["label"][s]))]
+        assert a[0]["count"][s] == len(idx) and a[0]["first"][s] == idx[0]
+        c = np.mean(pts[idx][:, :2], axis=0)
+        assert a[0]["cx"][s] == c[0] and a[0]["cy"][s] == c[1]
+
+
+@pytest.mark.parametrize("crowded", [False, True])
 def test_summaries_frame_sort_matches_radix_path(gpu, crowded):
     """K9's per-frame counting sort and its radix path (RPT_K9_RADIX=1, in a child process) give
     the same segments — frame-major vs label-major — on frames of ragged sizes, empty frames,
