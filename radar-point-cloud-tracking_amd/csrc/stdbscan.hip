@@ -1885,7 +1885,9 @@ __global__ __launch_bounds__(kBlock) void k_core_fill(const int32_t* __restrict_
 // Level 4, one wave per queued point: lanes classify up to 64 candidate cells at a time against
 // the cells' boxes (whole-cell accept adds the cell's count), then every undecided cell's points
 // are tested 64 at a time; the wave stops as soon as min_samples neighbours are seen.
-template <int D>
+template <int D, int KR = kR>
+// KR: candidate positions per lane per super-round (2 when the exact integral-time window of
+// (2 rt + 1) x 25 positions fits 128: the other two rounds only masked positions off)
 // 8 waves/SIMD (64 VGPRs, one spill; 72 gave 7): -3 % on the latency-bound queue pass
 __global__ __launch_bounds__(kBlock, 8) void k_core_slow(const float4* __restrict__ pts,
                                                      const int32_t* __restrict__ skey, Geom g,
@@ -1924,21 +1926,21 @@ __global__ __launch_bounds__(kBlock, 8) void k_core_slow(const float4* __restric
       w = make_window<D, false>(cx, cy, cz, p.w, p.w, g, slab_t);
     }
     int cnt = 0;
-    // super-rounds of kR candidates per lane: every lane's bitmap words, then records, are
-    // loaded together (one dependent level each for up to 64*kR candidates)
-    for (int base = 0; base < w.total && cnt < need; base += 64 * kR) {
-      int64_t c[kR];
-      uint32_t wb[kR];
+    // super-rounds of KR candidates per lane: every lane's bitmap words, then records, are
+    // loaded together (one dependent level each for up to 64*KR candidates)
+    for (int base = 0; base < w.total && cnt < need; base += 64 * KR) {
+      int64_t c[KR];
+      uint32_t wb[KR];
 #pragma unroll
-      for (int r = 0; r < kR; ++r) {
+      for (int r = 0; r < KR; ++r) {
         const int qq = base + r * 64 + lane;
         c[r] = (qq < w.total) ? window_cell<D>(w, qq, g, slab_t, p.w, p.w) : -1;
       }
 #pragma unroll
-      for (int r = 0; r < kR; ++r) wb[r] = (c[r] >= 0) ? occ_bits[c[r] >> 5] : 0u;
-      int b[kR], e[kR], cls[kR];
+      for (int r = 0; r < KR; ++r) wb[r] = (c[r] >= 0) ? occ_bits[c[r] >> 5] : 0u;
+      int b[KR], e[KR], cls[KR];
 #pragma unroll
-      for (int r = 0; r < kR; ++r) {
+      for (int r = 0; r < KR; ++r) {
         b[r] = e[r] = cls[r] = 0;
         if (c[r] >= 0 && ((wb[r] >> (c[r] & 31)) & 1u)) {
           const CellRec<D> cr = crec[c[r]];
@@ -1952,15 +1954,15 @@ __global__ __launch_bounds__(kBlock, 8) void k_core_slow(const float4* __restric
       // is decided without a pair test
       int add = 0, may = 0;
 #pragma unroll
-      for (int r = 0; r < kR; ++r) {
+      for (int r = 0; r < KR; ++r) {
         add += (cls[r] == 1) ? e[r] - b[r] : 0;
         may += (cls[r] == 2) ? e[r] - b[r] : 0;
       }
       cnt += wave_sum(add);
-      const bool last = base + 64 * kR >= w.total;
+      const bool last = base + 64 * KR >= w.total;
       if (last && cnt + wave_sum(may) < need) break;
 #pragma unroll
-      for (int r = 0; r < kR; ++r) {
+      for (int r = 0; r < KR; ++r) {
         uint64_t pm = __ballot(cls[r] == 2);
         while (pm && cnt < need) {
           const int l = __ffsll((unsigned long long)pm) - 1;
@@ -4631,8 +4633,12 @@ int32_t DbscanState::core_pass(hipStream_t st) {
     hipLaunchKernelGGL(k_core_cells_oct<true>, dim3((grid_for(8 * n, kBlock, 8192) + 7) & ~7),
                        dim3(kBlock), 0, st, g, (int)rs, occ, n_occ, rec<2>(), mutual, occ_bits,
                        slab_t, (int32_t*)nullptr, (int32_t*)nullptr, core, cm, slow, cq, n_slow);
-    hipLaunchKernelGGL(k_core_slow<2>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
-                       rec<2>(), occ_bits, slab_t, slow, n_slow, core, sorig, cm, cq);
+    if (g.rt >= 0 && (2 * g.rt + 1) * 25 <= 128)
+      hipLaunchKernelGGL((k_core_slow<2, 2>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey,
+                         g, rec<2>(), occ_bits, slab_t, slow, n_slow, core, sorig, cm, cq);
+    else
+      hipLaunchKernelGGL(k_core_slow<2>, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
+                         rec<2>(), occ_bits, slab_t, slow, n_slow, core, sorig, cm, cq);
     RPT_CHECK_LAUNCH();
     cmin_ready = true;
     tm.mark();
