@@ -24,6 +24,7 @@ so the ranks cooperate; the result is identical to a single-device run:
 from __future__ import annotations
 
 import contextlib
+import os
 import threading
 import time
 from concurrent.futures import Future, ThreadPoolExecutor
@@ -43,21 +44,25 @@ _MIN, _MAX, _SUM = dist.ReduceOp.MIN, dist.ReduceOp.MAX, dist.ReduceOp.SUM
 class Comm:
     """torch.distributed helpers; tensors are staged through host memory for gloo."""
 
-    def __init__(self, dev: torch.device, group=None):
+    def __init__(self, dev: torch.device, group=None, force_collectives: bool | None = None):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.dev = dev
         self.host = dist.get_backend(group) == "gloo"
         self.cdev = torch.device("cpu") if self.host else dev
+        if force_collectives is None:
+            force_collectives = os.environ.get("RPT_COMM_FORCE_COLLECTIVES", "0") == "1"
+        # solo: a one-member group's collectives are the identity (no device round trip).
+        # force_collectives (tests): run them through the backend anyway, so that on a one-GPU
+        # box the RCCL branch (device tensors, stream order, lanes) executes end to end
+        self.solo = self.world == 1 and not force_collectives
 
     def _c(self, t: torch.Tensor) -> torch.Tensor:
         return t.to(self.cdev).contiguous()
 
-    # a one-member group's collectives are the identity: no device round trip at world 1
-
     def all_reduce(self, t: torch.Tensor, op) -> torch.Tensor:
-        if self.world == 1:
+        if self.solo:
             return t
         c = self._c(t).clone()
         dist.all_reduce(c, op=op, group=self.group)
@@ -65,7 +70,7 @@ class Comm:
 
     def all_gather_fixed(self, t: torch.Tensor) -> torch.Tensor:
         """all_gather of a 1-D tensor of the same length on every rank -> [world][len] (host)."""
-        if self.world == 1:
+        if self.solo:
             return t.reshape(1, -1).cpu()
         c = self._c(t).reshape(-1)
         out = torch.empty(self.world * c.numel(), dtype=c.dtype, device=self.cdev)
@@ -75,7 +80,7 @@ class Comm:
     def all_gather_dev(self, t: torch.Tensor) -> torch.Tensor:
         """all_gather of a 1-D tensor of the same length on every rank -> [world * len] on the
         input's device (RCCL: stays in stream order, no host wait)."""
-        if self.world == 1:
+        if self.solo:
             return t.reshape(-1)
         c = self._c(t).reshape(-1)
         out = torch.empty(self.world * c.numel(), dtype=c.dtype, device=self.cdev)
@@ -84,7 +89,7 @@ class Comm:
 
     def all_gather_var(self, t: torch.Tensor) -> List[torch.Tensor]:
         """all_gather of 1-D tensors of different lengths (returned on the input's device)."""
-        if self.world == 1:
+        if self.solo:
             return [t.reshape(-1)]
         c = self._c(t).reshape(-1)
         n = torch.tensor([c.numel()], dtype=torch.int64, device=self.cdev)
@@ -104,7 +109,7 @@ class Comm:
         exact below 2^53), everyone reads the lengths from the same gathered block, and only when
         some length exceeds cap do all ranks (consistently) fall back to the two-round form.
         Returns (pieces on the input's device, longest length)."""
-        if self.world == 1:
+        if self.solo:
             t = t.reshape(-1)
             return [t], int(t.numel())
         c = self._c(t).reshape(-1)
@@ -390,7 +395,7 @@ class ShardedStackPipeline:
         rep = ops.remap(comp, base, keys, vals)
         # 7. global representatives and labels
         roots = ops.select_roots(rep, base, n_prev, n_prev + n_own)
-        all_roots = comm.all_gather_var(roots) if W > 1 else [roots]
+        all_roots = comm.all_gather_var(roots) if not comm.solo else [roots]
         reps_sorted = torch.cat([a.to(rep.device) for a in all_roots])
         labels_all = ops.dbscan_labels_global(rep, reps_sorted)
         labels = labels_all[n_prev:n_prev + n_own]
@@ -405,7 +410,7 @@ class ShardedStackPipeline:
             [S, frame0], built_local.astype(np.float64), [-1.0] * (F - len(built_local)),
             first_noise, seg["frame"], seg["label"], seg["count"], seg["first"], seg["cx"],
             seg["cy"], seg["mi"]]).astype(np.float64)
-        parts = comm.all_gather_var(torch.from_numpy(packed)) if W > 1 else \
+        parts = comm.all_gather_var(torch.from_numpy(packed)) if not comm.solo else \
             [torch.from_numpy(packed)]
         mark("summaries")
         res = ShardResult(n_points_local=n_local, n_points_global=n_global,
@@ -831,7 +836,7 @@ class NativeShardPipeline:
             return pb, cap
 
         def gather(t):
-            return comm.all_gather_dev(t) if W > 1 else t
+            return comm.all_gather_dev(t) if not comm.solo else t
 
         def finish_step(pb, gp, row, keys=None, vals=None, radix=False):
             cap_out = self._cap_out
@@ -999,7 +1004,7 @@ class ShardLanes:
         self.dev = dev
         comm = Comm(dev)
         self.world = comm.world
-        self.sequenced = comm.world > 1 if sequenced is None else bool(sequenced)
+        self.sequenced = not comm.solo if sequenced is None else bool(sequenced)
         self.pipes = [NativeShardPipeline(comm, gains, rows, bins, params, timing=timing,
                                           async_host=async_host, host_workers=host_workers)
                       for _ in range(lanes)]

@@ -37,7 +37,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n_frames, out_dir):
+def _worker(rank, world, port, n_frames, out_dir, force=False):
     import torch
     import torch.distributed as dist
 
@@ -53,7 +53,9 @@ def _worker(rank, world, port, n_frames, out_dir):
     F = n_frames // world
     echo = numpy_echo(cfg, geo, frames=range(rank * F, (rank + 1) * F))
     ops = CpuOps(cfg.scale, geo.cos_t, geo.sin_t)
-    pipe = ShardedStackPipeline(ops, Comm(torch.device("cpu")), cfg.gains, cfg.rows, cfg.bins,
+    comm = Comm(torch.device("cpu"), force_collectives=force)
+    assert comm.solo == (world == 1 and not force)
+    pipe = ShardedStackPipeline(ops, comm, cfg.gains, cfg.rows, cfg.bins,
                                 PathParams(eps_space=8.0, eps_time=2.0, min_samples=15))
     pipe.set_geometry(None, torch.tensor(list(cfg.gains) * F, dtype=torch.int32))
     res = pipe.run(torch.from_numpy(echo), 1, rank * F)
@@ -86,14 +88,15 @@ def _oracle(n_frames):
     return op.run_path(frames)
 
 
-@pytest.mark.parametrize("world,n_frames", [(2, 14), (3, 15)])
-def test_sharded_protocol_matches_single_process(world, n_frames):
+@pytest.mark.parametrize("world,n_frames,force", [(2, 14, False), (3, 15, False), (1, 6, True)])
+def test_sharded_protocol_matches_single_process(world, n_frames, force):
+    """force: world 1 with Comm's identity shortcut off (every gather runs through gloo)."""
     import torch.multiprocessing as mp
 
     frames, labels, clusters, trk = _oracle(n_frames)
     assert labels.max() >= 3, "scene should produce several clusters"
     with tempfile.TemporaryDirectory() as td:
-        mp.start_processes(_worker, args=(world, _free_port(), n_frames, td), nprocs=world,
+        mp.start_processes(_worker, args=(world, _free_port(), n_frames, td, force), nprocs=world,
                            join=True, start_method="spawn")
         parts = [np.load(Path(td) / f"rank{r}.npz") for r in range(world)]
         got = np.concatenate([p["labels"] for p in parts])

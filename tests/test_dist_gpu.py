@@ -23,18 +23,19 @@ def _free_port():
     return p
 
 
-def _run(world, frames, impl, lanes, extra, timeout=600):
+def _run(world, frames, impl, lanes, extra, timeout=600, backend="gloo"):
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={world}", "--master-addr=127.0.0.1",
            f"--master-port={_free_port()}", str(ROOT / "tools" / "dist_check.py"),
-           "--backend", "gloo", "--frames", str(frames), "--impl", impl, "--lanes", str(lanes),
+           "--backend", backend, "--frames", str(frames), "--impl", impl, "--lanes", str(lanes),
            *extra]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-4000:]
     assert "ok=True" in out, out[-4000:]
+    return out
 
 
 @pytest.mark.gpu
@@ -65,3 +66,14 @@ def test_sharded_dense_giant_component_matches_oracle(world, frames, lanes):
     with the oracle's run_path (union-find ST-DBSCAN) over the whole stack
     (4_temporal_object_tracker.py:466-506, 508-536, 984-991)."""
     _run(world, frames, "native", lanes, ["--dense", "--oracle"], timeout=840)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_rccl_world1_forced_collectives_match_single_gpu(lanes):
+    """The RCCL (nccl backend) branch of rpt.dist.Comm on one GPU: world 1 with the identity
+    shortcut off, so the land-grid all_reduce, the info all_gather, the device-resident pair and
+    result gathers (all_gather_into_tensor on the lane's stream) and, at lanes = 2, the
+    CommSequencer all run through RCCL; the result must equal the single-GPU pipeline's."""
+    out = _run(1, 10, "native", lanes, ["--force-collectives"], backend="nccl", timeout=300)
+    assert "backend=nccl" in out, out[-4000:]

@@ -51,7 +51,12 @@ def main():
     ap.add_argument("--tiny-caps", action="store_true",
                     help="native: one-pair / 16-word capacities for the pair and result gathers "
                          "(every step is finished again with grown ones)")
+    ap.add_argument("--force-collectives", action="store_true",
+                    help="run world-1 collectives through the backend (rpt.dist.Comm.solo off): "
+                         "with --backend nccl this executes the RCCL branch on one GPU")
     args = ap.parse_args()
+    if args.force_collectives:
+        os.environ["RPT_COMM_FORCE_COLLECTIVES"] = "1"
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", "0"))
