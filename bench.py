@@ -27,8 +27,10 @@ no better); `one_stack_in_flight` repeats the steps strictly one after
 another, and K5's roofline is taken from that leg (K5 alone on the GPU).
 At N>1 (the frame-sharded path) one stack is in flight per rank by default; `--lanes 3` keeps
 three, their collectives through ONE communicator in a fixed software-pipeline order
-(rpt.dist.CommSequencer, validated with gloo at 8 ranks, not yet on RCCL across GPUs, hence not
-the default).  With one rank (`--sharded`, the 125-frame per-rank share of 8 GPUs) the default
+(rpt.dist.CommSequencer, validated with gloo at 8 ranks and on RCCL at one rank with every
+collective forced through it -- RPT_COMM_FORCE_COLLECTIVES=1: 1.66 ms per step with 3 lanes against
+2.27 with 1, profiles/r4/rccl_ab/ -- but not yet on RCCL across GPUs, hence not the default).
+With one rank (`--sharded`, the 125-frame per-rank share of 8 GPUs) the default
 stays 3: the shard driver v2 measured 1.48 ms per step with 3 lanes (1.62 ms with the
 sequencer's order kept, --sequenced) against 2.12 ms with 1
 (profiles/r4/bench_sharded1rank_125f_*.json).
@@ -219,8 +221,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     if args.lanes is None:
         # several lanes share one RCCL communicator only through CommSequencer's order, which has
-        # run on gloo (8 ranks) and at one rank, never on RCCL across GPUs: one lane per rank
-        # until it has (--lanes 3 opts in)
+        # run on gloo (8 ranks) and on RCCL at one rank (forced collectives), never on RCCL across
+        # GPUs: one lane per rank until it has (--lanes 3 opts in)
         args.lanes = 3 if world == 1 else 1
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # --sharded: the frame-sharded multi-GPU path even at one rank (measures its per-rank cost)
