@@ -882,18 +882,20 @@ __device__ __forceinline__ float4 rec_boxB(const CellRec<3>& r) {
   return make_float4(r.z0, r.z1, r.t0, r.t1);
 }
 
-// Per-cell bounding boxes, EIGHT lanes per occupied cell (eight cells per wave: most cells hold a
-// few dozen points, so a wave per cell would mostly wait on its loads).  boxA = {xmin, xmax,
-// ymin, ymax}, boxB = {zmin, zmax, tmin, tmax}.  mutual[c] = 1 when every pair of points in the
-// cell passes the neighbour test (computed conservatively from the box with the same rounding as
-// the pair test).
+// Per-cell records (point range and bounding box in space and time; the only copy of the boxes:
+// the per-point union reads them from the records too), kCbLanes lanes per occupied cell, four
+// cells per wave.  A wave waits for its densest cell (a few hundred points at the standard
+// density, thousands in the dense stacks), so lanes per cell set the rate: same-box A/B
+// (tools/kab2.sh, 1000 standard / 125 dense frames) 4 lanes 434 / 403 us, 8 lanes 353 / 347,
+// 16 lanes 347 / 321, 32 lanes 453 / 387.  mutual[c] = 1 when every pair of points in the cell
+// passes the neighbour test (computed conservatively from the box with the same rounding as the
+// pair test).
+constexpr int kCbLanes = 16;
 template <int D>
 __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ pts,
                                                     const int32_t* __restrict__ cell_start,
                                                     const int32_t* __restrict__ occ,
                                                     const int32_t* __restrict__ n_occ, Geom g,
-                                                    float4* __restrict__ boxA,
-                                                    float4* __restrict__ boxB,
                                                     uint8_t* __restrict__ mutual,
                                                     CellRec<D>* __restrict__ crec,
                                                     unsigned long long* __restrict__ cmin =
@@ -901,11 +903,12 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ 
                                                     const int32_t* __restrict__ sorig = nullptr) {
   // sorig (kernel-uniform): cmin[c] = the (min original, sorted) pair over ALL the cell's points
   // (the fused K5 keeps it for all-core cells), read alongside the points; otherwise none (~0)
-  const int j = threadIdx.x & 7;
+  constexpr int L = kCbLanes;
+  const int j = threadIdx.x & (L - 1);
   const int64_t no = *n_occ;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t - j < no * 8;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t - j < no * L;
        t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t q = t >> 3;
+    const int64_t q = t / L;
     const bool act = q < no;
     int c = 0, b = 0, e = 0;
     if (act) {
@@ -917,14 +920,14 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ 
     float z0 = FLT_MAX, z1 = -FLT_MAX, t0 = FLT_MAX, t1 = -FLT_MAX;
     uint64_t mn = ~0ull;
     // 8 loads in flight per lane: a dense cell (hundreds of points) is otherwise a chain of
-    // dependent load round trips on its 8 lanes
+    // dependent load round trips on its lanes
     constexpr int kU = 8;
-    for (int s0 = b + j; s0 < e; s0 += 8 * kU) {
+    for (int s0 = b + j; s0 < e; s0 += L * kU) {
       float4 pp[kU];
       uint32_t so[kU];
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        const int s2 = s0 + 8 * u;
+        const int s2 = s0 + L * u;
         const int sc = (s2 < e) ? s2 : s0;  // duplicates of a cell point leave the box as is
         pp[u] = pts[sc];
         if (sorig) so[u] = (uint32_t)sorig[sc];
@@ -937,7 +940,7 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ 
         z0 = fminf(z0, p.z); z1 = fmaxf(z1, p.z);
         t0 = fminf(t0, p.w); t1 = fmaxf(t1, p.w);
         if (sorig) {
-          const int s2 = s0 + 8 * u;
+          const int s2 = s0 + L * u;
           const uint64_t v = ((uint64_t)so[u] << 32) | (uint32_t)((s2 < e) ? s2 : s0);
           mn = v < mn ? v : mn;
         }
@@ -945,27 +948,25 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ 
     }
     if (sorig) {
 #pragma unroll
-      for (int off = 4; off > 0; off >>= 1) {
-        const uint32_t olo = (uint32_t)__shfl_xor((int)(uint32_t)mn, off, 8);
-        const uint32_t ohi = (uint32_t)__shfl_xor((int)(uint32_t)(mn >> 32), off, 8);
+      for (int off = L / 2; off > 0; off >>= 1) {
+        const uint32_t olo = (uint32_t)__shfl_xor((int)(uint32_t)mn, off, L);
+        const uint32_t ohi = (uint32_t)__shfl_xor((int)(uint32_t)(mn >> 32), off, L);
         const uint64_t o = ((uint64_t)ohi << 32) | olo;
         mn = o < mn ? o : mn;
       }
     }
 #pragma unroll
-    for (int off = 4; off > 0; off >>= 1) {
-      x0 = fminf(x0, __shfl_xor(x0, off, 8)); x1 = fmaxf(x1, __shfl_xor(x1, off, 8));
-      y0 = fminf(y0, __shfl_xor(y0, off, 8)); y1 = fmaxf(y1, __shfl_xor(y1, off, 8));
-      z0 = fminf(z0, __shfl_xor(z0, off, 8)); z1 = fmaxf(z1, __shfl_xor(z1, off, 8));
-      t0 = fminf(t0, __shfl_xor(t0, off, 8)); t1 = fmaxf(t1, __shfl_xor(t1, off, 8));
+    for (int off = L / 2; off > 0; off >>= 1) {
+      x0 = fminf(x0, __shfl_xor(x0, off, L)); x1 = fmaxf(x1, __shfl_xor(x1, off, L));
+      y0 = fminf(y0, __shfl_xor(y0, off, L)); y1 = fmaxf(y1, __shfl_xor(y1, off, L));
+      z0 = fminf(z0, __shfl_xor(z0, off, L)); z1 = fmaxf(z1, __shfl_xor(z1, off, L));
+      t0 = fminf(t0, __shfl_xor(t0, off, L)); t1 = fmaxf(t1, __shfl_xor(t1, off, L));
     }
     if (D != 3) {
       z0 = t0;  // 2-D: pts[].z carries t (unused by the 2-D tests)
       z1 = t1;
     }
     if (act && j == 0) {
-      boxA[c] = make_float4(x0, x1, y0, y1);
-      boxB[c] = make_float4(z0, z1, t0, t1);
       CellRec<D> r{};
       r.b = b;
       r.e = e;
@@ -1123,8 +1124,7 @@ __device__ __forceinline__ int classify(const float4& p, const float4& A, const 
 template <int D, class F>
 __device__ __forceinline__ void for_each_cell(const float4& p, int32_t key, const Geom& g,
                                               const int32_t* __restrict__ cell_start,
-                                              const float4* __restrict__ boxA,
-                                              const float4* __restrict__ boxB,
+                                              const CellRec<D>* __restrict__ crec,
                                               const float2* __restrict__ slab_t, F&& f) {
   int cx, cy, cz, cs;
   g.split((uint32_t)key, cx, cy, cz, cs);
@@ -1149,7 +1149,8 @@ __device__ __forceinline__ void for_each_cell(const float4& p, int32_t key, cons
           const int e = cell_start[row + xx + 1];
           if (e > b) {
             const int64_t c = row + xx;
-            const int cls = classify<D>(p, boxA[c], boxB[c], g);
+            const CellRec<D> cr = crec[c];
+            const int cls = classify<D>(p, rec_boxA<D>(cr), rec_boxB(cr), g);
             if (cls != 0 && f(c, b, e, cls)) return;
           }
           b = e;
@@ -3005,8 +3006,7 @@ template <int D>
 __global__ __launch_bounds__(kBlock) void k_union(const float4* __restrict__ pts,
                                                  const int32_t* __restrict__ skey, int64_t n,
                                                  Geom g, const int32_t* __restrict__ cell_start,
-                                                 const float4* __restrict__ boxA,
-                                                 const float4* __restrict__ boxB,
+                                                 const CellRec<D>* __restrict__ crec,
                                                  const float2* __restrict__ slab_t,
                                                  const uint8_t* __restrict__ core,
                                                  const int32_t* __restrict__ rep,
@@ -3020,7 +3020,7 @@ __global__ __launch_bounds__(kBlock) void k_union(const float4* __restrict__ pts
   if (mutual[key]) return;  // handled by the star init + k_union_cells
   const float4 p = pts[s];
   const int si = (int)s;
-  for_each_cell<D>(p, key, g, cell_start, boxA, boxB, slab_t,
+  for_each_cell<D>(p, key, g, cell_start, crec, slab_t,
                    [&](int64_t c, int b, int e, int cls) -> bool {
                      const int r = rep[c];
                      if (r < 0) return false;
@@ -4117,7 +4117,6 @@ struct DbscanState {
   int64_t C = 0, nt = 0;
   float4* pts = nullptr;
   int32_t *sorig = nullptr, *skey = nullptr, *cell_start = nullptr, *rep = nullptr;
-  float4 *boxA = nullptr, *boxB = nullptr;
   uint8_t *mutual = nullptr, *core = nullptr;
   float2* slab_t = nullptr;
   int32_t *parent = nullptr, *ccmin = nullptr, *cid = nullptr, *nc_list = nullptr;
@@ -4350,8 +4349,6 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   bud.add<int32_t>(n);       // skey
   bud.add<int32_t>(C1 + 1);  // cell_start
   bud.add<int64_t>(scan_tmp_elems(C1 + 1) + scan_tmp_elems(n + 1));
-  bud.add<float4>(C1);
-  bud.add<float4>(C1);
   bud.add<uint8_t>(C1);
   bud.add<int32_t>(C1);  // rep
   bud.add<float2>(nt);
@@ -4389,8 +4386,6 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   skey = arena.carve_n<int32_t>(n);
   cell_start = arena.carve_n<int32_t>(C1 + 1);
   stmp = arena.carve_n<int64_t>(scan_tmp_elems(C1 + 1) + scan_tmp_elems(n + 1));
-  boxA = arena.carve_n<float4>(C1);
-  boxB = arena.carve_n<float4>(C1);
   mutual = arena.carve_n<uint8_t>(C1);
   rep = arena.carve_n<int32_t>(C1);
   slab_t = arena.carve_n<float2>(nt);
@@ -4527,8 +4522,8 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
     RPT_CHECK_LAUNCH();
     n_occ_dev = hpos + n;
   }
-  hipLaunchKernelGGL(k_cell_box<D>, dim3(grid_for(8 * n, kBlock, 8192)), dim3(kBlock), 0, st,
-                     pts, cell_start, occ, n_occ_dev, g, boxA, boxB, mutual, cr,
+  hipLaunchKernelGGL(k_cell_box<D>, dim3(grid_for(kCbLanes * n, kBlock, 8192)), dim3(kBlock), 0,
+                     st, pts, cell_start, occ, n_occ_dev, g, mutual, cr,
                      bucket_allmin ? nullptr
                                    : reinterpret_cast<unsigned long long*>(cell_min_pair),
                      (k5_fused_path() && !bucket_allmin) ? (const int32_t*)sorig : nullptr);
@@ -4728,7 +4723,7 @@ int32_t DbscanState::union_pass(hipStream_t st) {
                          cell_start, occ, n_occ, rec<2>(), occ_bits, slab_t, core, rep, mutual,
                          sorig, parent, uf_flags, pm, plist, pcount);
     hipLaunchKernelGGL(k_union<2>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
-                       boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
+                       rec<2>(), slab_t, core, rep, mutual, sorig, parent);
   } else {
     hipLaunchKernelGGL((k_union_cells<3, false>), dim3(gw), dim3(kBlock), 0, st, pts, g,
                        cell_start, occ, n_occ, rec<3>(), occ_bits, slab_t, core, rep, mutual, sorig,
@@ -4737,7 +4732,7 @@ int32_t DbscanState::union_pass(hipStream_t st) {
                        cell_start, occ, n_occ, rec<3>(), occ_bits, slab_t, core, rep, mutual, sorig,
                        parent, uf_flags);
     hipLaunchKernelGGL(k_union<3>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
-                       boxA, boxB, slab_t, core, rep, mutual, sorig, parent);
+                       rec<3>(), slab_t, core, rep, mutual, sorig, parent);
   }
   RPT_CHECK_LAUNCH();
   // every later reader walks to the root with path halving (k_ccmin, k_comp_out, ...), so a
