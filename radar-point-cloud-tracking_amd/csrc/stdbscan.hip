@@ -1618,7 +1618,7 @@ __device__ __forceinline__ void cells_fill_epilogue(const Geom& g, bool act, int
 // undecided cells' points appended to the level-4 queue (one atomic per wave).  The all-core
 // cells' (min original, sorted) pairs are k_cell_box's (allmin).  No per-point loads at all.
 constexpr int kCwMaxR = 3;
-constexpr int kCwBatch = 5;  // candidate records per lane in flight together (k_core_cells_oct)
+constexpr int kCwBatch = 4;  // candidate records per lane in flight together (k_core_cells_oct)
 template <bool FUSED = false>
 // 5 waves/SIMD (<= 96 VGPRs; the fused epilogue and its LDS queue would take 99: 4 waves)
 __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
@@ -1669,32 +1669,50 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
     } else if (act) {
       int cx, cy, cz, cs;
       g.split((uint32_t)ca, cx, cy, cz, cs);
+      // window of W = 2R + 1 slabs; lane j < W tests the time reach of slab cs - R + j
+      const int W = 2 * R + 1;
       const int sl = cs + j - R;
-      const bool sv = j <= 2 * R && sl >= 0 && sl < g.nt;
+      const bool sv = j < W && sl >= 0 && sl < g.nt;
       const CellRec<2> ra = crec[ca];
       const uint8_t mu = mutual[ca];
       b = ra.b;
       e = ra.e;
       const float2 own = slab_t[cs];
       float2 sr = make_float2(1.f, 0.f);
-      uint32_t m5[5] = {0u, 0u, 0u, 0u, 0u};
+      // The window's 5 W (slab, row) pairs are spread over ALL eight lanes of the cell: pair
+      // p = k W + si (row rank k: dy = 0, -1, +1, -2, +2, own row first; slab index si) is slot
+      // p / 8 of lane p % 8.  (A lane per slab left 8 - W lanes idle through the candidate loop
+      // -- 3 of 8 at the usual W = 5 -- and the busiest slab set the loop's trip count.)
+      uint32_t m5[5];  // slot i: occupied columns dx = 0..4 of its row (x = cx - 2 + dx)
+      int psi[5];      // slot i: slab index
+      const uint32_t mg = (65535u + (uint32_t)W) / (uint32_t)W;  // p / W = (p * mg) >> 16
+      // key of column dx = 0 of pair p's row (recomputed per candidate: five more registers
+      // for the slots' keys spilled)
+      auto pair_key0 = [&](int p) -> int {
+        const int k = (int)__umul24((uint32_t)p, mg) >> 16;
+        const int si = p - k * W;
+        return (int)__umul24((uint32_t)((cs + si - R) * g.ny + cy + cw_row(k) - 2),
+                             (uint32_t)g.nx) + (cx - 2);
+      };
       {
-        // branch-free: a lane out of the window reads its own slab's words and masks them off,
-        // so the eleven loads of every lane are in flight together (a conditional load is a
-        // branch ending in a full vmcnt wait)
+        // branch-free: an invalid slot reads a valid word and masks it off, so all eleven loads
+        // of every lane are in flight together (a conditional load is a branch ending in a full
+        // vmcnt wait)
         const int slc = sv ? sl : cs;
         const float2 srv = slab_t[slc];
         sr = sv ? srv : sr;
         const int lo_x = cx - 2 < 0 ? 2 - cx : 0;
         const int hi_x = cx + 2 - (g.nx - 1);
 #pragma unroll
-        for (int dy = 0; dy < 5; ++dy) {
-          const int y = cy + dy - 2;
-          const bool yv = sv && y >= 0 && y < g.ny;
-          const int yc = min(max(y, 0), g.ny - 1);
-          // bit dx <-> key k0 + dx (x = cx - 2 + dx); columns outside [0, nx) are cleared
+        for (int i = 0; i < 5; ++i) {
+          const int p = j + 8 * i;
+          const int k = min((int)(((uint32_t)p * mg) >> 16), 4);
+          const int si = p - k * W;
+          const int s2 = cs + si - R;
+          const int y = cy + cw_row(k) - 2;
+          const bool v = p < 5 * W && s2 >= 0 && s2 < g.nt && y >= 0 && y < g.ny;
           // (int32 keys: cells < 2^30)
-          const int k0 = (slc * g.ny + yc) * g.nx + (cx - 2);
+          const int k0 = ((v ? s2 : cs) * g.ny + (v ? y : cy)) * g.nx + (cx - 2);
           const int kk = k0 < 0 ? 0 : k0;
           const int w = kk >> 5;
           const uint32_t lo_w = occ_bits[w], hi_w = occ_bits[w + 1];
@@ -1702,34 +1720,31 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
                                 : (__builtin_amdgcn_alignbit(hi_w, lo_w, (uint32_t)(kk & 31)) & 31u);
           m &= ~((1u << lo_x) - 1u);
           if (hi_x > 0) m &= (31u >> hi_x);
-          m5[dy] = yv ? m : 0u;
+          m5[i] = v ? m : 0u;
+          psi[i] = v ? si : 0;
         }
       }
       const float gap =
           (own.x > sr.y) ? (own.x - sr.y) : ((sr.x > own.y) ? (sr.x - own.y) : 0.f);
-      const bool reach = sv && sr.x <= sr.y && gap <= g.epst;  // this lane's slab is in reach
+      const bool reach = sv && sr.x <= sr.y && gap <= g.epst;  // slab j is in reach
+      // the cell's reach bits (slab index -> bit), from its eight lanes (group-uniform branch)
+      const uint32_t rbits =
+          (uint32_t)(__ballot(reach) >> (threadIdx.x & 56)) & 0xffu;
+      // the lane's occupied candidates as one 25-bit mask, slot-major (bits 5i .. 5i + 4 = slot
+      // i's columns): rows nearest first
+      uint32_t m25 = 0;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) m25 |= (((rbits >> psi[i]) & 1u) ? m5[i] : 0u) << (5 * i);
       if (need <= 0 || (mu && e - b >= need)) {
         flag = 1;
       } else {
         int lo = 0, hi = 0;
         const float4 A1 = rec_boxA<2>(ra), A2 = rec_boxB(ra);
-        // the lane's occupied candidates as one 25-bit mask, rows nearest first (bits 0-4 the
-        // cell's own row, 5-14 rows -1 / +1, 15-24 rows -2 / +2), taken kCwBatch at a time with
-        // all their record loads in flight together: a sparse cell's few candidates cost ONE
-        // round trip instead of one per row; the eight lanes stop as soon as the adjacent-to-
-        // every-point count reaches min_samples (dense cells: after the own row's batch)
-        uint32_t m25 = 0;
-        if (reach) {
-#pragma unroll
-          for (int k = 0; k < 5; ++k) {
-            const int dy = (k == 0) ? 2 : ((k & 1) ? 2 - (k + 1) / 2 : 2 + k / 2);
-            m25 |= m5[dy] << (5 * k);
-          }
-        }
+        // taken kCwBatch at a time with all their record loads in flight together: a sparse
+        // cell's few candidates cost ONE round trip instead of one per row; the eight lanes stop
+        // as soon as the adjacent-to-every-point count reaches min_samples (dense cells: after
+        // the own row's batch)
         bool decided = false;
-        // key of window row dy = -2, column dx = -2 in this lane's slab (candidate key = rowbase
-        // + (dy + 2) * nx + (dx + 2))
-        const int rowbase = (sl * g.ny + (cy - 2)) * g.nx + (cx - 2);
         while (true) {
           int rem = m25 ? 1 : 0;
 #pragma unroll
@@ -1743,10 +1758,8 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
             has[i] = m25 != 0;
             const int p = __builtin_ctz(m25 | (1u << 31));
             m25 &= m25 - 1;
-            const int k = p / 5, dx = p - 5 * k;
-            // (24-bit multiply: full rate, where a 32-bit v_mul_lo is quarter rate)
-            const int key = rowbase + (int)__umul24((uint32_t)cw_row(k),
-                                                    (uint32_t)g.nx) + dx;
+            const int sl5 = (p * 13) >> 6;  // slot p / 5 (p < 32)
+            const int key = pair_key0(j + 8 * sl5) + (p - 5 * sl5);
             cr[i] = crec[has[i] ? key : ca];
           }
 #pragma unroll
