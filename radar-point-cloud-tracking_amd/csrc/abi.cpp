@@ -26,7 +26,8 @@ int32_t polar_write(const void* echo, int32_t dt, int64_t n_files, int32_t rows,
                     const float* scale, const float* cos_t, const float* sin_t,
                     const int32_t* gain, float thr, int32_t stride, const int64_t* row_prefix,
                     const int64_t* file_offsets, int32_t files_per_frame, float* x, float* y,
-                    float* v, int32_t* gout, int32_t* pf, hipStream_t st, const uint32_t* entries);
+                    float* v, int32_t* gout, int32_t* pf, hipStream_t st, const uint32_t* entries,
+                    uint32_t* bnd = nullptr, bool* bnd_done = nullptr);
 int64_t polar_stage_words(int64_t n_files, int32_t rows);
 int32_t frame_times(const int32_t* pf, int64_t n, const int64_t* ids, float* t, hipStream_t st);
 int32_t sweep_to_points(const float* inten, const float* ranges, const float* cos_t,

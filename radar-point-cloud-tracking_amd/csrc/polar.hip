@@ -306,6 +306,61 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// xy bounds of the written points, folded into the K1 write kernels (the land grid's edges need
+// them; a separate pass re-read x and y: ~0.1 ms at 1000 frames).  Floats as order-preserving
+// u32 (-0 below +0), as k_bounds_xy: {min x, max x, min y, max y}; each block leaves one
+// partial, k_bounds_parts reduces them.
+__device__ __forceinline__ uint32_t f2ord(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+struct XyBounds {
+  uint32_t v[4] = {0xffffffffu, 0u, 0xffffffffu, 0u};
+  __device__ void add(float x, float y) {
+    const uint32_t a = f2ord(x), b = f2ord(y);
+    v[0] = min(v[0], a);
+    v[1] = max(v[1], a);
+    v[2] = min(v[2], b);
+    v[3] = max(v[3], b);
+  }
+  // whole block (every thread calls it once, after its last add): partial of block blockIdx.x.
+  // scratch: 4 LDS words per wave at scratch + 4 * wstride * wave, free for the caller by now
+  // (a kernel's own LDS, so the reduction does not add to its LDS size and cost occupancy)
+  __device__ void store_block(uint32_t* __restrict__ part, uint32_t* scratch, int wstride) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      v[0] = min(v[0], (uint32_t)__shfl_xor((int)v[0], off));
+      v[1] = max(v[1], (uint32_t)__shfl_xor((int)v[1], off));
+      v[2] = min(v[2], (uint32_t)__shfl_xor((int)v[2], off));
+      v[3] = max(v[3], (uint32_t)__shfl_xor((int)v[3], off));
+    }
+    if ((threadIdx.x & 63) == 0)
+      for (int k = 0; k < 4; ++k) scratch[4 * wstride * (threadIdx.x / 64) + k] = v[k];
+    __syncthreads();
+    if (threadIdx.x < 4) {
+      const int k = threadIdx.x;
+      uint32_t r = scratch[k];
+      for (int w = 1; w < kWavesPerBlock; ++w) {
+        const uint32_t o = scratch[4 * wstride * w + k];
+        r = (k & 1) ? max(r, o) : min(r, o);
+      }
+      part[4 * blockIdx.x + k] = r;
+    }
+  }
+};
+__global__ __launch_bounds__(kBlock) void k_bounds_parts(const uint32_t* __restrict__ part, int nb,
+                                                        uint32_t* __restrict__ out) {
+  XyBounds b;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+    b.v[0] = min(b.v[0], part[4 * i + 0]);
+    b.v[1] = max(b.v[1], part[4 * i + 1]);
+    b.v[2] = min(b.v[2], part[4 * i + 2]);
+    b.v[3] = max(b.v[3], part[4 * i + 3]);
+  }
+  __shared__ uint32_t sm[4 * kWavesPerBlock];
+  b.store_block(out - 4 * blockIdx.x, sm, 1);  // one block: out[0..3]
+}
+
 __device__ __forceinline__ void group_to_lds(GroupLds& L, int lane, const uint32_t (&m)[kGroupRows],
                                              const int (&incl)[kGroupRows],
                                              const uint4 (&vv)[kGroupRows]) {
@@ -475,7 +530,7 @@ __global__ void k_file_counts_groups(const int64_t* __restrict__ gprefix, int64_
 // LIST: the groups are the first *list_n entries of list (the unstaged groups of the expand
 // write below), not 0 .. n_groups-1.
 template <bool HI, bool STAGED, bool LIST = false>
-__global__ __launch_bounds__(kBlock) void k_group_write_u8(
+__global__ __launch_bounds__(kBlock, 8) void k_group_write_u8(
     const uint8_t* __restrict__ echo, uint32_t n_groups, GroupMap gm, uint32_t K, int stride,
     const float* __restrict__ scale, const float* __restrict__ cos_t,
     const float* __restrict__ sin_t, const int32_t* __restrict__ gain,
@@ -483,8 +538,10 @@ __global__ __launch_bounds__(kBlock) void k_group_write_u8(
     int files_per_frame, float* __restrict__ x, float* __restrict__ y, float* __restrict__ val,
     int32_t* __restrict__ gain_out, int32_t* __restrict__ pf_out, int64_t cap,
     const uint32_t* __restrict__ entries, const uint32_t* __restrict__ list = nullptr,
-    const uint32_t* __restrict__ list_n = nullptr) {
+    const uint32_t* __restrict__ list_n = nullptr, uint32_t* __restrict__ bpart = nullptr) {
+  // bpart (nullable, kernel-uniform): this block's xy-bounds partial (XyBounds)
   __shared__ GroupLds s_lds[kWavesPerBlock];
+  XyBounds xb;
   const int lane = threadIdx.x & 63;
   GroupLds& L = s_lds[threadIdx.x / 64];
   const uint32_t wave0 = blockIdx.x * kWavesPerBlock + threadIdx.x / 64;
@@ -560,14 +617,20 @@ __global__ __launch_bounds__(kBlock) void k_group_write_u8(
       const float cc = rk == 0 ? r_c[0] : (rk == 1 ? r_c[1] : (rk == 2 ? r_c[2] : r_c[3]));
       const float ss = rk == 0 ? r_s[0] : (rk == 1 ? r_s[1] : (rk == 2 ? r_s[2] : r_s[3]));
       const float rr = sc * inv_bins * (float)((ent >> 8) & 1023u);
-      x[oo] = rr * cc;
-      y[oo] = rr * ss;
+      const float px = rr * cc, py = rr * ss;
+      x[oo] = px;
+      y[oo] = py;
+      if (bpart) xb.add(px, py);
       val[oo] = (float)(ent & 0xffu);
       if (gain_out) gain_out[oo] = g;
       if (pf_out) pf_out[oo] = fr;
     }
     if (!staged) wave_lds_sync();  // the slice is rewritten by the next group
   }
+  // (every wave is past its last group: each one's own LDS slice is free)
+  if (bpart)
+    xb.store_block(bpart, reinterpret_cast<uint32_t*>(&s_lds[0]),
+                   (int)(sizeof(GroupLds) / sizeof(uint32_t) / 4));
 }
 
 // ---- expand write: output slots to threads (staged groups)
@@ -672,14 +735,20 @@ __global__ __launch_bounds__(kBlock) void k_expand_write(
     const float* __restrict__ sin_t, const int32_t* __restrict__ gain,
     const int64_t* __restrict__ total_out, int files_per_frame, float* __restrict__ x,
     float* __restrict__ y, float* __restrict__ val, int32_t* __restrict__ gain_out,
-    int32_t* __restrict__ pf_out, int64_t cap, const uint32_t* __restrict__ entries) {
+    int32_t* __restrict__ pf_out, int64_t cap, const uint32_t* __restrict__ entries,
+    uint32_t* __restrict__ bpart = nullptr) {
+  // bpart (nullable): this block's xy-bounds partial of the outputs it writes (XyBounds)
   __shared__ uint64_t s_win[kWin];
   __shared__ uint32_t s_glo;
   const int64_t total = min(*total_out, cap);
   const int64_t n_tiles = (total + kTileOut - 1) / kTileOut;
   const int64_t t0 = n_tiles * blockIdx.x / gridDim.x;
   const int64_t t1 = n_tiles * (blockIdx.x + 1) / gridDim.x;
-  if (t0 >= t1) return;  // block-uniform
+  if (t0 >= t1) {  // block-uniform
+    if (bpart && threadIdx.x < 4)  // (no outputs: the identity)
+      bpart[4 * blockIdx.x + threadIdx.x] = (threadIdx.x & 1) ? 0u : 0xffffffffu;
+    return;
+  }
   if (threadIdx.x < 64) {
     const uint32_t g = wave_find_group(gword, 0u, n_groups, (uint64_t)t0 * kTileOut);
     if (threadIdx.x == 0) s_glo = g;
@@ -702,6 +771,7 @@ __global__ __launch_bounds__(kBlock) void k_expand_write(
     for (int q = 0; q < kWinPer; ++q) s_win[threadIdx.x + q * kBlock] = wv[q];
   };
   uint32_t glo = s_glo;
+  XyBounds xb;
   load_win(glo);
   store_win();
   __syncthreads();
@@ -808,6 +878,7 @@ __global__ __launch_bounds__(kBlock) void k_expand_write(
       og[k] = gain ? gain[fl[k]] : 0;
       op[k] = (int32_t)pfl[k];
       all_ok = all_ok && ok[k];
+      if (bpart && ok[k]) xb.add(ox[k], oy[k]);
     }
     if (VEC && all_ok) {  // 16-B stores (the common case)
 #pragma unroll
@@ -836,6 +907,7 @@ __global__ __launch_bounds__(kBlock) void k_expand_write(
     if (t + 1 < t1) store_win();
     __syncthreads();  // the next tile's window
   }
+  if (bpart) xb.store_block(bpart, reinterpret_cast<uint32_t*>(s_win), 1);  // (window done)
 }
 
 // integer threshold of u8 samples (see keep_bits)
@@ -865,6 +937,7 @@ inline uint32_t u8_k(int T) {
 // k_expand_write: a persistent grid (8 blocks per CU of the 256; each walks a contiguous tile
 // range).  RPT_K1_EXPAND=0 keeps the wave-per-group write for A/B runs.
 constexpr int kExpandBlocks = 2048;
+constexpr int kListBlocks = 2048;  // blocks of the unstaged groups' write (at most)
 inline bool expand_write_enabled() {
   static const bool on = [] {
     const char* e = ab_env("RPT_K1_EXPAND");
@@ -941,7 +1014,11 @@ int32_t write_impl(const T* echo, int64_t n_files, int rows, int bins, float thr
                    RowGeo geo, const int32_t* gain, const int64_t* row_prefix,
                    const int64_t* file_offsets, int fpf, float* x, float* y, float* v,
                    int32_t* gout, int32_t* pf, hipStream_t st, int64_t cap = INT64_MAX,
-                   const uint32_t* entries = nullptr) {
+                   const uint32_t* entries = nullptr, uint32_t* bnd = nullptr,
+                   bool* bnd_done = nullptr) {
+  // bnd (nullable; polar_bounds_words() words): on the expand-write path the written points' xy
+  // bounds land in bnd[0..3] (ordered u32, as k_bounds_xy) and *bnd_done is set
+  if (bnd_done) *bnd_done = false;
   const int64_t n_rows = n_files * rows;
   if ((int64_t)rows * bins >= (int64_t(1) << 32) || n_rows >= (int64_t(1) << 32) || stride < 1 ||
       fpf < 1) {
@@ -979,24 +1056,29 @@ int32_t write_impl(const T* echo, int64_t n_files, int rows, int bins, float thr
         hipLaunchKernelGGL(k_expand_write<true>, dim3(kExpandBlocks), dim3(kBlock), 0, st, gword,
                            (uint32_t)n_groups, gm, (uint32_t)stride, geo.scale, geo.cos_t,
                            geo.sin_t, gain, file_offsets + n_files, fpf, x, y, v, gout, pf, cap,
-                           entries);
+                           entries, bnd ? bnd + 4 : nullptr);
       else
         hipLaunchKernelGGL(k_expand_write<false>, dim3(kExpandBlocks), dim3(kBlock), 0, st,
                            gword, (uint32_t)n_groups, gm, (uint32_t)stride, geo.scale, geo.cos_t,
                            geo.sin_t, gain, file_offsets + n_files, fpf, x, y, v, gout, pf, cap,
-                           entries);
+                           entries, bnd ? bnd + 4 : nullptr);
       RPT_CHECK_LAUNCH();
-      const int lgrid = std::min(grid, 2048);
+      const int lgrid = std::min(grid, kListBlocks);
 #define RPT_K1L(HI)                                                                            \
   hipLaunchKernelGGL((k_group_write_u8<HI, false, true>), dim3(lgrid), dim3(kBlock), 0, st, e8, \
                      (uint32_t)n_groups, gm, u8_k(T8), stride, geo.scale, geo.cos_t, geo.sin_t,  \
                      gain, row_prefix, file_offsets, fpf, x, y, v, gout, pf, cap, entries, list, \
-                     list_n)
+                     list_n, bnd ? bnd + 4 + 4 * kExpandBlocks : nullptr)
       if (T8 <= 127)
         RPT_K1L(false);
       else
         RPT_K1L(true);
 #undef RPT_K1L
+      if (bnd) {
+        hipLaunchKernelGGL(k_bounds_parts, dim3(1), dim3(kBlock), 0, st, bnd + 4,
+                           kExpandBlocks + lgrid, bnd);
+        if (bnd_done) *bnd_done = true;
+      }
       RPT_CHECK_LAUNCH();
       return RPT_OK;
     }
@@ -1207,7 +1289,9 @@ int32_t polar_write(const void* echo, int32_t dt, int64_t n_files, int32_t rows,
                     const float* scale, const float* cos_t, const float* sin_t,
                     const int32_t* gain, float thr, int32_t stride, const int64_t* row_prefix,
                     const int64_t* file_offsets, int32_t fpf, float* x, float* y, float* v,
-                    int32_t* gout, int32_t* pf, hipStream_t st, const uint32_t* entries) {
+                    int32_t* gout, int32_t* pf, hipStream_t st, const uint32_t* entries,
+                    uint32_t* bnd, bool* bnd_done) {
+  if (bnd_done) *bnd_done = false;
   if (n_files == 0) return RPT_OK;
   if (fpf < 1) {
     set_error("rpt_polar_write: files_per_frame must be >= 1");
@@ -1222,7 +1306,8 @@ int32_t polar_write(const void* echo, int32_t dt, int64_t n_files, int32_t rows,
   if (dt == RPT_ECHO_U8)
     return write_impl<uint8_t>((const uint8_t*)echo, n_files, rows, bins, thr, stride, geo, gain,
                                row_prefix, file_offsets, fpf, x, y, v, gout, pf, st, INT64_MAX,
-                               grouped_u8((const uint8_t*)echo, bins) ? entries : nullptr);
+                               grouped_u8((const uint8_t*)echo, bins) ? entries : nullptr, bnd,
+                               bnd_done);
   if (dt == RPT_ECHO_F32)
     return write_impl<float>((const float*)echo, n_files, rows, bins, thr, stride, geo, gain,
                              row_prefix, file_offsets, fpf, x, y, v, gout, pf, st);
@@ -1237,15 +1322,20 @@ int32_t polar_write_cap(const uint8_t* echo, int64_t n_files, int32_t rows, floa
                         const float* sin_t, const int32_t* gain, const int64_t* row_prefix,
                         const int64_t* file_offsets, int32_t fpf, float* x, float* y, float* v,
                         int32_t* gout, int32_t* pf, int64_t cap, hipStream_t st,
-                        const uint32_t* entries) {
+                        const uint32_t* entries, uint32_t* bnd, bool* bnd_done) {
+  if (bnd_done) *bnd_done = false;
   if (!grouped_u8(echo, 1024)) {
     set_error("polar_write_cap: u8 sweeps of 1024 bins with 16-B aligned rows only");
     return RPT_ENOTSUP;
   }
   RowGeo geo{scale, nullptr, cos_t, sin_t};
   return write_impl<uint8_t>(echo, n_files, rows, 1024, thr, stride, geo, gain, row_prefix,
-                             file_offsets, fpf, x, y, v, gout, pf, st, cap, entries);
+                             file_offsets, fpf, x, y, v, gout, pf, st, cap, entries, bnd,
+                             bnd_done);
 }
+
+// words of the bnd buffer of polar_write / polar_write_cap: 4 + the blocks' partials
+int64_t polar_bounds_words() { return 4 + 4 * (int64_t)(kExpandBlocks + kListBlocks); }
 
 int32_t sweep_to_points(const float* inten, const float* ranges, const float* cos_t,
                         const float* sin_t, int32_t rows, int32_t bins, float thr,

@@ -669,7 +669,7 @@ int32_t rpt_shard_polar(rpt_shard* h, const rpt_stack_params* p, const void* ech
   const int64_t n_files = (int64_t)F * G;
   RPT_TRY(S.file_off.ensure((size_t)n_files + 1, st));
   RPT_TRY(S.row_prefix.ensure((size_t)n_files * p->rows + 1, st));
-  RPT_TRY(h->bnd.ensure(8, st));
+  RPT_TRY(h->bnd.ensure((size_t)std::max<int64_t>(8, polar_bounds_words()), st));
   const size_t down_bytes = sizeof(int64_t) * (size_t)(n_files + 2) + 16;
   RPT_TRY(S.down.ensure(down_bytes, st));
   const bool grouped = p->echo_dtype == RPT_ECHO_U8 && p->bins == 1024 &&
@@ -691,12 +691,18 @@ int32_t rpt_shard_polar(rpt_shard* h, const rpt_stack_params* p, const void* ech
     // the write and the bounds are queued with the previous run's capacity; both are redone
     // below when the count exceeds it
     spec_cap = (int64_t)std::min({S.x.cap, S.y.cap, S.v.cap, S.g.cap, S.pf.cap});
+    // (the expand write leaves the bounds in h->bnd itself; otherwise a bounds pass)
+    bool fused = false;
     RPT_TRY(polar_write_cap((const uint8_t*)echo, n_files, p->rows, p->threshold, p->stride,
                             scale, cos_t, sin_t, gain, S.row_prefix.p, S.file_off.p, G, S.x.p,
-                            S.y.p, S.v.p, gain ? S.g.p : nullptr, S.pf.p, spec_cap, st, mk));
-    hipLaunchKernelGGL(k_init_bounds, dim3(1), dim3(64), 0, st, h->bnd.p);
-    hipLaunchKernelGGL(k_xy_bounds_part, dim3(grid_for(std::max<int64_t>(spec_cap, 1), 256, 512)),
-                       dim3(256), 0, st, S.x.p, S.y.p, spec_cap, n_dev, h->bnd.p);
+                            S.y.p, S.v.p, gain ? S.g.p : nullptr, S.pf.p, spec_cap, st, mk,
+                            mk ? h->bnd.p : nullptr, &fused));
+    if (!fused) {
+      hipLaunchKernelGGL(k_init_bounds, dim3(1), dim3(64), 0, st, h->bnd.p);
+      hipLaunchKernelGGL(k_xy_bounds_part,
+                         dim3(grid_for(std::max<int64_t>(spec_cap, 1), 256, 512)), dim3(256), 0,
+                         st, S.x.p, S.y.p, spec_cap, n_dev, h->bnd.p);
+    }
     RPT_CHECK_LAUNCH();
   }
   // one readback: file offsets (their last entry is the count) and the bounds
@@ -715,12 +721,16 @@ int32_t rpt_shard_polar(rpt_shard* h, const rpt_stack_params* p, const void* ech
     RPT_TRY(S.v.ensure(cap, st));
     RPT_TRY(S.g.ensure(cap, st));
     RPT_TRY(S.pf.ensure(cap, st));
+    bool fused = false;
     RPT_TRY(polar_write(echo, p->echo_dtype, n_files, p->rows, p->bins, scale, cos_t, sin_t, gain,
                         p->threshold, p->stride, S.row_prefix.p, S.file_off.p, G, S.x.p, S.y.p,
-                        S.v.p, gain ? S.g.p : nullptr, S.pf.p, st, mk));
-    hipLaunchKernelGGL(k_init_bounds, dim3(1), dim3(64), 0, st, h->bnd.p);
-    hipLaunchKernelGGL(k_xy_bounds_part, dim3(grid_for(std::max<int64_t>(N, 1), 256, 512)),
-                       dim3(256), 0, st, S.x.p, S.y.p, N, (const int64_t*)nullptr, h->bnd.p);
+                        S.v.p, gain ? S.g.p : nullptr, S.pf.p, st, mk, mk ? h->bnd.p : nullptr,
+                        &fused));
+    if (!fused) {
+      hipLaunchKernelGGL(k_init_bounds, dim3(1), dim3(64), 0, st, h->bnd.p);
+      hipLaunchKernelGGL(k_xy_bounds_part, dim3(grid_for(std::max<int64_t>(N, 1), 256, 512)),
+                         dim3(256), 0, st, S.x.p, S.y.p, N, (const int64_t*)nullptr, h->bnd.p);
+    }
     RPT_CHECK_LAUNCH();
     RPT_HIP(hipMemcpyAsync(hb, h->bnd.p, 16, hipMemcpyDeviceToHost, st));
     RPT_TRY(wait_stream(st));

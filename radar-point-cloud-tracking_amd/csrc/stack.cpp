@@ -118,13 +118,18 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
   // the readback (capacity-bounded) instead of after the host has seen the count; when the
   // count exceeds the capacity the buffers grow and the write runs again
   int64_t spec_cap = -1;
+  // the write leaves the points' xy bounds (the land grid's edges) in k1_bnd when it takes the
+  // expand path: no separate bounds pass over x and y
+  bool k1_bounds = false;
+  if (grouped && mk) RPT_TRY(k1_bnd.ensure((size_t)polar_bounds_words(), st));
+  uint32_t* kb = (grouped && mk) ? k1_bnd.p : nullptr;
   if (grouped && x.p && y.p && v.p && g.p && pf.p) {
     spec_cap = (int64_t)std::min({x.cap, y.cap, v.cap, g.cap, pf.cap});
     if (!ev_rb) RPT_HIP(hipEventCreateWithFlags(&ev_rb, hipEventDisableTiming));
     RPT_HIP(hipEventRecord(ev_rb, st));
     RPT_TRY(polar_write_cap((const uint8_t*)echo, n_files, p.rows, p.threshold, p.stride, scale,
                             cos_t, sin_t, gain, row_prefix.p, file_off.p, G, x.p, y.p, v.p,
-                            gain ? g.p : nullptr, pf.p, spec_cap, st, mk));
+                            gain ? g.p : nullptr, pf.p, spec_cap, st, mk, kb, &k1_bounds));
     RPT_HIP(hipEventSynchronize(ev_rb));  // the readback only; the write keeps running
   } else {
     RPT_TRY(wait_stream(st));
@@ -145,7 +150,7 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
     RPT_TRY(pf.ensure(cap, st));
     RPT_TRY(polar_write(echo, p.echo_dtype, n_files, p.rows, p.bins, scale, cos_t, sin_t, gain,
                         p.threshold, p.stride, row_prefix.p, file_off.p, G, x.p, y.p, v.p,
-                        gain ? g.p : nullptr, pf.p, st, mk));
+                        gain ? g.p : nullptr, pf.p, st, mk, kb, &k1_bounds));
   }
   if (timing) RPT_HIP(hipEventRecord(ev[1], st));
   if (N == 0) {
@@ -177,7 +182,18 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
   r.n_land_cells = 0;
   if (p.land_filter && n_built > 10 && N > 0) {
     float b4[4];
-    RPT_TRY(bounds_xy(x.p, y.p, N, b4, st));  // synchronises
+    if (k1_bounds) {
+      uint32_t hb[4];
+      RPT_HIP(hipMemcpyAsync(hb, kb, sizeof hb, hipMemcpyDeviceToHost, st));
+      RPT_TRY(wait_stream(st));
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t u = hb[k];
+        const uint32_t w = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
+        std::memcpy(b4 + k, &w, 4);
+      }
+    } else {
+      RPT_TRY(bounds_xy(x.p, y.p, N, b4, st));  // synchronises
+    }
     const std::vector<double> xe = arange_edges(b4[0], b4[1], p.land_resolution);
     const std::vector<double> ye = arange_edges(b4[2], b4[3], p.land_resolution);
     const int32_t nxe = (int32_t)xe.size(), nye = (int32_t)ye.size();

@@ -19,12 +19,16 @@ int32_t polar_write_cap(const uint8_t* echo, int64_t n_files, int32_t rows, floa
                         const float* sin_t, const int32_t* gain, const int64_t* row_prefix,
                         const int64_t* file_offsets, int32_t fpf, float* x, float* y, float* v,
                         int32_t* gout, int32_t* pf, int64_t cap, hipStream_t st,
-                        const uint32_t* entries);
+                        const uint32_t* entries, uint32_t* bnd = nullptr,
+                        bool* bnd_done = nullptr);
 int32_t polar_write(const void* echo, int32_t dt, int64_t n_files, int32_t rows, int32_t bins,
                     const float* scale, const float* cos_t, const float* sin_t,
                     const int32_t* gain, float thr, int32_t stride, const int64_t* row_prefix,
                     const int64_t* file_offsets, int32_t files_per_frame, float* x, float* y,
-                    float* v, int32_t* gout, int32_t* pf, hipStream_t st, const uint32_t* entries);
+                    float* v, int32_t* gout, int32_t* pf, hipStream_t st, const uint32_t* entries,
+                    uint32_t* bnd = nullptr, bool* bnd_done = nullptr);
+// words of polar_write's bnd buffer; the bounds it leaves in bnd[0..3] read back as floats
+int64_t polar_bounds_words();
 int64_t polar_stage_words(int64_t n_files, int32_t rows);
 int32_t frame_times(const int32_t* pf, int64_t n, const int64_t* ids, float* t, hipStream_t st);
 int32_t bounds_xy(const float* x, const float* y, int64_t n, float* out4, hipStream_t st);
@@ -181,6 +185,7 @@ struct rpt_stack {
   DevBuf<double> land_tot, edges;
   DevBuf<uint8_t> land_mask;
   DevBuf<uint32_t> k1_stage;           // K1 staged kept samples (count pass -> write pass)
+  DevBuf<uint32_t> k1_bnd;             // K1 write's xy bounds + block partials
   int k1_staged = -1;                  // RPT_K1_STAGE (default on), read once
   DevBuf<uint8_t> bnd;                 // ST-DBSCAN bounds (+ partials) of the kept points
   std::vector<char> dbscan_bounds;     // their host copy, from the land readback
@@ -214,6 +219,7 @@ struct rpt_stack {
     bnd.release();
     land_mask.release();
     k1_stage.release();
+    k1_bnd.release();
     up.release();
     down.release();
     if (ev_ok)
