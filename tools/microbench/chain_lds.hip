@@ -358,6 +358,120 @@ __global__ __launch_bounds__(64) void k_share(const float* gx, const float* gy, 
   if (lane == 0) out[2 * r] = acc;
   if (lane == 16) out[2 * r + 1] = acc;
 }
+
+// the chain lanes load their own operands straight from global memory into a ring of RING float4
+// registers (lane 0 the x run, lane 1 the y run, 16 B per load, RING loads in flight): no LDS, no
+// cross-lane operand; the loads complete in order, so each add waits for a load issued RING
+// float4s earlier
+template <int RING>
+__global__ __launch_bounds__(64) void k_gring(const float* gx, const float* gy, float* out) {
+  const int r = blockIdx.x, lane = threadIdx.x;
+  if (lane >= 2) return;
+  const float4* p4 = reinterpret_cast<const float4*>(((lane & 1) ? gy : gx) + (size_t)r * kLen);
+  constexpr int n4 = kLen / 4;
+  static_assert(kLen % 4 == 0, "whole float4s");
+  float4 q[RING];
+#pragma unroll
+  for (int k = 0; k < RING; ++k) q[k] = p4[k];
+  // -0 + x == x for every x: the chain may start from -0 instead of its first element
+  float acc = -0.0f;
+  int i = 0;
+  for (; i + 2 * RING <= n4; i += RING) {
+#pragma unroll
+    for (int k = 0; k < RING; ++k) {
+      const float4 v = q[k];
+      q[k] = p4[i + RING + k];
+      acc = acc + v.x;
+      acc = acc + v.y;
+      acc = acc + v.z;
+      acc = acc + v.w;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < RING; ++k) {
+    const float4 v = q[k];
+    acc = acc + v.x;
+    acc = acc + v.y;
+    acc = acc + v.z;
+    acc = acc + v.w;
+  }
+  for (int t = i + RING; t < n4; ++t) {
+    const float4 v = p4[t];
+    acc = acc + v.x;
+    acc = acc + v.y;
+    acc = acc + v.z;
+    acc = acc + v.w;
+  }
+  out[2 * r + lane] = acc;
+}
+
+// gring + a prefetch wave: wave 1 of the block streams the run's x and y through L2 (coalesced
+// 16-B loads, results folded into a sink) at most LOOK elements ahead of the chain's progress,
+// which lane 0 of wave 0 publishes in LDS once per ring; the chain lanes' own ring loads then hit
+// L2 instead of HBM
+template <int RING, int LOOK>
+__global__ __launch_bounds__(128) void k_gpf(const float* gx, const float* gy, float* out) {
+  const int r = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ volatile int progress;
+  if (threadIdx.x == 0) progress = 0;
+  __syncthreads();
+  constexpr int n4 = kLen / 4;
+  if (wave == 1) {
+    const float4* x4 = reinterpret_cast<const float4*>(gx + (size_t)r * kLen);
+    const float4* y4 = reinterpret_cast<const float4*>(gy + (size_t)r * kLen);
+    float sink = 0.f;
+    for (int p = 0; p < n4; p += 256) {  // 256 float4 = 1024 elements per step
+      while (p * 4 > progress + LOOK) __builtin_amdgcn_s_sleep(4);
+      float4 a[4], c[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = min(p + u * 64 + lane, n4 - 1);
+        a[u] = x4[q];
+        c[u] = y4[q];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sink += a[u].x + c[u].y;
+    }
+    if (sink == 1234.5f) out[2 * kRuns + r] = sink;  // keeps the loads
+    return;
+  }
+  if (lane >= 2) return;
+  const float4* p4 = reinterpret_cast<const float4*>(((lane & 1) ? gy : gx) + (size_t)r * kLen);
+  float4 q[RING];
+#pragma unroll
+  for (int k = 0; k < RING; ++k) q[k] = p4[k];
+  float acc = -0.0f;
+  int i = 0;
+  for (; i + 2 * RING <= n4; i += RING) {
+    if (lane == 0) progress = i * 4;
+#pragma unroll
+    for (int k = 0; k < RING; ++k) {
+      const float4 v = q[k];
+      q[k] = p4[i + RING + k];
+      acc = acc + v.x;
+      acc = acc + v.y;
+      acc = acc + v.z;
+      acc = acc + v.w;
+    }
+  }
+  if (lane == 0) progress = kLen;
+#pragma unroll
+  for (int k = 0; k < RING; ++k) {
+    const float4 v = q[k];
+    acc = acc + v.x;
+    acc = acc + v.y;
+    acc = acc + v.z;
+    acc = acc + v.w;
+  }
+  for (int t = i + RING; t < n4; ++t) {
+    const float4 v = p4[t];
+    acc = acc + v.x;
+    acc = acc + v.y;
+    acc = acc + v.z;
+    acc = acc + v.w;
+  }
+  out[2 * r + lane] = acc;
+}
 }  // namespace
 
 int main() {
@@ -371,7 +485,7 @@ int main() {
   (void)hipMalloc(&gx, n * 4);
   (void)hipMalloc(&gy, n * 4);
   (void)hipMalloc(&o1, kRuns * 8);
-  (void)hipMalloc(&o2, kRuns * 8);
+  (void)hipMalloc(&o2, kRuns * 16);
   (void)hipMemcpy(gx, hx.data(), n * 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(gy, hy.data(), n * 4, hipMemcpyHostToDevice);
   std::vector<float> ref(2 * kRuns);
@@ -489,6 +603,13 @@ int main() {
            ms * 1e3, ms * 1e6 / kWalkFull * 2.4, bad);
   }
   run("prod", [&] { hipLaunchKernelGGL(k_prod, kRuns, 64, 0, 0, gx, gy, o1); }, o1);
+  run("gring-8", [&] { hipLaunchKernelGGL(k_gring<8>, kRuns, 64, 0, 0, gx, gy, o2); }, o2);
+  run("gring-16", [&] { hipLaunchKernelGGL(k_gring<16>, kRuns, 64, 0, 0, gx, gy, o2); }, o2);
+  run("gring-32", [&] { hipLaunchKernelGGL(k_gring<32>, kRuns, 64, 0, 0, gx, gy, o2); }, o2);
+  run("gpf-16-8k", [&] { hipLaunchKernelGGL((k_gpf<16, 8192>), kRuns, 128, 0, 0, gx, gy, o2); }, o2);
+  run("gpf-32-8k", [&] { hipLaunchKernelGGL((k_gpf<32, 8192>), kRuns, 128, 0, 0, gx, gy, o2); }, o2);
+  run("gpf-32-32k", [&] { hipLaunchKernelGGL((k_gpf<32, 32768>), kRuns, 128, 0, 0, gx, gy, o2); }, o2);
+  run("gpf-8-8k", [&] { hipLaunchKernelGGL((k_gpf<8, 8192>), kRuns, 128, 0, 0, gx, gy, o2); }, o2);
   run("ldswin2-16", [&] { hipLaunchKernelGGL(k_lds_window2<16>, kRuns, 64, 0, 0, gx, gy, o2); }, o2);
   run("ldswin2-8", [&] { hipLaunchKernelGGL(k_lds_window2<8>, kRuns, 64, 0, 0, gx, gy, o2); }, o2);
   run("ldswin2-32", [&] { hipLaunchKernelGGL(k_lds_window2<32>, kRuns, 64, 0, 0, gx, gy, o2); }, o2);
