@@ -20,6 +20,8 @@ segment-count guesses from the previous run are exercised inside the timed regio
   --dense        configs[4]'s density (~500k points per frame, rpt.synth.dense_config)
   --h2d-steps K  also time K steps that first copy the echo from pinned host memory (reported
                  as `h2d_inclusive`, never as `value`)
+40 timed steps by default: with stacks in flight the timed region holds the pipeline's fill and
+drain (about one step), so short runs report less; `steady_state` gives the rate without them.
 At N=1 three stacks are in flight by default (`--lanes 3`: native handles on three streams;
 step k+1's device work runs while step k's host stage and readbacks finish, and the stacks'
 latency-bound kernels share the CUs; 3 measured +4-5 % over 2 in interleaved same-box runs, 4
@@ -174,7 +176,7 @@ def _k5_share(dev, cfg, label, wkey):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--total-frames", type=int, default=1000,
                     help="frames of the one global stack, split over the ranks (strong scaling)")

@@ -653,20 +653,35 @@ static bool land_u8_enabled() {
   return on;
 }
 
+// the grid's counts and sums (and a caller's 64-bit counter) zeroed in ONE launch: two fills
+// and a third for the counter each cost a launch right after the host-synchronous bounds
+// readback, when the GPU idles on the host issuing them
+__global__ void k_zero_land(int32_t* __restrict__ cnt, double* __restrict__ tot, int64_t cells,
+                            int64_t* __restrict__ extra) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cells;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    cnt[i] = 0;
+    tot[i] = 0.0;
+  }
+  if (extra && blockIdx.x == 0 && threadIdx.x == 0) *extra = 0;
+}
+
 // cell_out (nullable, [n], int32 cells < 2^31): each point's grid cell, for land_filter_cells
 // u8_vals: every val is an integer in [0, 255] (points of a u8 echo; packed-atomic kernel)
+// zero_also (nullable): a 64-bit device counter zeroed with the grid
 int32_t land_grid_cells(const float* x, const float* y, const float* val, int64_t n,
                         const double* xe, int32_t nxe, const double* ye, int32_t nye,
                         int32_t* cnt, double* tot, int32_t* cell_out, hipStream_t st,
-                        int32_t u8_vals) {
+                        int32_t u8_vals, int64_t* zero_also) {
   if (nxe < 2 || nye < 2) {
     set_error("rpt_land_grid: need at least two edges per axis");
     return RPT_EINVAL;
   }
   const int64_t cells = (int64_t)(nxe - 1) * (nye - 1);
   if (cell_out && cells >= (int64_t(1) << 31)) cell_out = nullptr;
-  RPT_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t) * cells, st));
-  RPT_HIP(hipMemsetAsync(tot, 0, sizeof(double) * cells, st));
+  hipLaunchKernelGGL(k_zero_land, dim3(grid_for(cells, 256, 1024)), dim3(256), 0, st, cnt, tot,
+                     cells, zero_also);
+  RPT_CHECK_LAUNCH();
   if (n == 0) return RPT_OK;
   const int64_t ne_al = ((int64_t)nxe + nye + 1) & ~int64_t(1);
   const size_t lds = (size_t)ne_al * 8 + (size_t)cells * 12;
@@ -698,7 +713,7 @@ int32_t land_grid_cells(const float* x, const float* y, const float* val, int64_
 int32_t land_grid(const float* x, const float* y, const float* val, int64_t n, const double* xe,
                   int32_t nxe, const double* ye, int32_t nye, int32_t* cnt, double* tot,
                   hipStream_t st) {
-  return land_grid_cells(x, y, val, n, xe, nxe, ye, nye, cnt, tot, nullptr, st, 0);
+  return land_grid_cells(x, y, val, n, xe, nxe, ye, nye, cnt, tot, nullptr, st, 0, nullptr);
 }
 
 // n_land_dev: int32 land-cell counter on the device, zeroed by the caller (no readback)

@@ -217,11 +217,12 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
     RPT_TRY(land_tot.ensure((size_t)cells, st));
     RPT_TRY(land_mask.ensure((size_t)cells, st));
     RPT_TRY(land_cell.ensure(cap, st));
-    RPT_TRY(land_grid_cells(x.p, y.p, v.p, N, edges.p, nxe, edges.p + nxe, nye, land_cnt.p,
-                            land_tot.p, land_cell.p, st, p.echo_dtype == RPT_ECHO_U8 ? 1 : 0));
-    // the land-cell count accumulates (int32) into the low half of a zeroed int64 slot
+    // the land-cell count accumulates (int32) into the low half of an int64 slot, zeroed with
+    // the grid
     RPT_TRY(scal.ensure(4, st));
-    RPT_HIP(hipMemsetAsync(scal.p, 0, sizeof(int64_t), st));
+    RPT_TRY(land_grid_cells(x.p, y.p, v.p, N, edges.p, nxe, edges.p + nxe, nye, land_cnt.p,
+                            land_tot.p, land_cell.p, st, p.echo_dtype == RPT_ECHO_U8 ? 1 : 0,
+                            reinterpret_cast<int64_t*>(scal.p)));
     RPT_TRY(land_mask_dev(land_cnt.p, land_tot.p, cells, n_built, p.land_persistence,
                           p.land_min_intensity, land_mask.p, reinterpret_cast<int32_t*>(scal.p),
                           st));

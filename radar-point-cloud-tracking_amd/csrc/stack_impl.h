@@ -35,7 +35,7 @@ int32_t bounds_xy(const float* x, const float* y, int64_t n, float* out4, hipStr
 int32_t land_grid_cells(const float* x, const float* y, const float* val, int64_t n,
                         const double* xe, int32_t nxe, const double* ye, int32_t nye,
                         int32_t* cnt, double* tot, int32_t* cell_out, hipStream_t st,
-                        int32_t u8_vals);
+                        int32_t u8_vals, int64_t* zero_also = nullptr);
 int32_t land_mask(const int32_t* cnt, const double* tot, int64_t cells, int64_t num_frames,
                   double pthr, double ithr, uint8_t* land, int64_t* n_land_host,
                   hipStream_t st);
