@@ -20,12 +20,16 @@ segment-count guesses from the previous run are exercised inside the timed regio
   --dense        configs[4]'s density (~500k points per frame, rpt.synth.dense_config)
   --h2d-steps K  also time K steps that first copy the echo from pinned host memory (reported
                  as `h2d_inclusive`, never as `value`)
-40 timed steps by default: with stacks in flight the timed region holds the pipeline's fill and
-drain (about one step), so short runs report less; `steady_state` gives the rate without them.
-At N=1 three stacks are in flight by default (`--lanes 3`: native handles on three streams;
+100 timed steps by default: with stacks in flight the timed region holds the pipeline's fill and
+drain (about one stack time per lane in flight), so short runs report less (1000 frames, same box:
+6.12 Gpoints/s at 20 steps, 6.47 at 40, 6.9 at 100); `steady_state` gives the rate without them.
+At N=1 five stacks are in flight by default (`--lanes 5`: native handles on five streams;
 step k+1's device work runs while step k's host stage and readbacks finish, and the stacks'
-latency-bound kernels share the CUs; 3 measured +4-5 % over 2 in interleaved same-box runs, 4
-no better); `one_stack_in_flight` repeats the steps strictly one after
+latency-bound kernels share the CUs; interleaved same-box runs with every lane set up, 40 steps:
+2 lanes 8.4 ms per step, 3 lanes 7.9-8.3, 4 lanes 8.1, 5 lanes 7.95, 6 lanes 7.9-8.2; 100 steps:
+3 lanes 7.34-7.67, 5 lanes 7.35-7.43, steady state 7.06-7.38 against 6.77-6.92).  Every lane runs
+one untimed stack before the warm-up steps (its buffers are allocated on first use: a lane left
+cold cost ~80 ms inside the timed region); `one_stack_in_flight` repeats the steps strictly one after
 another, and K5's roofline is taken from that leg (K5 alone on the GPU).
 At N>1 (the frame-sharded path) one stack is in flight per rank by default; `--lanes 3` keeps
 three, their collectives through ONE communicator in a fixed software-pipeline order
@@ -176,7 +180,7 @@ def _k5_share(dev, cfg, label, wkey):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--total-frames", type=int, default=1000,
                     help="frames of the one global stack, split over the ranks (strong scaling)")
@@ -201,8 +205,9 @@ def main():
                     help="sharded runs: ShardedStackPipeline (HipOps stages composed in Python) "
                          "instead of the native shard driver")
     ap.add_argument("--lanes", type=int, default=None,
-                    help="stacks in flight at once (default 3 at one rank: native handles on "
-                         "separate streams; default 1 at N>1 ranks, where a lane is a "
+                    help="stacks in flight at once (default 5 at one rank, 3 with --sharded: "
+                         "native handles on separate streams; default 1 at N>1 ranks, where a "
+                         "lane is a "
                          "NativeShardPipeline with its own stream and thread, all lanes on ONE "
                          "process group in rpt.dist.CommSequencer's order); 1 = strictly one "
                          "after another")
@@ -225,7 +230,7 @@ def main():
         # several lanes share one RCCL communicator only through CommSequencer's order, which has
         # run on gloo (8 ranks) and on RCCL at one rank (forced collectives), never on RCCL across
         # GPUs: one lane per rank until it has (--lanes 3 opts in)
-        args.lanes = 3 if world == 1 else 1
+        args.lanes = (3 if args.sharded else 5) if world == 1 else 1
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # --sharded: the frame-sharded multi-GPU path even at one rank (measures its per-rank cost)
     dist = world > 1 or args.sharded
@@ -318,6 +323,11 @@ def main():
     def points_of(r):  # K1 points of the whole (global) stack of a run
         return float(r.n_points_global if dist else r.n_points)
 
+    if not dist and args.lanes > 1:
+        # lane setup (untimed, before the warm-up steps): one stack per lane allocates that lane's
+        # buffers, whatever --warmup is
+        for k in range(args.lanes):
+            resolve(run(echoes[k % E])).finish()
     for k in range(args.warmup):
         resolve(run(echoes[k % E])).finish()
     torch.cuda.synchronize(dev)
