@@ -44,8 +44,12 @@ def _cfg(name):
     return SynthConfig(**_gold(name)["synth"])
 
 
-@pytest.mark.timeout(600)
-def test_bench_stacks_lanes3_match_oracle(gpu):
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("lanes", [3, 5])
+def test_bench_stacks_lanes3_match_oracle(gpu, lanes):
+    """The bench's submit path with `lanes` stacks in flight (5: the N=1 default): every run's
+    labels, per-frame cluster rows and tracks against the oracle digests; the first two lanes
+    switch workloads on their second run."""
     from rpt.pipeline import FrameStackPipeline, PathParams
     from rpt.synth import DeviceSynth
 
@@ -57,15 +61,16 @@ def test_bench_stacks_lanes3_match_oracle(gpu):
     c0 = cfgs[0]
     assert all(np.array_equal(d.geo.cos_t, dss[0].geo.cos_t) for d in dss)
     pipe = FrameStackPipeline(c0.gains, c0.rows, c0.bins, PathParams(), gpu, async_host=True,
-                              lanes=3)
+                              lanes=lanes)
     pipe.set_geometry(np.full(c0.rows, c0.scale, np.float32), dss[0].geo.cos_t,
                       dss[0].geo.sin_t, c0.n_frames * len(c0.gains))
-    order = [0, 1, 0, 1, 0]   # lanes 0,1,2,0,1: lanes 0 and 1 switch workloads on their 2nd run
+    # lanes 0 .. lanes-1, then 0 and 1 again: lanes 0 and 1 switch workloads on their 2nd run
+    order = [k % 2 for k in range(lanes)] + [lanes % 2, (lanes + 1) % 2]
     futs = [pipe.submit(echoes[k], keep_points=True) for k in order]
     for i, (k, f) in enumerate(zip(order, futs)):
         res = f.result().finish()
         got = device_digest(res)
-        compare(got, _gold(names[k]), f"run {i} ({names[k]}, lane {i % 3})")
+        compare(got, _gold(names[k]), f"run {i} ({names[k]}, lane {i % lanes})")
         del res
 
 
