@@ -15,6 +15,7 @@ stream.
 """
 from __future__ import annotations
 
+import queue
 import time
 from concurrent.futures import Future, ThreadPoolExecutor
 from dataclasses import dataclass, field
@@ -79,16 +80,19 @@ class FrameStackPipeline:
 
     def __init__(self, gains: Sequence[int], rows: int, bins: int, params: PathParams = None,
                  device=None, timing: bool = False, async_host: bool = False,
-                 host_workers: int = 2, lanes: int = 1):
+                 host_workers: int = 2, lanes: int = 1, round_robin: bool = False):
         """async_host: the host stage (cluster order + tracker, sequential C++) of a run executes
         on a pool of host_workers threads while the caller goes on to the next runs' device
         work (runs are independent, so their host stages may overlap each other);
         StackResult.finish() waits for a run's host stage.
 
         lanes > 1: submit() runs successive stacks on `lanes` native handles, each on its own
-        HIP stream and submission thread, so one stack's kernels fill the GPU while another
-        waits on a size readback or runs a latency-bound stage (the library keeps its scratch
-        and look-back state per stream)."""
+        HIP stream, so one stack's kernels fill the GPU while another waits on a size readback
+        or runs a latency-bound stage (the library keeps its scratch and look-back state per
+        stream).  A run takes whichever lane is free when a worker thread picks it up: streams
+        beyond the process's hardware queues share a queue and progress slower, and a fixed
+        round-robin left the last runs of the slow lanes finishing long after the others
+        (round_robin=True keeps that policy for comparisons)."""
         self.dev = require_gpu(device)
         self.gains = [int(g) for g in gains]
         if sorted(self.gains) != self.gains:
@@ -101,9 +105,13 @@ class FrameStackPipeline:
         self._hs = [self.lib.rpt_stack_create() for _ in range(lanes)]
         self._h = self._hs[0]
         self._streams = [torch.cuda.Stream(self.dev) for _ in range(lanes)] if lanes > 1 else None
-        self._lane_pool = [ThreadPoolExecutor(max_workers=1) for _ in range(lanes)] \
-            if lanes > 1 else None
+        self._lane_pool = ThreadPoolExecutor(max_workers=lanes) if lanes > 1 else None
+        self._rr = [ThreadPoolExecutor(max_workers=1) for _ in range(lanes)] \
+            if lanes > 1 and round_robin else None
         self._next_lane = 0
+        self._free_lanes = queue.SimpleQueue()
+        for k in range(lanes):
+            self._free_lanes.put(k)
         self.timing = timing
         self._host = ThreadPoolExecutor(max_workers=host_workers) if async_host else None
         self._geo_key = None
@@ -153,12 +161,27 @@ class FrameStackPipeline:
             f = Future()
             f.set_result(self.run(echo, keep_points, keep_core))
             return f
-        lane = self._next_lane
-        self._next_lane = (lane + 1) % len(self._hs)
-        s = self._streams[lane]
-        s.wait_stream(torch.cuda.current_stream(self.dev))  # the echo's producer
-        return self._lane_pool[lane].submit(self._run_lane, self._hs[lane], s.cuda_stream, echo,
-                                            keep_points, keep_core)
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(self.dev))  # the echo's producer
+        if self._rr is not None:
+            lane = self._next_lane
+            self._next_lane = (lane + 1) % len(self._hs)
+            s = self._streams[lane]
+            s.wait_event(ready)
+            return self._rr[lane].submit(self._run_lane, self._hs[lane], s.cuda_stream, echo,
+                                         keep_points, keep_core)
+
+        def task():
+            lane = self._free_lanes.get()
+            try:
+                s = self._streams[lane]
+                s.wait_event(ready)
+                return self._run_lane(self._hs[lane], s.cuda_stream, echo, keep_points,
+                                      keep_core)
+            finally:
+                self._free_lanes.put(lane)
+
+        return self._lane_pool.submit(task)
 
     def _run_lane(self, h, stream: int, echo: torch.Tensor, keep_points: bool,
                   keep_core: bool = False) -> StackResult:
@@ -253,8 +276,10 @@ class FrameStackPipeline:
         return res
 
     def __del__(self):
-        for pool in getattr(self, "_lane_pool", None) or []:
-            pool.shutdown(wait=True)
+        pools = [getattr(self, "_lane_pool", None)] + list(getattr(self, "_rr", None) or [])
+        for pool in pools:
+            if pool is not None:
+                pool.shutdown(wait=True)
         for h in getattr(self, "_hs", None) or []:
             if h:
                 self.lib.rpt_stack_destroy(h)

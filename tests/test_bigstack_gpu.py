@@ -48,8 +48,8 @@ def _cfg(name):
 @pytest.mark.parametrize("lanes", [3, 5])
 def test_bench_stacks_lanes3_match_oracle(gpu, lanes):
     """The bench's submit path with `lanes` stacks in flight (5: the N=1 default): every run's
-    labels, per-frame cluster rows and tracks against the oracle digests; the first two lanes
-    switch workloads on their second run."""
+    labels, per-frame cluster rows and tracks against the oracle digests; two runs more than
+    lanes, alternating the two stacks, so lanes switch workloads."""
     from rpt.pipeline import FrameStackPipeline, PathParams
     from rpt.synth import DeviceSynth
 
@@ -64,13 +64,14 @@ def test_bench_stacks_lanes3_match_oracle(gpu, lanes):
                               lanes=lanes)
     pipe.set_geometry(np.full(c0.rows, c0.scale, np.float32), dss[0].geo.cos_t,
                       dss[0].geo.sin_t, c0.n_frames * len(c0.gains))
-    # lanes 0 .. lanes-1, then 0 and 1 again: lanes 0 and 1 switch workloads on their 2nd run
+    # every lane busy, then two more runs: the lanes that take them switch workloads (a run takes
+    # whichever lane is free)
     order = [k % 2 for k in range(lanes)] + [lanes % 2, (lanes + 1) % 2]
     futs = [pipe.submit(echoes[k], keep_points=True) for k in order]
     for i, (k, f) in enumerate(zip(order, futs)):
         res = f.result().finish()
         got = device_digest(res)
-        compare(got, _gold(names[k]), f"run {i} ({names[k]}, lane {i % lanes})")
+        compare(got, _gold(names[k]), f"run {i} ({names[k]}, {lanes} lanes)")
         del res
 
 
