@@ -658,35 +658,49 @@ __global__ __launch_bounds__(kBlock) void k_group_starts(const int64_t* __restri
                                                         uint64_t* __restrict__ gword,
                                                         uint32_t* __restrict__ list,
                                                         uint32_t* __restrict__ list_n) {
+  // the unstaged groups collect in a block LDS list over the whole grid-stride loop and go out
+  // with ONE global atomic per block (one per block iteration was ~12 k same-address atomics per
+  // 1000-frame stack, serialised in L2); a block whose list fills appends the rest directly
+  constexpr uint32_t kCap = 2048;
+  __shared__ uint32_t s_list[kCap];
   __shared__ uint32_t s_n, s_base;
+  if (threadIdx.x == 0) s_n = 0u;
+  __syncthreads();
+  // power-of-two strides (the reference's 4) by shifts instead of 64-bit divisions
+  const bool pow2 = (stride & (stride - 1u)) == 0u;
+  const uint32_t sh = (uint32_t)__builtin_ctz(stride);
   for (uint32_t b0 = blockIdx.x * kBlock; b0 < n_groups; b0 += gridDim.x * kBlock) {
-    if (threadIdx.x == 0) s_n = 0u;
-    __syncthreads();
     const uint32_t g = b0 + threadIdx.x;
-    bool un = false;
-    uint32_t slot = 0u;
     if (g < n_groups) {
       const uint32_t f = g / gpf;
       const int64_t p0 = gprefix[g];
       const uint64_t rank = (uint64_t)(p0 - gprefix[(int64_t)f * gpf]);
       const uint64_t total = (uint64_t)(gprefix[g + 1] - p0);
-      const uint64_t first = (rank + stride - 1u) / stride;
-      const uint64_t last = (rank + total + stride - 1u) / stride;
+      const uint64_t first = pow2 ? ((rank + stride - 1u) >> sh) : (rank + stride - 1u) / stride;
+      const uint64_t last =
+          pow2 ? ((rank + total + stride - 1u) >> sh) : (rank + total + stride - 1u) / stride;
       const uint64_t gs = (uint64_t)file_offsets[f] + first;
       // slot position of the first emitted output's entry: its in-group rank, or with stride 4
       // (residues packed, stage_pos) the base of its residue
       const uint64_t ph = first * stride - rank;
       const uint64_t phase = stride == 4u ? (uint64_t)phase_base((uint32_t)ph, (uint32_t)total)
                                           : ph;
-      un = last > first && total > (uint64_t)kStageSlots;
+      const bool un = last > first && total > (uint64_t)kStageSlots;
       gword[g] = gs | (phase << kGsBits) | (un ? kUnstaged : 0ull);
-      if (un) slot = atomicAdd(&s_n, 1u);
+      if (un) {
+        const uint32_t slot = atomicAdd(&s_n, 1u);
+        if (slot < kCap)
+          s_list[slot] = g;
+        else
+          list[atomicAdd(list_n, 1u)] = g;
+      }
     }
-    __syncthreads();
-    if (threadIdx.x == 0 && s_n) s_base = atomicAdd(list_n, s_n);
-    __syncthreads();
-    if (un) list[s_base + slot] = g;
   }
+  __syncthreads();
+  const uint32_t m = min(s_n, kCap);
+  if (threadIdx.x == 0 && m) s_base = atomicAdd(list_n, m);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < m; i += kBlock) list[s_base + i] = s_list[i];
 }
 
 // largest g in [lo, hi) with gs(g) <= O, given gs(lo) <= O: one wave, 64-ary search
