@@ -415,16 +415,30 @@ __global__ void k_cell_start_end(int32_t* __restrict__ cell_start, int64_t cells
   if (threadIdx.x == 0) cell_start[cells + 1] = cell_start[cells];
 }
 
-// slab_lo[s] = first point of slab s (points ordered by slab), slab_lo[nt] = n
+// slab_lo[s] = first point of slab s (points ordered by slab), slab_lo[nt] = n: ONE WAVE per
+// slab, a 64-ary search (64 probes per round: ~5 dependent rounds over 50 M points instead of a
+// thread's 26-step binary search)
 __global__ void k_slab_lo(const float* __restrict__ t, int64_t n, Geom g,
                           int32_t* __restrict__ slab_lo) {
-  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s <= g.nt; s += gridDim.x * blockDim.x) {
-    int64_t lo = 0, hi = n;
+  const int lane = threadIdx.x & 63;
+  const int64_t wpb = blockDim.x / 64;
+  for (int64_t s = (int64_t)blockIdx.x * wpb + threadIdx.x / 64; s <= g.nt;
+       s += (int64_t)gridDim.x * wpb) {
+    int64_t lo = 0, hi = n;  // the first point of slab >= s lies in [lo, hi]
     while (lo < hi) {
-      const int64_t m = (lo + hi) >> 1;
-      if (slab_of(t[m], g) < s) lo = m + 1; else hi = m;
+      const int64_t step = (hi - lo + 63) / 64;
+      const int64_t idx = lo + (int64_t)lane * step;
+      const bool below = idx < hi && slab_of(t[idx < hi ? idx : lo], g) < s;  // a lane prefix
+      const int c = __popcll(__ballot(below));
+      if (c == 0) {
+        hi = lo;
+      } else {
+        const int64_t nlo = lo + (int64_t)(c - 1) * step + 1;
+        hi = min(hi, lo + (int64_t)c * step);
+        lo = nlo;
+      }
     }
-    slab_lo[s] = (int32_t)(s == g.nt ? n : lo);
+    if (lane == 0) slab_lo[s] = (int32_t)(s == g.nt ? n : lo);
   }
 }
 
@@ -4438,8 +4452,8 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
   const bool bucket = bucket_mode && D == 2 && hb.n_finite_t == n && !hb.t_descends &&
                       (int64_t)nx * ny <= kBucketCells && nt < (int64_t(1) << 31);
   if (bucket) {
-    hipLaunchKernelGGL(k_slab_lo, dim3(grid_for(nt + 1, kBlock, 1024)), dim3(kBlock), 0, st, t, n,
-                       g, slab_lo);
+    hipLaunchKernelGGL(k_slab_lo, dim3(grid_for(64 * (nt + 1), kBlock, 4096)), dim3(kBlock), 0,
+                       st, t, n, g, slab_lo);
     RPT_HIP(hipMemsetAsync(occ_bits, 0, sizeof(uint32_t) * (C1 / 32 + 2), st));
     // the slabs write their occupied cells (ascending) into hpos at their point offsets, the
     // occupancy bits and their counts; one scan over the slabs and a gather give the list
