@@ -400,6 +400,15 @@ int32_t rpt_shard_finish(rpt_shard* h, const int64_t* gathered_pairs, int32_t wo
 int32_t rpt_shard_labels(const rpt_shard* h, const int32_t* local_to_global, int64_t n_reps,
                          int32_t* out, void* stream);
 int32_t rpt_shard_frame_offsets(const rpt_shard* h, int32_t which, int64_t* out);
+/* ids the device equivalence merge of rpt_shard_finish takes (default and maximum 8192); a step
+ * whose gathered pairs hold more is merged on the host (flag 2, rpt_merge_equivalences).  Lower
+ * limits (0: always the host merge) exist so tests reach that path. */
+int32_t rpt_shard_set_merge_limit(rpt_shard* h, int32_t max_ids);
+/* device copies of the own kept points of the last step (each output nullable, dev [n_kept]):
+ * x, y, intensity, frame slot, and (after rpt_shard_window) their K5 core flags -- for
+ * full-size invariant checks, on the stream of that step, before the handle's next step */
+int32_t rpt_shard_points(const rpt_shard* h, float* x, float* y, float* intensity,
+                         int32_t* point_frame, uint8_t* core, void* stream);
 /* host, over the all-gathered packed results (host int64 [world][row_words]): sizes[4] = total
  * segments, built frames, frames, clusters (distinct representatives) */
 int32_t rpt_shard_gathered_sizes(const int64_t* gathered, int32_t world, int64_t row_words,

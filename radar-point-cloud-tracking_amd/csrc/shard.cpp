@@ -304,10 +304,11 @@ __global__ void k_store_count(const unsigned long long* __restrict__ count,
 // Union of every rank's equivalence pairs (the all-gathered rows [count | 2*count ids], rows of
 // row_words int64): ONE workgroup, ids in LDS -- bitonic sort, distinct ids, min-hooking
 // union-find -- so every rank derives the same (keys sorted, vals = class minimum).  meta[0] = the
-// number of ids, or -1 when more than kMergeMax would be merged (the caller merges on the host);
+// number of ids, or -1 when more than merge_max (<= kMergeMax) would be merged (the caller merges
+// on the host; rpt_shard_set_merge_limit lowers merge_max so tests reach that path);
 // meta[1] = 1 when some row holds more pairs than its capacity (the step is redone).
 __global__ __launch_bounds__(1024) void k_merge_pairs(const int64_t* __restrict__ g, int world,
-                                                      int64_t row_words,
+                                                      int64_t row_words, int merge_max,
                                                       int64_t* __restrict__ keys,
                                                       int64_t* __restrict__ vals,
                                                       int64_t* __restrict__ meta) {
@@ -325,7 +326,7 @@ __global__ __launch_bounds__(1024) void k_merge_pairs(const int64_t* __restrict_
       ovf |= c > cap ? 1 : 0;
       tot += c < cap ? c : cap;
     }
-    s_total = 2 * tot > kMergeMax ? -1 : (int32_t)tot;
+    s_total = 2 * tot > merge_max ? -1 : (int32_t)tot;
     s_ovf = ovf;
   }
   __syncthreads();
@@ -608,6 +609,7 @@ struct rpt_shard {
   int64_t n_window = 0, k_prev_total = 0;
   bool land = false;
   bool k9_radix = false;
+  int32_t merge_max = kMergeMax;  // ids the device merge takes (rpt_shard_set_merge_limit)
   hipEvent_t ev[2] = {};         // around the core-flag pass (params.timing)
   bool ev_ok = false, core_timed = false;
   ~rpt_shard() {
@@ -1050,7 +1052,7 @@ int32_t rpt_shard_finish(rpt_shard* h, const int64_t* gathered_pairs, int32_t wo
   RPT_TRY(h->meta.ensure(4, st));
   if (gathered_pairs) {
     hipLaunchKernelGGL(k_merge_pairs, dim3(1), dim3(1024), 0, st, gathered_pairs, world,
-                       row_words, h->keys.p, h->vals.p, h->meta.p);
+                       row_words, (int)h->merge_max, h->keys.p, h->vals.p, h->meta.p);
     RPT_CHECK_LAUNCH();
   } else {
     RPT_TRY(S.up.ensure(sizeof(int64_t) * (size_t)(2 * n_keys + 2), st));
@@ -1292,6 +1294,44 @@ int32_t rpt_shard_host_stage(const int64_t* g, int32_t world, int64_t row_words,
                                          cys.data(), nullptr);
     if (r < 0) return -r;
   }
+  return RPT_OK;
+}
+
+int32_t rpt_shard_set_merge_limit(rpt_shard* h, int32_t max_ids) {
+  clear_error();
+  if (!h || max_ids < 0) {
+    set_error("rpt_shard_set_merge_limit: bad arguments");
+    return RPT_EINVAL;
+  }
+  h->merge_max = std::min<int32_t>(max_ids, kMergeMax);
+  return RPT_OK;
+}
+
+int32_t rpt_shard_points(const rpt_shard* h, float* x, float* y, float* intensity,
+                         int32_t* point_frame, uint8_t* core, void* stream) {
+  clear_error();
+  if (!h) {
+    set_error("rpt_shard_points: bad arguments");
+    return RPT_EINVAL;
+  }
+  const int64_t K = h->info.n_kept;
+  if (K == 0) return RPT_OK;
+  const rpt_stack& S = h->st;
+  if (core && (!h->core.p || h->core.cap < (size_t)(h->info.n_prev + K))) {
+    set_error("rpt_shard_points: no core flags (rpt_shard_window first)");
+    return RPT_EINVAL;
+  }
+  const hipStream_t st = as_stream(stream);
+  const bool l = S.land_applied;
+  auto cp = [&](void* dst, const void* src, size_t bytes) -> int32_t {
+    if (dst) RPT_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st));
+    return RPT_OK;
+  };
+  RPT_TRY(cp(x, l ? S.x2.p : S.x.p, sizeof(float) * (size_t)K));
+  RPT_TRY(cp(y, l ? S.y2.p : S.y.p, sizeof(float) * (size_t)K));
+  RPT_TRY(cp(intensity, l ? S.v2.p : S.v.p, sizeof(float) * (size_t)K));
+  RPT_TRY(cp(point_frame, l ? S.pf2.p : S.pf.p, sizeof(int32_t) * (size_t)K));
+  RPT_TRY(cp(core, h->core.p + h->info.n_prev, (size_t)K));
   return RPT_OK;
 }
 

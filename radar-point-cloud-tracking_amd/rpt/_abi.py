@@ -221,6 +221,8 @@ _SIGS = [
                                      C.c_int64, C.c_int32, vp, C.c_int64, vp]),
     ("rpt_shard_labels", C.c_int32, [vp, vp, C.c_int64, vp, vp]),
     ("rpt_shard_frame_offsets", C.c_int32, [vp, C.c_int32, c_i64p]),
+    ("rpt_shard_set_merge_limit", C.c_int32, [vp, C.c_int32]),
+    ("rpt_shard_points", C.c_int32, [vp, vp, vp, vp, vp, vp, vp]),
     ("rpt_shard_gathered_sizes", C.c_int32, [c_i64p, C.c_int32, C.c_int64, c_i64p]),
     ("rpt_shard_host_stage", C.c_int32, [c_i64p, C.c_int32, C.c_int64, vp, c_i32p, c_i32p,
                                          c_i64p, c_i64p, c_f32p, c_f32p, c_f32p, c_i64p, c_i64p,

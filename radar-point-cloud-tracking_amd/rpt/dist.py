@@ -540,6 +540,11 @@ class CommSequencer:
                 raise RuntimeError("collective sequence aborted by another stack") \
                     from self.failed
 
+    def _skip(self, step: int, phase: int):
+        """A slot the step does not use: it issues no collective, so it needs no turn (waiting
+        for it could wait on a step that is not submitted yet); the step just moves past it."""
+        self._release(step, phase)
+
     def _release(self, step: int, phase: int):
         with self.cv:
             if phase + 1 >= self.P:
@@ -564,16 +569,16 @@ class CommSequencer:
 
 
 class _StepSlots:
-    """One step's walk through its slots: slot(k) first passes the skipped slots < k (their
-    turns still come in order), close() passes the remaining ones."""
+    """One step's walk through its slots: slot(k) first moves past the skipped slots < k
+    without taking their turns (no collective runs in them), close() past the remaining ones
+    (e.g. the rare redo slot) -- so a finished step never waits on later submissions."""
 
     def __init__(self, seq: CommSequencer, step: int):
         self.seq, self.step, self.next = seq, step, 0
 
     def _pass(self, upto: int):
         while self.next < upto:
-            self.seq._acquire(self.step, self.next)
-            self.seq._release(self.step, self.next)
+            self.seq._skip(self.step, self.next)
             self.next += 1
 
     @contextlib.contextmanager
@@ -766,6 +771,7 @@ class NativeShardPipeline:
                                  fsn.data_ptr() if has_n else None, C_.byref(info), st),
             "rpt_shard_window")
         n_own, n_head, n_tail = int(info.n_kept), int(info.n_head), int(info.n_tail)
+        self._n_own = n_own
         n_prev, n_next = int(info.n_prev), int(info.n_next)
         n_tot = n_prev + n_own + n_next
         self._core_ms = self.timing and n_tot > 0
@@ -937,6 +943,29 @@ class NativeShardPipeline:
 
         return host_stage
 
+    def set_merge_limit(self, max_ids: int):
+        """Ids the device equivalence merge takes (default and maximum 8192); a step whose
+        gathered pairs hold more is merged on the host (rpt_merge_equivalences, the redo slot).
+        0 sends every step with a pair there: tests use it to reach that path."""
+        self._abi.check(self.lib.rpt_shard_set_merge_limit(self.h, int(max_ids)),
+                        "rpt_shard_set_merge_limit")
+
+    def points_local(self) -> Dict[str, torch.Tensor]:
+        """The own kept points of the last run (device copies, for checks): x, y, v, frame slot
+        and the K5 core flag of each."""
+        from ._device import stream_handle
+        n = int(getattr(self, "_n_own", 0))
+        out = {"x": torch.empty(n, dtype=torch.float32, device=self.dev),
+               "y": torch.empty(n, dtype=torch.float32, device=self.dev),
+               "v": torch.empty(n, dtype=torch.float32, device=self.dev),
+               "frame": torch.empty(n, dtype=torch.int32, device=self.dev),
+               "core": torch.empty(n, dtype=torch.uint8, device=self.dev)}
+        if n:
+            self._abi.check(self.lib.rpt_shard_points(
+                self.h, *[out[k].data_ptr() for k in ("x", "y", "v", "frame", "core")],
+                stream_handle(self.dev)), "rpt_shard_points")
+        return out
+
     def labels_local(self) -> torch.Tensor:
         """Global labels (device int32, a copy) of this rank's kept points of the last run (reads
         every rank's representative table back: for checks, not the hot path)."""
@@ -1026,8 +1055,10 @@ class ShardLanes:
         self._step += 1
         li = step % len(self.pipes)
         pipe, s = self.pipes[li], self.streams[li]
-        self.seq.register(step)
-        # one rank: every collective is the identity, nothing to order
+        # one rank: every collective is the identity, nothing to order (and nothing registered:
+        # an unsequenced step never releases its sequencer entries)
+        if self.sequenced:
+            self.seq.register(step)
         slots = self.seq.step(step) if self.sequenced else _NoSlots()
         fut = ShardStepFuture(self.seq)
 

@@ -193,7 +193,30 @@ def test_dense_config4_share_invariants(gpu):
 
 @pytest.mark.timeout(900)
 def test_dense_above_2_26_points_invariants(gpu):
-    """140 dense frames: ~68.7 M points enter ST-DBSCAN, past 2^26 = 67.1 M, where K5's fill
-    pass keeps its per-cell (original, sorted) minima in 64 bits (csrc/stdbscan.hip
-    k_core_fill); the configs[4] share at fewer than 8 GPUs is above it.  _dense_invariants."""
+    """140 dense frames: ~68.7 M points enter ST-DBSCAN, past 2^26 = 67.1 M (the configs[4] share
+    at fewer than 8 GPUs is above it), through the shipped (fused) K5: its per-cell (original,
+    sorted) minima are u64 pairs at every size (k_slab_bucket / k_cell_box / k_core_slow), so this
+    covers the index arithmetic of the default path past 2^26.  _dense_invariants."""
     _dense_invariants(gpu, 140, 1 << 26)
+
+
+@pytest.mark.timeout(900)
+def test_dense_above_2_26_unfused_k5_invariants():
+    """The same 140 dense frames through the A/B build's separate K5 fill pass (librpt_ab.so,
+    RPT_K5_FUSED=0): the only K5 form that packs a cell's (original << 6 | lane) minimum into 32
+    bits below 2^26 points and switches to the 64-bit segmented minimum above it
+    (csrc/stdbscan.hip k_core_fill); that branch runs here.  _dense_invariants in a child
+    process (the library is chosen at load time)."""
+    from rpt import _build
+
+    assert _build.LIB_AB.exists(), "librpt_ab.so missing: run __graft_entry__.build()"
+    tests = str(Path(__file__).resolve().parent)
+    code = (f"import sys\nsys.path[:0] = {[tests, *sys.path]!r}\n"
+            "import torch\nfrom rpt import _abi\n"
+            "assert _abi.load()._name.endswith('librpt_ab.so')\n"
+            "from test_bigstack_gpu import _dense_invariants\n"
+            "_dense_invariants(torch.device('cuda', 0), 140, 1 << 26)\nprint('UNFUSED_OK')\n")
+    env = dict(os.environ, RPT_LIB=str(_build.LIB_AB), RPT_K5_FUSED="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=840)
+    assert r.returncode == 0 and "UNFUSED_OK" in r.stdout, (r.stdout + r.stderr)[-4000:]

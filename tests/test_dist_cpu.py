@@ -316,3 +316,37 @@ def test_comm_sequencer_abort_releases_waiters():
     seq.abort(ValueError("step 0 failed"))
     t.join(5)
     assert not t.is_alive() and err
+
+
+def test_comm_sequencer_skipped_redo_slot_does_not_wait():
+    """The advisor's case (L = 3, P = 8, d = 3): step 1's unused redo slot 7 falls at time 10,
+    after the not-yet-submitted step 3's slot 0 at time 9.  Skipped slots issue no collective, so
+    moving past them takes no turn: steps 0 and 1 finish with the group still open and step 3
+    never submitted; step 2 (its phase 6 at time 12 follows step 3's phase 0) finishes once the
+    group closes."""
+    import threading
+
+    from rpt.dist import CommSequencer
+
+    seq = CommSequencer(3, 8)
+    for s in range(3):
+        seq.register(s)
+    done = {s: threading.Event() for s in range(3)}
+
+    def run(step):
+        slots = seq.step(step)
+        for p in range(7):          # the seven collectives of a step; slot 7 (redo) unused
+            with slots.slot(p):
+                pass
+        slots.close()
+        done[step].set()
+
+    ts = [threading.Thread(target=run, args=(s,)) for s in range(3)]
+    for t in ts:
+        t.start()
+    assert done[0].wait(5) and done[1].wait(5)
+    assert not done[2].is_set()
+    seq.close_group()
+    assert done[2].wait(5)
+    for t in ts:
+        t.join(5)

@@ -43,16 +43,22 @@ def _run(world, frames, impl, lanes, extra, timeout=600, backend="gloo"):
                                                      (2, 14, "python", 1), (2, 8, "native", 2),
                                                      (3, 6, "native", 3),
                                                      (3, 6, "native-tinycaps", 1),
-                                                     (4, 4, "native-tinycaps", 2)])
+                                                     (4, 4, "native-tinycaps", 2),
+                                                     (3, 6, "native-hostmerge", 1),
+                                                     (2, 8, "native-hostmerge", 2)])
 def test_sharded_gpu_matches_single_gpu(world, frames, impl, lanes):
     """lanes = 2 / 3: stacks in flight (rpt.dist.ShardLanes: a stream and thread per lane, every
     lane's collectives through the ONE process group in the CommSequencer's software-pipeline
     order); each lane's last run is checked.  native-tinycaps: one-pair / 16-word capacities for
     the pair and packed-result gathers, so every step is finished again with grown capacities
-    (the redo slot)."""
+    (the redo slot).  native-hostmerge: device merge limit 0, so every step's equivalence pairs
+    are merged on the host (rpt_merge_equivalences, rpt/dist.py's flag-2 branch of the redo
+    slot: the path a merge of more than 8192 ids takes) and the step finished again with them."""
     extra = []
     if impl == "native-tinycaps":
         impl, extra = "native", ["--tiny-caps"]
+    elif impl == "native-hostmerge":
+        impl, extra = "native", ["--force-host-merge"]
     _run(world, frames, impl, lanes, extra)
 
 
@@ -66,6 +72,21 @@ def test_sharded_dense_giant_component_matches_oracle(world, frames, lanes):
     with the oracle's run_path (union-find ST-DBSCAN) over the whole stack
     (4_temporal_object_tracker.py:466-506, 508-536, 984-991)."""
     _run(world, frames, "native", lanes, ["--dense", "--oracle"], timeout=840)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(1000)
+def test_sharded_config4_full_share_sample_check():
+    """BASELINE configs[4] at its real per-rank shape: 8 gloo ranks sharing the GPU, each with
+    125 dense frames (~490k points per frame, ~61 M points per rank, ~490 M in all, one component
+    chaining the whole stack) through NativeShardPipeline.  No whole-stack reference fits, so
+    every rank checks its core flags and labels against oracle.sample_check's exact
+    neighbourhoods on every point of its first and last floor(eps_t) = 2 frames (the halo, the
+    cross-rank merge and the global numbering all meet there) plus 50,000 random points; rank 0
+    checks the global cluster numbering and its frames' K9 rows (tools/dist_check.py
+    run_sample_check; 4_temporal_object_tracker.py:466-506, 527-531)."""
+    out = _run(8, 125, "native", 1, ["--dense", "--sample-check"], timeout=960)
+    assert out.count("edge-frame points") == 8, out[-4000:]
 
 
 @pytest.mark.gpu

@@ -51,6 +51,14 @@ def main():
     ap.add_argument("--tiny-caps", action="store_true",
                     help="native: one-pair / 16-word capacities for the pair and result gathers "
                          "(every step is finished again with grown ones)")
+    ap.add_argument("--force-host-merge", action="store_true",
+                    help="native: device equivalence-merge limit 0, so every step with a pair "
+                         "is merged on the host (rpt_merge_equivalences, the redo slot)")
+    ap.add_argument("--sample-check", action="store_true",
+                    help="no whole-stack reference: every rank checks its own kept points' core "
+                         "flags and labels with oracle.sample_check (every point of its first "
+                         "and last floor(eps_t) frames + random frames), rank 0 the global "
+                         "cluster numbering and its frames' K9 rows (configs[4] at 8 x 125)")
     ap.add_argument("--force-collectives", action="store_true",
                     help="run world-1 collectives through the backend (rpt.dist.Comm.solo off): "
                          "with --backend nccl this executes the RCCL branch on one GPU")
@@ -77,6 +85,8 @@ def main():
     F = args.frames
     if args.digest:
         sys.exit(run_digest(args, rank, world, dev))
+    if args.sample_check:
+        sys.exit(run_sample_check(args, rank, world, dev))
     cfg = _config(args, F, rank * F)
     ds = DeviceSynth(cfg, dev)
     echo = ds.echo()
@@ -87,6 +97,9 @@ def main():
         lanes = ShardLanes(dev, args.lanes, cfg.gains, cfg.rows, cfg.bins, PathParams())
         lanes.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t,
                            ds.geo.sin_t, F * 3)
+        if args.force_host_merge:
+            for p in lanes.pipes:
+                p.set_merge_limit(0)
         futs = [lanes.submit(echo, rank * F) for _ in range(2 * args.lanes)]
         outs = [f.result().finish() for f in futs]
         torch.cuda.synchronize(dev)
@@ -99,6 +112,8 @@ def main():
                           F * 3)
         if args.tiny_caps:
             pipe._cap_pairs, pipe._cap_out = 1, 16
+        if args.force_host_merge:
+            pipe.set_merge_limit(0)
         res = pipe.run(echo, rank * F)
         runs.append((res, pipe.labels_local()))
     else:
@@ -177,6 +192,154 @@ def run_digest(args, rank, world, dev):
     flag = comm.all_reduce(torch.tensor([1 if ok else 0], dtype=torch.int32), dist.ReduceOp.MIN)
     if rank == 0:
         print(f"[dist_check] digest ok={bool(int(flag.item()) == 1)}", flush=True)
+    dist.destroy_process_group()
+    return 0 if int(flag.item()) == 1 else 1
+
+
+def run_sample_check(args, rank, world, dev):
+    """configs[4] (or any stack) at its real per-rank shape, where no whole-stack reference fits:
+    every rank runs NativeShardPipeline on its F frames, then checks its own kept points against
+    the exact neighbourhoods of oracle.sample_check (4_temporal_object_tracker.py:466-506):
+      * core flag == (neighbour count >= min_samples); a core point's core neighbours all carry
+        its label; a non-core point carries the smallest label among its core neighbours (-1
+        without one) -- on EVERY point of its first and last floor(eps_t) frames (their
+        neighbourhoods cross the rank boundary: the halo, the cross-rank merge and the global
+        label numbering are all in these) and on 10,000 random points of each of 5 random inner
+        frames; the neighbours' edge frames (points, flags, labels) come from them by P2P;
+      * rank 0: the labels in order of their first core point over the whole stack (rank by rank)
+        are exactly 0, 1, 2, ... (ids ascend with each cluster's minimum core index, dense), and
+        its own frames' K9 rows: segment counts = the (frame, label) histogram, the largest and
+        40 random segments' centroids / mean intensities = np.mean (:527-531)."""
+    import oracle
+    from rpt.dist import Comm, NativeShardPipeline
+    from rpt.pipeline import PathParams
+    from rpt.synth import DeviceSynth
+
+    F, p = args.frames, PathParams()
+    hf = int(np.floor(p.eps_time))
+    cfg = _config(args, F, rank * F)
+    ds = DeviceSynth(cfg, dev)
+    echo = ds.echo()
+    comm = Comm(dev)
+    pipe = NativeShardPipeline(comm, cfg.gains, cfg.rows, cfg.bins, p)
+    pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
+                      F * len(cfg.gains))
+    if args.force_host_merge:
+        pipe.set_merge_limit(0)
+    res = pipe.run(echo, rank * F).finish()
+    del echo
+    lab = pipe.labels_local().cpu().numpy()
+    pts = {k: v.cpu().numpy() for k, v in pipe.points_local().items()}
+    torch.cuda.synchronize(dev)
+    n = len(lab)
+    pf = pts["frame"].astype(np.int64)
+    gf = pf + rank * F                       # global frame ids
+    fo = np.searchsorted(pf, np.arange(F + 1))
+    assert len(pf) == n and (np.diff(pf) >= 0).all()
+
+    def rows(a, b):   # [x bits, y bits, global frame, core, label] of own points a..b
+        return np.column_stack([pts["x"][a:b].view(np.int32).astype(np.int64),
+                                pts["y"][a:b].view(np.int32).astype(np.int64), gf[a:b],
+                                pts["core"][a:b].astype(np.int64),
+                                lab[a:b].astype(np.int64)]).reshape(-1)
+
+    cpu = Comm(dev)
+    rp, rn = cpu.exchange(torch.from_numpy(rows(0, fo[hf])),
+                          torch.from_numpy(rows(fo[F - hf], n)))
+    halo_p = rp.cpu().numpy().reshape(-1, 5) if rp is not None else np.zeros((0, 5), np.int64)
+    halo_n = rn.cpu().numpy().reshape(-1, 5) if rn is not None else np.zeros((0, 5), np.int64)
+    W = np.concatenate([halo_p, rows(0, n).reshape(-1, 5), halo_n])
+    wx = W[:, 0].astype(np.int32).view(np.float32)
+    wy = W[:, 1].astype(np.int32).view(np.float32)
+    wf, wcore, wlab = W[:, 2], W[:, 3].astype(np.uint8), W[:, 4].astype(np.int32)
+    off = len(halo_p)                        # window index of own point 0
+    wfo = np.searchsorted(wf, np.arange(rank * F - hf, rank * F + F + hf + 1))
+
+    ok = True
+    checked = 0
+
+    def check(f_lo, f_hi, idx_own, what):
+        """sample_check of own points idx_own over the window frames [f_lo, f_hi) (global)"""
+        nonlocal ok, checked
+        a = wfo[max(f_lo - (rank * F - hf), 0)]
+        b = wfo[min(f_hi - (rank * F - hf), len(wfo) - 1)]
+        idx = idx_own + off - a
+        assert (idx >= 0).all() and (idx < b - a).all()
+        xy = np.column_stack([wx[a:b], wy[a:b]])
+        cnt, lo, hi = oracle.sample_check(xy, wf[a:b].astype(np.float32), p.eps_space,
+                                          p.eps_time, idx, wcore[a:b], wlab[a:b])
+        c, l_ = wcore[a:b][idx], wlab[a:b][idx]
+        good = bool(np.array_equal(c, (cnt >= p.min_samples).astype(np.uint8)))
+        cm = c == 1
+        good &= bool(np.array_equal(lo[cm], l_[cm]) and np.array_equal(hi[cm], l_[cm]))
+        good &= bool(np.array_equal(l_[~cm], lo[~cm]))
+        if not good:
+            print(f"[dist_check] rank {rank} MISMATCH in {what}: core "
+                  f"{int((c != (cnt >= p.min_samples)).sum())} wrong, labels "
+                  f"{int((lo[cm] != l_[cm]).sum() + (hi[cm] != l_[cm]).sum())} / "
+                  f"{int((l_[~cm] != lo[~cm]).sum())} wrong", flush=True)
+        ok &= good
+        checked += len(idx)
+
+    g0 = rank * F
+    check(g0 - hf, g0 + 2 * hf, np.arange(0, fo[hf]), "head frames")
+    check(g0 + F - 2 * hf, g0 + F + hf, np.arange(fo[F - hf], n), "tail frames")
+    rng = np.random.default_rng(100 + rank)
+    for f in rng.choice(np.arange(hf, F - hf), 5, replace=False):
+        a, b = fo[f], fo[f + 1]
+        s = np.sort(rng.choice(np.arange(a, b), min(10_000, b - a), replace=False))
+        check(g0 + f - hf, g0 + f + hf + 1, s, f"frame {g0 + f}")
+    edge = int(fo[hf] + n - fo[F - hf])
+    print(f"[dist_check] rank {rank}: {n} own points, {edge} edge-frame points + "
+          f"{checked - edge} random checked ({len(halo_p)} / {len(halo_n)} halo points) ok={ok}",
+          flush=True)
+
+    # global numbering: labels by first core point, rank by rank
+    cl = lab[pts["core"] == 1].astype(np.int64)
+    u, first = np.unique(cl, return_index=True)
+    firsts = u[np.argsort(first)]
+    ok &= bool((cl >= 0).all() and (lab >= -1).all())
+    allf = comm.all_gather_var(torch.from_numpy(firsts))
+    if rank == 0:
+        seen, order = set(), []
+        for t in allf:
+            for v in t.cpu().numpy().tolist():
+                if v not in seen:
+                    seen.add(v)
+                    order.append(v)
+        num_ok = order == list(range(res.n_clusters))
+        if not num_ok:
+            print(f"[dist_check] cluster numbering wrong: {len(order)} ids, "
+                  f"{res.n_clusters} clusters, first {order[:10]}", flush=True)
+        ok &= num_ok
+        # K9 rows of rank 0's frames against its points
+        seg = res.seg
+        sel = seg["frame"] < F
+        m = lab >= 0
+        key = pf[m] << 32 | lab[m].astype(np.int64)
+        uk, uc = np.unique(key, return_counts=True)
+        sk = seg["frame"][sel].astype(np.int64) << 32 | seg["label"][sel].astype(np.int64)
+        o = np.argsort(sk)
+        k9_ok = bool(np.array_equal(sk[o], uk) and np.array_equal(seg["count"][sel][o], uc))
+        xy = np.column_stack([pts["x"], pts["y"]])
+        ids = np.nonzero(sel)[0]
+        pick = np.unique(np.concatenate([[ids[int(np.argmax(seg["count"][sel]))]],
+                                         rng.choice(ids, min(40, len(ids)), replace=False)]))
+        for s_ in pick:
+            f, lb = int(seg["frame"][s_]), int(seg["label"][s_])
+            a, b = fo[f], fo[f + 1]
+            w = lab[a:b] == lb
+            cxy = np.mean(xy[a:b][w], axis=0)
+            k9_ok &= (seg["cx"][s_], seg["cy"][s_]) == (cxy[0], cxy[1])
+            k9_ok &= seg["mi"][s_] == np.float32(np.mean(pts["v"][a:b][w]))
+        ok &= k9_ok
+        print(f"[dist_check] sample-check world={world} frames/rank={F} dense={args.dense} "
+              f"points={res.n_points_global} clusters={res.n_clusters} segments={res.n_segments} "
+              f"numbering={num_ok} k9_rank0={k9_ok} host_merge={args.force_host_merge}",
+              flush=True)
+    flag = comm.all_reduce(torch.tensor([1 if ok else 0], dtype=torch.int32), dist.ReduceOp.MIN)
+    if rank == 0:
+        print(f"[dist_check] ok={bool(int(flag.item()) == 1)}", flush=True)
     dist.destroy_process_group()
     return 0 if int(flag.item()) == 1 else 1
 

@@ -1,0 +1,46 @@
+#!/bin/bash
+# Round-5 GPU steps, run on the GPU box from the repo root:  bash tools/gpu_r5.sh <step> [...]
+# Every step has its own time limit; the script stops at the first failing step.  Output under
+# gpurun_out/r5/ (gpurun brings it back).
+#   tests_new     the GPU tests added this round (host merge, configs[4] 8 x 125 sample check,
+#                 unfused K5 above 2^26)
+#   tests_all     the whole -m gpu suite
+#   shard_trace   kernel trace of the sharded per-rank step at one rank (125 frames, one lane,
+#                 every collective forced through RCCL) + the host-side profile (identity)
+#   bench         the default bench line (driver command)
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R" || exit 1
+O=gpurun_out/r5
+mkdir -p $O
+export TMPDIR=/tmp
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+PYT="python -u -m pytest -x -v --timeout-method thread"
+BS="python bench.py --sharded --total-frames 125 --no-cpu-baseline --h2d-steps 0"
+run() {  # run <name> <seconds> <cmd...>: output to $O/<name>.log
+  local name=$1 lim=$2; shift 2
+  echo "[gpu_r5] $name ..."
+  timeout -k 10 "$lim" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "[gpu_r5] $name rc=$rc"
+  tail -3 "$O/$name.log"
+  return $rc
+}
+for step in "$@"; do
+  case $step in
+    tests_new)
+      run tests_new 1000 $PYT --timeout 990 tests/test_dist_gpu.py \
+        "tests/test_bigstack_gpu.py::test_dense_above_2_26_unfused_k5_invariants" || exit 1 ;;
+    tests_all)
+      run tests_all 1100 $PYT --timeout 990 -m gpu tests/ || exit 1 ;;
+    shard_trace)
+      RPT_COMM_FORCE_COLLECTIVES=1 run shard_trace 300 rocprofv3 --kernel-trace --stats \
+        --output-format csv -d "$R/$O/prof_shard" -o shard -- \
+        python bench.py --sharded --total-frames 125 --no-cpu-baseline --h2d-steps 0 \
+        --lanes 1 --steps 20 --warmup 3 --no-one-stack || exit 1
+      run shard_host 200 python tools/prof_shard.py 125 20 || exit 1
+      RPT_COMM_FORCE_COLLECTIVES=1 run shard_l1 200 $BS --lanes 1 --steps 40 --warmup 6 || exit 1 ;;
+    bench)
+      run bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
