@@ -132,6 +132,83 @@ struct Bounds {
   int32_t t_descends;     // some t[i] < t[i-1]: the points are not in time order
 };
 
+// Device accumulator of a Bounds partial with k_bounds' semantics (stdbscan.hip), for kernels
+// that produce the ST-DBSCAN bounds of points they write anyway (the shard window).  add() per
+// point (t_prev: the previous point's t in the set's order, has_prev false for the first point),
+// then block_store() by EVERY thread of a block of kBoundsBlock threads: one partial per block,
+// reduced by stdbscan_bounds_final_dev.
+constexpr int kBoundsBlock = 256;
+struct BoundsAcc {
+  uint32_t mn[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+  uint32_t mx[4] = {0u, 0u, 0u, 0u};
+  int nonfin = 0, nonint = 0, nfin = 0, desc = 0;
+  __device__ static uint32_t ord(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  }
+  __device__ void add(float x, float y, float t, float t_prev, bool has_prev) {
+    const float v[3] = {x, y, 0.f};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (!isfinite(v[k])) nonfin = 1;
+      const uint32_t o = ord(v[k]);
+      mn[k] = min(mn[k], o);
+      mx[k] = max(mx[k], o);
+    }
+    if (isfinite(t)) {
+      ++nfin;
+      const uint32_t o = ord(t);
+      mn[3] = min(mn[3], o);
+      mx[3] = max(mx[3], o);
+      if (t != floorf(t) || fabsf(t) >= 16777216.f) nonint = 1;
+    }
+    if (has_prev && !(t_prev <= t)) desc = 1;  // NaN counts as out of order
+  }
+  __device__ void block_store(Bounds* __restrict__ out) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        mn[k] = min(mn[k], (uint32_t)__shfl_xor((int)mn[k], off));
+        mx[k] = max(mx[k], (uint32_t)__shfl_xor((int)mx[k], off));
+      }
+      nonfin |= __shfl_xor(nonfin, off);
+      nonint |= __shfl_xor(nonint, off);
+      nfin += __shfl_xor(nfin, off);
+      desc |= __shfl_xor(desc, off);
+    }
+    __shared__ Bounds sb[kBoundsBlock / 64];
+    const int w = threadIdx.x / 64;
+    if ((threadIdx.x & 63) == 0) {
+      for (int k = 0; k < 4; ++k) {
+        sb[w].mn[k] = mn[k];
+        sb[w].mx[k] = mx[k];
+      }
+      sb[w].nonfinite_xyz = nonfin;
+      sb[w].nonintegral_t = nonint;
+      sb[w].n_finite_t = nfin;
+      sb[w].t_descends = desc;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      Bounds o = sb[0];
+      for (int v = 1; v < kBoundsBlock / 64; ++v) {
+        for (int k = 0; k < 4; ++k) {
+          o.mn[k] = min(o.mn[k], sb[v].mn[k]);
+          o.mx[k] = max(o.mx[k], sb[v].mx[k]);
+        }
+        o.nonfinite_xyz |= sb[v].nonfinite_xyz;
+        o.nonintegral_t |= sb[v].nonintegral_t;
+        o.n_finite_t += sb[v].n_finite_t;
+        o.t_descends |= sb[v].t_descends;
+      }
+      out[blockIdx.x] = o;
+    }
+  }
+};
+// the partials of nb blocks -> out (one launch, k_bounds_final)
+int32_t stdbscan_bounds_final_dev(const void* part_dev, int nb, void* out_dev, hipStream_t st);
+
 struct PackList {
   const uint32_t* src[kPackMax];
   int64_t off[kPackMax + 1];  // word offsets in dst, off[0] = 0

@@ -134,7 +134,9 @@ __global__ void k_cnt_to_f64(const int32_t* __restrict__ cnt, int64_t cells,
     out[i] = (double)cnt[i];
 }
 __global__ void k_f64_to_cnt(const double* __restrict__ in, int64_t cells,
-                             int32_t* __restrict__ cnt) {
+                             int32_t* __restrict__ cnt, int64_t* __restrict__ zero) {
+  // zero: the land mask's cell counter, cleared here instead of by a memset launch
+  if (blockIdx.x == 0 && threadIdx.x == 0) *zero = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cells;
        i += (int64_t)gridDim.x * blockDim.x)
     cnt[i] = (int32_t)in[i];
@@ -186,13 +188,15 @@ __device__ __forceinline__ int64_t halo_total(const int32_t* h) {
   return (int64_t)(((uint64_t)(uint32_t)h[2] << 32) | (uint64_t)(uint32_t)h[1]);
 }
 
-// [prev halo | own | next halo] as x / y / t, and the window's counts
-__global__ void k_window(const int32_t* __restrict__ rp, int64_t cap_rp,
-                         const int32_t* __restrict__ rn, int64_t cap_rn,
-                         const float* __restrict__ x, const float* __restrict__ y,
-                         const int32_t* __restrict__ pf, const int64_t* __restrict__ off,
-                         int32_t F, int32_t hf, int64_t frame0, float* __restrict__ X,
-                         float* __restrict__ Y, float* __restrict__ T, WinMeta* __restrict__ meta) {
+// [prev halo | own | next halo] as x / y / t, the window's counts, and per block the partial of
+// the window's ST-DBSCAN bounds (k_bounds' semantics, reduced by stdbscan_bounds_final_dev: no
+// separate bounds pass over the window)
+__global__ __launch_bounds__(kBoundsBlock) void k_window(
+    const int32_t* __restrict__ rp, int64_t cap_rp, const int32_t* __restrict__ rn,
+    int64_t cap_rn, const float* __restrict__ x, const float* __restrict__ y,
+    const int32_t* __restrict__ pf, const int64_t* __restrict__ off, int32_t F, int32_t hf,
+    int64_t frame0, float* __restrict__ X, float* __restrict__ Y, float* __restrict__ T,
+    WinMeta* __restrict__ meta, Bounds* __restrict__ part) {
   const int64_t np = rp ? (int64_t)rp[0] : 0;
   const int64_t nn = rn ? (int64_t)rn[0] : 0;
   const int64_t K = off[F];
@@ -210,6 +214,12 @@ __global__ void k_window(const int32_t* __restrict__ rp, int64_t cap_rp,
     m.pad = 0;
     *meta = m;
   }
+  auto time_of = [&](int64_t i) -> float {
+    if (i < np) return __int_as_float(rp[kHaloHdr + 2 * cap_rp + i]);
+    if (i < np + K) return (float)(frame0 + (int64_t)pf[i - np]);
+    return __int_as_float(rn[kHaloHdr + 2 * cap_rn + (i - np - K)]);
+  };
+  BoundsAcc acc;
   for (int64_t i = i0; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     float a, b, c;
     if (i < np) {
@@ -230,7 +240,9 @@ __global__ void k_window(const int32_t* __restrict__ rp, int64_t cap_rp,
     X[i] = a;
     Y[i] = b;
     T[i] = c;
+    acc.add(a, b, c, i > 0 ? time_of(i - 1) : 0.f, i > 0);
   }
+  acc.block_store(part);
 }
 
 // own edge points' global component ids for the neighbours (-1: not core)
@@ -294,6 +306,14 @@ __global__ void k_pairs(const int32_t* __restrict__ comp, int64_t c0, WinIds w,
       out[2 + 2 * k] = hi;
     }
   }
+}
+
+// the pair count and the distinct-pair set (all ones = empty) of rpt_shard_pairs, in one launch
+__global__ void k_pairs_init(unsigned long long* __restrict__ count,
+                             unsigned long long* __restrict__ set, uint64_t size) {
+  const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i0 == 0) *count = 0ull;
+  for (uint64_t i = i0; i < size; i += (uint64_t)gridDim.x * blockDim.x) set[i] = ~0ull;
 }
 
 __global__ void k_store_count(const unsigned long long* __restrict__ count,
@@ -489,34 +509,51 @@ __device__ __forceinline__ int64_t lookup(const int64_t* __restrict__ keys,
 
 // rep[i] = the global representative (class minimum id) of window point i's component, -1 for
 // non-core; flags of the representative list: the merge table's class minima below the window
-// (external representatives) and the window points that are their own representative
+// (external representatives) and the window points that are their own representative -- one bit
+// per list entry k < keys_cap + n (a wave per 64 entries: its two words and their popcounts), so
+// the list's order comes from a scan over n / 32 words instead of one over every entry
 __global__ void k_reps(const int32_t* __restrict__ comp, int64_t n, WinIds w,
                        const int64_t* __restrict__ keys, const int64_t* __restrict__ vals,
                        const int64_t* __restrict__ meta, int64_t keys_cap,
-                       int64_t* __restrict__ rep, int32_t* __restrict__ flag) {
+                       int64_t* __restrict__ rep, uint32_t* __restrict__ bits,
+                       int32_t* __restrict__ wcnt) {
   const int64_t m = meta[0] > 0 ? meta[0] : 0;
   const int64_t wstart = w.gid(0);
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < keys_cap + n;
-       k += (int64_t)gridDim.x * blockDim.x) {
+  const int lane = threadIdx.x & 63;
+  const int64_t total = keys_cap + n;
+  for (int64_t c0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 64; c0 < total;
+       c0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = c0 + lane;
+    bool f = false;
     if (k < keys_cap) {
-      flag[k] = (k < m && keys[k] == vals[k] && keys[k] < wstart) ? 1 : 0;
-      continue;
+      f = k < m && keys[k] == vals[k] && keys[k] < wstart;
+    } else if (k < total) {
+      const int64_t i = k - keys_cap;
+      const int32_t c = comp[i];
+      int64_t r = -1;
+      if (c >= 0) r = lookup(keys, vals, m, w.gid(c));
+      rep[i] = r;
+      f = c >= 0 && r == w.gid(i);
     }
-    const int64_t i = k - keys_cap;
-    const int32_t c = comp[i];
-    int64_t r = -1;
-    if (c >= 0) r = lookup(keys, vals, m, w.gid(c));
-    rep[i] = r;
-    flag[k] = (c >= 0 && r == w.gid(i)) ? 1 : 0;
+    const uint64_t b = __ballot(f);
+    if (lane < 2) {
+      const uint32_t word = (uint32_t)(b >> (32 * lane));
+      bits[(c0 >> 5) + lane] = word;
+      wcnt[(c0 >> 5) + lane] = __popc(word);
+    }
   }
 }
 
-__global__ void k_reps_write(const int32_t* __restrict__ flag, const int64_t* __restrict__ pos,
+__global__ void k_reps_write(const uint32_t* __restrict__ bits, const int64_t* __restrict__ wpre,
                              int64_t keys_cap, int64_t n, WinIds w,
                              const int64_t* __restrict__ keys, int64_t* __restrict__ reps) {
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < keys_cap + n;
-       k += (int64_t)gridDim.x * blockDim.x)
-    if (flag[k]) reps[pos[k]] = k < keys_cap ? keys[k] : w.gid(k - keys_cap);
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t word = bits[k >> 5];
+    const uint32_t bit = 1u << (k & 31);
+    if (word & bit)
+      reps[wpre[k >> 5] + __popc(word & (bit - 1u))] = k < keys_cap ? keys[k] : w.gid(k - keys_cap);
+  }
 }
 
 // built[f] = frame f holds a K1 point (file offsets of F frames x G files)
@@ -822,13 +859,12 @@ int32_t rpt_shard_halo(rpt_shard* h, const double* grid, int64_t cells, int32_t 
   h->frame0 = frame0;
   RPT_TRY(S.new_off.ensure((size_t)F + 2, st));
   RPT_TRY(S.scal.ensure(4, st));
-  RPT_HIP(hipMemsetAsync(S.scal.p, 0, sizeof(int64_t), st));
   h->land = grid != nullptr && cells > 0;
   if (h->land) {
     RPT_TRY(S.land_cnt.ensure((size_t)cells, st));
     RPT_TRY(S.land_mask.ensure((size_t)cells, st));
     hipLaunchKernelGGL(k_f64_to_cnt, dim3(grid_for(cells, 256, 1024)), dim3(256), 0, st, grid,
-                       cells, S.land_cnt.p);
+                       cells, S.land_cnt.p, reinterpret_cast<int64_t*>(S.scal.p));
     RPT_CHECK_LAUNCH();
     RPT_TRY(land_mask_dev(S.land_cnt.p, grid + cells, cells, n_built_global, h->p.land_persistence,
                           h->p.land_min_intensity, S.land_mask.p,
@@ -849,6 +885,7 @@ int32_t rpt_shard_halo(rpt_shard* h, const double* grid, int64_t cells, int32_t 
     else
       RPT_HIP(hipMemsetAsync(S.new_off.p, 0, sizeof(int64_t) * (F + 1), st));
   } else {
+    RPT_HIP(hipMemsetAsync(S.scal.p, 0, sizeof(int64_t), st));  // (read back with the window)
     // no land filter: the kept points are the K1 points, offsets from the host copy
     RPT_TRY(S.up.ensure(sizeof(int64_t) * (size_t)(F + 1), st));
     std::memcpy(S.up.p, S.fo_k1.data(), sizeof(int64_t) * (F + 1));
@@ -895,12 +932,15 @@ int32_t rpt_shard_window(rpt_shard* h, const int32_t* recv_prev, int64_t cap_pre
   WinMeta* meta = reinterpret_cast<WinMeta*>(h->wbnd.p);
   char* bnd = h->wbnd.p + sizeof(WinMeta);
   char* bpart = bnd + align_up(bb, 16);
-  hipLaunchKernelGGL(k_window, dim3(grid_for(wcap, 256, 4096)), dim3(256), 0, st,
+  // (the partials' count is the bounds pass's grid: stdbscan_bounds_part_bytes)
+  const int nbw = grid_for(wcap, kBoundsBlock, 1024);
+  hipLaunchKernelGGL(k_window, dim3(nbw), dim3(kBoundsBlock), 0, st,
                      cap_prev > 0 ? recv_prev : nullptr, cap_prev,
                      cap_next > 0 ? recv_next : nullptr, cap_next, cx, cy, cpf, S.new_off.p, F,
-                     h->hf, h->frame0, h->X.p, h->Y.p, h->T.p, meta);
+                     h->hf, h->frame0, h->X.p, h->Y.p, h->T.p, meta,
+                     reinterpret_cast<Bounds*>(bpart));
   RPT_CHECK_LAUNCH();
-  RPT_TRY(stdbscan_bounds_dev(h->X.p, h->Y.p, h->T.p, wcap, &meta->n_window, bnd, bpart, st));
+  RPT_TRY(stdbscan_bounds_final_dev(bpart, nbw, bnd, st));
   // ONE readback: window counts, grid bounds, land-cell count, the kept frame offsets
   PackList pl;
   pl.add(meta, sizeof(WinMeta));
@@ -1010,12 +1050,12 @@ int32_t rpt_shard_pairs(rpt_shard* h, const int64_t* owner_prev, const int64_t* 
   }
   const hipStream_t st = as_stream(stream);
   RPT_TRY(h->cnt64.ensure(2, st));
-  RPT_HIP(hipMemsetAsync(h->cnt64.p, 0, sizeof(int64_t), st));
   auto* cnt = reinterpret_cast<unsigned long long*>(h->cnt64.p);
   uint64_t tsize = 64;
   while (tsize < (uint64_t)(2 * (I.n_prev + I.n_next))) tsize <<= 1;
   RPT_TRY(h->pset.ensure((size_t)tsize, st));
-  RPT_HIP(hipMemsetAsync(h->pset.p, 0xFF, tsize * sizeof(unsigned long long), st));
+  hipLaunchKernelGGL(k_pairs_init, dim3(grid_for((int64_t)tsize, 256, 1024)), dim3(256), 0, st,
+                     cnt, h->pset.p, tsize);
   const WinIds w = h->ids();
   if (I.n_prev > 0 && h->n_window > 0)
     hipLaunchKernelGGL(k_pairs, dim3(grid_for(I.n_prev, 256, 1024)), dim3(256), 0, st, h->comp.p,
@@ -1073,22 +1113,27 @@ int32_t rpt_shard_finish(rpt_shard* h, const int64_t* gathered_pairs, int32_t wo
   // ---- representatives: rep per window point, the sorted list of those the window sees
   const WinIds w = h->ids();
   RPT_TRY(h->rep.ensure((size_t)std::max<int64_t>(n, 1), st));
-  RPT_TRY(h->flag.ensure((size_t)(keys_cap + n + 1), st));
-  RPT_TRY(h->pos.ensure((size_t)(keys_cap + n + 1), st));
+  const size_t lw = (size_t)(2 * ((keys_cap + n + 63) / 64));  // list words (k_reps)
+  RPT_TRY(h->flag.ensure(std::max((size_t)(keys_cap + n + 1), 2 * lw), st));
+  RPT_TRY(h->pos.ensure(std::max((size_t)(keys_cap + n + 1), lw + 1), st));
   RPT_TRY(h->reps.ensure((size_t)(keys_cap + n + 1), st));
+  // list entries as bits: nw words (a multiple of two), their popcounts after them in flag
+  const int64_t nw = 2 * ((keys_cap + n + 63) / 64);
+  uint32_t* rbits = reinterpret_cast<uint32_t*>(h->flag.p);
+  int32_t* rcnt = h->flag.p + nw;
   if (n > 0) {
     hipLaunchKernelGGL(k_reps, dim3(grid_for(keys_cap + n, 256, 4096)), dim3(256), 0, st,
                        h->comp.p, n, w, h->keys.p, h->vals.p, h->meta.p, keys_cap, h->rep.p,
-                       h->flag.p);
+                       rbits, rcnt);
     RPT_CHECK_LAUNCH();
-    RPT_TRY(exclusive_scan_total_i32_to_i64(h->flag.p, h->pos.p, keys_cap + n, st));
+    RPT_TRY(exclusive_scan_total_i32_to_i64(rcnt, h->pos.p, nw, st));
     hipLaunchKernelGGL(k_reps_write, dim3(grid_for(keys_cap + n, 256, 4096)), dim3(256), 0, st,
-                       h->flag.p, h->pos.p, keys_cap, n, w, h->keys.p, h->reps.p);
+                       rbits, h->pos.p, keys_cap, n, w, h->keys.p, h->reps.p);
     RPT_CHECK_LAUNCH();
   } else {
-    RPT_HIP(hipMemsetAsync(h->pos.p + keys_cap + n, 0, sizeof(int64_t), st));
+    RPT_HIP(hipMemsetAsync(h->pos.p + nw, 0, sizeof(int64_t), st));
   }
-  const int64_t* nr_dev = h->pos.p + keys_cap + n;
+  const int64_t* nr_dev = h->pos.p + nw;
   // ---- labels of the window (local numbering), K9 of the own points
   RPT_TRY(h->labels.ensure((size_t)std::max<int64_t>(n, 1), st));
   if (n > 0) RPT_TRY(dbscan_labels_global_dev(h->db, h->rep.p, h->reps.p, nr_dev, h->labels.p, st));

@@ -2012,451 +2012,6 @@ __global__ __launch_bounds__(kBlock, 8) void k_core_slow(const float4* __restric
   }
 }
 
-// Level 4 by cells: waves stride over the occupied cells (no queue: a cell flag read per occupied
-// cell replaces the per-point fill + append), and every undecided cell (flag 2) is
-// settled by its wave: the cell's candidate window, box-classified against the CELL once, stays
-// in registers (up to 64*kR candidate cells) while the wave walks the cell's points -- per point
-// a box test per candidate (whole-cell accept adds the count), then the undecided candidates'
-// points 64 at a time, stopping at min_samples.  Windows larger than 64*kR cells fall back to the
-// per-point window walk of k_core_slow.
-template <int D>
-__device__ __forceinline__ int core_count_point(const float4& p, int32_t key,
-                                                const float4* __restrict__ pts, const Geom& g,
-                                                const CellRec<D>* __restrict__ crec,
-                                                const uint32_t* __restrict__ occ_bits,
-                                                const float2* __restrict__ slab_t) {
-  const int lane = threadIdx.x & 63;
-  const int need = g.min_samples;
-  int cx, cy, cz;
-  decode_key<D>(key, g, cx, cy, cz);
-  const Window w = make_window<D, false>(cx, cy, cz, p.w, p.w, g, slab_t);
-  int cnt = 0;
-  for (int base = 0; base < w.total && cnt < need; base += 64 * kR) {
-    int64_t c[kR];
-    uint32_t wb[kR];
-#pragma unroll
-    for (int r = 0; r < kR; ++r) {
-      const int qq = base + r * 64 + lane;
-      c[r] = (qq < w.total) ? window_cell<D>(w, qq, g, slab_t, p.w, p.w) : -1;
-    }
-#pragma unroll
-    for (int r = 0; r < kR; ++r) wb[r] = (c[r] >= 0) ? occ_bits[c[r] >> 5] : 0u;
-    int b[kR], e[kR], cls[kR];
-#pragma unroll
-    for (int r = 0; r < kR; ++r) {
-      b[r] = e[r] = cls[r] = 0;
-      if (c[r] >= 0 && ((wb[r] >> (c[r] & 31)) & 1u)) {
-        const CellRec<D> cr = crec[c[r]];
-        b[r] = cr.b;
-        e[r] = cr.e;
-        cls[r] = classify<D>(p, rec_boxA<D>(cr), rec_boxB(cr), g);
-      }
-    }
-    int add = 0;
-#pragma unroll
-    for (int r = 0; r < kR; ++r) add += (cls[r] == 1) ? e[r] - b[r] : 0;
-    cnt += wave_sum(add);
-#pragma unroll
-    for (int r = 0; r < kR; ++r) {
-      uint64_t pm = __ballot(cls[r] == 2);
-      while (pm && cnt < need) {
-        const int l = __ffsll((unsigned long long)pm) - 1;
-        pm &= pm - 1;
-        const int bb = __shfl(b[r], l), ee = __shfl(e[r], l);
-        for (int j0 = bb; j0 < ee && cnt < need; j0 += 64) {
-          const int j = j0 + lane;
-          cnt += __popcll(__ballot((j < ee) && adjacent<D>(p, pts[j], g)));
-        }
-      }
-    }
-  }
-  return cnt;
-}
-
-template <int D>
-__global__ __launch_bounds__(kBlock) void k_core_slow_cells(const float4* __restrict__ pts, Geom g,
-                                                           const CellRec<D>* __restrict__ crec,
-                                                           const uint32_t* __restrict__ occ_bits,
-                                                           const float2* __restrict__ slab_t,
-                                                           const int32_t* __restrict__ occ,
-                                                           const int32_t* __restrict__ n_occ,
-                                                           const int32_t* __restrict__ cflag,
-                                                           uint8_t* __restrict__ core) {
-  const int lane = threadIdx.x & 63;
-  const int64_t w0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
-  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
-  const int64_t no = *n_occ;
-  const int need = g.min_samples;
-  // lane l of wave w looks at occupied cell w + l*nw (+ 64*nw per round): undecided cells are
-  // spatially clustered, i.e. consecutive in the occupied list, and this spreads them over all
-  // waves instead of handing a cluster of them to one wave
-  for (int64_t q0 = w0; q0 < no; q0 += nw * 64) {
-    const int64_t q = q0 + (int64_t)lane * nw;
-    const int32_t cq = (q < no) ? occ[q] : -1;
-    uint64_t um = __ballot(cq >= 0 && (int64_t)cq < g.cells && cflag[cq] == 2);
-    while (um) {
-      const int l = __ffsll((unsigned long long)um) - 1;
-      um &= um - 1;
-      const int32_t ca = __builtin_amdgcn_readlane(cq, l);
-      const CellRec<D> ra = crec[ca];
-      const float4 A1 = rec_boxA<D>(ra), A2 = rec_boxB(ra);
-      int cx, cy, cz;
-      decode_key<D>(ca, g, cx, cy, cz);
-      const Window w = make_window<D, true>(cx, cy, cz, A2.z, A2.w, g, slab_t);
-      if (w.total > 64 * kR) {  // wide windows: the per-point walk
-        for (int s = ra.b; s < ra.e; ++s) {
-          const int cnt = core_count_point<D>(pts[s], ca, pts, g, crec, occ_bits, slab_t);
-          if (lane == 0) core[s] = (cnt >= need) ? 1 : 0;
-        }
-        continue;
-      }
-      // the window's candidate cells that may hold a neighbour of SOME point of the cell
-      float4 cA[kR], cB[kR];
-      int cb[kR], ce[kR];
-      int64_t c[kR];
-      uint32_t wb[kR];
-#pragma unroll
-      for (int r = 0; r < kR; ++r) {
-        const int qq = r * 64 + lane;
-        c[r] = (qq < w.total) ? window_cell<D>(w, qq, g, slab_t, A2.z, A2.w) : -1;
-      }
-#pragma unroll
-      for (int r = 0; r < kR; ++r) wb[r] = (c[r] >= 0) ? occ_bits[c[r] >> 5] : 0u;
-#pragma unroll
-      for (int r = 0; r < kR; ++r) {
-        cb[r] = ce[r] = 0;
-        cA[r] = cB[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (c[r] >= 0 && ((wb[r] >> (c[r] & 31)) & 1u)) {
-          const CellRec<D> cr = crec[c[r]];
-          if (classify_cells<D>(A1, rec_boxA<D>(cr), A2, rec_boxB(cr), g) != 0) {
-            cb[r] = cr.b;
-            ce[r] = cr.e;
-            cA[r] = rec_boxA<D>(cr);
-            cB[r] = rec_boxB(cr);
-          }
-        }
-      }
-      for (int s = ra.b; s < ra.e; ++s) {
-        const float4 p = pts[s];
-        int cls[kR];
-#pragma unroll
-        for (int r = 0; r < kR; ++r) cls[r] = (ce[r] > cb[r]) ? classify<D>(p, cA[r], cB[r], g) : 0;
-        int add = 0;
-#pragma unroll
-        for (int r = 0; r < kR; ++r) add += (cls[r] == 1) ? ce[r] - cb[r] : 0;
-        int cnt = wave_sum(add);
-#pragma unroll
-        for (int r = 0; r < kR; ++r) {
-          uint64_t pm = __ballot(cls[r] == 2);
-          while (pm && cnt < need) {
-            const int l2 = __ffsll((unsigned long long)pm) - 1;
-            pm &= pm - 1;
-            const int bb = __shfl(cb[r], l2), ee = __shfl(ce[r], l2);
-            for (int j0 = bb; j0 < ee && cnt < need; j0 += 64) {
-              const int j = j0 + lane;
-              cnt += __popcll(__ballot((j < ee) && adjacent<D>(p, pts[j], g)));
-            }
-          }
-        }
-        if (lane == 0) core[s] = (cnt >= need) ? 1 : 0;
-      }
-    }
-  }
-}
-
-// ---- K5 by LDS tiles (2-D, slab window <= 7): the occupied-cell records a slab-row band needs
-// are staged in LDS ONCE per workgroup instead of fetched from HBM/L2 by every cell that has them
-// as a candidate (~30 record loads per sparse cell).  A tile = slab s x rows [y0, y0 + BY); its
-// workgroup stages the records of rows [y0 - 2, y0 + BY + 2) of slabs s - R .. s + R (ranges of
-// the ascending occupied list, found through rowq: the first occupied index of every (slab, row))
-// and a dense u16 map (slab offset, row, x) -> staged index, then
-//   cell pass: eight lanes per own cell as k_core_cells_oct (lane j = slab offset; own row first,
-//     early exit once the adjacent-to-every-point count reaches min_samples), records from LDS;
-//     decided cells write their points' flags;
-//   slow pass: one wave per undecided own cell, its candidate cells (LDS) classified against the
-//     CELL once, then its points one by one: a box test per candidate, the undecided candidates'
-//     points (global, 64 at a time) until min_samples.
-// A tile whose records exceed kTileCap reads them from global memory instead (the same code).
-constexpr int kTileBlock = 512;
-constexpr int kTileCap = 1536;   // staged CellRec<2> per tile (48 KiB)
-constexpr int kTileMap = 8192;   // u16 map entries (16 KiB): W * (BY + 4) * nx <= this
-constexpr int kTileUnd = 1024;   // undecided own cells per tile: BY * nx <= this
-
-// rowcnt[r] = occupied cells of row r = (slab, y) (bits [r nx, (r + 1) nx) of occ_bits)
-__global__ __launch_bounds__(kBlock) void k_row_occ(const uint32_t* __restrict__ occ_bits,
-                                                   int64_t nrows, int nx,
-                                                   int32_t* __restrict__ rowcnt) {
-  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nrows;
-       r += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t b0 = r * nx, b1 = b0 + nx;
-    int c = 0;
-    for (int64_t w = b0 >> 5; w <= (b1 - 1) >> 5; ++w) {
-      uint32_t m = occ_bits[w];
-      const int64_t lo = w << 5;
-      if (lo < b0) m &= ~0u << (b0 - lo);
-      if (lo + 32 > b1) m &= ~0u >> (lo + 32 - b1);
-      c += __popc(m);
-    }
-    rowcnt[r] = c;
-  }
-}
-
-__global__ __launch_bounds__(kTileBlock) void k_core_tiles(
-    Geom g, int R, int BY, int nbands, int64_t ntiles, const int32_t* __restrict__ occ,
-    const int32_t* __restrict__ n_occ, const int32_t* __restrict__ rowq,
-    const CellRec<2>* __restrict__ crec, const uint8_t* __restrict__ mutual,
-    const uint32_t* __restrict__ occ_bits, const float2* __restrict__ slab_t,
-    const float4* __restrict__ pts, uint8_t* __restrict__ core) {
-  __shared__ CellRec<2> srec[kTileCap];
-  __shared__ uint16_t smap[kTileMap];
-  __shared__ int s_und[kTileUnd];
-  __shared__ int s_q0[8], s_base[8], s_reach[8];
-  __shared__ int s_total, s_nund;
-  const int need = g.min_samples;
-  const int W = 2 * R + 1, MR = BY + 4;
-  // XCD-contiguous tile ranges (grid a multiple of 8: blockIdx % 8 is the XCD): neighbouring
-  // tiles stage overlapping records, which then stay in one XCD's L2
-  const int64_t tile = (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-  if (tile > ntiles) return;
-  if (tile == ntiles) {  // the isolated cell (non-finite times: no neighbour, not even itself)
-    const int64_t no = *n_occ;
-    if (no > 0 && (int64_t)occ[no - 1] >= g.cells) {
-      const CellRec<2> ri = crec[occ[no - 1]];
-      write_cell_flags(core, ri.b, ri.e, threadIdx.x, blockDim.x, need <= 0 ? 1 : 0);
-    }
-    return;
-  }
-  const int s = (int)(tile / nbands), band = (int)(tile % nbands);
-  const int y0 = band * BY, y1 = min(y0 + BY, g.ny);
-  const int ya = max(y0 - 2, 0), yb = min(y1 + 2, g.ny);
-  const int qo0 = rowq[(int64_t)s * g.ny + y0], qo1 = rowq[(int64_t)s * g.ny + y1];
-  if (qo1 <= qo0) return;  // no own cell (uniform over the block)
-  if (threadIdx.x < 8) {
-    const int so = threadIdx.x, sl = s - R + so;
-    int q0 = 0, cnt = 0, rc = 0;
-    if (so < W && sl >= 0 && sl < g.nt) {
-      const float2 own = slab_t[s], sr = slab_t[sl];
-      const float gap = (own.x > sr.y) ? (own.x - sr.y) : ((sr.x > own.y) ? (sr.x - own.y) : 0.f);
-      rc = (sr.x <= sr.y && gap <= g.epst) ? 1 : 0;
-      if (rc) {
-        q0 = rowq[(int64_t)sl * g.ny + ya];
-        cnt = rowq[(int64_t)sl * g.ny + yb] - q0;
-      }
-    }
-    // exclusive scan of the eight counts inside the first eight lanes
-    int incl = cnt;
-#pragma unroll
-    for (int off = 1; off < 8; off <<= 1) {
-      const int o = __shfl_up(incl, off, 8);
-      if (so >= off) incl += o;
-    }
-    s_q0[so] = q0;
-    s_base[so] = incl - cnt;
-    s_reach[so] = rc;
-    if (so == 7) s_total = incl;
-  }
-  if (threadIdx.x == 0) s_nund = 0;
-  __syncthreads();
-  const bool lds = s_total <= kTileCap;
-  if (lds) {
-    const int mapn = W * MR * g.nx;
-    for (int i = threadIdx.x; i < mapn; i += blockDim.x) smap[i] = 0xFFFF;
-    __syncthreads();
-    for (int so = 0; so < W; ++so) {
-      const int q0 = s_q0[so], base = s_base[so];
-      const int cnt = (so + 1 < 8 ? s_base[so + 1] : s_total) - base;
-      for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
-        const int32_t key = occ[q0 + i];
-        srec[base + i] = crec[key];
-        int x, y, z_, s_;
-        g.split((uint32_t)key, x, y, z_, s_);
-        smap[(so * MR + (y - y0 + 2)) * g.nx + x] = (uint16_t)(base + i);
-      }
-    }
-    __syncthreads();
-  }
-  // the five candidate cells (x = cx - 2 .. cx + 2) of row y of slab offset so: present flags
-  // and records, from LDS or (overflowing tile) from occ_bits + crec
-  auto row5 = [&](int so, int y, int cx, CellRec<2>* cr) -> uint32_t {
-    uint32_t m = 0;
-    if (lds) {
-      const int mrow = (so * MR + (y - y0 + 2)) * g.nx;
-      uint16_t id[5];
-#pragma unroll
-      for (int dx = 0; dx < 5; ++dx) {
-        const int x = cx + dx - 2;
-        id[dx] = (x >= 0 && x < g.nx) ? smap[mrow + x] : (uint16_t)0xFFFF;
-      }
-#pragma unroll
-      for (int dx = 0; dx < 5; ++dx)
-        if (id[dx] != 0xFFFF) {
-          cr[dx] = srec[id[dx]];
-          m |= 1u << dx;
-        }
-      return m;
-    }
-    const int k0 = ((s - R + so) * g.ny + y) * g.nx + (cx - 2);
-    const int kk = k0 < 0 ? 0 : k0;
-    const uint32_t lo_w = occ_bits[kk >> 5], hi_w = occ_bits[(kk >> 5) + 1];
-    m = (k0 < 0) ? ((lo_w << (-k0)) & 31u)
-                 : (__builtin_amdgcn_alignbit(hi_w, lo_w, (uint32_t)(kk & 31)) & 31u);
-    const int lo_x = cx - 2 < 0 ? 2 - cx : 0;
-    const int hi_x = cx + 2 - (g.nx - 1);
-    m &= ~((1u << lo_x) - 1u);
-    if (hi_x > 0) m &= (31u >> hi_x);
-#pragma unroll
-    for (int dx = 0; dx < 5; ++dx)
-      if ((m >> dx) & 1u) cr[dx] = crec[k0 + dx];
-    return m;
-  };
-  auto own_rec = [&](int q, int32_t ca) -> CellRec<2> {
-    return lds ? srec[s_base[R] + (q - s_q0[R])] : crec[ca];
-  };
-
-  // ---- cell pass: eight lanes per own cell
-  const int j = threadIdx.x & 7;
-  const int cpr = blockDim.x / 8;
-  for (int qc = qo0; qc < qo1; qc += cpr) {
-    const int q = qc + (int)threadIdx.x / 8;
-    const bool act = q < qo1;
-    int flag = 0, b = 0, e = 0;
-    if (act) {
-      const int32_t ca = occ[q];
-      int cx, cy, cz_, cs_;
-      g.split((uint32_t)ca, cx, cy, cz_, cs_);
-      const CellRec<2> ra = own_rec(q, ca);
-      b = ra.b;
-      e = ra.e;
-      if (need <= 0 || (mutual[ca] && e - b >= need)) {
-        flag = 1;
-      } else {
-        const bool sv = j < W && s_reach[j];
-        const float4 A1 = rec_boxA<2>(ra), A2 = rec_boxB(ra);
-        int lo = 0, hi = 0;
-        bool decided = false;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-          const int dy = (k == 0) ? 2 : ((k & 1) ? 2 - (k + 1) / 2 : 2 + k / 2);
-          const int y = cy + dy - 2;
-          if (sv && y >= 0 && y < g.ny) {
-            CellRec<2> cr[5];
-            const uint32_t m = row5(j, y, cx, cr);
-#pragma unroll
-            for (int dx = 0; dx < 5; ++dx) {
-              if (!((m >> dx) & 1u)) continue;
-              const int cls =
-                  classify_cells<2, true>(A1, rec_boxA<2>(cr[dx]), A2, rec_boxB(cr[dx]), g);
-              lo += (cls == 1) ? cr[dx].e - cr[dx].b : 0;
-              hi += (cls != 0) ? cr[dx].e - cr[dx].b : 0;
-            }
-          }
-          if (k == 0 || k == 2) {
-            int ls = lo;
-#pragma unroll
-            for (int off = 4; off > 0; off >>= 1) ls += __shfl_xor(ls, off, 8);
-            if (ls >= need) {
-              decided = true;
-              break;
-            }
-          }
-        }
-        if (decided) {
-          flag = 1;
-        } else {
-#pragma unroll
-          for (int off = 4; off > 0; off >>= 1) {
-            lo += __shfl_xor(lo, off, 8);
-            hi += __shfl_xor(hi, off, 8);
-          }
-          flag = (lo >= need) ? 1 : ((hi < need) ? 0 : 2);
-        }
-      }
-      if (flag == 2 && j == 0) s_und[atomicAdd(&s_nund, 1)] = q;  // < BY * nx <= kTileUnd
-    }
-    if (act && flag != 2) write_cell_flags(core, b, e, j, 8, (uint8_t)flag);
-  }
-  __syncthreads();
-
-  // ---- slow pass: one wave per undecided own cell
-  const int lane = threadIdx.x & 63;
-  const int nund = s_nund;
-  constexpr int kSR = 3;  // candidate positions per lane: W * 25 <= 175 <= 3 * 64
-  for (int u = (int)threadIdx.x / 64; u < nund; u += (int)blockDim.x / 64) {
-    const int q = s_und[u];
-    const int32_t ca = occ[q];
-    const CellRec<2> ra = own_rec(q, ca);
-    const float4 A1 = rec_boxA<2>(ra), A2 = rec_boxB(ra);
-    int cx, cy, cz_, cs_;
-    g.split((uint32_t)ca, cx, cy, cz_, cs_);
-    float4 cA[kSR], cB[kSR];
-    int cb[kSR], ce[kSR], ccls[kSR];
-#pragma unroll
-    for (int r = 0; r < kSR; ++r) {
-      cb[r] = ce[r] = ccls[r] = 0;
-      cA[r] = cB[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-      const int pos = r * 64 + lane;
-      const int so = pos / 25, rem = pos - so * 25;
-      const int y = cy + rem / 5 - 2, x = cx + rem % 5 - 2;
-      if (pos < W * 25 && s_reach[so] && y >= 0 && y < g.ny && x >= 0 && x < g.nx) {
-        bool have = false;
-        CellRec<2> cr;
-        if (lds) {
-          const uint16_t id = smap[(so * MR + (y - y0 + 2)) * g.nx + x];
-          if (id != 0xFFFF) {
-            cr = srec[id];
-            have = true;
-          }
-        } else {
-          const int64_t k = ((int64_t)(s - R + so) * g.ny + y) * g.nx + x;
-          if ((occ_bits[k >> 5] >> (k & 31)) & 1u) {
-            cr = crec[k];
-            have = true;
-          }
-        }
-        if (have) {
-          const int cls = classify_cells<2, true>(A1, rec_boxA<2>(cr), A2, rec_boxB(cr), g);
-          if (cls) {
-            cb[r] = cr.b;
-            ce[r] = cr.e;
-            ccls[r] = cls;
-            cA[r] = rec_boxA<2>(cr);
-            cB[r] = rec_boxB(cr);
-          }
-        }
-      }
-    }
-    int full = 0;
-#pragma unroll
-    for (int r = 0; r < kSR; ++r) full += (ccls[r] == 1) ? ce[r] - cb[r] : 0;
-    const int lo_c = wave_sum(full);  // adjacent to every point of the cell
-    for (int sp = ra.b; sp < ra.e; ++sp) {
-      const float4 p = pts[sp];
-      int cls[kSR];
-      int add = 0;
-#pragma unroll
-      for (int r = 0; r < kSR; ++r) {
-        cls[r] = (ccls[r] == 2) ? classify<2>(p, cA[r], cB[r], g) : 0;
-        add += (cls[r] == 1) ? ce[r] - cb[r] : 0;
-      }
-      int cnt = lo_c + wave_sum(add);
-#pragma unroll
-      for (int r = 0; r < kSR; ++r) {
-        uint64_t pm = __ballot(cls[r] == 2);
-        while (pm && cnt < need) {
-          const int l = __ffsll((unsigned long long)pm) - 1;
-          pm &= pm - 1;
-          const int bb = __shfl(cb[r], l), ee = __shfl(ce[r], l);
-          for (int j0 = bb; j0 < ee && cnt < need; j0 += 64) {
-            const int jj = j0 + lane;
-            cnt += __popcll(__ballot((jj < ee) && adjacent<2>(p, pts[jj], g)));
-          }
-        }
-      }
-      if (lane == 0) core[sp] = (cnt >= need) ? 1 : 0;
-    }
-  }
-}
-
 // Per cell the smallest (original index << 32 | sorted index) over its core points (segmented
 // wave minimum over the sorted points, one atomicMin per run): the core point with the smallest
 // ORIGINAL index is the cell's representative, which keeps every union-find root its component's
@@ -3073,19 +2628,6 @@ __global__ __launch_bounds__(kBlock) void k_union(const float4* __restrict__ pts
                    });
 }
 
-// root of every core point; ccmin = component minimum original index (filled in two steps)
-__global__ __launch_bounds__(kBlock) void k_compress(int32_t* parent,
-                                                    const uint8_t* __restrict__ core, int64_t n,
-                                                    const int32_t* __restrict__ sorig,
-                                                    int32_t* __restrict__ cmin) {
-  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
-       s += (int64_t)gridDim.x * blockDim.x) {
-    if (!core[s]) continue;
-    const int r = uf_find(parent, (int)s);  // path halving keeps every walk short
-    uf_store(parent + s, r);
-  }
-}
-
 __global__ __launch_bounds__(kBlock) void k_fill_i32(int32_t* p, int64_t n, int32_t v) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -3122,7 +2664,10 @@ __global__ __launch_bounds__(kBlock) void k_cell_roots(int32_t* parent,
                                                       int64_t cells,
                                                       const uint8_t* __restrict__ mutual,
                                                       const int32_t* __restrict__ rep,
-                                                      int32_t* __restrict__ cell_root) {
+                                                      int32_t* __restrict__ cell_root,
+                                                      int32_t* __restrict__ zero = nullptr) {
+  // zero (nullable): a counter of the next kernel, cleared here instead of by a memset launch
+  if (zero && blockIdx.x == 0 && threadIdx.x == 0) *zero = 0;
   const int64_t m = *n_occ;
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m;
        q += (int64_t)gridDim.x * blockDim.x) {
@@ -3272,30 +2817,6 @@ __global__ __launch_bounds__(kBlock) void k_label_core(const int32_t* __restrict
   }
 }
 
-// Per cell, the smallest component key among its core points (INT_MAX: none) -- the same
-// segmented wave minimum over the sorted points as k_cell_min_pair.
-__global__ __launch_bounds__(kBlock) void k_cell_min_key(const int32_t* __restrict__ skey,
-                                                        const int32_t* __restrict__ key_of,
-                                                        int64_t n, int64_t cells,
-                                                        int32_t* __restrict__ cell_key) {
-  const int lane = threadIdx.x & 63;
-  for (int64_t s0 = (int64_t)blockIdx.x * blockDim.x; s0 < n;
-       s0 += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t s = s0 + threadIdx.x;
-    const int key = (s < n) ? skey[s] : -1;
-    const int kv = (s < n) ? key_of[s] : -1;
-    int v = (kv >= 0 && (int64_t)key < cells) ? kv : INT_MAX;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int ov = __shfl_up(v, off, 64);
-      const int ok = __shfl_up(key, off, 64);
-      if (lane >= off && ok == key) v = min(v, ov);
-    }
-    const int next = __shfl_down(key, 1, 64);
-    if ((lane == 63 || next != key) && key >= 0 && v != INT_MAX) atomicMin(cell_key + key, v);
-  }
-}
-
 // K7/K8 (non-core points, queued): the smallest component key over adjacent core points, else
 // none.  One wave per point, one lane per candidate cell of its window.  A cell whose box is
 // wholly adjacent contributes its smallest key (cell_key) with no point read; the others are
@@ -3442,228 +2963,9 @@ __global__ __launch_bounds__(kBlock, 6) void k_label(const float4* __restrict__ 
   }
 }
 
-// K7/K8 by LDS tiles (2-D, slab window <= 7; k_core_tiles' tiles and rowq): the border labels of
-// the non-core points of a tile's own cells, with every candidate cell's record, smallest
-// component key (cell_key) and mutual flag staged in LDS once per tile.  One wave per own cell
-// holding non-core points: its candidates (lanes) classified against the CELL once, then per
-// non-core point the k_label rule -- wholly adjacent cells give their key, the partial ones are
-// resolved in increasing key order while the key can still win (a mutual cell by any adjacent
-// core point, another cell by the smallest key among its adjacent core points).  Overflowing
-// tiles read the same data from global memory.  GLOBAL as in k_label.
-constexpr int kTileCapL = 1280;  // staged cells per tile (32 B record + key + mutual each)
-template <bool GLOBAL>
-__global__ __launch_bounds__(kTileBlock) void k_label_tiles(
-    Geom g, int R, int BY, int nbands, int64_t ntiles, const int32_t* __restrict__ occ,
-    const int32_t* __restrict__ n_occ, const int32_t* __restrict__ rowq,
-    const CellRec<2>* __restrict__ crec,
-    const uint8_t* __restrict__ mutual, const uint32_t* __restrict__ occ_bits,
-    const float2* __restrict__ slab_t, const float4* __restrict__ pts,
-    const int32_t* __restrict__ key_of, const int32_t* __restrict__ cell_key,
-    const int32_t* __restrict__ sorig, MinRank cid, int32_t need, int32_t* __restrict__ labels) {
-  __shared__ CellRec<2> srec[kTileCapL];
-  __shared__ int sck[kTileCapL];
-  __shared__ uint8_t smu[kTileCapL];
-  __shared__ uint16_t smap[kTileMap];
-  __shared__ int s_q0[8], s_base[8], s_reach[8];
-  __shared__ int s_total;
-  const int W = 2 * R + 1, MR = BY + 4;
-  const int64_t tile = (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-  if (tile > ntiles) return;
-  if (tile == ntiles) {  // the isolated cell (non-finite times): its non-core points are noise
-    const int64_t no = *n_occ;
-    if (no > 0 && (int64_t)occ[no - 1] >= g.cells) {
-      const CellRec<2> ri = crec[occ[no - 1]];
-      for (int sp = ri.b + (int)threadIdx.x; sp < ri.e; sp += blockDim.x)
-        if (key_of[sp] < 0) labels[sorig[sp]] = -1;
-    }
-    return;
-  }
-  const int s = (int)(tile / nbands), band = (int)(tile % nbands);
-  const int y0 = band * BY, y1 = min(y0 + BY, g.ny);
-  const int ya = max(y0 - 2, 0), yb = min(y1 + 2, g.ny);
-  const int qo0 = rowq[(int64_t)s * g.ny + y0], qo1 = rowq[(int64_t)s * g.ny + y1];
-  if (qo1 <= qo0) return;
-  if (threadIdx.x < 8) {
-    const int so = threadIdx.x, sl = s - R + so;
-    int q0 = 0, cnt = 0, rc = 0;
-    if (so < W && sl >= 0 && sl < g.nt) {
-      const float2 own = slab_t[s], sr = slab_t[sl];
-      const float gap = (own.x > sr.y) ? (own.x - sr.y) : ((sr.x > own.y) ? (sr.x - own.y) : 0.f);
-      rc = (sr.x <= sr.y && gap <= g.epst) ? 1 : 0;
-      if (rc) {
-        q0 = rowq[(int64_t)sl * g.ny + ya];
-        cnt = rowq[(int64_t)sl * g.ny + yb] - q0;
-      }
-    }
-    int incl = cnt;
-#pragma unroll
-    for (int off = 1; off < 8; off <<= 1) {
-      const int o = __shfl_up(incl, off, 8);
-      if (so >= off) incl += o;
-    }
-    s_q0[so] = q0;
-    s_base[so] = incl - cnt;
-    s_reach[so] = rc;
-    if (so == 7) s_total = incl;
-  }
-  __syncthreads();
-  const bool lds = s_total <= kTileCapL;
-  if (lds) {
-    const int mapn = W * MR * g.nx;
-    for (int i = threadIdx.x; i < mapn; i += blockDim.x) smap[i] = 0xFFFF;
-    __syncthreads();
-    for (int so = 0; so < W; ++so) {
-      const int q0 = s_q0[so], base = s_base[so];
-      const int cnt = (so + 1 < 8 ? s_base[so + 1] : s_total) - base;
-      for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
-        const int32_t key = occ[q0 + i];
-        srec[base + i] = crec[key];
-        sck[base + i] = cell_key[key];
-        smu[base + i] = mutual[key];
-        int x, y, z_, s_;
-        g.split((uint32_t)key, x, y, z_, s_);
-        smap[(so * MR + (y - y0 + 2)) * g.nx + x] = (uint16_t)(base + i);
-      }
-    }
-    __syncthreads();
-  }
-  const int lane = threadIdx.x & 63;
-  constexpr int kSR = 3;
-  for (int q = qo0 + (int)threadIdx.x / 64; q < qo1; q += (int)blockDim.x / 64) {
-    const int32_t ca = occ[q];
-    const CellRec<2> ra = lds ? srec[s_base[R] + (q - s_q0[R])] : crec[ca];
-    if ((lds ? smu[s_base[R] + (q - s_q0[R])] : mutual[ca]) && ra.e - ra.b >= need)
-      continue;  // all core
-    // the cell's non-core points, 64 flags at a time (key_of < 0: not core)
-    const float4 A1 = rec_boxA<2>(ra), A2 = rec_boxB(ra);
-    int cx, cy, cz_, cs_;
-    g.split((uint32_t)ca, cx, cy, cz_, cs_);
-    bool have_cands = false;
-    float4 cA[kSR], cB[kSR];
-    int cb[kSR], ce[kSR], ck[kSR], mu[kSR];
-    for (int sp0 = ra.b; sp0 < ra.e; sp0 += 64) {
-      const int spl = sp0 + lane;
-      uint64_t ncm = __ballot(spl < ra.e && key_of[spl] < 0);
-      if (!ncm) continue;
-      if (!have_cands) {  // candidates of the cell with core points that may reach its box
-        have_cands = true;
-#pragma unroll
-        for (int r = 0; r < kSR; ++r) {
-          cb[r] = ce[r] = 0;
-          ck[r] = INT_MAX;
-          mu[r] = 0;
-          cA[r] = cB[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-          const int pos = r * 64 + lane;
-          const int so = pos / 25, rem = pos - so * 25;
-          const int y = cy + rem / 5 - 2, x = cx + rem % 5 - 2;
-          if (pos < W * 25 && s_reach[so] && y >= 0 && y < g.ny && x >= 0 && x < g.nx) {
-            int id = -1;
-            int kk = INT_MAX;
-            CellRec<2> cr;
-            uint8_t m = 0;
-            if (lds) {
-              const uint16_t u = smap[(so * MR + (y - y0 + 2)) * g.nx + x];
-              if (u != 0xFFFF) {
-                id = u;
-                kk = sck[u];
-              }
-              if (kk != INT_MAX) {
-                cr = srec[id];
-                m = smu[id];
-              }
-            } else {
-              const int64_t k = ((int64_t)(s - R + so) * g.ny + y) * g.nx + x;
-              if ((occ_bits[k >> 5] >> (k & 31)) & 1u) kk = cell_key[k];
-              if (kk != INT_MAX) {
-                cr = crec[k];
-                m = mutual[k];
-              }
-            }
-            if (kk != INT_MAX &&
-                classify_cells<2, true>(A1, rec_boxA<2>(cr), A2, rec_boxB(cr), g) != 0) {
-              cb[r] = cr.b;
-              ce[r] = cr.e;
-              ck[r] = kk;
-              mu[r] = m;
-              cA[r] = rec_boxA<2>(cr);
-              cB[r] = rec_boxB(cr);
-            }
-          }
-        }
-      }
-      while (ncm) {
-        const int l0 = __ffsll((unsigned long long)ncm) - 1;
-        ncm &= ncm - 1;
-        const int sp = sp0 + l0;
-        const float4 p = pts[sp];
-        int cls[kSR];
-        int v = INT_MAX;
-#pragma unroll
-        for (int r = 0; r < kSR; ++r) {
-          cls[r] = (ck[r] != INT_MAX) ? classify<2>(p, cA[r], cB[r], g) : 0;
-          if (cls[r] == 1) v = min(v, ck[r]);
-        }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off));
-        int best = v;
-        uint32_t pend = 0;
-#pragma unroll
-        for (int r = 0; r < kSR; ++r) pend |= (cls[r] == 2) ? (1u << r) : 0u;
-        while (true) {
-          int mine = INT_MAX, mk = -1;
-#pragma unroll
-          for (int r = 0; r < kSR; ++r)
-            if (((pend >> r) & 1u) && ck[r] < best && ck[r] < mine) {
-              mine = ck[r];
-              mk = r;
-            }
-          int mm = mine;
-#pragma unroll
-          for (int off = 32; off > 0; off >>= 1) mm = min(mm, __shfl_xor(mm, off));
-          if (mm == INT_MAX) break;
-          const uint64_t at = __ballot(mine == mm);
-          const int l = __ffsll((unsigned long long)at) - 1;
-          const int kl = __shfl(mk, l);
-          int bsel = 0, esel = 0, msel = 0;
-#pragma unroll
-          for (int r = 0; r < kSR; ++r)
-            if (r == kl) {
-              bsel = cb[r];
-              esel = ce[r];
-              msel = mu[r];
-            }
-          if (lane == l) pend &= ~(1u << kl);
-          const int bl = __shfl(bsel, l), el = __shfl(esel, l);
-          if (__shfl(msel, l)) {  // one component: a single adjacent core point decides
-            bool hit = false;
-            for (int j0 = bl; j0 < el && !hit; j0 += 64) {
-              const int j = j0 + lane;
-              hit = __ballot((j < el) && key_of[j] >= 0 && adjacent<2>(p, pts[j], g)) != 0;
-            }
-            if (hit) best = mm;
-          } else {
-            int lb = INT_MAX;
-            for (int j0 = bl; j0 < el; j0 += 64) {
-              const int j = j0 + lane;
-              if (j < el) {
-                const int m = key_of[j];
-                if (m >= 0 && m < best && m < lb && adjacent<2>(p, pts[j], g)) lb = m;
-              }
-            }
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) lb = min(lb, __shfl_xor(lb, off));
-            best = min(best, lb);
-          }
-        }
-        if (lane == 0) {
-          int32_t out = -1;
-          if (best != INT_MAX) out = GLOBAL ? best : cid[best];
-          labels[sorig[sp]] = out;
-        }
-      }
-    }
-  }
-}
+#ifdef RPT_AB
+#include "stdbscan_ab.inc"
+#endif
 
 // Degenerate parameters (negative/NaN eps): nobody has a neighbour, not even itself.
 __global__ __launch_bounds__(kBlock) void k_isolated_labels(int32_t* labels, int64_t n,
@@ -3768,21 +3070,41 @@ __global__ __launch_bounds__(kBlock) void k_ccmin_global(int32_t* parent,
   }
 }
 // slab[s] = final label of core point s (-1 for non-core); core labels written out
+// The core points' final labels (slab[s] = label, -1 for non-core) and, k_cell_min_key folded in,
+// per cell the smallest label of its core points (cell_key pre-filled with INT_MAX): a segmented
+// wave minimum over the sorted points, one atomic per cell run of a wave.
 __global__ __launch_bounds__(kBlock) void k_label_global_core(const uint8_t* __restrict__ core,
                                                              const int32_t* __restrict__ ccmin,
                                                              const int32_t* __restrict__ gl,
                                                              const int32_t* __restrict__ sorig,
                                                              int64_t n,
                                                              int32_t* __restrict__ slab,
-                                                             int32_t* __restrict__ labels) {
-  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
-       s += (int64_t)gridDim.x * blockDim.x) {
-    int32_t l = -1;
-    if (core[s]) {
-      l = gl[ccmin[s]];
-      labels[sorig[s]] = l;
+                                                             int32_t* __restrict__ labels,
+                                                             const int32_t* __restrict__ skey,
+                                                             int64_t cells,
+                                                             int32_t* __restrict__ cell_key) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t s0 = (int64_t)blockIdx.x * blockDim.x; s0 < n;
+       s0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = s0 + threadIdx.x;
+    int32_t l = -1, key = -1;
+    if (s < n) {
+      key = skey[s];
+      if (core[s]) {
+        l = gl[ccmin[s]];
+        labels[sorig[s]] = l;
+      }
+      slab[s] = l;
     }
-    slab[s] = l;
+    int v = (l >= 0 && (int64_t)key < cells) ? l : INT_MAX;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int ov = __shfl_up(v, off, 64);
+      const int ok = __shfl_up(key, off, 64);
+      if (lane >= off && ok == key) v = min(v, ov);
+    }
+    const int next = __shfl_down(key, 1, 64);
+    if ((lane == 63 || next != key) && key >= 0 && v != INT_MAX) atomicMin(cell_key + key, v);
   }
 }
 
@@ -4162,7 +3484,7 @@ struct DbscanState {
   int32_t* min_pref = nullptr;   // exclusive popcount prefix of min_bits' words (+ total)
   int64_t min_words() const { return n / 32 + 1; }
   int32_t* n_clusters_ptr() const { return min_pref + min_words(); }
-  int32_t cluster_ids(hipStream_t st, int32_t* cell_key);
+  int32_t cluster_ids(hipStream_t st, int32_t* cell_key, int32_t* zero = nullptr);
   int32_t* cell_root = nullptr;  // per cell: root of a mutual cell's core points (k_cell_roots)
   int uf_flags = -1;                         // see XcdRange; -1 = read RPT_UF_FLAGS once
   int k5_legacy = -1;                        // 1: round-1 K5 (fill + point queue); RPT_K5_MODE
@@ -4589,6 +3911,7 @@ int32_t DbscanState::core_pass(hipStream_t st) {
   k5_env();
   const double rs = slab_reach();
   const bool oct = oct_ok();
+#ifdef RPT_AB  // A/B-only forms (stdbscan_ab.inc)
   if (oct && k5_tiles) {
     // LDS tiles: band height BY with the map (W slabs x BY + 4 rows x nx) and the undecided list
     // (BY x nx own cells) within their LDS arrays; rowq (kept for the label pass's tiles)
@@ -4648,6 +3971,7 @@ int32_t DbscanState::core_pass(hipStream_t st) {
     tm.mark();
     return RPT_OK;
   }
+#endif
   // oct: the union's per-cell minima (cell_min_pair) come out of the fill and slow passes
   auto* cm = oct ? reinterpret_cast<unsigned long long*>(cell_min_pair) : nullptr;
   if (k5_fused_path()) {
@@ -4768,9 +4092,11 @@ int32_t DbscanState::union_pass(hipStream_t st) {
     const char* e = ab_env("RPT_UF_COMPRESS");
     uf_compress = (e && std::atoi(e) == 1) ? 1 : 0;
   }
+#ifdef RPT_AB
   if (uf_compress)
     hipLaunchKernelGGL(k_compress, dim3(gb), dim3(kBlock), 0, st, parent, core, n, sorig,
                        (int32_t*)nullptr);
+#endif
   RPT_CHECK_LAUNCH();
   tm.mark();
   return RPT_OK;
@@ -4778,14 +4104,17 @@ int32_t DbscanState::union_pass(hipStream_t st) {
 
 // component minima (k_ccmin; also queues the non-core points) -> MinRank prefix and cluster count
 // cell_key (nullable, pre-filled with INT_MAX): also the per-cell smallest component key
-int32_t DbscanState::cluster_ids(hipStream_t st, int32_t* cell_key) {
+int32_t DbscanState::cluster_ids(hipStream_t st, int32_t* cell_key, int32_t* zero) {
   const int64_t W = min_words();
   RPT_HIP(hipMemsetAsync(min_bits, 0, sizeof(uint32_t) * W, st));
-  // per-cell roots of the mutual cells (read by k_ccmin for their core points)
+  // per-cell roots of the mutual cells (read by k_ccmin for their core points); zero (nullable):
+  // k_ccmin's non-core queue counter, cleared by k_cell_roots
   const bool cr = cell_roots_enabled();
   if (cr)
     hipLaunchKernelGGL(k_cell_roots, dim3(grid_for(n, kBlock, 2048)), dim3(kBlock), 0, st, parent,
-                       occ, n_occ_dev, C, mutual, rep, cell_root);
+                       occ, n_occ_dev, C, mutual, rep, cell_root, zero);
+  else if (zero)
+    RPT_HIP(hipMemsetAsync(zero, 0, sizeof(int32_t), st));
   hipLaunchKernelGGL(k_ccmin, dim3(tile_grid(n)), dim3(kBlock), 0, st, parent, core, n, sorig,
                      ccmin, min_bits, nc_list, nc_list + n, skey, mutual,
                      cr ? (const int32_t*)cell_root : nullptr, C, cell_key);
@@ -4809,20 +4138,27 @@ int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hi
     return RPT_OK;
   }
   int32_t* nc_count = nc_list + n;
-  RPT_HIP(hipMemsetAsync(nc_count, 0, sizeof(int32_t), st));
   const int gc = grid_for(C, kBlock, 8192);
   hipLaunchKernelGGL(k_fill_i32, dim3(gc), dim3(kBlock), 0, st, cell_min, C, INT_MAX);
-  RPT_TRY(cluster_ids(st, cell_min));  // also the per-cell smallest keys (k_cell_min_key fused)
+  // also the per-cell smallest keys (k_cell_min_key fused) and nc_count cleared
+  RPT_TRY(cluster_ids(st, cell_min, nc_count));
   const MinRank mr{min_bits, min_pref};
   hipLaunchKernelGGL(k_label_core, dim3((grid_for(n, kBlock * kPU, 2048) + 7) & ~7), dim3(kBlock), 0, st,
                      ccmin, n, sorig, mr, labels);
+#ifdef RPT_AB
   if (use_label_tiles())
     hipLaunchKernelGGL((k_label_tiles<false>), dim3(tile_grid_blocks()), dim3(kTileBlock), 0, st,
                        g, tile_R, tile_by, tile_nbands, (int64_t)g.nt * tile_nbands, occ,
                        n_occ_dev, rowq, rec<2>(), mutual, occ_bits, slab_t, pts, ccmin, cell_min,
                        sorig, mr, min_samples, labels);
-  else if (dim == 2)
-    hipLaunchKernelGGL(label_w() == 32 ? (k_label<2, false, 32>) : (k_label<2, false, 64>),
+  else if (dim == 2 && label_w() == 64)
+    hipLaunchKernelGGL((k_label<2, false, 64>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts,
+                       skey, g, rec<2>(), occ_bits, slab_t, ccmin, cell_min, mutual, sorig, mr,
+                       nc_list, nc_count, labels);
+  else
+#endif
+  if (dim == 2)
+    hipLaunchKernelGGL((k_label<2, false, 32>),
                        dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
                        rec<2>(), occ_bits, slab_t, ccmin, cell_min, mutual, sorig, mr, nc_list,
                        nc_count, labels);
@@ -4873,26 +4209,34 @@ int32_t DbscanState::labels_global(const int64_t* rep_orig, const int64_t* reps,
   }
   const int gb = grid_for(n, kBlock, 2048);
   int32_t* nc_count = nc_list + n;
-  RPT_HIP(hipMemsetAsync(nc_count, 0, sizeof(int32_t), st));
   const bool cr = cell_roots_enabled();
-  if (cr)
+  if (cr)  // (also clears nc_count for k_ccmin_global)
     hipLaunchKernelGGL(k_cell_roots, dim3(grid_for(n, kBlock, 2048)), dim3(kBlock), 0, st, parent,
-                       occ, n_occ_dev, C, mutual, rep, cell_root);
+                       occ, n_occ_dev, C, mutual, rep, cell_root, nc_count);
+  else
+    RPT_HIP(hipMemsetAsync(nc_count, 0, sizeof(int32_t), st));
+  const int gc = grid_for(C, kBlock, 8192);
+  hipLaunchKernelGGL(k_fill_i32, dim3(gc), dim3(kBlock), 0, st, cell_min, C, INT_MAX);
   hipLaunchKernelGGL(k_ccmin_global, dim3(tile_grid(n)), dim3(kBlock), 0, st, parent, core, n,
                      sorig, rep_orig, reps, nr, ccmin, cid, nc_list, nc_count, skey, mutual,
                      cr ? (const int32_t*)cell_root : nullptr, C, nr_dev);
+  // the core labels with the per-cell smallest label folded in (k_cell_min_key's pass)
   hipLaunchKernelGGL(k_label_global_core, dim3(gb), dim3(kBlock), 0, st, core, ccmin, cid, sorig,
-                     n, slab, labels);
-  const int gc = grid_for(C, kBlock, 8192);
-  hipLaunchKernelGGL(k_fill_i32, dim3(gc), dim3(kBlock), 0, st, cell_min, C, INT_MAX);
-  hipLaunchKernelGGL(k_cell_min_key, dim3(gb), dim3(kBlock), 0, st, skey, slab, n, C, cell_min);
+                     n, slab, labels, skey, C, cell_min);
+#ifdef RPT_AB
   if (use_label_tiles())
     hipLaunchKernelGGL((k_label_tiles<true>), dim3(tile_grid_blocks()), dim3(kTileBlock), 0, st,
                        g, tile_R, tile_by, tile_nbands, (int64_t)g.nt * tile_nbands, occ,
                        n_occ_dev, rowq, rec<2>(), mutual, occ_bits, slab_t, pts, slab, cell_min,
                        sorig, MinRank{nullptr, nullptr}, min_samples, labels);
-  else if (dim == 2)
-    hipLaunchKernelGGL(label_w() == 32 ? (k_label<2, true, 32>) : (k_label<2, true, 64>),
+  else if (dim == 2 && label_w() == 64)
+    hipLaunchKernelGGL((k_label<2, true, 64>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts,
+                       skey, g, rec<2>(), occ_bits, slab_t, slab, cell_min, mutual, sorig,
+                       MinRank{nullptr, nullptr}, nc_list, nc_count, labels);
+  else
+#endif
+  if (dim == 2)
+    hipLaunchKernelGGL((k_label<2, true, 32>),
                        dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
                        rec<2>(), occ_bits, slab_t, slab, cell_min, mutual, sorig,
                        MinRank{nullptr, nullptr}, nc_list, nc_count, labels);
@@ -5098,6 +4442,12 @@ int32_t stdbscan_bounds_dev(const float* x, const float* y, const float* t, int6
                      (int64_t)1, t, n_max, static_cast<Bounds*>(part_dev), n_dev);
   hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(kBlock), 0, st,
                      static_cast<const Bounds*>(part_dev), nbb, static_cast<Bounds*>(out_dev));
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
+}
+int32_t stdbscan_bounds_final_dev(const void* part_dev, int nb, void* out_dev, hipStream_t st) {
+  hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(kBlock), 0, st,
+                     static_cast<const Bounds*>(part_dev), nb, static_cast<Bounds*>(out_dev));
   RPT_CHECK_LAUNCH();
   return RPT_OK;
 }

@@ -57,7 +57,8 @@ def _sources() -> list[Path]:
 
 
 def _headers_mtime() -> float:
-    hs = list(CSRC.glob("*.h")) + list(INCLUDE.glob("*.h"))
+    # (*.inc: kernel sources included by one .hip, e.g. the A/B-only stdbscan_ab.inc)
+    hs = list(CSRC.glob("*.h")) + list(CSRC.glob("*.inc")) + list(INCLUDE.glob("*.h"))
     return max((h.stat().st_mtime for h in hs), default=0.0)
 
 

@@ -7,6 +7,10 @@
 #   tests_all     the whole -m gpu suite
 #   shard_trace   kernel trace of the sharded per-rank step at one rank (125 frames, one lane,
 #                 every collective forced through RCCL) + the host-side profile (identity)
+#   shard_lanes   per-rank step, forced RCCL at one rank: 1 and 3 lanes
+#   tests_dist    the sharded-path GPU tests + the A/B-variant tests
+#   tests_core    ST-DBSCAN parity tests (after a K5-K8 change)
+#   kab           same-box ABBA kernel A/B against abl/librpt_base.so (tools/ab_base.sh)
 #   bench         the default bench line (driver command)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
@@ -39,6 +43,21 @@ for step in "$@"; do
         --lanes 1 --steps 20 --warmup 3 --no-one-stack || exit 1
       run shard_host 200 python tools/prof_shard.py 125 20 || exit 1
       RPT_COMM_FORCE_COLLECTIVES=1 run shard_l1 200 $BS --lanes 1 --steps 40 --warmup 6 || exit 1 ;;
+    shard_lanes)  # per-rank step at one rank, every collective through RCCL: 1 and 3 lanes
+                  # (two rounds, interleaved)
+      for rep in 1 2; do
+        RPT_COMM_FORCE_COLLECTIVES=1 run sl1_$rep 200 $BS --lanes 1 --steps 40 --warmup 6 || exit 1
+        RPT_COMM_FORCE_COLLECTIVES=1 run sl3_$rep 200 $BS --lanes 3 --steps 40 --warmup 6 || exit 1
+      done ;;
+    tests_dist)
+      run tests_dist 1000 $PYT --timeout 990 tests/test_dist_gpu.py tests/test_ab_variants_gpu.py \
+        || exit 1 ;;
+    tests_core)   # ST-DBSCAN parity (g2, full-size configs, 1000-frame digests, dense share)
+      run tests_core 900 $PYT --timeout 600 tests/test_stdbscan_gpu.py tests/test_fullsize_gpu.py \
+        "tests/test_bigstack_gpu.py::test_bench_stacks_lanes3_match_oracle" \
+        "tests/test_bigstack_gpu.py::test_dense_config4_share_invariants" || exit 1 ;;
+    kab)          # same-box ABBA kernel traces: in-tree build vs abl/librpt_base.so
+      TAG=$KABTAG WL="${KABWL:-std std1000 dense}" run kab 1000 bash tools/kab2.sh || exit 1 ;;
     bench)
       run bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;

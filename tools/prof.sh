@@ -4,16 +4,18 @@
 #   1. bench.py with hipEvent stage timing under rocprofv3 --kernel-trace --stats: the bench line
 #      (gpurun_out/prof_<key>.json) and the kernel summary of the SAME command;
 #   2. FETCH_SIZE and WRITE_SIZE in separate --pmc passes (counters only) ->
-#      profiles/r3/k5_traffic_<key>.json / k1_traffic_<key>.json (tools/pmc_traffic.py);
-#   3. the summaries copied to gpurun_out/r3/ (kernel_stats_<key>.csv, bench_prof_<key>.json,
-#      the traffic JSONs): gpurun brings gpurun_out/ back; `cp gpurun_out/r3/* profiles/r3/`.
-# Usage on the GPU box, from the repo root:  bash tools/prof_r3.sh <key> [bench args...]
+#      profiles/$RD/k5_traffic_<key>.json / k1_traffic_<key>.json (tools/pmc_traffic.py);
+#   3. the summaries copied to gpurun_out/$RD/ (kernel_stats_<key>.csv, bench_prof_<key>.json,
+#      the traffic JSONs): gpurun brings gpurun_out/ back; `cp gpurun_out/$RD/* profiles/$RD/`.
+# RD = the round's profile directory (default r5).
+# Usage on the GPU box, from the repo root:  [RD=r5] bash tools/prof.sh <key> [bench args...]
 #   keys used: std_1000f (default workload), std_125f (--total-frames 125),
 #              dense_125f (--dense --total-frames 125)
 KEY=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
-mkdir -p gpurun_out/r3
+RD=${RD:-r5}
+mkdir -p gpurun_out/$RD
 export TMPDIR=/tmp
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 STEPS=${STEPS:-6}
@@ -27,9 +29,9 @@ for C in FETCH_SIZE WRITE_SIZE; do
     -- python "$R/bench.py" $ARGS --no-timing > "gpurun_out/pmc_${C}_$KEY.log" 2>&1
   rc=$?; echo "pmc $C rc=$rc" >> "gpurun_out/pmc_${C}_$KEY.log"; [ $rc -eq 0 ] || exit $rc
 done
-RPT_PROFILE_OUT="$R/gpurun_out/r3" python tools/pmc_traffic.py r3 "k5_traffic_$KEY.json" "bench.py $ARGS (one stack in flight)" \
+RPT_PROFILE_OUT="$R/gpurun_out/$RD" python tools/pmc_traffic.py $RD "k5_traffic_$KEY.json" "bench.py $ARGS (one stack in flight)" \
   > "gpurun_out/pmc_traffic_$KEY.log" || exit 1
 ST=$(find "$R/gpurun_out/prof_$KEY" -name '*kernel_stats.csv' | head -1)
-cp "$ST" "gpurun_out/r3/kernel_stats_$KEY.csv"
-tail -1 "gpurun_out/prof_$KEY.json" > "gpurun_out/r3/bench_prof_$KEY.json"
-echo "[prof_r3] $KEY done; steps=$STEPS (+1 warm-up) per command"
+cp "$ST" "gpurun_out/$RD/kernel_stats_$KEY.csv"
+tail -1 "gpurun_out/prof_$KEY.json" > "gpurun_out/$RD/bench_prof_$KEY.json"
+echo "[prof] $KEY done; steps=$STEPS (+1 warm-up) per command"
