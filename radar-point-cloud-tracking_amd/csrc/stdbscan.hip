@@ -2498,8 +2498,12 @@ __global__ __launch_bounds__(kBlock) void k_union_listed(const float4* __restric
     const int sa = g.slab_of_key(ca);
     const Window w = make_window<2, false>(cx, cy, cz, A2.z, A2.w, g, slab_t, sa);
     // the undecided candidate of this lane (rb >= 0) -> one adjacent core pair unites A and B
+    // Candidates sharing a root (e.g. one cell column over the slab window, united whole by the
+    // first pass) need ONE adjacent pair between them: once a search unites A with a root, the
+    // remaining candidates of that root are connected too and are dropped without a search.
     auto settle = [&](int rb, int bb, int eb) {
-      const bool cand = rb >= 0 && uf_find(parent, ra, halve) != uf_find(parent, rb, halve);
+      const int rbr = rb >= 0 ? uf_find(parent, rb, halve) : -1;
+      const bool cand = rb >= 0 && uf_find(parent, ra, halve) != rbr;
       uint64_t cm = __ballot(cand);
       while (cm) {
         const int l = __ffsll((unsigned long long)cm) - 1;
@@ -2536,7 +2540,11 @@ __global__ __launch_bounds__(kBlock) void k_union_listed(const float4* __restric
             hit = __ballot(adj) != 0;
           }
         }
-        if (hit && lane == 0) uf_unite(parent, sorig, ra, rbl, halve);
+        if (hit) {
+          if (lane == 0) uf_unite(parent, sorig, ra, rbl, halve);
+          const int rr = __shfl(rbr, l);
+          cm &= ~__ballot(rbr == rr);
+        }
       }
     };
     if (!(pm.w & kPmaskFull)) {
@@ -3479,6 +3487,14 @@ struct DbscanState {
                            // the grid build's radix key buffers, dead after the build)
   int union_list = -1;     // RPT_UNION_LIST=0: the second union pass enumerates every window
   int union_pair = -1;     // RPT_UNION_PAIR=0: one cell per wave in the box-certain union pass
+  // occupied cells per wave iteration of k_union_cells_pair: 64 on large stacks (one header load
+  // per lane), 16 on small ones (RPT_UNION_CPW in the A/B build)
+  int union_cpw() const {
+    const char* e = ab_env("RPT_UNION_CPW");
+    const int v = e ? std::atoi(e) : 0;
+    if (v >= 1 && v <= 64) return v;
+    return n > (int64_t(1) << 24) ? 64 : 16;
+  }
   int uf_compress = -1;    // RPT_UF_COMPRESS=1: a compression pass closes the union stage
   uint32_t* min_bits = nullptr;  // component minima, 1 bit per original index (MinRank)
   int32_t* min_pref = nullptr;   // exclusive popcount prefix of min_bits' words (+ total)
@@ -3987,6 +4003,14 @@ int32_t DbscanState::core_pass(hipStream_t st) {
                          rec<2>(), occ_bits, slab_t, slow, n_slow, core, sorig, cm, cq);
     RPT_CHECK_LAUNCH();
     cmin_ready = true;
+#ifdef RPT_AB
+    if (ab_env("RPT_STATS")) {  // A/B diagnostics: K5's slow queue (syncs)
+      int32_t h = 0;
+      (void)hipMemcpyAsync(&h, n_slow, 4, hipMemcpyDeviceToHost, st);
+      (void)hipStreamSynchronize(st);
+      std::fprintf(stderr, "[rpt stats] n=%lld k5_slow_queue=%d\n", (long long)n, h);
+    }
+#endif
     tm.mark();
     return RPT_OK;
   }
@@ -4060,7 +4084,7 @@ int32_t DbscanState::union_pass(hipStream_t st) {
     if (union_pair)  // two cells per wave (RPT_UNION_PAIR=0 in the A/B build: one)
       hipLaunchKernelGGL(k_union_cells_pair, dim3(gw), dim3(kBlock), 0, st, pts, g, occ, n_occ,
                          rec<2>(), occ_bits, slab_t, rep, mutual, sorig, parent, uf_flags, pm,
-                         plist, pcount, n > (int64_t(1) << 24) ? 64 : 16);
+                         plist, pcount, union_cpw());
     else
       hipLaunchKernelGGL((k_union_cells<2, false>), dim3(gw), dim3(kBlock), 0, st, pts, g,
                          cell_start, occ, n_occ, rec<2>(), occ_bits, slab_t, core, rep, mutual,
@@ -4096,6 +4120,14 @@ int32_t DbscanState::union_pass(hipStream_t st) {
   if (uf_compress)
     hipLaunchKernelGGL(k_compress, dim3(gb), dim3(kBlock), 0, st, parent, core, n, sorig,
                        (int32_t*)nullptr);
+  if (ab_env("RPT_STATS")) {  // A/B diagnostics: the queue and list sizes of this run (syncs)
+    int32_t h[2] = {0, 0};
+    (void)hipMemcpyAsync(&h[0], n_occ_dev, 4, hipMemcpyDeviceToHost, st);
+    if (listing) (void)hipMemcpyAsync(&h[1], pcount, 4, hipMemcpyDeviceToHost, st);
+    (void)hipStreamSynchronize(st);
+    std::fprintf(stderr, "[rpt stats] n=%lld occupied=%d listed_cells=%d\n", (long long)n, h[0],
+                 h[1]);
+  }
 #endif
   RPT_CHECK_LAUNCH();
   tm.mark();

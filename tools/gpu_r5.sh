@@ -8,6 +8,7 @@
 #   shard_trace   kernel trace of the sharded per-rank step at one rank (125 frames, one lane,
 #                 every collective forced through RCCL) + the host-side profile (identity)
 #   shard_lanes   per-rank step, forced RCCL at one rank: 1 and 3 lanes
+#   diag          A/B-build diagnostics (queue sizes, union cells per wave)
 #   tests_dist    the sharded-path GPU tests + the A/B-variant tests
 #   tests_core    ST-DBSCAN parity tests (after a K5-K8 change)
 #   kab           same-box ABBA kernel A/B against abl/librpt_base.so (tools/ab_base.sh)
@@ -48,6 +49,20 @@ for step in "$@"; do
       for rep in 1 2; do
         RPT_COMM_FORCE_COLLECTIVES=1 run sl1_$rep 200 $BS --lanes 1 --steps 40 --warmup 6 || exit 1
         RPT_COMM_FORCE_COLLECTIVES=1 run sl3_$rep 200 $BS --lanes 3 --steps 40 --warmup 6 || exit 1
+      done ;;
+    diag)         # A/B build: queue / list sizes (RPT_STATS) per workload, union cells per wave
+      AB=radar-point-cloud-tracking_amd/rpt/librpt_ab.so
+      for w in "125" "1000" "125 --dense"; do
+        RPT_LIB=$AB RPT_STATS=1 run "stats_${w// /_}" 200 python bench.py --total-frames $w \
+          --lanes 1 --steps 1 --warmup 0 --no-one-stack --no-dense-k5 --no-cpu-baseline \
+          --h2d-steps 0 --no-timing || exit 1
+        grep "rpt stats" "$O/stats_${w// /_}.log" | sort | uniq -c | head -8
+      done
+      for c in ${CPWS:-4 8 16 32}; do
+        RPT_LIB=$PWD/$AB RPT_UNION_CPW=$c bash tools/kprof.sh cpw$c --lanes 1 --total-frames 125 \
+          || exit 1
+        python tools/kstats.py "$(ls gpurun_out/kprof_cpw$c/*kernel_stats.csv | head -1)" 4 \
+          | grep -i "union\|label<" | sed "s/^/cpw=$c /"
       done ;;
     tests_dist)
       run tests_dist 1000 $PYT --timeout 990 tests/test_dist_gpu.py tests/test_ab_variants_gpu.py \
