@@ -2294,8 +2294,10 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
         }
 #pragma unroll
         for (int k = 0; k < kR; ++k) {
-          const bool cand =
-              (cls[k] == 2) && uf_find(parent, ra, halve) != uf_find(parent, rb[k], halve);
+          // (candidates of one root need one adjacent pair: dropped after a hit, as in
+          // k_union_listed)
+          const int rbr = (cls[k] == 2) ? uf_find(parent, rb[k], halve) : -1;
+          const bool cand = (cls[k] == 2) && uf_find(parent, ra, halve) != rbr;
           uint64_t pm = __ballot(cand);
           while (pm) {
             const int l = __ffsll((unsigned long long)pm) - 1;
@@ -2324,7 +2326,11 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
                 }
               }
             }
-            if (hit && lane == 0) uf_unite(parent, sorig, ra, rbl, halve);
+            if (hit) {
+              if (lane == 0) uf_unite(parent, sorig, ra, rbl, halve);
+              const int rr = __shfl(rbr, l);
+              pm &= ~__ballot(rbr == rr);
+            }
           }
         }
       }
@@ -2511,6 +2517,8 @@ __global__ __launch_bounds__(kBlock) void k_union_listed(const float4* __restric
         const int rbl = __shfl(rb, l);
         const int ebl = __shfl(eb, l);
         const int bbl = __shfl(bb, l);
+        // other waves may have connected A and this candidate since the roots were read
+        if (uf_find(parent, ra, halve) == uf_find(parent, rbl, halve)) continue;
         bool hit = false;
         for (int jb0 = bbl; jb0 < ebl && !hit; jb0 += 64) {
           const int jb = jb0 + lane;
