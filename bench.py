@@ -242,8 +242,8 @@ def main():
                     help="sharded runs at one rank: keep the CommSequencer's slot order although "
                          "every collective is the identity (what the ordering costs)")
     ap.add_argument("--host-workers", type=int, default=8,
-                    help="threads for rank 0's host stage (cluster order + tracker) of "
-                         "consecutive steps")
+                    help="threads for the host stages (cluster order + tracker; rank 0's on the "
+                         "sharded path) of consecutive steps")
     ap.add_argument("--no-one-stack", action="store_true",
                     help="skip the one-stack-in-flight leg (and so K5's roofline)")
     ap.add_argument("--sync-host", action="store_true",
@@ -338,8 +338,12 @@ def main():
                               ds.geo.sin_t, cfg.n_frames * len(cfg.gains))
             run = lambda e: pipe.run(e, rank * F)  # noqa: E731
     else:
+        # host stages of consecutive stacks are independent (one tracker per stack): with fewer
+        # workers than lanes, the stacks that finish together at the end of the timed region
+        # queue their host stages (~6 ms each at 1000 frames) behind one another
         pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), dev, timing=timing,
-                                  async_host=not args.sync_host, lanes=args.lanes)
+                                  async_host=not args.sync_host, lanes=args.lanes,
+                                  host_workers=args.host_workers)
         pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
                           cfg.n_frames * len(cfg.gains))
         run = lambda e: pipe.submit(e)  # noqa: E731

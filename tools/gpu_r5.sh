@@ -12,6 +12,7 @@
 #   tests_dist    the sharded-path GPU tests + the A/B-variant tests
 #   tests_core    ST-DBSCAN parity tests (after a K5-K8 change)
 #   kab           same-box ABBA kernel A/B against abl/librpt_base.so (tools/ab_base.sh)
+#   prof          profiles/r5 kernel traces + PMC traffic (tools/prof.sh) for the three workloads
 #   bench         the default bench line (driver command)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
@@ -73,6 +74,21 @@ for step in "$@"; do
         "tests/test_bigstack_gpu.py::test_dense_config4_share_invariants" || exit 1 ;;
     kab)          # same-box ABBA kernel traces: in-tree build vs abl/librpt_base.so
       TAG=$KABTAG WL="${KABWL:-std std1000 dense}" run kab 1000 bash tools/kab2.sh || exit 1 ;;
+    prof)         # profiles/r5: kernel traces + FETCH/WRITE passes, one stack in flight, per workload
+      RD=r5 run prof_std_1000f 900 bash tools/prof.sh std_1000f || exit 1
+      RD=r5 run prof_std_125f 600 bash tools/prof.sh std_125f --total-frames 125 || exit 1
+      RD=r5 run prof_dense_125f 600 bash tools/prof.sh dense_125f --dense --total-frames 125 \
+        || exit 1 ;;
+    bench_ab)     # the driver's bench line: host workers 2 (round 4) vs 8, lanes 5 vs 4, interleaved
+      BB="python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-dense-k5 --h2d-steps 0"
+      for rep in 1 2; do
+        run bab_hw2_$rep 300 $BB --host-workers 2 || exit 1
+        run bab_hw8_$rep 300 $BB || exit 1
+        run bab_l4_$rep 300 $BB --lanes 4 || exit 1
+      done
+      for f in $O/bab_*.log; do
+        python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['value'], d['ms_per_step'], d['steady_state']['ms_per_step'])" $f
+      done ;;
     bench)
       run bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
