@@ -31,15 +31,13 @@ latency-bound kernels share the CUs; interleaved same-box runs with every lane s
 one untimed stack before the warm-up steps (its buffers are allocated on first use: a lane left
 cold cost ~80 ms inside the timed region); `one_stack_in_flight` repeats the steps strictly one after
 another, and K5's roofline is taken from that leg (K5 alone on the GPU).
-At N>1 (the frame-sharded path) one stack is in flight per rank by default; `--lanes 3` keeps
-three, their collectives through ONE communicator in a fixed software-pipeline order
-(rpt.dist.CommSequencer, validated with gloo at 8 ranks and on RCCL at one rank with every
-collective forced through it -- RPT_COMM_FORCE_COLLECTIVES=1: 1.66 ms per step with 3 lanes against
-2.27 with 1, profiles/r4/rccl_ab/ -- but not yet on RCCL across GPUs, hence not the default).
-With one rank (`--sharded`, the 125-frame per-rank share of 8 GPUs) the default
-stays 3: the shard driver v2 measured 1.48 ms per step with 3 lanes (1.62 ms with the
-sequencer's order kept, --sequenced) against 2.12 ms with 1
-(profiles/r4/bench_sharded1rank_125f_*.json).
+At N>1 (the frame-sharded path) three stacks are in flight per rank by default, their
+collectives through ONE communicator in a fixed software-pipeline order (rpt.dist.CommSequencer:
+every rank issues the same collectives in the same order; validated with gloo at 8 ranks and on
+RCCL at one rank with every collective forced through it -- RPT_COMM_FORCE_COLLECTIVES=1: 1.58-1.63
+ms per 125-frame step with 3 lanes against 2.15-2.27 with 1, profiles/r5/rccl_lanes/); `--lanes 1`
+runs one stack at a time.  With one rank (`--sharded`, the 125-frame per-rank share of 8 GPUs)
+the default is 3 as well (identity collectives).
 After the timed region (N=1, timing on), K5 is also timed on the per-GPU shares at 8 GPUs, where
 SURVEY.md §8(d) sets the 0.40 roofline target: `roofline_c4_share` (125 standard frames, the
 configs[3] stack's share) and `roofline_configs4_share` (125 dense frames, configs[4]'s), one
@@ -232,9 +230,8 @@ def main():
                     help="sharded runs: ShardedStackPipeline (HipOps stages composed in Python) "
                          "instead of the native shard driver")
     ap.add_argument("--lanes", type=int, default=None,
-                    help="stacks in flight at once (default 5 at one rank, 3 with --sharded: "
-                         "native handles on separate streams; default 1 at N>1 ranks, where a "
-                         "lane is a "
+                    help="stacks in flight at once (default 5 at one rank: native handles on "
+                         "separate streams; 3 with --sharded and at N>1 ranks, where a lane is a "
                          "NativeShardPipeline with its own stream and thread, all lanes on ONE "
                          "process group in rpt.dist.CommSequencer's order); 1 = strictly one "
                          "after another")
@@ -254,10 +251,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if args.lanes is None:
-        # several lanes share one RCCL communicator only through CommSequencer's order, which has
-        # run on gloo (8 ranks) and on RCCL at one rank (forced collectives), never on RCCL across
-        # GPUs: one lane per rank until it has (--lanes 3 opts in)
-        args.lanes = (3 if args.sharded else 5) if world == 1 else 1
+        # N > 1: three stacks in flight per rank, their collectives through ONE communicator in
+        # CommSequencer's order -- every rank issues the same collectives in the same order, at
+        # most one thread inside a collective at a time (validated on gloo up to 8 ranks and on
+        # RCCL at one rank with every collective forced through it); --lanes 1 = one at a time
+        args.lanes = (3 if args.sharded else 5) if world == 1 else 3
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # --sharded: the frame-sharded multi-GPU path even at one rank (measures its per-rank cost)
     dist = world > 1 or args.sharded

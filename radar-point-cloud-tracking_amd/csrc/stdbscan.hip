@@ -64,6 +64,50 @@ inline float ord2f(uint32_t u) {  // host side
   return f;
 }
 
+// ---------------------------------------------------------------- cross-lane reductions by DPP
+// __shfl_xor compiles to a ds_bpermute round trip through LDS, each one waited for; DPP moves
+// are VALU.  Within an aligned row of 16 lanes, step k of row_reduce makes every lane of the
+// aligned 2^k-lane group hold the group's result: lane i reads i^1, i^2 (quad permutes), then
+// 7-i of its eight (row_half_mirror), then 15-i of its row (row_mirror).  Every lane of a group
+// must be active.
+template <int Ctl>
+__device__ __forceinline__ int dpp_mov(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, Ctl, 0xF, 0xF, false);
+}
+template <int Ctl>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(dpp_mov<Ctl>(__float_as_int(v)));
+}
+template <int Ctl>
+__device__ __forceinline__ uint64_t dpp_mov(uint64_t v) {
+  const uint32_t lo = (uint32_t)dpp_mov<Ctl>((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)dpp_mov<Ctl>((int)(uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+template <int G, class T, class F>
+__device__ __forceinline__ T row_reduce(T v, F op) {
+  static_assert(G == 2 || G == 4 || G == 8 || G == 16, "groups within a row");
+  v = op(v, dpp_mov<0xB1>(v));                 // quad_perm [1,0,3,2]
+  if (G >= 4) v = op(v, dpp_mov<0x4E>(v));     // quad_perm [2,3,0,1]
+  if (G >= 8) v = op(v, dpp_mov<0x141>(v));    // row_half_mirror
+  if (G >= 16) v = op(v, dpp_mov<0x140>(v));   // row_mirror
+  return v;
+}
+struct OpMin {  // floats: fminf (the ignore-NaN minimum the shuffle form used)
+  template <class T>
+  __device__ T operator()(T a, T b) const { return b < a ? b : a; }
+  __device__ float operator()(float a, float b) const { return fminf(a, b); }
+};
+struct OpMax {
+  template <class T>
+  __device__ T operator()(T a, T b) const { return a < b ? b : a; }
+  __device__ float operator()(float a, float b) const { return fmaxf(a, b); }
+};
+struct OpAdd {
+  template <class T>
+  __device__ T operator()(T a, T b) const { return a + b; }
+};
+
 
 template <int D>
 __global__ __launch_bounds__(kBlock) void k_bounds(const float* __restrict__ x,
@@ -845,10 +889,11 @@ __device__ __forceinline__ float wave_maxf(float v) {
   for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
   return v;
 }
+// whole-wave sum (every lane active): rows by DPP, then the four row sums read as scalars
 __device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  return v;
+  v = row_reduce<16>(v, OpAdd{});
+  return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) +
+         __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
 }
 __device__ __forceinline__ int wave_excl_sum(int v, int* total) {
   const int lane = threadIdx.x & 63;
@@ -960,22 +1005,12 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ 
         }
       }
     }
-    if (sorig) {
-#pragma unroll
-      for (int off = L / 2; off > 0; off >>= 1) {
-        const uint32_t olo = (uint32_t)__shfl_xor((int)(uint32_t)mn, off, L);
-        const uint32_t ohi = (uint32_t)__shfl_xor((int)(uint32_t)(mn >> 32), off, L);
-        const uint64_t o = ((uint64_t)ohi << 32) | olo;
-        mn = o < mn ? o : mn;
-      }
-    }
-#pragma unroll
-    for (int off = L / 2; off > 0; off >>= 1) {
-      x0 = fminf(x0, __shfl_xor(x0, off, L)); x1 = fmaxf(x1, __shfl_xor(x1, off, L));
-      y0 = fminf(y0, __shfl_xor(y0, off, L)); y1 = fmaxf(y1, __shfl_xor(y1, off, L));
-      z0 = fminf(z0, __shfl_xor(z0, off, L)); z1 = fmaxf(z1, __shfl_xor(z1, off, L));
-      t0 = fminf(t0, __shfl_xor(t0, off, L)); t1 = fmaxf(t1, __shfl_xor(t1, off, L));
-    }
+    // (the cell loop is uniform over the aligned 16-lane group: all its lanes are active)
+    if (sorig) mn = row_reduce<L>(mn, OpMin{});
+    x0 = row_reduce<L>(x0, OpMin{}); x1 = row_reduce<L>(x1, OpMax{});
+    y0 = row_reduce<L>(y0, OpMin{}); y1 = row_reduce<L>(y1, OpMax{});
+    z0 = row_reduce<L>(z0, OpMin{}); z1 = row_reduce<L>(z1, OpMax{});
+    t0 = row_reduce<L>(t0, OpMin{}); t1 = row_reduce<L>(t1, OpMax{});
     if (D != 3) {
       z0 = t0;  // 2-D: pts[].z carries t (unused by the 2-D tests)
       z1 = t1;
@@ -1631,6 +1666,11 @@ __device__ __forceinline__ void cells_fill_epilogue(const Geom& g, bool act, int
 // points at a time: the point flags (byte stores, 64 consecutive bytes per instruction) and the
 // undecided cells' points appended to the level-4 queue (one atomic per wave).  The all-core
 // cells' (min original, sorted) pairs are k_cell_box's (allmin).  No per-point loads at all.
+// Sum over each aligned group of eight lanes, every lane of the group getting it (row_reduce:
+// DPP, no LDS round trips).  Every lane of a group must be active (the cell kernels' branches
+// are group-uniform).
+__device__ __forceinline__ int sum8(int v) { return row_reduce<8>(v, OpAdd{}); }
+
 constexpr int kCwMaxR = 3;
 constexpr int kCwBatch = 4;  // candidate records per lane in flight together (k_core_cells_oct)
 template <bool FUSED = false>
@@ -1654,6 +1694,10 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
   // (k_core_fill, the next kernel on the stream, is its first user)
   if (!FUSED && zero_counter && blockIdx.x == 0 && threadIdx.x == 0) *zero_counter = 0;
   __shared__ CwQueue lq;
+  // per lane its five (slab, row) slots' keys of column dx = 0, written once per cell and read
+  // per candidate (recomputing them took ~20 VALU per candidate, three 32-bit multiplies among
+  // them; five more registers spilled)
+  __shared__ int32_t s_k0[5][kBlock];
   if (FUSED) {
     if (threadIdx.x == 0) {
       lq.n = 0;
@@ -1700,14 +1744,6 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
       uint32_t m5[5];  // slot i: occupied columns dx = 0..4 of its row (x = cx - 2 + dx)
       int psi[5];      // slot i: slab index
       const uint32_t mg = (65535u + (uint32_t)W) / (uint32_t)W;  // p / W = (p * mg) >> 16
-      // key of column dx = 0 of pair p's row (recomputed per candidate: five more registers
-      // for the slots' keys spilled)
-      auto pair_key0 = [&](int p) -> int {
-        const int k = (int)__umul24((uint32_t)p, mg) >> 16;
-        const int si = p - k * W;
-        return (int)__umul24((uint32_t)((cs + si - R) * g.ny + cy + cw_row(k) - 2),
-                             (uint32_t)g.nx) + (cx - 2);
-      };
       {
         // branch-free: an invalid slot reads a valid word and masks it off, so all eleven loads
         // of every lane are in flight together (a conditional load is a branch ending in a full
@@ -1727,6 +1763,7 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
           const bool v = p < 5 * W && s2 >= 0 && s2 < g.nt && y >= 0 && y < g.ny;
           // (int32 keys: cells < 2^30)
           const int k0 = ((v ? s2 : cs) * g.ny + (v ? y : cy)) * g.nx + (cx - 2);
+          s_k0[i][threadIdx.x] = k0;  // column dx = 0 of slot i (the lane's own LDS words)
           const int kk = k0 < 0 ? 0 : k0;
           const int w = kk >> 5;
           const uint32_t lo_w = occ_bits[w], hi_w = occ_bits[w + 1];
@@ -1761,8 +1798,7 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
         bool decided = false;
         while (true) {
           int rem = m25 ? 1 : 0;
-#pragma unroll
-          for (int off = 4; off > 0; off >>= 1) rem += __shfl_xor(rem, off, 8);
+          rem = sum8(rem);
           if (rem == 0) break;  // (uniform over the cell's eight lanes)
           CellRec<2> cr[kCwBatch];
           bool has[kCwBatch];
@@ -1773,7 +1809,7 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
             const int p = __builtin_ctz(m25 | (1u << 31));
             m25 &= m25 - 1;
             const int sl5 = (p * 13) >> 6;  // slot p / 5 (p < 32)
-            const int key = pair_key0(j + 8 * sl5) + (p - 5 * sl5);
+            const int key = s_k0[sl5][threadIdx.x] + (p - 5 * sl5);
             cr[i] = crec[has[i] ? key : ca];
           }
 #pragma unroll
@@ -1785,8 +1821,7 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
             hi += (cls != 0) ? cr[i].e - cr[i].b : 0;
           }
           int ls = lo;
-#pragma unroll
-          for (int off = 4; off > 0; off >>= 1) ls += __shfl_xor(ls, off, 8);
+          ls = sum8(ls);
           if (ls >= need) {
             decided = true;
             break;
@@ -1795,11 +1830,8 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
         if (decided) {
           flag = 1;
         } else {
-#pragma unroll
-          for (int off = 4; off > 0; off >>= 1) {
-            lo += __shfl_xor(lo, off, 8);
-            hi += __shfl_xor(hi, off, 8);
-          }
+          lo = sum8(lo);
+          hi = sum8(hi);
           flag = (lo >= need) ? 1 : ((hi < need) ? 0 : 2);
         }
       }
@@ -2870,9 +2902,10 @@ __global__ __launch_bounds__(kBlock, 6) void k_label(const float4* __restrict__ 
     const uint64_t b = __ballot(v);
     return (W == 64) ? b : ((b >> shift) & 0xffffffffull);
   };
-  auto gmin = [&](int v) -> int {
-#pragma unroll
-    for (int off = W / 2; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off));
+  auto gmin = [&](int v) -> int {  // rows by DPP, then the 16 (and 32) lane steps
+    v = row_reduce<16>(v, OpMin{});
+    v = min(v, __shfl_xor(v, 16));
+    if (W == 64) v = min(v, __shfl_xor(v, 32));
     return v;
   };
   const int64_t nc = *nc_count;
