@@ -2376,6 +2376,7 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
   }
 }
 
+constexpr int kPlistBlockCap = 1024;  // k_union_cells_pair's block list (4 KiB of LDS)
 // K6a (2-D, box-certain pass) with TWO cells per wave: each half-wave takes one mutual cell with
 // core points of the 64-cell chunk, lanes over its candidate cells B > A (window positions
 // k * 32 + lane, k < kR: the exact-slab windows of integral times hold 75 positions), so two
@@ -2402,6 +2403,18 @@ __global__ __launch_bounds__(kBlock, 6) void k_union_cells_pair(
   // of the GPU idles
   const int64_t items = (no + cpw - 1) / cpw;
   const XcdRange xr = xcd_items(items, (uf_flags & 2) != 0);
+  // plist entries gather in a block LDS list, appended to the global list by ONE atomic per
+  // block at the end (a same-address global atomic per wave iteration serialised: ~4 ns each,
+  // 10 k of them at 125 frames: 147 -> 123 us at 16 cells per wave, 278 -> 130 at 4); a wave
+  // whose entries no longer fit appends them itself
+  __shared__ int32_t s_pl[kPlistBlockCap];
+  __shared__ int s_pn, s_pvalid, s_pdone;
+  if (threadIdx.x == 0) {
+    s_pn = 0;
+    s_pvalid = 0;
+    s_pdone = 0;
+  }
+  __syncthreads();
   for (int64_t it = xr.first; it < xr.end; it += xr.step) {
     int ql = -1, cal = INT_MAX, ral = -1;
     uint8_t mal = 0;
@@ -2493,10 +2506,38 @@ __global__ __launch_bounds__(kBlock, 6) void k_union_cells_pair(
       if (u1 && l1 >= 0) lmask |= 1ull << l1;
     }
     if (plist && lmask) {
+      const int m = __popcll(lmask);
       int base = 0;
-      if (lane == 0) base = atomicAdd(pcount, __popcll(lmask));
+      if (lane == 0) base = atomicAdd(&s_pn, m);
       base = __shfl(base, 0);
-      if ((lmask >> lane) & 1ull) plist[base + __popcll(lmask & ((1ull << lane) - 1ull))] = ql;
+      const bool fits = base + m <= kPlistBlockCap;  // (wave-uniform; s_pn only grows)
+      if (fits) {
+        if (lane == 0) atomicMax(&s_pvalid, base + m);
+      } else {
+        if (lane == 0) base = atomicAdd(pcount, m);
+        base = __shfl(base, 0);
+      }
+      if ((lmask >> lane) & 1ull) {
+        const int at = base + __popcll(lmask & ((1ull << lane) - 1ull));
+        if (fits)
+          s_pl[at] = ql;
+        else
+          plist[at] = ql;
+      }
+    }
+  }
+  if (plist) {  // (kernel-uniform) the block's list -> plist, by the block's last wave to finish
+    // (no block barrier: the other waves leave at once and free their slots)
+    __threadfence_block();
+    int last = 0;
+    if (lane == 0) last = atomicAdd(&s_pdone, 1) == (int)(blockDim.x / 64) - 1;
+    if (__shfl(last, 0)) {
+      __threadfence_block();
+      const int cnt = s_pvalid;
+      int base = 0;
+      if (lane == 0 && cnt) base = atomicAdd(pcount, cnt);
+      base = __shfl(base, 0);
+      for (int k = lane; k < cnt; k += 64) plist[base + k] = s_pl[k];
     }
   }
 }

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build abl/librpt_base.so from a commit (default HEAD) in a temporary worktree: the same-box A/B
-# baseline of tools/r4_suite_ab.sh.   bash tools/ab_base.sh [rev]
+# baseline of tools/kab2.sh.   bash tools/ab_base.sh [rev]
 set -e
 cd "$(dirname "$0")/.."
 REV=${1:-HEAD}
