@@ -364,7 +364,8 @@ __global__ __launch_bounds__(kBlock) void k_gather(const float* __restrict__ x,
                                                   const uint32_t* __restrict__ svals,
                                                   float4* __restrict__ pts,
                                                   int32_t* __restrict__ sorig,
-                                                  int32_t* __restrict__ skey) {
+                                                  int32_t* __restrict__ skey,
+                                                  int32_t* __restrict__ spos) {
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
        s += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = svals[s];
@@ -375,6 +376,7 @@ __global__ __launch_bounds__(kBlock) void k_gather(const float* __restrict__ x,
     p.z = (D == 3) ? z[i * stride] : p.w;
     pts[s] = p;
     sorig[s] = (int32_t)i;
+    if (spos) spos[i] = (int32_t)s;
     skey[s] = (int32_t)skeys[s];
   }
 }
@@ -436,6 +438,15 @@ static int slab_chunks_override() {
   return v;
 }
 
+// RPT_LABEL_ORIG=0: core labels scattered from sorted order (k_label_core; A/B)
+static bool label_core_orig() {
+  static const bool v = [] {
+    const char* e = ab_env("RPT_LABEL_ORIG");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return v;
+}
+
 // RPT_CHUNK_SCAN=1: the one-block-per-slab k_slab_chunk_scan (A/B)
 static bool chunk_scan_legacy() {
   static const bool v = [] {
@@ -490,7 +501,7 @@ __global__ __launch_bounds__(kBucketBlock) void k_slab_bucket(
     const float* __restrict__ x, const float* __restrict__ y, int64_t stride,
     const float* __restrict__ t, Geom g, const int32_t* __restrict__ slab_lo,
     float4* __restrict__ pts, int32_t* __restrict__ sorig, int32_t* __restrict__ skey,
-    int32_t* __restrict__ cell_start, int32_t* __restrict__ occ_tmp,
+    int32_t* __restrict__ spos, int32_t* __restrict__ cell_start, int32_t* __restrict__ occ_tmp,
     int32_t* __restrict__ slab_occ, uint32_t* __restrict__ occ_bits,
     unsigned long long* __restrict__ cmin_all = nullptr) {
   // the slab's nx * ny cell counts, sized at launch (a 463-m sweep at cells of 5.6 m: 27 KiB, so
@@ -631,6 +642,7 @@ __global__ __launch_bounds__(kBucketBlock) void k_slab_bucket(
         const int dst = lo + base + rank;
         pts[dst] = make_float4(px[u], py[u], pt[u], pt[u]);
         sorig[dst] = i;
+        if (spos) spos[i] = dst;  // (kernel-uniform; coalesced: i runs over the lanes)
         skey[dst] = s * P + c;
         if (cmin_all && mn[c] == i)
           cmin_all[(int64_t)s * P + c] = ((unsigned long long)(uint32_t)i << 32) | (uint32_t)dst;
@@ -823,7 +835,7 @@ __global__ __launch_bounds__(kBucketBlock) void k_slab_chunk_scatter(
     const float* __restrict__ x, const float* __restrict__ y, int64_t stride,
     const float* __restrict__ t, Geom g, const int32_t* __restrict__ slab_lo, int CH,
     const int32_t* __restrict__ hist_g, float4* __restrict__ pts, int32_t* __restrict__ sorig,
-    int32_t* __restrict__ skey) {
+    int32_t* __restrict__ skey, int32_t* __restrict__ spos) {
   extern __shared__ int32_t cur[];
   const int s = blockIdx.x / CH, ch = blockIdx.x - s * CH;
   const int P = g.nx * g.ny;
@@ -851,6 +863,7 @@ __global__ __launch_bounds__(kBucketBlock) void k_slab_chunk_scatter(
         const int dst = base + atomicAdd(&cur[c], 1);
         pts[dst] = make_float4(px[u], py[u], pt[u], pt[u]);
         sorig[dst] = i;
+        if (spos) spos[i] = dst;  // (kernel-uniform; coalesced: i runs over the lanes)
         skey[dst] = s * P + c;
       }
     }
@@ -2560,7 +2573,10 @@ __global__ __launch_bounds__(kBlock) void k_union_listed(const float4* __restric
                                                         int32_t* __restrict__ parent, int uf_flags,
                                                         const uint4* __restrict__ pmask,
                                                         const int32_t* __restrict__ plist,
-                                                        const int32_t* __restrict__ pcount) {
+                                                        const int32_t* __restrict__ pcount,
+                                                        int32_t* __restrict__ lstat = nullptr) {
+  // lstat (A/B build, RPT_STATS): undecided candidates, candidates whose roots differed, searches,
+  // hits
   const int lane = threadIdx.x & 63;
   const bool halve = !(uf_flags & 1);
   const XcdRange xr = xcd_items(*pcount, false);
@@ -2584,6 +2600,15 @@ __global__ __launch_bounds__(kBlock) void k_union_listed(const float4* __restric
       const int rbr = rb >= 0 ? uf_find(parent, rb, halve) : -1;
       const bool cand = rb >= 0 && uf_find(parent, ra, halve) != rbr;
       uint64_t cm = __ballot(cand);
+#ifdef RPT_AB
+      if (lstat) {
+        const int nb = __popcll(__ballot(rb >= 0));
+        if (lane == 0) {
+          atomicAdd(&lstat[0], nb);
+          atomicAdd(&lstat[1], __popcll(cm));
+        }
+      }
+#endif
       while (cm) {
         const int l = __ffsll((unsigned long long)cm) - 1;
         cm &= cm - 1;
@@ -2592,6 +2617,9 @@ __global__ __launch_bounds__(kBlock) void k_union_listed(const float4* __restric
         const int bbl = __shfl(bb, l);
         // other waves may have connected A and this candidate since the roots were read
         if (uf_find(parent, ra, halve) == uf_find(parent, rbl, halve)) continue;
+#ifdef RPT_AB
+        if (lstat && lane == 0) atomicAdd(&lstat[2], 1);
+#endif
         bool hit = false;
         for (int jb0 = bbl; jb0 < ebl && !hit; jb0 += 64) {
           const int jb = jb0 + lane;
@@ -2622,6 +2650,9 @@ __global__ __launch_bounds__(kBlock) void k_union_listed(const float4* __restric
           }
         }
         if (hit) {
+#ifdef RPT_AB
+          if (lstat && lane == 0) atomicAdd(&lstat[3], 1);
+#endif
           if (lane == 0) uf_unite(parent, sorig, ra, rbl, halve);
           const int rr = __shfl(rbr, l);
           cm &= ~__ballot(rbr == rr);
@@ -2906,6 +2937,46 @@ __global__ __launch_bounds__(kBlock) void k_label_core(const int32_t* __restrict
   }
 }
 
+// The same in ORIGINAL order through the grid build's inverse permutation spos: the labels are
+// written in whole lines and the component keys gathered (a frame's keys stay in L2) instead of
+// 4-byte label writes scattered over each frame, whose partly written lines L2 evicts (dense
+// share: 1.23 GB written for 0.25 GB of labels).  Non-core points are left to k_label.
+__global__ __launch_bounds__(kBlock) void k_label_core_orig(const int32_t* __restrict__ ccmin,
+                                                           int64_t n,
+                                                           const int32_t* __restrict__ spos,
+                                                           MinRank cid,
+                                                           int32_t* __restrict__ labels) {
+  const int64_t T = (n + (int64_t)kBlock * kPU - 1) / ((int64_t)kBlock * kPU);
+  const bool xm = (gridDim.x & 7) == 0;  // XCD-contiguous tiles (runs of whole frames)
+  const int64_t xg = blockIdx.x & 7, nbx = gridDim.x >> 3;
+  const int64_t t_lo = xm ? T * xg / 8 : blockIdx.x, t_hi = xm ? T * (xg + 1) / 8 : T;
+  const int64_t t_step = xm ? nbx : gridDim.x;
+  for (int64_t ti = t_lo + (xm ? (int64_t)(blockIdx.x >> 3) : 0); ti < t_hi; ti += t_step) {
+    const int64_t tile = ti * kBlock * kPU;
+    int32_t sp[kPU], own[kPU];
+#pragma unroll
+    for (int u = 0; u < kPU; ++u)  // branch-free (clamped); streamed once
+      sp[u] = __builtin_nontemporal_load(spos + min(tile + (int64_t)u * kBlock + threadIdx.x,
+                                                     n - 1));
+#pragma unroll
+    for (int u = 0; u < kPU; ++u) own[u] = ccmin[sp[u]];
+    uint32_t w[kPU];
+    int32_t pr[kPU];
+#pragma unroll
+    for (int u = 0; u < kPU; ++u) {
+      const int32_t m = own[u] >= 0 ? own[u] : 0;
+      w[u] = cid.bits[m >> 5];
+      pr[u] = cid.pref[m >> 5];
+    }
+#pragma unroll
+    for (int u = 0; u < kPU; ++u) {
+      const int64_t i = tile + (int64_t)u * kBlock + threadIdx.x;
+      if (i < n && own[u] >= 0)
+        labels[i] = pr[u] + __popc(w[u] & ((1u << (own[u] & 31)) - 1u));
+    }
+  }
+}
+
 // K7/K8 (non-core points, queued): the smallest component key over adjacent core points, else
 // none.  One wave per point, one lane per candidate cell of its window.  A cell whose box is
 // wholly adjacent contributes its smallest key (cell_key) with no point read; the others are
@@ -3159,6 +3230,36 @@ __global__ __launch_bounds__(kBlock) void k_ccmin_global(int32_t* parent,
     block_append_bits(tile, nbits, nc_list, nc_count);
   }
 }
+// The core labels in original order through the grid build's inverse permutation (spos, the
+// slab buffer before k_label_global_core reuses it): whole-line label writes (k_label_core_orig)
+__global__ __launch_bounds__(kBlock) void k_label_global_orig(const uint8_t* __restrict__ core,
+                                                             const int32_t* __restrict__ ccmin,
+                                                             const int32_t* __restrict__ gl,
+                                                             const int32_t* __restrict__ spos,
+                                                             int64_t n,
+                                                             int32_t* __restrict__ labels) {
+  const int64_t T = (n + (int64_t)kBlock * kPU - 1) / ((int64_t)kBlock * kPU);
+  for (int64_t ti = blockIdx.x; ti < T; ti += gridDim.x) {
+    const int64_t tile = ti * kBlock * kPU;
+    int32_t sp[kPU], m[kPU];
+    uint8_t c[kPU];
+#pragma unroll
+    for (int u = 0; u < kPU; ++u)  // branch-free (clamped)
+      sp[u] = __builtin_nontemporal_load(spos + min(tile + (int64_t)u * kBlock + threadIdx.x,
+                                                     n - 1));
+#pragma unroll
+    for (int u = 0; u < kPU; ++u) {
+      c[u] = core[sp[u]];
+      m[u] = ccmin[sp[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < kPU; ++u) {
+      const int64_t i = tile + (int64_t)u * kBlock + threadIdx.x;
+      if (i < n && c[u]) labels[i] = gl[m[u]];
+    }
+  }
+}
+
 // slab[s] = final label of core point s (-1 for non-core); core labels written out
 // The core points' final labels (slab[s] = label, -1 for non-core) and, k_cell_min_key folded in,
 // per cell the smallest label of its core points (cell_key pre-filled with INT_MAX): a segmented
@@ -3182,7 +3283,7 @@ __global__ __launch_bounds__(kBlock) void k_label_global_core(const uint8_t* __r
       key = skey[s];
       if (core[s]) {
         l = gl[ccmin[s]];
-        labels[sorig[s]] = l;
+        if (labels) labels[sorig[s]] = l;  // (kernel-uniform; null: k_label_global_orig's)
       }
       slab[s] = l;
     }
@@ -3420,7 +3521,7 @@ __global__ __launch_bounds__(kBlock) void k_frames_points_list(
   }
 }
 
-// spos[orig] = sorted position
+// spos[orig] = sorted position (when the grid build did not write it)
 __global__ void k_inverse_perm(const int32_t* __restrict__ sorig, int64_t n,
                                int32_t* __restrict__ spos) {
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
@@ -3655,7 +3756,11 @@ struct DbscanState {
   const CellRec<D>* rec() const {
     return static_cast<const CellRec<D>*>(crec);
   }
-  int32_t* slab = nullptr;   // per sorted point: final label of core points (global path)
+  // per original point: its sorted position (the grid build's inverse permutation, read by the
+  // label passes, when spos_on); the global path then reuses it for the sorted points' final
+  // core labels
+  int32_t* slab = nullptr;
+  bool spos_on = false;
   int32_t* cell_min = nullptr;  // per cell: smallest component key (label pass)
   uint8_t* fok = nullptr;    // per cell: frame condition met by every core point (denoise)
   bool integral_t = false;   // every finite t integral (slab = one frame id)
@@ -3884,6 +3989,11 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
     // (three chunks measured 1.10 -> 1.25 ms).  The chunk histograms live in the radix key
     // buffers (4 n words, dead on this path).
     const int64_t avg = n / std::max<int64_t>(nt, 1);
+    // dense slabs: the label passes' scattered core-label writes cost more than the inverse
+    // permutation written here (configs[4] share: 676 -> 253 us for +57 in the scatter; at
+    // standard density the scattered writes stay in L2 and the extra store costs +68 us)
+    spos_on = avg > 8 * kChunkPts;
+    int32_t* spos_w = spos_on ? slab : nullptr;
     int64_t ch = avg > 8 * kChunkPts ? (avg + kChunkPts - 1) / kChunkPts : 1;
     ch = std::max<int64_t>(ch, (512 + nt - 1) / std::max<int64_t>(nt, 1));
     int CH = (int)std::min<int64_t>(ch, 64);
@@ -3926,7 +4036,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
       }
       hipLaunchKernelGGL(k_slab_chunk_scatter, dim3((unsigned)(nt * CH)), dim3(kBucketBlock),
                          hist_bytes, st, x, y, stride, t, g, slab_lo, CH, hist_g, pts, sorig,
-                         skey);
+                         skey, spos_w);
     } else {
       // the fused K5's all-core cell minima from the counting sort when both LDS arrays fit 64 KiB
       bucket_allmin = k5_fused_path() && 2 * hist_bytes <= 65536;
@@ -3934,7 +4044,8 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
       RPT_HIP(hipFuncSetAttribute((const void*)k_slab_bucket,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       hipLaunchKernelGGL(k_slab_bucket, dim3((unsigned)nt), dim3(kBucketBlock), lds, st, x, y,
-                         stride, t, g, slab_lo, pts, sorig, skey, cell_start, hpos, slab_occ,
+                         stride, t, g, slab_lo, pts, sorig, skey, spos_w, cell_start, hpos,
+                         slab_occ,
                          occ_bits,
                          bucket_allmin ? reinterpret_cast<unsigned long long*>(cell_min_pair)
                                        : nullptr);
@@ -3957,8 +4068,9 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
     while ((int64_t(1) << bits) <= C1) ++bits;
     uint32_t *sk, *sv;
     RPT_TRY(radix_sort_pairs(keys, vals, keys_alt, vals_alt, n, bits, rtmp, &sk, &sv, st));
+    spos_on = false;
     hipLaunchKernelGGL(k_gather<D>, dim3(gb), dim3(kBlock), 0, st, x, y, z, stride, t, n, sk, sv,
-                       pts, sorig, skey);
+                       pts, sorig, skey, nullptr);
     RPT_HIP(hipMemsetAsync(cell_start, 0, sizeof(int32_t) * C1, st));
     hipLaunchKernelGGL(k_cell_runs, dim3(gb), dim3(kBlock), 0, st, skey, n, cell_start, hpos);
     RPT_CHECK_LAUNCH();
@@ -4161,6 +4273,7 @@ int32_t DbscanState::union_pass(hipStream_t st) {
                        cmin);
   hipLaunchKernelGGL(k_parent_init_pair, dim3(grid_for(n, kBlock * kPU, 2048)), dim3(kBlock), 0,
                      st, parent, n, core, skey, mutual, cmin, C, rep);
+  int32_t* lstat_dev = nullptr;  // (A/B diagnostics)
   if (dim == 2) {
     uint4* pm = listing ? pmask : nullptr;
     if (union_pair)  // two cells per wave (RPT_UNION_PAIR=0 in the A/B build: one)
@@ -4171,10 +4284,18 @@ int32_t DbscanState::union_pass(hipStream_t st) {
       hipLaunchKernelGGL((k_union_cells<2, false>), dim3(gw), dim3(kBlock), 0, st, pts, g,
                          cell_start, occ, n_occ, rec<2>(), occ_bits, slab_t, core, rep, mutual,
                          sorig, parent, uf_flags, pm, plist, pcount);
+#ifdef RPT_AB
+    if (listing && ab_env("RPT_STATS")) {  // (A/B diagnostics: a leaked 16 B per process)
+      static int32_t* buf = nullptr;
+      if (!buf) (void)hipMalloc(&buf, 16);
+      lstat_dev = buf;
+      (void)hipMemsetAsync(lstat_dev, 0, 16, st);
+    }
+#endif
     if (listing)
       hipLaunchKernelGGL(k_union_listed, dim3(gw), dim3(kBlock), 0, st, pts, g, occ, rec<2>(),
                          occ_bits, slab_t, core, rep, mutual, sorig, parent, uf_flags, pm, plist,
-                         pcount);
+                         pcount, lstat_dev);
     else
       hipLaunchKernelGGL((k_union_cells<2, true>), dim3(gw), dim3(kBlock), 0, st, pts, g,
                          cell_start, occ, n_occ, rec<2>(), occ_bits, slab_t, core, rep, mutual,
@@ -4203,12 +4324,15 @@ int32_t DbscanState::union_pass(hipStream_t st) {
     hipLaunchKernelGGL(k_compress, dim3(gb), dim3(kBlock), 0, st, parent, core, n, sorig,
                        (int32_t*)nullptr);
   if (ab_env("RPT_STATS")) {  // A/B diagnostics: the queue and list sizes of this run (syncs)
-    int32_t h[2] = {0, 0};
+    int32_t h[2] = {0, 0}, ls[4] = {0, 0, 0, 0};
     (void)hipMemcpyAsync(&h[0], n_occ_dev, 4, hipMemcpyDeviceToHost, st);
     if (listing) (void)hipMemcpyAsync(&h[1], pcount, 4, hipMemcpyDeviceToHost, st);
+    if (lstat_dev) (void)hipMemcpyAsync(ls, lstat_dev, 16, hipMemcpyDeviceToHost, st);
     (void)hipStreamSynchronize(st);
-    std::fprintf(stderr, "[rpt stats] n=%lld occupied=%d listed_cells=%d\n", (long long)n, h[0],
-                 h[1]);
+    std::fprintf(stderr,
+                 "[rpt stats] n=%lld occupied=%d listed_cells=%d listed: undecided=%d "
+                 "roots_differ=%d searches=%d hits=%d\n",
+                 (long long)n, h[0], h[1], ls[0], ls[1], ls[2], ls[3]);
   }
 #endif
   RPT_CHECK_LAUNCH();
@@ -4257,8 +4381,12 @@ int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hi
   // also the per-cell smallest keys (k_cell_min_key fused) and nc_count cleared
   RPT_TRY(cluster_ids(st, cell_min, nc_count));
   const MinRank mr{min_bits, min_pref};
-  hipLaunchKernelGGL(k_label_core, dim3((grid_for(n, kBlock * kPU, 2048) + 7) & ~7), dim3(kBlock), 0, st,
-                     ccmin, n, sorig, mr, labels);
+  if (spos_on && label_core_orig())
+    hipLaunchKernelGGL(k_label_core_orig, dim3((grid_for(n, kBlock * kPU, 2048) + 7) & ~7),
+                       dim3(kBlock), 0, st, ccmin, n, slab, mr, labels);
+  else
+    hipLaunchKernelGGL(k_label_core, dim3((grid_for(n, kBlock * kPU, 2048) + 7) & ~7),
+                       dim3(kBlock), 0, st, ccmin, n, sorig, mr, labels);
 #ifdef RPT_AB
   if (use_label_tiles())
     hipLaunchKernelGGL((k_label_tiles<false>), dim3(tile_grid_blocks()), dim3(kTileBlock), 0, st,
@@ -4334,9 +4462,15 @@ int32_t DbscanState::labels_global(const int64_t* rep_orig, const int64_t* reps,
   hipLaunchKernelGGL(k_ccmin_global, dim3(tile_grid(n)), dim3(kBlock), 0, st, parent, core, n,
                      sorig, rep_orig, reps, nr, ccmin, cid, nc_list, nc_count, skey, mutual,
                      cr ? (const int32_t*)cell_root : nullptr, C, nr_dev);
-  // the core labels with the per-cell smallest label folded in (k_cell_min_key's pass)
+  // the core labels in original order (before slab's inverse permutation is overwritten), then
+  // per sorted point the final core labels with the per-cell smallest label folded in
+  // (k_cell_min_key's pass)
+  const bool orig = spos_on && label_core_orig();
+  if (orig)
+    hipLaunchKernelGGL(k_label_global_orig, dim3(grid_for(n, kBlock * kPU, 2048)), dim3(kBlock), 0,
+                       st, core, ccmin, cid, slab, n, labels);
   hipLaunchKernelGGL(k_label_global_core, dim3(gb), dim3(kBlock), 0, st, core, ccmin, cid, sorig,
-                     n, slab, labels, skey, C, cell_min);
+                     n, slab, orig ? nullptr : labels, skey, C, cell_min);
 #ifdef RPT_AB
   if (use_label_tiles())
     hipLaunchKernelGGL((k_label_tiles<true>), dim3(tile_grid_blocks()), dim3(kTileBlock), 0, st,
@@ -4409,16 +4543,16 @@ int32_t DbscanState::frames_pass(int32_t min_frames, hipStream_t st) {
 }
 
 int32_t DbscanState::labels_fifo(int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st) {
-  const int gb = grid_for(n, kBlock, 2048);
   int32_t* nc_count = nc_list + n;
   int32_t* spos = slab;
   RPT_HIP(hipMemsetAsync(nc_count, 0, sizeof(int32_t), st));
   RPT_TRY(cluster_ids(st, nullptr));
-  hipLaunchKernelGGL(k_inverse_perm, dim3(gb), dim3(kBlock), 0, st, sorig, n, spos);
-  RPT_CHECK_LAUNCH();
+  if (!spos_on)  // (else the grid build's)
+    hipLaunchKernelGGL(k_inverse_perm, dim3(grid_for(n, kBlock, 2048)), dim3(kBlock), 0, st,
+                       sorig, n, spos);
   const MinRank mr{min_bits, min_pref};
-  hipLaunchKernelGGL(k_label_core, dim3((grid_for(n, kBlock * kPU, 2048) + 7) & ~7), dim3(kBlock), 0, st,
-                     ccmin, n, sorig, mr, labels);
+  hipLaunchKernelGGL(k_label_core_orig, dim3((grid_for(n, kBlock * kPU, 2048) + 7) & ~7),
+                     dim3(kBlock), 0, st, ccmin, n, spos, mr, labels);
   if (dim == 2)
     hipLaunchKernelGGL((k_label_fifo<2>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
                        rec<2>(), occ_bits, slab_t, ccmin, rep, sorig, spos, mr, nc_list,
