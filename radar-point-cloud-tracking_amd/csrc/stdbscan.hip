@@ -2097,9 +2097,14 @@ __global__ __launch_bounds__(kBlock) void k_init_occ_cells(const int32_t* __rest
                                                           int32_t* __restrict__ rep,
                                                           unsigned long long* __restrict__ cmin,
                                                           int32_t* __restrict__ zero_counter =
+                                                              nullptr,
+                                                          int32_t* __restrict__ zero_counter2 =
                                                               nullptr) {
-  // the union passes' cell-list counter, zeroed here (its first user is two launches later)
-  if (zero_counter && blockIdx.x == 0 && threadIdx.x == 0) *zero_counter = 0;
+  // the union passes' cell-list counters, zeroed here (their first user is two launches later)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (zero_counter) *zero_counter = 0;
+    if (zero_counter2) *zero_counter2 = 0;
+  }
   const int64_t m = *n_occ;
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m;
        q += (int64_t)gridDim.x * blockDim.x) {
@@ -2389,7 +2394,58 @@ __global__ __launch_bounds__(kBlock) void k_union_cells(const float4* __restrict
   }
 }
 
-constexpr int kPlistBlockCap = 1024;  // k_union_cells_pair's block list (4 KiB of LDS)
+// A block's LDS list of ints, appended to a global list (count at *gcount) by ONE global atomic
+// issued by the block's last wave to finish (no block barrier: the other waves leave at once):
+// a same-address global atomic per wave iteration serialised, ~4 ns each (k_union_cells_pair's
+// undecided-cell list, 10 k of them at 125 frames: 147 -> 123 us at 16 cells per wave, 278 -> 130
+// at 4).  A wave whose entries no longer fit appends them itself.
+template <int Cap>
+struct BlockList {
+  int32_t buf[Cap];
+  int n, valid;
+  __device__ void init() {  // (one thread, before a block barrier)
+    n = 0;
+    valid = 0;
+  }
+  // the lanes of m append v (wave-uniform call)
+  __device__ void push(uint64_t m, int v, int lane, int32_t* glist, int32_t* gcount) {
+    if (!m) return;
+    const int c = __popcll(m);
+    int base = 0;
+    if (lane == 0) base = atomicAdd(&n, c);
+    base = __shfl(base, 0);
+    const bool fits = base + c <= Cap;  // (wave-uniform; n only grows, so the fits are a prefix)
+    if (fits) {
+      if (lane == 0) atomicMax(&valid, base + c);
+    } else {
+      if (lane == 0) base = atomicAdd(gcount, c);
+      base = __shfl(base, 0);
+    }
+    if ((m >> lane) & 1ull) {
+      const int at = base + __popcll(m & ((1ull << lane) - 1ull));
+      if (fits)
+        buf[at] = v;
+      else
+        glist[at] = v;
+    }
+  }
+  __device__ void flush(int lane, int32_t* glist, int32_t* gcount) {  // (the block's last wave)
+    const int cnt = valid;
+    int base = 0;
+    if (lane == 0 && cnt) base = atomicAdd(gcount, cnt);
+    base = __shfl(base, 0);
+    for (int k = lane; k < cnt; k += 64) glist[base + k] = buf[k];
+  }
+};
+// true in the block's last wave to reach it (the LDS lists are complete then)
+__device__ __forceinline__ bool block_last_wave(int* done, int lane) {
+  __threadfence_block();
+  int last = 0;
+  if (lane == 0) last = atomicAdd(done, 1) == (int)(blockDim.x / 64) - 1;
+  last = __shfl(last, 0);
+  if (last) __threadfence_block();
+  return last != 0;
+}
 // K6a (2-D, box-certain pass) with TWO cells per wave: each half-wave takes one mutual cell with
 // core points of the 64-cell chunk, lanes over its candidate cells B > A (window positions
 // k * 32 + lane, k < kR: the exact-slab windows of integral times hold 75 positions), so two
@@ -2404,7 +2460,8 @@ __global__ __launch_bounds__(kBlock, 6) void k_union_cells_pair(
     const int32_t* __restrict__ rep, const uint8_t* __restrict__ mutual,
     const int32_t* __restrict__ sorig, int32_t* __restrict__ parent, int uf_flags,
     uint4* __restrict__ pmask, int32_t* __restrict__ plist, int32_t* __restrict__ pcount,
-    int cpw) {
+    int cpw, int32_t* __restrict__ nm_list, int32_t* __restrict__ nm_count) {
+  // nm_list (nullable): the non-mutual cells with core points (k_union_nm's list)
   constexpr int W = 32;
   const int lane = threadIdx.x & 63;
   const int hl = lane & (W - 1), h0 = lane - hl;
@@ -2416,16 +2473,13 @@ __global__ __launch_bounds__(kBlock, 6) void k_union_cells_pair(
   // of the GPU idles
   const int64_t items = (no + cpw - 1) / cpw;
   const XcdRange xr = xcd_items(items, (uf_flags & 2) != 0);
-  // plist entries gather in a block LDS list, appended to the global list by ONE atomic per
-  // block at the end (a same-address global atomic per wave iteration serialised: ~4 ns each,
-  // 10 k of them at 125 frames: 147 -> 123 us at 16 cells per wave, 278 -> 130 at 4); a wave
-  // whose entries no longer fit appends them itself
-  __shared__ int32_t s_pl[kPlistBlockCap];
-  __shared__ int s_pn, s_pvalid, s_pdone;
+  __shared__ BlockList<1024> s_pl;  // plist entries (4 KiB)
+  __shared__ BlockList<256> s_nm;   // nm_list entries
+  __shared__ int s_done;
   if (threadIdx.x == 0) {
-    s_pn = 0;
-    s_pvalid = 0;
-    s_pdone = 0;
+    s_pl.init();
+    s_nm.init();
+    s_done = 0;
   }
   __syncthreads();
   for (int64_t it = xr.first; it < xr.end; it += xr.step) {
@@ -2437,6 +2491,7 @@ __global__ __launch_bounds__(kBlock, 6) void k_union_cells_pair(
       ral = rep[cal];
       mal = mutual[cal];
     }
+    if (nm_list) s_nm.push(__ballot(ral >= 0 && !mal), cal, lane, nm_list, nm_count);
     uint64_t todo = __ballot(ral >= 0 && mal);
     uint64_t lmask = 0;  // cells of this chunk with undecided candidates (plist)
     while (todo) {  // (wave-uniform) two cells at a time, one per half
@@ -2518,40 +2573,33 @@ __global__ __launch_bounds__(kBlock, 6) void k_union_cells_pair(
       if (u0) lmask |= 1ull << l0;
       if (u1 && l1 >= 0) lmask |= 1ull << l1;
     }
-    if (plist && lmask) {
-      const int m = __popcll(lmask);
-      int base = 0;
-      if (lane == 0) base = atomicAdd(&s_pn, m);
-      base = __shfl(base, 0);
-      const bool fits = base + m <= kPlistBlockCap;  // (wave-uniform; s_pn only grows)
-      if (fits) {
-        if (lane == 0) atomicMax(&s_pvalid, base + m);
-      } else {
-        if (lane == 0) base = atomicAdd(pcount, m);
-        base = __shfl(base, 0);
-      }
-      if ((lmask >> lane) & 1ull) {
-        const int at = base + __popcll(lmask & ((1ull << lane) - 1ull));
-        if (fits)
-          s_pl[at] = ql;
-        else
-          plist[at] = ql;
-      }
-    }
+    if (plist) s_pl.push(lmask, ql, lane, plist, pcount);
   }
-  if (plist) {  // (kernel-uniform) the block's list -> plist, by the block's last wave to finish
-    // (no block barrier: the other waves leave at once and free their slots)
-    __threadfence_block();
-    int last = 0;
-    if (lane == 0) last = atomicAdd(&s_pdone, 1) == (int)(blockDim.x / 64) - 1;
-    if (__shfl(last, 0)) {
-      __threadfence_block();
-      const int cnt = s_pvalid;
-      int base = 0;
-      if (lane == 0 && cnt) base = atomicAdd(pcount, cnt);
-      base = __shfl(base, 0);
-      for (int k = lane; k < cnt; k += 64) plist[base + k] = s_pl[k];
-    }
+  if ((plist || nm_list) && block_last_wave(&s_done, lane)) {  // the block's lists -> global
+    if (plist) s_pl.flush(lane, plist, pcount);
+    if (nm_list) s_nm.flush(lane, nm_list, nm_count);
+  }
+}
+
+// Root snapshot after the box-certain pass: croot[c] = root of rep[c] per occupied cell with core
+// points (-1 otherwise).  Unions only merge, so equal snapshot roots stay connected: the listed
+// pass then settles a candidate with ONE load instead of two parent-chain walks -- 99.5 % of the
+// undecided candidates share A's root by then (1000 frames: 4.0 M candidates, 19 k roots
+// different; configs[4] share: 33.7 M, 282 k).
+__global__ __launch_bounds__(kBlock) void k_cell_root_snapshot(const int32_t* __restrict__ occ,
+                                                              const int32_t* __restrict__ n_occ,
+                                                              const int32_t* __restrict__ rep,
+                                                              int32_t* __restrict__ parent,
+                                                              int64_t cells, int uf_flags,
+                                                              int32_t* __restrict__ croot) {
+  const bool halve = !(uf_flags & 1);
+  const int64_t no = *n_occ;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < no;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int c = occ[q];
+    if ((int64_t)c >= cells) continue;  // (the isolated, non-finite time cell)
+    const int r = rep[c];
+    croot[c] = r >= 0 ? uf_find(parent, r, halve) : -1;
   }
 }
 
@@ -2574,18 +2622,27 @@ __global__ __launch_bounds__(kBlock) void k_union_listed(const float4* __restric
                                                         const uint4* __restrict__ pmask,
                                                         const int32_t* __restrict__ plist,
                                                         const int32_t* __restrict__ pcount,
+                                                        const int32_t* __restrict__ croot,
                                                         int32_t* __restrict__ lstat = nullptr) {
   // lstat (A/B build, RPT_STATS): undecided candidates, candidates whose roots differed, searches,
   // hits
   const int lane = threadIdx.x & 63;
   const bool halve = !(uf_flags & 1);
   const XcdRange xr = xcd_items(*pcount, false);
+  if (xr.first >= xr.end) return;
+  // software-pipelined headers (as k_cell_box): the next cell's key and mask and the one after's
+  // list entry load while this cell is settled; branch-free from clamped list positions
+  auto list_at = [&](int64_t ii) { return plist[ii < xr.end ? ii : xr.end - 1]; };
+  int ca = occ[list_at(xr.first)];
+  uint4 pm = pmask[list_at(xr.first)];
+  int qn = list_at(xr.first + xr.step);
   for (int64_t i = xr.first; i < xr.end; i += xr.step) {
-    const int q = plist[i];
-    const int ca = occ[q];
     const int ra = rep[ca];
-    const uint4 pm = pmask[q];
+    const int sra = croot ? croot[ca] : -1;  // A's snapshot root (kernel-uniform)
     const CellRec<2> ra_rec = crec[ca];
+    const int can = occ[qn];
+    const uint4 pmn = pmask[qn];
+    const int qnn = list_at(i + 2 * xr.step);
     const int ba = ra_rec.b, ea = ra_rec.e;
     const float4 A1 = rec_boxA<2>(ra_rec), A2 = rec_boxB(ra_rec);
     int cx, cy, cz;
@@ -2668,10 +2725,12 @@ __global__ __launch_bounds__(kBlock) void k_union_listed(const float4* __restric
         const uint32_t word = k == 0 ? (lane < 32 ? pm.x : pm.y) : (lane < 32 ? pm.z : pm.w);
         if ((word >> (lane & 31)) & 1u) {
           const int64_t c = window_cell<2>(w, k * 64 + lane, g, slab_t, A2.z, A2.w);
-          const CellRec<2> cr = crec[c];
-          rb[k] = rep[c];
-          ebv[k] = cr.e;
-          bbv[k] = cr.b;
+          if (!croot || croot[c] != sra) {  // (else connected already: no record, no walk)
+            const CellRec<2> cr = crec[c];
+            rb[k] = rep[c];
+            ebv[k] = cr.e;
+            bbv[k] = cr.b;
+          }
         }
       }
       settle(rb[0], bbv[0], ebv[0]);
@@ -2695,33 +2754,24 @@ __global__ __launch_bounds__(kBlock) void k_union_listed(const float4* __restric
         settle(rb, bb, eb);
       }
     }
+    ca = can;
+    pm = pmn;
+    qn = qnn;
   }
 }
 
-// K6: core-core union.  Edge (s, j) with j in cell c:
-//   * c mutual: all of c's core points are pairwise adjacent, hence one component; one edge
-//     from s into c (to rep[c] when the whole cell is adjacent, else to the first adjacent core
-//     point) spans every edge from s into c.
-//   * c not mutual: every adjacent core j > s (the edge from the smaller end covers the pair;
-//     when cell(s) is mutual the larger end's first-hit edge covers it too).
+// one core point's unions (k_union, k_union_nm)
 template <int D>
-__global__ __launch_bounds__(kBlock) void k_union(const float4* __restrict__ pts,
-                                                 const int32_t* __restrict__ skey, int64_t n,
-                                                 Geom g, const int32_t* __restrict__ cell_start,
-                                                 const CellRec<D>* __restrict__ crec,
-                                                 const float2* __restrict__ slab_t,
-                                                 const uint8_t* __restrict__ core,
-                                                 const int32_t* __restrict__ rep,
-                                                 const uint8_t* __restrict__ mutual,
-                                                 const int32_t* __restrict__ sorig,
-                                                 int32_t* __restrict__ parent) {
-  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n || !core[s]) return;
-  const int32_t key = skey[s];
-  if ((int64_t)key >= g.cells) return;
-  if (mutual[key]) return;  // handled by the star init + k_union_cells
-  const float4 p = pts[s];
-  const int si = (int)s;
+__device__ __forceinline__ void union_point(int si, int32_t key, const float4* __restrict__ pts,
+                                            Geom g, const int32_t* __restrict__ cell_start,
+                                            const CellRec<D>* __restrict__ crec,
+                                            const float2* __restrict__ slab_t,
+                                            const uint8_t* __restrict__ core,
+                                            const int32_t* __restrict__ rep,
+                                            const uint8_t* __restrict__ mutual,
+                                            const int32_t* __restrict__ sorig,
+                                            int32_t* __restrict__ parent) {
+  const float4 p = pts[si];
   for_each_cell<D>(p, key, g, cell_start, crec, slab_t,
                    [&](int64_t c, int b, int e, int cls) -> bool {
                      const int r = rep[c];
@@ -2746,6 +2796,60 @@ __global__ __launch_bounds__(kBlock) void k_union(const float4* __restrict__ pts
                      }
                      return false;
                    });
+}
+
+// K6: core-core union.  Edge (s, j) with j in cell c:
+//   * c mutual: all of c's core points are pairwise adjacent, hence one component; one edge
+//     from s into c (to rep[c] when the whole cell is adjacent, else to the first adjacent core
+//     point) spans every edge from s into c.
+//   * c not mutual: every adjacent core j > s (the edge from the smaller end covers the pair;
+//     when cell(s) is mutual the larger end's first-hit edge covers it too).
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_union(const float4* __restrict__ pts,
+                                                 const int32_t* __restrict__ skey, int64_t n,
+                                                 Geom g, const int32_t* __restrict__ cell_start,
+                                                 const CellRec<D>* __restrict__ crec,
+                                                 const float2* __restrict__ slab_t,
+                                                 const uint8_t* __restrict__ core,
+                                                 const int32_t* __restrict__ rep,
+                                                 const uint8_t* __restrict__ mutual,
+                                                 const int32_t* __restrict__ sorig,
+                                                 int32_t* __restrict__ parent) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n || !core[s]) return;
+  const int32_t key = skey[s];
+  if ((int64_t)key >= g.cells) return;
+  if (mutual[key]) return;  // handled by the star init + k_union_cells
+  union_point<D>((int)s, key, pts, g, cell_start, crec, slab_t, core, rep, mutual, sorig, parent);
+}
+
+// K6c (2-D pair path): k_union's unions for the core points of the NON-mutual cells with core
+// points, listed by the box-certain pass -- one wave per listed cell, lanes over its points.
+// With one-frame slabs every 2-D cell is mutual (box diagonal below eps, time span 0), so the
+// bench stacks list none, where k_union read every point's flag for nothing (123 us at 1000
+// frames).
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_union_nm(const float4* __restrict__ pts, Geom g,
+                                                    const int32_t* __restrict__ cell_start,
+                                                    const CellRec<D>* __restrict__ crec,
+                                                    const float2* __restrict__ slab_t,
+                                                    const uint8_t* __restrict__ core,
+                                                    const int32_t* __restrict__ rep,
+                                                    const uint8_t* __restrict__ mutual,
+                                                    const int32_t* __restrict__ sorig,
+                                                    int32_t* __restrict__ parent,
+                                                    const int32_t* __restrict__ nm_list,
+                                                    const int32_t* __restrict__ nm_count) {
+  const int lane = threadIdx.x & 63;
+  const XcdRange xr = xcd_items(*nm_count, false);
+  for (int64_t i = xr.first; i < xr.end; i += xr.step) {
+    const int32_t key = nm_list[i];
+    const int b = crec[key].b, e = crec[key].e;
+    for (int s = b + lane; s < e; s += 64)
+      if (core[s])
+        union_point<D>(s, key, pts, g, cell_start, crec, slab_t, core, rep, mutual, sorig,
+                       parent);
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void k_fill_i32(int32_t* p, int64_t n, int32_t v) {
@@ -3670,6 +3774,7 @@ struct DbscanState {
                            // the grid build's radix key buffers, dead after the build)
   int union_list = -1;     // RPT_UNION_LIST=0: the second union pass enumerates every window
   int union_pair = -1;     // RPT_UNION_PAIR=0: one cell per wave in the box-certain union pass
+  int union_nm = -1;       // RPT_UNION_NM=0: k_union over every point (not the listed cells')
   // occupied cells per wave iteration of k_union_cells_pair: 64 on large stacks (one header load
   // per lane), 16 on small ones (RPT_UNION_CPW in the A/B build)
   int union_cpw() const {
@@ -4265,9 +4370,19 @@ int32_t DbscanState::union_pass(hipStream_t st) {
   const bool listing = union_list && dim == 2;
   int32_t* plist = listing ? nc_list : nullptr;
   int32_t* pcount = listing ? nc_list + n : nullptr;
+  // 2-D pair path: the non-mutual cells with core points listed by the first pass in cid (free
+  // until the label pass), their count at cid[n]; k_union_nm then takes only their points
+  // (RPT_UNION_NM=0 in the A/B build: k_union over every point)
+  if (union_nm < 0) {
+    const char* e = ab_env("RPT_UNION_NM");
+    union_nm = (e && std::atoi(e) == 0) ? 0 : 1;
+  }
+  const bool nm = dim == 2 && union_pair && union_nm;
+  int32_t* nm_list = nm ? cid : nullptr;
+  int32_t* nm_count = nm ? cid + n : nullptr;
   // the per-cell minima: from the core pass (cmin_ready) or from the final core flags here
   hipLaunchKernelGGL(k_init_occ_cells, dim3(gb), dim3(kBlock), 0, st, occ, n_occ, C, rep,
-                     cmin_ready ? nullptr : cmin, pcount);
+                     cmin_ready ? nullptr : cmin, pcount, nm_count);
   if (!cmin_ready)
     hipLaunchKernelGGL(k_cell_min_pair, dim3(gb), dim3(kBlock), 0, st, skey, core, sorig, n, C,
                        cmin);
@@ -4279,7 +4394,7 @@ int32_t DbscanState::union_pass(hipStream_t st) {
     if (union_pair)  // two cells per wave (RPT_UNION_PAIR=0 in the A/B build: one)
       hipLaunchKernelGGL(k_union_cells_pair, dim3(gw), dim3(kBlock), 0, st, pts, g, occ, n_occ,
                          rec<2>(), occ_bits, slab_t, rep, mutual, sorig, parent, uf_flags, pm,
-                         plist, pcount, union_cpw());
+                         plist, pcount, union_cpw(), nm_list, nm_count);
     else
       hipLaunchKernelGGL((k_union_cells<2, false>), dim3(gw), dim3(kBlock), 0, st, pts, g,
                          cell_start, occ, n_occ, rec<2>(), occ_bits, slab_t, core, rep, mutual,
@@ -4292,16 +4407,28 @@ int32_t DbscanState::union_pass(hipStream_t st) {
       (void)hipMemsetAsync(lstat_dev, 0, 16, st);
     }
 #endif
-    if (listing)
+    if (listing) {
+      // the snapshot in cell_root (free until the label stage's k_cell_roots); not on dense
+      // slabs, where it measured slower (configs[4] share: +38 us snapshot, listed 867 -> 916 us;
+      // 1000 standard frames: listed 348 -> 202 us for +28)
+      const bool snap = !spos_on;
+      if (snap)
+        hipLaunchKernelGGL(k_cell_root_snapshot, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock),
+                           0, st, occ, n_occ, rep, parent, g.cells, uf_flags, cell_root);
       hipLaunchKernelGGL(k_union_listed, dim3(gw), dim3(kBlock), 0, st, pts, g, occ, rec<2>(),
                          occ_bits, slab_t, core, rep, mutual, sorig, parent, uf_flags, pm, plist,
-                         pcount, lstat_dev);
+                         pcount, snap ? (const int32_t*)cell_root : nullptr, lstat_dev);
+    }
     else
       hipLaunchKernelGGL((k_union_cells<2, true>), dim3(gw), dim3(kBlock), 0, st, pts, g,
                          cell_start, occ, n_occ, rec<2>(), occ_bits, slab_t, core, rep, mutual,
                          sorig, parent, uf_flags, pm, plist, pcount);
-    hipLaunchKernelGGL(k_union<2>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
-                       rec<2>(), slab_t, core, rep, mutual, sorig, parent);
+    if (nm)
+      hipLaunchKernelGGL(k_union_nm<2>, dim3(gw), dim3(kBlock), 0, st, pts, g, cell_start,
+                         rec<2>(), slab_t, core, rep, mutual, sorig, parent, nm_list, nm_count);
+    else
+      hipLaunchKernelGGL(k_union<2>, dim3(gp), dim3(kBlock), 0, st, pts, skey, n, g, cell_start,
+                         rec<2>(), slab_t, core, rep, mutual, sorig, parent);
   } else {
     hipLaunchKernelGGL((k_union_cells<3, false>), dim3(gw), dim3(kBlock), 0, st, pts, g,
                        cell_start, occ, n_occ, rec<3>(), occ_bits, slab_t, core, rep, mutual, sorig,
