@@ -438,6 +438,15 @@ static int slab_chunks_override() {
   return v;
 }
 
+// RPT_CELL_BOX_MIXED=0: 16 lanes for every cell's box (k_cell_box; A/B)
+static bool cell_box_mixed() {
+  static const bool v = [] {
+    const char* e = ab_env("RPT_CELL_BOX_MIXED");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return v;
+}
+
 // RPT_LABEL_ORIG=0: core labels scattered from sorted order (k_label_core; A/B)
 static bool label_core_orig() {
   static const bool v = [] {
@@ -1053,6 +1062,159 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(const float4* __restrict__ 
       const float dt = t1 - t0;
       mutual[c] = (d2 <= g.eps2 && dt <= g.epst) ? 1 : 0;
       if (cmin) cmin[c] = sorig ? mn : ~0ull;  // the core pass's per-cell minima
+    }
+  }
+}
+
+// The same records with the small cells one LANE each: a wave takes 64 consecutive occupied
+// cells, every lane the box of its own cell when it holds at most kCbSmall points (its points
+// loaded together, branch-free), then the wave's other cells four at a time at kCbLanes lanes
+// each.  Clutter singletons (most of the occupied cells at the standard density) no longer take
+// a 16-lane group each.
+constexpr int kCbSmall = 4;
+template <int D>
+__device__ __forceinline__ void cell_box_store(int c, int b, int e, float x0, float x1, float y0,
+                                               float y1, float z0, float z1, float t0, float t1,
+                                               uint64_t mn, bool has_mn, const Geom& g,
+                                               uint8_t* __restrict__ mutual,
+                                               CellRec<D>* __restrict__ crec,
+                                               unsigned long long* __restrict__ cmin) {
+  CellRec<D> r{};
+  r.b = b;
+  r.e = e;
+  r.x0 = x0;
+  r.x1 = x1;
+  r.y0 = y0;
+  r.y1 = y1;
+  if constexpr (D == 3) {
+    r.z0 = z0;
+    r.z1 = z1;
+  }
+  r.t0 = t0;
+  r.t1 = t1;
+  crec[c] = r;
+  const double dx = (double)x1 - (double)x0;
+  const double dy = (double)y1 - (double)y0;
+  double d2 = dx * dx + dy * dy;
+  if (D == 3) {
+    const double dz = (double)z1 - (double)z0;
+    d2 = d2 + dz * dz;
+  }
+  const float dt = t1 - t0;
+  mutual[c] = (d2 <= g.eps2 && dt <= g.epst) ? 1 : 0;
+  if (cmin) cmin[c] = has_mn ? mn : ~0ull;  // the core pass's per-cell minima
+}
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_cell_box_mixed(const float4* __restrict__ pts,
+                                                          const int32_t* __restrict__ cell_start,
+                                                          const int32_t* __restrict__ occ,
+                                                          const int32_t* __restrict__ n_occ,
+                                                          Geom g, uint8_t* __restrict__ mutual,
+                                                          CellRec<D>* __restrict__ crec,
+                                                          unsigned long long* __restrict__ cmin =
+                                                              nullptr,
+                                                          const int32_t* __restrict__ sorig =
+                                                              nullptr) {
+  constexpr int L = kCbLanes;
+  const int lane = threadIdx.x & 63;
+  const int grp = lane / L, j = lane & (L - 1);
+  const int64_t no = *n_occ;
+  if (no == 0) return;
+  const int64_t wpb = kBlock / 64;
+  for (int64_t q0 = ((int64_t)blockIdx.x * wpb + threadIdx.x / 64) * 64; q0 < no;
+       q0 += (int64_t)gridDim.x * wpb * 64) {
+    const int64_t q = q0 + lane;
+    const bool act = q < no;
+    const int c = occ[act ? q : no - 1];
+    const int b = cell_start[c], e = cell_start[c + 1];
+    const bool small = act && e - b <= kCbSmall;
+    {  // this lane's cell when small (every lane loads: branch-free)
+      float4 pp[kCbSmall];
+      uint32_t so[kCbSmall];
+#pragma unroll
+      for (int u = 0; u < kCbSmall; ++u) {
+        const int sc = (b + u < e) ? b + u : b;  // duplicates of a cell point leave the box as is
+        pp[u] = pts[sc];
+        if (sorig) so[u] = (uint32_t)sorig[sc];
+      }
+      float x0 = FLT_MAX, x1 = -FLT_MAX, y0 = FLT_MAX, y1 = -FLT_MAX;
+      float z0 = FLT_MAX, z1 = -FLT_MAX, t0 = FLT_MAX, t1 = -FLT_MAX;
+      uint64_t mn = ~0ull;
+#pragma unroll
+      for (int u = 0; u < kCbSmall; ++u) {
+        const float4 p = pp[u];
+        x0 = fminf(x0, p.x); x1 = fmaxf(x1, p.x);
+        y0 = fminf(y0, p.y); y1 = fmaxf(y1, p.y);
+        z0 = fminf(z0, p.z); z1 = fmaxf(z1, p.z);
+        t0 = fminf(t0, p.w); t1 = fmaxf(t1, p.w);
+        if (sorig) {
+          const uint64_t v = ((uint64_t)so[u] << 32) | (uint32_t)((b + u < e) ? b + u : b);
+          mn = v < mn ? v : mn;
+        }
+      }
+      if (D != 3) {
+        z0 = t0;  // 2-D: pts[].z carries t
+        z1 = t1;
+      }
+      if (small)
+        cell_box_store<D>(c, b, e, x0, x1, y0, y1, z0, z1, t0, t1, mn, sorig != nullptr, g,
+                          mutual, crec, cmin);
+    }
+    // the wave's other cells, four at a time (group grp takes the grp-th of them)
+    uint64_t big = __ballot(act && !small);
+    while (big) {  // (wave-uniform)
+      int pick = -1;
+#pragma unroll
+      for (int k = 0; k < 64 / L; ++k) {
+        const int lk = big ? __ffsll((unsigned long long)big) - 1 : -1;
+        if (grp == k) pick = lk;
+        if (big) big &= big - 1;
+      }
+      // (every lane takes part in the shuffles: a conditional one would read inactive lanes)
+      const int src = pick < 0 ? 0 : pick;
+      const int cc = __shfl(c, src), bb = __shfl(b, src), es = __shfl(e, src);
+      const int ee = pick < 0 ? bb : es;
+      float x0 = FLT_MAX, x1 = -FLT_MAX, y0 = FLT_MAX, y1 = -FLT_MAX;
+      float z0 = FLT_MAX, z1 = -FLT_MAX, t0 = FLT_MAX, t1 = -FLT_MAX;
+      uint64_t mn = ~0ull;
+      constexpr int kU = 8;  // loads in flight per lane (as k_cell_box)
+      for (int s0 = bb + j; s0 < ee; s0 += L * kU) {
+        float4 pp[kU];
+        uint32_t so[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int s2 = s0 + L * u;
+          const int sc = (s2 < ee) ? s2 : s0;
+          pp[u] = pts[sc];
+          if (sorig) so[u] = (uint32_t)sorig[sc];
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const float4 p = pp[u];
+          x0 = fminf(x0, p.x); x1 = fmaxf(x1, p.x);
+          y0 = fminf(y0, p.y); y1 = fmaxf(y1, p.y);
+          z0 = fminf(z0, p.z); z1 = fmaxf(z1, p.z);
+          t0 = fminf(t0, p.w); t1 = fmaxf(t1, p.w);
+          if (sorig) {
+            const int s2 = s0 + L * u;
+            const uint64_t v = ((uint64_t)so[u] << 32) | (uint32_t)((s2 < ee) ? s2 : s0);
+            mn = v < mn ? v : mn;
+          }
+        }
+      }
+      if (sorig) mn = row_reduce<L>(mn, OpMin{});
+      x0 = row_reduce<L>(x0, OpMin{}); x1 = row_reduce<L>(x1, OpMax{});
+      y0 = row_reduce<L>(y0, OpMin{}); y1 = row_reduce<L>(y1, OpMax{});
+      z0 = row_reduce<L>(z0, OpMin{}); z1 = row_reduce<L>(z1, OpMax{});
+      t0 = row_reduce<L>(t0, OpMin{}); t1 = row_reduce<L>(t1, OpMax{});
+      if (D != 3) {
+        z0 = t0;
+        z1 = t1;
+      }
+      if (pick >= 0 && j == 0)
+        cell_box_store<D>(cc, bb, ee, x0, x1, y0, y1, z0, z1, t0, t1, mn, sorig != nullptr, g,
+                          mutual, crec, cmin);
     }
   }
 }
@@ -4186,11 +4348,20 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
     RPT_CHECK_LAUNCH();
     n_occ_dev = hpos + n;
   }
-  hipLaunchKernelGGL(k_cell_box<D>, dim3(grid_for(kCbLanes * n, kBlock, 8192)), dim3(kBlock), 0,
-                     st, pts, cell_start, occ, n_occ_dev, g, mutual, cr,
-                     bucket_allmin ? nullptr
-                                   : reinterpret_cast<unsigned long long*>(cell_min_pair),
-                     (k5_fused_path() && !bucket_allmin) ? (const int32_t*)sorig : nullptr);
+  {
+    auto* cmin_w = bucket_allmin ? nullptr : reinterpret_cast<unsigned long long*>(cell_min_pair);
+    const int32_t* so_w = (k5_fused_path() && !bucket_allmin) ? (const int32_t*)sorig : nullptr;
+    // small cells one lane each on large standard-density stacks (1000 frames: 346 -> 273 us);
+    // the 125-frame share has too few 64-cell waves to fill the GPU (48 -> 60 us) and dense
+    // slabs' cells are large (324 -> 402 us): 16 lanes for every cell there
+    // (RPT_CELL_BOX_MIXED=0 in the A/B build: always)
+    if (cell_box_mixed() && !spos_on && n > (int64_t(1) << 24))
+      hipLaunchKernelGGL(k_cell_box_mixed<D>, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, st,
+                         pts, cell_start, occ, n_occ_dev, g, mutual, cr, cmin_w, so_w);
+    else
+      hipLaunchKernelGGL(k_cell_box<D>, dim3(grid_for(kCbLanes * n, kBlock, 8192)), dim3(kBlock),
+                         0, st, pts, cell_start, occ, n_occ_dev, g, mutual, cr, cmin_w, so_w);
+  }
   RPT_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_slab_range<D>, dim3((unsigned)nt), dim3(kBlock), 0, st, cr, occ, hpos,
                      cell_start, (int64_t)(C / nt), (int)nt, slab_t, bucket ? occ_base : nullptr);
