@@ -438,21 +438,28 @@ static int slab_chunks_override() {
   return v;
 }
 
-// RPT_CELL_BOX_MIXED=0: 16 lanes for every cell's box (k_cell_box; A/B)
-static bool cell_box_mixed() {
-  static const bool v = [] {
-    const char* e = ab_env("RPT_CELL_BOX_MIXED");
-    return !(e && std::atoi(e) == 0);
-  }();
+// A/B switch with three values: 0 off, 1 the default rule, 2 forced on (the parity tests of the
+// A/B build run a path on inputs its default rule would not take it for)
+static int ab_mode(const char* name) {
+  const char* e = ab_env(name);
+  const int v = e ? std::atoi(e) : 1;
+  return (v == 0 || v == 2) ? v : 1;
+}
+// RPT_CELL_BOX_MIXED=0: 16 lanes for every cell's box (k_cell_box); 2: k_cell_box_mixed always
+static int cell_box_mixed() {
+  static const int v = ab_mode("RPT_CELL_BOX_MIXED");
+  return v;
+}
+// RPT_UNION_SNAP=0: no root snapshot before the listed union pass; 2: also on dense slabs
+static int union_snapshot() {
+  static const int v = ab_mode("RPT_UNION_SNAP");
   return v;
 }
 
-// RPT_LABEL_ORIG=0: core labels scattered from sorted order (k_label_core; A/B)
-static bool label_core_orig() {
-  static const bool v = [] {
-    const char* e = ab_env("RPT_LABEL_ORIG");
-    return !(e && std::atoi(e) == 0);
-  }();
+// RPT_LABEL_ORIG=0: core labels scattered from sorted order (k_label_core); 2: the inverse
+// permutation and original-order labels at every density
+static int label_core_orig() {
+  static const int v = ab_mode("RPT_LABEL_ORIG");
   return v;
 }
 
@@ -3268,7 +3275,10 @@ __global__ __launch_bounds__(kBlock, 6) void k_label(const float4* __restrict__ 
                                                  MinRank cid,
                                                  const int32_t* __restrict__ nc_list,
                                                  const int32_t* __restrict__ nc_count,
-                                                 int32_t* __restrict__ labels) {
+                                                 int32_t* __restrict__ labels,
+                                                 int32_t* __restrict__ kstat = nullptr) {
+  // kstat (A/B build, RPT_STATS): queued points, points with a core cell in their window, points
+  // that searched a partly reachable cell, points labelled
   static_assert(W == 32 || W == 64, "a point per wave or per half-wave");
   constexpr int P = 64 / W;  // points per wave
   const int lane = threadIdx.x & 63;
@@ -3295,6 +3305,9 @@ __global__ __launch_bounds__(kBlock, 6) void k_label(const float4* __restrict__ 
     const int s = nc_list[q];
     const int32_t key = skey[s];
     int best = INT_MAX;
+#ifdef RPT_AB
+    bool st_core = false, st_search = false;
+#endif
     if ((int64_t)key < g.cells) {
       const float4 p = pts[s];
       int cx, cy, cz;
@@ -3327,6 +3340,14 @@ __global__ __launch_bounds__(kBlock, 6) void k_label(const float4* __restrict__ 
           }
         }
         best = min(best, gmin(v));
+#ifdef RPT_AB
+        {
+          bool anyc = false;
+#pragma unroll
+          for (int k = 0; k < kR; ++k) anyc = anyc || ck[k] != INT_MAX;
+          st_core = st_core || gbal(anyc) != 0;
+        }
+#endif
         // the partially reachable cells, smallest key first, while a key can still win
         uint32_t pend = 0;
 #pragma unroll
@@ -3341,6 +3362,9 @@ __global__ __launch_bounds__(kBlock, 6) void k_label(const float4* __restrict__ 
             }
           const int mm = gmin(mine);
           if (mm == INT_MAX) break;
+#ifdef RPT_AB
+          st_search = true;
+#endif
           const uint64_t at = gbal(mine == mm);
           const int l = h0 + __ffsll((unsigned long long)at) - 1;
           const int kl = __shfl(mk, l);
@@ -3386,6 +3410,14 @@ __global__ __launch_bounds__(kBlock, 6) void k_label(const float4* __restrict__ 
       int32_t out = -1;
       if (best != INT_MAX) out = GLOBAL ? best : cid[best];
       labels[sorig[s]] = out;
+#ifdef RPT_AB
+      if (kstat) {
+        atomicAdd(&kstat[0], 1);
+        if (st_core) atomicAdd(&kstat[1], 1);
+        if (st_search) atomicAdd(&kstat[2], 1);
+        if (best != INT_MAX) atomicAdd(&kstat[3], 1);
+      }
+#endif
     }
   }
 }
@@ -4028,6 +4060,7 @@ struct DbscanState {
   // core labels
   int32_t* slab = nullptr;
   bool spos_on = false;
+  bool dense_slabs = false;  // more than 8 kChunkPts points per slab on average (bucket path)
   int32_t* cell_min = nullptr;  // per cell: smallest component key (label pass)
   uint8_t* fok = nullptr;    // per cell: frame condition met by every core point (denoise)
   bool integral_t = false;   // every finite t integral (slab = one frame id)
@@ -4259,7 +4292,8 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
     // dense slabs: the label passes' scattered core-label writes cost more than the inverse
     // permutation written here (configs[4] share: 676 -> 253 us for +57 in the scatter; at
     // standard density the scattered writes stay in L2 and the extra store costs +68 us)
-    spos_on = avg > 8 * kChunkPts;
+    dense_slabs = avg > 8 * kChunkPts;
+    spos_on = label_core_orig() == 2 || (label_core_orig() == 1 && dense_slabs);
     int32_t* spos_w = spos_on ? slab : nullptr;
     int64_t ch = avg > 8 * kChunkPts ? (avg + kChunkPts - 1) / kChunkPts : 1;
     ch = std::max<int64_t>(ch, (512 + nt - 1) / std::max<int64_t>(nt, 1));
@@ -4335,9 +4369,10 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
     while ((int64_t(1) << bits) <= C1) ++bits;
     uint32_t *sk, *sv;
     RPT_TRY(radix_sort_pairs(keys, vals, keys_alt, vals_alt, n, bits, rtmp, &sk, &sv, st));
-    spos_on = false;
+    dense_slabs = false;
+    spos_on = label_core_orig() == 2;
     hipLaunchKernelGGL(k_gather<D>, dim3(gb), dim3(kBlock), 0, st, x, y, z, stride, t, n, sk, sv,
-                       pts, sorig, skey, nullptr);
+                       pts, sorig, skey, spos_on ? slab : nullptr);
     RPT_HIP(hipMemsetAsync(cell_start, 0, sizeof(int32_t) * C1, st));
     hipLaunchKernelGGL(k_cell_runs, dim3(gb), dim3(kBlock), 0, st, skey, n, cell_start, hpos);
     RPT_CHECK_LAUNCH();
@@ -4355,7 +4390,8 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
     // the 125-frame share has too few 64-cell waves to fill the GPU (48 -> 60 us) and dense
     // slabs' cells are large (324 -> 402 us): 16 lanes for every cell there
     // (RPT_CELL_BOX_MIXED=0 in the A/B build: always)
-    if (cell_box_mixed() && !spos_on && n > (int64_t(1) << 24))
+    if (cell_box_mixed() == 2 ||
+        (cell_box_mixed() == 1 && !dense_slabs && n > (int64_t(1) << 24)))
       hipLaunchKernelGGL(k_cell_box_mixed<D>, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, st,
                          pts, cell_start, occ, n_occ_dev, g, mutual, cr, cmin_w, so_w);
     else
@@ -4582,7 +4618,7 @@ int32_t DbscanState::union_pass(hipStream_t st) {
       // the snapshot in cell_root (free until the label stage's k_cell_roots); not on dense
       // slabs, where it measured slower (configs[4] share: +38 us snapshot, listed 867 -> 916 us;
       // 1000 standard frames: listed 348 -> 202 us for +28)
-      const bool snap = !spos_on;
+      const bool snap = union_snapshot() == 2 || (union_snapshot() == 1 && !dense_slabs);
       if (snap)
         hipLaunchKernelGGL(k_cell_root_snapshot, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock),
                            0, st, occ, n_occ, rep, parent, g.cells, uf_flags, cell_root);
@@ -4679,12 +4715,21 @@ int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hi
   // also the per-cell smallest keys (k_cell_min_key fused) and nc_count cleared
   RPT_TRY(cluster_ids(st, cell_min, nc_count));
   const MinRank mr{min_bits, min_pref};
-  if (spos_on && label_core_orig())
+  if (spos_on)
     hipLaunchKernelGGL(k_label_core_orig, dim3((grid_for(n, kBlock * kPU, 2048) + 7) & ~7),
                        dim3(kBlock), 0, st, ccmin, n, slab, mr, labels);
   else
     hipLaunchKernelGGL(k_label_core, dim3((grid_for(n, kBlock * kPU, 2048) + 7) & ~7),
                        dim3(kBlock), 0, st, ccmin, n, sorig, mr, labels);
+  int32_t* kstat = nullptr;  // (A/B diagnostics)
+#ifdef RPT_AB
+  if (ab_env("RPT_STATS")) {  // (a leaked 16 B per process)
+    static int32_t* buf = nullptr;
+    if (!buf) (void)hipMalloc(&buf, 16);
+    kstat = buf;
+    (void)hipMemsetAsync(kstat, 0, 16, st);
+  }
+#endif
 #ifdef RPT_AB
   if (use_label_tiles())
     hipLaunchKernelGGL((k_label_tiles<false>), dim3(tile_grid_blocks()), dim3(kTileBlock), 0, st,
@@ -4701,13 +4746,23 @@ int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hi
     hipLaunchKernelGGL((k_label<2, false, 32>),
                        dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
                        rec<2>(), occ_bits, slab_t, ccmin, cell_min, mutual, sorig, mr, nc_list,
-                       nc_count, labels);
+                       nc_count, labels, kstat);
   else
     hipLaunchKernelGGL((k_label<3, false, 64>),
                        dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey, g,
                        rec<3>(), occ_bits, slab_t, ccmin, cell_min, mutual, sorig, mr, nc_list,
                        nc_count, labels);
   RPT_CHECK_LAUNCH();
+#ifdef RPT_AB
+  if (kstat) {
+    int32_t ks[4] = {0, 0, 0, 0};
+    (void)hipMemcpyAsync(ks, kstat, 16, hipMemcpyDeviceToHost, st);
+    (void)hipStreamSynchronize(st);
+    std::fprintf(stderr,
+                 "[rpt stats] n=%lld label: queued=%d core_in_window=%d searched=%d labelled=%d\n",
+                 (long long)n, ks[0], ks[1], ks[2], ks[3]);
+  }
+#endif
   tm.mark();
   if (stats && defer) return RPT_OK;  // fill_stats after the caller's sync
   if (stats) {
@@ -4763,7 +4818,7 @@ int32_t DbscanState::labels_global(const int64_t* rep_orig, const int64_t* reps,
   // the core labels in original order (before slab's inverse permutation is overwritten), then
   // per sorted point the final core labels with the per-cell smallest label folded in
   // (k_cell_min_key's pass)
-  const bool orig = spos_on && label_core_orig();
+  const bool orig = spos_on;
   if (orig)
     hipLaunchKernelGGL(k_label_global_orig, dim3(grid_for(n, kBlock * kPU, 2048)), dim3(kBlock), 0,
                        st, core, ccmin, cid, slab, n, labels);

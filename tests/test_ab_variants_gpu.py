@@ -23,6 +23,11 @@ COMBOS = [
     {"RPT_K1_EXPAND": "0", "RPT_SLAB_CHUNKS": "3", "RPT_K5_MODE": "2", "RPT_F32_SCREEN": "0",
      "RPT_UF_FLAGS": "0"},
     {"RPT_K5_TILES": "1", "RPT_K7_TILES": "1", "RPT_CELL_SIDE": "0.5"},
+    # round-5 paths forced on a stack their default rules would not take them for (and off):
+    # small cells one lane each, the inverse permutation with original-order core labels, no
+    # root snapshot before the listed union pass, k_union over every point
+    {"RPT_CELL_BOX_MIXED": "2", "RPT_LABEL_ORIG": "2", "RPT_UNION_SNAP": "0",
+     "RPT_UNION_NM": "0"},
 ]
 
 RUN = r'''

@@ -59,7 +59,7 @@ for step in "$@"; do
           --h2d-steps 0 --no-timing || exit 1
         grep "rpt stats" "$O/stats_${w// /_}.log" | sort | uniq -c | head -8
       done
-      for c in ${CPWS:-4 8 16 32}; do
+      for c in ${CPWS-4 8 16 32}; do  # (CPWS= : none)
         RPT_LIB=$PWD/$AB RPT_UNION_CPW=$c bash tools/kprof.sh cpw$c --lanes 1 --total-frames 125 \
           || exit 1
         python tools/kstats.py "$(ls gpurun_out/kprof_cpw$c/*kernel_stats.csv | head -1)" 4 \
