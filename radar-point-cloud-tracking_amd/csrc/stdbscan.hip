@@ -4340,10 +4340,19 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
                          skey, spos_w);
     } else {
       // the fused K5's all-core cell minima from the counting sort when both LDS arrays fit 64 KiB
-      bucket_allmin = k5_fused_path() && 2 * hist_bytes <= 65536;
+      bucket_allmin = k5_fused_path() && 2 * hist_bytes <= 65536 &&
+                      ab_mode("RPT_BUCKET_ALLMIN") != 0;  // (=0: from k_cell_box; A/B)
       const size_t lds = bucket_allmin ? 2 * hist_bytes : hist_bytes;
       RPT_HIP(hipFuncSetAttribute((const void*)k_slab_bucket,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+#ifdef RPT_AB
+      if (ab_env("RPT_STATS")) {  // A/B diagnostics: blocks per CU the runtime admits
+        int nb = -1;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_slab_bucket, kBucketBlock, lds);
+        std::fprintf(stderr, "[rpt stats] slab_bucket lds=%zu nx=%d ny=%d blocks_per_cu=%d\n", lds,
+                     (int)nx, (int)ny, nb);
+      }
+#endif
       hipLaunchKernelGGL(k_slab_bucket, dim3((unsigned)nt), dim3(kBucketBlock), lds, st, x, y,
                          stride, t, g, slab_lo, pts, sorig, skey, spos_w, cell_start, hpos,
                          slab_occ,

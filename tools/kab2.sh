@@ -3,7 +3,8 @@
 # abl/librpt_base.so, per workload (WL: std std1000 dense); the first run on a fresh box is
 # slower across the board, so a plain new-then-base order biases every kernel.  Output:
 # gpurun_out/kab2[_TAG]/<W>_{new,base}.txt (NEWLIB / BASE: other libraries than the in-tree
-# build / abl/librpt_base.so) (per-kernel means over both runs of a variant) + a diff.
+# build / abl/librpt_base.so; NEWENV: VAR=value switches for the NEWLIB runs only, e.g. the A/B
+# build against itself) (per-kernel means over both runs of a variant) + a diff.
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -18,7 +19,7 @@ for W in ${WL:-std1000 dense}; do
     if [[ $v == base* ]]; then
       RPT_LIB="$BASE" bash tools/kprof.sh $K "${A[@]}" || exit 1
     elif [ -n "$NEWLIB" ]; then
-      RPT_LIB="$NEWLIB" bash tools/kprof.sh $K "${A[@]}" || exit 1
+      env $NEWENV RPT_LIB="$NEWLIB" bash tools/kprof.sh $K "${A[@]}" || exit 1
     else
       bash tools/kprof.sh $K "${A[@]}" || exit 1
     fi
