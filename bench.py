@@ -64,6 +64,12 @@ for p in (str(ROOT / "radar-point-cloud-tracking_amd"), str(ROOT)):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# Eight hardware queues per process before HIP initialises (HIP's default is four): the five
+# stacks in flight (three lanes per rank sharded) each get a queue of their own instead of two
+# lanes sharing one -- same box, interleaved: 6.91 / 6.87 against 6.51 / 6.80 Gpoints/s, steady
+# state 6.27 / 6.50 against 6.94 / 6.77 ms (profiles/r5/bench_hwq/).  An explicit setting wins.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 

@@ -35,12 +35,14 @@
 // lies within +-2 cells, and small enough that a full cell's diagonal (0.99 eps in 2-D,
 // eps*sqrt(3)/2 in 3-D) stays within eps, so dense cells can be "mutual" (decided from their
 // actual boxes, k_cell_box).
+#include <algorithm>
 #include <cfloat>
 #include <climits>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <vector>
 
 #include "common.h"
 
@@ -3450,13 +3452,23 @@ __global__ void k_core_from_orig(const uint8_t* __restrict__ in, const int32_t* 
        s += (int64_t)gridDim.x * blockDim.x)
     core[s] = in[sorig[s]] ? 1 : 0;
 }
-// comp[orig] = minimum original index of the point's core component, -1 for non-core
+// comp[orig] = minimum original index of the point's core component, -1 for non-core; a core
+// point of a mutual cell takes its cell's root (k_cell_roots: one load instead of a parent-chain
+// walk per point)
 __global__ void k_comp_out(int32_t* parent, const uint8_t* __restrict__ core,
                            const int32_t* __restrict__ sorig, int64_t n,
-                           int32_t* __restrict__ comp) {
+                           int32_t* __restrict__ comp, const int32_t* __restrict__ skey,
+                           const int32_t* __restrict__ cell_root, int64_t cells) {
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
-       s += (int64_t)gridDim.x * blockDim.x)
-    comp[sorig[s]] = core[s] ? sorig[uf_find(parent, (int)s)] : -1;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    int32_t out = -1;
+    if (core[s]) {
+      const int32_t key = skey[s];
+      const int32_t cr = ((int64_t)key < cells) ? cell_root[key] : -1;  // -1: not mutual
+      out = sorig[cr >= 0 ? cr : uf_find(parent, (int)s)];
+    }
+    comp[sorig[s]] = out;
+  }
 }
 // Global labelling, core points: ccmin[s] = component-min original index; each component's
 // label = rank of its global representative (rep[min], from the equivalence merge) among the
@@ -4519,11 +4531,21 @@ int32_t DbscanState::core_pass(hipStream_t st) {
     RPT_CHECK_LAUNCH();
     cmin_ready = true;
 #ifdef RPT_AB
-    if (ab_env("RPT_STATS")) {  // A/B diagnostics: K5's slow queue (syncs)
+    if (ab_env("RPT_STATS")) {  // A/B diagnostics: K5's slow queue and its cells (syncs)
       int32_t h = 0;
       (void)hipMemcpyAsync(&h, n_slow, 4, hipMemcpyDeviceToHost, st);
       (void)hipStreamSynchronize(st);
-      std::fprintf(stderr, "[rpt stats] n=%lld k5_slow_queue=%d\n", (long long)n, h);
+      std::vector<int32_t> keys((size_t)std::max(h, 0));
+      if (h > 0) (void)hipMemcpy(keys.data(), cq, sizeof(int32_t) * (size_t)h, hipMemcpyDeviceToHost);
+      std::sort(keys.begin(), keys.end());
+      int64_t distinct = 0, max_run = 0, run = 0;
+      for (size_t i = 0; i < keys.size(); ++i) {
+        run = (i > 0 && keys[i] == keys[i - 1]) ? run + 1 : 1;
+        if (run == 1) ++distinct;
+        max_run = std::max(max_run, run);
+      }
+      std::fprintf(stderr, "[rpt stats] n=%lld k5_slow_queue=%d cells=%lld max_per_cell=%lld\n",
+                   (long long)n, h, (long long)distinct, (long long)max_run);
     }
 #endif
     tm.mark();
@@ -5158,8 +5180,18 @@ int32_t dbscan_set_core(DbscanState* S, const uint8_t* core_in, hipStream_t st) 
 }
 int32_t dbscan_components(DbscanState* S, int32_t* comp_out, hipStream_t st) {
   RPT_TRY(S->union_pass(st));
-  hipLaunchKernelGGL(k_comp_out, dim3(grid_for(S->n, kBlock, 2048)), dim3(kBlock), 0, st,
-                     S->parent, S->core, S->sorig, S->n, comp_out);
+  if (S->degenerate || S->n == 0) {  // (no cell structure: every core point walks its chain)
+    hipLaunchKernelGGL(k_comp_out, dim3(grid_for(S->n, kBlock, 2048)), dim3(kBlock), 0, st,
+                       S->parent, S->core, S->sorig, S->n, comp_out, S->skey,
+                       (const int32_t*)nullptr, (int64_t)0);
+  } else {
+    hipLaunchKernelGGL(k_cell_roots, dim3(grid_for(S->n, kBlock, 2048)), dim3(kBlock), 0, st,
+                       S->parent, S->occ, S->n_occ_dev, S->C, S->mutual, S->rep, S->cell_root,
+                       (int32_t*)nullptr);
+    hipLaunchKernelGGL(k_comp_out, dim3(grid_for(S->n, kBlock, 2048)), dim3(kBlock), 0, st,
+                       S->parent, S->core, S->sorig, S->n, comp_out, S->skey,
+                       (const int32_t*)S->cell_root, S->C);
+  }
   RPT_CHECK_LAUNCH();
   return RPT_OK;
 }

@@ -14,6 +14,7 @@
 #   kab           same-box ABBA kernel A/B against abl/librpt_base.so (tools/ab_base.sh)
 #   prof          profiles/r5 kernel traces + PMC traffic (tools/prof.sh) for the three workloads
 #   bench         the default bench line (driver command)
+#   bench_hwq     the bench line at 4 (default) and 8 hardware queues per process, interleaved
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
 O=gpurun_out/r5
@@ -91,6 +92,15 @@ for step in "$@"; do
       done ;;
     bench)
       run bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1 ;;
+    bench_hwq)    # the driver's bench line with the default 4 hardware queues vs 8, interleaved
+      BB="python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --h2d-steps 0"
+      for rep in 1 2; do
+        run bhq4_$rep 300 $BB || exit 1
+        GPU_MAX_HW_QUEUES=8 run bhq8_$rep 300 $BB || exit 1
+      done
+      for f in $O/bhq*.log; do
+        python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['value'], d['ms_per_step'], d['steady_state']['ms_per_step'])" $f
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
