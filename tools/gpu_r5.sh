@@ -14,6 +14,7 @@
 #   kab           same-box ABBA kernel A/B against abl/librpt_base.so (tools/ab_base.sh)
 #   prof          profiles/r5 kernel traces + PMC traffic (tools/prof.sh) for the three workloads
 #   bench         the default bench line (driver command)
+#   smoke         __graft_entry__.smoke()
 #   bench_hwq     the bench line at 4 (default) and 8 hardware queues per process, interleaved
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
@@ -51,6 +52,11 @@ for step in "$@"; do
       for rep in 1 2; do
         RPT_COMM_FORCE_COLLECTIVES=1 run sl1_$rep 200 $BS --lanes 1 --steps 40 --warmup 6 || exit 1
         RPT_COMM_FORCE_COLLECTIVES=1 run sl3_$rep 200 $BS --lanes 3 --steps 40 --warmup 6 || exit 1
+      done ;;
+    shard_lanes5) # per-rank step at one rank, every collective through RCCL: 3 vs 5 lanes
+      for rep in 1 2; do
+        RPT_COMM_FORCE_COLLECTIVES=1 run sl3b_$rep 200 $BS --lanes 3 --steps 40 --warmup 6 || exit 1
+        RPT_COMM_FORCE_COLLECTIVES=1 run sl5_$rep 200 $BS --lanes 5 --steps 40 --warmup 6 || exit 1
       done ;;
     diag)         # A/B build: queue / list sizes (RPT_STATS) per workload, union cells per wave
       AB=radar-point-cloud-tracking_amd/rpt/librpt_ab.so
@@ -92,6 +98,8 @@ for step in "$@"; do
       done ;;
     bench)
       run bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1 ;;
+    smoke)
+      run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench_lanes)  # the driver's bench line at 5 (default), 6 and 8 stacks in flight, interleaved
       BB="python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --h2d-steps 0"
       for rep in 1 2; do
