@@ -2663,6 +2663,10 @@ __global__ __launch_bounds__(kBlock, 6) void k_union_cells_pair(
       mal = mutual[cal];
     }
     if (nm_list) s_nm.push(__ballot(ral >= 0 && !mal), cal, lane, nm_list, nm_count);
+    // every todo cell's record loaded here, with the chunk's headers (one dependent level), and
+    // handed to its half by shuffles: the pair loop starts at the window's occupancy loads
+    CellRec<2> rl{};
+    if (ral >= 0 && mal) rl = crec[cal];
     uint64_t todo = __ballot(ral >= 0 && mal);
     uint64_t lmask = 0;  // cells of this chunk with undecided candidates (plist)
     while (todo) {  // (wave-uniform) two cells at a time, one per half
@@ -2676,8 +2680,16 @@ __global__ __launch_bounds__(kBlock, 6) void k_union_cells_pair(
       const int ca = __shfl(cal, lsrc);
       const int ra = __shfl(ral, lsrc);
       bool any_und = false;
+      CellRec<2> ra_rec;  // (every lane takes part in the shuffles)
+      ra_rec.b = __shfl(rl.b, lsrc);
+      ra_rec.e = __shfl(rl.e, lsrc);
+      ra_rec.x0 = __shfl(rl.x0, lsrc);
+      ra_rec.x1 = __shfl(rl.x1, lsrc);
+      ra_rec.y0 = __shfl(rl.y0, lsrc);
+      ra_rec.y1 = __shfl(rl.y1, lsrc);
+      ra_rec.t0 = __shfl(rl.t0, lsrc);
+      ra_rec.t1 = __shfl(rl.t1, lsrc);
       if (lq >= 0) {  // (half-uniform)
-        const CellRec<2> ra_rec = crec[ca];
         const float4 A1 = rec_boxA<2>(ra_rec), A2 = rec_boxB(ra_rec);
         int cx, cy, cz;
         decode_key<2>(ca, g, cx, cy, cz);
