@@ -51,6 +51,30 @@ def test_set_order_matches_cpython(seed):
     assert set_order(seq) == [int(v) for v in ref]
 
 
+def test_order_clusters_threaded_matches_per_frame():
+    """rpt_order_clusters splits a long stack's frames over host threads (>= 8192 segments and
+    >= 64 frames): every frame's order must equal the single-frame call's (CPython set order of
+    its labels by first index, noise included)."""
+    from rpt import stages
+
+    rng = np.random.default_rng(7)
+    F, per = 300, 40
+    frames = np.repeat(np.arange(F, dtype=np.int32), per)
+    labels = np.concatenate([rng.choice(60000, per, replace=False) for _ in range(F)])
+    first = np.concatenate([np.sort(rng.choice(10**6, per, replace=False)) for _ in range(F)])
+    perm = rng.permutation(len(frames))  # segments in arbitrary order
+    seg = {"frame": frames[perm], "label": labels[perm].astype(np.int32),
+           "first": first[perm].astype(np.int64)}
+    noise = rng.integers(-1, 10**6, F).astype(np.int64)
+    fo, order = stages.order_frames(F, seg, noise)
+    for f in range(F):
+        idx = np.nonzero(seg["frame"] == f)[0]
+        sub = {"frame": np.zeros(len(idx), np.int32), "label": seg["label"][idx],
+               "first": seg["first"][idx]}
+        _, o1 = stages.order_frames(1, sub, noise[f:f + 1])
+        np.testing.assert_array_equal(order[fo[f]:fo[f + 1]], idx[o1], err_msg=f"frame {f}")
+
+
 def _lsap_cases():
     rng = np.random.default_rng(0)
     for k in range(60):
