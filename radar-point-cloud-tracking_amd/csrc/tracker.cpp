@@ -21,7 +21,6 @@
 #include <cstring>
 #include <limits>
 #include <numeric>
-#include <thread>
 #include <vector>
 
 #include <immintrin.h>
@@ -148,46 +147,28 @@ int32_t order_clusters(int32_t n_frames, int64_t n_seg, const int32_t* seg_frame
   std::vector<int64_t> byf(n_seg);
   std::vector<int64_t> cur(cnt.begin(), cnt.end() - 1);
   for (int64_t s = 0; s < n_seg; ++s) byf[cur[seg_frame[s]]++] = s;
-  // frames are independent (each writes its own order range): a long stack's frames go to a few
-  // host threads (the order is ~1/4 of a 1000-frame stack's host stage; set_order's emulated set
-  // is thread-local)
-  auto frames = [&](int32_t f0, int32_t f1) {
-    std::vector<std::pair<int64_t, int32_t>> occ;  // (first index, label)
-    std::vector<int32_t> keys, ord;
-    std::vector<std::pair<int32_t, int64_t>> l2s;
-    for (int32_t f = f0; f < f1; ++f) {
-      const int64_t b = cnt[f], e = cnt[f + 1];
-      occ.clear();
-      for (int64_t q = b; q < e; ++q) occ.emplace_back(seg_first[byf[q]], seg_label[byf[q]]);
-      if (frame_first_noise && frame_first_noise[f] >= 0)
-        occ.emplace_back(frame_first_noise[f], -1);
-      std::sort(occ.begin(), occ.end());
-      keys.resize(occ.size());
-      for (size_t q = 0; q < occ.size(); ++q) keys[q] = occ[q].second;
-      ord.resize(occ.size());
-      const int32_t m = set_order(keys.data(), (int32_t)keys.size(), ord.data());
-      // label -> segment (labels are unique within a frame)
-      l2s.clear();
-      for (int64_t q = b; q < e; ++q) l2s.emplace_back(seg_label[byf[q]], byf[q]);
-      std::sort(l2s.begin(), l2s.end());
-      for (int32_t q = 0; q < m; ++q) {
-        auto it = std::lower_bound(l2s.begin(), l2s.end(), std::make_pair(ord[q], int64_t(-1)));
-        order[b + q] = it->second;
-      }
+  std::vector<std::pair<int64_t, int32_t>> occ;  // (first index, label)
+  std::vector<int32_t> keys, ord;
+  std::vector<std::pair<int32_t, int64_t>> l2s;
+  for (int32_t f = 0; f < n_frames; ++f) {
+    const int64_t b = cnt[f], e = cnt[f + 1];
+    occ.clear();
+    for (int64_t q = b; q < e; ++q) occ.emplace_back(seg_first[byf[q]], seg_label[byf[q]]);
+    if (frame_first_noise && frame_first_noise[f] >= 0) occ.emplace_back(frame_first_noise[f], -1);
+    std::sort(occ.begin(), occ.end());
+    keys.resize(occ.size());
+    for (size_t q = 0; q < occ.size(); ++q) keys[q] = occ[q].second;
+    ord.resize(occ.size());
+    const int32_t m = set_order(keys.data(), (int32_t)keys.size(), ord.data());
+    // label -> segment (labels are unique within a frame)
+    l2s.clear();
+    for (int64_t q = b; q < e; ++q) l2s.emplace_back(seg_label[byf[q]], byf[q]);
+    std::sort(l2s.begin(), l2s.end());
+    for (int32_t q = 0; q < m; ++q) {
+      auto it = std::lower_bound(l2s.begin(), l2s.end(), std::make_pair(ord[q], int64_t(-1)));
+      order[b + q] = it->second;
     }
-  };
-  const int nt = n_seg >= 8192 && n_frames >= 64 ? 4 : 1;
-  if (nt == 1) {
-    frames(0, n_frames);
-    return RPT_OK;
   }
-  std::vector<std::thread> th;
-  th.reserve(nt - 1);
-  for (int t = 1; t < nt; ++t)
-    th.emplace_back(frames, (int32_t)((int64_t)n_frames * t / nt),
-                    (int32_t)((int64_t)n_frames * (t + 1) / nt));
-  frames(0, (int32_t)((int64_t)n_frames / nt));
-  for (auto& x : th) x.join();
   return RPT_OK;
 }
 

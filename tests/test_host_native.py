@@ -51,10 +51,10 @@ def test_set_order_matches_cpython(seed):
     assert set_order(seq) == [int(v) for v in ref]
 
 
-def test_order_clusters_threaded_matches_per_frame():
-    """rpt_order_clusters splits a long stack's frames over host threads (>= 8192 segments and
-    >= 64 frames): every frame's order must equal the single-frame call's (CPython set order of
-    its labels by first index, noise included)."""
+def test_order_clusters_stack_matches_per_frame():
+    """rpt_order_clusters over a whole stack (segments in arbitrary order, bucketed by frame):
+    every frame's order must equal the single-frame call's (CPython set order of its labels by
+    first index, noise included)."""
     from rpt import stages
 
     rng = np.random.default_rng(7)
