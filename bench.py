@@ -34,10 +34,14 @@ another, and K5's roofline is taken from that leg (K5 alone on the GPU).
 At N>1 (the frame-sharded path) three stacks are in flight per rank by default, their
 collectives through ONE communicator in a fixed software-pipeline order (rpt.dist.CommSequencer:
 every rank issues the same collectives in the same order; validated with gloo at 8 ranks and on
-RCCL at one rank with every collective forced through it -- RPT_COMM_FORCE_COLLECTIVES=1: 1.58-1.63
-ms per 125-frame step with 3 lanes against 2.15-2.27 with 1, profiles/r5/rccl_lanes/); `--lanes 1`
-runs one stack at a time.  With one rank (`--sharded`, the 125-frame per-rank share of 8 GPUs)
-the default is 3 as well (identity collectives).
+RCCL at one rank with every collective forced through it -- RPT_COMM_FORCE_COLLECTIVES=1: 1.62-1.73
+ms per 125-frame step with 3 lanes against 2.04 with 1 in round 5, profiles/r5/rccl_lanes/);
+`--lanes 1` runs one stack at a time.  With one rank (`--sharded`, the 125-frame per-rank share of
+8 GPUs) the default is 3 as well (identity collectives).  The process group has a finite timeout
+(RPT_PG_TIMEOUT_S, default 240 s) and a hang guard (RPT_HANG_S, default 180 s without a step
+submitted or finished) dumps every thread's Python stack -- the lane threads name the collective
+slot they wait in -- and exits non-zero, so a cross-GPU ordering fault ends the run instead of
+hanging it.
 After the timed region (N=1, timing on), K5 is also timed on the per-GPU shares at 8 GPUs, where
 SURVEY.md §8(d) sets the 0.40 roofline target: `roofline_c4_share` (125 standard frames, the
 configs[3] stack's share) and `roofline_configs4_share` (125 dense frames, configs[4]'s), one
@@ -270,8 +274,14 @@ def main():
     if dist:
         import torch.distributed as tdist
 
+        from datetime import timedelta
+
+        # RCCL errors and timeouts tear the process down (non-zero exit) instead of hanging
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        tdist.init_process_group(
+            "nccl", device_id=torch.device("cuda", local),
+            timeout=timedelta(seconds=float(os.environ.get("RPT_PG_TIMEOUT_S", "240"))))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -306,7 +316,7 @@ def main():
         from rpt.dist import Comm, NativeShardPipeline, ShardedStackPipeline
 
         # rank 0's host stage (order + tracker over N*F frames, ~6 us/frame) of consecutive
-        # steps runs on 4 worker threads: the steps are independent stacks
+        # steps runs on --host-workers threads (default 8): the steps are independent stacks
         if args.python_shard:
             from rpt.stages import HipOps
 
@@ -352,8 +362,22 @@ def main():
                           cfg.n_frames * len(cfg.gains))
         run = lambda e: pipe.submit(e)  # noqa: E731
 
+    import faulthandler
+
+    hang_s = float(os.environ.get("RPT_HANG_S", "180"))
+
+    def alive():
+        # hang guard (sharded runs): no step submitted or finished for hang_s seconds -> every
+        # thread's stack to stderr (a lane thread shows the CommSequencer slot it waits in) and
+        # exit 1, instead of waiting for the driver's limit
+        if dist and hang_s > 0:
+            faulthandler.dump_traceback_later(hang_s, exit=True)
+
     def resolve(r):
-        return r.result() if hasattr(r, "result") else r
+        alive()
+        out = r.result() if hasattr(r, "result") else r
+        alive()
+        return out
 
     def points_of(r):  # K1 points of the whole (global) stack of a run
         return float(r.n_points_global if dist else r.n_points)
@@ -369,12 +393,16 @@ def main():
     if dist:
         tdist.barrier()
     torch.cuda.synchronize(dev)
+    sharded_lanes = dist and not args.python_shard and args.lanes > 1
+    if sharded_lanes:  # slot waits of the timed steps only
+        lanes_.seq.wait_s = [0.0] * lanes_.seq.P
+        lanes_.seq.wait_n = [0] * lanes_.seq.P
     t0 = time.perf_counter()
     stage_acc = {}
     k5 = []      # (K5 ms, points entering ST-DBSCAN) per timed run
     results = []
-    sharded_lanes = dist and not args.python_shard and args.lanes > 1
     for k in range(args.steps):
+        alive()
         results.append(run(echoes[k % E]))
         if timing and dist and not sharded_lanes:
             k5.append((ops.last_core_ms(), ops.core_points))
@@ -388,6 +416,14 @@ def main():
         tdist.barrier()
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
+    slot_wait = None
+    if sharded_lanes:
+        slot_wait = {"ms_per_step_by_phase": [round(w / args.steps * 1e3, 4)
+                                              for w in lanes_.seq.wait_s],
+                     "entered_by_phase": list(lanes_.seq.wait_n),
+                     "note": "time a lane thread waited for its CommSequencer turn, per "
+                             "collective slot (0 info, 1 land, 2 halo, 3 flags, 4 comp ids, "
+                             "5 pairs, 6 results, 7 redo), summed over lanes, per timed step"}
     for r in results:
         for key, v in r.stage_ms.items():
             stage_acc[key] = stage_acc.get(key, 0.0) + v
@@ -619,6 +655,7 @@ def main():
                        "overlapped: step k's order+tracker runs on a host thread during step "
                        "k+1's device work; the timed region ends after the last one"},
             "steady_state": steady,
+            "slot_wait": slot_wait,
             "one_stack_in_flight": seq,
             "roofline": roof, "roofline_c4_share": roof_c4, "roofline_configs4_share": roof_c4d,
             "roofline_k1": roof_k1,
@@ -627,6 +664,7 @@ def main():
             "stage_ms_from": "one_stack_in_flight" if seq is not None else "timed steps",
         }
         print(json.dumps(out), flush=True)
+    faulthandler.cancel_dump_traceback_later()
     if dist:
         tdist.destroy_process_group()
 

@@ -7,7 +7,6 @@
 #include "common.h"
 
 namespace rpt {
-const char* last_error_cstr();
 void release_scratch_current();
 int32_t label_means(const int32_t* labels, const float* x, const float* y, const float* inten,
                     int64_t n, int64_t n_labels, int64_t* o_count, float* o_x, float* o_y,
@@ -136,9 +135,7 @@ int32_t rpt_select_roots(const int64_t* rep, int64_t base, int64_t lo, int64_t h
 }
 
 
-int32_t rpt_version(void) { return 100; }  // 0.1.0
 
-const char* rpt_last_error(void) { return rpt::last_error_cstr(); }
 
 int32_t rpt_device_count(void) {
   int n = 0;

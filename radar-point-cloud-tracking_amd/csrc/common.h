@@ -8,13 +8,9 @@
 #include <string>
 #include <vector>
 
-#include "../../include/rpt.h"
+#include "host_common.h"
 
 namespace rpt {
-
-// ---- error plumbing (thread-local last error, no exceptions across the ABI) -----------
-void set_error(const char* fmt, ...);
-void clear_error();
 
 #define RPT_HIP(expr)                                                               \
   do {                                                                              \
@@ -24,12 +20,6 @@ void clear_error();
                        __FILE__, __LINE__);                                         \
       return RPT_EHIP;                                                              \
     }                                                                               \
-  } while (0)
-
-#define RPT_TRY(expr)              \
-  do {                             \
-    int32_t s__ = (expr);          \
-    if (s__ != RPT_OK) return s__; \
   } while (0)
 
 #define RPT_CHECK_LAUNCH() RPT_HIP(hipGetLastError())
@@ -73,7 +63,6 @@ class Scratch {
 };
 Scratch& scratch(hipStream_t st);  // for the current device and this stream
 
-inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // Byte budget helper: sum of aligned array sizes.
 struct Budget {
   size_t bytes = 0;

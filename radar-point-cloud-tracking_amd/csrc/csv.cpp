@@ -29,7 +29,7 @@
 #include <thread>
 #include <vector>
 
-#include "common.h"
+#include "host_common.h"
 
 namespace rpt {
 namespace {

@@ -2,7 +2,7 @@
 //  * exclusive scan — single pass with decoupled look-back (one launch, no memset),
 //  * stable LSD radix sort of (u32 key, u32 value) pairs, 8-bit digits, wave-granular
 //    histograms so that a pass needs no block-level barriers inside the scatter loop.
-// Plus the library's error plumbing and per-(device, stream) scratch pools.
+// Plus the per-(device, stream) scratch pools.
 #include <algorithm>
 #include <chrono>
 #include <cstdarg>
@@ -13,19 +13,7 @@
 
 namespace rpt {
 
-// ------------------------------------------------------------------ error plumbing
-static thread_local std::string g_last_error;
-
-void set_error(const char* fmt, ...) {
-  char buf[1024];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof buf, fmt, ap);
-  va_end(ap);
-  g_last_error = buf;
-}
-void clear_error() { g_last_error.clear(); }
-const char* last_error_cstr() { return g_last_error.c_str(); }
+// (the error plumbing lives in errors.cpp)
 
 // ------------------------------------------------------------------ readback wait
 // The path's size readbacks are tiny and the GPU idles until the host has launched the next

@@ -89,6 +89,17 @@ __device__ __forceinline__ uint64_t dpp_mov(uint64_t v) {
 template <int G, class T, class F>
 __device__ __forceinline__ T row_reduce(T v, F op) {
   static_assert(G == 2 || G == 4 || G == 8 || G == 16, "groups within a row");
+#ifdef RPT_DEBUG_DPP
+  // (debug builds, -DRPT_DEBUG_DPP) the DPP moves read 0 from an inactive lane: a min would
+  // return 0 and a sum drop terms, so every lane of this lane's aligned G-lane group must be
+  // active -- all callers keep their loops group-uniform
+  {
+    const uint64_t act = __ballot(1);
+    const int g0 = (int)(threadIdx.x & 63) & ~(G - 1);
+    const uint64_t need = (G == 64 ? ~0ull : ((1ull << G) - 1)) << g0;
+    if ((act & need) != need) __builtin_trap();
+  }
+#endif
   v = op(v, dpp_mov<0xB1>(v));                 // quad_perm [1,0,3,2]
   if (G >= 4) v = op(v, dpp_mov<0x4E>(v));     // quad_perm [2,3,0,1]
   if (G >= 8) v = op(v, dpp_mov<0x141>(v));    // row_half_mirror
@@ -4867,6 +4878,10 @@ int32_t DbscanState::labels_global(const int64_t* rep_orig, const int64_t* reps,
                        st, core, ccmin, cid, slab, n, labels);
   hipLaunchKernelGGL(k_label_global_core, dim3(gb), dim3(kBlock), 0, st, core, ccmin, cid, sorig,
                      n, slab, orig ? nullptr : labels, skey, C, cell_min);
+  // slab now holds the sorted points' core labels, no longer the inverse permutation: a second
+  // call on this state (the shard driver's redo of a step whose pairs / results overflowed, a
+  // host merge, the K9 radix fallback) takes the sorted-order path
+  spos_on = false;
 #ifdef RPT_AB
   if (use_label_tiles())
     hipLaunchKernelGGL((k_label_tiles<true>), dim3(tile_grid_blocks()), dim3(kTileBlock), 0, st,
@@ -5095,8 +5110,11 @@ int32_t stdbscan_bounds_final_dev(const void* part_dev, int nb, void* out_dev, h
   RPT_CHECK_LAUNCH();
   return RPT_OK;
 }
+// the partials of a bounds pass of kBoundsBlock-thread blocks (k_bounds here, k_window in the
+// shard driver) over at most n_max points: one per block of grid_for(n_max, kBoundsBlock, 1024)
+static_assert(kBlock == kBoundsBlock, "k_bounds is launched with kBlock threads per block");
 size_t stdbscan_bounds_part_bytes(int64_t n_max) {
-  return sizeof(Bounds) * (size_t)grid_for(std::max<int64_t>(n_max, 1), kBlock, 1024);
+  return sizeof(Bounds) * (size_t)grid_for(std::max<int64_t>(n_max, 1), kBoundsBlock, 1024);
 }
 
 int32_t stdbscan_deferred(const float* x, const float* y, const float* z, int64_t stride,

@@ -25,7 +25,7 @@
 
 #include <immintrin.h>
 
-#include "common.h"
+#include "host_common.h"
 
 #pragma STDC FP_CONTRACT OFF
 

@@ -490,20 +490,25 @@ class CommSequencer:
         self.d = max(1, -(-self.P // self.L))
         self.cv = threading.Condition()
         self.failed: Optional[BaseException] = None
-        self.epochs: List[List[int]] = []   # [first step, base time, closed (0/1)]
-        self.epoch_of: Dict[int, int] = {}
+        # the open (last) epoch [first step, base time, closed (0/1)]; a step keeps a reference
+        # to its own epoch until its last slot is released, so nothing here grows with the
+        # number of steps run (a long-running service submits steps without bound)
+        self.epoch: Optional[List[int]] = None
+        self.epoch_of: Dict[int, List[int]] = {}  # steps not done -> their epoch
         self.next_phase: Dict[int, int] = {}  # step -> its next phase (steps not done)
         self.n_reg = 0
         self.t_end = 0                         # one past the last slot time of any step
+        # slot-wait accounting (seconds a step's thread waited for its turn, per phase)
+        self.wait_s = [0.0] * self.P
+        self.wait_n = [0] * self.P
 
     def register(self, step: int):
         """Called by the submitter, in step order, before the step runs."""
         with self.cv:
-            e = self.epochs[-1] if self.epochs else None
+            e = self.epoch
             if e is None or e[2]:
-                e = [step, self.t_end, 0]
-                self.epochs.append(e)
-            self.epoch_of[step] = len(self.epochs) - 1
+                e = self.epoch = [step, self.t_end, 0]
+            self.epoch_of[step] = e
             self.next_phase[step] = 0
             self.n_reg = step + 1
             self.t_end = max(self.t_end, self._time(step, self.P - 1) + 1)
@@ -512,12 +517,12 @@ class CommSequencer:
     def close_group(self):
         """No more steps join the open epoch (the submitter is about to wait on a result)."""
         with self.cv:
-            if self.epochs and not self.epochs[-1][2]:
-                self.epochs[-1][2] = 1
+            if self.epoch is not None and not self.epoch[2]:
+                self.epoch[2] = 1
                 self.cv.notify_all()
 
     def _time(self, step: int, phase: int) -> int:
-        e = self.epochs[self.epoch_of[step]]
+        e = self.epoch_of[step]
         return e[1] + (step - e[0]) * self.d + phase
 
     def _blocked(self, step: int, phase: int) -> bool:  # under self.cv
@@ -525,8 +530,8 @@ class CommSequencer:
         for s, q in self.next_phase.items():
             if s != step and (self._time(s, q), s) < key:
                 return True
-        e = self.epochs[-1]
-        if not e[2]:  # the open epoch's next (unsubmitted) step could come first
+        e = self.epoch
+        if e is not None and not e[2]:  # the open epoch's next (unsubmitted) step could come first
             t = e[1] + (self.n_reg - e[0]) * self.d
             if (t, self.n_reg) < key:
                 return True
@@ -534,8 +539,14 @@ class CommSequencer:
 
     def _acquire(self, step: int, phase: int):
         with self.cv:
+            t0 = None
             while self.failed is None and self._blocked(step, phase):
+                if t0 is None:
+                    t0 = time.perf_counter()
                 self.cv.wait()
+            if t0 is not None:
+                self.wait_s[phase] += time.perf_counter() - t0
+            self.wait_n[phase] += 1
             if self.failed is not None:
                 raise RuntimeError("collective sequence aborted by another stack") \
                     from self.failed
@@ -549,6 +560,7 @@ class CommSequencer:
         with self.cv:
             if phase + 1 >= self.P:
                 self.next_phase.pop(step, None)
+                self.epoch_of.pop(step, None)
             else:
                 self.next_phase[step] = phase + 1
             self.cv.notify_all()

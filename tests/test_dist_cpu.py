@@ -350,3 +350,43 @@ def test_comm_sequencer_skipped_redo_slot_does_not_wait():
     assert done[2].wait(5)
     for t in ts:
         t.join(5)
+
+
+def test_comm_sequencer_state_stays_bounded():
+    """A long run of steps (a serving process submitting stacks without end, with waits that
+    close epochs now and then) leaves no per-step entry behind in the sequencer once the steps
+    are done: its dicts hold at most the steps in flight."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from rpt.dist import CommSequencer
+
+    L, P = 3, 8
+    seq = CommSequencer(L, P)
+    pools = [ThreadPoolExecutor(max_workers=1) for _ in range(L)]
+
+    def run(step):
+        slots = seq.step(step)
+        try:
+            for p in range(P - 1):   # the redo slot unused
+                with slots.slot(p):
+                    pass
+        finally:
+            slots.close()
+
+    futs = []
+    peak = 0
+    for s in range(600):
+        seq.register(s)
+        futs.append(pools[s % L].submit(run, s))
+        peak = max(peak, len(seq.epoch_of), len(seq.next_phase))
+        if s % 7 == 6:          # the submitter waits now and then: closes the open epoch
+            seq.close_group()
+            futs[-3].result(timeout=30)
+    seq.close_group()
+    for f in futs:
+        f.result(timeout=30)
+    for p in pools:
+        p.shutdown()
+    assert seq.epoch_of == {} and seq.next_phase == {}
+    assert peak <= 16, peak   # the steps in flight (submitted, not done), not the 600 run
+    assert sum(seq.wait_n) == 600 * (P - 1)

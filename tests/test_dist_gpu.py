@@ -75,6 +75,19 @@ def test_sharded_dense_giant_component_matches_oracle(world, frames, lanes):
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("redo", ["--tiny-caps", "--force-host-merge"])
+def test_sharded_dense_redo_slot_matches_oracle(redo):
+    """The redo slot on DENSE slabs: there the grid build leaves the inverse permutation in the
+    slab buffer and the global label pass reads it once before overwriting it with the core
+    labels (k_label_global_orig, then k_label_global_core), so a step finished a second time
+    (pair / result capacities exceeded, or the equivalences merged on the host) must take the
+    sorted-order form on its second call.  2 ranks x 2 dense frames, every step finished again,
+    against the oracle's run_path over the whole stack (4_temporal_object_tracker.py:466-506)."""
+    _run(2, 2, "native", 1, ["--dense", "--oracle", redo], timeout=840)
+
+
+@pytest.mark.gpu
 @pytest.mark.timeout(1000)
 def test_sharded_config4_full_share_sample_check():
     """BASELINE configs[4] at its real per-rank shape: 8 gloo ranks sharing the GPU, each with
