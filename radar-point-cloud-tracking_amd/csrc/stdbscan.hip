@@ -120,6 +120,10 @@ struct OpAdd {
   template <class T>
   __device__ T operator()(T a, T b) const { return a + b; }
 };
+struct OpOr {
+  template <class T>
+  __device__ T operator()(T a, T b) const { return a | b; }
+};
 
 
 template <int D>
@@ -1780,8 +1784,9 @@ struct CwQueue {
   int fail;   // first reservation that did not fit
   int base;
 };
-__device__ __forceinline__ void cells_fill_epilogue(const Geom& g, bool act, int32_t ca, int b,
-                                                    int e, int flag, uint8_t* __restrict__ core,
+__device__ __forceinline__ void cells_fill_epilogue(const Geom& g, bool act, int32_t ca,
+                                                    int32_t qk, int b, int e, int flag,
+                                                    uint8_t* __restrict__ core,
                                                     unsigned long long* __restrict__ cmin,
                                                     int32_t* __restrict__ slow,
                                                     int32_t* __restrict__ slowk,
@@ -1796,7 +1801,7 @@ __device__ __forceinline__ void cells_fill_epilogue(const Geom& g, bool act, int
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     gb[k] = __builtin_amdgcn_readlane(b, 8 * k);
-    gc[k] = __builtin_amdgcn_readlane(ca, 8 * k);
+    gc[k] = __builtin_amdgcn_readlane(qk, 8 * k);  // the queue's per-point cell word
     const int ek = __builtin_amdgcn_readlane(e, 8 * k);
     gf[k] = __builtin_amdgcn_readlane(flag, 8 * k);
     if (k < na) {
@@ -1868,7 +1873,12 @@ __device__ __forceinline__ int sum8(int v) { return row_reduce<8>(v, OpAdd{}); }
 
 constexpr int kCwMaxR = 3;
 constexpr int kCwBatch = 4;  // candidate records per lane in flight together (k_core_cells_oct)
-template <bool FUSED = false>
+// MASK (with FUSED, windows of W = 2R + 1 <= 5 slabs): every undecided cell hands its decisions
+// to k_core_slow_masked -- its whole-accept count lo (clo[q], q = its occupied-list position) and
+// the 128-bit mask of its candidates that box classification left partial (pmask[q]; window
+// position 5 P + dx, P = the (slab, row) pair j + 8 i of lane j's slot i) -- and queues its points
+// with q instead of the cell key.
+template <bool FUSED = false, bool MASK = false>
 // 5 waves/SIMD (<= 96 VGPRs; the fused epilogue and its LDS queue would take 99: 4 waves)
 __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
                                                           const int32_t* __restrict__ occ,
@@ -1884,7 +1894,10 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
                                                               nullptr,
                                                           int32_t* __restrict__ slow = nullptr,
                                                           int32_t* __restrict__ slowk = nullptr,
-                                                          int32_t* __restrict__ n_slow = nullptr) {
+                                                          int32_t* __restrict__ n_slow = nullptr,
+                                                          uint4* __restrict__ pmask = nullptr,
+                                                          int32_t* __restrict__ clo = nullptr) {
+  static_assert(!MASK || FUSED, "the masks feed the fused pipeline's slow pass");
   // legacy pipeline: the level-4 queue counter, zeroed here instead of by a memset launch
   // (k_core_fill, the next kernel on the stream, is its first user)
   if (!FUSED && zero_counter && blockIdx.x == 0 && threadIdx.x == 0) *zero_counter = 0;
@@ -1991,12 +2004,14 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
         // as soon as the adjacent-to-every-point count reaches min_samples (dense cells: after
         // the own row's batch)
         bool decided = false;
+        uint32_t pm25 = 0;  // (MASK) the lane's candidates left partial, bits as m25's
         while (true) {
           int rem = m25 ? 1 : 0;
           rem = sum8(rem);
           if (rem == 0) break;  // (uniform over the cell's eight lanes)
           CellRec<2> cr[kCwBatch];
           bool has[kCwBatch];
+          const uint32_t mb = m25;  // (MASK) the batch takes the lowest set bits of mb
 #pragma unroll
           for (int i = 0; i < kCwBatch; ++i) {
             // branch-free record loads (a lane without a candidate re-reads its own cell's)
@@ -2007,6 +2022,7 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
             const int key = s_k0[sl5][threadIdx.x] + (p - 5 * sl5);
             cr[i] = crec[has[i] ? key : ca];
           }
+          uint32_t pf = 0;  // (MASK) batch entries left partial
 #pragma unroll
           for (int i = 0; i < kCwBatch; ++i) {
             if (!has[i]) continue;
@@ -2014,6 +2030,15 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
                 classify_cells<2, true>(A1, rec_boxA<2>(cr[i]), A2, rec_boxB(cr[i]), g);
             lo += (cls == 1) ? cr[i].e - cr[i].b : 0;
             hi += (cls != 0) ? cr[i].e - cr[i].b : 0;
+            if (MASK) pf |= (cls == 2) ? (1u << i) : 0u;
+          }
+          if (MASK) {
+            uint32_t tk = mb & ~m25;  // entry i = the i-th lowest bit taken
+#pragma unroll
+            for (int i = 0; i < kCwBatch; ++i) {
+              pm25 |= ((pf >> i) & 1u) ? (tk & (0u - tk)) : 0u;
+              tk &= tk - 1;
+            }
           }
           int ls = lo;
           ls = sum8(ls);
@@ -2028,6 +2053,29 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
           lo = sum8(lo);
           hi = sum8(hi);
           flag = (lo >= need) ? 1 : ((hi < need) ? 0 : 2);
+          if (MASK && flag == 2) {  // (group-uniform) hand the decisions to the slow pass
+            // slot i of lane j = pair P = j + 8 i; its five columns go to window positions
+            // 5 P .. 5 P + 4 (P < 5 W <= 25: slot 4 and most of slot 3 are never valid)
+            uint64_t mlo = 0, mhi = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const uint64_t ch = (pm25 >> (5 * i)) & 31u;
+              const int pos = 5 * (j + 8 * i);
+              if (pos < 64) {
+                mlo |= ch << pos;
+                if (pos > 59) mhi |= ch >> (64 - pos);
+              } else if (pos < 128) {
+                mhi |= ch << (pos - 64);
+              }
+            }
+            mlo = row_reduce<8>(mlo, OpOr{});
+            mhi = row_reduce<8>(mhi, OpOr{});
+            if (j == 0) {
+              pmask[q] = make_uint4((uint32_t)mlo, (uint32_t)(mlo >> 32), (uint32_t)mhi,
+                                    (uint32_t)(mhi >> 32));
+              clo[q] = lo;
+            }
+          }
         }
       }
     }
@@ -2036,7 +2084,9 @@ __global__ __launch_bounds__(kBlock, 5) void k_core_cells_oct(Geom g, int R,
       // decided cells write their points' flags here (the undecided ones are k_core_slow_cells')
       if (core && act && flag != 2) write_cell_flags(core, b, e, j, 8, (uint8_t)flag);
     } else {
-      cells_fill_epilogue(g, act, ca, b, e, flag, core, cmin, slow, slowk, n_slow, lq);
+      // (MASK: the queue carries the cell's occupied-list position instead of its key)
+      cells_fill_epilogue(g, act, ca, MASK ? (int32_t)q : ca, b, e, flag, core, cmin, slow, slowk,
+                          n_slow, lq);
     }
   }
   if constexpr (FUSED) {  // flush the block's queue (the cell loop is block-uniform)
@@ -2234,6 +2284,80 @@ __global__ __launch_bounds__(kBlock, 8) void k_core_slow(const float4* __restric
     if (lane == 0) {
       core[s] = (cnt >= need) ? 1 : 0;
       if (cmin && cnt >= need && (int64_t)key < g.cells)
+        atomicMin(cmin + key, ((unsigned long long)(uint32_t)sorig[s] << 32) | (uint32_t)s);
+    }
+  }
+}
+
+// Level 4 fed by the fused cell pass's decisions (k_core_cells_oct<true, true>; 2-D, W = 2R + 1
+// <= 5): one wave per queued point, whose cell's candidates are already split into whole accepts
+// (their count lo, exact for every point of the cell), rejects (no neighbour of any point of the
+// cell) and the partial ones (pmask).  So the point starts at cnt = lo and classifies ONLY the
+// partial candidates (lane l takes window positions l and l + 64 of the mask): no occupancy
+// words, no record loads or box tests of the decided candidates -- then the pair tests of the
+// candidates still partial for the point itself, early exit at min_samples, as k_core_slow.
+__device__ __forceinline__ int mask_pos_key(int pos, const Geom& g, int R, int W, uint32_t mg,
+                                            int cx, int cy, int cs) {
+  const int P = pos / 5, dx = pos - 5 * P;
+  const int k = min((int)(((uint32_t)P * mg) >> 16), 4);  // P / W
+  const int si = P - k * W;
+  const int s2 = cs + si - R;
+  const int y = cy + cw_row(k) - 2;
+  return (s2 * g.ny + y) * g.nx + (cx - 2 + dx);
+}
+__global__ __launch_bounds__(kBlock, 8) void k_core_slow_masked(
+    const float4* __restrict__ pts, Geom g, int R, const CellRec<2>* __restrict__ crec,
+    const int32_t* __restrict__ occ, const int32_t* __restrict__ slow,
+    const int32_t* __restrict__ slowq, const int32_t* __restrict__ n_slow,
+    const uint4* __restrict__ pmask, const int32_t* __restrict__ clo, uint8_t* __restrict__ core,
+    const int32_t* __restrict__ sorig, unsigned long long* __restrict__ cmin) {
+  const int lane = threadIdx.x & 63;
+  const int need = g.min_samples;
+  const int W = 2 * R + 1;
+  const uint32_t mg = (65535u + (uint32_t)W) / (uint32_t)W;
+  const XcdRange xr = xcd_items(*n_slow, true);
+  for (int64_t q = xr.first; q < xr.end; q += xr.step) {
+    const int s = slow[q];
+    const int32_t cq = slowq[q];
+    // all independent of each other: one round of memory latency
+    const float4 p = pts[s];
+    const int32_t key = occ[cq];
+    const uint4 m = pmask[cq];
+    int cnt = clo[cq];
+    int cx, cy, cz, cs;
+    g.split((uint32_t)key, cx, cy, cz, cs);
+    const uint32_t w0 = lane < 32 ? m.x : m.y;  // positions lane, lane + 64
+    const uint32_t w1 = lane < 32 ? m.z : m.w;
+    const bool h0 = (w0 >> (lane & 31)) & 1u, h1 = (w1 >> (lane & 31)) & 1u;
+    const int k0 = h0 ? mask_pos_key(lane, g, R, W, mg, cx, cy, cs) : key;
+    const int k1 = h1 ? mask_pos_key(lane + 64, g, R, W, mg, cx, cy, cs) : key;
+    const CellRec<2> c0 = crec[k0], c1 = crec[k1];  // (branch-free: the own record otherwise)
+    const int cl0 = h0 ? classify<2>(p, rec_boxA<2>(c0), rec_boxB(c0), g) : 0;
+    const int cl1 = h1 ? classify<2>(p, rec_boxA<2>(c1), rec_boxB(c1), g) : 0;
+    int add = (cl0 == 1 ? c0.e - c0.b : 0) + (cl1 == 1 ? c1.e - c1.b : 0);
+    int may = (cl0 == 2 ? c0.e - c0.b : 0) + (cl1 == 2 ? c1.e - c1.b : 0);
+    cnt += wave_sum(add);
+    if (cnt < need && cnt + wave_sum(may) >= need) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int cl = r ? cl1 : cl0;
+        const int bq = r ? c1.b : c0.b, eq = r ? c1.e : c0.e;
+        uint64_t pm = __ballot(cl == 2);
+        while (pm && cnt < need) {
+          const int l = __ffsll((unsigned long long)pm) - 1;
+          pm &= pm - 1;
+          const int bb = __shfl(bq, l), ee = __shfl(eq, l);
+          for (int j0 = bb; j0 < ee && cnt < need; j0 += 64) {
+            const int jj = j0 + lane;
+            const bool a = (jj < ee) && adjacent<2>(p, pts[jj], g);
+            cnt += __popcll(__ballot(a));
+          }
+        }
+      }
+    }
+    if (lane == 0) {
+      core[s] = (cnt >= need) ? 1 : 0;
+      if (cmin && cnt >= need)
         atomicMin(cmin + key, ((unsigned long long)(uint32_t)sorig[s] << 32) | (uint32_t)s);
     }
   }
@@ -4047,6 +4171,14 @@ struct DbscanState {
   }
   // the default K5 pipeline: the cell pass writes the point flags and the queue itself, with the
   // all-core cells' minima from k_cell_box (decided at build time, before k_cell_box runs)
+  int k5_mask_ = -1;  // 0: the slow pass re-classifies every window (k_core_slow); RPT_K5_MASK
+  bool k5_mask() {
+    if (k5_mask_ < 0) {
+      const char* e = ab_env("RPT_K5_MASK");
+      k5_mask_ = (e && std::atoi(e) == 0) ? 0 : 1;
+    }
+    return k5_mask_ == 1;
+  }
   bool k5_fused_path() {
     k5_env();
     return oct_ok() && k5_legacy && k5_fused && !k5_tiles;
@@ -4542,10 +4674,27 @@ int32_t DbscanState::core_pass(hipStream_t st) {
   auto* cm = oct ? reinterpret_cast<unsigned long long*>(cell_min_pair) : nullptr;
   if (k5_fused_path()) {
     RPT_HIP(hipMemsetAsync(n_slow, 0, sizeof(int32_t), st));
-    hipLaunchKernelGGL(k_core_cells_oct<true>, dim3((grid_for(8 * n, kBlock, 8192) + 7) & ~7),
-                       dim3(kBlock), 0, st, g, (int)rs, occ, n_occ, rec<2>(), mutual, occ_bits,
-                       slab_t, (int32_t*)nullptr, (int32_t*)nullptr, core, cm, slow, cq, n_slow);
-    if (g.rt >= 0 && (2 * g.rt + 1) * 25 <= 128)
+    // the cell pass's decisions handed to the slow pass when its window's 5 W (slab, row) pairs
+    // x 5 columns fit a 128-bit mask (W <= 5; pmask / clo per occupied cell in the dead radix
+    // buffers / cid, both rebuilt later)
+    const bool masked = (int)rs <= 2 && k5_mask();
+    uint4* k5m = reinterpret_cast<uint4*>(pmask);
+    if (masked) {
+      hipLaunchKernelGGL((k_core_cells_oct<true, true>),
+                         dim3((grid_for(8 * n, kBlock, 8192) + 7) & ~7), dim3(kBlock), 0, st, g,
+                         (int)rs, occ, n_occ, rec<2>(), mutual, occ_bits, slab_t,
+                         (int32_t*)nullptr, (int32_t*)nullptr, core, cm, slow, cq, n_slow, k5m,
+                         cid);
+      hipLaunchKernelGGL(k_core_slow_masked, dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, g,
+                         (int)rs, rec<2>(), occ, slow, cq, n_slow, k5m, cid, core, sorig, cm);
+    } else {
+      hipLaunchKernelGGL(k_core_cells_oct<true>, dim3((grid_for(8 * n, kBlock, 8192) + 7) & ~7),
+                         dim3(kBlock), 0, st, g, (int)rs, occ, n_occ, rec<2>(), mutual, occ_bits,
+                         slab_t, (int32_t*)nullptr, (int32_t*)nullptr, core, cm, slow, cq,
+                         n_slow);
+    }
+    if (masked) {
+    } else if (g.rt >= 0 && (2 * g.rt + 1) * 25 <= 128)
       hipLaunchKernelGGL((k_core_slow<2, 2>), dim3(wave_grid(n)), dim3(kBlock), 0, st, pts, skey,
                          g, rec<2>(), occ_bits, slab_t, slow, n_slow, core, sorig, cm, cq);
     else

@@ -485,9 +485,24 @@ class CommSequencer:
     steps submitted so far form a closed epoch and later submissions start a new one after it.
     A step that fails poisons the sequencer so the other lanes raise instead of waiting."""
 
-    def __init__(self, lanes: int, phases: int):
+    def __init__(self, lanes: int, phases: int, stagger: Optional[int] = None,
+                 offsets: Optional[Sequence[int]] = None):
+        """stagger / offsets: step s takes phase p at slot time s * stagger + offsets[p]
+        (default stagger ceil(phases / lanes), offsets 0, 1, ..., phases - 1).  Any
+        non-decreasing offsets give a valid order (the same on every rank); they only move where
+        the lanes wait."""
         self.L, self.P = int(lanes), int(phases)
-        self.d = max(1, -(-self.P // self.L))
+        self.d = max(1, -(-self.P // self.L)) if stagger is None else max(1, int(stagger))
+        self.off = list(range(self.P)) if offsets is None else [int(v) for v in offsets]
+        if len(self.off) != self.P or self.off[0] < 0 or \
+                any(b < a for a, b in zip(self.off, self.off[1:])):
+            raise ValueError("offsets: one non-decreasing slot time per phase")
+        # a lane runs its steps one after another: step s's last slot must come before step
+        # s + lanes' first (that step waits behind s on the same lane thread)
+        if self.off[-1] - self.off[0] >= self.L * self.d:
+            raise ValueError(f"offsets span {self.off[-1] - self.off[0]} >= lanes x stagger "
+                             f"({self.L} x {self.d}): a step would wait on a later step of its "
+                             f"own lane")
         self.cv = threading.Condition()
         self.failed: Optional[BaseException] = None
         # the open (last) epoch [first step, base time, closed (0/1)]; a step keeps a reference
@@ -512,6 +527,8 @@ class CommSequencer:
             self.next_phase[step] = 0
             self.n_reg = step + 1
             self.t_end = max(self.t_end, self._time(step, self.P - 1) + 1)
+            # (a later epoch starts after every slot of this one: its first step's phase 0 must
+            # not precede them)
             self.cv.notify_all()
 
     def close_group(self):
@@ -523,7 +540,7 @@ class CommSequencer:
 
     def _time(self, step: int, phase: int) -> int:
         e = self.epoch_of[step]
-        return e[1] + (step - e[0]) * self.d + phase
+        return e[1] + (step - e[0]) * self.d + self.off[phase]
 
     def _blocked(self, step: int, phase: int) -> bool:  # under self.cv
         key = (self._time(step, phase), step)
@@ -532,7 +549,7 @@ class CommSequencer:
                 return True
         e = self.epoch
         if e is not None and not e[2]:  # the open epoch's next (unsubmitted) step could come first
-            t = e[1] + (self.n_reg - e[0]) * self.d
+            t = e[1] + (self.n_reg - e[0]) * self.d + self.off[0]
             if (t, self.n_reg) < key:
                 return True
         return False
@@ -577,7 +594,7 @@ class CommSequencer:
     def order(self, steps: int) -> List[Tuple[int, int]]:
         """The (step, phase) slot order of `steps` steps submitted without a wait."""
         return sorted(((s, q) for s in range(steps) for q in range(self.P)),
-                      key=lambda a: (a[0] * self.d + a[1], a[0]))
+                      key=lambda a: (a[0] * self.d + self.off[a[1]], a[0]))
 
 
 class _StepSlots:
@@ -1049,7 +1066,11 @@ class ShardLanes:
         self.pipes = [NativeShardPipeline(comm, gains, rows, bins, params, timing=timing,
                                           async_host=async_host, host_workers=host_workers)
                       for _ in range(lanes)]
-        self.seq = CommSequencer(lanes, NativeShardPipeline.N_SLOTS)
+        st_env = os.environ.get("RPT_SEQ_STAGGER")
+        off_env = os.environ.get("RPT_SEQ_OFFSETS")
+        self.seq = CommSequencer(lanes, NativeShardPipeline.N_SLOTS,
+                                 stagger=int(st_env) if st_env else None,
+                                 offsets=[int(v) for v in off_env.split(",")] if off_env else None)
         self.streams = [torch.cuda.Stream(dev) for _ in range(lanes)] if lanes > 1 else [None]
         self.pools = [ThreadPoolExecutor(max_workers=1) for _ in range(lanes)]
         self._step = 0

@@ -214,9 +214,13 @@ def test_comm_sequencer_orders_lanes_deterministically():
 
     from rpt.dist import CommSequencer
 
-    for trial in range(5):
+    for trial in range(8):
         L, P, steps = 3, 6, 13
-        seq = CommSequencer(L, P)
+        # trials 4..7: other staggers / per-phase slot offsets (RPT_SEQ_STAGGER / _OFFSETS)
+        d_arg = None if trial < 4 else 2 + trial % 3
+        off = list(range(P)) if trial < 4 else sorted(random.Random(99 + trial).choices(
+            range(L * d_arg), k=P))
+        seq = CommSequencer(L, P, stagger=d_arg, offsets=None if trial < 4 else off)
         log, lock = [], threading.Lock()
         rng = random.Random(trial)
         skip = {(s, p) for s in range(steps) for p in range(P) if rng.random() < 0.3}
@@ -249,10 +253,10 @@ def test_comm_sequencer_orders_lanes_deterministically():
             f.result(timeout=30)
         # two epochs (the wait after step 4 closes the first): step s of an epoch starting at
         # step a with base time b takes phase p at time b + (s - a) * d + p, d = ceil(P / L)
-        d = -(-P // L)
-        base = {s: (0, 0) if s < 5 else (5, 4 * d + P) for s in range(steps)}
+        d = -(-P // L) if d_arg is None else d_arg
+        base = {s: (0, 0) if s < 5 else (5, 4 * d + off[P - 1] + 1) for s in range(steps)}
         exp = sorted(((s, p) for s in range(steps) for p in range(P) if (s, p) not in skip),
-                     key=lambda sp: (base[sp[0]][1] + (sp[0] - base[sp[0]][0]) * d + sp[1],
+                     key=lambda sp: (base[sp[0]][1] + (sp[0] - base[sp[0]][0]) * d + off[sp[1]],
                                      sp[0]))
         assert log == exp
 

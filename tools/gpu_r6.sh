@@ -84,6 +84,27 @@ for step in "$@"; do
         python tools/kstats.py "$(ls gpurun_out/kprof_cpw$c/*kernel_stats.csv | head -1)" 4 \
           | grep -i "union\|label<" | sed "s/^/cpw=$c /"
       done ;;
+    k5ab)         # K5 with the cell pass's masks (in-tree default) vs without (RPT_K5_MASK=0),
+                  # A/B build, one stack in flight, hipEvent K5 time; 3 workloads, ABBA
+      AB=radar-point-cloud-tracking_amd/rpt/librpt_ab.so
+      K5B="python bench.py --lanes 1 --steps 12 --warmup 3 --no-cpu-baseline --h2d-steps 0 --no-dense-k5 --no-one-stack"
+      for w in "1000" "125" "125 --dense"; do
+        for m in 1 0 0 1; do
+          RPT_LIB=$AB RPT_K5_MASK=$m run "k5m${m}_${w// /_}" 300 $K5B --total-frames $w || exit 1
+          python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('mask', sys.argv[2], sys.argv[3], 'K5 ms', d['roofline']['avg_ms'], 'step ms', d['ms_per_step'])" "$O/k5m${m}_${w// /_}.log" $m "$w"
+        done
+      done ;;
+    seqab)        # sharded 125-frame step, forced RCCL, 3 lanes: CommSequencer orders
+      for rep in 1 2; do
+        for v in "3:0,1,2,3,4,5,6,7" "4:0,1,2,6,7,8,9,10" "4:0,1,2,4,5,7,9,10" "3:0,1,2,4,5,6,7,8" "2:0,0,1,1,2,3,4,5"; do
+          tag=$(echo "$v" | tr ':,' '__')
+          RPT_COMM_FORCE_COLLECTIVES=1 RPT_SEQ_STAGGER=${v%%:*} RPT_SEQ_OFFSETS=${v#*:} \
+            run "seq_${tag}_$rep" 200 $BS --lanes 3 --steps 40 --warmup 6 || exit 1
+        done
+      done
+      for f in $O/seq_*.log; do
+        python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['ms_per_step'], d['steady_state']['ms_per_step'], d['slot_wait']['ms_per_step_by_phase'])" $f
+      done ;;
     tests_dist)
       run tests_dist 1000 $PYT --timeout 990 tests/test_dist_gpu.py tests/test_ab_variants_gpu.py \
         || exit 1 ;;
