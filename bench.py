@@ -156,6 +156,71 @@ def _traffic(name):
     return None, None
 
 
+def _pmc_stack_bytes(wkey):
+    """PMC-measured HBM bytes of ALL kernels of one stack (committed tools/pmc.sh summary,
+    one stack in flight; the synthetic echo generator excluded): per kernel bytes per launch x
+    launches, over the runs of the profiled command (launches of the K1 count pass)."""
+    import csv
+
+    for rd in ("r6", "r5", "r4"):
+        f = ROOT / "profiles" / rd / f"pmc_traffic_by_kernel_{wkey}.csv"
+        if not f.exists():
+            continue
+        rows = list(csv.DictReader(f.open()))
+        runs = sum(int(r["launches"]) for r in rows if "k_group_count_u8" in r["kernel"])
+        if runs <= 0:
+            continue
+        tot = sum(float(r["hbm_bytes_per_launch_corrected"]) * int(r["launches"])
+                  for r in rows if "k_synth" not in r["kernel"])
+        return tot / runs, str(f.relative_to(ROOT))
+    return None, None
+
+
+def _e2e_roof(echo_bytes_step: float, ms_step: float, world: int, wkey: str):
+    """End-to-end rate of the bench line against the HBM roofline of the GPUs used
+    (Mpoints/s also as a fraction of the HBM roofline): the u8 echo every step must
+    read, and (N = 1) the PMC-measured bytes all kernels of one stack move, each / ms_per_step."""
+    peak = HBM_PEAK_GBS * world
+    t = ms_step * 1e-3
+    out = {"bound": "hbm", "peak": peak, "unit": "GB/s", "ms_per_step": round(ms_step, 4),
+           "echo_bytes_per_step": int(echo_bytes_step),
+           "achieved_echo": round(echo_bytes_step / t / 1e9, 2),
+           "frac_echo": round(echo_bytes_step / t / 1e9 / peak, 4),
+           "note": "frac_echo: the compulsory echo read of every step (u8, 1 B per sample of all "
+                   "ranks) over the driver's step time; frac_pmc: every kernel's PMC-measured HBM "
+                   "bytes of one stack (tools/pmc.sh, FETCH x2 + WRITE) over the same time"}
+    b, src = (None, None) if world > 1 else _pmc_stack_bytes(wkey)
+    if b is not None:
+        out.update(pmc_bytes_per_stack=int(b), pmc_source=src,
+                   achieved_pmc=round(b / t / 1e9, 2), frac_pmc=round(b / t / 1e9 / peak, 4))
+    return out
+
+
+def best_cpu(echo_host: np.ndarray, cfg, geo):
+    """The oracle's fastest host path on every core this process may use (labelled, not the
+    reference): numpy polar scatter + fusion, land filter, the OpenMP union-find ST-DBSCAN
+    (oracle/stdbscan_oracle.c) and the tracker, over the first frames of the same stack.
+    Returns (points, frames, seconds)."""
+    import oracle
+    from oracle import path as op
+
+    t0 = time.perf_counter()
+    frames = _oracle_frames(echo_host, cfg, geo)
+    npts = sum(len(p) for _, p, _ in frames)
+    op.run_path(frames, dbscan=oracle.stdbscan_uf)
+    return npts, len(frames), time.perf_counter() - t0
+
+
+def _oracle_frames(echo_host, cfg, geo):
+    from oracle import path as op
+
+    F, G, R, B = echo_host.shape
+    per_frame = [{gain: op.polar_scatter(echo_host[f, k], np.full(R, cfg.scale, np.float32),
+                                         geo.cos_t, geo.sin_t)
+                  for k, gain in enumerate(cfg.gains)} for f in range(F)]
+    return op.build_frames(per_frame)
+
+
 def _k5_roof(n_points: float, k5_ms: float, traffic, tsrc):
     """K5's roofline fields.  The algorithmic bytes are SURVEY 8(d)'s 17 B/pt compulsory model;
     where the PMC-measured HBM bytes of the same workload are BELOW the model (K5 decides whole
@@ -231,6 +296,9 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=1,
                     help="frames of the stack the CPU baseline runs (reference structure)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--best-cpu-frames", type=int, default=12,
+                    help="frames of the all-cores OpenMP oracle line (cpu_baseline.best_cpu; "
+                         "0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="skip per-stage hipEvent timing")
     ap.add_argument("--no-dense-k5", action="store_true",
                     help="skip the K5 roofline legs at the 8-GPU per-GPU shares")
@@ -565,6 +633,9 @@ def main():
                 "measured_in": "one-stack-in-flight leg" if seq is not None else "timed steps",
                 **_k5_roof(n_in, k5_ms, traffic, tsrc), "runs": len(k5)}
     stage = {k: round(v / args.steps, 3) for k, v in stage_acc.items()}
+    e0 = echoes[0]
+    roof_e2e = _e2e_roof(float(e0.numel() * e0.element_size()) * world, ms_step, world,
+                         f"{'dense' if args.dense else 'std'}_{F}f")
     # the largest stage, K1 (count + scan + write): echo read once + 16 B per emitted point
     # (x, y, intensity, frame slot; no per-point gain without keep_points) + 12 B of row geometry
     # per row, over its event time
@@ -624,6 +695,18 @@ def main():
                                  "what": "oracle/ grid-indexed C BFS (not the reference's "
                                          "structure), 1 thread"},
                "reference_measured": _reference_measured()}
+        if args.best_cpu_frames > 0:
+            bf = min(args.best_cpu_frames, F)
+            bp, bfr, bdt = best_cpu(echoes[0][:bf].cpu().numpy(), cfg, ds.geo)
+            cpu["best_cpu"] = {
+                "value": round(bp / bdt / 1e6, 5), "unit": "Mpoints/s",
+                "cores": int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1),
+                "kind": "port",
+                "sample": f"first {bfr} frames of the same stack ({bp} points), {bdt:.1f} s",
+                "what": "oracle's OpenMP union-find ST-DBSCAN (oracle/stdbscan_oracle.c) + numpy "
+                        "polar scatter / land filter + oracle tracker on all cores the process "
+                        "may use (OMP_NUM_THREADS): the fastest CPU path here, not the "
+                        "reference's structure"}
     if rank == 0:
         what = "dense (configs[4] density, ~500k pts/frame)" if args.dense else \
             "3-gain fused"
@@ -659,6 +742,7 @@ def main():
             "one_stack_in_flight": seq,
             "roofline": roof, "roofline_c4_share": roof_c4, "roofline_configs4_share": roof_c4d,
             "roofline_k1": roof_k1,
+            "roofline_e2e": roof_e2e,
             "cpu_baseline": cpu,
             "h2d_inclusive": h2d, "stage_ms": stage,
             "stage_ms_from": "one_stack_in_flight" if seq is not None else "timed steps",

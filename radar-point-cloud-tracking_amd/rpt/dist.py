@@ -61,10 +61,14 @@ class Comm:
     def _c(self, t: torch.Tensor) -> torch.Tensor:
         return t.to(self.cdev).contiguous()
 
-    def all_reduce(self, t: torch.Tensor, op) -> torch.Tensor:
+    def all_reduce(self, t: torch.Tensor, op, inplace: bool = False) -> torch.Tensor:
+        """inplace: reduce t itself when it already lives on the backend's device (no copy;
+        the caller gives up its values)."""
         if self.solo:
             return t
-        c = self._c(t).clone()
+        c = self._c(t)
+        if not (inplace and c.data_ptr() == t.data_ptr()):
+            c = c.clone()
         dist.all_reduce(c, op=op, group=self.group)
         return c.to(t.device)
 
@@ -76,6 +80,17 @@ class Comm:
         out = torch.empty(self.world * c.numel(), dtype=c.dtype, device=self.cdev)
         dist.all_gather_into_tensor(out, c, group=self.group)
         return out.cpu().reshape(self.world, -1)
+
+    def all_gather_fixed_issue(self, t: torch.Tensor) -> torch.Tensor:
+        """all_gather_fixed without the wait: the gathered [world][len] tensor on the backend's
+        device (RCCL: in stream order); the caller's .cpu() waits.  Several stacks in flight
+        issue the collective inside their sequencer slot and wait outside it."""
+        if self.solo:
+            return t.reshape(1, -1)
+        c = self._c(t).reshape(-1)
+        out = torch.empty(self.world * c.numel(), dtype=c.dtype, device=self.cdev)
+        dist.all_gather_into_tensor(out, c, group=self.group)
+        return out.reshape(self.world, -1)
 
     def all_gather_dev(self, t: torch.Tensor) -> torch.Tensor:
         """all_gather of a 1-D tensor of the same length on every rank -> [world * len] on the
@@ -250,6 +265,7 @@ class ShardResult:
     stage_ms: Dict[str, float] = field(default_factory=dict)
     t_done: float = 0.0                         # perf_counter when the device part ended
     _pending: Optional[Future] = None
+    lane: int = -1                              # ShardLanes: the lane that ran the step
 
     def finish(self) -> "ShardResult":
         """Wait for rank 0's host stage when it runs asynchronously (async_host=True)."""
@@ -750,10 +766,12 @@ class NativeShardPipeline:
                                 cos_d.data_ptr(), sin_d.data_ptr(), None,  # no per-point gains
                                 C_.byref(info), st), "rpt_shard_polar")
         n_points = int(info.n_points)
+        # issued inside the slot, waited for outside it: the other lanes' collectives go on
         with slots.slot(0):
-            allinfo = comm.all_gather_fixed(torch.tensor(
+            allinfo = comm.all_gather_fixed_issue(torch.tensor(
                 [n_points, info.n_built, *[float(b) for b in info.bounds], info.n_head_k1,
-                 info.n_tail_k1], dtype=torch.float64)).numpy()
+                 info.n_tail_k1], dtype=torch.float64))
+        allinfo = allinfo.cpu().numpy()
         n_global = int(allinfo[:, 0].sum())
         n_built = int(allinfo[:, 1].sum())
         mark("polar")
@@ -770,7 +788,7 @@ class NativeShardPipeline:
             chk(lib.rpt_shard_land_grid(self.h, gbp, grid.data_ptr(), cells, st),
                 "rpt_shard_land_grid")
             with slots.slot(1):
-                grid = comm.all_reduce(grid, _SUM)
+                grid = comm.all_reduce(grid, _SUM, inplace=True)
         # 3. mask + compaction; the own edge frames for the neighbours (capacities: K1 counts)
         hf = int(info.halo_frames)
         halo = W > 1 and hf > 0
@@ -1053,10 +1071,15 @@ class ShardLanes:
     def __init__(self, dev: torch.device, lanes: int, gains: Sequence[int], rows: int,
                  bins: int, params: PathParams = None, timing: bool = False,
                  async_host: bool = False, host_workers: int = 2,
-                 sequenced: Optional[bool] = None):
+                 sequenced: Optional[bool] = None, free_lanes: bool = True,
+                 keep_labels: bool = False):
         """sequenced: order the lanes' collective slots (default: with more than one rank; at
         one rank every collective is the identity -- True keeps the ordering anyway, to measure
-        what it costs)."""
+        what it costs).  free_lanes: a step runs on whichever lane is free when its turn comes
+        (steps still start in submission order, and the collective order depends only on the
+        step numbers); False: step k on lane k % lanes.  keep_labels: each result also carries
+        the global labels of this rank's points (result.labels_local, read on the lane before
+        the lane takes its next step; for checks)."""
         if lanes < 1:
             raise ValueError("lanes must be >= 1")
         self.dev = dev
@@ -1072,7 +1095,19 @@ class ShardLanes:
                                  stagger=int(st_env) if st_env else None,
                                  offsets=[int(v) for v in off_env.split(",")] if off_env else None)
         self.streams = [torch.cuda.Stream(dev) for _ in range(lanes)] if lanes > 1 else [None]
-        self.pools = [ThreadPoolExecutor(max_workers=1) for _ in range(lanes)]
+        self.free_lanes = bool(free_lanes)
+        self.keep_labels = bool(keep_labels)
+        if self.free_lanes:
+            import queue
+
+            # one pool of `lanes` workers takes the steps in submission order; each takes a free
+            # lane (pipeline + stream) for its step
+            self.pools = [ThreadPoolExecutor(max_workers=lanes)]
+            self._free = queue.SimpleQueue()
+            for i in range(lanes):
+                self._free.put(i)
+        else:
+            self.pools = [ThreadPoolExecutor(max_workers=1) for _ in range(lanes)]
         self._step = 0
 
     def set_geometry(self, scale, cos_t, sin_t, n_files: int):
@@ -1086,33 +1121,50 @@ class ShardLanes:
         (concurrent.futures.wait, as_completed) calls flush() first."""
         step = self._step
         self._step += 1
-        li = step % len(self.pipes)
-        pipe, s = self.pipes[li], self.streams[li]
         # one rank: every collective is the identity, nothing to order (and nothing registered:
         # an unsequenced step never releases its sequencer entries)
         if self.sequenced:
             self.seq.register(step)
         slots = self.seq.step(step) if self.sequenced else _NoSlots()
         fut = ShardStepFuture(self.seq)
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(self.dev))  # the echo's producer
 
-        def work():
+        def work(li):
+            pipe, s = self.pipes[li], self.streams[li]
+            with torch.cuda.device(self.dev):
+                if s is None:
+                    r = pipe.run(echo, frame0, slots)
+                    lab = pipe.labels_local() if self.keep_labels else None
+                else:
+                    s.wait_event(ready)  # the echo is ready
+                    with torch.cuda.stream(s):
+                        r = pipe.run(echo, frame0, slots)
+                        lab = pipe.labels_local() if self.keep_labels else None
+            r.lane = li
+            if lab is not None:
+                r.labels_local = lab
+            return r
+
+        def task(li=None):
             if not fut.set_running_or_notify_cancel():
                 return
+            lane = self._free.get() if li is None else li
             try:
-                with torch.cuda.device(self.dev):
-                    if s is None:
-                        r = pipe.run(echo, frame0, slots)
-                    else:
-                        s.wait_stream(torch.cuda.default_stream(self.dev))  # the echo is ready
-                        with torch.cuda.stream(s):
-                            r = pipe.run(echo, frame0, slots)
+                r = work(lane)
             except BaseException as e:
                 self.seq.abort(e)
                 fut.set_exception(e)
                 return
+            finally:
+                if li is None:
+                    self._free.put(lane)
             fut.set_result(r)
 
-        self.pools[li].submit(work)
+        if self.free_lanes:
+            self.pools[0].submit(task)
+        else:
+            self.pools[step % len(self.pipes)].submit(task, step % len(self.pipes))
         return fut
 
     def flush(self):

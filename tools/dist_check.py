@@ -94,7 +94,8 @@ def main():
     if args.impl == "native" and args.lanes > 1:
         from rpt.dist import ShardLanes
 
-        lanes = ShardLanes(dev, args.lanes, cfg.gains, cfg.rows, cfg.bins, PathParams())
+        lanes = ShardLanes(dev, args.lanes, cfg.gains, cfg.rows, cfg.bins, PathParams(),
+                           keep_labels=True)
         lanes.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t,
                            ds.geo.sin_t, F * 3)
         if args.force_host_merge:
@@ -103,8 +104,8 @@ def main():
         futs = [lanes.submit(echo, rank * F) for _ in range(2 * args.lanes)]
         outs = [f.result().finish() for f in futs]
         torch.cuda.synchronize(dev)
-        for k, r in enumerate(outs[-args.lanes:]):  # the last run of every lane
-            runs.append((r, lanes.pipes[(len(outs) - args.lanes + k) % args.lanes].labels_local()))
+        for r in outs[-args.lanes:]:  # the last `lanes` steps (whichever lanes ran them)
+            runs.append((r, r.labels_local))
         lanes.close()
     elif args.impl == "native":
         pipe = NativeShardPipeline(Comm(dev), cfg.gains, cfg.rows, cfg.bins, PathParams())
@@ -152,8 +153,9 @@ def run_digest(args, rank, world, dev):
     echoes = {n: dss[n].echo() for n in names}
     torch.cuda.synchronize(dev)
     c0 = dss[names[0]].cfg
+    # (fixed lanes: the checks below read each lane's last run from its pipeline)
     lanes = ShardLanes(dev, args.lanes, c0.gains, c0.rows, c0.bins, PathParams(),
-                       async_host=True)
+                       async_host=True, free_lanes=False)
     lanes.set_geometry(np.full(c0.rows, c0.scale, np.float32), dss[names[0]].geo.cos_t,
                        dss[names[0]].geo.sin_t, F * len(c0.gains))
     # run k goes to lane k % lanes; each lane alternates the workloads over its runs, so every

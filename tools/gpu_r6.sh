@@ -89,10 +89,14 @@ for step in "$@"; do
       AB=radar-point-cloud-tracking_amd/rpt/librpt_ab.so
       K5B="python bench.py --lanes 1 --steps 12 --warmup 3 --no-cpu-baseline --h2d-steps 0 --no-dense-k5 --no-one-stack"
       for w in "1000" "125" "125 --dense"; do
+        i=0
         for m in 1 0 0 1; do
-          RPT_LIB=$AB RPT_K5_MASK=$m run "k5m${m}_${w// /_}" 300 $K5B --total-frames $w || exit 1
-          python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('mask', sys.argv[2], sys.argv[3], 'K5 ms', d['roofline']['avg_ms'], 'step ms', d['ms_per_step'])" "$O/k5m${m}_${w// /_}.log" $m "$w"
+          i=$((i + 1))
+          RPT_LIB=$AB RPT_K5_MASK=$m run "k5m${m}_${w// /_}_$i" 300 $K5B --total-frames $w || exit 1
         done
+      done
+      for f in $O/k5m*.log; do
+        python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], 'K5 ms', d['roofline']['avg_ms'], 'step ms', d['ms_per_step'])" $f
       done ;;
     seqab)        # sharded 125-frame step, forced RCCL, 3 lanes: CommSequencer orders
       for rep in 1 2; do
@@ -103,6 +107,18 @@ for step in "$@"; do
         done
       done
       for f in $O/seq_*.log; do
+        python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['ms_per_step'], d['steady_state']['ms_per_step'], d['slot_wait']['ms_per_step_by_phase'])" $f
+      done ;;
+    seqab2)       # sharded 125-frame step, forced RCCL: lanes x CommSequencer orders (SEQV)
+      for rep in 1 2; do
+        for v in ${SEQV:-"3:2:0,0,1,1,2,3,4,5" "4:2:0,0,1,1,2,3,4,5" "5:2:0,0,1,1,2,3,4,5" "3:4:0,1,2,2,3,3,4,5" "4:3:0,1,2,4,5,6,7,8" "5:2:0,1,2,3,4,5,6,7"}; do
+          IFS=: read -r L D OFF <<< "$v"
+          tag="${SEQTAG}L${L}_d${D}_$(echo "$OFF" | tr ',' '_')"
+          RPT_COMM_FORCE_COLLECTIVES=1 RPT_SEQ_STAGGER=$D RPT_SEQ_OFFSETS=$OFF \
+            run "sq_${tag}_$rep" 200 $BS --lanes $L --steps 40 --warmup 6 || exit 1
+        done
+      done
+      for f in $O/sq_*.log; do
         python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['ms_per_step'], d['steady_state']['ms_per_step'], d['slot_wait']['ms_per_step_by_phase'])" $f
       done ;;
     tests_dist)
