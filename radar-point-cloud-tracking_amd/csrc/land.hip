@@ -420,7 +420,7 @@ __global__ __launch_bounds__(kCompBlock) void k_land_compact(
     const int32_t* __restrict__ cell, const uint8_t* __restrict__ land,
     const int32_t* __restrict__ tile_base, float* __restrict__ xo, float* __restrict__ yo,
     float* __restrict__ vo, int32_t* __restrict__ go, int32_t* __restrict__ pfo,
-    float* __restrict__ to, BoundsPart* __restrict__ part) {
+    float* __restrict__ to, BoundsPart* __restrict__ part, int64_t t_base) {
   constexpr int NW = kCompBlock / 64;
   const int lane = threadIdx.x & 63, w = threadIdx.x / 64;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -494,7 +494,7 @@ __global__ __launch_bounds__(kCompBlock) void k_land_compact(
         vo[o] = vb[u];
         if (go) go[o] = gb[u];
         pfo[o] = f;
-        to[o] = (float)f;
+        to[o] = (float)(t_base + (int64_t)f);  // (t_base: the shard driver's first frame)
         if (!isfinite(px) || !isfinite(py)) flags |= 1;
         const uint32_t a = f2ord(px), b = f2ord(py);
         mnx = min(mnx, a);
@@ -570,7 +570,7 @@ __global__ void k_land_new_off(const int32_t* __restrict__ n_kept_dev,
 constexpr int kFinBlock = 1024;
 __global__ __launch_bounds__(kFinBlock) void k_land_compact_final(
     const BoundsPart* __restrict__ part, int nt, const int32_t* __restrict__ n_kept_dev,
-    Bounds* __restrict__ out) {
+    Bounds* __restrict__ out, int64_t t_base) {
   const int64_t nk = *n_kept_dev;
   uint32_t mnx = 0xffffffffu, mxx = 0u, mny = 0xffffffffu, mxy = 0u;
   int mnf = INT_MAX, mxf = INT_MIN, flags = 0;
@@ -623,10 +623,11 @@ __global__ __launch_bounds__(kFinBlock) void k_land_compact_final(
     b.mx[1] = r.mxy;
     b.mn[2] = any ? z : 0xffffffffu;
     b.mx[2] = any ? z : 0u;
-    b.mn[3] = any ? f2ord((float)r.mnf) : 0xffffffffu;
-    b.mx[3] = any ? f2ord((float)r.mxf) : 0u;
+    const int64_t t0 = t_base + r.mnf, t1 = t_base + r.mxf;
+    b.mn[3] = any ? f2ord((float)t0) : 0xffffffffu;
+    b.mx[3] = any ? f2ord((float)t1) : 0u;
     b.nonfinite_xyz = (r.flags & 1) ? 1 : 0;
-    b.nonintegral_t = (any && (r.mxf >= 16777216 || r.mnf <= -16777216)) ? 1 : 0;
+    b.nonintegral_t = (any && (t1 >= 16777216 || t0 <= -16777216)) ? 1 : 0;
     b.n_finite_t = (int32_t)nk;
     b.t_descends = (r.flags & 2) ? 1 : 0;
     *out = b;
@@ -825,7 +826,7 @@ int32_t land_compact_dev(const float* x, const float* y, const float* v, const i
                          const int32_t* pf, int64_t n, const int32_t* cell, const uint8_t* land,
                          int32_t n_frames, float* xo, float* yo, float* vo, int32_t* go,
                          int32_t* pfo, float* to, int64_t* new_off, Bounds* bounds_out,
-                         hipStream_t st) {
+                         hipStream_t st, int64_t t_base) {
   if (n < 0 || n >= (int64_t(1) << 31) - 1 || n_frames < 0) {
     set_error("land_compact_dev: bad sizes");
     return RPT_EINVAL;
@@ -845,11 +846,11 @@ int32_t land_compact_dev(const float* x, const float* y, const float* v, const i
   RPT_CHECK_LAUNCH();
   RPT_TRY(exclusive_scan_total_i32(cnt, base, nt, st));
   hipLaunchKernelGGL(k_land_compact, dim3((unsigned)nt), dim3(kCompBlock), 0, st, x, y, v, g, pf,
-                     n, cell, land, base, xo, yo, vo, go, pfo, to, part);
+                     n, cell, land, base, xo, yo, vo, go, pfo, to, part, t_base);
   hipLaunchKernelGGL(k_land_new_off, dim3((n_frames + 1 + 3) / 4), dim3(256), 0, st, base + nt,
                      pfo, n_frames, new_off);
   hipLaunchKernelGGL(k_land_compact_final, dim3(1), dim3(kFinBlock), 0, st, part, (int)nt,
-                     base + nt, bounds_out);
+                     base + nt, bounds_out, t_base);
   RPT_CHECK_LAUNCH();
   return RPT_OK;
 }

@@ -37,6 +37,14 @@ int32_t dbscan_build_given(DbscanState* S, const float* x, const float* y, const
 int32_t dbscan_labels_global_dev(DbscanState* S, const int64_t* rep, const int64_t* reps,
                                  const int64_t* nr_dev, int32_t* labels, hipStream_t st);
 int32_t dbscan_core_orig(DbscanState* S, uint8_t* out, hipStream_t st);
+int32_t dbscan_components_edges(DbscanState* S, int32_t* comp_out, int64_t lo_end,
+                                int64_t hi_begin, hipStream_t st);
+void dbscan_uf_arrays(const DbscanState* S, const uint8_t** core, const int32_t** parent,
+                      const int32_t** sorig, int64_t* n);
+int32_t dbscan_core_edges(DbscanState* S, int64_t a0, int64_t a1, uint8_t* out_a, int64_t b0,
+                          int64_t b1, uint8_t* out_b, hipStream_t st);
+int32_t dbscan_set_core_edges(DbscanState* S, const uint8_t* in_a, int64_t a1,
+                              const uint8_t* in_b, int64_t b0, hipStream_t st);
 
 namespace {
 
@@ -502,16 +510,15 @@ __device__ __forceinline__ int64_t lookup(const int64_t* __restrict__ keys,
   return (lo < m && keys[lo] == v) ? vals[lo] : v;
 }
 
-// rep[i] = the global representative (class minimum id) of window point i's component, -1 for
-// non-core; flags of the representative list: the merge table's class minima below the window
-// (external representatives) and the window points that are their own representative -- one bit
-// per list entry k < keys_cap + n (a wave per 64 entries: its two words and their popcounts), so
-// the list's order comes from a scan over n / 32 words instead of one over every entry
-__global__ void k_reps(const int32_t* __restrict__ comp, int64_t n, WinIds w,
-                       const int64_t* __restrict__ keys, const int64_t* __restrict__ vals,
-                       const int64_t* __restrict__ meta, int64_t keys_cap,
-                       int64_t* __restrict__ rep, uint32_t* __restrict__ bits,
-                       int32_t* __restrict__ wcnt) {
+// Flags of the representative list, one bit per entry k < keys_cap + n: the merge table's class
+// minima below the window (external representatives) here -- a wave per 64 entries writes their
+// two words and popcounts, which also clears the window part of both -- and the window points
+// that are their own representative by k_root_reps after it.  The list's order comes from a
+// scan over the (keys_cap + n) / 32 word counts.
+__global__ void k_reps_keys(int64_t n, WinIds w, const int64_t* __restrict__ keys,
+                            const int64_t* __restrict__ vals, const int64_t* __restrict__ meta,
+                            int64_t keys_cap, uint32_t* __restrict__ bits,
+                            int32_t* __restrict__ wcnt) {
   const int64_t m = meta[0] > 0 ? meta[0] : 0;
   const int64_t wstart = w.gid(0);
   const int lane = threadIdx.x & 63;
@@ -519,22 +526,42 @@ __global__ void k_reps(const int32_t* __restrict__ comp, int64_t n, WinIds w,
   for (int64_t c0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 64; c0 < total;
        c0 += (int64_t)gridDim.x * blockDim.x) {
     const int64_t k = c0 + lane;
-    bool f = false;
-    if (k < keys_cap) {
-      f = k < m && keys[k] == vals[k] && keys[k] < wstart;
-    } else if (k < total) {
-      const int64_t i = k - keys_cap;
-      const int32_t c = comp[i];
-      int64_t r = -1;
-      if (c >= 0) r = lookup(keys, vals, m, w.gid(c));
-      rep[i] = r;
-      f = c >= 0 && r == w.gid(i);
-    }
+    const bool f = k < keys_cap && k < m && keys[k] == vals[k] && keys[k] < wstart;
     const uint64_t b = __ballot(f);
     if (lane < 2) {
       const uint32_t word = (uint32_t)(b >> (32 * lane));
       bits[(c0 >> 5) + lane] = word;
       wcnt[(c0 >> 5) + lane] = __popc(word);
+    }
+  }
+}
+
+// Per ROOT of the window's core components (a core point s with parent[s] == s; its window
+// index i = sorig[s] is the component's id, its minimum original index): rep[i] = the global
+// representative (the merge table's class minimum of gid(i), else gid(i) itself) -- the only
+// entries of rep the global label pass reads -- and, when the root is its own representative,
+// its list flag (after k_reps_keys).  Components are few: the atomics are rare.  Replaces a
+// representative per window point (which needed every point's component id).
+__global__ void k_root_reps(const uint8_t* __restrict__ core, const int32_t* __restrict__ parent,
+                            const int32_t* __restrict__ sorig, int64_t n, WinIds w,
+                            const int64_t* __restrict__ keys, const int64_t* __restrict__ vals,
+                            const int64_t* __restrict__ meta, int64_t keys_cap,
+                            int64_t* __restrict__ rep, uint32_t* __restrict__ bits,
+                            int32_t* __restrict__ wcnt) {
+  const int64_t m = meta[0] > 0 ? meta[0] : 0;
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t c = core[s];  // (both loads issued together)
+    const int32_t p = parent[s];
+    if (!c || p != (int32_t)s) continue;
+    const int32_t i = sorig[s];
+    const int64_t g = w.gid(i);
+    const int64_t r = lookup(keys, vals, m, g);
+    rep[i] = r;
+    if (r == g) {
+      const int64_t k = keys_cap + i;
+      atomicOr(&bits[k >> 5], 1u << (k & 31));
+      atomicAdd(&wcnt[k >> 5], 1);
     }
   }
 }
@@ -629,7 +656,8 @@ struct rpt_shard {
   rpt::DbscanState* db = nullptr;
   DevBuf<uint32_t> bnd;          // xy bounds (ordered u32)
   DevBuf<float> X, Y, T;         // the window
-  DevBuf<uint8_t> core;          // core flags of the window (original order)
+  // core flags of the window in original order: filled on demand by rpt_shard_points (checks)
+  mutable DevBuf<uint8_t> core;
   DevBuf<int32_t> comp, labels, flag;
   DevBuf<int64_t> rep, reps, keys, vals, pos, cnt64, meta;
   DevBuf<unsigned long long> pset;  // distinct-pair hash set
@@ -981,17 +1009,13 @@ int32_t rpt_shard_window(rpt_shard* h, const int32_t* recv_prev, int64_t cap_pre
     }
     RPT_HIP(hipEventRecord(h->ev[0], st));
   }
-  RPT_TRY(h->core.ensure((size_t)n, st));
-  RPT_TRY(dbscan_core(h->db, h->core.p, st));
+  RPT_TRY(dbscan_core(h->db, nullptr, st));  // (flags stay in sorted order)
   if (h->p.timing) RPT_HIP(hipEventRecord(h->ev[1], st));
   h->core_timed = h->p.timing != 0;
-  // the own edge points' flags for the neighbours (their halo)
-  if (flags_prev && hm.n_head > 0)
-    RPT_HIP(hipMemcpyAsync(flags_prev, h->core.p + hm.n_prev, (size_t)hm.n_head,
-                           hipMemcpyDeviceToDevice, st));
-  if (flags_next && hm.n_tail > 0)
-    RPT_HIP(hipMemcpyAsync(flags_next, h->core.p + hm.n_prev + hm.n_own - hm.n_tail,
-                           (size_t)hm.n_tail, hipMemcpyDeviceToDevice, st));
+  // the own edge points' flags for the neighbours (their halo), straight into the send buffers
+  RPT_TRY(dbscan_core_edges(h->db, hm.n_prev, hm.n_prev + hm.n_head, flags_prev,
+                            hm.n_prev + hm.n_own - hm.n_tail, hm.n_prev + hm.n_own, flags_next,
+                            st));
   return RPT_OK;
 }
 
@@ -1016,14 +1040,15 @@ int32_t rpt_shard_link(rpt_shard* h, const uint8_t* flags_prev, const uint8_t* f
   if (n <= 0) return RPT_OK;
   const rpt_shard_info& I = h->info;
   // halo points take their owners' flags (the owners see all their neighbours)
-  if (I.n_prev > 0)
-    RPT_HIP(hipMemcpyAsync(h->core.p, flags_prev, (size_t)I.n_prev, hipMemcpyDeviceToDevice, st));
-  if (I.n_next > 0)
-    RPT_HIP(hipMemcpyAsync(h->core.p + I.n_prev + I.n_kept, flags_next, (size_t)I.n_next,
-                           hipMemcpyDeviceToDevice, st));
   RPT_TRY(h->comp.ensure((size_t)n, st));
-  if (I.n_prev > 0 || I.n_next > 0) RPT_TRY(dbscan_set_core(h->db, h->core.p, st));
-  RPT_TRY(dbscan_components(h->db, h->comp.p, st));
+  RPT_TRY(dbscan_set_core_edges(h->db, I.n_prev > 0 ? flags_prev : nullptr, I.n_prev,
+                                I.n_next > 0 ? flags_next : nullptr, I.n_prev + I.n_kept, st));
+  // component ids only where they are read: the halo points (k_pairs) and the own edge points
+  // sent to the neighbours (k_comp_send); the labels take each root's representative directly
+  // (k_root_reps)
+  const int64_t lo_end = I.n_prev + (comp_prev ? I.n_head : 0);
+  const int64_t hi_begin = I.n_prev + I.n_kept - (comp_next ? I.n_tail : 0);
+  RPT_TRY(dbscan_components_edges(h->db, h->comp.p, lo_end, hi_begin, st));
   if ((comp_prev && I.n_head > 0) || (comp_next && I.n_tail > 0)) {
     hipLaunchKernelGGL(k_comp_send,
                        dim3(grid_for(std::max<int64_t>(std::max(I.n_head, I.n_tail), 1), 256, 1024)),
@@ -1117,9 +1142,15 @@ int32_t rpt_shard_finish(rpt_shard* h, const int64_t* gathered_pairs, int32_t wo
   uint32_t* rbits = reinterpret_cast<uint32_t*>(h->flag.p);
   int32_t* rcnt = h->flag.p + nw;
   if (n > 0) {
-    hipLaunchKernelGGL(k_reps, dim3(grid_for(keys_cap + n, 256, 4096)), dim3(256), 0, st,
-                       h->comp.p, n, w, h->keys.p, h->vals.p, h->meta.p, keys_cap, h->rep.p,
-                       rbits, rcnt);
+    hipLaunchKernelGGL(k_reps_keys, dim3(grid_for(keys_cap + n, 256, 4096)), dim3(256), 0, st, n,
+                       w, h->keys.p, h->vals.p, h->meta.p, keys_cap, rbits, rcnt);
+    const uint8_t* dcore;
+    const int32_t *dpar, *dsorig;
+    int64_t dn = 0;
+    dbscan_uf_arrays(h->db, &dcore, &dpar, &dsorig, &dn);
+    hipLaunchKernelGGL(k_root_reps, dim3(grid_for(dn, 256, 4096)), dim3(256), 0, st, dcore, dpar,
+                       dsorig, dn, w, h->keys.p, h->vals.p, h->meta.p, keys_cap, h->rep.p, rbits,
+                       rcnt);
     RPT_CHECK_LAUNCH();
     RPT_TRY(exclusive_scan_total_i32_to_i64(rcnt, h->pos.p, nw, st));
     hipLaunchKernelGGL(k_reps_write, dim3(grid_for(keys_cap + n, 256, 4096)), dim3(256), 0, st,
@@ -1214,11 +1245,15 @@ int32_t rpt_shard_points(const rpt_shard* h, float* x, float* y, float* intensit
   const int64_t K = h->info.n_kept;
   if (K == 0) return RPT_OK;
   const rpt_stack& S = h->st;
-  if (core && (!h->core.p || h->core.cap < (size_t)(h->info.n_prev + K))) {
+  if (core && h->n_window < h->info.n_prev + K) {
     set_error("rpt_shard_points: no core flags (rpt_shard_window first)");
     return RPT_EINVAL;
   }
   const hipStream_t st = as_stream(stream);
+  if (core) {  // the window's final core flags in original order (checks only)
+    RPT_TRY(h->core.ensure((size_t)h->n_window, st));
+    RPT_TRY(dbscan_core_orig(h->db, h->core.p, st));
+  }
   const bool l = S.land_applied;
   auto cp = [&](void* dst, const void* src, size_t bytes) -> int32_t {
     if (dst) RPT_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st));

@@ -46,7 +46,7 @@ int32_t land_compact_dev(const float* x, const float* y, const float* v, const i
                          const int32_t* pf, int64_t n, const int32_t* cell, const uint8_t* land,
                          int32_t n_frames, float* xo, float* yo, float* vo, int32_t* go,
                          int32_t* pfo, float* to, int64_t* new_off, Bounds* bounds_out,
-                         hipStream_t st);
+                         hipStream_t st, int64_t t_base = 0);
 int32_t stdbscan(const float* x, const float* y, const float* z, int64_t stride, const float* t,
                  int64_t n, double eps_space, double eps_time, int32_t min_samples,
                  int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st, int dim);

@@ -3617,6 +3617,28 @@ __global__ void k_comp_out(int32_t* parent, const uint8_t* __restrict__ core,
     comp[sorig[s]] = out;
   }
 }
+// k_comp_out for the original indices outside [lo_end, hi_begin) only (the frame-sharded
+// driver needs the component ids of its halo points and of its own edge points, not of the
+// window's interior): every sorted point is read (one coalesced index load), only the edge
+// points pay a root lookup and a scattered store
+__global__ void k_comp_out_edges(int32_t* parent, const uint8_t* __restrict__ core,
+                                 const int32_t* __restrict__ sorig, int64_t n,
+                                 int32_t* __restrict__ comp, const int32_t* __restrict__ skey,
+                                 const int32_t* __restrict__ cell_root, int64_t cells,
+                                 int64_t lo_end, int64_t hi_begin) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t i = sorig[s];
+    if (i >= lo_end && i < hi_begin) continue;
+    int32_t out = -1;
+    if (core[s]) {
+      const int32_t key = skey[s];
+      const int32_t cr = (cell_root && (int64_t)key < cells) ? cell_root[key] : -1;
+      out = sorig[cr >= 0 ? cr : uf_find(parent, (int)s)];
+    }
+    comp[i] = out;
+  }
+}
 // Global labelling, core points: ccmin[s] = component-min original index; each component's
 // label = rank of its global representative (rep[min], from the equivalence merge) among the
 // sorted representatives -- one binary search per component, at its root; non-core queued.
@@ -5374,6 +5396,33 @@ int32_t dbscan_components(DbscanState* S, int32_t* comp_out, hipStream_t st) {
   RPT_CHECK_LAUNCH();
   return RPT_OK;
 }
+// the component ids (as dbscan_components) of the original indices outside [lo_end, hi_begin)
+int32_t dbscan_components_edges(DbscanState* S, int32_t* comp_out, int64_t lo_end,
+                                int64_t hi_begin, hipStream_t st) {
+  if (lo_end >= hi_begin) return dbscan_components(S, comp_out, st);
+  RPT_TRY(S->union_pass(st));
+  if (S->n == 0) return RPT_OK;
+  const bool cells = !S->degenerate;
+  if (cells)
+    hipLaunchKernelGGL(k_cell_roots, dim3(grid_for(S->n, kBlock, 2048)), dim3(kBlock), 0, st,
+                       S->parent, S->occ, S->n_occ_dev, S->C, S->mutual, S->rep, S->cell_root,
+                       (int32_t*)nullptr);
+  hipLaunchKernelGGL(k_comp_out_edges, dim3(grid_for(S->n, kBlock, 2048)), dim3(kBlock), 0, st,
+                     S->parent, S->core, S->sorig, S->n, comp_out, S->skey,
+                     cells ? (const int32_t*)S->cell_root : nullptr, cells ? S->C : (int64_t)0,
+                     lo_end, hi_begin);
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
+}
+// the union-find state for the shard driver's per-root passes: a core point s is its
+// component's root iff parent[s] == s (the component's minimum original index is sorig[s])
+void dbscan_uf_arrays(const DbscanState* S, const uint8_t** core, const int32_t** parent,
+                      const int32_t** sorig, int64_t* n) {
+  *core = S->core;
+  *parent = S->parent;
+  *sorig = S->sorig;
+  *n = S->n;
+}
 int32_t dbscan_labels_global(DbscanState* S, const int64_t* rep, const int64_t* reps, int64_t nr,
                              int32_t* labels, hipStream_t st) {
   return S->labels_global(rep, reps, nr, labels, st);
@@ -5399,6 +5448,52 @@ int32_t dbscan_labels_global_dev(DbscanState* S, const int64_t* rep, const int64
   return S->labels_global(rep, reps, 0, labels, st, nr_dev);
 }
 // device u8 core flags in the state's sorted order -> original order (out) without a pass
+// the shard driver's edge forms of dbscan_core / dbscan_set_core: core flags of the original
+// indices [a0, a1) -> out_a and [b0, b1) -> out_b (its own edge frames, for the neighbours), and
+// the halo points' flags from their owners (original indices [0, a1) <- in_a, [b0, n) <- in_b):
+// one coalesced index read per sorted point instead of full-length scattered conversions both
+// ways around the halo update
+__global__ void k_core_to_orig_ranges(const uint8_t* __restrict__ core,
+                                      const int32_t* __restrict__ sorig, int64_t n, int64_t a0,
+                                      int64_t a1, uint8_t* __restrict__ out_a, int64_t b0,
+                                      int64_t b1, uint8_t* __restrict__ out_b) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = sorig[s];
+    if (out_a && i >= a0 && i < a1) out_a[i - a0] = core[s];
+    if (out_b && i >= b0 && i < b1) out_b[i - b0] = core[s];
+  }
+}
+__global__ void k_core_from_orig_ranges(const uint8_t* __restrict__ in_a, int64_t a1,
+                                        const uint8_t* __restrict__ in_b, int64_t b0,
+                                        const int32_t* __restrict__ sorig, int64_t n,
+                                        uint8_t* __restrict__ core) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = sorig[s];
+    if (in_a && i < a1) core[s] = in_a[i];
+    if (in_b && i >= b0) core[s] = in_b[i - b0];
+  }
+}
+int32_t dbscan_core_edges(DbscanState* S, int64_t a0, int64_t a1, uint8_t* out_a, int64_t b0,
+                          int64_t b1, uint8_t* out_b, hipStream_t st) {
+  if (S->n <= 0 || (!(out_a && a1 > a0) && !(out_b && b1 > b0))) return RPT_OK;
+  hipLaunchKernelGGL(k_core_to_orig_ranges, dim3(grid_for(S->n, kBlock, 2048)), dim3(kBlock), 0,
+                     st, S->core, S->sorig, S->n, a0, a1, a1 > a0 ? out_a : nullptr, b0, b1,
+                     b1 > b0 ? out_b : nullptr);
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
+}
+int32_t dbscan_set_core_edges(DbscanState* S, const uint8_t* in_a, int64_t a1,
+                              const uint8_t* in_b, int64_t b0, hipStream_t st) {
+  const bool a = in_a && a1 > 0, b = in_b && b0 < S->n;
+  if (S->n <= 0 || (!a && !b)) return RPT_OK;
+  S->cmin_ready = false;  // core flags change: the core pass's cell minima no longer hold
+  hipLaunchKernelGGL(k_core_from_orig_ranges, dim3(grid_for(S->n, kBlock, 2048)), dim3(kBlock), 0,
+                     st, a ? in_a : nullptr, a1, b ? in_b : nullptr, b0, S->sorig, S->n, S->core);
+  RPT_CHECK_LAUNCH();
+  return RPT_OK;
+}
 int32_t dbscan_core_orig(DbscanState* S, uint8_t* out, hipStream_t st) {
   hipLaunchKernelGGL(k_core_to_orig, dim3(grid_for(S->n, kBlock, 2048)), dim3(kBlock), 0, st,
                      S->core, S->sorig, S->n, out);

@@ -115,11 +115,18 @@ for step in "$@"; do
           IFS=: read -r L D OFF <<< "$v"
           tag="${SEQTAG}L${L}_d${D}_$(echo "$OFF" | tr ',' '_')"
           RPT_COMM_FORCE_COLLECTIVES=1 RPT_SEQ_STAGGER=$D RPT_SEQ_OFFSETS=$OFF \
-            run "sq_${tag}_$rep" 200 $BS --lanes $L --steps 40 --warmup 6 || exit 1
+            run "sq_${tag}_$rep" 200 $BS --lanes $L --steps ${SEQSTEPS:-40} --warmup 6 || exit 1
         done
       done
       for f in $O/sq_*.log; do
         python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['ms_per_step'], d['steady_state']['ms_per_step'], d['slot_wait']['ms_per_step_by_phase'])" $f
+      done ;;
+    tests_shard)
+      run tests_shard 900 $PYT --timeout 600 tests/test_dist_gpu.py \
+        "tests/test_bigstack_gpu.py::test_sharded_share_matches_oracle" || exit 1 ;;
+    sl1)
+      for rep in 1 2; do
+        RPT_COMM_FORCE_COLLECTIVES=1 run sl1${SEQTAG}_$rep 200 $BS --lanes 1 --steps 40 --warmup 6 || exit 1
       done ;;
     tests_dist)
       run tests_dist 1000 $PYT --timeout 990 tests/test_dist_gpu.py tests/test_ab_variants_gpu.py \
