@@ -31,17 +31,17 @@ latency-bound kernels share the CUs; interleaved same-box runs with every lane s
 one untimed stack before the warm-up steps (its buffers are allocated on first use: a lane left
 cold cost ~80 ms inside the timed region); `one_stack_in_flight` repeats the steps strictly one after
 another, and K5's roofline is taken from that leg (K5 alone on the GPU).
-At N>1 (the frame-sharded path) three stacks are in flight per rank by default, their
-collectives through ONE communicator in a fixed software-pipeline order (rpt.dist.CommSequencer:
-every rank issues the same collectives in the same order; validated with gloo at 8 ranks and on
-RCCL at one rank with every collective forced through it -- RPT_COMM_FORCE_COLLECTIVES=1: 1.62-1.73
-ms per 125-frame step with 3 lanes against 2.04 with 1 in round 5, profiles/r5/rccl_lanes/);
-`--lanes 1` runs one stack at a time.  With one rank (`--sharded`, the 125-frame per-rank share of
-8 GPUs) the default is 3 as well (identity collectives).  The process group has a finite timeout
-(RPT_PG_TIMEOUT_S, default 240 s) and a hang guard (RPT_HANG_S, default 180 s without a step
-submitted or finished) dumps every thread's Python stack -- the lane threads name the collective
-slot they wait in -- and exits non-zero, so a cross-GPU ordering fault ends the run instead of
-hanging it.
+At N>1 (the frame-sharded path) four stacks are in flight per rank by default, their
+collectives through ONE communicator in a fixed software-pipeline order (rpt.dist.CommSequencer
+with NativeShardPipeline.SLOT_OFFSETS: every rank issues the same collectives in the same order;
+validated with gloo at 8 ranks and on RCCL at one rank with every collective forced through it
+-- RPT_COMM_FORCE_COLLECTIVES=1: 1.41 ms per 125-frame step at 4 lanes, 2.01 with 1,
+profiles/r6/rccl_lanes/); `--lanes 1` runs one stack at a time.  With one rank (`--sharded`,
+the 125-frame per-rank share of 8 GPUs) the default is 4 as well (identity collectives).  The
+process group has a finite timeout (RPT_PG_TIMEOUT_S, default 240 s) and a hang guard
+(RPT_HANG_S, default 180 s without a step submitted or finished) dumps every thread's Python
+stack -- the lane threads name the collective slot they wait in -- and exits non-zero, so a
+cross-GPU ordering fault ends the run instead of hanging it.
 After the timed region (N=1, timing on), K5 is also timed on the per-GPU shares at 8 GPUs, where
 SURVEY.md §8(d) sets the 0.40 roofline target: `roofline_c4_share` (125 standard frames, the
 configs[3] stack's share) and `roofline_configs4_share` (125 dense frames, configs[4]'s), one
@@ -148,7 +148,7 @@ def _reference_measured():
 def _traffic(name):
     """PMC-measured HBM bytes per launch committed for a workload (tools/pmc.sh: separate
     FETCH_SIZE / WRITE_SIZE passes, gfx950 read correction), newest round first."""
-    for rd in ("r5", "r4", "r3", "r2"):
+    for rd in ("r6", "r5", "r4", "r3", "r2"):
         f = ROOT / "profiles" / rd / name
         if f.exists():
             d = json.loads(f.read_text())
@@ -309,7 +309,7 @@ def main():
                          "instead of the native shard driver")
     ap.add_argument("--lanes", type=int, default=None,
                     help="stacks in flight at once (default 5 at one rank: native handles on "
-                         "separate streams; 3 with --sharded and at N>1 ranks, where a lane is a "
+                         "separate streams; 4 with --sharded and at N>1 ranks, where a lane is a "
                          "NativeShardPipeline with its own stream and thread, all lanes on ONE "
                          "process group in rpt.dist.CommSequencer's order); 1 = strictly one "
                          "after another")
@@ -329,11 +329,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if args.lanes is None:
-        # N > 1: three stacks in flight per rank, their collectives through ONE communicator in
+        # N > 1: four stacks in flight per rank, their collectives through ONE communicator in
         # CommSequencer's order -- every rank issues the same collectives in the same order, at
         # most one thread inside a collective at a time (validated on gloo up to 8 ranks and on
         # RCCL at one rank with every collective forced through it); --lanes 1 = one at a time
-        args.lanes = (3 if args.sharded else 5) if world == 1 else 3
+        args.lanes = (4 if args.sharded else 5) if world == 1 else 4
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # --sharded: the frame-sharded multi-GPU path even at one rank (measures its per-rank cost)
     dist = world > 1 or args.sharded

@@ -355,10 +355,12 @@ int32_t rpt_shard_land_grid(rpt_shard* h, const float* global_bounds, double* gr
  * compaction, and the own first / last hf frames packed for the neighbours: send_prev / send_next
  * (dev int32 [4 + 3 * n_head_k1] / [4 + 3 * n_tail_k1], nullable) = {count, own kept total lo,
  * hi, 0} then x, y, t (float32 bits; t = frame0 + frame slot) at offsets 4, 4 + cap, 4 + 2 cap.
- * No sync. */
+ * recv_cap_prev / recv_cap_next: the capacities of the halo buffers this rank will receive (the
+ * same values rpt_shard_window gets): with the land filter the compaction writes the kept points
+ * straight into the window at that offset.  No sync. */
 int32_t rpt_shard_halo(rpt_shard* h, const double* grid, int64_t cells, int32_t n_built_global,
                        int32_t rank, int64_t frame0, int32_t* send_prev, int32_t* send_next,
-                       void* stream);
+                       int64_t recv_cap_prev, int64_t recv_cap_next, void* stream);
 /* the window [prev halo | own | next halo] from the received halo buffers (capacities as sent;
  * NULL / 0 at the ends of the rank chain), its grid build and K5 core flags; flags_prev /
  * flags_next (dev u8, capacity n_head_k1 / n_tail_k1) receive the own edge points' flags for the

@@ -248,6 +248,86 @@ __global__ __launch_bounds__(kBoundsBlock) void k_window(
   acc.block_store(part);
 }
 
+// the bounds of no point (the identity of k_bounds_final's reduction)
+__global__ void k_empty_bounds(Bounds* __restrict__ out) {
+  if (threadIdx.x == 0) {
+    Bounds b;
+    for (int k = 0; k < 4; ++k) {
+      b.mn[k] = 0xffffffffu;
+      b.mx[k] = 0u;
+    }
+    b.nonfinite_xyz = b.nonintegral_t = b.n_finite_t = b.t_descends = 0;
+    *out = b;
+  }
+}
+
+// The direct window (the land compaction already wrote the own points at own_off): the halo
+// points placed around them -- prev halo at [own_off - np, own_off), next halo at
+// [own_off + K, own_off + K + nn) -- the window's counts, and per block the partial of the halo
+// points' bounds (k_window's semantics: every point's time against its window predecessor's);
+// partial nb is the own points' bounds from the compaction, with the prev halo -> own junction
+// folded in, so k_bounds_final over nb + 1 partials gives the window's bounds.
+__global__ __launch_bounds__(kBoundsBlock) void k_window_halo(
+    const int32_t* __restrict__ rp, int64_t cap_rp, const int32_t* __restrict__ rn,
+    int64_t cap_rn, const int64_t* __restrict__ off, int32_t F, int32_t hf, int64_t own_off,
+    float* __restrict__ X, float* __restrict__ Y, float* __restrict__ T,
+    WinMeta* __restrict__ meta, Bounds* __restrict__ part, int nb,
+    const Bounds* __restrict__ own_bnd) {
+  const int64_t np = rp ? (int64_t)rp[0] : 0;
+  const int64_t nn = rn ? (int64_t)rn[0] : 0;
+  const int64_t K = off[F];
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i0 == 0) {
+    WinMeta m;
+    m.n_prev = np;
+    m.n_own = K;
+    m.n_next = nn;
+    m.k_prev_total = rp ? halo_total(rp) : 0;
+    m.n_head = off[hf];
+    m.n_tail = K - off[F - hf];
+    m.n_window = np + K + nn;
+    m.pad = 0;
+    *meta = m;
+    Bounds o = *own_bnd;
+    if (np > 0 && K > 0 && !(__int_as_float(rp[kHaloHdr + 2 * cap_rp + np - 1]) <= T[own_off]))
+      o.t_descends = 1;  // (NaN counts as out of order, as in BoundsAcc)
+    part[nb] = o;
+  }
+  BoundsAcc acc;
+  for (int64_t h = i0; h < np + nn; h += (int64_t)gridDim.x * blockDim.x) {
+    float a, b, c, tp;
+    bool hp;
+    if (h < np) {
+      a = __int_as_float(rp[kHaloHdr + h]);
+      b = __int_as_float(rp[kHaloHdr + cap_rp + h]);
+      c = __int_as_float(rp[kHaloHdr + 2 * cap_rp + h]);
+      const int64_t i = own_off - np + h;
+      X[i] = a;
+      Y[i] = b;
+      T[i] = c;
+      hp = h > 0;
+      tp = hp ? __int_as_float(rp[kHaloHdr + 2 * cap_rp + h - 1]) : 0.f;
+    } else {
+      const int64_t j = h - np;
+      a = __int_as_float(rn[kHaloHdr + j]);
+      b = __int_as_float(rn[kHaloHdr + cap_rn + j]);
+      c = __int_as_float(rn[kHaloHdr + 2 * cap_rn + j]);
+      const int64_t i = own_off + K + j;
+      X[i] = a;
+      Y[i] = b;
+      T[i] = c;
+      // predecessor: the next halo's previous point, else the last own point, else the last
+      // prev halo point
+      hp = j > 0 || K > 0 || np > 0;
+      tp = j > 0 ? __int_as_float(rn[kHaloHdr + 2 * cap_rn + j - 1])
+                 : (K > 0 ? T[own_off + K - 1]
+                          : (np > 0 ? __int_as_float(rp[kHaloHdr + 2 * cap_rp + np - 1]) : 0.f));
+    }
+    acc.add(a, b, c, tp, hp);
+  }
+  acc.block_store(part);
+}
+
 // own edge points' global component ids for the neighbours (-1: not core)
 __global__ void k_comp_send(const int32_t* __restrict__ comp, WinIds w, int64_t n_head,
                             int64_t n_tail, int64_t* __restrict__ cp, int64_t* __restrict__ cn) {
@@ -667,6 +747,11 @@ struct rpt_shard {
   int32_t F = 0, G = 0, hf = 0, rank = 0;
   rpt_shard_info info{};
   int64_t n_window = 0, k_prev_total = 0;
+  // direct window (land filter on): the compaction wrote the own kept points' x / y / t into
+  // X / Y / T at own_off (= the prev halo's capacity); the window then starts at win_base =
+  // own_off - n_prev.  Otherwise the window is assembled from the K1 points at 0.
+  bool direct = false;
+  int64_t own_off = 0, own_cap_next = 0, win_base = 0;
   bool land = false;
   bool k9_radix = false;
   int32_t merge_max = kMergeMax;  // ids the device merge takes (rpt_shard_set_merge_limit)
@@ -697,6 +782,9 @@ struct rpt_shard {
   WinIds ids() const {
     return WinIds{rank, info.n_prev, info.n_kept, k_prev_total};
   }
+  // the own kept points' x / y (after the land filter, if any)
+  const float* own_x() const { return direct ? X.p + own_off : (st.land_applied ? st.x2.p : st.x.p); }
+  const float* own_y() const { return direct ? Y.p + own_off : (st.land_applied ? st.y2.p : st.y.p); }
 };
 
 extern "C" {
@@ -868,9 +956,9 @@ int32_t rpt_shard_land_grid(rpt_shard* h, const float* gbounds, double* grid, in
 
 int32_t rpt_shard_halo(rpt_shard* h, const double* grid, int64_t cells, int32_t n_built_global,
                        int32_t rank, int64_t frame0, int32_t* send_prev, int32_t* send_next,
-                       void* stream) {
+                       int64_t recv_cap_prev, int64_t recv_cap_next, void* stream) {
   clear_error();
-  if (!h || rank < 0) {
+  if (!h || rank < 0 || recv_cap_prev < 0 || recv_cap_next < 0) {
     set_error("rpt_shard_halo: bad arguments");
     return RPT_EINVAL;
   }
@@ -893,21 +981,36 @@ int32_t rpt_shard_halo(rpt_shard* h, const double* grid, int64_t cells, int32_t 
                           h->p.land_min_intensity, S.land_mask.p,
                           reinterpret_cast<int32_t*>(S.scal.p), st));
     const size_t cap = (size_t)std::max<int64_t>(N, 1);
-    RPT_TRY(S.x2.ensure(cap, st));
-    RPT_TRY(S.y2.ensure(cap, st));
     RPT_TRY(S.v2.ensure(cap, st));
     RPT_TRY(S.g2.ensure(cap, st));
     RPT_TRY(S.pf2.ensure(cap, st));
-    RPT_TRY(S.t.ensure(cap, st));
     RPT_TRY(S.bnd.ensure(2 * sizeof(Bounds), st));
-    if (N > 0)  // the fused compaction (kept points in order, new frame offsets on the device)
+    // the window's arrays: [prev halo capacity | own (<= N) | next halo capacity]; the fused
+    // compaction (kept points in order, new frame offsets and the own points' ST-DBSCAN bounds
+    // on the device) writes x / y / t (= frame0 + frame slot) straight into the own part, so the
+    // window phase only places the halo points around them
+    const int64_t wcap = std::max<int64_t>(recv_cap_prev + N + recv_cap_next, 1);
+    RPT_TRY(h->X.ensure((size_t)wcap, st));
+    RPT_TRY(h->Y.ensure((size_t)wcap, st));
+    RPT_TRY(h->T.ensure((size_t)wcap, st));
+    h->direct = true;
+    h->own_off = recv_cap_prev;
+    h->own_cap_next = recv_cap_next;
+    if (N > 0)
       RPT_TRY(land_compact_dev(S.x.p, S.y.p, S.v.p, S.had_gain ? S.g.p : nullptr, S.pf.p, N,
-                               S.land_cell.p, S.land_mask.p, F, S.x2.p, S.y2.p, S.v2.p,
-                               S.had_gain ? S.g2.p : nullptr, S.pf2.p, S.t.p, S.new_off.p,
-                               reinterpret_cast<Bounds*>(S.bnd.p), st));
-    else
+                               S.land_cell.p, S.land_mask.p, F, h->X.p + h->own_off,
+                               h->Y.p + h->own_off, S.v2.p, S.had_gain ? S.g2.p : nullptr,
+                               S.pf2.p, h->T.p + h->own_off, S.new_off.p,
+                               reinterpret_cast<Bounds*>(S.bnd.p), st, frame0));
+    else {
       RPT_HIP(hipMemsetAsync(S.new_off.p, 0, sizeof(int64_t) * (F + 1), st));
+      hipLaunchKernelGGL(k_empty_bounds, dim3(1), dim3(64), 0, st,
+                         reinterpret_cast<Bounds*>(S.bnd.p));
+      RPT_CHECK_LAUNCH();
+    }
   } else {
+    h->direct = false;
+    h->own_off = 0;
     RPT_HIP(hipMemsetAsync(S.scal.p, 0, sizeof(int64_t), st));  // (read back with the window)
     // no land filter: the kept points are the K1 points, offsets from the host copy
     RPT_TRY(S.up.ensure(sizeof(int64_t) * (size_t)(F + 1), st));
@@ -916,8 +1019,8 @@ int32_t rpt_shard_halo(rpt_shard* h, const double* grid, int64_t cells, int32_t 
                            st));
   }
   S.land_applied = h->land;
-  const float* cx = h->land ? S.x2.p : S.x.p;
-  const float* cy = h->land ? S.y2.p : S.y.p;
+  const float* cx = h->own_x();
+  const float* cy = h->own_y();
   const int32_t* cpf = h->land ? S.pf2.p : S.pf.p;
   if (send_prev || send_next) {
     const int64_t m = std::max(h->info.n_head_k1, h->info.n_tail_k1);
@@ -942,28 +1045,49 @@ int32_t rpt_shard_window(rpt_shard* h, const int32_t* recv_prev, int64_t cap_pre
   rpt_stack& S = h->st;
   const int32_t F = h->F;
   const int64_t N = h->n_points;
-  const float* cx = h->land ? S.x2.p : S.x.p;
-  const float* cy = h->land ? S.y2.p : S.y.p;
-  const int32_t* cpf = h->land ? S.pf2.p : S.pf.p;
+  if (h->direct && (cap_prev != h->own_off || cap_next != h->own_cap_next)) {
+    set_error("rpt_shard_window: halo capacities %lld / %lld differ from rpt_shard_halo's "
+              "%lld / %lld", (long long)cap_prev, (long long)cap_next, (long long)h->own_off,
+              (long long)h->own_cap_next);
+    return RPT_EINVAL;
+  }
   const int64_t wcap = std::max<int64_t>(cap_prev + N + cap_next, 1);
-  RPT_TRY(h->X.ensure((size_t)wcap, st));
-  RPT_TRY(h->Y.ensure((size_t)wcap, st));
-  RPT_TRY(h->T.ensure((size_t)wcap, st));
+  if (!h->direct) {
+    RPT_TRY(h->X.ensure((size_t)wcap, st));
+    RPT_TRY(h->Y.ensure((size_t)wcap, st));
+    RPT_TRY(h->T.ensure((size_t)wcap, st));
+  }
   const size_t bb = stdbscan_bounds_bytes();
   const size_t part = stdbscan_bounds_part_bytes(wcap);
-  RPT_TRY(h->wbnd.ensure(sizeof(WinMeta) + bb + part + 256, st));
+  RPT_TRY(h->wbnd.ensure(sizeof(WinMeta) + bb + part + sizeof(Bounds) + 256, st));
   WinMeta* meta = reinterpret_cast<WinMeta*>(h->wbnd.p);
   char* bnd = h->wbnd.p + sizeof(WinMeta);
   char* bpart = bnd + align_up(bb, 16);
-  // (the partials' count is the bounds pass's grid: stdbscan_bounds_part_bytes)
-  const int nbw = grid_for(wcap, kBoundsBlock, 1024);
-  hipLaunchKernelGGL(k_window, dim3(nbw), dim3(kBoundsBlock), 0, st,
-                     cap_prev > 0 ? recv_prev : nullptr, cap_prev,
-                     cap_next > 0 ? recv_next : nullptr, cap_next, cx, cy, cpf, S.new_off.p, F,
-                     h->hf, h->frame0, h->X.p, h->Y.p, h->T.p, meta,
-                     reinterpret_cast<Bounds*>(bpart));
-  RPT_CHECK_LAUNCH();
-  RPT_TRY(stdbscan_bounds_final_dev(bpart, nbw, bnd, st));
+  if (h->direct) {
+    // (halo partials: at most grid_for(cap_prev + cap_next) <= grid_for(wcap), + the own one)
+    const int nbh = grid_for(std::max<int64_t>(cap_prev + cap_next, 1), kBoundsBlock, 1024);
+    hipLaunchKernelGGL(k_window_halo, dim3(nbh), dim3(kBoundsBlock), 0, st,
+                       cap_prev > 0 ? recv_prev : nullptr, cap_prev,
+                       cap_next > 0 ? recv_next : nullptr, cap_next, S.new_off.p, F, h->hf,
+                       h->own_off, h->X.p, h->Y.p, h->T.p, meta,
+                       reinterpret_cast<Bounds*>(bpart), nbh,
+                       reinterpret_cast<const Bounds*>(S.bnd.p));
+    RPT_CHECK_LAUNCH();
+    RPT_TRY(stdbscan_bounds_final_dev(bpart, nbh + 1, bnd, st));
+  } else {
+    const float* cx = h->own_x();
+    const float* cy = h->own_y();
+    const int32_t* cpf = h->land ? S.pf2.p : S.pf.p;
+    // (the partials' count is the bounds pass's grid: stdbscan_bounds_part_bytes)
+    const int nbw = grid_for(wcap, kBoundsBlock, 1024);
+    hipLaunchKernelGGL(k_window, dim3(nbw), dim3(kBoundsBlock), 0, st,
+                       cap_prev > 0 ? recv_prev : nullptr, cap_prev,
+                       cap_next > 0 ? recv_next : nullptr, cap_next, cx, cy, cpf, S.new_off.p, F,
+                       h->hf, h->frame0, h->X.p, h->Y.p, h->T.p, meta,
+                       reinterpret_cast<Bounds*>(bpart));
+    RPT_CHECK_LAUNCH();
+    RPT_TRY(stdbscan_bounds_final_dev(bpart, nbw, bnd, st));
+  }
   // ONE readback: window counts, grid bounds, land-cell count, the kept frame offsets
   PackList pl;
   pl.add(meta, sizeof(WinMeta));
@@ -997,10 +1121,12 @@ int32_t rpt_shard_window(rpt_shard* h, const int32_t* recv_prev, int64_t cap_pre
   S.n_in = hm.n_own;
   *info = I;
   const int64_t n = hm.n_window;
+  h->win_base = h->direct ? h->own_off - hm.n_prev : 0;
   if (n <= 0) return RPT_OK;
   // grid build sized on the host from the bounds just read, then K5
-  RPT_TRY(dbscan_build_given(h->db, h->X.p, h->Y.p, h->T.p, n, h->p.eps_space, h->p.eps_time,
-                             h->p.min_samples, hb.data(), st));
+  const int64_t wb = h->win_base;
+  RPT_TRY(dbscan_build_given(h->db, h->X.p + wb, h->Y.p + wb, h->T.p + wb, n, h->p.eps_space,
+                             h->p.eps_time, h->p.min_samples, hb.data(), st));
   if (h->p.timing) {
     if (!h->ev_ok) {
       RPT_HIP(hipEventCreate(&h->ev[0]));
@@ -1164,8 +1290,8 @@ int32_t rpt_shard_finish(rpt_shard* h, const int64_t* gathered_pairs, int32_t wo
   RPT_TRY(h->labels.ensure((size_t)std::max<int64_t>(n, 1), st));
   if (n > 0) RPT_TRY(dbscan_labels_global_dev(h->db, h->rep.p, h->reps.p, nr_dev, h->labels.p, st));
   const bool l = S.land_applied;
-  const float* x = l ? S.x2.p : S.x.p;
-  const float* y = l ? S.y2.p : S.y.p;
+  const float* x = h->own_x();
+  const float* y = h->own_y();
   const float* v = l ? S.v2.p : S.v.p;
   const int32_t* pf = l ? S.pf2.p : S.pf.p;
   const size_t cap2 = (size_t)std::max<int64_t>(K, 1);
@@ -1259,8 +1385,8 @@ int32_t rpt_shard_points(const rpt_shard* h, float* x, float* y, float* intensit
     if (dst) RPT_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st));
     return RPT_OK;
   };
-  RPT_TRY(cp(x, l ? S.x2.p : S.x.p, sizeof(float) * (size_t)K));
-  RPT_TRY(cp(y, l ? S.y2.p : S.y.p, sizeof(float) * (size_t)K));
+  RPT_TRY(cp(x, h->own_x(), sizeof(float) * (size_t)K));
+  RPT_TRY(cp(y, h->own_y(), sizeof(float) * (size_t)K));
   RPT_TRY(cp(intensity, l ? S.v2.p : S.v.p, sizeof(float) * (size_t)K));
   RPT_TRY(cp(point_frame, l ? S.pf2.p : S.pf.p, sizeof(int32_t) * (size_t)K));
   RPT_TRY(cp(core, h->core.p + h->info.n_prev, (size_t)K));

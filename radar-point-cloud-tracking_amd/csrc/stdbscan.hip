@@ -918,8 +918,18 @@ __device__ __forceinline__ bool occupied(const uint32_t* __restrict__ bits, int6
 }
 
 // grids of the persistent wave-per-item kernels (item counts live on the device)
+// A/B build: RPT_WAVE_GRID_CAP caps the wave-per-item kernels' grids (fewer resident waves
+// leave room for other stacks' kernels on the same CUs)
+static int wave_grid_cap() {
+  static const int cap = [] {
+    const char* e = ab_env("RPT_WAVE_GRID_CAP");
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 8 ? v : 4096;
+  }();
+  return cap;
+}
 inline int wave_grid(int64_t max_items) {  // a multiple of 8 blocks (XCD-aware ranges)
-  const int g = grid_for(max_items, kBlock / 64, 4096);
+  const int g = grid_for(max_items, kBlock / 64, wave_grid_cap());
   return (g + 7) & ~7;
 }
 constexpr int kDefaultUfFlags = 2;

@@ -210,7 +210,7 @@ _SIGS = [
     ("rpt_shard_land_cells", C.c_int64, [c_f32p, C.c_double]),
     ("rpt_shard_land_grid", C.c_int32, [vp, c_f32p, vp, C.c_int64, vp]),
     ("rpt_shard_halo", C.c_int32, [vp, vp, C.c_int64, C.c_int32, C.c_int32, C.c_int64, vp, vp,
-                                   vp]),
+                                   C.c_int64, C.c_int64, vp]),
     ("rpt_shard_window", C.c_int32, [vp, vp, C.c_int64, vp, C.c_int64, vp, vp,
                                      C.POINTER(ShardInfo), vp]),
     ("rpt_shard_core_ms", C.c_double, [vp]),

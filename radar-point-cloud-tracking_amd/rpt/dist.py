@@ -668,6 +668,15 @@ class NativeShardPipeline:
     stays as the CPU-testable restatement (tests/test_dist_cpu.py)."""
 
     N_SLOTS = 8  # collective phases of one step (CommSequencer slots): 7 + the rare redo
+    # the lanes' slot order (CommSequencer): step s takes phase p at time 4 s + SLOT_OFFSETS[p].
+    # Info, land and halo (0-2) together; flags and component ids (3, 4) after the window
+    # readback; the pair gather (5) before the NEXT step's info / land / halo, the result gather
+    # (6) after them -- so a step's pair gather does not wait for the next step's K1, and its
+    # label / K9 work is queued while the next step's K1 runs.  Measured at one rank with every
+    # collective forced through RCCL (profiles/r6/rccl_lanes/sq_*): 1.41 ms per 125-frame step at
+    # 4 lanes against 1.46-1.54 in the round-5 order (3 lanes)
+    SLOT_STAGGER = 4
+    SLOT_OFFSETS = (0, 0, 0, 2, 2, 3, 5, 5)
 
     def __init__(self, comm: Comm, gains: Sequence[int], rows: int, bins: int,
                  params: PathParams = None, timing: bool = False, async_host: bool = False,
@@ -800,7 +809,7 @@ class NativeShardPipeline:
         hsp = ws.get("hsp", 4 + 3 * cap_sp, torch.int32) if has_p else None
         hsn = ws.get("hsn", 4 + 3 * cap_sn, torch.int32) if has_n else None
         chk(lib.rpt_shard_halo(self.h, ptr(grid), cells, n_built, r, int(frame0), ptr(hsp),
-                               ptr(hsn), st), "rpt_shard_halo")
+                               ptr(hsn), cap_rp, cap_rn, st), "rpt_shard_halo")
         rp = rn = None
         if halo:
             empty = torch.empty(0, dtype=torch.int32, device=self.dev)
@@ -1089,11 +1098,19 @@ class ShardLanes:
         self.pipes = [NativeShardPipeline(comm, gains, rows, bins, params, timing=timing,
                                           async_host=async_host, host_workers=host_workers)
                       for _ in range(lanes)]
+        # (RPT_SEQ_STAGGER / RPT_SEQ_OFFSETS: other orders, for measurements)
         st_env = os.environ.get("RPT_SEQ_STAGGER")
         off_env = os.environ.get("RPT_SEQ_OFFSETS")
-        self.seq = CommSequencer(lanes, NativeShardPipeline.N_SLOTS,
-                                 stagger=int(st_env) if st_env else None,
-                                 offsets=[int(v) for v in off_env.split(",")] if off_env else None)
+        offs = [int(v) for v in off_env.split(",")] if off_env else \
+            list(NativeShardPipeline.SLOT_OFFSETS)
+        # (one lane runs its steps one after another: a step's slots must all come before the
+        # next step's, so the stagger grows to the offsets' span + 1 there)
+        span = offs[-1] - offs[0]
+        self.seq = CommSequencer(
+            lanes, NativeShardPipeline.N_SLOTS,
+            stagger=int(st_env) if st_env else
+            max(NativeShardPipeline.SLOT_STAGGER, -(-(span + 1) // lanes)),
+            offsets=offs)
         self.streams = [torch.cuda.Stream(dev) for _ in range(lanes)] if lanes > 1 else [None]
         self.free_lanes = bool(free_lanes)
         self.keep_labels = bool(keep_labels)

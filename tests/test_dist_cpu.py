@@ -394,3 +394,44 @@ def test_comm_sequencer_state_stays_bounded():
     assert seq.epoch_of == {} and seq.next_phase == {}
     assert peak <= 16, peak   # the steps in flight (submitted, not done), not the 600 run
     assert sum(seq.wait_n) == 600 * (P - 1)
+
+
+def test_shard_slot_order_valid_for_every_lane_count():
+    """ShardLanes' default slot order (NativeShardPipeline.SLOT_OFFSETS / SLOT_STAGGER, the
+    stagger grown for few lanes) satisfies CommSequencer's no-self-wait constraint at 1..8 lanes,
+    and its steps run to completion with every slot used and with the redo slot skipped."""
+    import threading
+    from concurrent.futures import ThreadPoolExecutor
+
+    from rpt.dist import CommSequencer, NativeShardPipeline
+
+    offs = list(NativeShardPipeline.SLOT_OFFSETS)
+    span = offs[-1] - offs[0]
+    for L in range(1, 9):
+        d = max(NativeShardPipeline.SLOT_STAGGER, -(-(span + 1) // L))
+        seq = CommSequencer(L, NativeShardPipeline.N_SLOTS, stagger=d, offsets=offs)
+        pools = [ThreadPoolExecutor(max_workers=1) for _ in range(L)]
+        done = []
+        lock = threading.Lock()
+
+        def run(step):
+            slots = seq.step(step)
+            try:
+                for p in range(NativeShardPipeline.N_SLOTS - (step % 2)):
+                    with slots.slot(p):
+                        pass
+            finally:
+                slots.close()
+            with lock:
+                done.append(step)
+
+        futs = []
+        for s in range(4 * L + 3):
+            seq.register(s)
+            futs.append(pools[s % L].submit(run, s))
+        seq.close_group()
+        for f in futs:
+            f.result(timeout=30)
+        for p in pools:
+            p.shutdown()
+        assert sorted(done) == list(range(4 * L + 3))

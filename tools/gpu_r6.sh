@@ -124,6 +124,29 @@ for step in "$@"; do
     tests_shard)
       run tests_shard 900 $PYT --timeout 600 tests/test_dist_gpu.py \
         "tests/test_bigstack_gpu.py::test_sharded_share_matches_oracle" || exit 1 ;;
+    digest8)      # the 8 x 125 sharded digest check with every rank's output kept
+      OMP_NUM_THREADS=2 run digest8 600 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node=8 --master-addr=127.0.0.1 --master-port=29611 --tee 3 \
+        tools/dist_check.py --backend gloo --frames 125 --lanes 1 --digest std0 || exit 1 ;;
+    gridcap)      # A/B build: the wave-per-item kernels' grid cap (RPT_WAVE_GRID_CAP), the driver's
+                  # bench line (5 stacks in flight, 1000 frames), interleaved
+      AB=radar-point-cloud-tracking_amd/rpt/librpt_ab.so
+      BB="python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --h2d-steps 0 --no-dense-k5 --no-one-stack"
+      for rep in 1 2; do
+        for c in ${CAPS:-4096 1024 512}; do
+          RPT_LIB=$AB RPT_WAVE_GRID_CAP=$c run gcap${c}_$rep 300 $BB || exit 1
+        done
+      done
+      for f in $O/gcap*.log; do
+        python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['value'], d['ms_per_step'], d['steady_state']['ms_per_step'])" $f
+      done ;;
+    sldef)        # the default sharded configuration (lanes, sequencer order), forced RCCL, 100 steps
+      for rep in 1 2; do
+        RPT_COMM_FORCE_COLLECTIVES=1 run sldef${SEQTAG}_$rep 300 $BS --steps 100 --warmup 6 || exit 1
+      done
+      for f in $O/sldef${SEQTAG}_*.log; do
+        python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['config']['stacks_in_flight'], d['ms_per_step'], d['steady_state']['ms_per_step'], d['slot_wait']['ms_per_step_by_phase'])" $f
+      done ;;
     sl1)
       for rep in 1 2; do
         RPT_COMM_FORCE_COLLECTIVES=1 run sl1${SEQTAG}_$rep 200 $BS --lanes 1 --steps 40 --warmup 6 || exit 1
