@@ -701,6 +701,11 @@ class NativeShardPipeline:
         # again with a larger one, consistently on every rank)
         self._cap_pairs, self._cap_out = 1024, 1 << 15
         self._last = None  # (gathered results on the device, rows, words per row) of the last run
+        # the info vector's host staging: pinned, so its upload for the RCCL gather is an async
+        # copy in stream order instead of a synchronous pageable one (reused: the next step's
+        # polar readback synchronises the lane's stream after this upload)
+        self._info_pin = torch.empty(8, dtype=torch.float64, pin_memory=True) \
+            if self.dev.type == "cuda" and not comm.host else None
 
     def set_geometry(self, scale, cos_t, sin_t, n_files: int):
         def rep(a):
@@ -776,10 +781,15 @@ class NativeShardPipeline:
                                 C_.byref(info), st), "rpt_shard_polar")
         n_points = int(info.n_points)
         # issued inside the slot, waited for outside it: the other lanes' collectives go on
+        vals = [n_points, info.n_built, *[float(b) for b in info.bounds], info.n_head_k1,
+                info.n_tail_k1]
+        if self._info_pin is not None and not comm.solo:
+            self._info_pin.numpy()[:] = vals
+            info_t = self._info_pin.to(self.dev, non_blocking=True)
+        else:
+            info_t = torch.tensor(vals, dtype=torch.float64)
         with slots.slot(0):
-            allinfo = comm.all_gather_fixed_issue(torch.tensor(
-                [n_points, info.n_built, *[float(b) for b in info.bounds], info.n_head_k1,
-                 info.n_tail_k1], dtype=torch.float64))
+            allinfo = comm.all_gather_fixed_issue(info_t)
         allinfo = allinfo.cpu().numpy()
         n_global = int(allinfo[:, 0].sum())
         n_built = int(allinfo[:, 1].sum())
