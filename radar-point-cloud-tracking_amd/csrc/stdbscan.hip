@@ -3217,9 +3217,22 @@ __global__ __launch_bounds__(kBlock) void k_cell_roots(int32_t* parent,
                                                       const uint8_t* __restrict__ mutual,
                                                       const int32_t* __restrict__ rep,
                                                       int32_t* __restrict__ cell_root,
-                                                      int32_t* __restrict__ zero = nullptr) {
-  // zero (nullable): a counter of the next kernel, cleared here instead of by a memset launch
+                                                      int32_t* __restrict__ zero = nullptr,
+                                                      uint32_t* __restrict__ zwords = nullptr,
+                                                      int64_t nzw = 0,
+                                                      int32_t* __restrict__ cmin_fill = nullptr) {
+  // zero (nullable): a counter of the next kernel, cleared here instead of by a memset launch;
+  // likewise the label pass's minimum bits (zwords, nzw words) and its per-cell smallest keys
+  // (cmin_fill: every cell INT_MAX) -- both first written by k_ccmin / k_ccmin_global next
   if (zero && blockIdx.x == 0 && threadIdx.x == 0) *zero = 0;
+  {
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t ts = (int64_t)gridDim.x * blockDim.x;
+    if (zwords)
+      for (int64_t i = t0; i < nzw; i += ts) zwords[i] = 0u;
+    if (cmin_fill)
+      for (int64_t i = t0; i < cells; i += ts) cmin_fill[i] = INT_MAX;
+  }
   const int64_t m = *n_occ;
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m;
        q += (int64_t)gridDim.x * blockDim.x) {
@@ -4913,15 +4926,20 @@ int32_t DbscanState::union_pass(hipStream_t st) {
 // cell_key (nullable, pre-filled with INT_MAX): also the per-cell smallest component key
 int32_t DbscanState::cluster_ids(hipStream_t st, int32_t* cell_key, int32_t* zero) {
   const int64_t W = min_words();
-  RPT_HIP(hipMemsetAsync(min_bits, 0, sizeof(uint32_t) * W, st));
   // per-cell roots of the mutual cells (read by k_ccmin for their core points); zero (nullable):
-  // k_ccmin's non-core queue counter, cleared by k_cell_roots
+  // k_ccmin's non-core queue counter, cleared by k_cell_roots, which also clears the minimum
+  // bits and fills cell_key (nullable) with INT_MAX (one launch instead of three)
   const bool cr = cell_roots_enabled();
-  if (cr)
+  if (cr) {
     hipLaunchKernelGGL(k_cell_roots, dim3(grid_for(n, kBlock, 2048)), dim3(kBlock), 0, st, parent,
-                       occ, n_occ_dev, C, mutual, rep, cell_root, zero);
-  else if (zero)
-    RPT_HIP(hipMemsetAsync(zero, 0, sizeof(int32_t), st));
+                       occ, n_occ_dev, C, mutual, rep, cell_root, zero, min_bits, W, cell_key);
+  } else {
+    RPT_HIP(hipMemsetAsync(min_bits, 0, sizeof(uint32_t) * W, st));
+    if (zero) RPT_HIP(hipMemsetAsync(zero, 0, sizeof(int32_t), st));
+    if (cell_key)
+      hipLaunchKernelGGL(k_fill_i32, dim3(grid_for(C, kBlock, 8192)), dim3(kBlock), 0, st,
+                         cell_key, C, INT_MAX);
+  }
   hipLaunchKernelGGL(k_ccmin, dim3(tile_grid(n)), dim3(kBlock), 0, st, parent, core, n, sorig,
                      ccmin, min_bits, nc_list, nc_list + n, skey, mutual,
                      cr ? (const int32_t*)cell_root : nullptr, C, cell_key);
@@ -4945,9 +4963,8 @@ int32_t DbscanState::labels_local(int32_t* labels, rpt_stdbscan_stats* stats, hi
     return RPT_OK;
   }
   int32_t* nc_count = nc_list + n;
-  const int gc = grid_for(C, kBlock, 8192);
-  hipLaunchKernelGGL(k_fill_i32, dim3(gc), dim3(kBlock), 0, st, cell_min, C, INT_MAX);
-  // also the per-cell smallest keys (k_cell_min_key fused) and nc_count cleared
+  // also the per-cell smallest keys (k_cell_min_key fused; cell_min filled with INT_MAX by
+  // cluster_ids' first kernel) and nc_count cleared
   RPT_TRY(cluster_ids(st, cell_min, nc_count));
   const MinRank mr{min_bits, min_pref};
   if (spos_on)
@@ -5040,13 +5057,15 @@ int32_t DbscanState::labels_global(const int64_t* rep_orig, const int64_t* reps,
   const int gb = grid_for(n, kBlock, 2048);
   int32_t* nc_count = nc_list + n;
   const bool cr = cell_roots_enabled();
-  if (cr)  // (also clears nc_count for k_ccmin_global)
+  if (cr) {  // (also clears nc_count for k_ccmin_global and fills cell_min with INT_MAX)
     hipLaunchKernelGGL(k_cell_roots, dim3(grid_for(n, kBlock, 2048)), dim3(kBlock), 0, st, parent,
-                       occ, n_occ_dev, C, mutual, rep, cell_root, nc_count);
-  else
+                       occ, n_occ_dev, C, mutual, rep, cell_root, nc_count, (uint32_t*)nullptr,
+                       (int64_t)0, cell_min);
+  } else {
     RPT_HIP(hipMemsetAsync(nc_count, 0, sizeof(int32_t), st));
-  const int gc = grid_for(C, kBlock, 8192);
-  hipLaunchKernelGGL(k_fill_i32, dim3(gc), dim3(kBlock), 0, st, cell_min, C, INT_MAX);
+    hipLaunchKernelGGL(k_fill_i32, dim3(grid_for(C, kBlock, 8192)), dim3(kBlock), 0, st, cell_min,
+                       C, INT_MAX);
+  }
   hipLaunchKernelGGL(k_ccmin_global, dim3(tile_grid(n)), dim3(kBlock), 0, st, parent, core, n,
                      sorig, rep_orig, reps, nr, ccmin, cid, nc_list, nc_count, skey, mutual,
                      cr ? (const int32_t*)cell_root : nullptr, C, nr_dev);

@@ -1228,7 +1228,9 @@ __global__ void k_seg_compact(int32_t F, const int32_t* __restrict__ fstart,
   }
 }
 
-__global__ void k_fill_i64(int64_t* p, int64_t n, int64_t v) {
+// p[0, n) = v; zero2 (nullable): two counters of the next kernel cleared (no memset launch)
+__global__ void k_fill_i64(int64_t* p, int64_t n, int64_t v, int32_t* zero2 = nullptr) {
+  if (zero2 && blockIdx.x == 0 && threadIdx.x < 2) zero2[threadIdx.x] = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     p[i] = v;
@@ -1255,9 +1257,16 @@ static int32_t summaries_impl(const int32_t* labels, const float* x, const float
     return RPT_ENOTSUP;
   }
   Scratch& sc = scratch(st);
-  if (n_frames > 0 && frame_first_noise)
-    hipLaunchKernelGGL(k_fill_i64, dim3(grid_for(n_frames, 256, 64)), dim3(256), 0, st,
-                       frame_first_noise, (int64_t)n_frames, (int64_t)-1);
+  // frame_first_noise = -1 (the frame-sort path clears its counters in the same launch)
+  auto fill_noise = [&](int32_t* zero2) -> int32_t {
+    if (n_frames > 0 && frame_first_noise) {
+      hipLaunchKernelGGL(k_fill_i64, dim3(grid_for(n_frames, 256, 64)), dim3(256), 0, st,
+                         frame_first_noise, (int64_t)n_frames, (int64_t)-1, zero2);
+    } else if (zero2) {
+      RPT_HIP(hipMemsetAsync(zero2, 0, 2 * sizeof(int32_t), st));
+    }
+    return RPT_OK;
+  };
   const int64_t sh = std::max<int64_t>(1, std::min<int64_t>(s_hint, n));
   // per-frame counting sort unless forced off (RPT_K9_RADIX=1, or a redo after a frame held more
   // than kFsMaxKeys labels) or frames are huge (one 8-wave block per frame)
@@ -1312,7 +1321,7 @@ static int32_t summaries_impl(const int32_t* labels, const float* x, const float
       nent = sc.carve_n<int32_t>(NC);
       fnoise_c = sc.carve_n<int32_t>(NC);
     }
-    RPT_HIP(hipMemsetAsync(ovf, 0, 2 * sizeof(int32_t), st));
+    RPT_TRY(fill_noise(ovf));
     if (C == 1) {
       hipLaunchKernelGGL(k_frame_sort, dim3(n_frames), dim3(kFsWaves * 64), 0, st, labels, pf, n,
                          x, y, inten, gx, gy, gi, fstart, tstart, tlen, tlabel, tfirst, nseg_f,
@@ -1346,6 +1355,7 @@ static int32_t summaries_impl(const int32_t* labels, const float* x, const float
     *n_seg_dev = base + n_frames;
     return RPT_OK;
   }
+  RPT_TRY(fill_noise(nullptr));
   Budget b;
   for (int k = 0; k < 4; ++k) b.add<uint32_t>(n + 1);
   b.add<int64_t>(radix_tmp_elems(n));
