@@ -110,7 +110,7 @@ for step in "$@"; do
         python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['ms_per_step'], d['steady_state']['ms_per_step'], d['slot_wait']['ms_per_step_by_phase'])" $f
       done ;;
     seqab2)       # sharded 125-frame step, forced RCCL: lanes x CommSequencer orders (SEQV)
-      for rep in 1 2; do
+      for rep in ${SEQREPS:-1 2}; do
         for v in ${SEQV:-"3:2:0,0,1,1,2,3,4,5" "4:2:0,0,1,1,2,3,4,5" "5:2:0,0,1,1,2,3,4,5" "3:4:0,1,2,2,3,3,4,5" "4:3:0,1,2,4,5,6,7,8" "5:2:0,1,2,3,4,5,6,7"}; do
           IFS=: read -r L D OFF <<< "$v"
           tag="${SEQTAG}L${L}_d${D}_$(echo "$OFF" | tr ',' '_')"
