@@ -1,6 +1,7 @@
 """Frame-sharded path on the GPU: 2 or 3 ranks (gloo, sharing cuda:0 on a one-GPU box) run
-rpt.dist.NativeShardPipeline (librpt's rpt_shard_* driver) or ShardedStackPipeline over librpt; rank 0 compares with the single-GPU
-FrameStackPipeline (labels, per-frame cluster rows in reference order, tracked objects).
+rpt.dist.NativeShardPipeline (librpt's rpt_shard_* driver) or ShardedStackPipeline over librpt; rank 0 compares with the oracle's
+run_path over the whole stack and with the single-GPU FrameStackPipeline (labels, per-frame
+cluster rows in reference order, tracked objects).
 The ranks are started by torch.distributed.run as child processes (tools/dist_check.py)."""
 from __future__ import annotations
 
@@ -59,7 +60,11 @@ def test_sharded_gpu_matches_single_gpu(world, frames, impl, lanes):
         impl, extra = "native", ["--tiny-caps"]
     elif impl == "native-hostmerge":
         impl, extra = "native", ["--force-host-merge"]
-    _run(world, frames, impl, lanes, extra)
+    # rank 0 checks every run against the oracle's run_path over the whole stack as well
+    # (labels, per-frame cluster rows in reference order, tracked objects), not only against
+    # the single-GPU pipeline
+    out = _run(world, frames, impl, lanes, extra + ["--oracle"])
+    assert "labels_equal=True rows_equal=True tracks_equal=True" in out, out[-4000:]
 
 
 @pytest.mark.gpu
