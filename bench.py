@@ -450,9 +450,10 @@ def main():
     def points_of(r):  # K1 points of the whole (global) stack of a run
         return float(r.n_points_global if dist else r.n_points)
 
-    if not dist and args.lanes > 1:
+    if args.lanes > 1 and not args.python_shard:
         # lane setup (untimed, before the warm-up steps): one stack per lane allocates that lane's
-        # buffers, whatever --warmup is
+        # buffers, whatever --warmup is (free lanes are taken in FIFO order: consecutive steps
+        # waited for one at a time visit every lane)
         for k in range(args.lanes):
             resolve(run(echoes[k % E])).finish()
     for k in range(args.warmup):
