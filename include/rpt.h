@@ -438,6 +438,20 @@ int32_t rpt_order_clusters(int32_t n_frames, int64_t n_segments, const int32_t* 
                            const int64_t* frame_first_noise, int64_t* frame_offsets_out,
                            int64_t* order_out);
 
+/* ---- host: cluster order + tracker of one stack in one call ------------------------------
+ * rpt_order_clusters (frame_offsets_out, order_out as there) followed by rpt_tracker_update on
+ * trk for each built slot (built_slots[n_built], strictly ascending, in [0, n_frames)) with the
+ * slot's segments' seg_cx/seg_cy in that order and frame id frame_ids[slot] (NULL: the slot) --
+ * the host stage of pipeline.py's order_and_track (4_temporal_object_tracker.py:519-522 then
+ * :984-991).  Frames are ordered on a second thread ahead of the tracker.  trk NULL: only the
+ * order.  Returns RPT_OK or an error code (the tracker's included). */
+int32_t rpt_order_and_track(int32_t n_frames, int64_t n_segments, const int32_t* seg_frame,
+                            const int32_t* seg_label, const int64_t* seg_first,
+                            const int64_t* frame_first_noise, const float* seg_cx,
+                            const float* seg_cy, int32_t n_built, const int64_t* built_slots,
+                            const int64_t* frame_ids, struct rpt_tracker* trk,
+                            int64_t* frame_offsets_out, int64_t* order_out);
+
 /* ---- host: CPython set iteration order --------------------------------------------------
  * keys = the distinct labels of a frame in first-occurrence order (may include -1).
  * order_out receives the keys in the order `iter(set(keys))` yields them on CPython 3.10

@@ -1,14 +1,17 @@
 // Rank 0's host stage of the frame-sharded driver (shard.cpp) over the all-gathered packed
 // per-rank results -- the global cluster numbering, every segment in global frame ids, the
 // reference cluster order per frame (4_temporal_object_tracker.py:519-522) and the tracker over
-// the built frames (:984-991) -- and the host equivalence merge used when a step's gathered pairs
+// the built frames (:984-991), the parts unpacked and ordered on a producer thread ahead of the
+// tracker -- and the host equivalence merge used when a step's gathered pairs
 // exceed the device merge.  No device work: host-only, so tools/asan/Makefile also builds it with
 // -fsanitize=address,undefined.
 #include <algorithm>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "host_common.h"
+#include "host_stage.h"
 #include "shard_pack.h"
 
 namespace rpt {
@@ -105,65 +108,113 @@ int32_t rpt_shard_host_stage(const int64_t* g, int32_t world, int64_t row_words,
     for (int64_t l = 0; l < a.R; ++l) local_to_global[l] = glabel(a.reps[l]);
   }
   if (!seg_frame) return RPT_OK;  // only the label map
-  int64_t s0 = 0, fbase = 0, nb = 0;
-  if (frame_off) frame_off[0] = 0;
-  std::vector<int32_t> lf, gl;
-  std::vector<int64_t> fo, ord;
+  if (!seg_label || !seg_count || !seg_first || !seg_cx || !seg_cy || !seg_mi ||
+      (trk && (!built_ids || !frame_off))) {
+    set_error("rpt_shard_host_stage: bad arguments");
+    return RPT_EINVAL;
+  }
+  // where each part's segments and frames go; the built frames (in order) from the headers
+  std::vector<int64_t> s0s, fbases;
+  int64_t s_tot = 0, f_tot = 0, nb = 0;
   for (const Part& a : parts) {
-    const int64_t S = a.S, F = a.F;
-    std::vector<int32_t> map((size_t)a.R);
-    for (int64_t l = 0; l < a.R; ++l) map[(size_t)l] = glabel(a.reps[l]);
-    lf.resize((size_t)S);
-    gl.resize((size_t)S);
-    for (int64_t s = 0; s < S; ++s) {
-      const int32_t fr = (int32_t)(a.fl[s] >> 32);
-      const int32_t ll = (int32_t)(uint32_t)(a.fl[s] & 0xffffffff);
-      lf[(size_t)s] = fr;
-      gl[(size_t)s] = (ll >= 0 && ll < a.R) ? map[(size_t)ll] : -2;
-      seg_frame[s0 + s] = (int32_t)(fr + a.frame0);
-      seg_label[s0 + s] = gl[(size_t)s];
-      seg_count[s0 + s] = a.cnt[s];
-      seg_first[s0 + s] = a.first[s];
-      const uint64_t b = (uint64_t)a.cxy[s];
-      const uint32_t bx = (uint32_t)b, by = (uint32_t)(b >> 32), bm = (uint32_t)(uint64_t)a.mi[s];
-      std::memcpy(&seg_cx[s0 + s], &bx, 4);
-      std::memcpy(&seg_cy[s0 + s], &by, 4);
-      std::memcpy(&seg_mi[s0 + s], &bm, 4);
-    }
-    // the reference cluster order of each frame of the part (local frame slots, local firsts)
-    fo.resize((size_t)F + 1);
-    ord.resize((size_t)std::max<int64_t>(S, 1));
-    RPT_TRY(order_clusters((int32_t)F, S, lf.data(), gl.data(), a.first, a.noise, fo.data(),
-                           ord.data()));
-    for (int64_t f = 0; f < F; ++f) {
-      if (frame_off) frame_off[fbase + f + 1] = fo[(size_t)f + 1] + s0;
+    s0s.push_back(s_tot);
+    fbases.push_back(f_tot);
+    for (int64_t f = 0; f < a.F; ++f) {
       if (a.built[f] && built_ids) built_ids[nb] = a.frame0 + f;
       nb += a.built[f] ? 1 : 0;
     }
-    if (order)
-      for (int64_t s = 0; s < S; ++s) order[s0 + s] = ord[(size_t)s] + s0;
-    s0 += S;
-    fbase += F;
+    s_tot += a.S;
+    f_tot += a.F;
   }
-  if (!trk) return RPT_OK;
-  // the tracker over the built frames in order, each frame's clusters in the reference order
-  // (frame slots are global frame ids less rank 0's first frame)
-  const int64_t f0 = parts.empty() ? 0 : parts[0].frame0;
-  std::vector<float> cxs, cys;
-  for (int64_t b = 0; b < nb; ++b) {
-    const int64_t slot = built_ids[b] - f0;
-    const int64_t lo = frame_off[slot], hi = frame_off[slot + 1];
-    cxs.resize((size_t)(hi - lo));
-    cys.resize((size_t)(hi - lo));
-    for (int64_t k = lo; k < hi; ++k) {
-      cxs[(size_t)(k - lo)] = seg_cx[order[k]];
-      cys[(size_t)(k - lo)] = seg_cy[order[k]];
+  if (frame_off) frame_off[0] = 0;
+  std::vector<int64_t> own_order;
+  if (!order) own_order.resize((size_t)std::max<int64_t>(s_tot, 1));
+  int64_t* ord_out = order ? order : own_order.data();
+  // producer: per part the segments in global numbering and frame ids, then the reference
+  // cluster order of its frames in chunks, published as global frame slots
+  constexpr int32_t kChunk = 32;
+  int32_t perr = RPT_OK;
+  std::string pmsg;
+  OrderAhead ahead;
+  ahead.start(
+      [&](OrderAhead& ah) {
+        std::vector<int32_t> lf, gl, map;
+        FrameBuckets fb;
+        for (size_t q = 0; q < parts.size(); ++q) {
+          const Part& a = parts[q];
+          const int64_t S = a.S, F = a.F, s0 = s0s[q], fbase = fbases[q];
+          map.resize((size_t)a.R);
+          for (int64_t l = 0; l < a.R; ++l) map[(size_t)l] = glabel(a.reps[l]);
+          lf.resize((size_t)S);
+          gl.resize((size_t)S);
+          for (int64_t s = 0; s < S; ++s) {
+            const int32_t fr = (int32_t)(a.fl[s] >> 32);
+            const int32_t ll = (int32_t)(uint32_t)(a.fl[s] & 0xffffffff);
+            lf[(size_t)s] = fr;
+            gl[(size_t)s] = (ll >= 0 && ll < a.R) ? map[(size_t)ll] : -2;
+            seg_frame[s0 + s] = (int32_t)(fr + a.frame0);
+            seg_label[s0 + s] = gl[(size_t)s];
+            seg_count[s0 + s] = a.cnt[s];
+            seg_first[s0 + s] = a.first[s];
+            const uint64_t b = (uint64_t)a.cxy[s];
+            const uint32_t bx = (uint32_t)b, by = (uint32_t)(b >> 32),
+                           bm = (uint32_t)(uint64_t)a.mi[s];
+            std::memcpy(&seg_cx[s0 + s], &bx, 4);
+            std::memcpy(&seg_cy[s0 + s], &by, 4);
+            std::memcpy(&seg_mi[s0 + s], &bm, 4);
+          }
+          // the reference cluster order of each frame of the part (local frame slots, local
+          // firsts), segment ids shifted to the global numbering
+          const int32_t st = fb.build((int32_t)F, S, lf.data(), nullptr);
+          if (st != RPT_OK) {
+            perr = st;
+            pmsg = last_error_cstr();
+            ah.publish(INT64_MAX);
+            return;
+          }
+          if (frame_off)
+            for (int64_t f = 0; f < F; ++f) frame_off[fbase + f + 1] = fb.cnt[(size_t)f + 1] + s0;
+          for (int64_t f = 0; f < F; f += kChunk) {
+            const int64_t hi = std::min<int64_t>(F, f + kChunk);
+            fb.order((int32_t)f, (int32_t)hi, gl.data(), a.first, a.noise, ord_out + s0, s0);
+            ah.publish(fbase + hi);
+          }
+        }
+        ah.publish(INT64_MAX);
+      },
+      trk != nullptr && f_tot >= 2 * kChunk);
+  int32_t r = 0;
+  if (trk) {
+    // the tracker over the built frames in order, each frame's clusters in the reference order
+    // (frame slots are global frame ids less rank 0's first frame), frame by frame as the
+    // producer publishes them
+    const int64_t f0 = parts.empty() ? 0 : parts[0].frame0;
+    std::vector<float> cxs, cys;
+    for (int64_t b = 0; b < nb && r >= 0; ++b) {
+      const int64_t slot = built_ids[b] - f0;
+      ahead.wait_for(slot);
+      if (perr != RPT_OK || ahead.failed()) break;
+      const int64_t lo = frame_off[slot], hi = frame_off[slot + 1];
+      cxs.resize((size_t)(hi - lo));
+      cys.resize((size_t)(hi - lo));
+      for (int64_t k = lo; k < hi; ++k) {
+        cxs[(size_t)(k - lo)] = seg_cx[ord_out[k]];
+        cys[(size_t)(k - lo)] = seg_cy[ord_out[k]];
+      }
+      r = rpt_tracker_update(trk, built_ids[b], (int32_t)(hi - lo), cxs.data(), cys.data(),
+                             nullptr);
     }
-    const int32_t r = rpt_tracker_update(trk, built_ids[b], (int32_t)(hi - lo), cxs.data(),
-                                         cys.data(), nullptr);
-    if (r < 0) return -r;
   }
-  return RPT_OK;
+  ahead.join();
+  if (perr != RPT_OK) {
+    set_error("%s", pmsg.c_str());
+    return perr;
+  }
+  if (ahead.failed()) {
+    set_error("rpt_shard_host_stage: host stage failed (out of memory)");
+    return RPT_ENOMEM;
+  }
+  return r < 0 ? -r : RPT_OK;
 }
 
 

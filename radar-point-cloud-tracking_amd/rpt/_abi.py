@@ -229,6 +229,9 @@ _SIGS = [
                                          c_i64p, c_i32p, C.c_int32]),
     ("rpt_order_clusters", C.c_int32, [C.c_int32, C.c_int64, c_i32p, c_i32p, c_i64p, c_i64p,
                                         c_i64p, c_i64p]),
+    ("rpt_order_and_track", C.c_int32, [C.c_int32, C.c_int64, c_i32p, c_i32p, c_i64p, c_i64p,
+                                         c_f32p, c_f32p, C.c_int32, c_i64p, c_i64p, vp, c_i64p,
+                                         c_i64p]),
     ("rpt_set_order", C.c_int32, [c_i32p, C.c_int32, c_i32p]),
     ("rpt_lsap", C.c_int32, [c_f64p, C.c_int32, C.c_int32, c_i64p, c_i64p]),
     ("rpt_tracker_new", vp, [C.POINTER(TrackerParams)]),

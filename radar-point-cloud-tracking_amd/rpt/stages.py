@@ -316,8 +316,28 @@ def track_ordered(slots: np.ndarray, fo: np.ndarray, order: np.ndarray,
 def order_and_track(n_frames: int, built: np.ndarray, seg: Dict[str, np.ndarray],
                     first_noise: np.ndarray, params, frame_ids: Optional[np.ndarray] = None):
     """Host: per-frame reference cluster order (CPython set emulation) + the C++ tracker over the
-    built frames.  frame_ids[f] is the frame id of slot f (default: the slot)."""
-    fo, order = order_frames(n_frames, seg, first_noise)
-    built = np.asarray(built, np.int64)
-    ids = None if frame_ids is None else np.asarray(frame_ids, np.int64)[built]
-    return fo, order, track_ordered(built, fo, order, seg, params, ids)
+    built frames, in one native call (rpt_order_and_track: frames ordered on a second thread
+    ahead of the tracker).  frame_ids[f] is the frame id of slot f (default: the slot)."""
+    from .native_tracker import NativeTracker
+
+    lib = _abi.load()
+    trk = NativeTracker(params.max_association_distance, params.max_missed_frames,
+                        params.motion_history_frames, params.stationary_velocity_threshold)
+    S = len(seg["frame"])
+    fo = np.empty(n_frames + 1, np.int64)
+    order = np.empty(max(S, 1), np.int64)
+    built = np.ascontiguousarray(built, np.int64)
+    ids = None if frame_ids is None else np.ascontiguousarray(frame_ids, np.int64)
+    if ids is not None and len(ids) < n_frames:
+        raise ValueError("frame_ids needs one id per frame slot")
+    a32 = lambda k: np.ascontiguousarray(seg[k], np.int32).ctypes.data_as(_abi.c_i32p)  # noqa: E731
+    af = lambda k: np.ascontiguousarray(seg[k], np.float32).ctypes.data_as(_abi.c_f32p)  # noqa: E731
+    _abi.check(lib.rpt_order_and_track(
+        n_frames, S, a32("frame"), a32("label"),
+        np.ascontiguousarray(seg["first"], np.int64).ctypes.data_as(_abi.c_i64p),
+        np.ascontiguousarray(first_noise, np.int64).ctypes.data_as(_abi.c_i64p),
+        af("cx"), af("cy"), len(built), built.ctypes.data_as(_abi.c_i64p),
+        ids.ctypes.data_as(_abi.c_i64p) if ids is not None else None, trk._h,
+        fo.ctypes.data_as(_abi.c_i64p), order.ctypes.data_as(_abi.c_i64p)),
+        "rpt_order_and_track")
+    return fo, order[:S], trk

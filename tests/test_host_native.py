@@ -75,6 +75,86 @@ def test_order_clusters_stack_matches_per_frame():
         np.testing.assert_array_equal(order[fo[f]:fo[f + 1]], idx[o1], err_msg=f"frame {f}")
 
 
+def _tracker_state(trk):
+    return [(o.object_id, o.object_type, np.vstack(o.positions).tobytes(), tuple(o.frames_seen),
+             np.vstack(o.velocities).astype(np.float64).tobytes()) for o in trk.objects()]
+
+
+@pytest.mark.parametrize("F,with_ids", [(0, False), (1, False), (50, True), (700, False),
+                                        (1500, True)])
+def test_order_and_track_matches_two_step(F, with_ids):
+    """rpt_order_and_track (frames ordered on a second thread ahead of the tracker) == the
+    order (rpt_order_clusters) then the tracker (rpt_tracker_run) over the gathered centroids:
+    same order, same tracker state -- segments in arbitrary order, empty and unbuilt frames,
+    noise, frame ids other than the slots."""
+    from rpt import stages
+    from rpt.pipeline import PathParams
+
+    rng = np.random.default_rng(F + 3)
+    tgt = rng.random((30, 2)) * 300 - 150
+    vel = rng.normal(0, 1.5, (30, 2))
+    frames, labels, firsts, cxs, cys = [], [], [], [], []
+    for f in range(F):
+        if rng.random() < 0.05:
+            continue  # no segment: frame not built, or built with noise only
+        keep = np.nonzero(rng.random(30) < 0.85)[0]
+        n_extra = int(rng.integers(0, 5))
+        k = len(keep) + n_extra
+        pos = np.vstack([tgt[keep] + vel[keep] * f + rng.normal(0, 0.4, (len(keep), 2)),
+                         rng.random((n_extra, 2)) * 400 - 200])
+        frames += [f] * k
+        labels += list(rng.choice(10**5, k, replace=False))
+        firsts += list(rng.choice(10**6, k, replace=False))
+        cxs += list(pos[:, 0])
+        cys += list(pos[:, 1])
+    perm = rng.permutation(len(frames))
+    seg = {"frame": np.asarray(frames, np.int32)[perm], "label": np.asarray(labels, np.int32)[perm],
+           "first": np.asarray(firsts, np.int64)[perm],
+           "cx": np.asarray(cxs, np.float32)[perm], "cy": np.asarray(cys, np.float32)[perm]}
+    noise = np.where(rng.random(F) < 0.7, rng.integers(0, 10**6, F), -1).astype(np.int64)
+    built = np.nonzero((np.bincount(seg["frame"], minlength=F) > 0) | (noise >= 0))[0]
+    ids = (np.arange(F, dtype=np.int64) * 3 + 1000) if with_ids else None
+    p = PathParams()
+    fo1, order1 = stages.order_frames(F, seg, noise)
+    trk1 = stages.track_ordered(built, fo1, order1, seg, p, None if ids is None else ids[built])
+    fo2, order2, trk2 = stages.order_and_track(F, built, seg, noise, p, ids)
+    np.testing.assert_array_equal(fo1, fo2)
+    np.testing.assert_array_equal(order1, order2)
+    assert len(trk2) == len(trk1)
+    assert _tracker_state(trk2) == _tracker_state(trk1)
+    if F:
+        assert len(trk1) > 0
+
+
+def test_order_and_track_invalid():
+    from rpt import _abi
+    from rpt.native_tracker import NativeTracker
+
+    lib = _abi.load()
+    trk = NativeTracker()
+    fr = np.array([0, 1], np.int32)
+    lab = np.array([3, 4], np.int32)
+    first = np.array([0, 5], np.int64)
+    noise = np.full(2, -1, np.int64)
+    c = np.zeros(2, np.float32)
+    fo = np.empty(3, np.int64)
+    order = np.empty(2, np.int64)
+
+    def call(built, frames=fr):
+        b = np.asarray(built, np.int64)
+        p = lambda a, t: a.ctypes.data_as(t)  # noqa: E731
+        return lib.rpt_order_and_track(2, 2, p(frames, _abi.c_i32p), p(lab, _abi.c_i32p),
+                                       p(first, _abi.c_i64p), p(noise, _abi.c_i64p),
+                                       p(c, _abi.c_f32p), p(c, _abi.c_f32p), len(b),
+                                       p(b, _abi.c_i64p), None, trk._h, p(fo, _abi.c_i64p),
+                                       p(order, _abi.c_i64p))
+
+    assert call([0, 1]) == 0
+    assert call([1, 0]) == 1  # not ascending
+    assert call([0, 2]) == 1  # out of range
+    assert call([0, 1], np.array([0, 2], np.int32)) == 1  # segment frame out of range
+
+
 def _lsap_cases():
     rng = np.random.default_rng(0)
     for k in range(60):

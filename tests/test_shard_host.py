@@ -77,15 +77,16 @@ def _synth(seed, W=4, F=6):
         segs = {k: np.array(v, dtype={"frame": np.int32, "llabel": np.int32, "count": np.int64,
                                       "first": np.int64}.get(k, np.float32))
                 for k, v in segs.items()}
-        parts.append(_pack(q, F, q * F, segs, noise, built, reps, 4096))
+        parts.append(_pack(q, F, q * F, segs, noise, built, reps, HDR + 27 * F + 64))
         truth.append((segs, noise, built, reps))
     return np.ascontiguousarray(np.stack(parts)), truth, F
 
 
-@pytest.mark.parametrize("seed", range(5))
-def test_shard_host_stage_matches_python(seed):
+# (the larger stacks run the producer thread that orders frames ahead of the tracker)
+@pytest.mark.parametrize("seed,W,F", [(s, 4, 6) for s in range(5)] + [(5, 4, 50), (6, 2, 300)])
+def test_shard_host_stage_matches_python(seed, W, F):
     lib = _abi.load()
-    g, truth, F = _synth(seed)
+    g, truth, F = _synth(seed, W, F)
     W, cap = g.shape
     sizes = np.zeros(4, np.int64)
     _abi.check(lib.rpt_shard_gathered_sizes(g.ctypes.data_as(_abi.c_i64p), W, cap,
