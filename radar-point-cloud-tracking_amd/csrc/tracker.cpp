@@ -518,7 +518,9 @@ struct Lsap {
     return sink;
   }
 
-  int32_t solve(const double* cost_in, int32_t nr_in, int32_t nc_in, int64_t* a, int64_t* b) {
+  // finite_known: the caller guarantees no NaN / -inf entry (the tracker, from finite inputs)
+  int32_t solve(const double* cost_in, int32_t nr_in, int32_t nc_in, int64_t* a, int64_t* b,
+                bool finite_known = false) {
     int64_t nr = nr_in, nc = nc_in;
     if (nr == 0 || nc == 0) return RPT_OK;
     const bool transpose = nc < nr;
@@ -531,7 +533,7 @@ struct Lsap {
       cost = tmp.data();
     }
     bool bad = false;
-    for (int64_t i = 0; i < nr * nc; ++i)
+    for (int64_t i = 0; i < (finite_known ? 0 : nr * nc); ++i)
       bad |= (cost[i] != cost[i]) | (cost[i] == -std::numeric_limits<double>::infinity());
     if (bad) {
       set_error("matrix contains invalid numeric entries");
@@ -599,6 +601,7 @@ enum { kUnknown = 0, kBuoy = 1, kBoat = 2 };
 struct Vel {
   float x, y;
   bool f64_zero;  // the float64 [0, 0] every object starts with
+  float nrm;      // f32_norm(x, y) (average_velocity's terms), computed once
 };
 
 struct Object {
@@ -621,6 +624,7 @@ inline float f32_norm(float x, float y) {  // np.linalg.norm float32: sdot witho
   const float yy = y * y;
   return std::sqrt(xx + yy);
 }
+inline Vel make_vel(float x, float y) { return Vel{x, y, false, f32_norm(x, y)}; }
 inline double f64_norm(double x, double y) {  // np.linalg.norm float64: ddot with FMA
   return std::sqrt(std::fma(y, y, x * x));
 }
@@ -628,7 +632,8 @@ inline double f64_norm(double x, double y) {  // np.linalg.norm float64: ddot wi
 // Cost matrix of one frame, [k clusters][m objects]: per object the prediction in the dtype numpy
 // uses (float64 while its velocity window holds the float64 zero, float32 after), cost =
 // np.linalg.norm of the difference.  Every entry gets the float32 norm (8-wide), then the columns
-// listed in c64 (float64 predictions: young objects) are overwritten with the float64 norm.  The
+// listed in c64 (float64 predictions p64x/p64y[q] of column c64[q]: young objects) are
+// overwritten with the float64 norm, computed 4-wide into t64 first.  The
 // float64 norm's fused multiply-add must be the hardware instruction for speed (libm's software
 // fma gives the same, correctly rounded, result), hence one build for AVX2+FMA hosts, dispatched
 // at run time, and a baseline build.
@@ -643,24 +648,24 @@ inline double f64_norm(double x, double y) {  // np.linalg.norm float64: ddot wi
       row[j] = (double)__builtin_sqrtf(exx + eyy);                       \
     }                                                                    \
     for (int32_t q = 0; q < n64; ++q) {                                  \
-      const int32_t j = c64[q];                                          \
-      const double dx = dxs - p64x[j], dy = dys - p64y[j];               \
-      row[j] = __builtin_sqrt(__builtin_fma(dy, dy, dx * dx));           \
+      const double dx = dxs - p64x[q], dy = dys - p64y[q];               \
+      t64[q] = __builtin_sqrt(__builtin_fma(dy, dy, dx * dx));           \
     }                                                                    \
+    for (int32_t q = 0; q < n64; ++q) row[c64[q]] = t64[q];              \
   }
 
 __attribute__((target("avx2,fma"))) void fill_costs_v3(
     int32_t k, int32_t m, const float* __restrict__ cx, const float* __restrict__ cy,
     int32_t n64, const int32_t* __restrict__ c64, const double* __restrict__ p64x,
     const double* __restrict__ p64y, const float* __restrict__ p32x,
-    const float* __restrict__ p32y, double* __restrict__ cost) {
+    const float* __restrict__ p32y, double* __restrict__ t64, double* __restrict__ cost) {
   RPT_FILL_COSTS_BODY
 }
 void fill_costs_base(int32_t k, int32_t m, const float* __restrict__ cx,
                      const float* __restrict__ cy, int32_t n64, const int32_t* __restrict__ c64,
                      const double* __restrict__ p64x, const double* __restrict__ p64y,
                      const float* __restrict__ p32x, const float* __restrict__ p32y,
-                     double* __restrict__ cost) {
+                     double* __restrict__ t64, double* __restrict__ cost) {
   RPT_FILL_COSTS_BODY
 }
 #undef RPT_FILL_COSTS_BODY
@@ -683,7 +688,7 @@ struct Tracker {
   std::vector<int> live;
   std::vector<char> assigned;
   std::vector<int32_t> c64;
-  std::vector<double> p64x, p64y;
+  std::vector<double> p64x, p64y, t64;  // float64 predictions of the columns in c64
   std::vector<float> p32x, p32y;
   Lsap solver;
 
@@ -713,7 +718,7 @@ struct Tracker {
     o.py.push_back(cy);
     o.frames.push_back(fid);
     o.last_seen = fid;
-    o.vel.push_back(Vel{0.f, 0.f, true});
+    o.vel.push_back(Vel{0.f, 0.f, true, 0.f});
     refresh_mean(o);
     color_of(next_id, o.color);
     objs.push_back(std::move(o));
@@ -732,11 +737,11 @@ struct Tracker {
     if (has64) {  // np.mean over float64 array (< 8 values: sequential from 0.)
       double s = 0.0;
       for (size_t k = b; k < o.vel.size(); ++k)
-        s = s + (o.vel[k].f64_zero ? 0.0 : (double)f32_norm(o.vel[k].x, o.vel[k].y));
+        s = s + (o.vel[k].f64_zero ? 0.0 : (double)o.vel[k].nrm);
       return s / (double)m;
     }
     float s = 0.f;
-    for (size_t k = b; k < o.vel.size(); ++k) s = s + f32_norm(o.vel[k].x, o.vel[k].y);
+    for (size_t k = b; k < o.vel.size(); ++k) s = s + o.vel[k].nrm;
     *is_f32 = true;
     return (double)(s / (float)m);
   }
@@ -811,26 +816,35 @@ struct Tracker {
     const int32_t m = (int32_t)live.size();
     cost.resize((size_t)k * m);
     c64.clear();
-    p64x.resize(m);
-    p64y.resize(m);
+    p64x.clear();
+    p64y.clear();
     p32x.resize(m);
     p32y.resize(m);
+    // every input finite: no cost entry can be NaN or -inf (a difference of finite floats is
+    // finite or +-inf, its norm finite or +inf), so the solver's scan of the matrix is skipped
+    bool finite = true;
     for (int32_t j = 0; j < m; ++j) {
       const Object& o = objs[live[j]];
       const Pred q = predict(o, fid - o.last_seen);  // depends on the object only
-      if (q.f64) c64.push_back(j);
-      p64x[j] = q.x;
-      p64y[j] = q.y;
+      if (q.f64) {
+        c64.push_back(j);
+        p64x.push_back(q.x);
+        p64y.push_back(q.y);
+      }
       p32x[j] = (float)q.x;
       p32y[j] = (float)q.y;
+      finite = finite && std::isfinite(q.x) && std::isfinite(q.y);
     }
+    for (int32_t i = 0; i < k; ++i) finite = finite && std::isfinite(cx[i]) && std::isfinite(cy[i]);
+    t64.resize(c64.size());
     (host_has_fma() ? fill_costs_v3 : fill_costs_base)(k, m, cx, cy, (int32_t)c64.size(),
                                                          c64.data(), p64x.data(), p64y.data(),
-                                                         p32x.data(), p32y.data(), cost.data());
+                                                         p32x.data(), p32y.data(), t64.data(),
+                                                         cost.data());
     const int32_t np_ = std::min(k, m);
     ra.resize(np_);
     ca.resize(np_);
-    const int32_t ls = solver.solve(cost.data(), k, m, ra.data(), ca.data());
+    const int32_t ls = solver.solve(cost.data(), k, m, ra.data(), ca.data(), finite);
     if (ls != RPT_OK) return -ls;  // negative = error (counts are >= 0)
     assigned.assign(k, 0);
     for (int32_t q = 0; q < np_; ++q) {
@@ -840,7 +854,7 @@ struct Tracker {
         const int64_t fe = fid - o.last_seen;
         if (fe > 0) {
           const float fef = (float)fe;
-          o.vel.push_back(Vel{(cx[i] - o.px.back()) / fef, (cy[i] - o.py.back()) / fef, false});
+          o.vel.push_back(make_vel((cx[i] - o.px.back()) / fef, (cy[i] - o.py.back()) / fef));
           refresh_mean(o);
         }
         o.px.push_back(cx[i]);
