@@ -8,7 +8,6 @@ interface (tests/_cpu_ops.py).  The product has no CPU implementation.
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 from typing import Dict, Optional
 
@@ -321,11 +320,6 @@ def order_and_track(n_frames: int, built: np.ndarray, seg: Dict[str, np.ndarray]
     ahead of the tracker).  frame_ids[f] is the frame id of slot f (default: the slot)."""
     from .native_tracker import NativeTracker
 
-    if os.environ.get("RPT_HOST_TWO_STEP") == "1":  # (temporary A/B: order, then the tracker)
-        fo, order = order_frames(n_frames, seg, first_noise)
-        built = np.asarray(built, np.int64)
-        ids = None if frame_ids is None else np.asarray(frame_ids, np.int64)[built]
-        return fo, order, track_ordered(built, fo, order, seg, params, ids)
     lib = _abi.load()
     trk = NativeTracker(params.max_association_distance, params.max_missed_frames,
                         params.motion_history_frames, params.stationary_velocity_threshold)

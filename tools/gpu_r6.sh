@@ -186,15 +186,6 @@ for step in "$@"; do
       for f in $O/bth_*.log $O/bnt_*.log; do
         python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['value'], d['ms_per_step'], d['steady_state']['ms_per_step'])" $f
       done ;;
-    bench_host)   # the driver's bench line: fused host stage (in-tree) vs the two-step form
-      BB="python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --h2d-steps 0"
-      for rep in 1 2; do
-        run bhf_$rep 300 $BB || exit 1
-        RPT_HOST_TWO_STEP=1 run bh2_$rep 300 $BB || exit 1
-      done
-      for f in $O/bhf_*.log $O/bh2_*.log; do
-        python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['value'], d['ms_per_step'], d['steady_state']['ms_per_step'])" $f
-      done ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench_lanes)  # the driver's bench line at 5 (default), 6 and 8 stacks in flight, interleaved
