@@ -397,7 +397,7 @@ __device__ __forceinline__ uint32_t kept_entry(const GroupLds& L,
 // kStageSlots words; the write pass then reads those instead of the group's 4 KiB of echo (one
 // read of the echo for the whole K1).  A group that keeps more (dense sweeps) is read from the
 // echo again by the write pass.
-constexpr int kStageSlots = 256;
+constexpr int kStageSlots = 512;  // (256: +39 us K1 at 1000 frames, profiles/r6/ab_stage512/)
 // Slot position of in-group kept rank i in a staged group of `total` entries.  With stride 4 (the
 // reference's POINT_STRIDE) the ranks of each residue mod 4 are contiguous and the four residues
 // packed back to back in [0, total): the write pass reads every 4th rank from one residue, i.e.
