@@ -63,6 +63,24 @@ class Scratch {
 };
 Scratch& scratch(hipStream_t st);  // for the current device and this stream
 
+// ---- pre-zeroed device words ---------------------------------------------------------------
+// Counters a call needs zeroed (atomic cursors, list lengths).  A driver that runs many calls on
+// one stream arms the stream's pool once per run -- one memset for all of them -- and
+// zero_words() then hands out zeroed words of the pool without a launch of its own; unarmed, or
+// once the armed pool is used up, zero_words() clears the words it hands out with a memset (the
+// standalone entry points).  Words are handed out in 64-byte slots, ring-wise per stream: a word
+// stays valid for the work queued on the stream before the ring comes round (kZeroSlots takes).
+constexpr int kZeroSlots = 256;
+int32_t zero_pool_arm(hipStream_t st);
+int32_t zero_words(hipStream_t st, size_t words, void** out);
+template <class T>
+int32_t zero_n(hipStream_t st, size_t n, T** out) {
+  void* p = nullptr;
+  const int32_t r = zero_words(st, (n * sizeof(T) + 3) / 4, &p);
+  *out = static_cast<T*>(p);
+  return r;
+}
+
 // Byte budget helper: sum of aligned array sizes.
 struct Budget {
   size_t bytes = 0;

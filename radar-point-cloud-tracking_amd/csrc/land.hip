@@ -751,10 +751,8 @@ int32_t land_mask_dev(const int32_t* cnt, const double* tot, int64_t cells, int6
 int32_t land_mask(const int32_t* cnt, const double* tot, int64_t cells, int64_t num_frames,
                   double pthr, double ithr, uint8_t* land, int64_t* n_land_host,
                   hipStream_t st) {
-  Scratch& sc = scratch(st);
-  RPT_TRY(sc.reserve(256, st));
-  int32_t* d = sc.carve_n<int32_t>(1);
-  RPT_HIP(hipMemsetAsync(d, 0, sizeof(int32_t), st));
+  int32_t* d = nullptr;
+  RPT_TRY(zero_n(st, 1, &d));
   const double nf = (double)(num_frames > 1 ? num_frames : 1);
   if (cells > 0) {
     hipLaunchKernelGGL(k_land_mask, dim3(grid_for(cells, 256, 1024)), dim3(256), 0, st, cnt, tot,

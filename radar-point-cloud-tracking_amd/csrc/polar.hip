@@ -1054,12 +1054,11 @@ int32_t write_impl(const T* echo, int64_t n_files, int rows, int bins, float thr
       Budget b;
       b.add<uint64_t>(n_groups);
       b.add<uint32_t>(n_groups);
-      b.add<uint32_t>(1);
       RPT_TRY(sc.reserve(b.bytes, st));
       uint64_t* gword = sc.carve_n<uint64_t>(n_groups);
       uint32_t* list = sc.carve_n<uint32_t>(n_groups);
-      uint32_t* list_n = sc.carve_n<uint32_t>(1);
-      RPT_HIP(hipMemsetAsync(list_n, 0, sizeof(uint32_t), st));
+      uint32_t* list_n = nullptr;
+      RPT_TRY(zero_n(st, 1, &list_n));
       hipLaunchKernelGGL(k_group_starts, dim3(grid_for(n_groups, kBlock, 4096)), dim3(kBlock), 0,
                          st, row_prefix, file_offsets, (uint32_t)n_groups, gm.gpf,
                          (uint32_t)stride, gword, list, list_n);

@@ -124,6 +124,74 @@ Scratch& scratch(hipStream_t st) {
   return *g_scratch.back().second;
 }
 
+// ------------------------------------------------------------------ pre-zeroed words
+namespace {
+struct ZeroPool {
+  std::mutex mu;
+  uint32_t* base = nullptr;  // kZeroSlots slots of 16 words
+  int64_t next = 0;          // slots handed out since the pool was created (ring position)
+  int64_t armed_end = -1;    // slots up to this ring position are zero from the last arm()
+};
+constexpr int kZeroSlotWords = 16;
+std::mutex g_zero_mu;
+std::vector<std::pair<std::pair<int, hipStream_t>, ZeroPool*>> g_zero;
+
+int32_t zero_pool(hipStream_t st, ZeroPool** out) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  ZeroPool* z = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_zero_mu);
+    for (auto& e : g_zero)
+      if (e.first.first == dev && e.first.second == st) z = e.second;
+    if (!z) {
+      z = new ZeroPool();
+      g_zero.push_back({{dev, st}, z});
+    }
+  }
+  if (!z->base) {
+    hipError_t e = hipMalloc(&z->base, sizeof(uint32_t) * kZeroSlots * kZeroSlotWords);
+    if (e != hipSuccess) {
+      z->base = nullptr;
+      set_error("zero pool hipMalloc failed: %s", hipGetErrorString(e));
+      return RPT_ENOMEM;
+    }
+  }
+  *out = z;
+  return RPT_OK;
+}
+}  // namespace
+
+int32_t zero_pool_arm(hipStream_t st) {
+  ZeroPool* z = nullptr;
+  RPT_TRY(zero_pool(st, &z));
+  std::lock_guard<std::mutex> lk(z->mu);
+  // one memset of the whole ring; the next kZeroSlots takes need none
+  RPT_HIP(hipMemsetAsync(z->base, 0, sizeof(uint32_t) * kZeroSlots * kZeroSlotWords, st));
+  z->next = (z->next + kZeroSlots - 1) / kZeroSlots * kZeroSlots;  // start of a ring round
+  z->armed_end = z->next + kZeroSlots;
+  return RPT_OK;
+}
+
+int32_t zero_words(hipStream_t st, size_t words, void** out) {
+  ZeroPool* z = nullptr;
+  RPT_TRY(zero_pool(st, &z));
+  const int64_t slots = (int64_t)((words + kZeroSlotWords - 1) / kZeroSlotWords);
+  if (slots < 1 || slots > kZeroSlots / 4) {
+    set_error("zero_words: %zu words", words);
+    return RPT_EINVAL;
+  }
+  std::lock_guard<std::mutex> lk(z->mu);
+  int64_t at = z->next;
+  if (at % kZeroSlots + slots > kZeroSlots) at = (at / kZeroSlots + 1) * kZeroSlots;  // no wrap
+  z->next = at + slots;
+  uint32_t* p = z->base + (at % kZeroSlots) * kZeroSlotWords;
+  if (at + slots > z->armed_end)  // not covered by the last arm(): clear with a memset
+    RPT_HIP(hipMemsetAsync(p, 0, sizeof(uint32_t) * slots * kZeroSlotWords, st));
+  *out = p;
+  return RPT_OK;
+}
+
 void release_scan_states(int dev);  // below, with the scan
 
 void release_scratch_current() {
@@ -133,6 +201,16 @@ void release_scratch_current() {
     std::lock_guard<std::mutex> lk(g_scratch_mu);
     for (auto& e : g_scratch)
       if (e.first.first == dev) e.second->release();
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_zero_mu);
+    for (auto& e : g_zero)
+      if (e.first.first == dev && e.second->base) {
+        std::lock_guard<std::mutex> lz(e.second->mu);
+        (void)hipFree(e.second->base);
+        e.second->base = nullptr;
+        e.second->armed_end = -1;
+      }
   }
   release_scan_states(dev);
 }

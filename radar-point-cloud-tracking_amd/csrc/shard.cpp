@@ -807,6 +807,7 @@ int32_t rpt_shard_polar(rpt_shard* h, const rpt_stack_params* p, const void* ech
     return RPT_EINVAL;
   }
   const hipStream_t st = as_stream(stream);
+  RPT_TRY(zero_pool_arm(st));  // the step's counters (this call and the step's later ones)
   rpt_stack& S = h->st;
   h->p = *p;
   S.had_gain = gain != nullptr;  // per-point gains only with a gain table

@@ -409,6 +409,8 @@ int32_t rpt_stack_run(rpt_stack* h, const rpt_stack_params* p, const void* echo,
     set_error("rpt_stack_run: null handle or params");
     return RPT_EINVAL;
   }
+  // the run's counters from one clear of the stream's zero pool (common.h)
+  RPT_TRY(zero_pool_arm(as_stream(stream)));
   return h->run(*p, echo, scale, cos_t, sin_t, gain, out, as_stream(stream));
 }
 

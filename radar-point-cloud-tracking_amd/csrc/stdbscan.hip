@@ -505,9 +505,14 @@ __global__ void k_cell_start_end(int32_t* __restrict__ cell_start, int64_t cells
 
 // slab_lo[s] = first point of slab s (points ordered by slab), slab_lo[nt] = n: ONE WAVE per
 // slab, a 64-ary search (64 probes per round: ~5 dependent rounds over 50 M points instead of a
-// thread's 26-step binary search)
+// thread's 26-step binary search).  Also clears zero[0, zwords) (the occupancy bits the slab
+// bucket sets next: one launch instead of a memset and this).
 __global__ void k_slab_lo(const float* __restrict__ t, int64_t n, Geom g,
-                          int32_t* __restrict__ slab_lo) {
+                          int32_t* __restrict__ slab_lo, uint32_t* __restrict__ zero,
+                          int64_t zwords) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < zwords;
+       i += (int64_t)gridDim.x * blockDim.x)
+    zero[i] = 0u;
   const int lane = threadIdx.x & 63;
   const int64_t wpb = blockDim.x / 64;
   for (int64_t s = (int64_t)blockIdx.x * wpb + threadIdx.x / 64; s <= g.nt;
@@ -4490,8 +4495,7 @@ int32_t DbscanState::build_t(const float* x, const float* y, const float* z, int
                       (int64_t)nx * ny <= kBucketCells && nt < (int64_t(1) << 31);
   if (bucket) {
     hipLaunchKernelGGL(k_slab_lo, dim3(grid_for(64 * (nt + 1), kBlock, 4096)), dim3(kBlock), 0,
-                       st, t, n, g, slab_lo);
-    RPT_HIP(hipMemsetAsync(occ_bits, 0, sizeof(uint32_t) * (C1 / 32 + 2), st));
+                       st, t, n, g, slab_lo, occ_bits, (int64_t)(C1 / 32 + 2));
     // the slabs write their occupied cells (ascending) into hpos at their point offsets, the
     // occupancy bits and their counts; one scan over the slabs and a gather give the list
     const size_t hist_bytes = sizeof(int32_t) * (size_t)nx * ny;
@@ -4691,7 +4695,7 @@ int32_t DbscanState::core_pass(hipStream_t st) {
         hipLaunchKernelGGL(k_core_fill<false>, dim3(tile_grid(n)), dim3(kBlock), 0, st, skey, n,
                            cflag, core, slow, n_slow);
     } else {
-      RPT_HIP(hipMemsetAsync(n_cq, 0, sizeof(int32_t), st));
+      RPT_TRY(zero_n(st, 1, &n_cq));
       hipLaunchKernelGGL(k_core_cell_fast, dim3(tile_grid(n)), dim3(kBlock), 0, st, occ, n_occ,
                          g, cell_start, mutual, cflag, cq, n_cq);
       if (dim == 2)
@@ -4718,7 +4722,7 @@ int32_t DbscanState::core_pass(hipStream_t st) {
   // oct: the union's per-cell minima (cell_min_pair) come out of the fill and slow passes
   auto* cm = oct ? reinterpret_cast<unsigned long long*>(cell_min_pair) : nullptr;
   if (k5_fused_path()) {
-    RPT_HIP(hipMemsetAsync(n_slow, 0, sizeof(int32_t), st));
+    RPT_TRY(zero_n(st, 1, &n_slow));
     // the cell pass's decisions handed to the slow pass when its window's 5 W (slab, row) pairs
     // x 5 columns fit a 128-bit mask (W <= 5; pmask / clo per occupied cell in the dead radix
     // buffers / cid, both rebuilt later)
@@ -4773,8 +4777,8 @@ int32_t DbscanState::core_pass(hipStream_t st) {
                        st, g, (int)rs, occ, n_occ, rec<2>(), mutual, occ_bits, slab_t, cflag,
                        n_slow, (uint8_t*)nullptr);
   } else {
-    RPT_HIP(hipMemsetAsync(n_slow, 0, sizeof(int32_t), st));
-    RPT_HIP(hipMemsetAsync(n_cq, 0, sizeof(int32_t), st));
+    RPT_TRY(zero_n(st, 1, &n_slow));
+    RPT_TRY(zero_n(st, 1, &n_cq));
     hipLaunchKernelGGL(k_core_cell_fast, dim3(tile_grid(n)), dim3(kBlock), 0, st, occ, n_occ, g,
                        cell_start, mutual, cflag, cq, n_cq);
     if (dim == 2)
@@ -5124,7 +5128,7 @@ int32_t DbscanState::frames_pass(int32_t min_frames, hipStream_t st) {
     hipLaunchKernelGGL(k_frames_cells, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, st, g, R,
                        occ, n_occ, rec<2>(), occ_bits, min_frames, fok);
   }
-  RPT_HIP(hipMemsetAsync(count, 0, sizeof(int32_t), st));
+  RPT_TRY(zero_n(st, 1, &count));
   hipLaunchKernelGGL(k_frames_queue, dim3(tile_grid(n)), dim3(kBlock), 0, st, skey, n, C,
                      cells ? (const uint8_t*)fok : (const uint8_t*)nullptr, (int)min_frames,
                      refine ? 1 : 0, core, list, count);
@@ -5154,9 +5158,9 @@ int32_t DbscanState::frames_pass(int32_t min_frames, hipStream_t st) {
 }
 
 int32_t DbscanState::labels_fifo(int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st) {
-  int32_t* nc_count = nc_list + n;
+  int32_t* nc_count = nullptr;
   int32_t* spos = slab;
-  RPT_HIP(hipMemsetAsync(nc_count, 0, sizeof(int32_t), st));
+  RPT_TRY(zero_n(st, 1, &nc_count));
   RPT_TRY(cluster_ids(st, nullptr));
   if (!spos_on)  // (else the grid build's)
     hipLaunchKernelGGL(k_inverse_perm, dim3(grid_for(n, kBlock, 2048)), dim3(kBlock), 0, st,
