@@ -470,9 +470,12 @@ def main():
     stage_acc = {}
     k5 = []      # (K5 ms, points entering ST-DBSCAN) per timed run
     results = []
+    stagger_s = float(os.environ.get("RPT_BENCH_STAGGER_MS", "0")) / 1e3  # (temporary A/B)
     for k in range(args.steps):
         alive()
         results.append(run(echoes[k % E]))
+        if stagger_s and k + 1 < args.lanes:
+            time.sleep(stagger_s)
         if timing and dist and not sharded_lanes:
             k5.append((ops.last_core_ms(), ops.core_points))
     results = [resolve(r) for r in results]

@@ -5158,10 +5158,9 @@ int32_t DbscanState::frames_pass(int32_t min_frames, hipStream_t st) {
 }
 
 int32_t DbscanState::labels_fifo(int32_t* labels, rpt_stdbscan_stats* stats, hipStream_t st) {
-  int32_t* nc_count = nullptr;
+  int32_t* nc_count = nc_list + n;  // k_ccmin's non-core queue counter, cleared by cluster_ids
   int32_t* spos = slab;
-  RPT_TRY(zero_n(st, 1, &nc_count));
-  RPT_TRY(cluster_ids(st, nullptr));
+  RPT_TRY(cluster_ids(st, nullptr, nc_count));
   if (!spos_on)  // (else the grid build's)
     hipLaunchKernelGGL(k_inverse_perm, dim3(grid_for(n, kBlock, 2048)), dim3(kBlock), 0, st,
                        sorig, n, spos);

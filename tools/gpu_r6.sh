@@ -186,6 +186,14 @@ for step in "$@"; do
       for f in $O/bth_*.log $O/bnt_*.log; do
         python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['value'], d['ms_per_step'], d['steady_state']['ms_per_step'])" $f
       done ;;
+    bench_stagger)  # the driver's bench line: the first stacks' starts staggered (A/B, interleaved)
+      BB="python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --h2d-steps 0"
+      for rep in 1 2; do
+        for ms in ${STAGGERS:-0 3}; do RPT_BENCH_STAGGER_MS=$ms run bst${ms}_$rep 300 $BB || exit 1; done
+      done
+      for f in $O/bst*.log; do
+        python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['value'], d['ms_per_step'], d['steady_state']['ms_per_step'])" $f
+      done ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench_lanes)  # the driver's bench line at 5 (default), 6 and 8 stacks in flight, interleaved
