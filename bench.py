@@ -321,6 +321,10 @@ def main():
                          "sharded path) of consecutive steps")
     ap.add_argument("--no-one-stack", action="store_true",
                     help="skip the one-stack-in-flight leg (and so K5's roofline)")
+    ap.add_argument("--k1-gate", action="store_true",
+                    help="the lanes' K1 passes take turns (rpt_k1_gate; default: they overlap "
+                         "freely: over 20 steps the turns cost more than they save, "
+                         "profiles/r6/ab_k1_gate/)")
     ap.add_argument("--sync-host", action="store_true",
                     help="run each step's host stage (order + tracker) inline instead of "
                          "overlapping it with the next step's device work")
@@ -425,7 +429,7 @@ def main():
         # queue their host stages (~6 ms each at 1000 frames) behind one another
         pipe = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), dev, timing=timing,
                                   async_host=not args.sync_host, lanes=args.lanes,
-                                  host_workers=args.host_workers)
+                                  host_workers=args.host_workers, k1_gate=args.k1_gate)
         pipe.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
                           cfg.n_frames * len(cfg.gains))
         run = lambda e: pipe.submit(e)  # noqa: E731
@@ -470,12 +474,9 @@ def main():
     stage_acc = {}
     k5 = []      # (K5 ms, points entering ST-DBSCAN) per timed run
     results = []
-    stagger_s = float(os.environ.get("RPT_BENCH_STAGGER_MS", "0")) / 1e3  # (temporary A/B)
     for k in range(args.steps):
         alive()
         results.append(run(echoes[k % E]))
-        if stagger_s and k + 1 < args.lanes:
-            time.sleep(stagger_s)
         if timing and dist and not sharded_lanes:
             k5.append((ops.last_core_ms(), ops.core_points))
     results = [resolve(r) for r in results]
@@ -531,8 +532,10 @@ def main():
         steady = {"value": round(pts_ss / span / 1e6, 3), "unit": "Mpoints/s",
                   "ms_per_step": round(span / (args.steps - L_) * 1e3, 3),
                   "steps": args.steps - L_,
+                  "done_ms": [round((x - t0) * 1e3, 2) for x in td],
                   "note": f"steps {L_}..{args.steps - 1}: from step {L_ - 1}'s device completion "
-                          f"to the last step's (pipeline fill and the last host stage excluded)"}
+                          f"to the last step's (pipeline fill and the last host stage excluded); "
+                          f"done_ms: every run's device completion after the timed region's start"}
 
     # one stack in flight (lanes = 1): the same steps strictly one after another.  K5's roofline
     # is taken here, where its kernels have the GPU to themselves (with several stacks in flight

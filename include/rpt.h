@@ -294,6 +294,15 @@ typedef struct rpt_stack_result {
 } rpt_stack_result;
 rpt_stack* rpt_stack_create(void);
 void rpt_stack_destroy(rpt_stack* h);
+/* K1 turns for several handles in flight on one GPU (one stream each): runs of handles that share
+ * a gate enqueue their K1 (count + write) one at a time, in the order they reach it, each behind
+ * the previous one on the device -- the HBM-bound K1 passes of concurrent stacks never coincide
+ * and always overlap other stacks' latency-bound stages.  NULL detaches.  The gate must outlive
+ * every run of the handles attached to it. */
+typedef struct rpt_k1_gate rpt_k1_gate;
+rpt_k1_gate* rpt_k1_gate_create(void);
+void rpt_k1_gate_destroy(rpt_k1_gate* g);
+int32_t rpt_stack_set_k1_gate(rpt_stack* h, rpt_k1_gate* g);
 int32_t rpt_stack_run(rpt_stack* h, const rpt_stack_params* params, const void* echo /*dev*/,
                       const float* scale /*dev [files*rows]*/, const float* cos_t,
                       const float* sin_t, const int32_t* gain /*dev [files], nullable*/,

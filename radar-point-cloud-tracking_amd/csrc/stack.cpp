@@ -69,6 +69,44 @@ __global__ void k_pack_segs(const int32_t* __restrict__ n_seg, const int32_t* __
 
 using namespace rpt;
 
+namespace {
+// One run's K1 turn at a gate (nullable: no gate, no-op).  enter() waits for the turn and makes
+// the stream wait for the previous K1; leave() records this K1's end and passes the turn (also
+// on an error path, from the destructor, so no later run waits forever).
+class K1Turn {
+ public:
+  K1Turn(rpt_k1_gate* g, hipStream_t st) : g_(g), st_(st) {}
+  int32_t enter() {
+    if (!g_) return RPT_OK;
+    std::unique_lock<std::mutex> lk(g_->mu);
+    t_ = g_->issued++;
+    g_->cv.wait(lk, [&] { return g_->next == t_; });
+    in_ = true;
+    hipEvent_t& mine = g_->ev[t_ % rpt_k1_gate::kRing];
+    if (!mine) RPT_HIP(hipEventCreateWithFlags(&mine, hipEventDisableTiming));
+    if (t_ > 0) RPT_HIP(hipStreamWaitEvent(st_, g_->ev[(t_ - 1) % rpt_k1_gate::kRing], 0));
+    return RPT_OK;
+  }
+  int32_t leave() {
+    if (!g_ || !in_) return RPT_OK;
+    in_ = false;
+    std::lock_guard<std::mutex> lk(g_->mu);
+    const hipError_t e = hipEventRecord(g_->ev[t_ % rpt_k1_gate::kRing], st_);
+    g_->next = t_ + 1;
+    g_->cv.notify_all();
+    RPT_HIP(e);
+    return RPT_OK;
+  }
+  ~K1Turn() { (void)leave(); }
+
+ private:
+  rpt_k1_gate* g_;
+  hipStream_t st_;
+  int64_t t_ = -1;
+  bool in_ = false;
+};
+}  // namespace
+
 int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float* scale,
                        const float* cos_t, const float* sin_t, const int32_t* gain,
                        rpt_stack_result* out, hipStream_t st) {
@@ -110,6 +148,8 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
     RPT_TRY(k1_stage.ensure((size_t)polar_stage_words(n_files, p.rows), st));
     mk = k1_stage.p;
   }
+  K1Turn k1turn(k1_gate, st);
+  RPT_TRY(k1turn.enter());
   RPT_TRY(polar_count(echo, p.echo_dtype, n_files, p.rows, p.bins, p.threshold, p.stride,
                       row_prefix.p, file_off.p, nullptr, st, mk));
   RPT_HIP(hipMemcpyAsync(hfo, file_off.p, sizeof(int64_t) * (n_files + 1), hipMemcpyDeviceToHost,
@@ -152,6 +192,7 @@ int32_t rpt_stack::run(const rpt_stack_params& p, const void* echo, const float*
                         p.threshold, p.stride, row_prefix.p, file_off.p, G, x.p, y.p, v.p,
                         gain ? g.p : nullptr, pf.p, st, mk, kb, &k1_bounds));
   }
+  RPT_TRY(k1turn.leave());
   if (timing) RPT_HIP(hipEventRecord(ev[1], st));
   if (N == 0) {
     // no frame built: st_dbscan(frames) stacks nothing and returns {} (:463-464) -- no error,
@@ -398,6 +439,16 @@ int32_t rpt_arange_edges(float lo, float hi, double res, double* out, int32_t ca
 }
 
 rpt_stack* rpt_stack_create(void) { return new rpt_stack(); }
+
+rpt_k1_gate* rpt_k1_gate_create(void) { return new rpt_k1_gate(); }
+
+void rpt_k1_gate_destroy(rpt_k1_gate* g) { delete g; }
+
+int32_t rpt_stack_set_k1_gate(rpt_stack* h, rpt_k1_gate* g) {
+  if (!h) return RPT_EINVAL;
+  h->k1_gate = g;
+  return RPT_OK;
+}
 
 void rpt_stack_destroy(rpt_stack* h) { delete h; }
 

@@ -4,8 +4,10 @@
 #pragma once
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "common.h"
@@ -177,8 +179,26 @@ struct PinnedBuf {
 
 using rpt::DevBuf;
 using rpt::PinnedBuf;
+// K1 turns of several stack handles (lanes): each run's K1 (count + write, HBM-bound) is
+// enqueued only after the previous run's, and its stream waits on the device for that one to end,
+// so the lanes' K1 passes never share the HBM and always overlap other lanes' latency-bound
+// stages.  Turns go in arrival order (a run takes the next ticket when it reaches K1): a waiting
+// run only waits for runs already inside their K1 enqueue, so no cycle can form.
+struct rpt_k1_gate {
+  static constexpr int kRing = 16;
+  std::mutex mu;
+  std::condition_variable cv;
+  int64_t issued = 0, next = 0;  // tickets handed out / the ticket whose turn it is
+  hipEvent_t ev[kRing] = {};     // ev[t % kRing]: recorded after ticket t's K1
+  ~rpt_k1_gate() {
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+  }
+};
+
 struct rpt_stack {
   DevBuf<uint32_t> pack_d;  // packed readback staging
+  rpt_k1_gate* k1_gate = nullptr;  // (not owned) rpt_stack_set_k1_gate
   DevBuf<int64_t> row_prefix, file_off, new_off, first_noise, seg_count, seg_first, scal;
   DevBuf<float> x, y, v, x2, y2, v2, t, seg_cx, seg_cy, seg_mi;
   DevBuf<int32_t> g, pf, g2, pf2, labels, land_cnt, land_cell, seg_frame, seg_label;

@@ -229,6 +229,9 @@ _SIGS = [
                                          c_i64p, c_i32p, C.c_int32]),
     ("rpt_order_clusters", C.c_int32, [C.c_int32, C.c_int64, c_i32p, c_i32p, c_i64p, c_i64p,
                                         c_i64p, c_i64p]),
+    ("rpt_k1_gate_create", vp, []),
+    ("rpt_k1_gate_destroy", None, [vp]),
+    ("rpt_stack_set_k1_gate", C.c_int32, [vp, vp]),
     ("rpt_order_and_track", C.c_int32, [C.c_int32, C.c_int64, c_i32p, c_i32p, c_i64p, c_i64p,
                                          c_f32p, c_f32p, C.c_int32, c_i64p, c_i64p, vp, c_i64p,
                                          c_i64p]),

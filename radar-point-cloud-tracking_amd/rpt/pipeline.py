@@ -80,7 +80,8 @@ class FrameStackPipeline:
 
     def __init__(self, gains: Sequence[int], rows: int, bins: int, params: PathParams = None,
                  device=None, timing: bool = False, async_host: bool = False,
-                 host_workers: int = 2, lanes: int = 1, round_robin: bool = False):
+                 host_workers: int = 2, lanes: int = 1, round_robin: bool = False,
+                 k1_gate: bool = False):
         """async_host: the host stage (cluster order + tracker, sequential C++) of a run executes
         on a pool of host_workers threads while the caller goes on to the next runs' device
         work (runs are independent, so their host stages may overlap each other);
@@ -92,7 +93,12 @@ class FrameStackPipeline:
         stream).  A run takes whichever lane is free when a worker thread picks it up: streams
         beyond the process's hardware queues share a queue and progress slower, and a fixed
         round-robin left the last runs of the slow lanes finishing long after the others
-        (round_robin=True keeps that policy for comparisons)."""
+        (round_robin=True keeps that policy for comparisons).  k1_gate (lanes > 1): the lanes'
+        K1 passes (HBM-bound) take turns, each behind the previous one on the device
+        (rpt_k1_gate), so they never share the HBM and always overlap other lanes' latency-bound
+        stages.  Measured: the steady state of a run 0-6 % faster from box to box, the 20-step
+        bench line 4-19 % slower (the turns delay the first and last stacks of a batch), hence
+        off by default (profiles/r6/ab_k1_gate/)."""
         self.dev = require_gpu(device)
         self.gains = [int(g) for g in gains]
         if sorted(self.gains) != self.gains:
@@ -104,6 +110,9 @@ class FrameStackPipeline:
             raise ValueError("lanes must be >= 1")
         self._hs = [self.lib.rpt_stack_create() for _ in range(lanes)]
         self._h = self._hs[0]
+        self._gate = self.lib.rpt_k1_gate_create() if lanes > 1 and k1_gate else None
+        for h in self._hs if self._gate else []:
+            _abi.check(self.lib.rpt_stack_set_k1_gate(h, self._gate), "rpt_stack_set_k1_gate")
         self._streams = [torch.cuda.Stream(self.dev) for _ in range(lanes)] if lanes > 1 else None
         self._lane_pool = ThreadPoolExecutor(max_workers=lanes) if lanes > 1 else None
         self._rr = [ThreadPoolExecutor(max_workers=1) for _ in range(lanes)] \
@@ -284,3 +293,6 @@ class FrameStackPipeline:
             if h:
                 self.lib.rpt_stack_destroy(h)
         self._hs, self._h = [], None
+        if getattr(self, "_gate", None):  # after every handle attached to it
+            self.lib.rpt_k1_gate_destroy(self._gate)
+            self._gate = None

@@ -186,12 +186,13 @@ for step in "$@"; do
       for f in $O/bth_*.log $O/bnt_*.log; do
         python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['value'], d['ms_per_step'], d['steady_state']['ms_per_step'])" $f
       done ;;
-    bench_stagger)  # the driver's bench line: the first stacks' starts staggered (A/B, interleaved)
+    bench_gate)   # the driver's bench line: K1 turns across lanes (--k1-gate) vs overlapping K1s
       BB="python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --h2d-steps 0"
       for rep in 1 2; do
-        for ms in ${STAGGERS:-0 3}; do RPT_BENCH_STAGGER_MS=$ms run bst${ms}_$rep 300 $BB || exit 1; done
+        run bg1_$rep 300 $BB --k1-gate || exit 1
+        run bg0_$rep 300 $BB || exit 1
       done
-      for f in $O/bst*.log; do
+      for f in $O/bg1_*.log $O/bg0_*.log; do
         python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['value'], d['ms_per_step'], d['steady_state']['ms_per_step'])" $f
       done ;;
     smoke)
