@@ -585,10 +585,12 @@ def test_k1_stack_driver_matches_public_k1(gpu, rows, thr, stride, p):
             np.testing.assert_array_equal(a, b, err_msg=name)
 
 
-def test_concurrent_lanes_match_single_lane(gpu):
-    """Two lanes (two native handles on two streams, submitted from two threads, the library's
-    scratch and scan state per stream) give the same results as one lane, run after run: four
-    stacks of different content alternate between the lanes."""
+@pytest.mark.parametrize("lanes,k1_gate", [(2, False), (3, True)])
+def test_concurrent_lanes_match_single_lane(gpu, lanes, k1_gate):
+    """Two or three lanes (native handles on their own streams, submitted from as many threads,
+    the library's scratch, scan state and zeroed counters per stream; with k1_gate the lanes'
+    K1 passes take turns, rpt_k1_gate) give the same results as one lane, run after run: four
+    stacks of different content spread over the lanes."""
     from rpt.pipeline import FrameStackPipeline, PathParams
     from rpt.synth import DeviceSynth, SynthConfig
 
@@ -599,8 +601,8 @@ def test_concurrent_lanes_match_single_lane(gpu):
         stacks.append(ds.echo())
     torch.cuda.synchronize(gpu)
     one = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), gpu)
-    two = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), gpu, lanes=2,
-                             async_host=True)
+    two = FrameStackPipeline(cfg.gains, cfg.rows, cfg.bins, PathParams(), gpu, lanes=lanes,
+                             async_host=True, k1_gate=k1_gate)
     for p in (one, two):
         p.set_geometry(np.full(cfg.rows, cfg.scale, np.float32), ds.geo.cos_t, ds.geo.sin_t,
                        cfg.n_frames * 3)
