@@ -200,7 +200,7 @@ for step in "$@"; do
     bench_lanes)  # the driver's bench line at 5 (default), 6 and 8 stacks in flight, interleaved
       BB="python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --h2d-steps 0"
       for rep in 1 2; do
-        for l in 5 6 8; do run bln${l}_$rep 300 $BB --lanes $l || exit 1; done
+        for l in ${LANESET:-5 6 8}; do run bln${l}_$rep 300 $BB --lanes $l || exit 1; done
       done
       for f in $O/bln*.log; do
         python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['value'], d['ms_per_step'], d['steady_state']['ms_per_step'])" $f
